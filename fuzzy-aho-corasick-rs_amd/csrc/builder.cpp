@@ -1,0 +1,394 @@
+// builder.cpp — host construction of the device automaton tables.
+//
+// Mirrors FuzzyAhoCorasickBuilder::build (src/builder.rs:181-484) and emits the flat
+// structure-of-arrays layout of fac_internal.h instead of the reference's per-node Vecs/maps:
+//   * graphemes are interned to ids and the trie is one (node, grapheme-id) -> child hash map;
+//   * children keep insertion order (the reference uses hashbrown order, builder.rs:336-342 —
+//     see DESIGN.md §3 for why this only affects tie-breaks);
+//   * fail links exist only to merge suffix-pattern outputs (builder.rs:239-276); they are not
+//     uploaded, because the search never follows them;
+//   * prune coefficients come from the reach-len / reach-weight pass (builder.rs:344-381).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <unordered_map>
+
+#include "fac_internal.h"
+
+namespace fac {
+namespace {
+
+struct U32Hash {
+  size_t operator()(const std::u32string& s) const {
+    uint64_t h = 1469598103934665603ull;
+    for (char32_t c : s) h = (h ^ (uint64_t)c) * 1099511628211ull;
+    return (size_t)h;
+  }
+};
+
+void default_similarity(std::vector<float>& t) {  // builder.rs:492-526, structs.rs:36-48
+  t.assign(128 * 128, 0.f);
+  for (int i = 0; i < 128; ++i) t[i * 128 + i] = 1.f;
+  auto vowel = [](int c) { return c == 'a' || c == 'e' || c == 'i' || c == 'o' || c == 'u'; };
+  for (int a = 'a'; a <= 'z'; ++a)
+    for (int b = 'a'; b <= 'z'; ++b) {
+      if (a == b) continue;
+      if (vowel(a) == vowel(b)) t[a * 128 + b] = vowel(a) ? 0.6f : 0.4f;
+    }
+  const struct { char a, b; float s; } ocr[] = {{'o', '0', 0.6f}, {'l', '1', 0.7f}, {'i', '1', 0.6f},
+                                                {'s', '5', 0.5f}};
+  for (auto& o : ocr) {
+    t[o.a * 128 + o.b] = o.s;
+    t[o.b * 128 + o.a] = o.s;
+  }
+}
+
+int32_t lim_max(int32_t acc, int32_t v) {
+  if (v == LIM_NONE) return acc;
+  return std::max(acc == LIM_NONE ? 0 : acc, v);
+}
+
+DevLimits to_dev(const fac_limits& l) { return {l.insertions, l.deletions, l.substitutions, l.swaps, l.edits}; }
+
+bool lim_ok(int32_t v) { return v == LIM_NONE || (v >= 0 && v <= 255); }
+
+}  // namespace
+
+int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, Engine& e, std::string& err) {
+  e.cfg = *cfg;
+  e.device = cfg->device;
+  e.case_insensitive = cfg->case_insensitive != 0;
+  e.p_ins = cfg->penalty_insertion;
+  e.p_del = cfg->penalty_deletion;
+  e.p_sub = cfg->penalty_substitution;
+  e.p_swp = cfg->penalty_swap;
+  e.min_sym = cfg->min_symbol_similarity;
+  e.beam_width = cfg->beam_width;
+  e.has_auto_beam = cfg->has_auto_beam != 0;
+  e.ab_budget = cfg->auto_beam_budget;
+  e.ab_width = cfg->auto_beam_width;
+  if (cfg->n_mappings > 0) {
+    err = "multi-character mappings are not supported on the GPU path";
+    return FAC_E_UNSUPPORTED;
+  }
+  if (e.has_auto_beam && e.ab_width == 0 && e.beam_width == 0) {
+    err = "auto_beam width must be >= 1";
+    return FAC_E_INVALID;
+  }
+  if (e.has_auto_beam && e.beam_width == 0) {  // an explicit beam_width takes precedence (builder.rs:93-106)
+    err = "auto_beam is not implemented on the GPU path yet";
+    return FAC_E_UNSUPPORTED;
+  }
+  e.has_limits = cfg->has_limits != 0;
+  if (e.has_limits) {
+    e.limits = to_dev(cfg->limits);
+    const fac_limits& l = cfg->limits;
+    if (!lim_ok(l.insertions) || !lim_ok(l.deletions) || !lim_ok(l.substitutions) || !lim_ok(l.swaps) ||
+        !lim_ok(l.edits)) {
+      err = "limits must be 0..255 or None";
+      return FAC_E_INVALID;
+    }
+  }
+
+  // ---- patterns: segment, fold, intern graphemes (builder.rs:195-205, structs.rs:660-754)
+  std::unordered_map<std::u32string, uint32_t, U32Hash> gid_of;
+  std::vector<std::u32string> gstr;
+  std::vector<std::vector<uint32_t>> pat_gids(np);
+  e.pats.resize(np);
+  std::vector<uint64_t> starts;
+  std::u32string folded;
+  for (uint64_t i = 0; i < np; ++i) {
+    const uint8_t* s = reinterpret_cast<const uint8_t*>(pats[i].utf8);
+    uint64_t len = pats[i].len;
+    if (len && !s) { err = "NULL pattern"; return FAC_E_INVALID; }
+    if (!utf8_valid(s, len)) { err = "pattern is not valid UTF-8"; return FAC_E_INVALID; }
+    segment_graphemes(s, len, starts);
+    for (size_t g = 0; g < starts.size(); ++g) {
+      uint64_t b = starts[g], en = g + 1 < starts.size() ? starts[g + 1] : len;
+      fold_grapheme(s, b, en, e.case_insensitive, folded);
+      auto it = gid_of.find(folded);
+      uint32_t id;
+      if (it == gid_of.end()) {
+        id = (uint32_t)gstr.size();
+        gid_of.emplace(folded, id);
+        gstr.push_back(folded);
+      } else {
+        id = it->second;
+      }
+      pat_gids[i].push_back(id);
+    }
+    DevPattern& dp = e.pats[i];
+    dp.glen = (float)starts.size();
+    dp.weight = pats[i].weight;
+    dp.has_limits = pats[i].has_limits != 0;
+    dp.lim = dp.has_limits ? to_dev(pats[i].limits) : DevLimits{LIM_NONE, LIM_NONE, LIM_NONE, LIM_NONE, LIM_NONE};
+    e.max_glen = std::max<uint32_t>(e.max_glen, (uint32_t)starts.size());
+    if (dp.has_limits) {
+      const fac_limits& l = pats[i].limits;
+      if (!lim_ok(l.insertions) || !lim_ok(l.deletions) || !lim_ok(l.substitutions) || !lim_ok(l.swaps) ||
+          !lim_ok(l.edits)) {
+        err = "limits must be 0..255 or None";
+        return FAC_E_INVALID;
+      }
+    }
+  }
+
+  // ---- trie (builder.rs:207-237)
+  std::unordered_map<uint64_t, uint32_t> go;  // (node << 32 | gid) -> child
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> kids(1);  // (gid, child), insertion order
+  std::vector<int32_t> pidx(1, -1);
+  std::vector<std::vector<uint32_t>> output(1);
+  for (uint64_t i = 0; i < np; ++i) {
+    uint32_t cur = 0;
+    for (uint32_t g : pat_gids[i]) {
+      uint64_t key = ((uint64_t)cur << 32) | g;
+      auto it = go.find(key);
+      uint32_t next;
+      if (it == go.end()) {
+        next = (uint32_t)kids.size();
+        go.emplace(key, next);
+        kids[cur].push_back({g, next});
+        kids.emplace_back();
+        pidx.push_back(-1);
+        output.emplace_back();
+      } else {
+        next = it->second;
+      }
+      if (pidx[next] < 0) pidx[next] = (int32_t)i;
+      cur = next;
+    }
+    output[cur].push_back((uint32_t)i);
+  }
+  const size_t nn = kids.size();
+  if (nn >= (size_t)EDGE_NEXT_MASK) { err = "automaton too large"; return FAC_E_UNSUPPORTED; }
+
+  // ---- fail links, used only to merge outputs (builder.rs:239-276); BFS by depth
+  {
+    std::vector<uint32_t> fail(nn, 0), queue;
+    queue.reserve(nn);
+    for (auto& k : kids[0]) queue.push_back(k.second);
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+      uint32_t cur = queue[qi];
+      for (auto& k : kids[cur]) {
+        uint32_t g = k.first, next = k.second;
+        uint32_t f = fail[cur];
+        while (f != 0 && go.find(((uint64_t)f << 32) | g) == go.end()) f = fail[f];
+        auto it = go.find(((uint64_t)f << 32) | g);
+        uint32_t fb = it == go.end() ? 0 : it->second;
+        fail[next] = fb;
+        for (uint32_t p : output[fb])
+          if (std::find(output[next].begin(), output[next].end(), p) == output[next].end())
+            output[next].push_back(p);
+        queue.push_back(next);
+      }
+    }
+  }
+
+  // ---- effective limits (builder.rs:289-329), has_pattern_limits, max_edits_fast (:444-468)
+  e.has_pattern_limits = false;
+  for (auto& p : e.pats) e.has_pattern_limits |= p.has_limits != 0;
+  if (!e.has_limits && e.has_pattern_limits) {
+    DevLimits m{LIM_NONE, LIM_NONE, LIM_NONE, LIM_NONE, LIM_NONE};
+    for (auto& p : e.pats) {
+      if (!p.has_limits) continue;
+      m.edits = lim_max(m.edits, p.lim.edits);
+      m.ins = lim_max(m.ins, p.lim.ins);
+      m.del = lim_max(m.del, p.lim.del);
+      m.sub = lim_max(m.sub, p.lim.sub);
+      m.swp = lim_max(m.swp, p.lim.swp);
+    }
+    e.has_limits = true;
+    e.limits = m;
+  }
+  if (e.has_pattern_limits) e.max_edits_fast = 255;
+  else if (!e.has_limits) e.max_edits_fast = 0;
+  else if (e.limits.edits != LIM_NONE && e.limits.ins == LIM_NONE && e.limits.del == LIM_NONE &&
+           e.limits.sub == LIM_NONE && e.limits.swp == LIM_NONE)
+    e.max_edits_fast = (uint32_t)e.limits.edits;
+  else
+    e.max_edits_fast = 255;
+  // search.rs:204-248 dispatch: 1..=6 specialise, everything else (incl. 0) is the 255 path
+  e.mef = (e.max_edits_fast >= 1 && e.max_edits_fast <= 6) ? e.max_edits_fast : 255;
+
+  // ---- flat tables
+  e.nodes.assign(nn, DevNode{});
+  e.edges.clear();
+  e.out_pat.clear();
+  e.sb_bits.assign(nn, uint4{0, 0, 0, 0});
+  e.max_degree = 0;
+  for (size_t i = 0; i < nn; ++i) {
+    DevNode& d = e.nodes[i];
+    d.edge_begin = (uint32_t)e.edges.size();
+    for (auto& k : kids[i]) {
+      const std::u32string& g = gstr[k.first];
+      uint32_t fc = g.empty() ? 0 : (uint32_t)g[0];
+      bool single = g.size() == 1 && g[0] < 0x80;  // grapheme byte length == 1 (builder.rs:340)
+      uint32_t nx = k.second;
+      if (!output[nx].empty()) nx |= EDGE_CHILD_OUTPUT;
+      if (single) nx |= EDGE_SINGLE_BYTE;
+      e.edges.push_back({fc, nx});
+      if (single && fc < 128) (&e.sb_bits[i].x)[fc >> 5] |= 1u << (fc & 31);
+    }
+    d.edge_end = (uint32_t)e.edges.size();
+    e.max_degree = std::max(e.max_degree, d.edge_end - d.edge_begin);
+    d.out_begin = (uint32_t)e.out_pat.size();
+    for (uint32_t p : output[i]) e.out_pat.push_back(p);
+    d.out_end = (uint32_t)e.out_pat.size();
+    d.pidx = pidx[i];
+    d.pad = 0;
+  }
+  // reach fixpoint (builder.rs:348-381): children always have larger ids than their parent in a
+  // freshly built trie, so one reverse pass reaches the fixpoint.
+  std::vector<uint64_t> rl(nn, 0);
+  std::vector<float> rw(nn, 0.f);
+  for (size_t i = 0; i < nn; ++i)
+    for (uint32_t p : output[i]) {
+      rl[i] = std::max<uint64_t>(rl[i], (uint64_t)e.pats[p].glen);
+      rw[i] = std::fmax(rw[i], e.pats[p].weight);
+    }
+  for (size_t i = nn; i-- > 0;)
+    for (auto& k : kids[i]) {
+      rl[i] = std::max(rl[i], rl[k.second]);
+      rw[i] = std::fmax(rw[i], rw[k.second]);
+    }
+  for (size_t i = 0; i < nn; ++i) {
+    float len = (float)rl[i];
+    e.nodes[i].prune_len = len;
+    e.nodes[i].prune_lw = len / rw[i];
+  }
+
+  // ---- similarity (structs.rs:30-54)
+  if (cfg->similarity_ascii) {
+    e.sim_ascii.assign(cfg->similarity_ascii, cfg->similarity_ascii + 128 * 128);
+    std::vector<std::pair<uint64_t, float>> pr;
+    for (uint64_t k = 0; k < cfg->n_similarity_pairs; ++k) {
+      uint32_t a = cfg->similarity_pairs[2 * k], b = cfg->similarity_pairs[2 * k + 1];
+      if (a < 128 && b < 128) continue;  // lives in the ASCII table
+      pr.push_back({((uint64_t)a << 32) | b, cfg->similarity_pair_values[k]});
+    }
+    std::stable_sort(pr.begin(), pr.end(), [](auto& x, auto& y) { return x.first < y.first; });
+    e.sim_keys.clear();
+    e.sim_vals.clear();
+    for (size_t k = 0; k < pr.size(); ++k) {
+      if (!e.sim_keys.empty() && e.sim_keys.back() == pr[k].first) { e.sim_vals.back() = pr[k].second; continue; }
+      e.sim_keys.push_back(pr[k].first);
+      e.sim_vals.push_back(pr[k].second);
+    }
+  } else {
+    default_similarity(e.sim_ascii);
+  }
+
+  // ---- 2-gram window skip (search.rs:504-521)
+  std::memset(e.first_bits, 0, sizeof(e.first_bits));
+  std::memset(e.second_bits, 0, sizeof(e.second_bits));
+  e.window_skip = false;
+  if (e.mef == 1 && output[0].empty()) {
+    bool child_output = false;
+    uint32_t f[4] = {e.sb_bits[0].x, e.sb_bits[0].y, e.sb_bits[0].z, e.sb_bits[0].w};
+    uint32_t s2[4] = {0, 0, 0, 0};
+    for (auto& k : kids[0]) {
+      const uint4& cb = e.sb_bits[k.second];
+      const uint32_t c[4] = {cb.x, cb.y, cb.z, cb.w};
+      for (int w = 0; w < 4; ++w) { s2[w] |= c[w]; f[w] |= c[w]; }
+      if (!output[k.second].empty()) child_output = true;
+    }
+    if (!child_output) {
+      e.window_skip = true;
+      std::memcpy(e.first_bits, f, sizeof(f));
+      std::memcpy(e.second_bits, s2, sizeof(s2));
+    }
+  }
+
+  // ---- max_match_graphemes (stream.rs:213-253), no mappings => mapping factor 1
+  {
+    uint64_t max_edits = 0;
+    auto edits_of = [](const DevLimits& l) -> uint64_t {
+      if (l.edits != LIM_NONE) return (uint64_t)l.edits;
+      auto z = [](int32_t v) { return v == LIM_NONE ? 0ull : (uint64_t)v; };
+      return z(l.ins) + z(l.del) + z(l.sub) + z(l.swp);
+    };
+    for (auto& p : e.pats) {
+      const DevLimits* l = p.has_limits ? &p.lim : (e.has_limits ? &e.limits : nullptr);
+      max_edits = std::max<uint64_t>(max_edits, l ? edits_of(*l) : 0);
+    }
+    e.max_match_graphemes = (uint64_t)e.max_glen + max_edits;
+    if (e.max_match_graphemes + 4 > 0xFFFFu) {
+      err = "pattern length + edit budget exceeds the 16-bit window span";
+      return FAC_E_UNSUPPORTED;
+    }
+  }
+
+  // ---- bitap pre-filter tables (prefilter.rs:161-245)
+  e.bitap_ok = false;
+  do {
+    if (np == 0) break;
+    float max_sim = 0.f;  // structs.rs:61-76
+    for (int i = 0; i < 128; ++i)
+      for (int j = 0; j < 128; ++j)
+        if (i != j) max_sim = std::fmax(max_sim, e.sim_ascii[i * 128 + j]);
+    for (size_t k = 0; k < e.sim_keys.size(); ++k)
+      if ((e.sim_keys[k] >> 32) != (e.sim_keys[k] & 0xFFFFFFFFull)) max_sim = std::fmax(max_sim, e.sim_vals[k]);
+    float p_sub_min = e.p_sub * (1.0f - max_sim);
+    float mults[4] = {1.0f / e.p_ins, 1.0f / e.p_del, 1.0f / p_sub_min, 2.0f / e.p_swp};
+    bool ok = true;
+    for (float m : mults)
+      if (!std::isfinite(m) || m <= 0.0f) ok = false;
+    if (!ok) break;
+    float ecm = 0.f;
+    for (float m : mults) ecm = std::fmax(ecm, m);
+    std::unordered_map<uint32_t, uint32_t> sym_of_gid;  // gid -> symbol id
+    std::vector<std::vector<uint32_t>> ids(np);
+    for (uint64_t i = 0; i < np && ok; ++i) {
+      size_t m = pat_gids[i].size();
+      if (m == 0 || m > 63) { ok = false; break; }
+      for (uint32_t g : pat_gids[i]) {
+        auto it = sym_of_gid.find(g);
+        uint32_t id;
+        if (it == sym_of_gid.end()) {
+          id = (uint32_t)sym_of_gid.size() + 1;
+          sym_of_gid.emplace(g, id);
+        } else {
+          id = it->second;
+        }
+        if (id > 255) { ok = false; break; }
+        ids[i].push_back(id);
+      }
+    }
+    if (!ok) break;
+    e.edit_cost_mult = ecm;
+    e.alphabet = (uint32_t)sym_of_gid.size();
+    e.symbol_ids.clear();
+    for (auto& kv : sym_of_gid) e.symbol_ids.push_back({gstr[kv.first], kv.second});
+    std::sort(e.symbol_ids.begin(), e.symbol_ids.end());
+    std::memset(e.ascii_id, 0, sizeof(e.ascii_id));
+    for (int b = 0; b < 128; ++b) {
+      uint32_t ch = (uint32_t)b;
+      if (e.case_insensitive && ch >= 'A' && ch <= 'Z') ch += 32;
+      std::u32string key(1, (char32_t)ch);
+      auto it = gid_of.find(key);
+      if (it != gid_of.end()) {
+        auto s = sym_of_gid.find(it->second);
+        if (s != sym_of_gid.end()) e.ascii_id[b] = (uint8_t)s->second;
+      }
+    }
+    e.bp_m.assign(np, 0);
+    e.bp_weight.assign(np, 0.f);
+    e.bp_k_limit.assign(np, -1);
+    e.bp_mask.assign(np * (e.alphabet + 1), 0);
+    for (uint64_t i = 0; i < np; ++i) {
+      e.bp_m[i] = (uint32_t)ids[i].size();
+      e.bp_weight[i] = e.pats[i].weight;
+      const DevLimits* l = e.pats[i].has_limits ? &e.pats[i].lim : (e.has_limits ? &e.limits : nullptr);
+      if (l) {  // k_from_limits (prefilter.rs:388-405)
+        if (l->edits != LIM_NONE) e.bp_k_limit[i] = l->swp == 0 ? l->edits : 2 * (int64_t)l->edits;
+        else if (l->ins != LIM_NONE && l->del != LIM_NONE && l->sub != LIM_NONE && l->swp != LIM_NONE)
+          e.bp_k_limit[i] = (int64_t)l->ins + l->del + l->sub + 2 * (int64_t)l->swp;
+      }
+      for (size_t k = 0; k < ids[i].size(); ++k) e.bp_mask[i * (e.alphabet + 1) + ids[i][k]] |= 1ull << k;
+    }
+    e.bitap_ok = true;
+  } while (false);
+  return FAC_OK;
+}
+
+}  // namespace fac

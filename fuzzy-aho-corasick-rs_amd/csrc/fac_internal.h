@@ -1,0 +1,212 @@
+// fac_internal.h — host/device data layout of the MI355X fuzzy Aho–Corasick engine.
+//
+// The reference keeps a `Vec<Node>` of 112-byte nodes, each owning two heap `Vec`s and a
+// hash map (structs.rs:249-281). On MI355X the automaton is flattened into structure-of-arrays
+// tables that stay L2-resident (≈1-5 MB at 10K patterns) and are read with wave-uniform loads:
+//
+//   DevNode[N]   32 B  prune_len, prune_len_over_weight, edge range, output range, pattern_index
+//   DevEdge[E]    8 B  first code point | target node + (child-has-output, single-byte) flag bits
+//   sb_bits[N]   16 B  128-bit map of the node's single-ASCII-byte edge chars (structs.rs:471-493)
+//   out_pat[O]    4 B  output pattern ids (own + fail-merged, builder.rs:235,264-268)
+//   DevPattern[P]32 B  grapheme_len as f32, weight, per-pattern limits
+//   sim_ascii  64 KiB  128x128 f32 similarity table (structs.rs:36-48) + sorted non-ASCII pairs
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/fac.h"
+
+namespace fac {
+
+// ---------------------------------------------------------------- unicode.cpp
+uint32_t utf8_decode(const uint8_t* s, uint64_t n, uint64_t& i);
+bool utf8_valid(const uint8_t* s, uint64_t n);
+void segment_graphemes(const uint8_t* s, uint64_t n, std::vector<uint64_t>& starts);
+int lower_full(uint32_t cp, uint32_t out[3]);
+void fold_grapheme(const uint8_t* s, uint64_t b, uint64_t e, bool ci, std::u32string& out);
+uint32_t fold_first_char(const uint8_t* s, uint64_t b, uint64_t e, bool ci);
+
+// ---------------------------------------------------------------- device layout
+constexpr uint32_t EDGE_SINGLE_BYTE = 1u << 31;
+constexpr uint32_t EDGE_CHILD_OUTPUT = 1u << 30;
+constexpr uint32_t EDGE_NEXT_MASK = (1u << 30) - 1;
+constexpr int32_t LIM_NONE = -1;
+
+struct alignas(16) DevNode {
+  float prune_len;
+  float prune_lw;
+  uint32_t edge_begin, edge_end;
+  uint32_t out_begin, out_end;
+  int32_t pidx;  // pattern_index (first pattern touching the node), -1 = None
+  uint32_t pad;
+};
+static_assert(sizeof(DevNode) == 32, "DevNode layout");
+
+struct DevEdge {
+  uint32_t ch;    // first char of the folded grapheme
+  uint32_t next;  // target | EDGE_CHILD_OUTPUT | EDGE_SINGLE_BYTE
+};
+
+struct DevLimits {
+  int32_t ins, del, sub, swp, edits;  // LIM_NONE = None
+};
+
+struct alignas(16) DevPattern {
+  float glen;    // grapheme_len as f32 (search.rs:696)
+  float weight;  // Pattern::weight
+  int32_t has_limits;
+  DevLimits lim;
+};
+static_assert(sizeof(DevPattern) == 32, "DevPattern layout");
+
+// Dedup entry / queued state, 16 B. j and matched_end are stored relative to the window start
+// (matched_start == start for every state of a window).
+struct KState {
+  uint32_t node;
+  uint32_t jm;     // j_rel | me_rel << 16
+  float pen;
+  uint32_t packed;  // ins | del << 8 | sub << 16 | swp << 24 (structs.rs:173-176)
+};
+
+// A (sub)haystack searched as if it were the whole `haystack` argument of search_raw: the prefilter
+// re-searches merged windows as independent slices (prefilter.rs:346-350), shards of one haystack
+// keep the global length but only own a window range, and batches hold several haystacks.
+struct SegDesc {
+  uint64_t text_base;  // ascii: byte index of local grapheme 0 in `utf8`; unicode: grapheme index
+  uint64_t n;          // text_len of the (sub)haystack (search.rs:440)
+  uint64_t avail;      // local graphemes resident (>= every j the windows can reach, else ERR_HALO)
+  uint64_t hay_len;    // byte length of the (sub)haystack (end_byte when me >= n, search.rs:672-676)
+  uint64_t byte_base;  // global byte offset of local byte 0 (added to every output offset)
+  uint64_t w_begin, w_end;  // local start windows to search
+  uint32_t ascii;      // 1: grapheme == byte (AsciiGraphemes), 0: Unicode graphemes
+  uint32_t pad;
+};
+
+struct SearchParams {
+  // automaton
+  const DevNode* nodes;
+  const DevEdge* edges;
+  const uint32_t* out_pat;
+  const uint4* sb_bits;
+  const DevPattern* pats;
+  const float* sim_ascii;
+  const uint64_t* sim_keys;  // (a << 32 | b), sorted
+  const float* sim_vals;
+  uint32_t n_sim;
+  // haystack storage
+  const uint8_t* utf8;     // raw bytes (ascii segments read graphemes from here)
+  const uint32_t* text32;  // folded first code point per grapheme (unicode segments)
+  const uint64_t* off;     // global byte offset per grapheme (unicode segments)
+  const SegDesc* segs;
+  const uint64_t* seg_prefix;  // exclusive prefix of (w_end - w_begin), n_segs + 1 entries
+  uint32_t n_segs;
+  uint64_t total_windows;
+  int32_t case_insensitive;
+  // scoring
+  float thr;
+  float max_penalties;
+  float p_ins, p_del, p_sub, p_swp;
+  float min_sym;
+  uint32_t mef;  // MAX_EDITS_FAST (1..6) or 255
+  int32_t has_glim;
+  DevLimits glim;
+  int32_t has_pattern_limits;
+  uint32_t beam;  // 0 = None
+  int32_t window_skip;
+  uint32_t first_bits[4], second_bits[4];
+  // work distribution / outputs
+  uint32_t chunk;
+  uint32_t ecap;            // per-wave emission list capacity
+  uint4* ebuf;              // per-wave emission scratch
+  fac_match* out;
+  uint64_t out_cap;
+  unsigned long long* counters;  // [0] = matches, [1] = states popped, [2] = error flags
+};
+
+constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8u, ERR_OUT = 16u;
+
+// ---------------------------------------------------------------- engine
+struct Engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  fac_config cfg{};
+  bool case_insensitive = false;
+  bool has_limits = false;
+  DevLimits limits{LIM_NONE, LIM_NONE, LIM_NONE, LIM_NONE, LIM_NONE};
+  bool has_pattern_limits = false;
+  uint32_t max_edits_fast = 0;
+  uint32_t mef = 255;
+  uint64_t beam_width = 0;
+  bool has_auto_beam = false;
+  uint64_t ab_budget = 0, ab_width = 0;
+  float p_ins, p_del, p_sub, p_swp, min_sym;
+  // host tables
+  std::vector<DevNode> nodes;
+  std::vector<DevEdge> edges;
+  std::vector<uint32_t> out_pat;
+  std::vector<uint4> sb_bits;
+  std::vector<DevPattern> pats;
+  std::vector<float> sim_ascii;
+  std::vector<uint64_t> sim_keys;
+  std::vector<float> sim_vals;
+  uint32_t max_degree = 0;
+  uint32_t max_glen = 0;
+  uint64_t max_match_graphemes = 0;
+  bool window_skip = false;
+  uint32_t first_bits[4] = {0, 0, 0, 0}, second_bits[4] = {0, 0, 0, 0};
+  // prefilter (prefilter.rs:69-93)
+  bool bitap_ok = false;
+  float edit_cost_mult = 0.f;
+  uint8_t ascii_id[128] = {0};
+  std::vector<std::pair<std::u32string, uint32_t>> symbol_ids;  // sorted by key
+  uint32_t alphabet = 0;
+  std::vector<uint32_t> bp_m;
+  std::vector<float> bp_weight;
+  std::vector<int64_t> bp_k_limit;  // -1 = None
+  std::vector<uint64_t> bp_mask;    // P x (alphabet+1)
+  // device copies
+  DevNode* d_nodes = nullptr;
+  DevEdge* d_edges = nullptr;
+  uint32_t* d_out_pat = nullptr;
+  uint4* d_sb = nullptr;
+  DevPattern* d_pats = nullptr;
+  float* d_sim_ascii = nullptr;
+  uint64_t* d_sim_keys = nullptr;
+  float* d_sim_vals = nullptr;
+  uint64_t* d_bp_mask = nullptr;
+  uint8_t* d_ascii_id = nullptr;
+  std::mutex mu;  // guards lazily grown scratch below
+};
+
+struct Haystack {
+  bool ascii = true;
+  uint64_t len = 0;  // bytes
+  uint64_t n = 0;    // graphemes
+  uint8_t* d_utf8 = nullptr;
+  uint32_t* d_text32 = nullptr;  // Unicode only
+  uint64_t* d_off = nullptr;     // Unicode only
+  std::vector<uint8_t> utf8;     // host copy (prefilter slices re-decide is_ascii)
+  std::vector<uint64_t> starts;  // grapheme byte starts (Unicode only)
+  std::vector<uint8_t> sym;      // prefilter symbol ids per grapheme (Unicode only)
+  int device = 0;
+};
+
+// builder.cpp
+int build_engine(const fac_pattern* pats, uint64_t n, const fac_config* cfg, Engine& e, std::string& err);
+// search_kernels.hip
+int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs, float thr,
+                  hipStream_t stream, std::vector<fac_match>& out, fac_stats* stats, std::string& err);
+// bitap pre-filter: candidate windows (grapheme ranges, merged) for a staged haystack
+int prefilter_windows(const Engine& e, const Haystack& h, const std::vector<uint32_t>& ks, hipStream_t stream,
+                      std::vector<std::pair<uint64_t, uint64_t>>& windows, fac_stats* stats, std::string& err);
+int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack& h, std::string& err);
+void free_haystack(Haystack& h);
+int upload_engine(Engine& e, std::string& err);
+void free_engine_device(Engine& e);
+
+}  // namespace fac

@@ -1,0 +1,1061 @@
+// search_kernels.hip — CDNA4 (gfx950) kernels for the per-start-window fuzzy automaton search
+// and the bit-parallel pre-filter.
+//
+// Reference hot path: FuzzyAhoCorasick::search_unsorted_impl (src/search.rs:418-1119). For every
+// grapheme position `start` the reference restarts a FIFO breadth-first exploration of
+// (node, j, matched_end, penalties, edit counts) states from the trie root, deduplicates states
+// per window (search.rs:608-628), prunes against per-node ceilings (:638-642), emits
+// best-per-(start,end,pattern) matches (:659-737) and fans out exact / substitution / swap /
+// insertion / deletion successors (:742-1089), optionally beaming the frontier (:577-589).
+//
+// MI355X mapping:
+//   * windows are independent (the best-map key holds the start byte), so they are the unit of
+//     parallelism; `bfs_window_kernel` gives each start window to ONE wavefront;
+//   * the wave pops states in exact FIFO order (so beam cuts and dedup see the reference's
+//     sequence), while its 64 lanes evaluate the popped state's edges in parallel; pushes are
+//     compacted in edge order with ballot + mbcnt, so the queue order equals the reference's
+//     push order;
+//   * the frontier ring and the dedup table live in LDS (per-wave slices), probed 64 slots at a
+//     time; per-node data is read with wave-uniform loads from L2-resident tables;
+//   * every f32 expression keeps the reference's operation order with no contraction
+//     (-ffp-contract=off plus explicit __fmul_rn/__fsub_rn/__fadd_rn/__fdiv_rn).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "fac_internal.h"
+
+namespace fac {
+namespace {
+
+constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint32_t prefix_below(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int l) { return (uint32_t)__shfl((int)v, l, 64); }
+__device__ __forceinline__ float shfl_f32(float v, int l) { return __shfl(v, l, 64); }
+__device__ __forceinline__ int first_lane(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
+
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t edits_of(uint32_t packed) {
+  return (packed & 0xFFu) + ((packed >> 8) & 0xFFu) + ((packed >> 16) & 0xFFu) + (packed >> 24);
+}
+
+__device__ __forceinline__ uint32_t total_order_key(float f) {  // f32::total_cmp as a u32 order
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ bool lim_lt(int32_t m, uint32_t v) { return m == LIM_NONE || (int32_t)v < m; }
+__device__ __forceinline__ bool lim_le(int32_t m, uint32_t v) { return m == LIM_NONE || (int32_t)v <= m; }
+
+struct Lim {  // Option<&FuzzyLimits> by value
+  bool has;
+  DevLimits l;
+};
+
+// limits.or(self.limits.as_ref()) (search.rs:93, 109, 125, 140, 160); `pi` = pattern whose limits
+// apply (-1 = None)
+__device__ __forceinline__ Lim pick_limits(const SearchParams& P, int32_t pi) {
+  if (pi >= 0) return Lim{true, P.pats[pi].lim};
+  return Lim{P.has_glim != 0, P.glim};
+}
+
+// get_node_limits (search.rs:67-71): the node's pattern, if that pattern has its own limits
+__device__ __forceinline__ int32_t node_limits(const SearchParams& P, uint32_t node) {
+  const int32_t pi = P.nodes[node].pidx;
+  if (pi < 0) return -1;
+  return P.pats[pi].has_limits ? pi : -1;
+}
+
+// get_similarity (search.rs:76-82) -> Similarity::get (structs.rs:82-92)
+__device__ __forceinline__ float similarity(const SearchParams& P, uint32_t a, uint32_t b) {
+  if (a == b) return 1.0f;
+  if (a < 128u && b < 128u) return P.sim_ascii[a * 128u + b];
+  if (P.n_sim == 0) return 0.0f;
+  const uint64_t key = ((uint64_t)a << 32) | b;
+  uint32_t lo = 0, hi = P.n_sim;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (P.sim_keys[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < P.n_sim && P.sim_keys[lo] == key) ? P.sim_vals[lo] : 0.0f;
+}
+
+// text_chars[j] of the (sub)haystack (search.rs:203/302 + grapheme.rs:66-68, 112-119)
+__device__ __forceinline__ uint32_t text_char(const SearchParams& P, const SegDesc& S, uint64_t j, unsigned& err) {
+  if (j >= S.avail) {  // beyond this shard's resident halo: host bug, flag it
+    err |= ERR_HALO;
+    return 0;
+  }
+  if (S.ascii) {
+    uint32_t b = P.utf8[S.text_base + j];
+    if (P.case_insensitive && b - 'A' < 26u) b += 32u;
+    return b;
+  }
+  return P.text32[S.text_base + j];
+}
+
+// gs_byte_offset, relative to the (sub)haystack (grapheme.rs:59-61, 95-97)
+__device__ __forceinline__ uint64_t local_byte(const SearchParams& P, const SegDesc& S, uint64_t g) {
+  if (S.ascii) return g;
+  return P.off[S.text_base + g] - S.byte_base;
+}
+
+// has_matching_edge_char (structs.rs:471-475) via the node's single-byte edge bitmap
+__device__ __forceinline__ bool sb_has(const SearchParams& P, uint32_t node, uint32_t ch) {
+  if (ch >= 128u) return false;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(P.sb_bits);
+  return (w[node * 4u + (ch >> 5)] >> (ch & 31u)) & 1u;
+}
+
+// find_transition_char_no_mappings (structs.rs:512-519): first edge whose first char is `ch`
+__device__ __forceinline__ int64_t goto_char(const SearchParams& P, uint32_t eb, uint32_t ee, uint32_t ch) {
+  const uint32_t lane = lane_id();
+  for (uint32_t base = eb; base < ee; base += 64) {
+    const uint32_t i = base + lane;
+    const bool valid = i < ee;
+    const DevEdge ed = valid ? P.edges[i] : DevEdge{0, 0};
+    const uint64_t m = __ballot(valid && ed.ch == ch);
+    if (m) return (int64_t)(shfl_u32(ed.next, first_lane(m)) & EDGE_NEXT_MASK);
+  }
+  return -1;
+}
+
+// Per-wave best map for one window (search.rs:444, 705-735), in global scratch: the start byte is
+// fixed per window so the key is (matched_end, pattern). Entries: x = me_rel, y = pattern,
+// z = similarity bits, w = packed counts. First-found wins ties; strictly greater replaces.
+struct EmitList {
+  uint4* buf;
+  uint32_t cap;
+  uint32_t n;
+};
+
+__device__ __forceinline__ void wave_mem_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup"); }
+
+__device__ void emit_update(EmitList& L, uint32_t me_rel, uint32_t p, float sim, uint32_t packed, unsigned& err) {
+  const uint32_t lane = lane_id();
+  wave_mem_fence();
+  for (uint32_t base = 0; base < L.n; base += 64) {
+    const uint32_t i = base + lane;
+    uint4 ent = make_uint4(EMPTY, EMPTY, 0, 0);
+    if (i < L.n) ent = L.buf[i];
+    const uint64_t m = __ballot(i < L.n && ent.x == me_rel && ent.y == p);
+    if (m) {
+      const int l = first_lane(m);
+      const float old = __uint_as_float(shfl_u32(ent.z, l));
+      if (sim > old && lane == (uint32_t)l) L.buf[i] = make_uint4(me_rel, p, __float_as_uint(sim), packed);
+      wave_mem_fence();
+      return;
+    }
+  }
+  if (L.n >= L.cap) {
+    err |= ERR_EMIT;
+    return;
+  }
+  if (lane == 0) L.buf[L.n] = make_uint4(me_rel, p, __float_as_uint(sim), packed);
+  L.n += 1;
+  wave_mem_fence();
+}
+
+// Canonical beam: keep the `bw` smallest pending states by (penalty total order,
+// queue position), in queue order — one legal outcome of the reference's
+// `select_nth_unstable_by(bw - 1, total_cmp)` + `truncate(q_idx + bw)` (search.rs:584-587).
+template <uint32_t QCAP>
+__device__ void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t bw) {
+  const uint32_t lane = lane_id();
+  const uint32_t P = tail - head;
+  uint32_t prefix = 0, rank = bw - 1;  // radix-select the key of the bw-th smallest (MSB first)
+  for (int bit = 31; bit >= 0; --bit) {
+    const uint32_t hi_mask = bit == 31 ? 0u : (0xFFFFFFFFu << (bit + 1));
+    uint32_t c0 = 0;
+    for (uint32_t base = 0; base < P; base += 64) {
+      const uint32_t i = base + lane;
+      bool hit = false;
+      if (i < P) {
+        const uint32_t k = total_order_key(q[(head + i) & (QCAP - 1)].pen);
+        hit = ((k & hi_mask) == prefix) && !((k >> bit) & 1u);
+      }
+      c0 += __popcll(__ballot(hit));
+    }
+    if (rank >= c0) {
+      rank -= c0;
+      prefix |= 1u << bit;
+    }
+  }
+  const uint32_t T = prefix, need_eq = rank + 1;  // keep all keys < T and the first need_eq == T
+  uint32_t w = head, eq_seen = 0;
+  for (uint32_t base = 0; base < P; base += 64) {
+    const uint32_t i = base + lane;
+    const bool valid = i < P;
+    KState s{};
+    uint32_t k = 0xFFFFFFFFu;
+    if (valid) {
+      s = q[(head + i) & (QCAP - 1)];
+      k = total_order_key(s.pen);
+    }
+    const bool eq = valid && k == T;
+    const uint64_t meq = __ballot(eq);
+    const bool keep = valid && (k < T || (eq && eq_seen + prefix_below(meq) < need_eq));
+    const uint64_t mk = __ballot(keep);
+    __builtin_amdgcn_wave_barrier();
+    if (keep) q[(w + prefix_below(mk)) & (QCAP - 1)] = s;
+    __builtin_amdgcn_wave_barrier();
+    w += __popcll(mk);
+    eq_seen += __popcll(meq);
+  }
+  tail = head + bw;
+}
+
+// Append the lanes whose `pred` holds, in lane order (= the reference's push order).
+template <uint32_t QCAP>
+__device__ __forceinline__ void push_lanes(KState* q, uint32_t head, uint32_t& tail, bool pred, const KState& s,
+                                           unsigned& err) {
+  const uint64_t m = __ballot(pred);
+  if (!m) return;
+  const uint32_t cnt = __popcll(m);
+  if (tail + cnt - head > QCAP) {
+    err |= ERR_QUEUE;
+    return;
+  }
+  if (pred) q[(tail + prefix_below(m)) & (QCAP - 1)] = s;
+  tail += cnt;
+}
+
+__device__ __forceinline__ uint32_t vis_hash(const KState& s) {
+  uint32_t h = s.node * 0x9E3779B1u;
+  h ^= s.jm * 0x85EBCA77u + (h >> 13);
+  h ^= s.packed * 0xC2B2AE3Du + (h >> 16);
+  h ^= h >> 15;
+  return h;
+}
+
+// State dedup (search.rs:608-628). Returns true when the state must be skipped.
+template <uint32_t VCAP>
+__device__ __forceinline__ bool visited_check(KState* vis, uint32_t& vcount, const KState& s, bool exact_needed,
+                                              unsigned& err) {
+  const uint32_t lane = lane_id();
+  const uint32_t h = vis_hash(s);
+  for (uint32_t probe = 0; probe < VCAP; probe += 64) {
+    const uint32_t slot = (h + probe + lane) & (VCAP - 1);
+    const KState e = vis[slot];
+    const bool is_empty = e.node == EMPTY;
+    const bool is_match = !is_empty && e.node == s.node && e.jm == s.jm && e.packed == s.packed;
+    const uint64_t me = __ballot(is_empty), mm = __ballot(is_match);
+    const int fe = me ? first_lane(me) : 64;
+    const int fm = mm ? first_lane(mm) : 64;
+    if (fm < fe) {
+      const float stored = shfl_f32(e.pen, fm);
+      if (stored <= s.pen) return true;
+      if (lane == (uint32_t)fm) vis[slot].pen = s.pen;
+      return false;
+    }
+    if (fe < 64) {
+      if (vcount + 1 >= VCAP - VCAP / 8) {  // table "full": keep probe chains short
+        if (exact_needed) err |= ERR_VISITED;
+        return false;  // without a beam, expanding a duplicate cannot change results
+      }
+      if (lane == (uint32_t)fe) vis[slot] = s;
+      vcount += 1;
+      return false;
+    }
+  }
+  if (exact_needed) err |= ERR_VISITED;
+  return false;
+}
+
+// One start window, explored by one wavefront.
+template <uint32_t VCAP, uint32_t QCAP>
+__device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, EmitList& EL,
+                           uint64_t start, uint64_t& popped, unsigned& err) {
+  const uint32_t lane = lane_id();
+  const bool fast = P.mef != 255u;
+  const uint64_t n = S.n;
+  for (uint32_t i = lane; i < VCAP; i += 64) vis[i].node = EMPTY;
+  uint32_t vcount = 0;
+  EL.n = 0;
+  uint32_t head = 0, tail = 1;
+  if (lane == 0) q[0] = KState{0u, 0u, 0.0f, 0u};
+  __builtin_amdgcn_wave_barrier();
+
+  while (head < tail) {
+    if (P.beam && tail - head > 2u * P.beam) beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
+    const KState st = q[head & (QCAP - 1)];
+    head += 1;
+    popped += 1;
+    if (visited_check<VCAP>(vis, vcount, st, P.beam != 0, err)) continue;  // :608-628
+
+    const DevNode nd = P.nodes[st.node];
+    const float pen = st.pen;
+    if (pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr))) continue;  // :638-642
+    const float remaining = __fsub_rn(P.max_penalties, pen);                     // :648
+    const uint32_t packed = st.packed;
+    const uint32_t edits = edits_of(packed);
+    const uint32_t j_rel = st.jm & 0xFFFFu, me_rel = st.jm >> 16;
+    const uint64_t j = start + j_rel;
+    const int32_t nlim = P.has_pattern_limits ? node_limits(P, st.node) : -1;  // :653-657
+
+    // ---- emission (:659-737)
+    if (nd.out_begin != nd.out_end) {
+      const uint32_t ins = packed & 0xFFu, del = (packed >> 8) & 0xFFu, sub = (packed >> 16) & 0xFFu,
+                     swp = packed >> 24;
+      for (uint32_t base = nd.out_begin; base < nd.out_end; base += 64) {
+        const uint32_t i = base + lane;
+        bool ok = i < nd.out_end;
+        uint32_t p = 0;
+        float sim = 0.f;
+        if (ok) {
+          p = P.out_pat[i];
+          const DevPattern pt = P.pats[p];
+          if (fast) {
+            ok = edits <= P.mef;
+          } else {  // within_limits (:151-169)
+            const Lim m = pick_limits(P, pt.has_limits ? (int32_t)p : -1);
+            ok = m.has ? (lim_le(m.l.edits, edits) && lim_le(m.l.ins, ins) && lim_le(m.l.del, del) &&
+                          lim_le(m.l.sub, sub) && lim_le(m.l.swp, swp))
+                       : (edits == 0);
+          }
+          if (ok) {
+            const float total = pt.glen;
+            sim = __fmul_rn(__fdiv_rn(__fsub_rn(total, pen), total), pt.weight);  // :696-699
+            ok = !(sim < P.thr);                                                   // :701
+          }
+        }
+        uint64_t m = __ballot(ok);
+        while (m) {
+          const int l = first_lane(m);
+          m &= m - 1;
+          emit_update(EL, me_rel, shfl_u32(p, l), shfl_f32(sim, l), packed, err);
+        }
+      }
+    }
+
+    const bool is_last_edit = fast && edits + 1u >= P.mef;  // :742
+    const uint32_t cur_ch = j < n ? text_char(P, S, j, err) : 0u;
+    if (j < n) {
+      bool have_next = false;
+      uint32_t next_ch = 0;
+      if (is_last_edit && (!fast || edits < P.mef) && j + 1 < n) {  // :758-765
+        have_next = true;
+        next_ch = text_char(P, S, j + 1, err);
+      }
+      // exact transition (:766-798); matched_start stays `start` for every state
+      const int64_t exact_next = goto_char(P, nd.edge_begin, nd.edge_end, cur_ch);
+      const uint32_t jm1 = (j_rel + 1u) | ((j_rel + 1u) << 16);
+      push_lanes<QCAP>(q, head, tail, lane == 0 && exact_next >= 0,
+                       KState{(uint32_t)exact_next, jm1, pen, packed}, err);
+
+      // substitutions (:803-874)
+      bool subst_ok;
+      if (fast) {
+        subst_ok = edits < P.mef;
+      } else {  // within_limits_subst (:134-146)
+        const Lim m = pick_limits(P, nlim);
+        subst_ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.sub, (packed >> 16) & 0xFFu))
+                         : (edits == 0 && ((packed >> 16) & 0xFFu) == 0);
+      }
+      if (subst_ok) {
+        for (uint32_t base = nd.edge_begin; base < nd.edge_end; base += 64) {
+          const uint32_t i = base + lane;
+          bool keep = i < nd.edge_end;
+          KState s{};
+          if (keep) {
+            const DevEdge ed = P.edges[i];
+            const uint32_t child = ed.next & EDGE_NEXT_MASK;
+            keep = !(exact_next >= 0 && child == (uint32_t)exact_next);
+            const float sim = similarity(P, ed.ch, cur_ch);
+            keep = keep && !(sim < P.min_sym);
+            const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
+            keep = keep && !(penalty > remaining);
+            if (keep && is_last_edit)  // dead-end filter (:839-847)
+              keep = (ed.next & EDGE_CHILD_OUTPUT) || (have_next && sb_has(P, child, next_ch));
+            s = KState{child, jm1, __fadd_rn(pen, penalty), packed + 0x10000u};
+          }
+          push_lanes<QCAP>(q, head, tail, keep, s, err);
+        }
+      }
+
+      // swap (:935-989)
+      if (j + 1 < n && P.p_swp <= remaining && (!fast || edits < P.mef)) {
+        const uint32_t nch = have_next ? next_ch : text_char(P, S, j + 1, err);
+        const int64_t x = goto_char(P, nd.edge_begin, nd.edge_end, nch);
+        if (x >= 0) {
+          const DevNode nx = P.nodes[(uint32_t)x];
+          const int64_t node2 = goto_char(P, nx.edge_begin, nx.edge_end, cur_ch);
+          bool ok = node2 >= 0;
+          if (ok && !fast) {  // within_limits_swap_ahead with node2's limits (:962-967)
+            const Lim m = pick_limits(P, node_limits(P, (uint32_t)node2));
+            ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.swp, packed >> 24)) : false;
+          }
+          const uint32_t jm2 = (j_rel + 2u) | ((j_rel + 2u) << 16);
+          push_lanes<QCAP>(q, head, tail, lane == 0 && ok,
+                           KState{(uint32_t)node2, jm2, __fadd_rn(pen, P.p_swp), packed + 0x1000000u}, err);
+        }
+      }
+
+      // insertion (:994-1029): never before the first consumed grapheme
+      if ((me_rel != 0u || j_rel != 0u) && P.p_ins <= remaining) {
+        bool ok;
+        if (fast) {
+          ok = edits < P.mef;
+        } else {
+          const Lim m = pick_limits(P, nlim);
+          ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.ins, packed & 0xFFu)) : false;
+        }
+        if (ok && is_last_edit && nd.out_begin == nd.out_end && !(have_next && sb_has(P, st.node, next_ch)))
+          ok = false;
+        const uint32_t jmi = (j_rel + 1u) | (me_rel << 16);
+        push_lanes<QCAP>(q, head, tail, lane == 0 && ok, KState{st.node, jmi, __fadd_rn(pen, P.p_ins), packed + 1u},
+                         err);
+      }
+    }
+
+    // deletion (:1035-1089), allowed even at j == n
+    if (P.p_del <= remaining) {
+      bool ok;
+      if (fast) {
+        ok = edits < P.mef;
+      } else {
+        const Lim m = pick_limits(P, nlim);
+        ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.del, (packed >> 8) & 0xFFu)) : false;
+      }
+      if (ok) {
+        const bool have_cur = is_last_edit && j < n;
+        const float npen = __fadd_rn(pen, P.p_del);
+        for (uint32_t base = nd.edge_begin; base < nd.edge_end; base += 64) {
+          const uint32_t i = base + lane;
+          bool keep = i < nd.edge_end;
+          uint32_t child = 0;
+          if (keep) {
+            const DevEdge ed = P.edges[i];
+            child = ed.next & EDGE_NEXT_MASK;
+            if (is_last_edit)  // dead-end filter (:1057-1063)
+              keep = (ed.next & EDGE_CHILD_OUTPUT) || (have_cur && sb_has(P, child, cur_ch));
+          }
+          push_lanes<QCAP>(q, head, tail, keep, KState{child, st.jm, npen, packed + 0x100u}, err);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (wave_or(err) & (ERR_QUEUE | ERR_VISITED | ERR_EMIT | ERR_HALO)) break;
+  }
+
+  // flush this window's best map (search.rs:1111-1118)
+  wave_mem_fence();
+  if (EL.n && !(err & ERR_EMIT)) {
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(P.counters, (unsigned long long)EL.n);
+    base = (unsigned long long)__shfl((long long)base, 0, 64);
+    const uint64_t sb = S.byte_base + local_byte(P, S, start);
+    for (uint32_t i = lane; i < EL.n; i += 64) {
+      if (base + i >= P.out_cap) break;
+      const uint4 ent = EL.buf[i];
+      const uint64_t me = start + ent.x;
+      fac_match m;
+      m.start = sb;
+      m.end = S.byte_base + (me < n ? local_byte(P, S, me) : S.hay_len);
+      m.pattern_index = ent.y;
+      m.similarity = __uint_as_float(ent.z);
+      m.insertions = ent.w & 0xFFu;
+      m.deletions = (ent.w >> 8) & 0xFFu;
+      m.substitutions = (ent.w >> 16) & 0xFFu;
+      m.swaps = ent.w >> 24;
+      m.edits = (uint8_t)edits_of(ent.w);
+      m.pad[0] = m.pad[1] = m.pad[2] = 0;
+      P.out[base + i] = m;
+    }
+  }
+}
+
+// 2-gram window skip (search.rs:535-553)
+__device__ __forceinline__ bool window_skipped(const SearchParams& P, const SegDesc& S, uint64_t s, unsigned& err) {
+  if (!P.window_skip) return false;
+  const uint32_t ch = text_char(P, S, s, err);
+  if (ch < 128u && !((P.first_bits[ch >> 5] >> (ch & 31u)) & 1u)) {
+    if (s + 1 >= S.n) return true;
+    const uint32_t nc = text_char(P, S, s + 1, err);
+    if (nc < 128u && !((P.second_bits[nc >> 5] >> (nc & 31u)) & 1u)) return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ uint32_t find_seg(const SearchParams& P, uint64_t v) {
+  uint32_t lo = 0, hi = P.n_segs;  // last k with prefix[k] <= v
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (P.seg_prefix[mid] <= v) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <uint32_t VCAP, uint32_t QCAP>
+__global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
+  __shared__ KState s_vis[VCAP];
+  __shared__ KState s_q[QCAP];
+  const uint32_t lane = lane_id();
+  EmitList EL{P.ebuf + (size_t)blockIdx.x * P.ecap, P.ecap, 0};
+  uint64_t popped = 0;
+  unsigned err = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * P.chunk;
+  for (uint64_t cb = (uint64_t)blockIdx.x * P.chunk; cb < P.total_windows; cb += stride) {
+    const uint64_t ce = min(cb + (uint64_t)P.chunk, P.total_windows);
+    for (uint64_t v0 = cb; v0 < ce; v0 += 64) {
+      const uint64_t v = v0 + lane;
+      bool active = v < ce;
+      uint32_t kl = 0;
+      uint64_t start = 0;
+      if (active) {
+        kl = find_seg(P, v);
+        const SegDesc S = P.segs[kl];
+        start = S.w_begin + (v - P.seg_prefix[kl]);
+        active = !window_skipped(P, S, start, err);
+      }
+      uint64_t m = __ballot(active);
+      while (m) {
+        const int l = first_lane(m);
+        m &= m - 1;
+        const uint32_t seg = shfl_u32(kl, l);
+        const uint64_t st = (uint64_t)__shfl((long long)start, l, 64);
+        const SegDesc S = P.segs[seg];
+        run_window<VCAP, QCAP>(P, S, s_vis, s_q, EL, st, popped, err);
+        if (wave_or(err)) break;
+      }
+      if (wave_or(err)) break;
+    }
+    if (wave_or(err)) break;
+  }
+  if (lane == 0) atomicAdd(P.counters + 1, (unsigned long long)popped);
+  const unsigned all = wave_or(err);
+  if (lane == 0 && all) atomicOr(reinterpret_cast<unsigned int*>(P.counters + 2), all);
+}
+
+// ------------------------------------------------------------------------------------------
+// Bit-parallel pre-filter (prefilter.rs:247-435)
+// ------------------------------------------------------------------------------------------
+
+// transcode, ASCII fast path (prefilter.rs:253-260): ids[i] = ascii_id[byte]
+__global__ void transcode_ascii_kernel(const uint8_t* __restrict__ utf8, uint64_t n, const uint8_t* __restrict__ ascii_id,
+                                       uint8_t* __restrict__ ids) {
+  const uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (i0 + 16 <= n) {
+    const uint4 v = *reinterpret_cast<const uint4*>(utf8 + i0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+    for (int q = 0; q < 4; ++q) {
+      uint32_t r = 0;
+      for (int b = 0; b < 4; ++b) r |= (uint32_t)ascii_id[(w[q] >> (8 * b)) & 0x7Fu] << (8 * b);
+      o[q] = r;
+    }
+    *reinterpret_cast<uint4*>(ids + i0) = make_uint4(o[0], o[1], o[2], o[3]);
+  } else {
+    for (uint64_t i = i0; i < n; ++i) ids[i] = ascii_id[utf8[i] & 0x7Fu];
+  }
+}
+
+struct BitapParams {
+  const uint8_t* ids;
+  uint64_t n;
+  const uint64_t* mask_t;  // [(alphabet+1)][P] transposed masks
+  const uint32_t* m;       // pattern length (graphemes)
+  const uint32_t* k;       // edit budget per pattern
+  uint32_t n_pat;
+  uint32_t seg_len;        // text positions owned by one wave
+  uint32_t* cover;         // coverage bitmap, 1 bit per grapheme
+};
+
+// Each lane runs one pattern's shift-AND automaton over the wave's text segment
+// (bitap_windows, prefilter.rs:410-435). The state after `m + k` symbols no longer depends on the
+// initial state, so a segment starts `m + k` symbols early from the reference's initial state and
+// only reports ends inside its own range. Every hit covers [end - m - k, end) in the bitmap;
+// maximal runs of the bitmap are exactly the sorted + merged windows of prefilter.rs:334-342.
+template <int KMAX>
+__global__ __launch_bounds__(256) void bitap_kernel(BitapParams B) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t pat_groups = (B.n_pat + 63) / 64;
+  const uint64_t seg = wave / pat_groups;
+  const uint32_t p = (wave % pat_groups) * 64 + lane;
+  const uint64_t a = seg * B.seg_len;
+  if (a >= B.n) return;
+  const uint64_t b = min(a + (uint64_t)B.seg_len, B.n);
+  const bool live = p < B.n_pat;
+  const uint32_t m = live ? B.m[p] : 1;
+  const uint32_t k = live ? B.k[p] : 0;
+  const uint64_t span = (uint64_t)m + k;
+  const uint64_t match_bit = 1ull << (m - 1);
+  uint64_t r[KMAX + 1];
+#pragma unroll
+  for (int d = 0; d <= KMAX; ++d) r[d] = d == 0 ? 0ull : ((1ull << d) - 1);
+  // Start 87 = 63 + 24 symbols early: from there on the automaton state equals the one obtained by
+  // scanning from the text start (an alignment with <= k errors spans <= m + k symbols).
+  const uint64_t warm = 63 + 24;
+  const uint64_t s0 = a > warm ? a - warm : 0;
+  for (uint64_t i = s0; i < b; ++i) {
+    const uint32_t c = B.ids[i];  // wave-uniform
+    const uint64_t bc = live ? B.mask_t[(uint64_t)c * B.n_pat + p] : 0ull;
+    uint64_t prev_old = r[0];
+    uint64_t prev_new = ((r[0] << 1) | 1ull) & bc;
+    r[0] = prev_new;
+    uint64_t hit_level = (k == 0) ? prev_new : 0ull;
+#pragma unroll
+    for (int d = 1; d <= KMAX; ++d) {
+      const uint64_t old = r[d];
+      const uint64_t nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | 1ull;
+      r[d] = nv;  // levels above k are computed but never read
+      prev_old = old;
+      prev_new = nv;
+      if ((uint32_t)d == k) hit_level = nv;
+    }
+    if (live && i >= a && (hit_level & match_bit)) {  // R[k] subsumes the lower levels
+      const uint64_t end = i + 1;
+      const uint64_t ws = end > span ? end - span : 0;
+      for (uint64_t x = ws; x < end;) {  // set bits [ws, end)
+        const uint64_t word = x >> 5;
+        const uint32_t lo = (uint32_t)(x & 31);
+        const uint32_t cnt = (uint32_t)min((uint64_t)(32 - lo), end - x);
+        const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << lo;
+        atomicOr(B.cover + word, bits);
+        x += cnt;
+      }
+    }
+  }
+}
+
+// Maximal runs of set bits -> [start, end) windows (unordered; the host sorts them).
+__global__ void runs_kernel(const uint32_t* __restrict__ cover, uint64_t n_words, uint64_t n,
+                            unsigned long long* __restrict__ out, unsigned long long* __restrict__ count,
+                            uint64_t cap) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= n_words) return;
+  const uint32_t cur = cover[w];
+  const uint32_t prev_hi = w > 0 ? (cover[w - 1] >> 31) : 0u;
+  uint32_t starts = cur & ~((cur << 1) | prev_hi);  // bit set, previous bit clear
+  while (starts) {
+    const uint32_t b = __ffs(starts) - 1;
+    starts &= starts - 1;
+    const uint64_t s = w * 32 + b;
+    if (s >= n) break;
+    uint64_t e;  // first clear bit at or after s
+    uint64_t ww = w;
+    uint32_t bits = cur | (b ? ((1u << b) - 1u) : 0u);
+    for (;;) {
+      const uint32_t inv = ~bits;
+      if (inv) {
+        e = ww * 32 + (uint64_t)__builtin_ctz(inv);
+        break;
+      }
+      if (++ww >= n_words) {
+        e = n_words * 32;
+        break;
+      }
+      bits = cover[ww];
+    }
+    if (e > n) e = n;
+    const unsigned long long idx = atomicAdd(count, 1ull);
+    if (idx < cap) {
+      out[2 * idx] = s;
+      out[2 * idx + 1] = e;
+    }
+  }
+}
+
+#define HIP_TRY(x)                                          \
+  do {                                                      \
+    hipError_t _e = (x);                                    \
+    if (_e != hipSuccess) {                                 \
+      err = std::string(#x) + ": " + hipGetErrorString(_e); \
+      return FAC_E_HIP;                                     \
+    }                                                       \
+  } while (0)
+
+template <typename T>
+int upload(const std::vector<T>& v, T** d, std::string& err) {
+  *d = nullptr;
+  const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+  HIP_TRY(hipMalloc((void**)d, bytes));
+  if (!v.empty()) HIP_TRY(hipMemcpy(*d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return FAC_OK;
+}
+
+struct Variant {
+  uint32_t vcap, qcap;
+};
+
+hipError_t launch_variant(const Variant& v, uint32_t grid, hipStream_t s, const SearchParams& P) {
+  if (v.vcap == 512 && v.qcap == 512)
+    hipLaunchKernelGGL((bfs_window_kernel<512, 512>), dim3(grid), dim3(64), 0, s, P);
+  else if (v.vcap == 1024 && v.qcap == 1024)
+    hipLaunchKernelGGL((bfs_window_kernel<1024, 1024>), dim3(grid), dim3(64), 0, s, P);
+  else
+    hipLaunchKernelGGL((bfs_window_kernel<2048, 2048>), dim3(grid), dim3(64), 0, s, P);
+  return hipGetLastError();
+}
+
+// RAII for stream-ordered scratch
+struct DevBuf {
+  void* p = nullptr;
+  hipStream_t s = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFreeAsync(p, s);
+  }
+  hipError_t alloc(size_t bytes, hipStream_t stream) {
+    if (p) (void)hipFreeAsync(p, s);
+    s = stream;
+    return hipMallocAsync(&p, std::max<size_t>(bytes, 16), stream);
+  }
+};
+
+struct Events {
+  hipEvent_t a = nullptr, b = nullptr;
+  ~Events() {
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+  }
+};
+
+}  // namespace
+
+int upload_engine(Engine& e, std::string& err) {
+  HIP_TRY(hipSetDevice(e.device));
+  if (!e.stream) HIP_TRY(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
+  int rc;
+  if ((rc = upload(e.nodes, &e.d_nodes, err))) return rc;
+  if ((rc = upload(e.edges, &e.d_edges, err))) return rc;
+  if ((rc = upload(e.out_pat, &e.d_out_pat, err))) return rc;
+  if ((rc = upload(e.sb_bits, &e.d_sb, err))) return rc;
+  if ((rc = upload(e.pats, &e.d_pats, err))) return rc;
+  if ((rc = upload(e.sim_ascii, &e.d_sim_ascii, err))) return rc;
+  if ((rc = upload(e.sim_keys, &e.d_sim_keys, err))) return rc;
+  if ((rc = upload(e.sim_vals, &e.d_sim_vals, err))) return rc;
+  if (e.bitap_ok) {
+    // transposed masks [(alphabet+1)][P] so the lanes of a wave (consecutive patterns) coalesce
+    const size_t np = e.bp_m.size(), A = e.alphabet + 1;
+    std::vector<uint64_t> mt(A * np);
+    for (size_t p = 0; p < np; ++p)
+      for (size_t c = 0; c < A; ++c) mt[c * np + p] = e.bp_mask[p * A + c];
+    if ((rc = upload(mt, &e.d_bp_mask, err))) return rc;
+    std::vector<uint8_t> aid(e.ascii_id, e.ascii_id + 128);
+    if ((rc = upload(aid, &e.d_ascii_id, err))) return rc;
+  }
+  return FAC_OK;
+}
+
+void free_engine_device(Engine& e) {
+  if (e.d_nodes == nullptr && e.stream == nullptr) return;
+  (void)hipSetDevice(e.device);
+  void* ptrs[] = {e.d_nodes, e.d_edges, e.d_out_pat, e.d_sb, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
+                  e.d_sim_vals, e.d_bp_mask, e.d_ascii_id};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (e.stream) (void)hipStreamDestroy(e.stream);
+  e.stream = nullptr;
+  e.d_nodes = nullptr;
+}
+
+int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack& h, std::string& err) {
+  h.device = e.device;
+  h.len = len;
+  h.ascii = true;
+  for (uint64_t i = 0; i < len; ++i)
+    if (utf8[i] & 0x80) {
+      h.ascii = false;
+      break;
+    }
+  h.utf8.assign(utf8, utf8 + len);
+  if (h.ascii) {
+    h.n = len;
+  } else {
+    segment_graphemes(utf8, len, h.starts);  // search.rs:398-416
+    h.n = h.starts.size();
+  }
+  if (h.n > 0xFFFFFFFFull) return FAC_E_HAYSTACK_TOO_LARGE;
+  HIP_TRY(hipSetDevice(e.device));
+  HIP_TRY(hipMalloc((void**)&h.d_utf8, std::max<uint64_t>(len, 16)));
+  if (len) HIP_TRY(hipMemcpy(h.d_utf8, utf8, len, hipMemcpyHostToDevice));
+  if (!h.ascii) {
+    std::vector<uint32_t> tc(h.n);
+    for (uint64_t g = 0; g < h.n; ++g) {
+      const uint64_t b = h.starts[g], en = g + 1 < h.n ? h.starts[g + 1] : len;
+      tc[g] = fold_first_char(utf8, b, en, e.case_insensitive);
+    }
+    HIP_TRY(hipMalloc((void**)&h.d_text32, std::max<uint64_t>(h.n * 4, 16)));
+    HIP_TRY(hipMemcpy(h.d_text32, tc.data(), h.n * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc((void**)&h.d_off, std::max<uint64_t>(h.n * 8, 16)));
+    HIP_TRY(hipMemcpy(h.d_off, h.starts.data(), h.n * 8, hipMemcpyHostToDevice));
+    if (e.bitap_ok) {  // transcode, grapheme path (prefilter.rs:262-280)
+      h.sym.assign(h.n, 0);
+      std::u32string g;
+      for (uint64_t i = 0; i < h.n; ++i) {
+        const uint64_t b = h.starts[i], en = i + 1 < h.n ? h.starts[i + 1] : len;
+        fold_grapheme(utf8, b, en, e.case_insensitive, g);
+        auto it = std::lower_bound(e.symbol_ids.begin(), e.symbol_ids.end(), std::make_pair(g, 0u));
+        if (it != e.symbol_ids.end() && it->first == g) h.sym[i] = (uint8_t)it->second;
+      }
+    }
+  }
+  return FAC_OK;
+}
+
+void free_haystack(Haystack& h) {
+  (void)hipSetDevice(h.device);
+  if (h.d_utf8) (void)hipFree(h.d_utf8);
+  if (h.d_text32) (void)hipFree(h.d_text32);
+  if (h.d_off) (void)hipFree(h.d_off);
+  h.d_utf8 = nullptr;
+  h.d_text32 = nullptr;
+  h.d_off = nullptr;
+}
+
+int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs_in, float thr,
+                  hipStream_t stream, std::vector<fac_match>& out, fac_stats* stats, std::string& err) {
+  out.clear();
+  HIP_TRY(hipSetDevice(e.device));
+  if (!stream) stream = e.stream;
+  std::vector<SegDesc> segs;
+  std::vector<uint64_t> prefix(1, 0);
+  for (const SegDesc& s : segs_in) {
+    SegDesc c = s;
+    c.w_end = std::min(c.w_end, c.n);
+    if (c.w_begin >= c.w_end) continue;
+    segs.push_back(c);
+    prefix.push_back(prefix.back() + (c.w_end - c.w_begin));
+  }
+  const uint64_t windows = prefix.back();
+  if (windows == 0) return FAC_OK;
+
+  SearchParams P{};
+  P.nodes = e.d_nodes;
+  P.edges = e.d_edges;
+  P.out_pat = e.d_out_pat;
+  P.sb_bits = e.d_sb;
+  P.pats = e.d_pats;
+  P.sim_ascii = e.d_sim_ascii;
+  P.sim_keys = e.d_sim_keys;
+  P.sim_vals = e.d_sim_vals;
+  P.n_sim = (uint32_t)e.sim_keys.size();
+  P.utf8 = h.d_utf8;
+  P.text32 = h.d_text32;
+  P.off = h.d_off;
+  P.n_segs = (uint32_t)segs.size();
+  P.total_windows = windows;
+  P.case_insensitive = e.case_insensitive;
+  P.thr = thr;
+  {  // search.rs:486-487, evaluated as two rounded f32 operations like the reference
+    volatile float prod = e.nodes[0].prune_lw * thr;
+    P.max_penalties = e.nodes[0].prune_len - prod;
+  }
+  P.p_ins = e.p_ins;
+  P.p_del = e.p_del;
+  P.p_sub = e.p_sub;
+  P.p_swp = e.p_swp;
+  P.min_sym = e.min_sym;
+  P.mef = e.mef;
+  P.has_glim = e.has_limits;
+  P.glim = e.limits;
+  P.has_pattern_limits = e.has_pattern_limits;
+  P.beam = (uint32_t)std::min<uint64_t>(e.beam_width, 0xFFFFFFFFull);
+  P.window_skip = e.window_skip;
+  std::memcpy(P.first_bits, e.first_bits, sizeof(P.first_bits));
+  std::memcpy(P.second_bits, e.second_bits, sizeof(P.second_bits));
+  P.chunk = 256;
+  P.ecap = 1024;
+
+  int cus = 256;
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
+  const uint64_t want = (windows + P.chunk - 1) / P.chunk;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * 16));
+
+  const uint64_t fan = 3ull + 2ull * e.max_degree;  // one state's fan-out bound
+  const Variant variants[] = {{512, 512}, {1024, 1024}, {2048, 2048}};
+  size_t vi = 0;
+  if (P.beam) {
+    while (vi < 3 && 2ull * P.beam + fan + 1 > variants[vi].qcap) ++vi;
+    if (vi == 3) {
+      err = "beam width too large for the on-chip frontier";
+      return FAC_E_UNSUPPORTED;
+    }
+  }
+
+  DevBuf d_segs, d_prefix, d_out, d_ebuf, d_cnt;
+  HIP_TRY(d_segs.alloc(segs.size() * sizeof(SegDesc), stream));
+  HIP_TRY(d_prefix.alloc(prefix.size() * sizeof(uint64_t), stream));
+  HIP_TRY(hipMemcpyAsync(d_segs.p, segs.data(), segs.size() * sizeof(SegDesc), hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(d_prefix.p, prefix.data(), prefix.size() * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+  uint64_t out_cap = std::max<uint64_t>(4096, windows / 64);
+  HIP_TRY(d_ebuf.alloc((size_t)grid * P.ecap * sizeof(uint4), stream));
+  HIP_TRY(d_cnt.alloc(4 * sizeof(unsigned long long), stream));
+  HIP_TRY(d_out.alloc(out_cap * sizeof(fac_match), stream));
+  Events ev;
+  HIP_TRY(hipEventCreate(&ev.a));
+  HIP_TRY(hipEventCreate(&ev.b));
+  P.segs = static_cast<const SegDesc*>(d_segs.p);
+  P.seg_prefix = static_cast<const uint64_t*>(d_prefix.p);
+
+  int rc = FAC_OK;
+  uint64_t retries = 0, launches = 0;
+  unsigned long long cnt[4] = {0, 0, 0, 0};
+  float ms_total = 0.f;
+  for (;;) {
+    P.ebuf = static_cast<uint4*>(d_ebuf.p);
+    P.out = static_cast<fac_match*>(d_out.p);
+    P.out_cap = out_cap;
+    P.counters = static_cast<unsigned long long*>(d_cnt.p);
+    HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 4 * sizeof(unsigned long long), stream));
+    HIP_TRY(hipEventRecord(ev.a, stream));
+    const hipError_t le = launch_variant(variants[vi], grid, stream, P);
+    if (le != hipSuccess) {
+      err = std::string("kernel launch: ") + hipGetErrorString(le);
+      rc = FAC_E_HIP;
+      break;
+    }
+    HIP_TRY(hipEventRecord(ev.b, stream));
+    HIP_TRY(hipMemcpyAsync(cnt, d_cnt.p, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+    ms_total += ms;
+    launches += 1;
+    const unsigned flags = (unsigned)cnt[2];
+    if (flags & ERR_HALO) {
+      err = "haystack shard does not hold the halo its windows need";
+      rc = FAC_E_INVALID;
+      break;
+    }
+    if (flags & (ERR_QUEUE | ERR_VISITED)) {
+      if (vi + 1 < 3) {
+        ++vi;
+        ++retries;
+        continue;
+      }
+      err = "per-window frontier exceeded the on-chip capacity";
+      rc = FAC_E_CAPACITY;
+      break;
+    }
+    if (flags & ERR_EMIT) {
+      if (P.ecap < (1u << 20)) {
+        P.ecap *= 8;
+        HIP_TRY(d_ebuf.alloc((size_t)grid * P.ecap * sizeof(uint4), stream));
+        ++retries;
+        continue;
+      }
+      err = "per-window match list exceeded capacity";
+      rc = FAC_E_CAPACITY;
+      break;
+    }
+    if (cnt[0] > out_cap) {
+      out_cap = cnt[0];
+      HIP_TRY(d_out.alloc(out_cap * sizeof(fac_match), stream));
+      ++retries;
+      continue;
+    }
+    out.resize(cnt[0]);
+    if (cnt[0]) HIP_TRY(hipMemcpyAsync(out.data(), d_out.p, cnt[0] * sizeof(fac_match), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    break;
+  }
+  if (stats) {
+    stats->kernel_ms += ms_total;
+    stats->kernel_launches += launches;
+    stats->windows += windows;
+    stats->states_popped += cnt[1];
+    stats->graphemes = h.n;
+    stats->bytes = h.len;
+    stats->retries += retries;
+  }
+  return rc;
+}
+
+int prefilter_windows(const Engine& e, const Haystack& h, const std::vector<uint32_t>& ks, hipStream_t stream,
+                      std::vector<std::pair<uint64_t, uint64_t>>& windows, fac_stats* stats, std::string& err) {
+  windows.clear();
+  HIP_TRY(hipSetDevice(e.device));
+  if (!stream) stream = e.stream;
+  const uint64_t n = h.n;
+  if (n == 0) return FAC_OK;
+  const uint32_t np = (uint32_t)e.bp_m.size();
+  DevBuf d_ids, d_m, d_k, d_cover, d_runs, d_cnt;
+  HIP_TRY(d_ids.alloc(n + 16, stream));
+  if (h.ascii) {
+    const uint64_t threads = (n + 15) / 16;
+    hipLaunchKernelGGL(transcode_ascii_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, stream, h.d_utf8, n,
+                       e.d_ascii_id, static_cast<uint8_t*>(d_ids.p));
+    HIP_TRY(hipGetLastError());
+  } else {
+    HIP_TRY(hipMemcpyAsync(d_ids.p, h.sym.data(), n, hipMemcpyHostToDevice, stream));
+  }
+  HIP_TRY(d_m.alloc(np * 4, stream));
+  HIP_TRY(d_k.alloc(np * 4, stream));
+  HIP_TRY(hipMemcpyAsync(d_m.p, e.bp_m.data(), np * 4, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(d_k.p, ks.data(), np * 4, hipMemcpyHostToDevice, stream));
+  const uint64_t n_words = (n + 31) / 32;
+  HIP_TRY(d_cover.alloc(n_words * 4, stream));
+  HIP_TRY(hipMemsetAsync(d_cover.p, 0, n_words * 4, stream));
+  Events ev;
+  HIP_TRY(hipEventCreate(&ev.a));
+  HIP_TRY(hipEventCreate(&ev.b));
+  HIP_TRY(hipEventRecord(ev.a, stream));
+  BitapParams B{};
+  B.ids = static_cast<const uint8_t*>(d_ids.p);
+  B.n = n;
+  B.mask_t = e.d_bp_mask;
+  B.m = static_cast<const uint32_t*>(d_m.p);
+  B.k = static_cast<const uint32_t*>(d_k.p);
+  B.n_pat = np;
+  B.seg_len = 4096;
+  B.cover = static_cast<uint32_t*>(d_cover.p);
+  const uint64_t segs = (n + B.seg_len - 1) / B.seg_len;
+  const uint64_t waves = segs * ((np + 63) / 64);
+  const uint32_t kmax = ks.empty() ? 0 : *std::max_element(ks.begin(), ks.end());
+  const dim3 bgrid((uint32_t)((waves + 3) / 4));
+  if (kmax <= 2) hipLaunchKernelGGL((bitap_kernel<2>), bgrid, dim3(256), 0, stream, B);
+  else if (kmax <= 4) hipLaunchKernelGGL((bitap_kernel<4>), bgrid, dim3(256), 0, stream, B);
+  else if (kmax <= 8) hipLaunchKernelGGL((bitap_kernel<8>), bgrid, dim3(256), 0, stream, B);
+  else if (kmax <= 16) hipLaunchKernelGGL((bitap_kernel<16>), bgrid, dim3(256), 0, stream, B);
+  else hipLaunchKernelGGL((bitap_kernel<24>), bgrid, dim3(256), 0, stream, B);
+  HIP_TRY(hipGetLastError());
+  uint64_t cap = 1 << 16;
+  HIP_TRY(d_cnt.alloc(8, stream));
+  for (;;) {
+    HIP_TRY(d_runs.alloc(cap * 16, stream));
+    HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 8, stream));
+    hipLaunchKernelGGL(runs_kernel, dim3((uint32_t)((n_words + 255) / 256)), dim3(256), 0, stream,
+                       static_cast<const uint32_t*>(d_cover.p), n_words, n, static_cast<unsigned long long*>(d_runs.p),
+                       static_cast<unsigned long long*>(d_cnt.p), cap);
+    HIP_TRY(hipGetLastError());
+    unsigned long long c = 0;
+    HIP_TRY(hipMemcpyAsync(&c, d_cnt.p, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (c > cap) {
+      cap = c;
+      continue;
+    }
+    std::vector<unsigned long long> buf(2 * c);
+    if (c) HIP_TRY(hipMemcpyAsync(buf.data(), d_runs.p, c * 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipEventRecord(ev.b, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    windows.resize(c);
+    for (uint64_t i = 0; i < c; ++i) windows[i] = {buf[2 * i], buf[2 * i + 1]};
+    std::sort(windows.begin(), windows.end());
+    break;
+  }
+  if (stats) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+    stats->prefilter_ms += ms;
+  }
+  return FAC_OK;
+}
+
+}  // namespace fac

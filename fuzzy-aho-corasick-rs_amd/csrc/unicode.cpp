@@ -1,0 +1,209 @@
+// unicode.cpp — host-side UTF-8 staging: UAX #29 extended grapheme clusters and case folding.
+//
+// Replaces the reference's third-party boundary: `unicode-segmentation` ^1.13
+// `graphemes(true)` / `grapheme_indices(true)` (builder.rs:197-205, search.rs:398-416,
+// prefilter.rs:264, structs.rs:664) and Rust `str::to_lowercase` (builder.rs:198-200,
+// search.rs:406-412). Property tables are generated offline (tools/gen_unicode_tables.py).
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fac_internal.h"
+
+namespace fac {
+namespace {
+
+struct GcbRange { uint32_t lo, hi; uint8_t prop; };
+struct CpRange { uint32_t lo, hi; };
+struct LowerMap { uint32_t cp; uint32_t out[3]; uint8_t n; };
+
+#include "unicode_data.inc"
+
+enum Gcb : uint8_t {
+  GCB_Other = 0, GCB_CR, GCB_LF, GCB_Control, GCB_Extend, GCB_ZWJ, GCB_RI, GCB_Prepend,
+  GCB_SpacingMark, GCB_L, GCB_V, GCB_T, GCB_LV, GCB_LVT
+};
+enum Incb : uint8_t { INCB_None = 0, INCB_Linker, INCB_Consonant, INCB_Extend };
+
+template <typename R>
+const R* find_range(const R* tab, size_t n, uint32_t cp) {
+  size_t lo = 0, hi = n;
+  while (lo < hi) {
+    size_t mid = (lo + hi) / 2;
+    if (tab[mid].hi < cp) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < n && tab[lo].lo <= cp && cp <= tab[lo].hi) return &tab[lo];
+  return nullptr;
+}
+
+inline uint8_t gcb(uint32_t cp) {
+  if (cp < 0x80) {  // ASCII fast path
+    if (cp == '\r') return GCB_CR;
+    if (cp == '\n') return GCB_LF;
+    if (cp < 0x20 || cp == 0x7F) return GCB_Control;
+    return GCB_Other;
+  }
+  const GcbRange* r = find_range(kGcbRanges, sizeof(kGcbRanges) / sizeof(kGcbRanges[0]), cp);
+  return r ? r->prop : GCB_Other;
+}
+inline bool ext_pict(uint32_t cp) {
+  if (cp < 0xA9) return false;
+  return find_range(kExtPictRanges, sizeof(kExtPictRanges) / sizeof(kExtPictRanges[0]), cp) != nullptr;
+}
+inline uint8_t incb(uint32_t cp) {
+  if (cp < 0x300) return INCB_None;
+  const GcbRange* r = find_range(kIncbRanges, sizeof(kIncbRanges) / sizeof(kIncbRanges[0]), cp);
+  return r ? r->prop : INCB_None;
+}
+
+struct Props {
+  uint8_t g, ib;
+  bool pict;
+};
+inline Props props(uint32_t cp) { return {gcb(cp), incb(cp), ext_pict(cp)}; }
+
+inline bool is_ctl(uint8_t g) { return g == GCB_Control || g == GCB_CR || g == GCB_LF; }
+
+}  // namespace
+
+uint32_t utf8_decode(const uint8_t* s, uint64_t n, uint64_t& i) {
+  uint8_t b0 = s[i];
+  if (b0 < 0x80) { i += 1; return b0; }
+  if ((b0 & 0xE0) == 0xC0 && i + 1 < n) {
+    uint32_t cp = ((b0 & 0x1Fu) << 6) | (s[i + 1] & 0x3Fu);
+    i += 2;
+    return cp;
+  }
+  if ((b0 & 0xF0) == 0xE0 && i + 2 < n) {
+    uint32_t cp = ((b0 & 0x0Fu) << 12) | ((s[i + 1] & 0x3Fu) << 6) | (s[i + 2] & 0x3Fu);
+    i += 3;
+    return cp;
+  }
+  if ((b0 & 0xF8) == 0xF0 && i + 3 < n) {
+    uint32_t cp = ((b0 & 0x07u) << 18) | ((s[i + 1] & 0x3Fu) << 12) | ((s[i + 2] & 0x3Fu) << 6) |
+                  (s[i + 3] & 0x3Fu);
+    i += 4;
+    return cp;
+  }
+  i += 1;  // invalid; callers validate first
+  return 0xFFFD;
+}
+
+bool utf8_valid(const uint8_t* s, uint64_t n) {
+  uint64_t i = 0;
+  while (i < n) {
+    uint8_t b = s[i];
+    if (b < 0x80) { ++i; continue; }
+    int len;
+    uint32_t min;
+    if ((b & 0xE0) == 0xC0) { len = 2; min = 0x80; }
+    else if ((b & 0xF0) == 0xE0) { len = 3; min = 0x800; }
+    else if ((b & 0xF8) == 0xF0) { len = 4; min = 0x10000; }
+    else return false;
+    if (i + len > n) return false;
+    for (int k = 1; k < len; ++k)
+      if ((s[i + k] & 0xC0) != 0x80) return false;
+    uint64_t j = i;
+    uint32_t cp = utf8_decode(s, n, j);
+    if (cp < min || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) return false;
+    i += len;
+  }
+  return true;
+}
+
+// UAX #29 extended grapheme cluster boundaries (rules GB3-GB13, GB999, with GB9c InCB).
+// Appends the byte offset of each grapheme start (the first is always 0 when n > 0).
+void segment_graphemes(const uint8_t* s, uint64_t n, std::vector<uint64_t>& starts) {
+  starts.clear();
+  if (n == 0) return;
+  uint64_t i = 0;
+  uint32_t cp = utf8_decode(s, n, i);
+  Props L = props(cp);
+  starts.push_back(0);
+  // state describing the text ending at the left character
+  uint32_t ri_run = L.g == GCB_RI ? 1 : 0;  // consecutive RIs ending at left
+  bool pict = L.pict;                         // left is in "ExtPict Extend*"
+  bool gb11 = false;                          // left is ZWJ preceded by ExtPict Extend*
+  int incb_state = L.ib == INCB_Consonant ? 1 : 0;  // 1: Consonant [Ext|Lnk]*, 2: ... with Linker
+  while (i < n) {
+    uint64_t pos = i;
+    uint32_t c = utf8_decode(s, n, i);
+    Props R = props(c);
+    bool brk;
+    if (L.g == GCB_CR && R.g == GCB_LF) brk = false;                        // GB3
+    else if (is_ctl(L.g)) brk = true;                                      // GB4
+    else if (is_ctl(R.g)) brk = true;                                      // GB5
+    else if (L.g == GCB_L && (R.g == GCB_L || R.g == GCB_V || R.g == GCB_LV || R.g == GCB_LVT)) brk = false;  // GB6
+    else if ((L.g == GCB_LV || L.g == GCB_V) && (R.g == GCB_V || R.g == GCB_T)) brk = false;  // GB7
+    else if ((L.g == GCB_LVT || L.g == GCB_T) && R.g == GCB_T) brk = false;                   // GB8
+    else if (R.g == GCB_Extend || R.g == GCB_ZWJ) brk = false;             // GB9
+    else if (R.g == GCB_SpacingMark) brk = false;                          // GB9a
+    else if (L.g == GCB_Prepend) brk = false;                              // GB9b
+    else if (incb_state == 2 && R.ib == INCB_Consonant) brk = false;       // GB9c
+    else if (gb11 && R.pict) brk = false;                                  // GB11
+    else if (L.g == GCB_RI && R.g == GCB_RI && (ri_run & 1)) brk = false;   // GB12/13
+    else brk = true;                                                       // GB999
+    if (brk) starts.push_back(pos);
+    // advance state: R becomes the left character
+    ri_run = R.g == GCB_RI ? ri_run + 1 : 0;
+    gb11 = R.g == GCB_ZWJ && pict;
+    pict = R.pict ? true : (R.g == GCB_Extend ? pict : false);
+    if (R.ib == INCB_Consonant) incb_state = 1;
+    else if (R.ib == INCB_Linker && incb_state >= 1) incb_state = 2;
+    else if (R.ib == INCB_Extend && incb_state >= 1) { /* unchanged */ }
+    else incb_state = 0;
+    L = R;
+  }
+}
+
+int lower_full(uint32_t cp, uint32_t out[3]) {
+  if (cp < 0x80) {
+    out[0] = (cp >= 'A' && cp <= 'Z') ? cp + 32 : cp;
+    return 1;
+  }
+  size_t lo = 0, hi = sizeof(kLowerMap) / sizeof(kLowerMap[0]);
+  while (lo < hi) {
+    size_t mid = (lo + hi) / 2;
+    if (kLowerMap[mid].cp < cp) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < sizeof(kLowerMap) / sizeof(kLowerMap[0]) && kLowerMap[lo].cp == cp) {
+    for (int k = 0; k < kLowerMap[lo].n; ++k) out[k] = kLowerMap[lo].out[k];
+    return kLowerMap[lo].n;
+  }
+  out[0] = cp;
+  return 1;
+}
+
+// One grapheme's folded code points: `to_lowercase()` when case-insensitive (search.rs:406-412;
+// builder.rs:198-200). Per-char full mapping; a lone capital sigma at grapheme start is never
+// word-final, so char-wise mapping equals Rust's context-sensitive `str::to_lowercase` here.
+void fold_grapheme(const uint8_t* s, uint64_t b, uint64_t e, bool ci, std::u32string& out) {
+  out.clear();
+  uint64_t i = b;
+  while (i < e) {
+    uint32_t cp = utf8_decode(s, e, i);
+    if (ci) {
+      uint32_t lo[3];
+      int k = lower_full(cp, lo);
+      for (int t = 0; t < k; ++t) out.push_back(lo[t]);
+    } else {
+      out.push_back(cp);
+    }
+  }
+}
+
+uint32_t fold_first_char(const uint8_t* s, uint64_t b, uint64_t e, bool ci) {
+  if (b >= e) return 0;
+  uint64_t i = b;
+  uint32_t cp = utf8_decode(s, e, i);
+  if (!ci) return cp;
+  uint32_t lo[3];
+  lower_full(cp, lo);
+  return lo[0];
+}
+
+}  // namespace fac

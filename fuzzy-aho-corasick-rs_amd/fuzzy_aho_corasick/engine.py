@@ -1,0 +1,287 @@
+"""FuzzyAhoCorasickBuilder / FuzzyAhoCorasick: the crate's public surface (builder.rs, query.rs,
+prefilter.rs, replacer.rs) over the C ABI of include/fac.h. Every search goes to the GPU."""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, List, Optional, Tuple
+
+from . import _native
+from .matches import FuzzyMatch, FuzzyMatches
+from .structs import (DeviceError, FuzzyLimits, FuzzyPenalties, HaystackTooLarge, Order, Overlap,
+                      Pattern, SearchOptions, Similarity, UnsupportedConfiguration, f32)
+
+
+def _default_device() -> int:
+    for var in ("FAC_DEVICE", "LOCAL_RANK"):
+        if var in os.environ:
+            return int(os.environ[var])
+    return 0
+
+
+def _raise(rc: int, err_graphemes: int = 0):
+    if rc == _native.FAC_E_HAYSTACK_TOO_LARGE:
+        raise HaystackTooLarge(err_graphemes)
+    if rc == _native.FAC_E_UNSUPPORTED:
+        raise UnsupportedConfiguration(_native.last_error())
+    raise DeviceError(rc, _native.last_error())
+
+
+class FuzzyAhoCorasickBuilder:
+    """builder.rs:22-168. Chainable; `build` uploads the automaton to the GPU."""
+
+    def __init__(self):
+        self._similarity: Optional[Similarity] = None
+        self._limits: Optional[FuzzyLimits] = None
+        self._penalties = FuzzyPenalties()
+        self._case_insensitive = False
+        self._beam_width: Optional[int] = None
+        self._auto_beam: Optional[Tuple[int, int]] = None
+        self._mappings: List[Tuple[str, str, float]] = []
+        self._min_symbol_similarity = 0.0
+        self._device = _default_device()
+
+    @classmethod
+    def new(cls) -> "FuzzyAhoCorasickBuilder":
+        return cls()
+
+    def similarity(self, sim: Similarity) -> "FuzzyAhoCorasickBuilder":
+        self._similarity = sim
+        return self
+
+    def fuzzy(self, limits: FuzzyLimits) -> "FuzzyAhoCorasickBuilder":
+        self._limits = limits.finalize()
+        return self
+
+    def penalties(self, p: FuzzyPenalties) -> "FuzzyAhoCorasickBuilder":
+        self._penalties = p
+        return self
+
+    def case_insensitive(self, value: bool) -> "FuzzyAhoCorasickBuilder":
+        self._case_insensitive = bool(value)
+        return self
+
+    def beam_width(self, width: int) -> "FuzzyAhoCorasickBuilder":
+        self._beam_width = int(width)
+        return self
+
+    def auto_beam(self, budget: int, width: int) -> "FuzzyAhoCorasickBuilder":
+        self._auto_beam = (int(budget), int(width))
+        return self
+
+    def mapping(self, a: str, b: str) -> "FuzzyAhoCorasickBuilder":
+        return self.mapping_scored(a, b, 1.0)
+
+    def mapping_scored(self, a: str, b: str, score: float) -> "FuzzyAhoCorasickBuilder":
+        self._mappings.append((a, b, f32(score)))
+        return self
+
+    def min_symbol_similarity(self, m: float) -> "FuzzyAhoCorasickBuilder":
+        self._min_symbol_similarity = f32(m)
+        return self
+
+    def device(self, ordinal: int) -> "FuzzyAhoCorasickBuilder":
+        """Extension: HIP device that holds this engine's tables."""
+        self._device = int(ordinal)
+        return self
+
+    def build(self, inputs: Iterable) -> "FuzzyAhoCorasick":
+        patterns = [Pattern.from_(x) for x in inputs]
+        return FuzzyAhoCorasick(self, patterns)
+
+    def build_replacer(self, pairs: Iterable) -> "FuzzyReplacer":
+        pats, repl = [], []
+        for p, r in pairs:
+            pats.append(Pattern.from_(p))
+            repl.append(str(r))
+        return FuzzyReplacer(self.build(pats), repl)
+
+
+class FuzzyAhoCorasick:
+    """structs.rs:528-567 + search/query entry points (query.rs:30-202)."""
+
+    def __init__(self, builder: FuzzyAhoCorasickBuilder, patterns: List[Pattern]):
+        self.patterns_ = patterns
+        self.builder = builder
+        self._keep = []  # keep ctypes buffers alive during the call
+        cfg = _native.fac_config()
+        cfg.case_insensitive = int(builder._case_insensitive)
+        cfg.has_limits = int(builder._limits is not None)
+        cfg.limits = (builder._limits or FuzzyLimits()).to_c()
+        pen = builder._penalties
+        cfg.penalty_insertion = pen.insertion
+        cfg.penalty_deletion = pen.deletion
+        cfg.penalty_substitution = pen.substitution
+        cfg.penalty_swap = pen.swap
+        cfg.beam_width = builder._beam_width or 0
+        if builder._beam_width == 0:
+            raise ValueError("beam_width must be >= 1")
+        cfg.has_auto_beam = int(builder._auto_beam is not None)
+        if builder._auto_beam:
+            cfg.auto_beam_budget, cfg.auto_beam_width = builder._auto_beam
+        cfg.min_symbol_similarity = builder._min_symbol_similarity
+        if builder._similarity is not None:
+            tab = (ctypes.c_float * (128 * 128))(*builder._similarity.ascii_table())
+            extra = builder._similarity.extra_pairs()
+            ab = (ctypes.c_uint32 * (2 * max(1, len(extra))))()
+            vals = (ctypes.c_float * max(1, len(extra)))()
+            for i, (a, b, s) in enumerate(extra):
+                ab[2 * i], ab[2 * i + 1], vals[i] = a, b, s
+            cfg.similarity_ascii = tab
+            cfg.n_similarity_pairs = len(extra)
+            cfg.similarity_pairs = ab
+            cfg.similarity_pair_values = vals
+            self._keep += [tab, ab, vals]
+        cfg.n_mappings = len(builder._mappings)
+        cfg.device = builder._device
+        arr = (_native.fac_pattern * max(1, len(patterns)))()
+        enc = []
+        for i, p in enumerate(patterns):
+            b = p.pattern.encode("utf-8")
+            enc.append(b)
+            arr[i].utf8 = b
+            arr[i].len = len(b)
+            arr[i].weight = p.weight
+            arr[i].has_limits = int(p.limits is not None)
+            arr[i].limits = (p.limits or FuzzyLimits()).to_c()
+        handle = ctypes.c_void_p()
+        rc = _native.lib.fac_build(arr, len(patterns), ctypes.byref(cfg), ctypes.byref(handle))
+        if rc:
+            _raise(rc)
+        self._h = handle
+        self.device = builder._device
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            _native.lib.fac_engine_free(h)
+            self._h = None
+
+    # -- introspection
+    def patterns(self) -> List[Pattern]:
+        return self.patterns_
+
+    def num_nodes(self) -> int:
+        return int(_native.lib.fac_engine_num_nodes(self._h))
+
+    def max_edits_fast(self) -> int:
+        return int(_native.lib.fac_engine_max_edits_fast(self._h))
+
+    def max_match_graphemes(self) -> int:
+        """stream.rs:213-253"""
+        return int(_native.lib.fac_max_match_graphemes(self._h))
+
+    # -- raw search (search.rs:187-395)
+    def _to_matches(self, haystack: str, data: bytes, rows) -> FuzzyMatches:
+        inner = []
+        for (s, e, p, sim, ins, dele, sub, swp, ed) in rows:
+            inner.append(FuzzyMatch(ins, dele, sub, swp, ed, p, self.patterns_[p], s, e, sim,
+                                    data[s:e].decode("utf-8")))
+        return FuzzyMatches(haystack, inner, data)
+
+    def search_raw(self, haystack: str, threshold: float, prefilter: bool = False) -> FuzzyMatches:
+        data = haystack.encode("utf-8")
+        out = ctypes.POINTER(_native.fac_match)()
+        n = ctypes.c_uint64()
+        eg = ctypes.c_uint64()
+        fn = _native.lib.fac_search_prefiltered if prefilter else _native.lib.fac_search_raw
+        rc = fn(self._h, data, len(data), f32(threshold), ctypes.byref(out), ctypes.byref(n), ctypes.byref(eg))
+        if rc:
+            _raise(rc, eg.value)
+        return self._to_matches(haystack, data, _native.take_matches(out, n.value))
+
+    # -- query.rs
+    def search(self, haystack: str, opts: SearchOptions = None) -> FuzzyMatches:
+        opts = opts or SearchOptions()
+        return self.search_raw(haystack, opts.threshold_).apply(opts.order_, opts.overlap_)
+
+    def _segmented(self, haystack: str, opts: SearchOptions) -> FuzzyMatches:
+        order = Order.Default if opts.order_ == Order.Unsorted else opts.order_
+        overlap = Overlap.NonOverlapping if opts.overlap_ == Overlap.Keep else opts.overlap_
+        return self.search_raw(haystack, opts.threshold_).apply(order, overlap)
+
+    def replace(self, text: str, opts: SearchOptions, callback) -> str:
+        return self._segmented(text, opts).replace(callback)
+
+    def strip_prefix(self, haystack: str, opts: SearchOptions) -> str:
+        return self._segmented(haystack, opts).strip_prefix()
+
+    def strip_suffix(self, haystack: str, opts: SearchOptions) -> str:
+        return self._segmented(haystack, opts).strip_suffix()
+
+    def split(self, haystack: str, opts: SearchOptions):
+        return self._segmented(haystack, opts).split()
+
+    def segment_iter(self, haystack: str, opts: SearchOptions):
+        return self._segmented(haystack, opts).segment_iter()
+
+    def segment_text(self, haystack: str, opts: SearchOptions) -> str:
+        return self._segmented(haystack, opts).segment_text()
+
+    # -- prefilter.rs:113-155
+    def with_prefilter(self) -> "Prefiltered":
+        return Prefiltered(self)
+
+    # -- device-resident haystacks (bench / sharding)
+    def stage(self, haystack: bytes) -> "StagedHaystack":
+        return StagedHaystack(self, haystack)
+
+
+class Prefiltered:
+    """prefilter.rs:57-156"""
+
+    def __init__(self, engine: FuzzyAhoCorasick):
+        self.engine = engine
+
+    def is_active(self) -> bool:
+        return bool(_native.lib.fac_prefilter_active(self.engine._h))
+
+    def search(self, haystack: str, opts: SearchOptions = None) -> FuzzyMatches:
+        opts = opts or SearchOptions()
+        return self.engine.search_raw(haystack, opts.threshold_, prefilter=True).apply(opts.order_, opts.overlap_)
+
+
+class StagedHaystack:
+    """A haystack staged into HBM once (fac_haystack_stage) and searched many times."""
+
+    def __init__(self, engine: FuzzyAhoCorasick, data: bytes):
+        self.engine = engine
+        self.data = data
+        h = ctypes.c_void_p()
+        eg = ctypes.c_uint64()
+        rc = _native.lib.fac_haystack_stage(engine._h, data, len(data), ctypes.byref(h), ctypes.byref(eg))
+        if rc:
+            _raise(rc, eg.value)
+        self._h = h
+        self.graphemes = int(_native.lib.fac_haystack_graphemes(h))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            _native.lib.fac_haystack_free(h)
+            self._h = None
+
+    def search_windows(self, threshold: float, window_begin: int = 0, window_end: int = None, stream=None):
+        """Raw rows (start, end, pattern, sim, ins, del, sub, swp, edits) + fac_stats."""
+        if window_end is None:
+            window_end = self.graphemes
+        out = ctypes.POINTER(_native.fac_match)()
+        n = ctypes.c_uint64()
+        st = _native.fac_stats()
+        rc = _native.lib.fac_search_staged(self.engine._h, self._h, window_begin, window_end, f32(threshold),
+                                           ctypes.c_void_p(stream or 0), ctypes.byref(out), ctypes.byref(n),
+                                           ctypes.byref(st))
+        if rc:
+            _raise(rc)
+        return _native.take_matches(out, n.value), st
+
+
+class FuzzyReplacer:
+    """replacer.rs:9-52"""
+
+    def __init__(self, engine: FuzzyAhoCorasick, replacements: List[str]):
+        self.engine = engine
+        self.replacements = replacements
+
+    def replace(self, text: str, opts: SearchOptions) -> str:
+        return self.engine.replace(text, opts, lambda m: self.replacements[m.pattern_index])

@@ -1,0 +1,183 @@
+/* fac.h — C ABI of the MI355X-native fuzzy Aho–Corasick engine (libfac.so).
+ *
+ * Drop-in boundary for the hot path of kakserpom/fuzzy-aho-corasick-rs v0.5.0 (reference at
+ * /root/reference). Everything public in the crate funnels through one crate-private seam,
+ *
+ *     pub(crate) fn search_raw(&'a self, haystack: &'a str, similarity_threshold: f32)
+ *         -> Result<FuzzyMatches<'a>, SearchError>                       (src/search.rs:187-191)
+ *
+ * plus the engine constructor `FuzzyAhoCorasickBuilder::build` (src/builder.rs:181) and the
+ * pre-filter wrapper `Prefiltered::search` (src/prefilter.rs:135-155). The entry points below are
+ * exactly what a Rust `extern "C"` block (or any FFI) would bind to replace those; see
+ * INTEGRATION.md for the binding a maintainer would add. Plain pointers and sizes only; no C++ or
+ * torch types cross this boundary. All functions are reentrant; an engine is immutable after
+ * fac_build and may be shared across host threads (structs.rs:528-567).
+ *
+ * Return codes (SearchError is #[non_exhaustive], src/error.rs:7-17, so new codes follow the
+ * reference's own convention):
+ *   FAC_OK                      0
+ *   FAC_E_HAYSTACK_TOO_LARGE    1   SearchError::HaystackTooLarge{graphemes} (search.rs:198-201)
+ *   FAC_E_INVALID             100   bad argument (NULL, invalid UTF-8, beam_width == 0, ...)
+ *   FAC_E_UNSUPPORTED         101   configuration outside the GPU path (mappings) — never a
+ *                                   silent CPU fallback
+ *   FAC_E_HIP                 102   HIP runtime error (fac_last_error() has the text)
+ *   FAC_E_NO_DEVICE           103   no usable MI355X (gfx950) device
+ *   FAC_E_OOM                 104   host or device allocation failure
+ *   FAC_E_CAPACITY            105   a per-window device work buffer overflowed even after the
+ *                                   automatic retries (pathological input)
+ */
+#ifndef FAC_H
+#define FAC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FAC_OK 0
+#define FAC_E_HAYSTACK_TOO_LARGE 1
+#define FAC_E_INVALID 100
+#define FAC_E_UNSUPPORTED 101
+#define FAC_E_HIP 102
+#define FAC_E_NO_DEVICE 103
+#define FAC_E_OOM 104
+#define FAC_E_CAPACITY 105
+
+#define FAC_LIMIT_NONE (-1)
+
+/* FuzzyLimits (src/structs.rs:293-299), already finalized (structs.rs:319-335):
+ * each field is a count 0..255 or FAC_LIMIT_NONE. */
+typedef struct fac_limits {
+  int32_t insertions;
+  int32_t deletions;
+  int32_t substitutions;
+  int32_t swaps;
+  int32_t edits;
+} fac_limits;
+
+/* One Pattern (src/structs.rs:598-610). `custom_unique_id` only matters for host-side
+ * overlap resolution and is not passed. */
+typedef struct fac_pattern {
+  const char* utf8; /* pattern text, valid UTF-8 */
+  uint64_t len;     /* bytes */
+  float weight;     /* Pattern::weight, default 1.0 */
+  int32_t has_limits;
+  fac_limits limits; /* per-pattern limits, finalized; used iff has_limits */
+} fac_pattern;
+
+/* Builder state (src/builder.rs:22-33, FuzzyPenalties structs.rs:370-393). */
+typedef struct fac_config {
+  int32_t case_insensitive;
+  int32_t has_limits;   /* FuzzyAhoCorasickBuilder::fuzzy(...) called */
+  fac_limits limits;    /* finalized global limits */
+  float penalty_insertion;
+  float penalty_deletion;
+  float penalty_substitution;
+  float penalty_swap;
+  uint64_t beam_width;  /* 0 = None (exact exploration) */
+  int32_t has_auto_beam;
+  uint64_t auto_beam_budget;
+  uint64_t auto_beam_width;
+  float min_symbol_similarity;
+  /* Custom Similarity (structs.rs:30-54); NULL = the crate's DEFAULT_SIMILARITY
+   * (builder.rs:492-526). similarity_ascii is a 128x128 row-major table indexed [a][b];
+   * the pair list holds entries with a or b >= 128. */
+  const float* similarity_ascii;
+  uint64_t n_similarity_pairs;
+  const uint32_t* similarity_pairs; /* 2*n code points (a, b) */
+  const float* similarity_pair_values;
+  /* Multi-character mappings (builder.rs:108-132): not on the GPU path; n_mappings > 0 makes
+   * fac_build return FAC_E_UNSUPPORTED. */
+  uint64_t n_mappings;
+  int32_t device; /* HIP device ordinal for this engine's tables */
+} fac_config;
+
+/* Owned match record: the crate's OwnedMatch/StreamMatch POD (src/stream.rs:719-745), 32 bytes,
+ * identical on host, device and the RCCL wire. `start`/`end` are byte offsets into the haystack;
+ * the host rebuilds `text = haystack[start..end]`. */
+typedef struct fac_match {
+  uint64_t start;
+  uint64_t end;
+  uint32_t pattern_index;
+  float similarity;
+  uint8_t insertions;
+  uint8_t deletions;
+  uint8_t substitutions;
+  uint8_t swaps;
+  uint8_t edits;
+  uint8_t pad[3];
+} fac_match;
+
+/* Per-call device statistics (filled when the pointer is non-NULL). */
+typedef struct fac_stats {
+  double kernel_ms;        /* HIP-event time of the search kernel(s) on the call's stream */
+  double prefilter_ms;     /* HIP-event time of the bitap scan + window merge (0 if unused) */
+  uint64_t kernel_launches;
+  uint64_t windows;        /* start windows searched */
+  uint64_t states_popped;  /* BFS states popped (work diagnostic) */
+  uint64_t graphemes;      /* haystack graphemes */
+  uint64_t bytes;          /* haystack UTF-8 bytes */
+  uint64_t retries;        /* capacity retries */
+} fac_stats;
+
+typedef struct fac_engine fac_engine;
+typedef struct fac_haystack fac_haystack;
+
+/* Last error text of the calling thread ("" if none). */
+const char* fac_last_error(void);
+
+/* FuzzyAhoCorasickBuilder::build (builder.rs:181-484): builds the trie, fail-link output merge
+ * and prune coefficients on the host and uploads the device tables to cfg->device. */
+int fac_build(const fac_pattern* patterns, uint64_t n_patterns, const fac_config* cfg,
+              fac_engine** out);
+void fac_engine_free(fac_engine* engine);
+
+/* FuzzyAhoCorasick::search_raw (search.rs:187-395): best-per-(start,end,pattern) matches at or
+ * above `threshold`, unordered. *out is allocated by the library (fac_matches_free). On
+ * FAC_E_HAYSTACK_TOO_LARGE, *err_graphemes receives the grapheme count. */
+int fac_search_raw(const fac_engine* engine, const uint8_t* utf8, uint64_t len, float threshold,
+                   fac_match** out, uint64_t* n_out, uint64_t* err_graphemes);
+void fac_matches_free(fac_match* matches);
+
+/* FuzzyAhoCorasick::with_prefilter + Prefiltered (prefilter.rs:113-155). */
+int fac_prefilter_active(const fac_engine* engine);
+int fac_search_prefiltered(const fac_engine* engine, const uint8_t* utf8, uint64_t len,
+                           float threshold, fac_match** out, uint64_t* n_out,
+                           uint64_t* err_graphemes);
+
+/* FuzzyAhoCorasick::max_match_graphemes (stream.rs:213-253). */
+uint64_t fac_max_match_graphemes(const fac_engine* engine);
+
+/* Device-resident haystacks (bench / sharded multi-GPU). fac_haystack_stage performs the
+ * search_raw staging (is_ascii, grapheme segmentation + folding, search.rs:196-203/296-302)
+ * and uploads the result to the engine's device; the staged haystack can then be searched
+ * repeatedly with no host->device traffic. */
+int fac_haystack_stage(const fac_engine* engine, const uint8_t* utf8, uint64_t len,
+                       fac_haystack** out, uint64_t* err_graphemes);
+uint64_t fac_haystack_graphemes(const fac_haystack* hay);
+void fac_haystack_free(fac_haystack* hay);
+
+/* Search start windows [window_begin, window_end) of a staged haystack (window_end is clamped
+ * to the grapheme count). Searching every window reproduces search_raw; disjoint window ranges
+ * give disjoint match sets (the best-map key holds the start byte), which is how the host shards
+ * one haystack across GPUs. `stream` is a hipStream_t (NULL = the engine's stream). */
+int fac_search_staged(const fac_engine* engine, const fac_haystack* hay, uint64_t window_begin,
+                      uint64_t window_end, float threshold, void* stream, fac_match** out,
+                      uint64_t* n_out, fac_stats* stats);
+
+/* Engine introspection (tests / diagnostics). */
+uint64_t fac_engine_num_nodes(const fac_engine* engine);
+uint32_t fac_engine_max_edits_fast(const fac_engine* engine);
+
+/* Host-side UTF-8 staging helpers exposed for tests: extended grapheme cluster segmentation
+ * (UAX #29) and per-grapheme first-code-point folding. Writes up to `cap` entries. */
+uint64_t fac_segment_graphemes(const uint8_t* utf8, uint64_t len, uint64_t* starts, uint64_t cap);
+uint32_t fac_fold_first_char(const uint8_t* utf8, uint64_t len, int32_t case_insensitive);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FAC_H */

@@ -1,0 +1,855 @@
+// oracle/oracle.cpp — TEST INFRASTRUCTURE ONLY. Never linked into, loaded by, or called from the
+// product path (`fuzzy-aho-corasick-rs_amd/`). Only `tests/`, `__graft_entry__.smoke()` and
+// `bench.py`'s `cpu_baseline` leg may load this library, and only as the checker / CPU baseline.
+//
+// A single-threaded CPU restatement of the reference crate's hot path
+// (kakserpom/fuzzy-aho-corasick-rs v0.5.0, mounted at /root/reference), following the cited lines:
+//
+//   builder   src/builder.rs:181-484   trie, fail-link output merge, reach-based prune coefficients,
+//                                      effective limits, max_edits_fast
+//   similarity src/builder.rs:492-526, src/structs.rs:30-92 (default table, get, max_off_diagonal)
+//   search    src/search.rs:418-1119   per-start-window FIFO BFS with dedup, node ceiling, emission,
+//                                      exact / substitution / swap / insertion / deletion fan-out,
+//                                      beam prune, auto-beam
+//   limits    src/search.rs:84-169     within_limits_* family
+//   prefilter src/prefilter.rs:161-435 bitap build, transcode, k_for, window merge + re-search
+//
+// Deliberate, documented deviations (see DESIGN.md "Oracle"):
+//   * Edge order. The reference iterates `Node.transitions` in hashbrown order (builder.rs:336-341),
+//     which cannot be reproduced without a Rust toolchain. Edges here are kept in insertion order
+//     (order in which the child grapheme was first inserted). Unbeamed match sets do not depend on
+//     it; edit-count tie-breaks and beam ties do.
+//   * Beam ties. `select_nth_unstable_by` (search.rs:584) leaves ties at the cut unspecified. The
+//     oracle uses the canonical rule: keep the `bw` smallest by (penalty total order, queue
+//     position) and keep the survivors in their queue order — one legal outcome of the reference's
+//     partial selection.
+//   * Output order: sorted by (start, end, pattern) instead of hash-bucket order (the reference
+//     documents raw output as unordered, search.rs:1105-1110).
+//
+// Grapheme segmentation and case folding are NOT done here: the caller (Python test harness, using
+// the `regex` module's UAX #29 `\X`) passes already-segmented, already-folded graphemes, which keeps
+// this restatement independent of the product's generated Unicode tables.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+constexpr int LIM_NONE = -1;
+
+struct Limits {  // FuzzyLimits (structs.rs:293-299); -1 = None
+  int ins = LIM_NONE, del = LIM_NONE, sub = LIM_NONE, swp = LIM_NONE, edits = LIM_NONE;
+};
+
+struct Pattern {  // structs.rs:598-610 (only what the hot path reads)
+  uint32_t glen = 0;
+  float weight = 1.f;
+  bool has_limits = false;
+  Limits lim;
+  std::vector<std::u32string> graphemes;  // folded graphemes
+};
+
+struct Edge {  // structs.rs:186-229
+  uint32_t first_char;
+  uint32_t next;
+  bool single_byte;
+};
+
+struct Node {  // structs.rs:249-281
+  std::vector<Edge> edges;
+  std::vector<uint32_t> output;
+  float prune_len = 0.f, prune_lw = 0.f;
+  int64_t pattern_index = -1;
+  uint32_t fail = 0;
+  std::map<std::u32string, uint32_t> transitions;  // lookup only; iteration uses `order`
+  std::vector<std::u32string> order;               // insertion order of transition keys
+};
+
+struct Similarity {  // structs.rs:9-14, 30-54, 82-92
+  float ascii[128][128];
+  std::map<std::pair<uint32_t, uint32_t>, float> map;
+  float get(uint32_t a, uint32_t b) const {
+    if (a < 128 && b < 128) return ascii[a][b];
+    auto it = map.find({a, b});
+    return it == map.end() ? 0.f : it->second;
+  }
+  float max_off_diagonal() const {  // structs.rs:61-76
+    float m = 0.f;
+    for (int i = 0; i < 128; ++i)
+      for (int j = 0; j < 128; ++j)
+        if (i != j) m = std::fmax(m, ascii[i][j]);
+    for (auto& kv : map)
+      if (kv.first.first != kv.first.second) m = std::fmax(m, kv.second);
+    return m;
+  }
+};
+
+struct Engine {
+  std::vector<Node> nodes;
+  std::vector<Pattern> patterns;
+  Similarity sim;
+  bool has_limits = false;
+  Limits limits;  // effective limits (builder.rs:289-329)
+  float p_ins, p_del, p_sub, p_swp;
+  bool case_insensitive = false;
+  bool has_pattern_limits = false;
+  uint32_t max_edits_fast = 0;
+  size_t beam_width = 0;  // 0 = None
+  bool has_auto_beam = false;
+  size_t ab_budget = 0, ab_width = 0;
+  float min_symbol_similarity = 0.f;
+  // prefilter (prefilter.rs:69-93)
+  bool bitap_ok = false;
+  std::map<std::u32string, uint32_t> symbol_ids;
+  uint8_t ascii_id[128];
+  float edit_cost_mult = 0.f;
+  struct BP { uint32_t m; float weight; std::vector<uint64_t> mask; bool has_k_limit; size_t k_limit; };
+  std::vector<BP> bitap;
+};
+
+struct Match {
+  uint64_t start, end;
+  uint32_t pattern;
+  float similarity;
+  uint8_t ins, del, sub, swp, edits;
+};
+
+// ------------------------------------------------------------------------------------------
+// Builder (builder.rs:181-484)
+// ------------------------------------------------------------------------------------------
+void default_similarity(Similarity& s) {  // builder.rs:492-526 + structs.rs:36-48
+  for (int i = 0; i < 128; ++i)
+    for (int j = 0; j < 128; ++j) s.ascii[i][j] = (i == j) ? 1.f : 0.f;
+  const char* vowels = "aeiou";
+  auto is_vowel = [&](char c) { return std::strchr(vowels, c) != nullptr; };
+  for (char a = 'a'; a <= 'z'; ++a)
+    for (char b = 'a'; b <= 'z'; ++b) {
+      if (a == b) continue;
+      if (is_vowel(a) && is_vowel(b)) s.ascii[(int)a][(int)b] = 0.6f;
+      if (!is_vowel(a) && !is_vowel(b)) s.ascii[(int)a][(int)b] = 0.4f;
+    }
+  s.ascii['o']['0'] = 0.6f; s.ascii['0']['o'] = 0.6f;
+  s.ascii['l']['1'] = 0.7f; s.ascii['1']['l'] = 0.7f;
+  s.ascii['i']['1'] = 0.6f; s.ascii['1']['i'] = 0.6f;
+  s.ascii['s']['5'] = 0.5f; s.ascii['5']['s'] = 0.5f;
+}
+
+size_t k_from_limits(const Limits& l, bool& bounded) {  // prefilter.rs:388-405
+  bounded = true;
+  if (l.edits != LIM_NONE) {
+    bool swaps_forbidden = l.swp == 0;
+    return swaps_forbidden ? (size_t)l.edits : 2 * (size_t)l.edits;
+  }
+  if (l.ins == LIM_NONE || l.del == LIM_NONE || l.sub == LIM_NONE || l.swp == LIM_NONE) {
+    bounded = false;
+    return 0;
+  }
+  return (size_t)l.ins + l.del + l.sub + 2 * (size_t)l.swp;
+}
+
+void build_bitap(Engine& e) {  // prefilter.rs:161-245 (mappings never configured in the oracle)
+  e.bitap_ok = false;
+  if (e.patterns.empty()) return;
+  float max_sim = e.sim.max_off_diagonal();
+  float p_sub_min = e.p_sub * (1.0f - max_sim);
+  float mults[4] = {1.0f / e.p_ins, 1.0f / e.p_del, 1.0f / p_sub_min, 2.0f / e.p_swp};
+  for (float m : mults)
+    if (!std::isfinite(m) || m <= 0.0f) return;
+  float ecm = 0.0f;
+  for (float m : mults) ecm = std::fmax(ecm, m);  // fold(0.0, f32::max)
+  e.edit_cost_mult = ecm;
+  e.symbol_ids.clear();
+  std::vector<std::vector<uint32_t>> pat_ids;
+  e.bitap.clear();
+  for (auto& p : e.patterns) {
+    size_t m = p.graphemes.size();
+    if (m == 0 || m > 63) return;
+    std::vector<uint32_t> ids;
+    for (auto& g : p.graphemes) {
+      uint32_t next_id = (uint32_t)e.symbol_ids.size() + 1;
+      auto it = e.symbol_ids.find(g);
+      uint32_t id;
+      if (it == e.symbol_ids.end()) { e.symbol_ids[g] = next_id; id = next_id; } else id = it->second;
+      if (id > 255) return;
+      ids.push_back(id);
+    }
+    Engine::BP bp;
+    bp.m = (uint32_t)m;
+    bp.weight = p.weight;
+    const Limits* app = p.has_limits ? &p.lim : (e.has_limits ? &e.limits : nullptr);
+    bp.has_k_limit = false;
+    bp.k_limit = 0;
+    if (app) {
+      bool bounded;
+      size_t k = k_from_limits(*app, bounded);
+      if (bounded) { bp.has_k_limit = true; bp.k_limit = k; }
+    }
+    e.bitap.push_back(bp);
+    pat_ids.push_back(ids);
+  }
+  for (int b = 0; b < 128; ++b) {
+    uint32_t ch = (uint32_t)b;
+    if (e.case_insensitive && ch >= 'A' && ch <= 'Z') ch += 32;
+    std::u32string key(1, ch);
+    auto it = e.symbol_ids.find(key);
+    e.ascii_id[b] = it == e.symbol_ids.end() ? 0 : (uint8_t)it->second;
+  }
+  size_t alphabet = e.symbol_ids.size();
+  for (size_t i = 0; i < e.bitap.size(); ++i) {
+    e.bitap[i].mask.assign(alphabet + 1, 0);
+    for (size_t k = 0; k < pat_ids[i].size(); ++k) e.bitap[i].mask[pat_ids[i][k]] |= 1ull << k;
+  }
+  e.bitap_ok = true;
+}
+
+void build(Engine& e) {
+  auto& nodes = e.nodes;
+  nodes.clear();
+  nodes.emplace_back();
+  for (size_t i = 0; i < e.patterns.size(); ++i) {  // builder.rs:195-237
+    size_t cur = 0;
+    for (auto& g : e.patterns[i].graphemes) {
+      size_t next;
+      auto it = nodes[cur].transitions.find(g);
+      if (it != nodes[cur].transitions.end()) {
+        next = it->second;
+      } else {
+        next = nodes.size();
+        nodes[cur].transitions[g] = (uint32_t)next;
+        nodes[cur].order.push_back(g);
+        nodes.emplace_back();
+      }
+      if (nodes[next].pattern_index < 0) nodes[next].pattern_index = (int64_t)i;  // :227
+      cur = next;
+    }
+    nodes[cur].output.push_back((uint32_t)i);  // :235
+  }
+  // fail links + output merge (builder.rs:239-276), BFS by depth
+  std::vector<uint32_t> queue;
+  for (auto& g : nodes[0].order) {
+    uint32_t c = nodes[0].transitions[g];
+    nodes[c].fail = 0;
+    queue.push_back(c);
+  }
+  for (size_t qi = 0; qi < queue.size(); ++qi) {
+    uint32_t current = queue[qi];
+    for (auto& g : nodes[current].order) {
+      uint32_t next = nodes[current].transitions[g];
+      uint32_t fail = nodes[current].fail;
+      while (fail != 0 && nodes[fail].transitions.find(g) == nodes[fail].transitions.end())
+        fail = nodes[fail].fail;
+      auto it = nodes[fail].transitions.find(g);
+      uint32_t fallback = it == nodes[fail].transitions.end() ? 0 : it->second;
+      nodes[next].fail = fallback;
+      std::vector<uint32_t> fo = nodes[fallback].output;
+      for (uint32_t entry : fo)
+        if (std::find(nodes[next].output.begin(), nodes[next].output.end(), entry) ==
+            nodes[next].output.end())
+          nodes[next].output.push_back(entry);
+      queue.push_back(next);
+    }
+  }
+  // effective limits (builder.rs:289-329): e.has_limits/e.limits already hold the global limits
+  e.has_pattern_limits = false;
+  if (!e.has_limits) {
+    Limits m;
+    bool any = false;
+    for (auto& p : e.patterns) {
+      if (!p.has_limits) continue;
+      any = true;
+      if (p.lim.edits != LIM_NONE) m.edits = std::max(m.edits == LIM_NONE ? 0 : m.edits, p.lim.edits);
+      if (p.lim.ins != LIM_NONE) m.ins = std::max(m.ins == LIM_NONE ? 0 : m.ins, p.lim.ins);
+      if (p.lim.del != LIM_NONE) m.del = std::max(m.del == LIM_NONE ? 0 : m.del, p.lim.del);
+      if (p.lim.sub != LIM_NONE) m.sub = std::max(m.sub == LIM_NONE ? 0 : m.sub, p.lim.sub);
+      if (p.lim.swp != LIM_NONE) m.swp = std::max(m.swp == LIM_NONE ? 0 : m.swp, p.lim.swp);
+    }
+    if (any) { e.has_limits = true; e.limits = m; }
+  }
+  for (auto& p : e.patterns) e.has_pattern_limits |= p.has_limits;
+  // edges (builder.rs:336-342) — insertion order (see header)
+  for (auto& nd : nodes) {
+    nd.edges.clear();
+    for (auto& g : nd.order) {
+      uint32_t fc = g.empty() ? 0 : g[0];
+      bool single = g.size() == 1 && g[0] < 0x80;  // g.len() == 1 (UTF-8 bytes)
+      nd.edges.push_back({fc, nd.transitions[g], single});
+    }
+  }
+  // reach fixpoint (builder.rs:348-381)
+  size_t nn = nodes.size();
+  std::vector<size_t> rl(nn, 0);
+  std::vector<float> rw(nn, 0.f);
+  for (size_t i = 0; i < nn; ++i)
+    for (uint32_t p : nodes[i].output) {
+      rl[i] = std::max(rl[i], (size_t)e.patterns[p].glen);
+      rw[i] = std::fmax(rw[i], e.patterns[p].weight);
+    }
+  bool changed = true;
+  while (changed) {
+    changed = false;
+    for (size_t ii = nn; ii-- > 0;) {
+      size_t bl = rl[ii];
+      float bw = rw[ii];
+      for (auto& ed : nodes[ii].edges) {
+        bl = std::max(bl, rl[ed.next]);
+        bw = std::fmax(bw, rw[ed.next]);
+      }
+      if (bl > rl[ii] || bw > rw[ii]) { rl[ii] = bl; rw[ii] = bw; changed = true; }
+    }
+  }
+  for (size_t i = 0; i < nn; ++i) {
+    float len = (float)rl[i];
+    nodes[i].prune_len = len;
+    nodes[i].prune_lw = len / rw[i];
+  }
+  // max_edits_fast (builder.rs:451-468)
+  if (e.has_pattern_limits) e.max_edits_fast = 255;
+  else if (!e.has_limits) e.max_edits_fast = 0;
+  else {
+    const Limits& l = e.limits;
+    if (l.edits != LIM_NONE && l.ins == LIM_NONE && l.del == LIM_NONE && l.sub == LIM_NONE &&
+        l.swp == LIM_NONE)
+      e.max_edits_fast = (uint32_t)l.edits;
+    else
+      e.max_edits_fast = 255;
+  }
+  build_bitap(e);
+}
+
+// ------------------------------------------------------------------------------------------
+// Search (search.rs:418-1119)
+// ------------------------------------------------------------------------------------------
+struct State {  // structs.rs:166-179
+  uint32_t node, j, ms, me;
+  float pen;
+  uint8_t edits;
+  uint32_t packed;
+};
+
+inline bool lim_lt(int max, int v) { return max == LIM_NONE || v < max; }
+inline bool lim_le(int max, int v) { return max == LIM_NONE || v <= max; }
+
+struct Searcher {
+  const Engine& e;
+  explicit Searcher(const Engine& en) : e(en) {}
+
+  const Limits* node_limits(uint32_t node) const {  // search.rs:67-71
+    int64_t pi = e.nodes[node].pattern_index;
+    if (pi < 0) return nullptr;
+    const Pattern& p = e.patterns[(size_t)pi];
+    return p.has_limits ? &p.lim : nullptr;
+  }
+  const Limits* pick(const Limits* l) const { return l ? l : (e.has_limits ? &e.limits : nullptr); }
+  bool ins_ahead(const Limits* l, int edits, int ins) const {  // :87-99
+    const Limits* m = pick(l);
+    return m ? (lim_lt(m->edits, edits) && lim_lt(m->ins, ins)) : false;
+  }
+  bool del_ahead(const Limits* l, int edits, int del) const {  // :103-115
+    const Limits* m = pick(l);
+    return m ? (lim_lt(m->edits, edits) && lim_lt(m->del, del)) : false;
+  }
+  bool swp_ahead(const Limits* l, int edits, int swp) const {  // :119-130
+    const Limits* m = pick(l);
+    return m ? (lim_lt(m->edits, edits) && lim_lt(m->swp, swp)) : false;
+  }
+  bool subst(const Limits* l, int edits, int sub) const {  // :134-146
+    const Limits* m = pick(l);
+    return m ? (lim_lt(m->edits, edits) && lim_lt(m->sub, sub)) : (edits == 0 && sub == 0);
+  }
+  bool within(const Limits* l, int edits, int ins, int del, int sub, int swp) const {  // :151-169
+    const Limits* m = pick(l);
+    if (!m) return edits == 0 && ins == 0 && del == 0 && sub == 0 && swp == 0;
+    return lim_le(m->edits, edits) && lim_le(m->ins, ins) && lim_le(m->del, del) &&
+           lim_le(m->sub, sub) && lim_le(m->swp, swp);
+  }
+  float similarity(uint32_t a, uint32_t b) const { return a == b ? 1.0f : e.sim.get(a, b); }  // :76-82
+
+  static int64_t find_no_mappings(const Node& n, uint32_t ch) {  // structs.rs:512-519
+    for (auto& ed : n.edges)
+      if (ed.first_char == ch) return ed.next;
+    return -1;
+  }
+  static bool has_matching_edge_char(const Node& n, uint32_t ch) {  // structs.rs:471-475
+    for (auto& ed : n.edges)
+      if (ed.first_char == ch && ed.single_byte) return true;
+    return false;
+  }
+  static __uint128_t single_char_edge_bits(const Node& n) {  // structs.rs:482-493
+    __uint128_t bits = 0;
+    for (auto& ed : n.edges)
+      if (ed.single_byte && ed.first_char < 128) bits |= (__uint128_t)1 << ed.first_char;
+    return bits;
+  }
+
+  // Dedup key (search.rs:30-50); matched_start is kept for fidelity although it equals `start`.
+  struct Key {
+    uint32_t node, j, ms, me, packed;
+    bool operator==(const Key& o) const {
+      return node == o.node && j == o.j && ms == o.ms && me == o.me && packed == o.packed;
+    }
+  };
+  struct KeyHash {  // FxHasher rounds (structs.rs:101-109) over the reference's write sequence
+    size_t operator()(const Key& k) const {
+      const uint64_t K = 0x517cc1b727220a95ull;
+      uint64_t h = 0;
+      auto add = [&](uint64_t i) { h = (((h << 5) | (h >> 59)) ^ i) * K; };
+      add((uint64_t)k.node | ((uint64_t)k.j << 32));
+      add((uint64_t)k.ms | ((uint64_t)k.me << 32));
+      add((uint64_t)k.packed);
+      return (size_t)h;
+    }
+  };
+
+  uint64_t states_popped = 0, states_pushed = 0;
+
+  // `text_chars`, grapheme byte offsets (nullptr = identity), haystack byte length.
+  void run(const uint32_t* tc, const uint64_t* off, uint32_t n, uint64_t hay_len, float thr,
+           std::vector<Match>& out) {
+    out.clear();
+    if (n == 0) return;
+    const uint32_t mef = e.max_edits_fast == 0 || e.max_edits_fast > 6 ? 255 : e.max_edits_fast;
+    const bool fast = mef != 255;
+    const uint32_t text_len = n;
+    auto OFF = [&](uint32_t i) -> uint64_t { return off ? off[i] : (uint64_t)i; };
+
+    std::map<std::pair<uint64_t, uint32_t>, size_t> best_idx;  // per window (start fixed): (end,pattern) -> idx
+    std::vector<State> queue;
+    queue.reserve(e.beam_width ? e.beam_width : 128);
+    std::unordered_map<Key, float, KeyHash> visited;
+    visited.reserve(256);
+
+    const Node& root = e.nodes[0];
+    const float max_penalties = root.prune_len - root.prune_lw * thr;  // :486-487
+    const float min_sym = e.min_symbol_similarity;
+
+    bool ws = false;  // :504-521
+    __uint128_t first_bits = 0, second_bits = 0;
+    if (mef == 1 && root.output.empty()) {
+      first_bits = single_char_edge_bits(root);
+      bool child_output = false;
+      for (auto& ed : root.edges) {
+        const Node& ch = e.nodes[ed.next];
+        __uint128_t cb = single_char_edge_bits(ch);
+        second_bits |= cb;
+        first_bits |= cb;
+        if (!ch.output.empty()) child_output = true;
+      }
+      ws = !child_output;
+    }
+
+    size_t effective_beam = e.beam_width;  // 0 = None
+    size_t states_expanded = 0;
+
+    for (uint32_t start = 0; start < text_len; ++start) {
+      if (ws) {  // :535-553
+        uint32_t ch = tc[start];
+        if (ch < 128 && !((first_bits >> ch) & 1)) {
+          uint32_t nx = start + 1;
+          if (nx >= text_len) continue;
+          uint32_t nch = tc[nx];
+          if (nch < 128 && !((second_bits >> nch) & 1)) continue;
+        }
+      }
+      queue.clear();
+      visited.clear();
+      best_idx.clear();
+      size_t window_first_out = out.size();
+      queue.push_back({0, start, start, start, 0.f, 0, 0});
+      size_t q_idx = 0;
+      while (q_idx < queue.size()) {
+        if (effective_beam) {  // :577-589, canonical tie rule (see header)
+          size_t bw = effective_beam;
+          size_t remaining = queue.size() - q_idx;
+          if (remaining > bw * 2) beam_select(queue, q_idx, bw);
+        }
+        State st = queue[q_idx];
+        ++q_idx;
+        ++states_popped;
+        Key key{st.node, st.j, st.ms, st.me, st.packed};
+        auto vit = visited.find(key);  // :618-628
+        if (vit != visited.end()) {
+          if (vit->second <= st.pen) continue;
+          vit->second = st.pen;
+        } else {
+          visited.emplace(key, st.pen);
+        }
+        const Node& nd = e.nodes[st.node];
+        if (st.pen > nd.prune_len - nd.prune_lw * thr) continue;  // :638-642
+        const float remaining = max_penalties - st.pen;            // :648
+        const Limits* nlim = e.has_pattern_limits ? node_limits(st.node) : nullptr;
+        const uint8_t edits = st.edits;
+        const uint32_t pc = st.packed;
+        if (!nd.output.empty()) {  // :659-737
+          uint8_t ins = pc & 0xFF, del = (pc >> 8) & 0xFF, sub = (pc >> 16) & 0xFF, swp = (pc >> 24) & 0xFF;
+          uint64_t sb = st.ms < text_len ? OFF(st.ms) : 0;
+          uint64_t eb = st.me < text_len ? OFF(st.me) : hay_len;
+          for (uint32_t p : nd.output) {
+            if (fast) {
+              if (edits > mef) continue;
+            } else {
+              const Pattern& P = e.patterns[p];
+              if (!within(P.has_limits ? &P.lim : nullptr, edits, ins, del, sub, swp)) continue;
+            }
+            float total = (float)e.patterns[p].glen;
+            float sim = (total - st.pen) / total * e.patterns[p].weight;
+            if (sim < thr) continue;
+            auto bk = std::make_pair(eb, p);  // start_byte is fixed within a window
+            auto bi = best_idx.find(bk);
+            if (bi == best_idx.end()) {
+              best_idx.emplace(bk, out.size());
+              out.push_back({sb, eb, p, sim, ins, del, sub, swp, edits});
+            } else if (sim > out[bi->second].similarity) {
+              out[bi->second] = {sb, eb, p, sim, ins, del, sub, swp, edits};
+            }
+          }
+        }
+        const bool is_last_edit = fast && (uint32_t)edits + 1 >= mef;  // :742
+        const uint32_t j = st.j;
+        const uint32_t current_ch = j < text_len ? tc[j] : 0;
+        if (j < text_len) {
+          bool have_next = false;
+          uint32_t next_ch = 0;
+          if (is_last_edit && (!fast || edits < mef) && j + 1 < text_len) { have_next = true; next_ch = tc[j + 1]; }
+          const uint32_t ms_next = st.me == st.ms ? j : st.ms;
+          int64_t exact_next = find_no_mappings(nd, current_ch);  // :776-780 (MAPPINGS=false)
+          if (exact_next >= 0) {
+            queue.push_back({(uint32_t)exact_next, j + 1, ms_next, j + 1, st.pen, edits, pc});
+            ++states_pushed;
+          }
+          bool subst_ok = fast ? (edits < mef) : subst(nlim, edits, (uint8_t)(pc >> 16));  // :803-811
+          if (subst_ok) {
+            for (auto& ed : nd.edges) {  // :814-874
+              if (exact_next >= 0 && ed.next == (uint32_t)exact_next) continue;
+              float sim = similarity(ed.first_char, current_ch);
+              if (sim < min_sym) continue;
+              float penalty = e.p_sub * (1.0f - sim);
+              if (penalty > remaining) continue;
+              if (is_last_edit) {
+                const Node& child = e.nodes[ed.next];
+                if (child.output.empty() && (!have_next || !has_matching_edge_char(child, next_ch))) continue;
+              }
+              queue.push_back({ed.next, j + 1, ms_next, j + 1, st.pen + penalty, (uint8_t)(edits + 1), pc + 0x10000});
+              ++states_pushed;
+            }
+          }
+          // swap :935-989
+          if (j + 1 < text_len && e.p_swp <= remaining && (!fast || edits < mef)) {
+            uint32_t nch = have_next ? next_ch : tc[j + 1];
+            int64_t x = find_no_mappings(nd, nch);
+            int64_t node2 = x >= 0 ? find_no_mappings(e.nodes[(size_t)x], current_ch) : -1;
+            if (node2 >= 0 && (fast || swp_ahead(node_limits((uint32_t)node2), edits, (uint8_t)(pc >> 24)))) {
+              queue.push_back({(uint32_t)node2, j + 2, st.ms, j + 2, st.pen + e.p_swp, (uint8_t)(edits + 1), pc + 0x1000000});
+              ++states_pushed;
+            }
+          }
+          // insertion :994-1029
+          if ((st.ms != st.me || st.ms != j) && e.p_ins <= remaining &&
+              (fast ? edits < mef : ins_ahead(nlim, edits, (uint8_t)(pc & 0xFF))) &&
+              !(is_last_edit && nd.output.empty() && (!have_next || !has_matching_edge_char(nd, next_ch)))) {
+            queue.push_back({st.node, j + 1, st.ms, st.me, st.pen + e.p_ins, (uint8_t)(edits + 1), pc + 1});
+            ++states_pushed;
+          }
+        }
+        // deletion :1035-1089
+        if (e.p_del <= remaining && (fast ? edits < mef : del_ahead(nlim, edits, (uint8_t)((pc >> 8) & 0xFF)))) {
+          bool have_cur = is_last_edit && j < text_len;
+          for (auto& ed : nd.edges) {
+            if (is_last_edit) {
+              const Node& child = e.nodes[ed.next];
+              if (child.output.empty() && (!have_cur || !has_matching_edge_char(child, current_ch))) continue;
+            }
+            queue.push_back({ed.next, j, st.ms, st.me, st.pen + e.p_del, (uint8_t)(edits + 1), pc + 0x100});
+            ++states_pushed;
+          }
+        }
+      }
+      (void)window_first_out;
+      if (e.has_auto_beam && effective_beam == 0) {  // :1096-1103
+        states_expanded += queue.size();
+        if (states_expanded > e.ab_budget) effective_beam = e.ab_width;
+      }
+    }
+    std::sort(out.begin(), out.end(), [](const Match& a, const Match& b) {
+      if (a.start != b.start) return a.start < b.start;
+      if (a.end != b.end) return a.end < b.end;
+      return a.pattern < b.pattern;
+    });
+  }
+
+  static uint32_t total_order_bits(float f) {  // f32::total_cmp as an unsigned key
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  }
+  // Canonical beam: keep the bw smallest by (penalty total order, position), stable.
+  static void beam_select(std::vector<State>& q, size_t q_idx, size_t bw) {
+    size_t n = q.size() - q_idx;
+    std::vector<uint64_t> keys(n);
+    for (size_t i = 0; i < n; ++i) keys[i] = ((uint64_t)total_order_bits(q[q_idx + i].pen) << 32) | (uint64_t)i;
+    std::vector<uint64_t> tmp = keys;
+    std::nth_element(tmp.begin(), tmp.begin() + (bw - 1), tmp.end());
+    uint64_t cut = tmp[bw - 1];
+    size_t w = q_idx;
+    for (size_t i = 0; i < n; ++i)
+      if (keys[i] <= cut) q[w++] = q[q_idx + i];
+    q.resize(q_idx + bw);
+  }
+};
+
+// Unit-cost bitap over a u8 id stream (prefilter.rs:410-435).
+void bitap_windows(const std::vector<uint64_t>& mask, size_t m, size_t k, const uint8_t* ids, size_t n,
+                   std::vector<std::pair<size_t, size_t>>& out) {
+  uint64_t match_bit = 1ull << (m - 1);
+  std::vector<uint64_t> r(k + 1), nr(k + 1);
+  for (size_t d = 0; d <= k; ++d) r[d] = (d >= 64 ? ~0ull : ((1ull << d) - 1));
+  size_t span = m + k;
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t bc = mask[ids[i]];
+    nr[0] = ((r[0] << 1) | 1) & bc;
+    for (size_t d = 1; d <= k; ++d)
+      nr[d] = ((r[d] << 1) & bc) | ((r[d - 1] | nr[d - 1]) << 1) | r[d - 1] | 1;
+    if (nr[k] & match_bit) {
+      size_t end = i + 1;
+      out.push_back({end >= span ? end - span : 0, end});
+    }
+    std::swap(r, nr);
+  }
+}
+
+// Staging for a (sub)haystack: ASCII fast path or caller-provided global graphemes.
+struct Staged {
+  std::vector<uint32_t> tc;
+  std::vector<uint64_t> off;  // empty = identity
+  uint64_t len = 0;
+};
+
+bool is_ascii(const uint8_t* p, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i)
+    if (p[i] & 0x80) return false;
+  return true;
+}
+
+struct Text {  // full haystack + its global segmentation (used when not ASCII)
+  const uint8_t* utf8;
+  uint64_t len;
+  uint32_t n;            // grapheme count (non-ASCII path)
+  const uint32_t* goff;  // [n+1] offsets into cps
+  const uint32_t* cps;   // folded code points of each grapheme
+  const uint64_t* boff;  // [n] grapheme byte offsets
+};
+
+// search_raw on bytes [b0, b1) of the text; grapheme range [g0, g1) used when non-ASCII.
+void search_raw_slice(const Engine& e, const Text& t, uint64_t b0, uint64_t b1, uint32_t g0, uint32_t g1,
+                      float thr, std::vector<Match>& out, uint64_t* popped) {
+  Staged s;
+  s.len = b1 - b0;
+  if (is_ascii(t.utf8 + b0, s.len)) {  // search.rs:196-203, grapheme.rs:76-125
+    s.tc.resize(s.len);
+    for (uint64_t i = 0; i < s.len; ++i) {
+      uint8_t b = t.utf8[b0 + i];
+      if (e.case_insensitive && b >= 'A' && b <= 'Z') b += 32;
+      s.tc[i] = b;
+    }
+  } else {  // search.rs:296-302 (global segmentation restricted to the slice)
+    uint32_t n = g1 - g0;
+    s.tc.resize(n);
+    s.off.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {
+      uint32_t g = g0 + i;
+      s.tc[i] = t.goff[g + 1] > t.goff[g] ? t.cps[t.goff[g]] : 0;
+      s.off[i] = t.boff[g] - b0;
+    }
+  }
+  if (s.tc.size() > 0xFFFFFFFFull) { out.clear(); return; }
+  Searcher S(e);
+  S.run(s.tc.data(), s.off.empty() ? nullptr : s.off.data(), (uint32_t)s.tc.size(), s.len, thr, out);
+  if (popped) *popped += S.states_popped;
+  for (auto& m : out) { m.start += b0; m.end += b0; }
+}
+
+}  // namespace
+
+// ==========================================================================================
+// C ABI (ctypes)
+// ==========================================================================================
+extern "C" {
+
+struct orc_config {
+  int32_t case_insensitive;
+  int32_t has_limits;
+  int32_t lim[5];  // ins, del, sub, swp, edits; -1 = None
+  float p_ins, p_del, p_sub, p_swp;
+  uint64_t beam_width;  // 0 = none
+  int32_t has_auto_beam;
+  uint64_t ab_budget, ab_width;
+  float min_symbol_similarity;
+  int32_t custom_similarity;      // 1 = use sim_ascii + sim_pairs below
+  const float* sim_ascii;         // 128*128
+  uint64_t n_sim_pairs;
+  const uint32_t* sim_pair_ab;    // 2*n
+  const float* sim_pair_val;      // n
+};
+
+struct orc_match {
+  uint64_t start, end;
+  uint32_t pattern;
+  float similarity;
+  uint8_t ins, del, sub, swp, edits, pad[3];
+};
+
+// patterns: n_patterns; per pattern: glen[i] graphemes (also the folded grapheme count),
+// weight[i], lim_flag[i] (1 = has limits), lim[i*5..]; graphemes as flat cps with offsets.
+void* orc_build(const orc_config* cfg, uint64_t n_patterns, const uint32_t* glen, const float* weight,
+                const int32_t* lim_flag, const int32_t* lim, const uint32_t* pg_off /* n_patterns+1 */,
+                const uint32_t* g_off /* total_graphemes+1 */, const uint32_t* cps) {
+  Engine* e = new Engine();
+  e->case_insensitive = cfg->case_insensitive != 0;
+  e->has_limits = cfg->has_limits != 0;
+  if (e->has_limits) {
+    e->limits.ins = cfg->lim[0]; e->limits.del = cfg->lim[1]; e->limits.sub = cfg->lim[2];
+    e->limits.swp = cfg->lim[3]; e->limits.edits = cfg->lim[4];
+  }
+  e->p_ins = cfg->p_ins; e->p_del = cfg->p_del; e->p_sub = cfg->p_sub; e->p_swp = cfg->p_swp;
+  e->beam_width = cfg->beam_width;
+  e->has_auto_beam = cfg->has_auto_beam != 0;
+  e->ab_budget = cfg->ab_budget; e->ab_width = cfg->ab_width;
+  e->min_symbol_similarity = cfg->min_symbol_similarity;
+  if (cfg->custom_similarity) {
+    for (int i = 0; i < 128; ++i)
+      for (int j = 0; j < 128; ++j) e->sim.ascii[i][j] = cfg->sim_ascii[i * 128 + j];
+    for (uint64_t k = 0; k < cfg->n_sim_pairs; ++k)
+      e->sim.map[{cfg->sim_pair_ab[2 * k], cfg->sim_pair_ab[2 * k + 1]}] = cfg->sim_pair_val[k];
+  } else {
+    default_similarity(e->sim);
+  }
+  e->patterns.resize(n_patterns);
+  for (uint64_t i = 0; i < n_patterns; ++i) {
+    Pattern& p = e->patterns[i];
+    p.glen = glen[i];
+    p.weight = weight[i];
+    p.has_limits = lim_flag[i] != 0;
+    if (p.has_limits) {
+      p.lim.ins = lim[i * 5 + 0]; p.lim.del = lim[i * 5 + 1]; p.lim.sub = lim[i * 5 + 2];
+      p.lim.swp = lim[i * 5 + 3]; p.lim.edits = lim[i * 5 + 4];
+    }
+    for (uint32_t g = pg_off[i]; g < pg_off[i + 1]; ++g)
+      p.graphemes.emplace_back(cps + g_off[g], cps + g_off[g + 1]);
+  }
+  build(*e);
+  return e;
+}
+
+void orc_free(void* h) { delete static_cast<Engine*>(h); }
+
+uint64_t orc_num_nodes(void* h) { return static_cast<Engine*>(h)->nodes.size(); }
+uint32_t orc_max_edits_fast(void* h) { return static_cast<Engine*>(h)->max_edits_fast; }
+int32_t orc_prefilter_active(void* h) { return static_cast<Engine*>(h)->bitap_ok ? 1 : 0; }
+
+// Full search_raw (search.rs:187-395) or Prefiltered::raw (prefilter.rs:146-155).
+// For non-ASCII text the caller supplies the global grapheme segmentation (folded).
+int32_t orc_search(void* h, const uint8_t* utf8, uint64_t len, uint32_t n_graphemes, const uint32_t* goff,
+                   const uint32_t* cps, const uint64_t* boff, float threshold, int32_t use_prefilter,
+                   orc_match** out, uint64_t* n_out, uint64_t* states_popped) {
+  const Engine& e = *static_cast<Engine*>(h);
+  Text t{utf8, len, n_graphemes, goff, cps, boff};
+  bool ascii = is_ascii(utf8, len);
+  uint32_t n = ascii ? (uint32_t)len : n_graphemes;
+  std::vector<Match> res;
+  uint64_t popped = 0;
+  if (ascii && len > 0xFFFFFFFFull) return 1;  // HaystackTooLarge
+  if (!use_prefilter || !e.bitap_ok) {
+    search_raw_slice(e, t, 0, len, 0, ascii ? 0 : n, threshold, res, &popped);
+  } else {
+    // prefilter.rs:304-374
+    std::vector<size_t> ks;
+    bool fallback = false;
+    for (auto& bp : e.bitap) {  // k_for :285-302
+      float nf = (float)bp.m;
+      float p_max = nf * (1.0f - threshold / bp.weight);
+      size_t k_pen = 0;
+      if (p_max <= 0.0f) k_pen = 0;
+      else {
+        float kf = std::floor(p_max * e.edit_cost_mult);
+        k_pen = kf >= 1.8446744e19f ? SIZE_MAX : (kf != kf ? 0 : (size_t)kf);  // Rust `as usize` saturates, NaN -> 0
+      }
+      size_t k = bp.has_k_limit ? std::min(k_pen, bp.k_limit) : k_pen;
+      if (k > 24) { fallback = true; break; }
+      ks.push_back(k);
+    }
+    if (fallback) {
+      search_raw_slice(e, t, 0, len, 0, ascii ? 0 : n, threshold, res, &popped);
+    } else {
+      std::vector<uint8_t> ids(n);
+      if (ascii) {
+        for (uint64_t i = 0; i < len; ++i) ids[i] = e.ascii_id[utf8[i]];
+      } else {
+        for (uint32_t g = 0; g < n; ++g) {
+          std::u32string key(cps + goff[g], cps + goff[g + 1]);
+          auto it = e.symbol_ids.find(key);
+          ids[g] = it == e.symbol_ids.end() ? 0 : (uint8_t)it->second;
+        }
+      }
+      std::vector<std::pair<size_t, size_t>> windows;
+      for (size_t i = 0; i < e.bitap.size(); ++i)
+        bitap_windows(e.bitap[i].mask, e.bitap[i].m, ks[i], ids.data(), n, windows);
+      if (!windows.empty()) {
+        std::sort(windows.begin(), windows.end());
+        std::vector<std::pair<size_t, size_t>> merged;
+        for (auto& w : windows) {
+          if (!merged.empty() && w.first <= merged.back().second)
+            merged.back().second = std::max(merged.back().second, w.second);
+          else
+            merged.push_back(w);
+        }
+        std::map<std::tuple<uint64_t, uint64_t, uint32_t>, Match> best;
+        for (auto& w : merged) {
+          size_t gs = w.first, ge = std::min(w.second, (size_t)n);
+          uint64_t bs = ascii ? gs : boff[gs];
+          uint64_t be = ascii ? ge : (ge < n ? boff[ge] : len);
+          std::vector<Match> part;
+          search_raw_slice(e, t, bs, be, (uint32_t)gs, (uint32_t)ge, threshold, part, &popped);
+          for (auto& m : part) {
+            auto key = std::make_tuple(m.start, m.end, m.pattern);
+            auto it = best.find(key);
+            if (it == best.end()) best.emplace(key, m);
+            else if (m.similarity > it->second.similarity) it->second = m;
+          }
+        }
+        for (auto& kv : best) res.push_back(kv.second);
+      }
+    }
+  }
+  *n_out = res.size();
+  *out = (orc_match*)std::malloc(sizeof(orc_match) * (res.size() ? res.size() : 1));
+  for (size_t i = 0; i < res.size(); ++i) {
+    orc_match& o = (*out)[i];
+    std::memset(&o, 0, sizeof(o));
+    o.start = res[i].start; o.end = res[i].end; o.pattern = res[i].pattern; o.similarity = res[i].similarity;
+    o.ins = res[i].ins; o.del = res[i].del; o.sub = res[i].sub; o.swp = res[i].swp; o.edits = res[i].edits;
+  }
+  if (states_popped) *states_popped = popped;
+  return 0;
+}
+
+void orc_matches_free(orc_match* m) { std::free(m); }
+
+// Standalone bitap over an id stream with an explicit mask (for the brute-force DP check,
+// examples/bitap_prototype.rs:21-56). Writes match END positions (1-based exclusive) into ends.
+uint64_t orc_bitap_ends(const uint8_t* pattern, uint64_t m, const uint8_t* text, uint64_t n, uint64_t k,
+                        uint64_t* ends) {
+  std::vector<uint64_t> mask(256, 0);
+  for (uint64_t i = 0; i < m; ++i) mask[pattern[i]] |= 1ull << i;
+  std::vector<std::pair<size_t, size_t>> w;
+  bitap_windows(mask, m, k, text, n, w);
+  for (size_t i = 0; i < w.size(); ++i) ends[i] = w[i].second;
+  return w.size();
+}
+
+}  // extern "C"

@@ -1,0 +1,133 @@
+"""GPU engine vs CPU oracle on identical seeded inputs (bit-exact spans, pattern ids, similarity
+bits and edit counts). Mirrors the reference's own differential fuzz (prefilter.rs:441-546:
+xorshift Rng, random vocab/filler haystacks, edits 0..=2, random case-insensitivity, thresholds
+0.6-0.9) and widens it to the options the hot path has (beam, per-pattern limits, penalties,
+min_symbol_similarity, custom similarity, Unicode, empty/edge inputs)."""
+import pytest
+
+from fuzzy_aho_corasick import (FuzzyAhoCorasickBuilder as B, FuzzyLimits as L, FuzzyPenalties, Pattern,
+                                SearchOptions as O, Similarity)
+from oracle_harness import OracleEngine
+
+pytestmark = pytest.mark.gpu
+
+
+class Rng:  # prefilter.rs:441-452
+    def __init__(self, s):
+        self.s = s
+
+    def next(self):
+        x = self.s
+        x ^= (x << 13) & 0xFFFFFFFFFFFFFFFF
+        x ^= x >> 7
+        x ^= (x << 17) & 0xFFFFFFFFFFFFFFFF
+        self.s = x
+        return x
+
+
+def rows(ms):
+    return sorted((m.start, m.end, m.pattern_index, m.sim_bits(), m.insertions, m.deletions, m.substitutions,
+                   m.swaps, m.edits) for m in ms)
+
+
+def compare(builder, patterns, hay, thr, prefilter=False):
+    gpu = builder.build(patterns)
+    orc = OracleEngine(builder, patterns)
+    if prefilter:
+        g = gpu.with_prefilter().search(hay, O().threshold(thr))
+        o = orc.with_prefilter().search(hay, O().threshold(thr))
+    else:
+        g = gpu.search(hay, O().threshold(thr))
+        o = orc.search(hay, O().threshold(thr))
+    gr, orr = rows(g), rows(o)
+    assert gr == orr, f"patterns={patterns!r} hay={hay!r} thr={thr} prefilter={prefilter}\n gpu={gr}\n orc={orr}"
+    return len(gr)
+
+
+ASCII_VOCAB = ["hello", "world", "vestibulum", "abc", "lorem", "cell", "saddam", "hussein", "ab", "x"]
+ASCII_FILLER = ["a", "b", "c", "d", "e", " ", "1", "o", "0", "l", "S", "H"]
+UNI_VOCAB = ["café", "naïve", "Ωμέγα", "Москва", "señor", "école", "résumé"]
+UNI_FILLER = ["a", "é", "ñ", "ω", "м", " ", "o", "0", "é", "Ω", "\r\n", "Σ"]
+
+
+def random_case(rng, vocab, filler, allow_beam=True, allow_limits=True):
+    npat = 1 + rng.next() % 4
+    pats = [vocab[rng.next() % len(vocab)] for _ in range(npat)]
+    edits = rng.next() % 4
+    b = B().case_insensitive(rng.next() & 1 == 0)
+    mode = rng.next() % 6
+    if edits > 0 and mode != 5:
+        b = b.fuzzy(L().edits(edits))
+    if mode == 5 and allow_limits:  # per-type / per-pattern limits -> the 255 path
+        b = b.fuzzy(L().insertions(rng.next() % 2).deletions(rng.next() % 2).substitutions(rng.next() % 2)
+                    .swaps(rng.next() % 2))
+        pats = [Pattern(p).fuzzy(L().edits(rng.next() % 3)) if rng.next() % 2 else p for p in pats]
+    if rng.next() % 5 == 0:
+        b = b.penalties(FuzzyPenalties.default().with_swap(0.6).with_insertion(0.5).with_deletion(0.8))
+    if allow_beam and rng.next() % 4 == 0:
+        b = b.beam_width(1 + rng.next() % 12)
+    if rng.next() % 7 == 0:
+        b = b.min_symbol_similarity(0.3)
+    hay = ""
+    for _ in range(rng.next() % 60):
+        if rng.next() % 7 == 0:
+            w = pats[rng.next() % len(pats)]
+            hay += (w if isinstance(w, str) else w.pattern) + " "
+        else:
+            hay += filler[rng.next() % len(filler)]
+    thr = 0.6 + (rng.next() % 4) * 0.1 if rng.next() % 5 else 0.0
+    return b, pats, hay, thr
+
+
+@pytest.mark.parametrize("seed,vocab,filler", [
+    (0x1234_5678_9abc_def1, ASCII_VOCAB, ASCII_FILLER),
+    (0xdead_beef_0bad_f00d, UNI_VOCAB, UNI_FILLER),
+])
+def test_differential_random(seed, vocab, filler):
+    rng = Rng(seed)
+    total = 0
+    for _ in range(150):
+        b, pats, hay, thr = random_case(rng, vocab, filler)
+        total += compare(b, pats, hay, thr)
+    assert total > 0
+
+
+@pytest.mark.parametrize("seed,vocab,filler", [
+    (0x1234_5678_9abc_def1, ASCII_VOCAB, ASCII_FILLER),
+    (0xdead_beef_0bad_f00d, UNI_VOCAB, UNI_FILLER),
+])
+def test_prefilter_differential(seed, vocab, filler):
+    """Prefiltered::search == engine.search (prefilter.rs:467-546), GPU vs oracle, both paths."""
+    rng = Rng(seed ^ 0x55)
+    for _ in range(120):
+        b, pats, hay, thr = random_case(rng, vocab, filler, allow_beam=False)
+        n = compare(b, pats, hay, thr, prefilter=True)
+        gpu = b.build(pats)
+        full = rows(gpu.search(hay, O().threshold(thr)))
+        pf = rows(gpu.with_prefilter().search(hay, O().threshold(thr)))
+        assert [r[:4] for r in full] == [r[:4] for r in pf]
+        assert len(pf) == n
+
+
+def test_edge_inputs():
+    b = B().fuzzy(L().edits(2))
+    compare(b, ["abc"], "", 0.0)                      # empty haystack
+    compare(b, [], "hello", 0.0)                      # no patterns
+    compare(b, [""], "ab", 0.0)                        # empty pattern: NaN similarity kept (Q7)
+    compare(b, ["a"], "a", 0.0)                        # 1-grapheme pattern, deletion-only empty spans (Q4)
+    compare(B(), ["JOINT STOCK COMPANY", "STOCK"], "JOINT STOCK COMPANY GAZPROM", 0.8)  # Q1
+    compare(B().fuzzy(L().edits(1)), ["ab\r\ncd"], "xx ab\r\ncd yy é", 0.5)           # Q3 unicode \r\n
+    compare(B().fuzzy(L().edits(1)), ["ab\r\ncd"], "xx ab\r\ncd yy", 0.5)             # Q3 ascii \r\n
+    compare(B().case_insensitive(True).fuzzy(L().edits(1)), ["ÉCOLE", "école"], "école école ÉCOLE", 0.5)
+    compare(B().fuzzy(L().edits(1)), [("heavy", 2.0), ("light", 0.5)], "heavy light hevy lihgt", 0.5)
+    sim = Similarity.from_map({("a", "b"): 0.9, ("b", "a"): 0.9, ("é", "e"): 0.8, ("ω", "o"): 0.5})
+    compare(B().fuzzy(L().edits(1)).similarity(sim), ["bab", "cafe", "omega"], "aab café ωmega", 0.6)
+
+
+def test_long_haystack_windows():
+    """Many windows spanning several kernel chunks; exercises the grid-stride loop."""
+    rng = Rng(77)
+    words = ["needle", "haystack", "fuzzy", "automaton"]
+    text = " ".join(words[rng.next() % 4][: 3 + rng.next() % 6] + "xyz"[rng.next() % 3] for _ in range(3000))
+    compare(B().fuzzy(L().edits(1)), words, text, 0.7)
+    compare(B().fuzzy(L().edits(2)).beam_width(8), words, text, 0.7)
