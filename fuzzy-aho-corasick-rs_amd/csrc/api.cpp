@@ -267,6 +267,26 @@ int fac_search_prefiltered(const fac_engine* engine, const uint8_t* utf8, uint64
   return copy_out(merged, out, n_out);
 }
 
+int64_t fac_prefilter_windows(const fac_engine* engine, const uint8_t* utf8, uint64_t len, float threshold,
+                              uint64_t* out, uint64_t cap) {
+  if (!engine) return fail(FAC_E_INVALID, "NULL argument"), -1;
+  const fac::Engine& e = engine->e;
+  std::vector<uint32_t> ks;
+  if (!e.bitap_ok || !prefilter_ks(e, threshold, ks)) return -1;
+  fac_haystack* hay = nullptr;
+  if (fac_haystack_stage(engine, utf8, len, &hay, nullptr)) return -1;
+  std::string err;
+  std::vector<std::pair<uint64_t, uint64_t>> windows;
+  int rc = fac::prefilter_windows(e, hay->h, ks, nullptr, windows, nullptr, err);
+  fac_haystack_free(hay);
+  if (rc) return fail(rc, err), -1;
+  for (size_t i = 0; i < windows.size() && i < cap; ++i) {
+    out[2 * i] = windows[i].first;
+    out[2 * i + 1] = windows[i].second;
+  }
+  return (int64_t)windows.size();
+}
+
 uint64_t fac_segment_graphemes(const uint8_t* utf8, uint64_t len, uint64_t* starts, uint64_t cap) {
   std::vector<uint64_t> s;
   fac::segment_graphemes(utf8, len, s);

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -703,17 +704,31 @@ hipError_t launch_variant(const Variant& v, uint32_t grid, hipStream_t s, const 
   return hipGetLastError();
 }
 
-// RAII for stream-ordered scratch
+bool debug_poison() {
+  static const bool v = [] {
+    const char* e = std::getenv("FAC_DEBUG_POISON");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+// RAII scratch. Plain hipMalloc/hipFree: with the stream-ordered pool (hipMallocAsync /
+// hipFreeAsync) on ROCm 7.2 the match counter of a recycled block intermittently came back short
+// (reproduced 6/60 calls; 0/60 with hipMalloc), so the pool is not used.
 struct DevBuf {
   void* p = nullptr;
   hipStream_t s = nullptr;
-  ~DevBuf() {
-    if (p) (void)hipFreeAsync(p, s);
+  ~DevBuf() { release(); }
+  void release() {
+    if (!p) return;
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(p);
+    p = nullptr;
   }
   hipError_t alloc(size_t bytes, hipStream_t stream) {
-    if (p) (void)hipFreeAsync(p, s);
+    release();
     s = stream;
-    return hipMallocAsync(&p, std::max<size_t>(bytes, 16), stream);
+    return hipMalloc(&p, std::max<size_t>(bytes, 16));
   }
 };
 
@@ -749,6 +764,9 @@ int upload_engine(Engine& e, std::string& err) {
     std::vector<uint8_t> aid(e.ascii_id, e.ascii_id + 128);
     if ((rc = upload(aid, &e.d_ascii_id, err))) return rc;
   }
+  // Pageable hipMemcpy may return before the DMA lands and the engine's stream is non-blocking:
+  // make the tables visible to every stream before the first launch.
+  HIP_TRY(hipDeviceSynchronize());
   return FAC_OK;
 }
 
@@ -782,8 +800,11 @@ int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack&
   }
   if (h.n > 0xFFFFFFFFull) return FAC_E_HAYSTACK_TOO_LARGE;
   HIP_TRY(hipSetDevice(e.device));
+  // All uploads go through the engine's stream and are synchronized before returning, so kernels
+  // on any stream see complete data (pageable copies may otherwise still be in flight).
+  hipStream_t st = e.stream;
   HIP_TRY(hipMalloc((void**)&h.d_utf8, std::max<uint64_t>(len, 16)));
-  if (len) HIP_TRY(hipMemcpy(h.d_utf8, utf8, len, hipMemcpyHostToDevice));
+  if (len) HIP_TRY(hipMemcpyAsync(h.d_utf8, utf8, len, hipMemcpyHostToDevice, st));
   if (!h.ascii) {
     std::vector<uint32_t> tc(h.n);
     for (uint64_t g = 0; g < h.n; ++g) {
@@ -791,9 +812,10 @@ int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack&
       tc[g] = fold_first_char(utf8, b, en, e.case_insensitive);
     }
     HIP_TRY(hipMalloc((void**)&h.d_text32, std::max<uint64_t>(h.n * 4, 16)));
-    HIP_TRY(hipMemcpy(h.d_text32, tc.data(), h.n * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(h.d_text32, tc.data(), h.n * 4, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMalloc((void**)&h.d_off, std::max<uint64_t>(h.n * 8, 16)));
-    HIP_TRY(hipMemcpy(h.d_off, h.starts.data(), h.n * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(h.d_off, h.starts.data(), h.n * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));  // `tc` is a local buffer
     if (e.bitap_ok) {  // transcode, grapheme path (prefilter.rs:262-280)
       h.sym.assign(h.n, 0);
       std::u32string g;
@@ -805,6 +827,7 @@ int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack&
       }
     }
   }
+  HIP_TRY(hipStreamSynchronize(st));
   return FAC_OK;
 }
 
@@ -913,6 +936,7 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
     P.out_cap = out_cap;
     P.counters = static_cast<unsigned long long*>(d_cnt.p);
     HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 4 * sizeof(unsigned long long), stream));
+    if (debug_poison()) HIP_TRY(hipMemsetAsync(d_out.p, 0xAB, out_cap * sizeof(fac_match), stream));
     HIP_TRY(hipEventRecord(ev.a, stream));
     const hipError_t le = launch_variant(variants[vi], grid, stream, P);
     if (le != hipSuccess) {

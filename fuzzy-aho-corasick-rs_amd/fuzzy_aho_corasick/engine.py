@@ -241,6 +241,17 @@ class Prefiltered:
         return self.engine.search_raw(haystack, opts.threshold_, prefilter=True).apply(opts.order_, opts.overlap_)
 
 
+def prefilter_windows(engine: "FuzzyAhoCorasick", haystack: str, threshold: float):
+    """Diagnostics: merged bitap candidate windows (grapheme ranges), or None on fallback."""
+    data = haystack.encode("utf-8")
+    cap = 2 * len(data) + 16
+    buf = (ctypes.c_uint64 * (2 * cap))()
+    n = _native.lib.fac_prefilter_windows(engine._h, data, len(data), f32(threshold), buf, cap)
+    if n < 0:
+        return None
+    return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
+
+
 class StagedHaystack:
     """A haystack staged into HBM once (fac_haystack_stage) and searched many times."""
 

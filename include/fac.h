@@ -167,6 +167,12 @@ int fac_search_staged(const fac_engine* engine, const fac_haystack* hay, uint64_
                       uint64_t window_end, float threshold, void* stream, fac_match** out,
                       uint64_t* n_out, fac_stats* stats);
 
+/* Diagnostics: the merged candidate windows (grapheme ranges [start, end)) of the bitap
+ * pre-filter for `threshold` (prefilter.rs:319-342). Returns the window count (writes up to `cap`
+ * pairs into `out`), or -1 if the pre-filter would fall back to a full search. */
+int64_t fac_prefilter_windows(const fac_engine* engine, const uint8_t* utf8, uint64_t len, float threshold,
+                              uint64_t* out, uint64_t cap);
+
 /* Engine introspection (tests / diagnostics). */
 uint64_t fac_engine_num_nodes(const fac_engine* engine);
 uint32_t fac_engine_max_edits_fast(const fac_engine* engine);

@@ -840,6 +840,44 @@ int32_t orc_search(void* h, const uint8_t* utf8, uint64_t len, uint32_t n_graphe
 
 void orc_matches_free(orc_match* m) { std::free(m); }
 
+// Merged bitap windows (prefilter.rs:319-342) for diagnostics; -1 = full-search fallback.
+int64_t orc_prefilter_windows(void* h, const uint8_t* utf8, uint64_t len, uint32_t n_graphemes, const uint32_t* goff,
+                              const uint32_t* cps, float threshold, uint64_t* out, uint64_t cap) {
+  const Engine& e = *static_cast<Engine*>(h);
+  if (!e.bitap_ok) return -1;
+  bool ascii = is_ascii(utf8, len);
+  uint32_t n = ascii ? (uint32_t)len : n_graphemes;
+  std::vector<size_t> ks;
+  for (auto& bp : e.bitap) {
+    float nf = (float)bp.m;
+    float p_max = nf * (1.0f - threshold / bp.weight);
+    size_t k_pen = 0;
+    if (!(p_max <= 0.0f)) {
+      float kf = std::floor(p_max * e.edit_cost_mult);
+      k_pen = kf >= 1.8446744e19f ? SIZE_MAX : (kf != kf ? 0 : (size_t)kf);
+    }
+    size_t k = bp.has_k_limit ? std::min(k_pen, bp.k_limit) : k_pen;
+    if (k > 24) return -1;
+    ks.push_back(k);
+  }
+  std::vector<uint8_t> ids(n);
+  for (uint32_t g = 0; g < n; ++g) {
+    if (ascii) { ids[g] = e.ascii_id[utf8[g]]; continue; }
+    std::u32string key(cps + goff[g], cps + goff[g + 1]);
+    auto it = e.symbol_ids.find(key);
+    ids[g] = it == e.symbol_ids.end() ? 0 : (uint8_t)it->second;
+  }
+  std::vector<std::pair<size_t, size_t>> windows, merged;
+  for (size_t i = 0; i < e.bitap.size(); ++i) bitap_windows(e.bitap[i].mask, e.bitap[i].m, ks[i], ids.data(), n, windows);
+  std::sort(windows.begin(), windows.end());
+  for (auto& w : windows) {
+    if (!merged.empty() && w.first <= merged.back().second) merged.back().second = std::max(merged.back().second, w.second);
+    else merged.push_back(w);
+  }
+  for (size_t i = 0; i < merged.size() && i < cap; ++i) { out[2 * i] = merged[i].first; out[2 * i + 1] = merged[i].second; }
+  return (int64_t)merged.size();
+}
+
 // Standalone bitap over an id stream with an explicit mask (for the brute-force DP check,
 // examples/bitap_prototype.rs:21-56). Writes match END positions (1-based exclusive) into ends.
 uint64_t orc_bitap_ends(const uint8_t* pattern, uint64_t m, const uint8_t* text, uint64_t n, uint64_t k,

@@ -67,6 +67,9 @@ _lib.orc_search.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, c
                             ctypes.POINTER(ctypes.POINTER(orc_match)), ctypes.POINTER(ctypes.c_uint64),
                             ctypes.POINTER(ctypes.c_uint64)]
 _lib.orc_matches_free.argtypes = [ctypes.POINTER(orc_match)]
+_lib.orc_prefilter_windows.restype = ctypes.c_int64
+_lib.orc_prefilter_windows.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, _U32P, _U32P,
+                                       ctypes.c_float, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64]
 _lib.orc_bitap_ends.restype = ctypes.c_uint64
 _lib.orc_bitap_ends.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
                                 ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
@@ -177,6 +180,22 @@ class OracleEngine:
         _lib.orc_matches_free(out)
         self.states_popped = popped.value
         return rows
+
+    def prefilter_windows(self, haystack, threshold):
+        data = haystack.encode("utf-8")
+        goff, cps = [0], []
+        if not data.isascii():
+            for g in graphemes(haystack):
+                cps += [ord(c) for c in fold(g, self.ci)]
+                goff.append(len(cps))
+        cap = 2 * len(data) + 16
+        buf = (ctypes.c_uint64 * (2 * cap))()
+        n = _lib.orc_prefilter_windows(self._h, data, len(data), len(goff) - 1,
+                                       (ctypes.c_uint32 * max(1, len(goff)))(*goff),
+                                       (ctypes.c_uint32 * max(1, len(cps)))(*cps), f32(threshold), buf, cap)
+        if n < 0:
+            return None
+        return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
 
     # same surface as FuzzyAhoCorasick
     def search_raw(self, haystack, threshold, prefilter=False):

@@ -109,6 +109,25 @@ def test_prefilter_differential(seed, vocab, filler):
         assert len(pf) == n
 
 
+@pytest.mark.parametrize("seed,vocab,filler", [
+    (0x1234_5678_9abc_def1, ASCII_VOCAB, ASCII_FILLER),
+    (0xdead_beef_0bad_f00d, UNI_VOCAB, UNI_FILLER),
+])
+def test_bitap_windows_match_reference_merge(seed, vocab, filler):
+    """GPU bitap + run extraction == bitap_windows + sort + merge (prefilter.rs:319-342), and is
+    deterministic across repeated calls."""
+    from fuzzy_aho_corasick.engine import prefilter_windows
+    rng = Rng(seed ^ 0x77)
+    for _ in range(120):
+        b, pats, hay, thr = random_case(rng, vocab, filler, allow_beam=False)
+        gpu = b.build(pats)
+        orc = OracleEngine(b, pats)
+        want = orc.prefilter_windows(hay, thr)
+        for _rep in range(3):
+            got = prefilter_windows(gpu, hay, thr)
+            assert got == want, f"patterns={pats!r} hay={hay!r} thr={thr}\n gpu={got}\n orc={want}"
+
+
 def test_edge_inputs():
     b = B().fuzzy(L().edits(2))
     compare(b, ["abc"], "", 0.0)                      # empty haystack
