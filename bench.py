@@ -62,20 +62,13 @@ def main():
     graphemes = staged.graphemes
     stream = torch.cuda.current_stream().cuda_stream
 
+    from fuzzy_aho_corasick.distributed import gather_rows
+    dev = torch.device("cuda", local)
+
     def step():
         rows, st = staged.search_windows(wl.threshold, stream=stream)
         if world > 1:  # gather the 32 B Match records to rank 0 over RCCL (xGMI)
-            import struct as _s
-            rec = torch.frombuffer(bytearray(b"".join(_s.pack("<QQIf5B3x", *r) for r in rows)) or bytearray(32),
-                                   dtype=torch.uint8).cuda()
-            n = torch.tensor([len(rows)], device="cuda", dtype=torch.int64)
-            counts = [torch.zeros_like(n) for _ in range(world)]
-            dist.all_gather(counts, n)
-            cap = int(max(c.item() for c in counts)) * 32 or 32
-            padded = torch.zeros(cap, dtype=torch.uint8, device="cuda")
-            padded[: rec.numel()] = rec[:cap]
-            bufs = [torch.empty_like(padded) for _ in range(world)] if rank == 0 else None
-            dist.gather(padded, bufs, dst=0)
+            gather_rows(rows, dev)
         return rows, st
 
     for _ in range(args.warmup):

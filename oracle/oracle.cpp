@@ -410,6 +410,8 @@ struct Searcher {
   uint64_t states_popped = 0, states_pushed = 0;
 
   // `text_chars`, grapheme byte offsets (nullptr = identity), haystack byte length.
+  uint32_t w_begin = 0, w_end = 0xFFFFFFFFu;  // start-window range (sharding diagnostics)
+
   void run(const uint32_t* tc, const uint64_t* off, uint32_t n, uint64_t hay_len, float thr,
            std::vector<Match>& out) {
     out.clear();
@@ -447,7 +449,7 @@ struct Searcher {
     size_t effective_beam = e.beam_width;  // 0 = None
     size_t states_expanded = 0;
 
-    for (uint32_t start = 0; start < text_len; ++start) {
+    for (uint32_t start = w_begin; start < text_len && start < w_end; ++start) {
       if (ws) {  // :535-553
         uint32_t ch = tc[start];
         if (ch < 128 && !((first_bits >> ch) & 1)) {
@@ -647,7 +649,8 @@ struct Text {  // full haystack + its global segmentation (used when not ASCII)
 
 // search_raw on bytes [b0, b1) of the text; grapheme range [g0, g1) used when non-ASCII.
 void search_raw_slice(const Engine& e, const Text& t, uint64_t b0, uint64_t b1, uint32_t g0, uint32_t g1,
-                      float thr, std::vector<Match>& out, uint64_t* popped) {
+                      float thr, std::vector<Match>& out, uint64_t* popped, uint32_t w_begin = 0,
+                      uint32_t w_end = 0xFFFFFFFFu) {
   Staged s;
   s.len = b1 - b0;
   if (is_ascii(t.utf8 + b0, s.len)) {  // search.rs:196-203, grapheme.rs:76-125
@@ -669,6 +672,8 @@ void search_raw_slice(const Engine& e, const Text& t, uint64_t b0, uint64_t b1, 
   }
   if (s.tc.size() > 0xFFFFFFFFull) { out.clear(); return; }
   Searcher S(e);
+  S.w_begin = w_begin;
+  S.w_end = w_end;
   S.run(s.tc.data(), s.off.empty() ? nullptr : s.off.data(), (uint32_t)s.tc.size(), s.len, thr, out);
   if (popped) *popped += S.states_popped;
   for (auto& m : out) { m.start += b0; m.end += b0; }
@@ -754,9 +759,24 @@ int32_t orc_prefilter_active(void* h) { return static_cast<Engine*>(h)->bitap_ok
 
 // Full search_raw (search.rs:187-395) or Prefiltered::raw (prefilter.rs:146-155).
 // For non-ASCII text the caller supplies the global grapheme segmentation (folded).
+int32_t orc_search_windows(void* h, const uint8_t* utf8, uint64_t len, uint32_t n_graphemes, const uint32_t* goff,
+                           const uint32_t* cps, const uint64_t* boff, float threshold, int32_t use_prefilter,
+                           orc_match** out, uint64_t* n_out, uint64_t* states_popped, uint32_t w_begin,
+                           uint32_t w_end);
+
 int32_t orc_search(void* h, const uint8_t* utf8, uint64_t len, uint32_t n_graphemes, const uint32_t* goff,
                    const uint32_t* cps, const uint64_t* boff, float threshold, int32_t use_prefilter,
                    orc_match** out, uint64_t* n_out, uint64_t* states_popped) {
+  return orc_search_windows(h, utf8, len, n_graphemes, goff, cps, boff, threshold, use_prefilter, out, n_out,
+                            states_popped, 0, 0xFFFFFFFFu);
+}
+
+// search_raw restricted to start windows [w_begin, w_end) (no prefilter): the per-rank work of a
+// sharded search; the union over a partition of [0, n) equals search_raw.
+int32_t orc_search_windows(void* h, const uint8_t* utf8, uint64_t len, uint32_t n_graphemes, const uint32_t* goff,
+                           const uint32_t* cps, const uint64_t* boff, float threshold, int32_t use_prefilter,
+                           orc_match** out, uint64_t* n_out, uint64_t* states_popped, uint32_t w_begin,
+                           uint32_t w_end) {
   const Engine& e = *static_cast<Engine*>(h);
   Text t{utf8, len, n_graphemes, goff, cps, boff};
   bool ascii = is_ascii(utf8, len);
@@ -765,7 +785,7 @@ int32_t orc_search(void* h, const uint8_t* utf8, uint64_t len, uint32_t n_graphe
   uint64_t popped = 0;
   if (ascii && len > 0xFFFFFFFFull) return 1;  // HaystackTooLarge
   if (!use_prefilter || !e.bitap_ok) {
-    search_raw_slice(e, t, 0, len, 0, ascii ? 0 : n, threshold, res, &popped);
+    search_raw_slice(e, t, 0, len, 0, ascii ? 0 : n, threshold, res, &popped, w_begin, w_end);
   } else {
     // prefilter.rs:304-374
     std::vector<size_t> ks;

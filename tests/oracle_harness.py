@@ -67,6 +67,8 @@ _lib.orc_search.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, c
                             ctypes.POINTER(ctypes.POINTER(orc_match)), ctypes.POINTER(ctypes.c_uint64),
                             ctypes.POINTER(ctypes.c_uint64)]
 _lib.orc_matches_free.argtypes = [ctypes.POINTER(orc_match)]
+_lib.orc_search_windows.restype = ctypes.c_int32
+_lib.orc_search_windows.argtypes = _lib.orc_search.argtypes + [ctypes.c_uint32, ctypes.c_uint32]
 _lib.orc_prefilter_windows.restype = ctypes.c_int64
 _lib.orc_prefilter_windows.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, _U32P, _U32P,
                                        ctypes.c_float, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64]
@@ -152,7 +154,7 @@ class OracleEngine:
     def max_edits_fast(self):
         return int(_lib.orc_max_edits_fast(self._h))
 
-    def raw_rows(self, haystack, threshold, prefilter=False):
+    def raw_rows(self, haystack, threshold, prefilter=False, windows=None):
         data = haystack.encode("utf-8") if isinstance(haystack, str) else haystack
         text = data.decode("utf-8")
         goff, cps, boff = [0], [], []
@@ -167,10 +169,11 @@ class OracleEngine:
         out = ctypes.POINTER(orc_match)()
         cnt = ctypes.c_uint64()
         popped = ctypes.c_uint64()
-        rc = _lib.orc_search(self._h, data, len(data), ng, (ctypes.c_uint32 * max(1, len(goff)))(*goff),
-                             (ctypes.c_uint32 * max(1, len(cps)))(*cps),
-                             (ctypes.c_uint64 * max(1, ng))(*boff), f32(threshold), int(prefilter),
-                             ctypes.byref(out), ctypes.byref(cnt), ctypes.byref(popped))
+        w0, w1 = windows if windows is not None else (0, 0xFFFFFFFF)
+        rc = _lib.orc_search_windows(self._h, data, len(data), ng, (ctypes.c_uint32 * max(1, len(goff)))(*goff),
+                                     (ctypes.c_uint32 * max(1, len(cps)))(*cps),
+                                     (ctypes.c_uint64 * max(1, ng))(*boff), f32(threshold), int(prefilter),
+                                     ctypes.byref(out), ctypes.byref(cnt), ctypes.byref(popped), w0, w1)
         if rc:
             raise RuntimeError(f"oracle error {rc}")
         rows = []
