@@ -66,7 +66,7 @@ static_assert(sizeof(DevPattern) == 32, "DevPattern layout");
 
 // Dedup entry / queued state, 16 B. j and matched_end are stored relative to the window start
 // (matched_start == start for every state of a window).
-struct KState {
+struct alignas(16) KState {
   uint32_t node;
   uint32_t jm;     // j_rel | me_rel << 16
   float pen;

@@ -39,13 +39,38 @@ __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint32_t prefix_below(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
-__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int l) { return (uint32_t)__shfl((int)v, l, 64); }
-__device__ __forceinline__ float shfl_f32(float v, int l) { return __shfl(v, l, 64); }
+// Reads from a wave-uniform lane: v_readlane (scalar path), not ds_bpermute through the LDS unit.
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ float shfl_f32(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int l) {
+  const uint32_t lo = shfl_u32((uint32_t)v, l), hi = shfl_u32((uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ int first_lane(uint64_t m) { return __ffsll((unsigned long long)m) - 1; }
+
+// err flags are set identically by every lane inside a window; a ballot is enough to test them.
+__device__ __forceinline__ bool any_err(unsigned err) { return __ballot(err != 0) != 0; }
 
 __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
   return v;
+}
+
+// Wave-wide minimum with DPP row shifts + row broadcasts (no LDS round trip); result is uniform.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+  const int I = -1;  // identity for unsigned min (0xFFFFFFFF)
+  int x = (int)v;
+  x = (int)min((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(I, x, 0x111, 0xF, 0xF, false));  // row_shr:1
+  x = (int)min((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(I, x, 0x112, 0xF, 0xF, false));  // row_shr:2
+  x = (int)min((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(I, x, 0x114, 0xF, 0xF, false));  // row_shr:4
+  x = (int)min((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(I, x, 0x118, 0xF, 0xF, false));  // row_shr:8
+  x = (int)min((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(I, x, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  x = (int)min((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(I, x, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane(x, 63);
 }
 
 __device__ __forceinline__ uint32_t edits_of(uint32_t packed) {
@@ -175,43 +200,52 @@ __device__ void emit_update(EmitList& L, uint32_t me_rel, uint32_t p, float sim,
 // `select_nth_unstable_by(bw - 1, total_cmp)` + `truncate(q_idx + bw)` (search.rs:584-587).
 template <uint32_t QCAP>
 __device__ void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t bw) {
+  constexpr int PER = QCAP / 64;  // keys per lane (pending <= QCAP)
   const uint32_t lane = lane_id();
   const uint32_t P = tail - head;
-  uint32_t prefix = 0, rank = bw - 1;  // radix-select the key of the bw-th smallest (MSB first)
-  for (int bit = 31; bit >= 0; --bit) {
-    const uint32_t hi_mask = bit == 31 ? 0u : (0xFFFFFFFFu << (bit + 1));
-    uint32_t c0 = 0;
-    for (uint32_t base = 0; base < P; base += 64) {
-      const uint32_t i = base + lane;
-      bool hit = false;
-      if (i < P) {
-        const uint32_t k = total_order_key(q[(head + i) & (QCAP - 1)].pen);
-        hit = ((k & hi_mask) == prefix) && !((k >> bit) & 1u);
-      }
-      c0 += __popcll(__ballot(hit));
-    }
-    if (rank >= c0) {
-      rank -= c0;
-      prefix |= 1u << bit;
-    }
+  uint32_t key[PER];
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    const uint32_t i = (uint32_t)t * 64 + lane;
+    key[t] = i < P ? total_order_key(q[(head + i) & (QCAP - 1)].pen) : 0xFFFFFFFFu;
   }
-  const uint32_t T = prefix, need_eq = rank + 1;  // keep all keys < T and the first need_eq == T
-  uint32_t w = head, eq_seen = 0;
-  for (uint32_t base = 0; base < P; base += 64) {
-    const uint32_t i = base + lane;
-    const bool valid = i < P;
-    KState s{};
-    uint32_t k = 0xFFFFFFFFu;
-    if (valid) {
-      s = q[(head + i) & (QCAP - 1)];
-      k = total_order_key(s.pen);
+  // Walk the distinct penalty keys upwards until `bw` states are covered: T = the bw-th smallest
+  // key, need_eq = how many states with key T survive (the first ones in queue order).
+  uint32_t left = bw, T = 0xFFFFFFFFu, need_eq = 0;
+  bool have_last = false;
+  uint32_t last = 0;
+  for (;;) {
+    uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+    for (int t = 0; t < PER; ++t)
+      if (!have_last || key[t] > last) m = min(m, key[t]);
+    m = wave_min_u32(m);
+    uint32_t c = 0;
+#pragma unroll
+    for (int t = 0; t < PER; ++t) c += __popcll(__ballot(key[t] == m && (uint32_t)t * 64 + lane < P));
+    if (c >= left || m == 0xFFFFFFFFu) {
+      T = m;
+      need_eq = left;
+      break;
     }
+    left -= c;
+    last = m;
+    have_last = true;
+  }
+  uint32_t w = head, eq_seen = 0;  // stable in-place compaction, chunk by chunk
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    const uint32_t i = (uint32_t)t * 64 + lane;
+    const bool valid = i < P;
+    const uint32_t k = key[t];
     const bool eq = valid && k == T;
     const uint64_t meq = __ballot(eq);
     const bool keep = valid && (k < T || (eq && eq_seen + prefix_below(meq) < need_eq));
     const uint64_t mk = __ballot(keep);
+    // read the whole chunk, then write the survivors (destination slots never exceed sources)
+    const uint4 v = keep ? reinterpret_cast<const uint4*>(q)[(head + i) & (QCAP - 1)] : make_uint4(0, 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
-    if (keep) q[(w + prefix_below(mk)) & (QCAP - 1)] = s;
+    if (keep) reinterpret_cast<uint4*>(q)[(w + prefix_below(mk)) & (QCAP - 1)] = v;
     __builtin_amdgcn_wave_barrier();
     w += __popcll(mk);
     eq_seen += __popcll(meq);
@@ -276,74 +310,86 @@ __device__ __forceinline__ bool visited_check(KState* vis, uint32_t& vcount, con
   return false;
 }
 
-// One start window, explored by one wavefront.
-template <uint32_t VCAP, uint32_t QCAP>
-__device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, EmitList& EL,
-                           uint64_t start, uint64_t& popped, unsigned& err) {
+// Emission (search.rs:659-737) for one accepted state; lanes spread over the node's output list.
+// Called in FIFO pop order, so the per-window best list keeps the reference's first-found ties.
+__device__ void emit_state(const SearchParams& P, EmitList& EL, uint32_t me_rel, float pen, uint32_t packed,
+                           uint32_t out_begin, uint32_t out_end, unsigned& err) {
+  const uint32_t lane = lane_id();
+  const bool fast = P.mef != 255u;
+  const uint32_t edits = edits_of(packed);
+  const uint32_t ins = packed & 0xFFu, del = (packed >> 8) & 0xFFu, sub = (packed >> 16) & 0xFFu, swp = packed >> 24;
+  for (uint32_t base = out_begin; base < out_end; base += 64) {
+    const uint32_t i = base + lane;
+    bool ok = i < out_end;
+    uint32_t p = 0;
+    float sim = 0.f;
+    if (ok) {
+      p = P.out_pat[i];
+      const DevPattern pt = P.pats[p];
+      if (fast) {
+        ok = edits <= P.mef;
+      } else {  // within_limits (:151-169)
+        const Lim m = pick_limits(P, pt.has_limits ? (int32_t)p : -1);
+        ok = m.has ? (lim_le(m.l.edits, edits) && lim_le(m.l.ins, ins) && lim_le(m.l.del, del) &&
+                      lim_le(m.l.sub, sub) && lim_le(m.l.swp, swp))
+                   : (edits == 0);
+      }
+      if (ok) {
+        const float total = pt.glen;
+        sim = __fmul_rn(__fdiv_rn(__fsub_rn(total, pen), total), pt.weight);  // :696-699
+        ok = !(sim < P.thr);                                                   // :701
+      }
+    }
+    uint64_t m = __ballot(ok);
+    while (m) {
+      const int l = first_lane(m);
+      m &= m - 1;
+      emit_update(EL, me_rel, shfl_u32(p, l), shfl_f32(sim, l), packed, err);
+    }
+  }
+}
+
+// Edge-parallel expansion of ONE accepted state (dedup and ceiling passed, emission done): the
+// exact / substitution / swap / insertion / deletion pushes with the 64 lanes spread over the
+// node's edges (search.rs:742-1089). Used for nodes with more than 64 edges.
+template <uint32_t QCAP>
+__device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, uint32_t head, uint32_t& tail,
+                            const KState& st, const DevNode& nd, uint64_t start, unsigned& err) {
   const uint32_t lane = lane_id();
   const bool fast = P.mef != 255u;
   const uint64_t n = S.n;
-  for (uint32_t i = lane; i < VCAP; i += 64) vis[i].node = EMPTY;
-  uint32_t vcount = 0;
-  EL.n = 0;
-  uint32_t head = 0, tail = 1;
-  if (lane == 0) q[0] = KState{0u, 0u, 0.0f, 0u};
-  __builtin_amdgcn_wave_barrier();
-
-  while (head < tail) {
-    if (P.beam && tail - head > 2u * P.beam) beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
-    const KState st = q[head & (QCAP - 1)];
-    head += 1;
-    popped += 1;
-    if (visited_check<VCAP>(vis, vcount, st, P.beam != 0, err)) continue;  // :608-628
-
-    const DevNode nd = P.nodes[st.node];
-    const float pen = st.pen;
-    if (pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr))) continue;  // :638-642
-    const float remaining = __fsub_rn(P.max_penalties, pen);                     // :648
-    const uint32_t packed = st.packed;
-    const uint32_t edits = edits_of(packed);
-    const uint32_t j_rel = st.jm & 0xFFFFu, me_rel = st.jm >> 16;
-    const uint64_t j = start + j_rel;
-    const int32_t nlim = P.has_pattern_limits ? node_limits(P, st.node) : -1;  // :653-657
-
-    // ---- emission (:659-737)
-    if (nd.out_begin != nd.out_end) {
-      const uint32_t ins = packed & 0xFFu, del = (packed >> 8) & 0xFFu, sub = (packed >> 16) & 0xFFu,
-                     swp = packed >> 24;
-      for (uint32_t base = nd.out_begin; base < nd.out_end; base += 64) {
-        const uint32_t i = base + lane;
-        bool ok = i < nd.out_end;
-        uint32_t p = 0;
-        float sim = 0.f;
-        if (ok) {
-          p = P.out_pat[i];
-          const DevPattern pt = P.pats[p];
-          if (fast) {
-            ok = edits <= P.mef;
-          } else {  // within_limits (:151-169)
-            const Lim m = pick_limits(P, pt.has_limits ? (int32_t)p : -1);
-            ok = m.has ? (lim_le(m.l.edits, edits) && lim_le(m.l.ins, ins) && lim_le(m.l.del, del) &&
-                          lim_le(m.l.sub, sub) && lim_le(m.l.swp, swp))
-                       : (edits == 0);
-          }
-          if (ok) {
-            const float total = pt.glen;
-            sim = __fmul_rn(__fdiv_rn(__fsub_rn(total, pen), total), pt.weight);  // :696-699
-            ok = !(sim < P.thr);                                                   // :701
-          }
-        }
-        uint64_t m = __ballot(ok);
-        while (m) {
-          const int l = first_lane(m);
-          m &= m - 1;
-          emit_update(EL, me_rel, shfl_u32(p, l), shfl_f32(sim, l), packed, err);
-        }
-      }
-    }
-
+  const float pen = st.pen;
+  const float remaining = __fsub_rn(P.max_penalties, pen);  // :648
+  const uint32_t packed = st.packed;
+  const uint32_t edits = edits_of(packed);
+  const uint32_t j_rel = st.jm & 0xFFFFu, me_rel = st.jm >> 16;
+  const uint64_t j = start + j_rel;
+  const int32_t nlim = P.has_pattern_limits ? node_limits(P, st.node) : -1;  // :653-657
     const bool is_last_edit = fast && edits + 1u >= P.mef;  // :742
     const uint32_t cur_ch = j < n ? text_char(P, S, j, err) : 0u;
+    // Nodes with <= 64 edges (all but the top trie levels) are handled from one register-resident
+    // chunk: lane l holds edge l and, at the last edit level, its child's single-byte edge map.
+    const uint32_t deg = nd.edge_end - nd.edge_begin;
+    const bool small = deg <= 64u;
+    uint32_t e_ch = 0, e_next = 0;
+    uint4 e_sb = make_uint4(0, 0, 0, 0);
+    const bool e_valid = small && lane < deg;
+    if (e_valid) {
+      const DevEdge ed = P.edges[nd.edge_begin + lane];
+      e_ch = ed.ch;
+      e_next = ed.next;
+      if (is_last_edit) e_sb = P.sb_bits[e_next & EDGE_NEXT_MASK];
+    }
+    auto sb_bit = [](uint4 m, uint32_t ch) -> bool {  // branch-free word select (no stack indexing)
+      const uint32_t lo = (ch & 32u) ? m.y : m.x;
+      const uint32_t hi = (ch & 32u) ? m.w : m.z;
+      const uint32_t w = (ch & 64u) ? hi : lo;
+      return ch < 128u && ((w >> (ch & 31u)) & 1u);
+    };
+    auto small_goto = [&](uint32_t ch) -> int64_t {
+      const uint64_t m = __ballot(e_valid && e_ch == ch);
+      return m ? (int64_t)(shfl_u32(e_next, first_lane(m)) & EDGE_NEXT_MASK) : -1;
+    };
     if (j < n) {
       bool have_next = false;
       uint32_t next_ch = 0;
@@ -352,7 +398,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
         next_ch = text_char(P, S, j + 1, err);
       }
       // exact transition (:766-798); matched_start stays `start` for every state
-      const int64_t exact_next = goto_char(P, nd.edge_begin, nd.edge_end, cur_ch);
+      const int64_t exact_next = small ? small_goto(cur_ch) : goto_char(P, nd.edge_begin, nd.edge_end, cur_ch);
       const uint32_t jm1 = (j_rel + 1u) | ((j_rel + 1u) << 16);
       push_lanes<QCAP>(q, head, tail, lane == 0 && exact_next >= 0,
                        KState{(uint32_t)exact_next, jm1, pen, packed}, err);
@@ -369,28 +415,39 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
       if (subst_ok) {
         for (uint32_t base = nd.edge_begin; base < nd.edge_end; base += 64) {
           const uint32_t i = base + lane;
-          bool keep = i < nd.edge_end;
-          KState s{};
+          bool keep;
+          uint32_t ch, nx;
+          if (small) {
+            keep = e_valid;
+            ch = e_ch;
+            nx = e_next;
+          } else {
+            keep = i < nd.edge_end;
+            const DevEdge ed = keep ? P.edges[i] : DevEdge{0, 0};
+            ch = ed.ch;
+            nx = ed.next;
+          }
+          KState st2{};
           if (keep) {
-            const DevEdge ed = P.edges[i];
-            const uint32_t child = ed.next & EDGE_NEXT_MASK;
+            const uint32_t child = nx & EDGE_NEXT_MASK;
             keep = !(exact_next >= 0 && child == (uint32_t)exact_next);
-            const float sim = similarity(P, ed.ch, cur_ch);
+            const float sim = similarity(P, ch, cur_ch);
             keep = keep && !(sim < P.min_sym);
             const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
             keep = keep && !(penalty > remaining);
             if (keep && is_last_edit)  // dead-end filter (:839-847)
-              keep = (ed.next & EDGE_CHILD_OUTPUT) || (have_next && sb_has(P, child, next_ch));
-            s = KState{child, jm1, __fadd_rn(pen, penalty), packed + 0x10000u};
+              keep = (nx & EDGE_CHILD_OUTPUT) ||
+                     (have_next && (small ? sb_bit(e_sb, next_ch) : sb_has(P, child, next_ch)));
+            st2 = KState{child, jm1, __fadd_rn(pen, penalty), packed + 0x10000u};
           }
-          push_lanes<QCAP>(q, head, tail, keep, s, err);
+          push_lanes<QCAP>(q, head, tail, keep, st2, err);
         }
       }
 
       // swap (:935-989)
       if (j + 1 < n && P.p_swp <= remaining && (!fast || edits < P.mef)) {
         const uint32_t nch = have_next ? next_ch : text_char(P, S, j + 1, err);
-        const int64_t x = goto_char(P, nd.edge_begin, nd.edge_end, nch);
+        const int64_t x = small ? small_goto(nch) : goto_char(P, nd.edge_begin, nd.edge_end, nch);
         if (x >= 0) {
           const DevNode nx = P.nodes[(uint32_t)x];
           const int64_t node2 = goto_char(P, nx.edge_begin, nx.edge_end, cur_ch);
@@ -436,20 +493,322 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
         const float npen = __fadd_rn(pen, P.p_del);
         for (uint32_t base = nd.edge_begin; base < nd.edge_end; base += 64) {
           const uint32_t i = base + lane;
-          bool keep = i < nd.edge_end;
-          uint32_t child = 0;
-          if (keep) {
-            const DevEdge ed = P.edges[i];
-            child = ed.next & EDGE_NEXT_MASK;
-            if (is_last_edit)  // dead-end filter (:1057-1063)
-              keep = (ed.next & EDGE_CHILD_OUTPUT) || (have_cur && sb_has(P, child, cur_ch));
+          bool keep;
+          uint32_t nx;
+          if (small) {
+            keep = e_valid;
+            nx = e_next;
+          } else {
+            keep = i < nd.edge_end;
+            nx = keep ? P.edges[i].next : 0u;
           }
+          const uint32_t child = nx & EDGE_NEXT_MASK;
+          if (keep && is_last_edit)  // dead-end filter (:1057-1063)
+            keep = (nx & EDGE_CHILD_OUTPUT) ||
+                   (have_cur && (small ? sb_bit(e_sb, cur_ch) : sb_has(P, child, cur_ch)));
           push_lanes<QCAP>(q, head, tail, keep, KState{child, st.jm, npen, packed + 0x100u}, err);
         }
       }
     }
+}
+
+// One state per lane: the expansion decisions of a <=64-edge node, computed lane-serially into
+// register bitmasks (bit e of msub/mdel = edge e pushes a substitution/deletion successor).
+struct LaneExp {
+  int64_t exact;     // exact successor node or -1
+  int64_t swap;      // swap successor node or -1
+  bool ins;          // insertion successor
+  uint64_t msub, mdel;
+  uint32_t count;    // pushes of this state
+};
+
+__device__ __forceinline__ bool sb_word_bit(uint4 m, uint32_t ch) {  // branch-free (no stack indexing)
+  const uint32_t lo = (ch & 32u) ? m.y : m.x;
+  const uint32_t hi = (ch & 32u) ? m.w : m.z;
+  const uint32_t w = (ch & 64u) ? hi : lo;
+  return ch < 128u && ((w >> (ch & 31u)) & 1u);
+}
+
+__device__ LaneExp lane_expand(const SearchParams& P, const SegDesc& S, const KState& st, const DevNode& nd,
+                               uint64_t start, unsigned& err) {
+  LaneExp x{-1, -1, false, 0ull, 0ull, 0u};
+  const bool fast = P.mef != 255u;
+  const uint64_t n = S.n;
+  const float pen = st.pen;
+  const float remaining = __fsub_rn(P.max_penalties, pen);  // :648
+  const uint32_t packed = st.packed;
+  const uint32_t edits = edits_of(packed);
+  const uint32_t j_rel = st.jm & 0xFFFFu, me_rel = st.jm >> 16;
+  const uint64_t j = start + j_rel;
+  const int32_t nlim = P.has_pattern_limits ? node_limits(P, st.node) : -1;
+  const bool is_last_edit = fast && edits + 1u >= P.mef;  // :742
+  const bool in_text = j < n;
+  const uint32_t cur_ch = in_text ? text_char(P, S, j, err) : 0u;
+  bool have_next = false;
+  uint32_t next_ch = 0;
+  if (in_text && is_last_edit && (!fast || edits < P.mef) && j + 1 < n) {  // :758-765
+    have_next = true;
+    next_ch = text_char(P, S, j + 1, err);
+  }
+  bool subst_ok = false, swap_ok = false, ins_ok = false, del_ok = false;
+  uint32_t nch = 0;
+  if (in_text) {
+    if (fast) {
+      subst_ok = edits < P.mef;
+    } else {  // within_limits_subst (:134-146)
+      const Lim m = pick_limits(P, nlim);
+      subst_ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.sub, (packed >> 16) & 0xFFu))
+                       : (edits == 0 && ((packed >> 16) & 0xFFu) == 0);
+    }
+    swap_ok = j + 1 < n && P.p_swp <= remaining && (!fast || edits < P.mef);  // :935-937
+    if (swap_ok) nch = have_next ? next_ch : text_char(P, S, j + 1, err);
+    if ((me_rel != 0u || j_rel != 0u) && P.p_ins <= remaining) {  // :994-1007
+      if (fast) {
+        ins_ok = edits < P.mef;
+      } else {
+        const Lim m = pick_limits(P, nlim);
+        ins_ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.ins, packed & 0xFFu)) : false;
+      }
+      if (ins_ok && is_last_edit && nd.out_begin == nd.out_end) {
+        const uint4 own = P.sb_bits[st.node];
+        ins_ok = have_next && sb_word_bit(own, next_ch);
+      }
+    }
+  }
+  if (P.p_del <= remaining) {  // :1035-1045
+    if (fast) {
+      del_ok = edits < P.mef;
+    } else {
+      const Lim m = pick_limits(P, nlim);
+      del_ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.del, (packed >> 8) & 0xFFu)) : false;
+    }
+  }
+  const bool have_cur = is_last_edit && in_text;
+  bool found_exact = false, found_x = false;
+  int64_t xnode = -1;
+  const uint32_t deg = nd.edge_end - nd.edge_begin;
+  for (uint32_t e = 0; e < deg; ++e) {
+    const DevEdge ed = P.edges[nd.edge_begin + e];
+    const uint32_t child = ed.next & EDGE_NEXT_MASK;
+    const bool child_out = (ed.next & EDGE_CHILD_OUTPUT) != 0;
+    uint4 csb = make_uint4(0, 0, 0, 0);
+    if (is_last_edit && !child_out && (subst_ok || del_ok)) csb = P.sb_bits[child];
+    bool is_exact = false;
+    if (in_text) {
+      if (!found_exact && ed.ch == cur_ch) {  // first edge with this first char (structs.rs:512-519)
+        found_exact = true;
+        is_exact = true;
+        x.exact = child;
+      }
+      if (swap_ok && !found_x && ed.ch == nch) {
+        found_x = true;
+        xnode = child;
+      }
+      if (subst_ok && !is_exact) {  // :814-874 (the exact target's edge is the only one skipped)
+        const float sim = similarity(P, ed.ch, cur_ch);
+        bool keep = !(sim < P.min_sym);
+        const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
+        keep = keep && !(penalty > remaining);
+        if (keep && is_last_edit) keep = child_out || (have_next && sb_word_bit(csb, next_ch));
+        if (keep) x.msub |= 1ull << e;
+      }
+    }
+    if (del_ok) {  // :1055-1088
+      const bool keep = !is_last_edit || child_out || (have_cur && sb_word_bit(csb, cur_ch));
+      if (keep) x.mdel |= 1ull << e;
+    }
+  }
+  if (found_x) {  // swap: node2 = goto(goto(node, text[j+1]), text[j]) (:945-961)
+    const DevNode xn = P.nodes[(uint32_t)xnode];
+    for (uint32_t e = xn.edge_begin; e < xn.edge_end; ++e) {
+      const DevEdge ed = P.edges[e];
+      if (ed.ch == cur_ch) {
+        x.swap = ed.next & EDGE_NEXT_MASK;
+        break;
+      }
+    }
+    if (x.swap >= 0 && !fast) {  // within_limits_swap_ahead with node2's limits (:962-967)
+      const Lim m = pick_limits(P, node_limits(P, (uint32_t)x.swap));
+      if (!(m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.swp, packed >> 24)) : false)) x.swap = -1;
+    }
+  }
+  x.ins = ins_ok;
+  x.count = (x.exact >= 0 ? 1u : 0u) + (uint32_t)__popcll(x.msub) + (x.swap >= 0 ? 1u : 0u) + (ins_ok ? 1u : 0u) +
+            (uint32_t)__popcll(x.mdel);
+  return x;
+}
+
+// Write one lane's pushes in the reference's order: exact, substitutions (edge order), swap,
+// insertion, deletions (edge order) (search.rs:787-1088).
+template <uint32_t QCAP>
+__device__ void lane_push(const SearchParams& P, const SegDesc& S, KState* q, uint32_t pos, const KState& st,
+                          const DevNode& nd, const LaneExp& x, uint64_t start, unsigned& err) {
+  const float pen = st.pen;
+  const uint32_t packed = st.packed;
+  const uint32_t j_rel = st.jm & 0xFFFFu;
+  const uint32_t jm1 = (j_rel + 1u) | ((j_rel + 1u) << 16);
+  if (x.exact >= 0) q[(pos++) & (QCAP - 1)] = KState{(uint32_t)x.exact, jm1, pen, packed};
+  if (x.msub) {
+    const uint32_t cur_ch = text_char(P, S, start + j_rel, err);
+    uint64_t m = x.msub;
+    while (m) {
+      const uint32_t e = (uint32_t)(__ffsll((unsigned long long)m) - 1);
+      m &= m - 1;
+      const DevEdge ed = P.edges[nd.edge_begin + e];
+      const float sim = similarity(P, ed.ch, cur_ch);
+      const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
+      q[(pos++) & (QCAP - 1)] = KState{ed.next & EDGE_NEXT_MASK, jm1, __fadd_rn(pen, penalty), packed + 0x10000u};
+    }
+  }
+  if (x.swap >= 0) {
+    const uint32_t jm2 = (j_rel + 2u) | ((j_rel + 2u) << 16);
+    q[(pos++) & (QCAP - 1)] = KState{(uint32_t)x.swap, jm2, __fadd_rn(pen, P.p_swp), packed + 0x1000000u};
+  }
+  if (x.ins) {
+    const uint32_t jmi = (j_rel + 1u) | ((st.jm >> 16) << 16);
+    q[(pos++) & (QCAP - 1)] = KState{st.node, jmi, __fadd_rn(pen, P.p_ins), packed + 1u};
+  }
+  if (x.mdel) {
+    const float npen = __fadd_rn(pen, P.p_del);
+    uint64_t m = x.mdel;
+    while (m) {
+      const uint32_t e = (uint32_t)(__ffsll((unsigned long long)m) - 1);
+      m &= m - 1;
+      const uint32_t child = P.edges[nd.edge_begin + e].next & EDGE_NEXT_MASK;
+      q[(pos++) & (QCAP - 1)] = KState{child, st.jm, npen, packed + 0x100u};
+    }
+  }
+}
+
+// Wave-wide inclusive prefix sum (DPP row shifts + row broadcasts).
+__device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
+  int x = (int)v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return (uint32_t)x;
+}
+
+// Read-only dedup lookup (per lane, linear probing). found/stored describe the table entry.
+template <uint32_t VCAP>
+__device__ __forceinline__ void vis_lookup(const KState* vis, const KState& s, bool& found, uint32_t& stored_bits) {
+  uint32_t h = vis_hash(s) & (VCAP - 1);
+  found = false;
+  stored_bits = 0;
+  for (uint32_t it = 0; it < VCAP; ++it) {
+    const uint4 e = reinterpret_cast<const uint4*>(vis)[h];
+    if (e.x == EMPTY) return;
+    if (e.x == s.node && e.y == s.jm && e.w == s.packed) {
+      found = true;
+      stored_bits = e.z;
+      return;
+    }
+    h = (h + 1) & (VCAP - 1);
+  }
+}
+
+// One start window, explored by one wavefront. States are popped in the reference's FIFO order in
+// batches of up to 64 (one state per lane); a batch is cut exactly where the reference's sequential
+// semantics would diverge: before the first in-batch dedup conflict, before the first pop at which
+// the beam would trigger, and before the first >64-edge node (expanded alone, edge-parallel).
+template <uint32_t VCAP, uint32_t QCAP>
+__device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, EmitList& EL,
+                           uint64_t start, uint64_t& popped, unsigned& err) {
+  const uint32_t lane = lane_id();
+  for (uint32_t i = lane; i < VCAP; i += 64) vis[i].node = EMPTY;
+  uint32_t vcount = 0;
+  EL.n = 0;
+  uint32_t head = 0, tail = 1;
+  if (lane == 0) q[0] = KState{0u, 0u, 0.0f, 0u};
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t beam2 = 2u * P.beam;
+
+  while (head < tail) {
+    if (P.beam && tail - head > beam2) beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
+    const uint32_t B = min(tail - head, 64u);
+    const bool in_b = lane < B;
+    KState st{EMPTY, 0u, 0.0f, 0u};
+    if (in_b) st = q[(head + lane) & (QCAP - 1)];
+    // ---- phase A: dedup (read-only), node ceiling, width
+    bool found = false;
+    uint32_t stored_bits = 0;
+    if (in_b) vis_lookup<VCAP>(vis, st, found, stored_bits);
+    const bool skip = in_b && found && __uint_as_float(stored_bits) <= st.pen;  // :620
+    DevNode nd{};
+    bool alive = false;
+    if (in_b && !skip) {
+      nd = P.nodes[st.node];
+      alive = !(st.pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr)));  // :638-642
+    }
+    const bool wide = alive && (nd.edge_end - nd.edge_begin) > 64u;
+    const uint64_t mwide = __ballot(wide);
+    if (mwide & 1ull) {  // first state alone, edge-parallel
+      const KState s0 = q[head & (QCAP - 1)];
+      head += 1;
+      popped += 1;
+      if (visited_check<VCAP>(vis, vcount, s0, P.beam != 0, err)) continue;
+      const DevNode n0 = P.nodes[s0.node];
+      if (n0.out_begin != n0.out_end) emit_state(P, EL, s0.jm >> 16, s0.pen, s0.packed, n0.out_begin, n0.out_end, err);
+      expand_wide<QCAP>(P, S, q, head, tail, s0, n0, start, err);
+      if (any_err(err)) break;
+      continue;
+    }
+    uint32_t Bc = mwide ? (uint32_t)first_lane(mwide) : B;
+    // ---- phase B: per-lane expansion decisions and push counts
+    LaneExp x{-1, -1, false, 0ull, 0ull, 0u};
+    if (alive && lane < Bc) x = lane_expand(P, S, st, nd, start, err);
+    const uint32_t cnt = (lane < Bc) ? x.count : 0u;
+    const uint32_t incl = wave_inclusive_sum(cnt);
+    const uint32_t excl = incl - cnt;
+    // cut: before pop k (k >= 1) the reference checks pending = P0 - k + S_k (:579-580); the queue
+    // ring must also hold everything pushed by the committed states.
+    const uint32_t P0 = tail - head;
+    const bool trig = lane >= 1 && lane < Bc && P.beam && (P0 - lane + excl > beam2);
+    const bool ovf = lane < Bc && (P0 - lane - 1 + incl > QCAP);
+    const uint64_t mcut = __ballot(trig) | __ballot(ovf);
+    if (mcut) Bc = min(Bc, (uint32_t)first_lane(mcut));
+    if (Bc == 0) {
+      err |= ERR_QUEUE;
+      break;
+    }
+    // ---- phase C: in-order dedup commit; cut at the first in-batch conflict
+    for (uint32_t t = 0; t < Bc; ++t) {
+      KState kt;
+      kt.node = shfl_u32(st.node, t);
+      kt.jm = shfl_u32(st.jm, t);
+      kt.pen = shfl_f32(st.pen, t);
+      kt.packed = shfl_u32(st.packed, t);
+      const bool f_t = __ballot(found) >> t & 1ull;
+      const uint32_t sb_t = shfl_u32(stored_bits, t);
+      const bool skip_t = __ballot(skip) >> t & 1ull;
+      if (t > 0) {  // did an earlier state of this batch write this key?
+        bool f2;
+        uint32_t sb2;
+        vis_lookup<VCAP>(vis, kt, f2, sb2);
+        if (f2 != f_t || (f2 && sb2 != sb_t)) {
+          Bc = t;
+          break;
+        }
+      }
+      if (!skip_t) visited_check<VCAP>(vis, vcount, kt, P.beam != 0, err);  // inserts / lowers the entry
+    }
+    // ---- phase D: emissions (FIFO order), then pushes at tail + exclusive prefix
+    uint64_t mem = __ballot(alive && lane < Bc && nd.out_begin != nd.out_end);
+    while (mem) {
+      const int l = first_lane(mem);
+      mem &= mem - 1;
+      emit_state(P, EL, shfl_u32(st.jm, l) >> 16, shfl_f32(st.pen, l), shfl_u32(st.packed, l),
+                 shfl_u32(nd.out_begin, l), shfl_u32(nd.out_end, l), err);
+    }
+    if (alive && lane < Bc && x.count) lane_push<QCAP>(P, S, q, tail + excl, st, nd, x, start, err);
     __builtin_amdgcn_wave_barrier();
-    if (wave_or(err) & (ERR_QUEUE | ERR_VISITED | ERR_EMIT | ERR_HALO)) break;
+    tail += shfl_u32(incl, Bc - 1);
+    head += Bc;
+    popped += Bc;
+    if (any_err(err)) break;
   }
 
   // flush this window's best map (search.rs:1111-1118)
@@ -457,8 +816,9 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
   if (EL.n && !(err & ERR_EMIT)) {
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(P.counters, (unsigned long long)EL.n);
-    base = (unsigned long long)__shfl((long long)base, 0, 64);
+    base = shfl_u64(base, 0);
     const uint64_t sb = S.byte_base + local_byte(P, S, start);
+    const uint64_t n = S.n;
     for (uint32_t i = lane; i < EL.n; i += 64) {
       if (base + i >= P.out_cap) break;
       const uint4 ent = EL.buf[i];
@@ -528,14 +888,14 @@ __global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
         const int l = first_lane(m);
         m &= m - 1;
         const uint32_t seg = shfl_u32(kl, l);
-        const uint64_t st = (uint64_t)__shfl((long long)start, l, 64);
+        const uint64_t st = shfl_u64(start, l);
         const SegDesc S = P.segs[seg];
         run_window<VCAP, QCAP>(P, S, s_vis, s_q, EL, st, popped, err);
-        if (wave_or(err)) break;
+        if (any_err(err)) break;
       }
-      if (wave_or(err)) break;
+      if (any_err(err)) break;
     }
-    if (wave_or(err)) break;
+    if (any_err(err)) break;
   }
   if (lane == 0) atomicAdd(P.counters + 1, (unsigned long long)popped);
   const unsigned all = wave_or(err);

@@ -408,6 +408,8 @@ struct Searcher {
   };
 
   uint64_t states_popped = 0, states_pushed = 0;
+  uint64_t* deg_hist = nullptr;  // optional diagnostics: [0..64] degree of expanded states, [65..] per-edits
+  uint64_t* batch_hist = nullptr;
 
   // `text_chars`, grapheme byte offsets (nullptr = identity), haystack byte length.
   uint32_t w_begin = 0, w_end = 0xFFFFFFFFu;  // start-window range (sharding diagnostics)
@@ -484,6 +486,10 @@ struct Searcher {
         }
         const Node& nd = e.nodes[st.node];
         if (st.pen > nd.prune_len - nd.prune_lw * thr) continue;  // :638-642
+        if (deg_hist) {
+          deg_hist[std::min<size_t>(nd.edges.size(), 64)]++;
+          deg_hist[65 + std::min<uint32_t>(st.edits, 7)]++;
+        }
         const float remaining = max_penalties - st.pen;            // :648
         const Limits* nlim = e.has_pattern_limits ? node_limits(st.node) : nullptr;
         const uint8_t edits = st.edits;
@@ -625,6 +631,8 @@ void bitap_windows(const std::vector<uint64_t>& mask, size_t m, size_t k, const 
   }
 }
 
+uint64_t g_deg_hist[80];  // diagnostics only (degree / edits histogram of expanded states)
+
 // Staging for a (sub)haystack: ASCII fast path or caller-provided global graphemes.
 struct Staged {
   std::vector<uint32_t> tc;
@@ -672,6 +680,7 @@ void search_raw_slice(const Engine& e, const Text& t, uint64_t b0, uint64_t b1, 
   }
   if (s.tc.size() > 0xFFFFFFFFull) { out.clear(); return; }
   Searcher S(e);
+  S.deg_hist = g_deg_hist;
   S.w_begin = w_begin;
   S.w_end = w_end;
   S.run(s.tc.data(), s.off.empty() ? nullptr : s.off.data(), (uint32_t)s.tc.size(), s.len, thr, out);
@@ -752,6 +761,7 @@ void* orc_build(const orc_config* cfg, uint64_t n_patterns, const uint32_t* glen
 }
 
 void orc_free(void* h) { delete static_cast<Engine*>(h); }
+uint64_t* orc_deg_hist() { return g_deg_hist; }
 
 uint64_t orc_num_nodes(void* h) { return static_cast<Engine*>(h)->nodes.size(); }
 uint32_t orc_max_edits_fast(void* h) { return static_cast<Engine*>(h)->max_edits_fast; }
