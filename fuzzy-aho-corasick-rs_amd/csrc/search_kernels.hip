@@ -530,7 +530,7 @@ __device__ __forceinline__ bool sb_word_bit(uint4 m, uint32_t ch) {  // branch-f
 }
 
 __device__ LaneExp lane_expand(const SearchParams& P, const SegDesc& S, const KState& st, const DevNode& nd,
-                               uint64_t start, unsigned& err) {
+                               uint64_t start, uint32_t maxdeg, unsigned& err) {
   LaneExp x{-1, -1, false, 0ull, 0ull, 0u};
   const bool fast = P.mef != 255u;
   const uint64_t n = S.n;
@@ -587,37 +587,47 @@ __device__ LaneExp lane_expand(const SearchParams& P, const SegDesc& S, const KS
   bool found_exact = false, found_x = false;
   int64_t xnode = -1;
   const uint32_t deg = nd.edge_end - nd.edge_begin;
-  for (uint32_t e = 0; e < deg; ++e) {
-    const DevEdge ed = P.edges[nd.edge_begin + e];
+  // Edge loop with a wave-uniform trip count (maxdeg, SGPR) and predicated bodies: no per-lane
+  // loop control or exec-mask branching; lanes past their own degree load edge 0 and discard it.
+  const bool sub_on = in_text && subst_ok, ex_on = in_text;
+  const bool need_csb = is_last_edit && (subst_ok || del_ok);
+  uint32_t sub_lo = 0, sub_hi = 0, del_lo = 0, del_hi = 0;
+#pragma unroll 2
+  for (uint32_t e = 0; e < maxdeg; ++e) {
+    const bool valid = e < deg;
+    const DevEdge ed = P.edges[valid ? nd.edge_begin + e : 0u];
     const uint32_t child = ed.next & EDGE_NEXT_MASK;
     const bool child_out = (ed.next & EDGE_CHILD_OUTPUT) != 0;
-    uint4 csb = make_uint4(0, 0, 0, 0);
-    if (is_last_edit && !child_out && (subst_ok || del_ok)) csb = P.sb_bits[child];
-    bool is_exact = false;
-    if (in_text) {
-      if (!found_exact && ed.ch == cur_ch) {  // first edge with this first char (structs.rs:512-519)
-        found_exact = true;
-        is_exact = true;
-        x.exact = child;
-      }
-      if (swap_ok && !found_x && ed.ch == nch) {
-        found_x = true;
-        xnode = child;
-      }
-      if (subst_ok && !is_exact) {  // :814-874 (the exact target's edge is the only one skipped)
-        const float sim = similarity(P, ed.ch, cur_ch);
-        bool keep = !(sim < P.min_sym);
-        const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
-        keep = keep && !(penalty > remaining);
-        if (keep && is_last_edit) keep = child_out || (have_next && sb_word_bit(csb, next_ch));
-        if (keep) x.msub |= 1ull << e;
-      }
-    }
-    if (del_ok) {  // :1055-1088
-      const bool keep = !is_last_edit || child_out || (have_cur && sb_word_bit(csb, cur_ch));
-      if (keep) x.mdel |= 1ull << e;
+    const uint4 csb = P.sb_bits[(valid && need_csb && !child_out) ? child : 0u];
+    // first edge with this first char (structs.rs:512-519)
+    const bool is_exact = valid && ex_on && !found_exact && ed.ch == cur_ch;
+    found_exact = found_exact || is_exact;
+    x.exact = is_exact ? (int64_t)child : x.exact;
+    const bool is_x = valid && swap_ok && !found_x && ed.ch == nch;
+    found_x = found_x || is_x;
+    xnode = is_x ? (int64_t)child : xnode;
+    // substitution (:814-874; the exact target's edge is the only one skipped)
+    const bool asc = ed.ch < 128u && cur_ch < 128u;
+    const float tv = P.sim_ascii[asc ? ed.ch * 128u + cur_ch : 0u];
+    float sim = ed.ch == cur_ch ? 1.0f : (asc ? tv : 0.0f);
+    if (P.n_sim != 0 && !asc && ed.ch != cur_ch) sim = similarity(P, ed.ch, cur_ch);
+    const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
+    const bool sb_next = child_out || (have_next && sb_word_bit(csb, next_ch));
+    const bool sb_cur = child_out || (have_cur && sb_word_bit(csb, cur_ch));
+    const bool keep_sub = valid && sub_on && !is_exact && !(sim < P.min_sym) && !(penalty > remaining) &&
+                          (!is_last_edit || sb_next);
+    const bool keep_del = valid && del_ok && (!is_last_edit || sb_cur);  // :1055-1088
+    const uint32_t bit = 1u << (e & 31u);
+    if (e < 32u) {  // wave-uniform
+      sub_lo |= keep_sub ? bit : 0u;
+      del_lo |= keep_del ? bit : 0u;
+    } else {
+      sub_hi |= keep_sub ? bit : 0u;
+      del_hi |= keep_del ? bit : 0u;
     }
   }
+  x.msub = ((uint64_t)sub_hi << 32) | sub_lo;
+  x.mdel = ((uint64_t)del_hi << 32) | del_lo;
   if (found_x) {  // swap: node2 = goto(goto(node, text[j+1]), text[j]) (:945-961)
     const DevNode xn = P.nodes[(uint32_t)xnode];
     for (uint32_t e = xn.edge_begin; e < xn.edge_end; ++e) {
@@ -694,16 +704,22 @@ __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
 
 // Read-only dedup lookup (per lane, linear probing). found/stored describe the table entry.
 template <uint32_t VCAP>
-__device__ __forceinline__ void vis_lookup(const KState* vis, const KState& s, bool& found, uint32_t& stored_bits) {
+__device__ __forceinline__ void vis_lookup(const KState* vis, const KState& s, bool& found, uint32_t& stored_bits,
+                                           uint32_t& slot) {
   uint32_t h = vis_hash(s) & (VCAP - 1);
   found = false;
   stored_bits = 0;
+  slot = EMPTY;
   for (uint32_t it = 0; it < VCAP; ++it) {
     const uint4 e = reinterpret_cast<const uint4*>(vis)[h];
-    if (e.x == EMPTY) return;
+    if (e.x == EMPTY) {
+      slot = h;
+      return;
+    }
     if (e.x == s.node && e.y == s.jm && e.w == s.packed) {
       found = true;
       stored_bits = e.z;
+      slot = h;
       return;
     }
     h = (h + 1) & (VCAP - 1);
@@ -715,8 +731,8 @@ __device__ __forceinline__ void vis_lookup(const KState* vis, const KState& s, b
 // semantics would diverge: before the first in-batch dedup conflict, before the first pop at which
 // the beam would trigger, and before the first >64-edge node (expanded alone, edge-parallel).
 template <uint32_t VCAP, uint32_t QCAP>
-__device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, EmitList& EL,
-                           uint64_t start, uint64_t& popped, unsigned& err) {
+__device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint8_t* claim,
+                           EmitList& EL, uint64_t start, uint64_t& popped, unsigned& err) {
   const uint32_t lane = lane_id();
   for (uint32_t i = lane; i < VCAP; i += 64) vis[i].node = EMPTY;
   uint32_t vcount = 0;
@@ -734,8 +750,8 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     if (in_b) st = q[(head + lane) & (QCAP - 1)];
     // ---- phase A: dedup (read-only), node ceiling, width
     bool found = false;
-    uint32_t stored_bits = 0;
-    if (in_b) vis_lookup<VCAP>(vis, st, found, stored_bits);
+    uint32_t stored_bits = 0, vslot = EMPTY;
+    if (in_b) vis_lookup<VCAP>(vis, st, found, stored_bits, vslot);
     const bool skip = in_b && found && __uint_as_float(stored_bits) <= st.pen;  // :620
     DevNode nd{};
     bool alive = false;
@@ -759,7 +775,9 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     uint32_t Bc = mwide ? (uint32_t)first_lane(mwide) : B;
     // ---- phase B: per-lane expansion decisions and push counts
     LaneExp x{-1, -1, false, 0ull, 0ull, 0u};
-    if (alive && lane < Bc) x = lane_expand(P, S, st, nd, start, err);
+    const bool act = alive && lane < Bc;
+    const uint32_t maxdeg = ~wave_min_u32(act ? ~(nd.edge_end - nd.edge_begin) : ~0u);  // uniform
+    if (act) x = lane_expand(P, S, st, nd, start, maxdeg, err);
     const uint32_t cnt = (lane < Bc) ? x.count : 0u;
     const uint32_t incl = wave_inclusive_sum(cnt);
     const uint32_t excl = incl - cnt;
@@ -774,26 +792,47 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
       err |= ERR_QUEUE;
       break;
     }
-    // ---- phase C: in-order dedup commit; cut at the first in-batch conflict
-    for (uint32_t t = 0; t < Bc; ++t) {
-      KState kt;
-      kt.node = shfl_u32(st.node, t);
-      kt.jm = shfl_u32(st.jm, t);
-      kt.pen = shfl_f32(st.pen, t);
-      kt.packed = shfl_u32(st.packed, t);
-      const bool f_t = __ballot(found) >> t & 1ull;
-      const uint32_t sb_t = shfl_u32(stored_bits, t);
-      const bool skip_t = __ballot(skip) >> t & 1ull;
-      if (t > 0) {  // did an earlier state of this batch write this key?
-        bool f2;
-        uint32_t sb2;
-        vis_lookup<VCAP>(vis, kt, f2, sb2);
-        if (f2 != f_t || (f2 && sb2 != sb_t)) {
-          Bc = t;
-          break;
+    // ---- phase C: dedup commit. Fast path: every lane claims its table slot (the slot holding its
+    // key, or the empty slot it would insert into); if no two lanes of the batch claim the same slot,
+    // no state of the batch can see another's write and all updates commit in parallel. Otherwise
+    // commit in FIFO order and cut the batch at the first state whose lookup changed.
+    {
+      const bool part = lane < Bc && vslot != EMPTY;
+      if (part) claim[vslot] = (uint8_t)lane;
+      __builtin_amdgcn_wave_barrier();
+      const bool clash = part && claim[vslot] != (uint8_t)lane;
+      const bool ins_new = lane < Bc && !skip && !found && vslot != EMPTY;
+      const uint32_t n_ins = (uint32_t)__popcll(__ballot(ins_new));
+      const bool full = vcount + n_ins >= VCAP - VCAP / 8;
+      if (!__ballot(clash) && !__ballot(lane < Bc && vslot == EMPTY) && !full) {
+        if (lane < Bc && !skip) {
+          if (found) vis[vslot].pen = st.pen;  // lower the stored penalty (:623)
+          else vis[vslot] = st;                // insert (:626)
+        }
+        vcount += n_ins;
+      } else {
+        for (uint32_t t = 0; t < Bc; ++t) {
+          KState kt;
+          kt.node = shfl_u32(st.node, t);
+          kt.jm = shfl_u32(st.jm, t);
+          kt.pen = shfl_f32(st.pen, t);
+          kt.packed = shfl_u32(st.packed, t);
+          const bool f_t = (__ballot(found) >> t) & 1ull;
+          const uint32_t sb_t = shfl_u32(stored_bits, t);
+          const bool skip_t = (__ballot(skip) >> t) & 1ull;
+          if (t > 0) {  // did an earlier state of this batch write this key?
+            bool f2;
+            uint32_t sb2, sl2;
+            vis_lookup<VCAP>(vis, kt, f2, sb2, sl2);
+            if (f2 != f_t || (f2 && sb2 != sb_t)) {
+              Bc = t;
+              break;
+            }
+          }
+          if (!skip_t) visited_check<VCAP>(vis, vcount, kt, P.beam != 0, err);
         }
       }
-      if (!skip_t) visited_check<VCAP>(vis, vcount, kt, P.beam != 0, err);  // inserts / lowers the entry
+      __builtin_amdgcn_wave_barrier();
     }
     // ---- phase D: emissions (FIFO order), then pushes at tail + exclusive prefix
     uint64_t mem = __ballot(alive && lane < Bc && nd.out_begin != nd.out_end);
@@ -865,6 +904,7 @@ template <uint32_t VCAP, uint32_t QCAP>
 __global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
   __shared__ KState s_vis[VCAP];
   __shared__ KState s_q[QCAP];
+  __shared__ uint8_t s_claim[VCAP];
   const uint32_t lane = lane_id();
   EmitList EL{P.ebuf + (size_t)blockIdx.x * P.ecap, P.ecap, 0};
   uint64_t popped = 0;
@@ -890,7 +930,7 @@ __global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
         const uint32_t seg = shfl_u32(kl, l);
         const uint64_t st = shfl_u64(start, l);
         const SegDesc S = P.segs[seg];
-        run_window<VCAP, QCAP>(P, S, s_vis, s_q, EL, st, popped, err);
+        run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, EL, st, popped, err);
         if (any_err(err)) break;
       }
       if (any_err(err)) break;

@@ -474,6 +474,7 @@ struct Searcher {
           if (remaining > bw * 2) beam_select(queue, q_idx, bw);
         }
         State st = queue[q_idx];
+        if (deg_hist) deg_hist[73] = std::max<uint64_t>(deg_hist[73], queue.size() - q_idx);
         ++q_idx;
         ++states_popped;
         Key key{st.node, st.j, st.ms, st.me, st.packed};
@@ -579,6 +580,11 @@ struct Searcher {
         }
       }
       (void)window_first_out;
+      if (deg_hist) {  // diagnostics: per-window maxima (pending queue, distinct visited keys)
+        deg_hist[74] = std::max<uint64_t>(deg_hist[74], visited.size());
+        deg_hist[75] += visited.size();
+        deg_hist[76] += 1;
+      }
       if (e.has_auto_beam && effective_beam == 0) {  // :1096-1103
         states_expanded += queue.size();
         if (states_expanded > e.ab_budget) effective_beam = e.ab_width;
