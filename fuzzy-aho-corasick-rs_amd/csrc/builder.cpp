@@ -216,6 +216,7 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
   e.out_pat.clear();
   e.sb_bits.assign(nn, uint4{0, 0, 0, 0});
   e.max_degree = 0;
+  e.max_degree_nonroot = 0;
   for (size_t i = 0; i < nn; ++i) {
     DevNode& d = e.nodes[i];
     d.edge_begin = (uint32_t)e.edges.size();
@@ -231,6 +232,7 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
     }
     d.edge_end = (uint32_t)e.edges.size();
     e.max_degree = std::max(e.max_degree, d.edge_end - d.edge_begin);
+    if (i) e.max_degree_nonroot = std::max(e.max_degree_nonroot, d.edge_end - d.edge_begin);
     d.out_begin = (uint32_t)e.out_pat.size();
     for (uint32_t p : output[i]) e.out_pat.push_back(p);
     d.out_end = (uint32_t)e.out_pat.size();

@@ -125,10 +125,14 @@ struct SearchParams {
   uint4* ebuf;              // per-wave emission scratch
   fac_match* out;
   uint64_t out_cap;
-  unsigned long long* counters;  // [0] = matches, [1] = states popped, [2] = error flags
+  unsigned long long* counters;  // [0] matches, [1] states popped, [2] error flags, [3] spilled windows
+  // window list mode (re-run of spilled windows) and the spill list of capacity overflows
+  const uint64_t* win_list;  // null: virtual windows 0..total_windows; else list of virtual ids
+  uint64_t* spill;           // virtual ids of windows that overflowed this variant's LDS frontier
+  uint64_t spill_cap;
 };
 
-constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8u, ERR_OUT = 16u;
+constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8u, ERR_OUT = 16u, ERR_SPILL = 32u;
 
 // ---------------------------------------------------------------- engine
 struct Engine {
@@ -155,6 +159,7 @@ struct Engine {
   std::vector<uint64_t> sim_keys;
   std::vector<float> sim_vals;
   uint32_t max_degree = 0;
+  uint32_t max_degree_nonroot = 0;
   uint32_t max_glen = 0;
   uint64_t max_match_graphemes = 0;
   bool window_skip = false;

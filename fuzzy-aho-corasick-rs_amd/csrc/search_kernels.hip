@@ -734,7 +734,8 @@ template <uint32_t VCAP, uint32_t QCAP>
 __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint8_t* claim,
                            EmitList& EL, uint64_t start, uint64_t& popped, unsigned& err) {
   const uint32_t lane = lane_id();
-  for (uint32_t i = lane; i < VCAP; i += 64) vis[i].node = EMPTY;
+  if constexpr (VCAP > 0)
+    for (uint32_t i = lane; i < VCAP; i += 64) vis[i].node = EMPTY;
   uint32_t vcount = 0;
   EL.n = 0;
   uint32_t head = 0, tail = 1;
@@ -751,7 +752,8 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     // ---- phase A: dedup (read-only), node ceiling, width
     bool found = false;
     uint32_t stored_bits = 0, vslot = EMPTY;
-    if (in_b) vis_lookup<VCAP>(vis, st, found, stored_bits, vslot);
+    if constexpr (VCAP > 0)  // VCAP == 0: no dedup (unbeamed only)
+      if (in_b) vis_lookup<VCAP>(vis, st, found, stored_bits, vslot);
     const bool skip = in_b && found && __uint_as_float(stored_bits) <= st.pen;  // :620
     DevNode nd{};
     bool alive = false;
@@ -765,7 +767,8 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
       const KState s0 = q[head & (QCAP - 1)];
       head += 1;
       popped += 1;
-      if (visited_check<VCAP>(vis, vcount, s0, P.beam != 0, err)) continue;
+      if constexpr (VCAP > 0)
+        if (visited_check<VCAP>(vis, vcount, s0, P.beam != 0, err)) continue;
       const DevNode n0 = P.nodes[s0.node];
       if (n0.out_begin != n0.out_end) emit_state(P, EL, s0.jm >> 16, s0.pen, s0.packed, n0.out_begin, n0.out_end, err);
       expand_wide<QCAP>(P, S, q, head, tail, s0, n0, start, err);
@@ -796,7 +799,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     // key, or the empty slot it would insert into); if no two lanes of the batch claim the same slot,
     // no state of the batch can see another's write and all updates commit in parallel. Otherwise
     // commit in FIFO order and cut the batch at the first state whose lookup changed.
-    {
+    if constexpr (VCAP > 0) {
       const bool part = lane < Bc && vslot != EMPTY;
       if (part) claim[vslot] = (uint8_t)lane;
       __builtin_amdgcn_wave_barrier();
@@ -852,7 +855,8 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
 
   // flush this window's best map (search.rs:1111-1118)
   wave_mem_fence();
-  if (EL.n && !(err & ERR_EMIT)) {
+  // a window that overflowed the frontier is spilled whole (re-run on a larger variant): no flush
+  if (EL.n && !(wave_or(err) & (ERR_EMIT | ERR_QUEUE | ERR_VISITED))) {
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(P.counters, (unsigned long long)EL.n);
     base = shfl_u64(base, 0);
@@ -902,9 +906,9 @@ __device__ __forceinline__ uint32_t find_seg(const SearchParams& P, uint64_t v) 
 
 template <uint32_t VCAP, uint32_t QCAP>
 __global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
-  __shared__ KState s_vis[VCAP];
+  __shared__ KState s_vis[VCAP ? VCAP : 1];
   __shared__ KState s_q[QCAP];
-  __shared__ uint8_t s_claim[VCAP];
+  __shared__ uint8_t s_claim[VCAP ? VCAP : 4];
   const uint32_t lane = lane_id();
   EmitList EL{P.ebuf + (size_t)blockIdx.x * P.ecap, P.ecap, 0};
   uint64_t popped = 0;
@@ -916,11 +920,12 @@ __global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
       const uint64_t v = v0 + lane;
       bool active = v < ce;
       uint32_t kl = 0;
-      uint64_t start = 0;
+      uint64_t start = 0, vid = 0;
       if (active) {
-        kl = find_seg(P, v);
+        vid = P.win_list ? P.win_list[v] : v;
+        kl = find_seg(P, vid);
         const SegDesc S = P.segs[kl];
-        start = S.w_begin + (v - P.seg_prefix[kl]);
+        start = S.w_begin + (vid - P.seg_prefix[kl]);
         active = !window_skipped(P, S, start, err);
       }
       uint64_t m = __ballot(active);
@@ -931,6 +936,15 @@ __global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
         const uint64_t st = shfl_u64(start, l);
         const SegDesc S = P.segs[seg];
         run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, EL, st, popped, err);
+        if (wave_or(err) & (ERR_QUEUE | ERR_VISITED)) {  // frontier overflow: spill the window
+          const uint64_t id = shfl_u64(vid, l);
+          if (lane == 0) {
+            const unsigned long long k = atomicAdd(P.counters + 3, 1ull);
+            if (k < P.spill_cap) P.spill[k] = id;
+            else err |= ERR_SPILL;
+          }
+          err &= ~(ERR_QUEUE | ERR_VISITED);
+        }
         if (any_err(err)) break;
       }
       if (any_err(err)) break;
@@ -1091,17 +1105,36 @@ int upload(const std::vector<T>& v, T** d, std::string& err) {
 }
 
 struct Variant {
-  uint32_t vcap, qcap;
+  uint32_t vcap, qcap;  // vcap 0: no dedup table (unbeamed engines only)
 };
 
+template <uint32_t V, uint32_t Q>
+void launch_one(uint32_t grid, hipStream_t s, const SearchParams& P) {
+  hipLaunchKernelGGL((bfs_window_kernel<V, Q>), dim3(grid), dim3(64), 0, s, P);
+}
+
+// LDS per wave: 16 B x (vcap + qcap) + vcap claim bytes
+constexpr Variant kVariants[] = {{0, 128},   {0, 256},    {0, 512},     {256, 256},
+                                 {512, 256}, {512, 512},  {1024, 1024}, {2048, 2048}};
+
 hipError_t launch_variant(const Variant& v, uint32_t grid, hipStream_t s, const SearchParams& P) {
-  if (v.vcap == 512 && v.qcap == 512)
-    hipLaunchKernelGGL((bfs_window_kernel<512, 512>), dim3(grid), dim3(64), 0, s, P);
-  else if (v.vcap == 1024 && v.qcap == 1024)
-    hipLaunchKernelGGL((bfs_window_kernel<1024, 1024>), dim3(grid), dim3(64), 0, s, P);
-  else
-    hipLaunchKernelGGL((bfs_window_kernel<2048, 2048>), dim3(grid), dim3(64), 0, s, P);
+  switch (v.vcap * 4096u + v.qcap) {
+    case 0 * 4096u + 128: launch_one<0, 128>(grid, s, P); break;
+    case 0 * 4096u + 256: launch_one<0, 256>(grid, s, P); break;
+    case 0 * 4096u + 512: launch_one<0, 512>(grid, s, P); break;
+    case 256 * 4096u + 256: launch_one<256, 256>(grid, s, P); break;
+    case 512 * 4096u + 256: launch_one<512, 256>(grid, s, P); break;
+    case 512 * 4096u + 512: launch_one<512, 512>(grid, s, P); break;
+    case 1024 * 4096u + 1024: launch_one<1024, 1024>(grid, s, P); break;
+    default: launch_one<2048, 2048>(grid, s, P); break;
+  }
   return hipGetLastError();
+}
+
+// first dedup-table size tried for beamed engines (FAC_BEAM_VCAP overrides; 256 / 512 / ...)
+uint32_t default_beam_vcap() {
+  const char* e = std::getenv("FAC_BEAM_VCAP");
+  return e ? (uint32_t)std::atoi(e) : 512u;
 }
 
 bool debug_poison() {
@@ -1297,48 +1330,81 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
 
   int cus = 256;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
-  const uint64_t want = (windows + P.chunk - 1) / P.chunk;
-  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * 16));
-
-  const uint64_t fan = 3ull + 2ull * e.max_degree;  // one state's fan-out bound
-  const Variant variants[] = {{512, 512}, {1024, 1024}, {2048, 2048}};
-  size_t vi = 0;
-  if (P.beam) {
-    while (vi < 3 && 2ull * P.beam + fan + 1 > variants[vi].qcap) ++vi;
-    if (vi == 3) {
-      err = "beam width too large for the on-chip frontier";
-      return FAC_E_UNSUPPORTED;
-    }
+  // Variant ladder. A variant fits when one state's fan-out always fits the ring: for a beam,
+  // after the selection (<= 2 bw pending, search.rs:577-589) plus one non-root state's pushes;
+  // without one, only the single-state bound (overflowing windows spill to the next variant).
+  const uint64_t fan_root = 3ull + 2ull * (e.nodes.empty() ? 0u : e.nodes[0].edge_end - e.nodes[0].edge_begin);
+  const uint64_t fan_nr = 3ull + 2ull * e.max_degree_nonroot;
+  auto fits = [&](const Variant& v) {
+    if (P.beam) return v.vcap > 0 && fan_root + 1 <= v.qcap && 2ull * P.beam + fan_nr + 1 <= v.qcap;
+    return fan_root + 1 <= v.qcap && fan_nr + 1 <= v.qcap;
+  };
+  const size_t nv = sizeof(kVariants) / sizeof(kVariants[0]);
+  size_t vi = nv;
+  // defaults (measured on MI355X): beamed -> 512-entry table + 256-entry ring
+  // (12.8 KB LDS); unbeamed -> no table + 512-entry ring (a 128 ring cuts batches too often)
+  for (size_t i = 0; i < nv && vi == nv; ++i)
+    if (fits(kVariants[i]) && (P.beam ? kVariants[i].vcap >= default_beam_vcap()
+                                      : kVariants[i].vcap == 0 && kVariants[i].qcap >= 512))
+      vi = i;
+  for (size_t i = 0; i < nv && vi == nv; ++i)
+    if (fits(kVariants[i])) vi = i;
+  if (const char* fv = std::getenv("FAC_VARIANT")) {  // tuning override "vcap,qcap"
+    unsigned a = 0, b = 0;
+    if (std::sscanf(fv, "%u,%u", &a, &b) == 2)
+      for (size_t i = 0; i < nv; ++i)
+        if (kVariants[i].vcap == a && kVariants[i].qcap == b && fits(kVariants[i])) vi = i;
   }
+  if (vi == nv) {
+    err = "beam width too large for the on-chip frontier";
+    return FAC_E_UNSUPPORTED;
+  }
+  auto escalate = [&](size_t cur) {  // next variant for spilled windows
+    const uint32_t want_v = std::max<uint32_t>(kVariants[cur].vcap * 2, 512);
+    for (size_t i = cur + 1; i < nv; ++i)
+      if (fits(kVariants[i]) && kVariants[i].vcap >= want_v && kVariants[i].qcap >= kVariants[cur].qcap) return i;
+    return nv;
+  };
 
-  DevBuf d_segs, d_prefix, d_out, d_ebuf, d_cnt;
+  DevBuf d_segs, d_prefix, d_out, d_ebuf, d_cnt, d_list, d_spill;
   HIP_TRY(d_segs.alloc(segs.size() * sizeof(SegDesc), stream));
   HIP_TRY(d_prefix.alloc(prefix.size() * sizeof(uint64_t), stream));
   HIP_TRY(hipMemcpyAsync(d_segs.p, segs.data(), segs.size() * sizeof(SegDesc), hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(d_prefix.p, prefix.data(), prefix.size() * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
   uint64_t out_cap = std::max<uint64_t>(4096, windows / 64);
-  HIP_TRY(d_ebuf.alloc((size_t)grid * P.ecap * sizeof(uint4), stream));
+  uint64_t spill_cap = std::max<uint64_t>(4096, windows / 32);
+  const uint32_t max_grid = (uint32_t)cus * 16;
+  HIP_TRY(d_ebuf.alloc((size_t)max_grid * P.ecap * sizeof(uint4), stream));
   HIP_TRY(d_cnt.alloc(4 * sizeof(unsigned long long), stream));
   HIP_TRY(d_out.alloc(out_cap * sizeof(fac_match), stream));
+  HIP_TRY(d_spill.alloc(spill_cap * sizeof(uint64_t), stream));
   Events ev;
   HIP_TRY(hipEventCreate(&ev.a));
   HIP_TRY(hipEventCreate(&ev.b));
   P.segs = static_cast<const SegDesc*>(d_segs.p);
   P.seg_prefix = static_cast<const uint64_t*>(d_prefix.p);
+  P.win_list = nullptr;
 
   int rc = FAC_OK;
-  uint64_t retries = 0, launches = 0;
+  uint64_t retries = 0, launches = 0, popped = 0, pass_windows = windows;
   unsigned long long cnt[4] = {0, 0, 0, 0};
   float ms_total = 0.f;
+  out.clear();
   for (;;) {
+    P.chunk = P.win_list ? 1u : 256u;  // spilled windows are few and heavy: one per block turn
+    P.total_windows = pass_windows;
+    const uint64_t want = (pass_windows + P.chunk - 1) / P.chunk;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, max_grid));
     P.ebuf = static_cast<uint4*>(d_ebuf.p);
     P.out = static_cast<fac_match*>(d_out.p);
     P.out_cap = out_cap;
+    P.spill = static_cast<uint64_t*>(d_spill.p);
+    P.spill_cap = spill_cap;
     P.counters = static_cast<unsigned long long*>(d_cnt.p);
     HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 4 * sizeof(unsigned long long), stream));
     if (debug_poison()) HIP_TRY(hipMemsetAsync(d_out.p, 0xAB, out_cap * sizeof(fac_match), stream));
     HIP_TRY(hipEventRecord(ev.a, stream));
-    const hipError_t le = launch_variant(variants[vi], grid, stream, P);
+    const hipError_t le = launch_variant(kVariants[vi], grid, stream, P);
     if (le != hipSuccess) {
       err = std::string("kernel launch: ") + hipGetErrorString(le);
       rc = FAC_E_HIP;
@@ -1351,26 +1417,18 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
     HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
     ms_total += ms;
     launches += 1;
+    popped += cnt[1];
     const unsigned flags = (unsigned)cnt[2];
     if (flags & ERR_HALO) {
       err = "haystack shard does not hold the halo its windows need";
       rc = FAC_E_INVALID;
       break;
     }
-    if (flags & (ERR_QUEUE | ERR_VISITED)) {
-      if (vi + 1 < 3) {
-        ++vi;
-        ++retries;
-        continue;
-      }
-      err = "per-window frontier exceeded the on-chip capacity";
-      rc = FAC_E_CAPACITY;
-      break;
-    }
+    // buffer growth: the whole pass is re-run (its counters were reset)
     if (flags & ERR_EMIT) {
       if (P.ecap < (1u << 20)) {
         P.ecap *= 8;
-        HIP_TRY(d_ebuf.alloc((size_t)grid * P.ecap * sizeof(uint4), stream));
+        HIP_TRY(d_ebuf.alloc((size_t)max_grid * P.ecap * sizeof(uint4), stream));
         ++retries;
         continue;
       }
@@ -1378,22 +1436,46 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
       rc = FAC_E_CAPACITY;
       break;
     }
+    if ((flags & ERR_SPILL) || cnt[3] > spill_cap) {
+      spill_cap = std::max<uint64_t>(cnt[3], spill_cap * 2);
+      HIP_TRY(d_spill.alloc(spill_cap * sizeof(uint64_t), stream));
+      ++retries;
+      continue;
+    }
     if (cnt[0] > out_cap) {
       out_cap = cnt[0];
       HIP_TRY(d_out.alloc(out_cap * sizeof(fac_match), stream));
       ++retries;
       continue;
     }
-    out.resize(cnt[0]);
-    if (cnt[0]) HIP_TRY(hipMemcpyAsync(out.data(), d_out.p, cnt[0] * sizeof(fac_match), hipMemcpyDeviceToHost, stream));
+    const size_t have = out.size();
+    out.resize(have + cnt[0]);
+    if (cnt[0]) HIP_TRY(hipMemcpyAsync(out.data() + have, d_out.p, cnt[0] * sizeof(fac_match), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
-    break;
+    if (cnt[3] == 0) break;
+    // windows that overflowed this variant's frontier: re-run just those on the next one
+    const size_t nx = escalate(vi);
+    if (nx == nv) {
+      err = "per-window frontier exceeded the on-chip capacity";
+      rc = FAC_E_CAPACITY;
+      break;
+    }
+    vi = nx;
+    pass_windows = cnt[3];
+    std::swap(d_list.p, d_spill.p);
+    std::swap(d_list.s, d_spill.s);
+    if (!d_spill.p || spill_cap < pass_windows) {
+      HIP_TRY(d_spill.alloc(std::max<uint64_t>(spill_cap, pass_windows) * sizeof(uint64_t), stream));
+      spill_cap = std::max<uint64_t>(spill_cap, pass_windows);
+    }
+    P.win_list = static_cast<const uint64_t*>(d_list.p);
+    ++retries;
   }
   if (stats) {
     stats->kernel_ms += ms_total;
     stats->kernel_launches += launches;
     stats->windows += windows;
-    stats->states_popped += cnt[1];
+    stats->states_popped += popped;
     stats->graphemes = h.n;
     stats->bytes = h.len;
     stats->retries += retries;

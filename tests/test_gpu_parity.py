@@ -150,3 +150,48 @@ def test_long_haystack_windows():
     text = " ".join(words[rng.next() % 4][: 3 + rng.next() % 6] + "xyz"[rng.next() % 3] for _ in range(3000))
     compare(B().fuzzy(L().edits(1)), words, text, 0.7)
     compare(B().fuzzy(L().edits(2)).beam_width(8), words, text, 0.7)
+
+
+def _staged_vs_oracle(builder, patterns, hay, thr):
+    gpu = builder.build(patterns)
+    got, st = gpu.stage(hay.encode("utf-8")).search_windows(thr)
+    want = OracleEngine(builder, patterns).raw_rows(hay, thr)
+    assert sorted(got) == sorted(want)
+    return st, len(want)
+
+
+def test_frontier_spill_unbeamed():
+    """Runs of one letter against one-letter patterns: duplicate states explode, the dedup-free
+    unbeamed variant overflows its ring, and those windows are re-run on the dedup variants."""
+    rng = Rng(5)
+    hay = "".join("aaaaaaaaaaaaaaaa" if rng.next() % 3 else "ab" for _ in range(40))
+    st, n = _staged_vs_oracle(B().fuzzy(L().edits(3)), ["aaaaaaaaaa", "aaaab", "baaaaaaaa"], hay, 0.5)
+    assert n > 0 and st.retries > 0
+
+
+@pytest.mark.parametrize("beam_vcap", ["256", "512"])
+def test_frontier_spill_beamed(monkeypatch, beam_vcap):
+    """Beamed searches whose windows fill the dedup table (oracle: up to 456 keys per window):
+    spilled windows are re-run on a larger variant with results identical to the oracle; and a
+    C3-shaped slice with the table first sized `beam_vcap`."""
+    from fuzzy_aho_corasick import workloads
+    monkeypatch.setenv("FAC_BEAM_VCAP", beam_vcap)
+    rng = Rng(5)
+    hay = "".join("aaaaaaaaaaaaaaaa" if rng.next() % 3 else "ab" for _ in range(40))
+    st, n = _staged_vs_oracle(B().fuzzy(L().edits(3)).beam_width(64), ["aaaaaaaaaa", "aaaab", "baaaaaaaa"], hay, 0.5)
+    assert n > 0 and st.retries > 0
+    w = workloads.config("c3", 24 << 10, 3)
+    st, n = _staged_vs_oracle(workloads.builder_for(w), w.patterns, w.haystack.decode("utf-8"), w.threshold)
+    assert n > 0
+
+
+@pytest.mark.parametrize("variant", ["0,128", "0,256", "0,512", "256,256", "512,256", "512,512", "1024,1024",
+                                     "2048,2048"])
+def test_every_frontier_variant(monkeypatch, variant):
+    """Each LDS frontier variant (dedup table x queue ring) gives oracle-identical results."""
+    monkeypatch.setenv("FAC_VARIANT", variant)
+    rng = Rng(0xabcdef)
+    words = ["needle", "haystack", "fuzzy", "automaton", "école", "Москва"]
+    text = " ".join(words[rng.next() % 6][: 3 + rng.next() % 6] + "xyzé"[rng.next() % 4] for _ in range(600))
+    _staged_vs_oracle(B().fuzzy(L().edits(2)), words, text, 0.6)
+    _staged_vs_oracle(B().fuzzy(L().edits(2)).beam_width(8).case_insensitive(True), words, text, 0.6)
