@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -726,14 +727,29 @@ __device__ __forceinline__ void vis_lookup(const KState* vis, const KState& s, b
   }
 }
 
+constexpr uint32_t claim_slots(uint32_t vcap) { return vcap / 2 < 64 ? 64 : vcap / 2; }
+
+#ifdef FAC_PHASE_PROF  // diagnostics build (make prof): cycles per phase of run_window
+__device__ unsigned long long g_prof[16];
+#define PROF_T(t) const uint64_t t = __builtin_amdgcn_s_memtime()
+#define PROF_ACC(i, t0) pr[i] += __builtin_amdgcn_s_memtime() - (t0)
+#else
+#define PROF_T(t)
+#define PROF_ACC(i, t0)
+#endif
+
 // One start window, explored by one wavefront. States are popped in the reference's FIFO order in
 // batches of up to 64 (one state per lane); a batch is cut exactly where the reference's sequential
 // semantics would diverge: before the first in-batch dedup conflict, before the first pop at which
 // the beam would trigger, and before the first >64-edge node (expanded alone, edge-parallel).
 template <uint32_t VCAP, uint32_t QCAP>
-__device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint8_t* claim,
-                           EmitList& EL, uint64_t start, uint64_t& popped, unsigned& err) {
+__device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
+                           uint32_t& cseq, EmitList& EL, uint64_t start, uint64_t& popped, unsigned& err) {
   const uint32_t lane = lane_id();
+#ifdef FAC_PHASE_PROF
+  uint64_t pr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  PROF_T(t_win);
   if constexpr (VCAP > 0)
     for (uint32_t i = lane; i < VCAP; i += 64) vis[i].node = EMPTY;
   uint32_t vcount = 0;
@@ -744,7 +760,10 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
   const uint32_t beam2 = 2u * P.beam;
 
   while (head < tail) {
+    PROF_T(t0);
     if (P.beam && tail - head > beam2) beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
+    PROF_ACC(0, t0);
+    PROF_T(t1);
     const uint32_t B = min(tail - head, 64u);
     const bool in_b = lane < B;
     KState st{EMPTY, 0u, 0.0f, 0u};
@@ -763,7 +782,9 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     }
     const bool wide = alive && (nd.edge_end - nd.edge_begin) > 64u;
     const uint64_t mwide = __ballot(wide);
+    PROF_ACC(1, t1);
     if (mwide & 1ull) {  // first state alone, edge-parallel
+      PROF_T(t2);
       const KState s0 = q[head & (QCAP - 1)];
       head += 1;
       popped += 1;
@@ -772,9 +793,11 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
       const DevNode n0 = P.nodes[s0.node];
       if (n0.out_begin != n0.out_end) emit_state(P, EL, s0.jm >> 16, s0.pen, s0.packed, n0.out_begin, n0.out_end, err);
       expand_wide<QCAP>(P, S, q, head, tail, s0, n0, start, err);
+      PROF_ACC(2, t2);
       if (any_err(err)) break;
       continue;
     }
+    PROF_T(t3);
     uint32_t Bc = mwide ? (uint32_t)first_lane(mwide) : B;
     // ---- phase B: per-lane expansion decisions and push counts
     LaneExp x{-1, -1, false, 0ull, 0ull, 0u};
@@ -795,48 +818,81 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
       err |= ERR_QUEUE;
       break;
     }
-    // ---- phase C: dedup commit. Fast path: every lane claims its table slot (the slot holding its
-    // key, or the empty slot it would insert into); if no two lanes of the batch claim the same slot,
-    // no state of the batch can see another's write and all updates commit in parallel. Otherwise
-    // commit in FIFO order and cut the batch at the first state whose lookup changed.
+    PROF_ACC(3, t3);
+    PROF_T(t4);
+    // ---- phase C: dedup commit (search.rs:617-627 in FIFO order). Only writers matter: a skipped
+    // state's decision cannot change within the batch (stored penalties only decrease). Lanes with
+    // the same key found the same slot in phase A, so each writer claims its slot (lowest lane
+    // wins); a writer whose key equals its slot's winner, or an earlier losing writer's key, would
+    // see a changed table entry in sequential order: the batch is cut before the first such lane.
+    // Winners write in parallel; losers (distinct keys that met at one empty slot) insert serially.
     if constexpr (VCAP > 0) {
-      const bool part = lane < Bc && vslot != EMPTY;
-      if (part) claim[vslot] = (uint8_t)lane;
+      const bool wr = lane < Bc && !skip;
+      cseq += 1;
+      if (cseq >= (1u << 26)) {  // sequence wrap: forget all claims
+        for (uint32_t i = lane; i < claim_slots(VCAP); i += 64) claim[i] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        cseq = 1;
+      }
+      // claims are hashed to VCAP/2 words: lanes of different slots may share one (then they are
+      // "losers" with distinct keys and take the serial insert, which also handles found keys)
+      const uint32_t cs = vslot & (claim_slots(VCAP) - 1);
+      if (wr && vslot != EMPTY) atomicMax(&claim[cs], (cseq << 6) | (63u - lane));
       __builtin_amdgcn_wave_barrier();
-      const bool clash = part && claim[vslot] != (uint8_t)lane;
-      const bool ins_new = lane < Bc && !skip && !found && vslot != EMPTY;
-      const uint32_t n_ins = (uint32_t)__popcll(__ballot(ins_new));
+      const uint32_t w = (wr && vslot != EMPTY) ? 63u - (claim[cs] & 63u) : lane;
+      const uint32_t wn = __shfl(st.node, (int)w), wj = __shfl(st.jm, (int)w), wp = __shfl(st.packed, (int)w);
+      const bool same = wr && w != lane && wn == st.node && wj == st.jm && wp == st.packed;
+      const bool loser = wr && w != lane && !same;
+      uint64_t dup = __ballot(same);
+      const uint64_t lmask = __ballot(loser);
+      if (lmask) {
+        bool d2 = false;
+        uint64_t mm = lmask;
+        while (mm) {
+          const int l = first_lane(mm);
+          mm &= mm - 1;
+          const uint32_t kn = shfl_u32(st.node, l), kj = shfl_u32(st.jm, l), kp = shfl_u32(st.packed, l);
+          d2 = d2 || (loser && lane > (uint32_t)l && kn == st.node && kj == st.jm && kp == st.packed);
+        }
+        dup |= __ballot(d2);
+      }
+      if (dup) Bc = min(Bc, (uint32_t)first_lane(dup));  // lane 0 is never a duplicate
+      const bool wrc = wr && lane < Bc;
+      const uint32_t n_ins = (uint32_t)__popcll(__ballot(wrc && !found));
       const bool full = vcount + n_ins >= VCAP - VCAP / 8;
-      if (!__ballot(clash) && !__ballot(lane < Bc && vslot == EMPTY) && !full) {
-        if (lane < Bc && !skip) {
+      if (!full && !__ballot(wrc && vslot == EMPTY)) {
+        if (wrc && w == lane) {
           if (found) vis[vslot].pen = st.pen;  // lower the stored penalty (:623)
           else vis[vslot] = st;                // insert (:626)
         }
-        vcount += n_ins;
-      } else {
+        vcount += (uint32_t)__popcll(__ballot(wrc && w == lane && !found));
+        __builtin_amdgcn_wave_barrier();
+        uint64_t ml = __ballot(wrc && loser);
+        while (ml) {
+          const int l = first_lane(ml);
+          ml &= ml - 1;
+          KState kt;
+          kt.node = shfl_u32(st.node, l);
+          kt.jm = shfl_u32(st.jm, l);
+          kt.pen = shfl_f32(st.pen, l);
+          kt.packed = shfl_u32(st.packed, l);
+          visited_check<VCAP>(vis, vcount, kt, P.beam != 0, err);
+        }
+      } else {  // near-full table: the reference order, one state at a time
         for (uint32_t t = 0; t < Bc; ++t) {
+          if (!((__ballot(wr) >> t) & 1ull)) continue;
           KState kt;
           kt.node = shfl_u32(st.node, t);
           kt.jm = shfl_u32(st.jm, t);
           kt.pen = shfl_f32(st.pen, t);
           kt.packed = shfl_u32(st.packed, t);
-          const bool f_t = (__ballot(found) >> t) & 1ull;
-          const uint32_t sb_t = shfl_u32(stored_bits, t);
-          const bool skip_t = (__ballot(skip) >> t) & 1ull;
-          if (t > 0) {  // did an earlier state of this batch write this key?
-            bool f2;
-            uint32_t sb2, sl2;
-            vis_lookup<VCAP>(vis, kt, f2, sb2, sl2);
-            if (f2 != f_t || (f2 && sb2 != sb_t)) {
-              Bc = t;
-              break;
-            }
-          }
-          if (!skip_t) visited_check<VCAP>(vis, vcount, kt, P.beam != 0, err);
+          visited_check<VCAP>(vis, vcount, kt, P.beam != 0, err);
         }
       }
       __builtin_amdgcn_wave_barrier();
     }
+    PROF_ACC(4, t4);
+    PROF_T(t5);
     // ---- phase D: emissions (FIFO order), then pushes at tail + exclusive prefix
     uint64_t mem = __ballot(alive && lane < Bc && nd.out_begin != nd.out_end);
     while (mem) {
@@ -845,11 +901,17 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
       emit_state(P, EL, shfl_u32(st.jm, l) >> 16, shfl_f32(st.pen, l), shfl_u32(st.packed, l),
                  shfl_u32(nd.out_begin, l), shfl_u32(nd.out_end, l), err);
     }
+    PROF_ACC(5, t5);
+    PROF_T(t6);
     if (alive && lane < Bc && x.count) lane_push<QCAP>(P, S, q, tail + excl, st, nd, x, start, err);
     __builtin_amdgcn_wave_barrier();
     tail += shfl_u32(incl, Bc - 1);
     head += Bc;
     popped += Bc;
+    PROF_ACC(6, t6);
+#ifdef FAC_PHASE_PROF
+    pr[8] += 1;  // batches
+#endif
     if (any_err(err)) break;
   }
 
@@ -880,6 +942,11 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
       P.out[base + i] = m;
     }
   }
+#ifdef FAC_PHASE_PROF
+  PROF_ACC(7, t_win);
+  if (lane == 0)
+    for (int i = 0; i < 9; ++i) atomicAdd(&g_prof[i], (unsigned long long)pr[i]);
+#endif
 }
 
 // 2-gram window skip (search.rs:535-553)
@@ -908,10 +975,15 @@ template <uint32_t VCAP, uint32_t QCAP>
 __global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
   __shared__ KState s_vis[VCAP ? VCAP : 1];
   __shared__ KState s_q[QCAP];
-  __shared__ uint8_t s_claim[VCAP ? VCAP : 4];
+  __shared__ uint32_t s_claim[VCAP ? claim_slots(VCAP) : 1];
   const uint32_t lane = lane_id();
   EmitList EL{P.ebuf + (size_t)blockIdx.x * P.ecap, P.ecap, 0};
   uint64_t popped = 0;
+  uint32_t cseq = 0;  // dedup-commit claim sequence (phase C)
+  if constexpr (VCAP > 0) {
+    for (uint32_t i = lane_id(); i < claim_slots(VCAP); i += 64) s_claim[i] = 0u;
+    __builtin_amdgcn_wave_barrier();
+  }
   unsigned err = 0;
   const uint64_t stride = (uint64_t)gridDim.x * P.chunk;
   for (uint64_t cb = (uint64_t)blockIdx.x * P.chunk; cb < P.total_windows; cb += stride) {
@@ -935,7 +1007,7 @@ __global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
         const uint32_t seg = shfl_u32(kl, l);
         const uint64_t st = shfl_u64(start, l);
         const SegDesc S = P.segs[seg];
-        run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, EL, st, popped, err);
+        run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, popped, err);
         if (wave_or(err) & (ERR_QUEUE | ERR_VISITED)) {  // frontier overflow: spill the window
           const uint64_t id = shfl_u64(vid, l);
           if (lane == 0) {
@@ -1418,6 +1490,17 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
     ms_total += ms;
     launches += 1;
     popped += cnt[1];
+#ifdef FAC_PHASE_PROF
+    {
+      unsigned long long pr[16];
+      HIP_TRY(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_prof), sizeof(pr)));
+      std::fprintf(stderr, "FAC_PROF variant=%u,%u beam_select=%llu phaseA=%llu wide=%llu phaseB=%llu phaseC=%llu "
+                   "emit=%llu push=%llu window_total=%llu batches=%llu popped=%llu\n", kVariants[vi].vcap,
+                   kVariants[vi].qcap, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], pr[8], cnt[1]);
+      std::memset(pr, 0, sizeof(pr));
+      HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), pr, sizeof(pr)));
+    }
+#endif
     const unsigned flags = (unsigned)cnt[2];
     if (flags & ERR_HALO) {
       err = "haystack shard does not hold the halo its windows need";
