@@ -530,13 +530,34 @@ __device__ __forceinline__ bool sb_word_bit(uint4 m, uint32_t ch) {  // branch-f
   return ch < 128u && ((w >> (ch & 31u)) & 1u);
 }
 
-__device__ LaneExp lane_expand(const SearchParams& P, const SegDesc& S, const KState& st, const DevNode& nd,
-                               uint64_t start, uint32_t maxdeg, unsigned& err) {
-  LaneExp x{-1, -1, false, 0ull, 0ull, 0u};
+// Wave-wide inclusive prefix sum (DPP row shifts + row broadcasts).
+__device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
+  int x = (int)v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return (uint32_t)x;
+}
+
+// Per-state expansion decisions that do not depend on the edge (search.rs:742-765, 787-800,
+// 935-937, 994-1045): one lane per state.
+struct Prep {
+  uint32_t cur_ch, next_ch, nch;
+  uint32_t flags;  // PF_* bits
+  float remaining;
+};
+constexpr uint32_t PF_SUB = 1u, PF_DEL = 2u, PF_LAST = 4u, PF_CSB = 8u, PF_NEXT = 16u, PF_CUR = 32u, PF_SWAP = 64u,
+                   PF_EX = 128u, PF_INS = 256u;
+
+__device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState& st, const DevNode& nd, uint64_t start,
+                          unsigned& err) {
+  Prep r{0u, 0u, 0u, 0u, 0.0f};
   const bool fast = P.mef != 255u;
   const uint64_t n = S.n;
-  const float pen = st.pen;
-  const float remaining = __fsub_rn(P.max_penalties, pen);  // :648
+  r.remaining = __fsub_rn(P.max_penalties, st.pen);  // :648
   const uint32_t packed = st.packed;
   const uint32_t edits = edits_of(packed);
   const uint32_t j_rel = st.jm & 0xFFFFu, me_rel = st.jm >> 16;
@@ -544,15 +565,13 @@ __device__ LaneExp lane_expand(const SearchParams& P, const SegDesc& S, const KS
   const int32_t nlim = P.has_pattern_limits ? node_limits(P, st.node) : -1;
   const bool is_last_edit = fast && edits + 1u >= P.mef;  // :742
   const bool in_text = j < n;
-  const uint32_t cur_ch = in_text ? text_char(P, S, j, err) : 0u;
+  r.cur_ch = in_text ? text_char(P, S, j, err) : 0u;
   bool have_next = false;
-  uint32_t next_ch = 0;
   if (in_text && is_last_edit && (!fast || edits < P.mef) && j + 1 < n) {  // :758-765
     have_next = true;
-    next_ch = text_char(P, S, j + 1, err);
+    r.next_ch = text_char(P, S, j + 1, err);
   }
   bool subst_ok = false, swap_ok = false, ins_ok = false, del_ok = false;
-  uint32_t nch = 0;
   if (in_text) {
     if (fast) {
       subst_ok = edits < P.mef;
@@ -561,9 +580,9 @@ __device__ LaneExp lane_expand(const SearchParams& P, const SegDesc& S, const KS
       subst_ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.sub, (packed >> 16) & 0xFFu))
                        : (edits == 0 && ((packed >> 16) & 0xFFu) == 0);
     }
-    swap_ok = j + 1 < n && P.p_swp <= remaining && (!fast || edits < P.mef);  // :935-937
-    if (swap_ok) nch = have_next ? next_ch : text_char(P, S, j + 1, err);
-    if ((me_rel != 0u || j_rel != 0u) && P.p_ins <= remaining) {  // :994-1007
+    swap_ok = j + 1 < n && P.p_swp <= r.remaining && (!fast || edits < P.mef);  // :935-937
+    if (swap_ok) r.nch = have_next ? r.next_ch : text_char(P, S, j + 1, err);
+    if ((me_rel != 0u || j_rel != 0u) && P.p_ins <= r.remaining) {  // :994-1007
       if (fast) {
         ins_ok = edits < P.mef;
       } else {
@@ -572,11 +591,11 @@ __device__ LaneExp lane_expand(const SearchParams& P, const SegDesc& S, const KS
       }
       if (ins_ok && is_last_edit && nd.out_begin == nd.out_end) {
         const uint4 own = P.sb_bits[st.node];
-        ins_ok = have_next && sb_word_bit(own, next_ch);
+        ins_ok = have_next && sb_word_bit(own, r.next_ch);
       }
     }
   }
-  if (P.p_del <= remaining) {  // :1035-1045
+  if (P.p_del <= r.remaining) {  // :1035-1045
     if (fast) {
       del_ok = edits < P.mef;
     } else {
@@ -584,67 +603,139 @@ __device__ LaneExp lane_expand(const SearchParams& P, const SegDesc& S, const KS
       del_ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.del, (packed >> 8) & 0xFFu)) : false;
     }
   }
-  const bool have_cur = is_last_edit && in_text;
-  bool found_exact = false, found_x = false;
-  int64_t xnode = -1;
-  const uint32_t deg = nd.edge_end - nd.edge_begin;
-  // Edge loop with a wave-uniform trip count (maxdeg, SGPR) and predicated bodies: no per-lane
-  // loop control or exec-mask branching; lanes past their own degree load edge 0 and discard it.
-  const bool sub_on = in_text && subst_ok, ex_on = in_text;
-  const bool need_csb = is_last_edit && (subst_ok || del_ok);
-  uint32_t sub_lo = 0, sub_hi = 0, del_lo = 0, del_hi = 0;
-#pragma unroll 2
-  for (uint32_t e = 0; e < maxdeg; ++e) {
-    const bool valid = e < deg;
-    const DevEdge ed = P.edges[valid ? nd.edge_begin + e : 0u];
-    const uint32_t child = ed.next & EDGE_NEXT_MASK;
-    const bool child_out = (ed.next & EDGE_CHILD_OUTPUT) != 0;
-    const uint4 csb = P.sb_bits[(valid && need_csb && !child_out) ? child : 0u];
-    // first edge with this first char (structs.rs:512-519)
-    const bool is_exact = valid && ex_on && !found_exact && ed.ch == cur_ch;
-    found_exact = found_exact || is_exact;
-    x.exact = is_exact ? (int64_t)child : x.exact;
-    const bool is_x = valid && swap_ok && !found_x && ed.ch == nch;
-    found_x = found_x || is_x;
-    xnode = is_x ? (int64_t)child : xnode;
-    // substitution (:814-874; the exact target's edge is the only one skipped)
-    const bool asc = ed.ch < 128u && cur_ch < 128u;
-    const float tv = P.sim_ascii[asc ? ed.ch * 128u + cur_ch : 0u];
-    float sim = ed.ch == cur_ch ? 1.0f : (asc ? tv : 0.0f);
-    if (P.n_sim != 0 && !asc && ed.ch != cur_ch) sim = similarity(P, ed.ch, cur_ch);
-    const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
-    const bool sb_next = child_out || (have_next && sb_word_bit(csb, next_ch));
-    const bool sb_cur = child_out || (have_cur && sb_word_bit(csb, cur_ch));
-    const bool keep_sub = valid && sub_on && !is_exact && !(sim < P.min_sym) && !(penalty > remaining) &&
-                          (!is_last_edit || sb_next);
-    const bool keep_del = valid && del_ok && (!is_last_edit || sb_cur);  // :1055-1088
-    const uint32_t bit = 1u << (e & 31u);
-    if (e < 32u) {  // wave-uniform
-      sub_lo |= keep_sub ? bit : 0u;
-      del_lo |= keep_del ? bit : 0u;
-    } else {
-      sub_hi |= keep_sub ? bit : 0u;
-      del_hi |= keep_del ? bit : 0u;
+  r.flags = (in_text && subst_ok ? PF_SUB : 0u) | (del_ok ? PF_DEL : 0u) | (is_last_edit ? PF_LAST : 0u) |
+            (is_last_edit && (subst_ok || del_ok) ? PF_CSB : 0u) | (have_next ? PF_NEXT : 0u) |
+            (is_last_edit && in_text ? PF_CUR : 0u) | (swap_ok ? PF_SWAP : 0u) | (in_text ? PF_EX : 0u) |
+            (ins_ok ? PF_INS : 0u);
+  return r;
+}
+
+// Wave-wide inclusive max-scan (DPP), unsigned.
+__device__ __forceinline__ uint32_t wave_inclusive_max(uint32_t v) {
+  int x = (int)v;
+  x = (int)max((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false));
+  x = (int)max((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false));
+  x = (int)max((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false));
+  x = (int)max((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false));
+  x = (int)max((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false));
+  x = (int)max((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false));
+  return (uint32_t)x;
+}
+
+// LDS scratch of one batch's edge expansion. It aliases the dedup claim words: zeroed before use
+// (claims of the previous batch) and after (the claim protocol reads values < 128 as stale).
+struct ExpScratch {
+  unsigned long long msub[64];
+  unsigned long long mdel[64];
+  uint32_t exx[128];  // [2s] = 0xFFFF - first exact edge (0: none), [2s+1] = same for the swap edge
+  uint32_t mark[64];  // unit -> owner state lane + 1 (per round)
+};
+static_assert(sizeof(ExpScratch) <= 4u * 512u, "scratch must fit the smallest claim region");
+
+// Edge work of a batch, balanced over lanes: each state's edges are cut into units of UK edges and
+// the units of all states are dealt to lanes in rounds of 64 (a lane-per-state loop would run
+// for the batch's largest degree). Per edge: the exact/swap first-char match (structs.rs:512-519),
+// substitution (:814-874) and deletion (:1055-1088) keep tests incl. the last-edit dead-end filter.
+template <uint32_t UK>
+__device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode& nd, const Prep& pr, bool act,
+                             uint64_t& msub, uint64_t& mdel, uint32_t& ex, uint32_t& xe) {
+  const uint32_t lane = lane_id();
+  const uint32_t deg = act ? nd.edge_end - nd.edge_begin : 0u;
+  const uint32_t nunit = (deg + UK - 1) / UK;
+  const uint32_t uincl = wave_inclusive_sum(nunit);
+  const uint32_t ubase = uincl - nunit;
+  const uint32_t U = (uint32_t)__builtin_amdgcn_readlane((int)uincl, 63);
+  const uint32_t pk = pr.flags | (deg << 9) | (ubase << 16);  // flags 9 bits, deg <= 64, ubase < 4096
+  // the words may hold dedup claims of the previous batch
+  X->msub[lane] = 0ull;
+  X->mdel[lane] = 0ull;
+  reinterpret_cast<uint2*>(X->exx)[lane] = make_uint2(0u, 0u);
+  uint32_t carry = 0;
+  for (uint32_t R = 0; R < U; R += 64) {
+    X->mark[lane] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (nunit && ubase >= R && ubase < R + 64u) X->mark[ubase - R] = lane + 1u;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t v = X->mark[lane];
+    if (lane == 0) v = max(v, carry);
+    v = wave_inclusive_max(v);
+    carry = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    const bool valid = R + lane < U;
+    const int o = (int)(valid ? v - 1u : lane);
+    const uint32_t o_pk = __shfl(pk, o), o_eb = __shfl(nd.edge_begin, o);
+    const uint32_t cur = __shfl(pr.cur_ch, o), nxt = __shfl(pr.next_ch, o), nc = __shfl(pr.nch, o);
+    const float rem = __shfl(pr.remaining, o);
+    const uint32_t o_deg = (o_pk >> 9) & 0x7Fu, e0 = (R + lane - (o_pk >> 16)) * UK;
+    const bool sub_on = o_pk & PF_SUB, del_ok = o_pk & PF_DEL, is_last = o_pk & PF_LAST, need_csb = o_pk & PF_CSB;
+    const bool have_next = o_pk & PF_NEXT, have_cur = o_pk & PF_CUR, swap_ok = o_pk & PF_SWAP, ex_on = o_pk & PF_EX;
+    uint32_t sb = 0, db = 0, fe = 0xFFFFu, fx = 0xFFFFu;
+#pragma unroll
+    for (uint32_t i = 0; i < UK; ++i) {
+      const uint32_t e = e0 + i;
+      const bool ok = valid && e < o_deg;
+      const DevEdge ed = P.edges[ok ? o_eb + e : 0u];
+      const uint32_t child = ed.next & EDGE_NEXT_MASK;
+      const bool child_out = (ed.next & EDGE_CHILD_OUTPUT) != 0;
+      const uint4 csb = P.sb_bits[(ok && need_csb && !child_out) ? child : 0u];
+      fe = (ok && ex_on && fe == 0xFFFFu && ed.ch == cur) ? e : fe;
+      fx = (ok && swap_ok && fx == 0xFFFFu && ed.ch == nc) ? e : fx;
+      const bool asc = ed.ch < 128u && cur < 128u;
+      const float tv = P.sim_ascii[asc ? ed.ch * 128u + cur : 0u];
+      float sim = ed.ch == cur ? 1.0f : (asc ? tv : 0.0f);
+      if (P.n_sim != 0 && !asc && ed.ch != cur) sim = similarity(P, ed.ch, cur);
+      const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
+      const bool sb_next = child_out || (have_next && sb_word_bit(csb, nxt));
+      const bool sb_cur = child_out || (have_cur && sb_word_bit(csb, cur));
+      // the exact edge's bit is cleared by the owner once the first match is known
+      const bool keep_sub = ok && sub_on && !(sim < P.min_sym) && !(penalty > rem) && (!is_last || sb_next);
+      const bool keep_del = ok && del_ok && (!is_last || sb_cur);
+      sb |= (keep_sub ? 1u : 0u) << i;
+      db |= (keep_del ? 1u : 0u) << i;
     }
+    if (sb) atomicOr(&X->msub[o], (unsigned long long)sb << e0);
+    if (db) atomicOr(&X->mdel[o], (unsigned long long)db << e0);
+    if (fe != 0xFFFFu) atomicMax(&X->exx[2 * o], 0xFFFFu - fe);
+    if (fx != 0xFFFFu) atomicMax(&X->exx[2 * o + 1], 0xFFFFu - fx);
   }
-  x.msub = ((uint64_t)sub_hi << 32) | sub_lo;
-  x.mdel = ((uint64_t)del_hi << 32) | del_lo;
-  if (found_x) {  // swap: node2 = goto(goto(node, text[j+1]), text[j]) (:945-961)
-    const DevNode xn = P.nodes[(uint32_t)xnode];
+  __builtin_amdgcn_wave_barrier();
+  msub = X->msub[lane];
+  mdel = X->mdel[lane];
+  const uint2 exw = reinterpret_cast<const uint2*>(X->exx)[lane];
+  ex = exw.x ? 0xFFFFu - exw.x : 0xFFFFu;
+  xe = exw.y ? 0xFFFFu - exw.y : 0xFFFFu;
+  __builtin_amdgcn_wave_barrier();
+  X->msub[lane] = 0ull;
+  X->mdel[lane] = 0ull;
+  reinterpret_cast<uint2*>(X->exx)[lane] = make_uint2(0u, 0u);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Per-state completion: exact successor, the exact edge leaves the substitution set, swap target
+// goto(goto(node, text[j+1]), text[j]) (:945-967), push count.
+__device__ LaneExp lane_finish(const SearchParams& P, const KState& st, const DevNode& nd, const Prep& pr,
+                               uint64_t msub, uint64_t mdel, uint32_t ex, uint32_t xe) {
+  LaneExp x{-1, -1, false, msub, mdel, 0u};
+  if (ex != 0xFFFFu) {
+    x.exact = (int64_t)(P.edges[nd.edge_begin + ex].next & EDGE_NEXT_MASK);
+    x.msub &= ~(1ull << ex);
+  }
+  if (xe != 0xFFFFu) {
+    const DevNode xn = P.nodes[P.edges[nd.edge_begin + xe].next & EDGE_NEXT_MASK];
     for (uint32_t e = xn.edge_begin; e < xn.edge_end; ++e) {
       const DevEdge ed = P.edges[e];
-      if (ed.ch == cur_ch) {
+      if (ed.ch == pr.cur_ch) {
         x.swap = ed.next & EDGE_NEXT_MASK;
         break;
       }
     }
-    if (x.swap >= 0 && !fast) {  // within_limits_swap_ahead with node2's limits (:962-967)
+    if (x.swap >= 0 && P.mef == 255u) {  // within_limits_swap_ahead with node2's limits (:962-967)
+      const uint32_t packed = st.packed, edits = edits_of(packed);
       const Lim m = pick_limits(P, node_limits(P, (uint32_t)x.swap));
       if (!(m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.swp, packed >> 24)) : false)) x.swap = -1;
     }
   }
-  x.ins = ins_ok;
-  x.count = (x.exact >= 0 ? 1u : 0u) + (uint32_t)__popcll(x.msub) + (x.swap >= 0 ? 1u : 0u) + (ins_ok ? 1u : 0u) +
+  x.ins = (pr.flags & PF_INS) != 0;
+  x.count = (x.exact >= 0 ? 1u : 0u) + (uint32_t)__popcll(x.msub) + (x.swap >= 0 ? 1u : 0u) + (x.ins ? 1u : 0u) +
             (uint32_t)__popcll(x.mdel);
   return x;
 }
@@ -691,18 +782,6 @@ __device__ void lane_push(const SearchParams& P, const SegDesc& S, KState* q, ui
   }
 }
 
-// Wave-wide inclusive prefix sum (DPP row shifts + row broadcasts).
-__device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
-  int x = (int)v;
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
-  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
-  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
-  return (uint32_t)x;
-}
-
 // Read-only dedup lookup (per lane, linear probing). found/stored describe the table entry.
 template <uint32_t VCAP>
 __device__ __forceinline__ void vis_lookup(const KState* vis, const KState& s, bool& found, uint32_t& stored_bits,
@@ -727,12 +806,12 @@ __device__ __forceinline__ void vis_lookup(const KState* vis, const KState& s, b
   }
 }
 
-constexpr uint32_t claim_slots(uint32_t vcap) { return vcap / 2 < 64 ? 64 : vcap / 2; }
+constexpr uint32_t claim_slots(uint32_t vcap) { return vcap / 2 < 512 ? 512 : vcap / 2; }  // >= ExpScratch
 
 #ifdef FAC_PHASE_PROF  // diagnostics build (make prof): cycles per phase of run_window
 __device__ unsigned long long g_prof[16];
 #define PROF_T(t) const uint64_t t = __builtin_amdgcn_s_memtime()
-#define PROF_ACC(i, t0) pr[i] += __builtin_amdgcn_s_memtime() - (t0)
+#define PROF_ACC(i, t0) prof_acc[i] += __builtin_amdgcn_s_memtime() - (t0)
 #else
 #define PROF_T(t)
 #define PROF_ACC(i, t0)
@@ -747,7 +826,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
                            uint32_t& cseq, EmitList& EL, uint64_t start, uint64_t& popped, unsigned& err) {
   const uint32_t lane = lane_id();
 #ifdef FAC_PHASE_PROF
-  uint64_t pr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t prof_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   PROF_T(t_win);
   if constexpr (VCAP > 0)
@@ -802,8 +881,12 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     // ---- phase B: per-lane expansion decisions and push counts
     LaneExp x{-1, -1, false, 0ull, 0ull, 0u};
     const bool act = alive && lane < Bc;
-    const uint32_t maxdeg = ~wave_min_u32(act ? ~(nd.edge_end - nd.edge_begin) : ~0u);  // uniform
-    if (act) x = lane_expand(P, S, st, nd, start, maxdeg, err);
+    Prep pr{0u, 0u, 0u, 0u, 0.0f};
+    if (act) pr = lane_prep(P, S, st, nd, start, err);
+    uint64_t msub = 0, mdel = 0;
+    uint32_t ex = 0xFFFFu, xe = 0xFFFFu;
+    expand_units<4>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act, msub, mdel, ex, xe);
+    if (act) x = lane_finish(P, st, nd, pr, msub, mdel, ex, xe);
     const uint32_t cnt = (lane < Bc) ? x.count : 0u;
     const uint32_t incl = wave_inclusive_sum(cnt);
     const uint32_t excl = incl - cnt;
@@ -832,7 +915,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
       if (cseq >= (1u << 26)) {  // sequence wrap: forget all claims
         for (uint32_t i = lane; i < claim_slots(VCAP); i += 64) claim[i] = 0u;
         __builtin_amdgcn_wave_barrier();
-        cseq = 1;
+        cseq = 2;
       }
       // claims are hashed to VCAP/2 words: lanes of different slots may share one (then they are
       // "losers" with distinct keys and take the serial insert, which also handles found keys)
@@ -910,7 +993,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     popped += Bc;
     PROF_ACC(6, t6);
 #ifdef FAC_PHASE_PROF
-    pr[8] += 1;  // batches
+    prof_acc[8] += 1;  // batches
 #endif
     if (any_err(err)) break;
   }
@@ -945,7 +1028,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
 #ifdef FAC_PHASE_PROF
   PROF_ACC(7, t_win);
   if (lane == 0)
-    for (int i = 0; i < 9; ++i) atomicAdd(&g_prof[i], (unsigned long long)pr[i]);
+    for (int i = 0; i < 9; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof_acc[i]);
 #endif
 }
 
@@ -975,15 +1058,15 @@ template <uint32_t VCAP, uint32_t QCAP>
 __global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
   __shared__ KState s_vis[VCAP ? VCAP : 1];
   __shared__ KState s_q[QCAP];
-  __shared__ uint32_t s_claim[VCAP ? claim_slots(VCAP) : 1];
+  __shared__ __attribute__((aligned(16))) uint32_t s_claim[claim_slots(VCAP)];
   const uint32_t lane = lane_id();
   EmitList EL{P.ebuf + (size_t)blockIdx.x * P.ecap, P.ecap, 0};
   uint64_t popped = 0;
-  uint32_t cseq = 0;  // dedup-commit claim sequence (phase C)
-  if constexpr (VCAP > 0) {
-    for (uint32_t i = lane_id(); i < claim_slots(VCAP); i += 64) s_claim[i] = 0u;
-    __builtin_amdgcn_wave_barrier();
-  }
+  // dedup-commit claim sequence (phase C): fresh claims are >= 128, above any stale word the
+  // expansion scratch leaves behind (<= 64)
+  uint32_t cseq = 1;
+  for (uint32_t i = lane_id(); i < claim_slots(VCAP); i += 64) s_claim[i] = 0u;
+  __builtin_amdgcn_wave_barrier();
   unsigned err = 0;
   const uint64_t stride = (uint64_t)gridDim.x * P.chunk;
   for (uint64_t cb = (uint64_t)blockIdx.x * P.chunk; cb < P.total_windows; cb += stride) {
