@@ -62,6 +62,11 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
 }
 
 // Wave-wide minimum with DPP row shifts + row broadcasts (no LDS round trip); result is uniform.
+__device__ __forceinline__ uint64_t shfl_var_u64(uint64_t v, int src) {  // per-lane source (ds_bpermute)
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   const int I = -1;  // identity for unsigned min (0xFFFFFFFF)
   int x = (int)v;
@@ -632,6 +637,22 @@ struct ExpScratch {
 };
 static_assert(sizeof(ExpScratch) <= 4u * 512u, "scratch must fit the smallest claim region");
 
+// Owner state lane of unit R + lane: states' unit ranges are consecutive in lane order, so the
+// owner is the last state whose first unit is at or before it (LDS marks + max-scan).
+__device__ __forceinline__ int unit_owner(ExpScratch* X, uint32_t R, uint32_t nunit, uint32_t ubase, bool valid,
+                                          uint32_t& carry) {
+  const uint32_t lane = lane_id();
+  X->mark[lane] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  if (nunit && ubase >= R && ubase < R + 64u) X->mark[ubase - R] = lane + 1u;
+  __builtin_amdgcn_wave_barrier();
+  uint32_t v = X->mark[lane];
+  if (lane == 0) v = max(v, carry);
+  v = wave_inclusive_max(v);
+  carry = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+  return (int)(valid ? v - 1u : lane);
+}
+
 // Edge work of a batch, balanced over lanes: each state's edges are cut into units of UK edges and
 // the units of all states are dealt to lanes in rounds of 64 (a lane-per-state loop would run
 // for the batch's largest degree). Per edge: the exact/swap first-char match (structs.rs:512-519),
@@ -652,16 +673,8 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
   reinterpret_cast<uint2*>(X->exx)[lane] = make_uint2(0u, 0u);
   uint32_t carry = 0;
   for (uint32_t R = 0; R < U; R += 64) {
-    X->mark[lane] = 0u;
-    __builtin_amdgcn_wave_barrier();
-    if (nunit && ubase >= R && ubase < R + 64u) X->mark[ubase - R] = lane + 1u;
-    __builtin_amdgcn_wave_barrier();
-    uint32_t v = X->mark[lane];
-    if (lane == 0) v = max(v, carry);
-    v = wave_inclusive_max(v);
-    carry = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
     const bool valid = R + lane < U;
-    const int o = (int)(valid ? v - 1u : lane);
+    const int o = unit_owner(X, R, nunit, ubase, valid, carry);
     const uint32_t o_pk = __shfl(pk, o), o_eb = __shfl(nd.edge_begin, o);
     const uint32_t cur = __shfl(pr.cur_ch, o), nxt = __shfl(pr.next_ch, o), nc = __shfl(pr.nch, o);
     const float rem = __shfl(pr.remaining, o);
@@ -740,47 +753,73 @@ __device__ LaneExp lane_finish(const SearchParams& P, const KState& st, const De
   return x;
 }
 
-// Write one lane's pushes in the reference's order: exact, substitutions (edge order), swap,
-// insertion, deletions (edge order) (search.rs:787-1088).
-template <uint32_t QCAP>
-__device__ void lane_push(const SearchParams& P, const SegDesc& S, KState* q, uint32_t pos, const KState& st,
-                          const DevNode& nd, const LaneExp& x, uint64_t start, unsigned& err) {
+// Pushes of the committed states in the reference's order (search.rs:787-1088): per state exact,
+// substitutions (edge order), swap, insertion, deletions (edge order), written at the state's
+// exclusive-prefix offset. The owner lane writes exact/swap/insertion; substitutions and deletions
+// are written by the units that cover their edges (balanced like expand_units).
+template <uint32_t QCAP, uint32_t UK>
+__device__ void push_units(const SearchParams& P, ExpScratch* X, KState* q, uint32_t base, const KState& st,
+                           const DevNode& nd, const LaneExp& x, uint32_t cur_ch, bool act) {
+  const uint32_t lane = lane_id();
   const float pen = st.pen;
-  const uint32_t packed = st.packed;
   const uint32_t j_rel = st.jm & 0xFFFFu;
   const uint32_t jm1 = (j_rel + 1u) | ((j_rel + 1u) << 16);
-  if (x.exact >= 0) q[(pos++) & (QCAP - 1)] = KState{(uint32_t)x.exact, jm1, pen, packed};
-  if (x.msub) {
-    const uint32_t cur_ch = text_char(P, S, start + j_rel, err);
-    uint64_t m = x.msub;
-    while (m) {
-      const uint32_t e = (uint32_t)(__ffsll((unsigned long long)m) - 1);
-      m &= m - 1;
-      const DevEdge ed = P.edges[nd.edge_begin + e];
-      const float sim = similarity(P, ed.ch, cur_ch);
-      const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
-      q[(pos++) & (QCAP - 1)] = KState{ed.next & EDGE_NEXT_MASK, jm1, __fadd_rn(pen, penalty), packed + 0x10000u};
+  const uint32_t nex = x.exact >= 0 ? 1u : 0u, nsw = x.swap >= 0 ? 1u : 0u, nins = x.ins ? 1u : 0u;
+  const uint32_t sub_base = base + nex;
+  const uint32_t sw_pos = sub_base + (uint32_t)__popcll(x.msub);
+  const uint32_t del_base = sw_pos + nsw + nins;
+  if (act) {
+    if (nex) q[base & (QCAP - 1)] = KState{(uint32_t)x.exact, jm1, pen, st.packed};
+    if (nsw) {
+      const uint32_t jm2 = (j_rel + 2u) | ((j_rel + 2u) << 16);
+      q[sw_pos & (QCAP - 1)] = KState{(uint32_t)x.swap, jm2, __fadd_rn(pen, P.p_swp), st.packed + 0x1000000u};
+    }
+    if (nins) {
+      const uint32_t jmi = (j_rel + 1u) | ((st.jm >> 16) << 16);
+      q[(sw_pos + nsw) & (QCAP - 1)] = KState{st.node, jmi, __fadd_rn(pen, P.p_ins), st.packed + 1u};
     }
   }
-  if (x.swap >= 0) {
-    const uint32_t jm2 = (j_rel + 2u) | ((j_rel + 2u) << 16);
-    q[(pos++) & (QCAP - 1)] = KState{(uint32_t)x.swap, jm2, __fadd_rn(pen, P.p_swp), packed + 0x1000000u};
-  }
-  if (x.ins) {
-    const uint32_t jmi = (j_rel + 1u) | ((st.jm >> 16) << 16);
-    q[(pos++) & (QCAP - 1)] = KState{st.node, jmi, __fadd_rn(pen, P.p_ins), packed + 1u};
-  }
-  if (x.mdel) {
-    const float npen = __fadd_rn(pen, P.p_del);
-    uint64_t m = x.mdel;
-    while (m) {
-      const uint32_t e = (uint32_t)(__ffsll((unsigned long long)m) - 1);
-      m &= m - 1;
-      const uint32_t child = P.edges[nd.edge_begin + e].next & EDGE_NEXT_MASK;
-      q[(pos++) & (QCAP - 1)] = KState{child, st.jm, npen, packed + 0x100u};
+  const uint64_t any = act ? (x.msub | x.mdel) : 0ull;
+  const uint32_t span = any ? 64u - (uint32_t)__clzll((long long)any) : 0u;  // edges up to the last push
+  const uint32_t nunit = (span + UK - 1) / UK;
+  const uint32_t uincl = wave_inclusive_sum(nunit);
+  const uint32_t ubase = uincl - nunit;
+  const uint32_t U = (uint32_t)__builtin_amdgcn_readlane((int)uincl, 63);
+  uint32_t carry = 0;
+  for (uint32_t R = 0; R < U; R += 64) {
+    const bool valid = R + lane < U;
+    const int o = unit_owner(X, R, nunit, ubase, valid, carry);
+    const uint32_t o_ub = __shfl(ubase, o), o_span = __shfl(span, o), o_eb = __shfl(nd.edge_begin, o);
+    const uint64_t o_ms = shfl_var_u64(x.msub, o), o_md = shfl_var_u64(x.mdel, o);
+    const uint32_t o_sb = __shfl(sub_base, o), o_db = __shfl(del_base, o), o_cur = __shfl(cur_ch, o);
+    const float o_pen = __shfl(pen, o);
+    const uint32_t o_jm = __shfl(st.jm, o), o_packed = __shfl(st.packed, o);
+    const uint32_t e0 = (R + lane - o_ub) * UK;
+    const uint32_t o_j1 = (o_jm & 0xFFFFu) + 1u;
+#pragma unroll
+    for (uint32_t i = 0; i < UK; ++i) {
+      const uint32_t e = e0 + i;
+      const uint64_t bit = 1ull << (e & 63u);
+      const bool ps = valid && e < o_span && (o_ms & bit);
+      const bool pd = valid && e < o_span && (o_md & bit);
+      if (ps || pd) {
+        const DevEdge ed = P.edges[o_eb + e];
+        const uint32_t child = ed.next & EDGE_NEXT_MASK;
+        if (ps) {
+          const float sim = similarity(P, ed.ch, o_cur);
+          const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
+          const uint32_t pos = o_sb + (uint32_t)__popcll(o_ms & (bit - 1ull));
+          q[pos & (QCAP - 1)] = KState{child, o_j1 | (o_j1 << 16), __fadd_rn(o_pen, penalty), o_packed + 0x10000u};
+        }
+        if (pd) {
+          const uint32_t pos = o_db + (uint32_t)__popcll(o_md & (bit - 1ull));
+          q[pos & (QCAP - 1)] = KState{child, o_jm, __fadd_rn(o_pen, P.p_del), o_packed + 0x100u};
+        }
+      }
     }
   }
 }
+
 
 // Read-only dedup lookup (per lane, linear probing). found/stored describe the table entry.
 template <uint32_t VCAP>
@@ -805,6 +844,10 @@ __device__ __forceinline__ void vis_lookup(const KState* vis, const KState& s, b
     h = (h + 1) & (VCAP - 1);
   }
 }
+
+#ifndef FAC_UK
+#define FAC_UK 2  // edges per expansion unit (measured: 2 > 4 > 8 on C2/C3)
+#endif
 
 constexpr uint32_t claim_slots(uint32_t vcap) { return vcap / 2 < 512 ? 512 : vcap / 2; }  // >= ExpScratch
 
@@ -885,7 +928,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     if (act) pr = lane_prep(P, S, st, nd, start, err);
     uint64_t msub = 0, mdel = 0;
     uint32_t ex = 0xFFFFu, xe = 0xFFFFu;
-    expand_units<4>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act, msub, mdel, ex, xe);
+    expand_units<FAC_UK>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act, msub, mdel, ex, xe);
     if (act) x = lane_finish(P, st, nd, pr, msub, mdel, ex, xe);
     const uint32_t cnt = (lane < Bc) ? x.count : 0u;
     const uint32_t incl = wave_inclusive_sum(cnt);
@@ -986,7 +1029,8 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     }
     PROF_ACC(5, t5);
     PROF_T(t6);
-    if (alive && lane < Bc && x.count) lane_push<QCAP>(P, S, q, tail + excl, st, nd, x, start, err);
+    push_units<QCAP, FAC_UK>(P, reinterpret_cast<ExpScratch*>(claim), q, tail + excl, st, nd, x, pr.cur_ch,
+                             alive && lane < Bc && x.count != 0);
     __builtin_amdgcn_wave_barrier();
     tail += shfl_u32(incl, Bc - 1);
     head += Bc;
