@@ -239,6 +239,8 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
     d.pidx = pidx[i];
     d.pad = 0;
   }
+  e.sb_edge.resize(e.edges.size());
+  for (size_t k = 0; k < e.edges.size(); ++k) e.sb_edge[k] = e.sb_bits[e.edges[k].next & EDGE_NEXT_MASK];
   // reach fixpoint (builder.rs:348-381): children always have larger ids than their parent in a
   // freshly built trie, so one reverse pass reaches the fixpoint.
   std::vector<uint64_t> rl(nn, 0);

@@ -7,6 +7,8 @@
 //   DevNode[N]   32 B  prune_len, prune_len_over_weight, edge range, output range, pattern_index
 //   DevEdge[E]    8 B  first code point | target node + (child-has-output, single-byte) flag bits
 //   sb_bits[N]   16 B  128-bit map of the node's single-ASCII-byte edge chars (structs.rs:471-493)
+//   sb_edge[E]   16 B  sb_bits of each edge's child (one parent edge per node: loads in parallel
+//                      with the edge record instead of after it)
 //   out_pat[O]    4 B  output pattern ids (own + fail-merged, builder.rs:235,264-268)
 //   DevPattern[P]32 B  grapheme_len as f32, weight, per-pattern limits
 //   sim_ascii  64 KiB  128x128 f32 similarity table (structs.rs:36-48) + sorted non-ASCII pairs
@@ -93,6 +95,7 @@ struct SearchParams {
   const DevEdge* edges;
   const uint32_t* out_pat;
   const uint4* sb_bits;
+  const uint4* sb_edge;
   const DevPattern* pats;
   const float* sim_ascii;
   const uint64_t* sim_keys;  // (a << 32 | b), sorted
@@ -154,6 +157,7 @@ struct Engine {
   std::vector<DevEdge> edges;
   std::vector<uint32_t> out_pat;
   std::vector<uint4> sb_bits;
+  std::vector<uint4> sb_edge;
   std::vector<DevPattern> pats;
   std::vector<float> sim_ascii;
   std::vector<uint64_t> sim_keys;
@@ -179,6 +183,7 @@ struct Engine {
   DevEdge* d_edges = nullptr;
   uint32_t* d_out_pat = nullptr;
   uint4* d_sb = nullptr;
+  uint4* d_sb_edge = nullptr;
   DevPattern* d_pats = nullptr;
   float* d_sim_ascii = nullptr;
   uint64_t* d_sim_keys = nullptr;

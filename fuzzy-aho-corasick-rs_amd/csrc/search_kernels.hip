@@ -384,7 +384,7 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
       const DevEdge ed = P.edges[nd.edge_begin + lane];
       e_ch = ed.ch;
       e_next = ed.next;
-      if (is_last_edit) e_sb = P.sb_bits[e_next & EDGE_NEXT_MASK];
+      if (is_last_edit) e_sb = P.sb_edge[nd.edge_begin + lane];
     }
     auto sb_bit = [](uint4 m, uint32_t ch) -> bool {  // branch-free word select (no stack indexing)
       const uint32_t lo = (ch & 32u) ? m.y : m.x;
@@ -687,15 +687,11 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
       const uint32_t e = e0 + i;
       const bool ok = valid && e < o_deg;
       const DevEdge ed = P.edges[ok ? o_eb + e : 0u];
-      const uint32_t child = ed.next & EDGE_NEXT_MASK;
       const bool child_out = (ed.next & EDGE_CHILD_OUTPUT) != 0;
-      const uint4 csb = P.sb_bits[(ok && need_csb && !child_out) ? child : 0u];
+      const uint4 csb = P.sb_edge[(ok && need_csb) ? o_eb + e : 0u];  // parallel with the edge load
       fe = (ok && ex_on && fe == 0xFFFFu && ed.ch == cur) ? e : fe;
       fx = (ok && swap_ok && fx == 0xFFFFu && ed.ch == nc) ? e : fx;
-      const bool asc = ed.ch < 128u && cur < 128u;
-      const float tv = P.sim_ascii[asc ? ed.ch * 128u + cur : 0u];
-      float sim = ed.ch == cur ? 1.0f : (asc ? tv : 0.0f);
-      if (P.n_sim != 0 && !asc && ed.ch != cur) sim = similarity(P, ed.ch, cur);
+      const float sim = similarity(P, ed.ch, cur);
       const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
       const bool sb_next = child_out || (have_next && sb_word_bit(csb, nxt));
       const bool sb_cur = child_out || (have_cur && sb_word_bit(csb, cur));
@@ -869,7 +865,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
                            uint32_t& cseq, EmitList& EL, uint64_t start, uint64_t& popped, unsigned& err) {
   const uint32_t lane = lane_id();
 #ifdef FAC_PHASE_PROF
-  uint64_t prof_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t prof_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   PROF_T(t_win);
   if constexpr (VCAP > 0)
@@ -925,11 +921,17 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     LaneExp x{-1, -1, false, 0ull, 0ull, 0u};
     const bool act = alive && lane < Bc;
     Prep pr{0u, 0u, 0u, 0u, 0.0f};
+    PROF_T(tb0);
     if (act) pr = lane_prep(P, S, st, nd, start, err);
+    PROF_ACC(9, tb0);
+    PROF_T(tb1);
     uint64_t msub = 0, mdel = 0;
     uint32_t ex = 0xFFFFu, xe = 0xFFFFu;
     expand_units<FAC_UK>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act, msub, mdel, ex, xe);
+    PROF_ACC(10, tb1);
+    PROF_T(tb2);
     if (act) x = lane_finish(P, st, nd, pr, msub, mdel, ex, xe);
+    PROF_ACC(11, tb2);
     const uint32_t cnt = (lane < Bc) ? x.count : 0u;
     const uint32_t incl = wave_inclusive_sum(cnt);
     const uint32_t excl = incl - cnt;
@@ -1072,7 +1074,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
 #ifdef FAC_PHASE_PROF
   PROF_ACC(7, t_win);
   if (lane == 0)
-    for (int i = 0; i < 9; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof_acc[i]);
+    for (int i = 0; i < 12; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof_acc[i]);
 #endif
 }
 
@@ -1382,6 +1384,7 @@ int upload_engine(Engine& e, std::string& err) {
   if ((rc = upload(e.edges, &e.d_edges, err))) return rc;
   if ((rc = upload(e.out_pat, &e.d_out_pat, err))) return rc;
   if ((rc = upload(e.sb_bits, &e.d_sb, err))) return rc;
+  if ((rc = upload(e.sb_edge, &e.d_sb_edge, err))) return rc;
   if ((rc = upload(e.pats, &e.d_pats, err))) return rc;
   if ((rc = upload(e.sim_ascii, &e.d_sim_ascii, err))) return rc;
   if ((rc = upload(e.sim_keys, &e.d_sim_keys, err))) return rc;
@@ -1405,7 +1408,7 @@ int upload_engine(Engine& e, std::string& err) {
 void free_engine_device(Engine& e) {
   if (e.d_nodes == nullptr && e.stream == nullptr) return;
   (void)hipSetDevice(e.device);
-  void* ptrs[] = {e.d_nodes, e.d_edges, e.d_out_pat, e.d_sb, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
+  void* ptrs[] = {e.d_nodes, e.d_edges, e.d_out_pat, e.d_sb, e.d_sb_edge, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
                   e.d_sim_vals, e.d_bp_mask, e.d_ascii_id};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -1495,6 +1498,7 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
   P.edges = e.d_edges;
   P.out_pat = e.d_out_pat;
   P.sb_bits = e.d_sb;
+  P.sb_edge = e.d_sb_edge;
   P.pats = e.d_pats;
   P.sim_ascii = e.d_sim_ascii;
   P.sim_keys = e.d_sim_keys;
@@ -1622,8 +1626,9 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
       unsigned long long pr[16];
       HIP_TRY(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_prof), sizeof(pr)));
       std::fprintf(stderr, "FAC_PROF variant=%u,%u beam_select=%llu phaseA=%llu wide=%llu phaseB=%llu phaseC=%llu "
-                   "emit=%llu push=%llu window_total=%llu batches=%llu popped=%llu\n", kVariants[vi].vcap,
-                   kVariants[vi].qcap, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], pr[8], cnt[1]);
+                   "emit=%llu push=%llu window_total=%llu batches=%llu popped=%llu [B: prep=%llu units=%llu finish=%llu]\n",
+                   kVariants[vi].vcap, kVariants[vi].qcap, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], pr[8],
+                   cnt[1], pr[9], pr[10], pr[11]);
       std::memset(pr, 0, sizeof(pr));
       HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), pr, sizeof(pr)));
     }
