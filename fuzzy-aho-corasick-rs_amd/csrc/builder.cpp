@@ -160,7 +160,7 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
     output[cur].push_back((uint32_t)i);
   }
   const size_t nn = kids.size();
-  if (nn >= (size_t)EDGE_NEXT_MASK) { err = "automaton too large"; return FAC_E_UNSUPPORTED; }
+  if (nn > (size_t)CHILD26_MASK) { err = "automaton too large (more than 2^26 nodes)"; return FAC_E_UNSUPPORTED; }
 
   // ---- fail links, used only to merge outputs (builder.rs:239-276); BFS by depth
   {

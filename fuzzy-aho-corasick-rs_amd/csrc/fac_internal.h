@@ -37,6 +37,7 @@ uint32_t fold_first_char(const uint8_t* s, uint64_t b, uint64_t e, bool ci);
 constexpr uint32_t EDGE_SINGLE_BYTE = 1u << 31;
 constexpr uint32_t EDGE_CHILD_OUTPUT = 1u << 30;
 constexpr uint32_t EDGE_NEXT_MASK = (1u << 30) - 1;
+constexpr uint32_t CHILD26_MASK = (1u << 26) - 1;  // node ids are < 2^26 (builder limit)
 constexpr int32_t LIM_NONE = -1;
 
 struct alignas(16) DevNode {

@@ -558,7 +558,7 @@ constexpr uint32_t PF_SUB = 1u, PF_DEL = 2u, PF_LAST = 4u, PF_CSB = 8u, PF_NEXT 
                    PF_EX = 128u, PF_INS = 256u;
 
 __device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState& st, const DevNode& nd, uint64_t start,
-                          unsigned& err) {
+                          uint32_t c0, uint32_t c1, uint4 own_sb) {  // c0/c1: text at j / j + 1 (0 past the end)
   Prep r{0u, 0u, 0u, 0u, 0.0f};
   const bool fast = P.mef != 255u;
   const uint64_t n = S.n;
@@ -570,11 +570,11 @@ __device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState&
   const int32_t nlim = P.has_pattern_limits ? node_limits(P, st.node) : -1;
   const bool is_last_edit = fast && edits + 1u >= P.mef;  // :742
   const bool in_text = j < n;
-  r.cur_ch = in_text ? text_char(P, S, j, err) : 0u;
+  r.cur_ch = in_text ? c0 : 0u;
   bool have_next = false;
   if (in_text && is_last_edit && (!fast || edits < P.mef) && j + 1 < n) {  // :758-765
     have_next = true;
-    r.next_ch = text_char(P, S, j + 1, err);
+    r.next_ch = c1;
   }
   bool subst_ok = false, swap_ok = false, ins_ok = false, del_ok = false;
   if (in_text) {
@@ -586,7 +586,7 @@ __device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState&
                        : (edits == 0 && ((packed >> 16) & 0xFFu) == 0);
     }
     swap_ok = j + 1 < n && P.p_swp <= r.remaining && (!fast || edits < P.mef);  // :935-937
-    if (swap_ok) r.nch = have_next ? r.next_ch : text_char(P, S, j + 1, err);
+    if (swap_ok) r.nch = c1;
     if ((me_rel != 0u || j_rel != 0u) && P.p_ins <= r.remaining) {  // :994-1007
       if (fast) {
         ins_ok = edits < P.mef;
@@ -594,10 +594,7 @@ __device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState&
         const Lim m = pick_limits(P, nlim);
         ins_ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.ins, packed & 0xFFu)) : false;
       }
-      if (ins_ok && is_last_edit && nd.out_begin == nd.out_end) {
-        const uint4 own = P.sb_bits[st.node];
-        ins_ok = have_next && sb_word_bit(own, r.next_ch);
-      }
+      if (ins_ok && is_last_edit && nd.out_begin == nd.out_end) ins_ok = have_next && sb_word_bit(own_sb, r.next_ch);
     }
   }
   if (P.p_del <= r.remaining) {  // :1035-1045
@@ -632,7 +629,7 @@ __device__ __forceinline__ uint32_t wave_inclusive_max(uint32_t v) {
 struct ExpScratch {
   unsigned long long msub[64];
   unsigned long long mdel[64];
-  uint32_t exx[128];  // [2s] = 0xFFFF - first exact edge (0: none), [2s+1] = same for the swap edge
+  uint32_t exx[128];  // [2s]: (63 - first exact edge) << 26 | its child (0: none); [2s+1]: same, swap edge
   uint32_t mark[64];  // unit -> owner state lane + 1 (per round)
 };
 static_assert(sizeof(ExpScratch) <= 4u * 512u, "scratch must fit the smallest claim region");
@@ -681,7 +678,7 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
     const uint32_t o_deg = (o_pk >> 9) & 0x7Fu, e0 = (R + lane - (o_pk >> 16)) * UK;
     const bool sub_on = o_pk & PF_SUB, del_ok = o_pk & PF_DEL, is_last = o_pk & PF_LAST, need_csb = o_pk & PF_CSB;
     const bool have_next = o_pk & PF_NEXT, have_cur = o_pk & PF_CUR, swap_ok = o_pk & PF_SWAP, ex_on = o_pk & PF_EX;
-    uint32_t sb = 0, db = 0, fe = 0xFFFFu, fx = 0xFFFFu;
+    uint32_t sb = 0, db = 0, fe = 0u, fx = 0u;  // fe/fx: exx encodings of the unit's first matches
 #pragma unroll
     for (uint32_t i = 0; i < UK; ++i) {
       const uint32_t e = e0 + i;
@@ -689,8 +686,9 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
       const DevEdge ed = P.edges[ok ? o_eb + e : 0u];
       const bool child_out = (ed.next & EDGE_CHILD_OUTPUT) != 0;
       const uint4 csb = P.sb_edge[(ok && need_csb) ? o_eb + e : 0u];  // parallel with the edge load
-      fe = (ok && ex_on && fe == 0xFFFFu && ed.ch == cur) ? e : fe;
-      fx = (ok && swap_ok && fx == 0xFFFFu && ed.ch == nc) ? e : fx;
+      const uint32_t enc = ((63u - e) << 26) | (ed.next & CHILD26_MASK);  // child ids < 2^26 (builder)
+      fe = (ok && ex_on && fe == 0u && ed.ch == cur) ? enc : fe;
+      fx = (ok && swap_ok && fx == 0u && ed.ch == nc) ? enc : fx;
       const float sim = similarity(P, ed.ch, cur);
       const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
       const bool sb_next = child_out || (have_next && sb_word_bit(csb, nxt));
@@ -703,15 +701,15 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
     }
     if (sb) atomicOr(&X->msub[o], (unsigned long long)sb << e0);
     if (db) atomicOr(&X->mdel[o], (unsigned long long)db << e0);
-    if (fe != 0xFFFFu) atomicMax(&X->exx[2 * o], 0xFFFFu - fe);
-    if (fx != 0xFFFFu) atomicMax(&X->exx[2 * o + 1], 0xFFFFu - fx);
+    if (fe) atomicMax(&X->exx[2 * o], fe);  // max = smallest edge index
+    if (fx) atomicMax(&X->exx[2 * o + 1], fx);
   }
   __builtin_amdgcn_wave_barrier();
   msub = X->msub[lane];
   mdel = X->mdel[lane];
   const uint2 exw = reinterpret_cast<const uint2*>(X->exx)[lane];
-  ex = exw.x ? 0xFFFFu - exw.x : 0xFFFFu;
-  xe = exw.y ? 0xFFFFu - exw.y : 0xFFFFu;
+  ex = exw.x;
+  xe = exw.y;
   __builtin_amdgcn_wave_barrier();
   X->msub[lane] = 0ull;
   X->mdel[lane] = 0ull;
@@ -724,12 +722,12 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
 __device__ LaneExp lane_finish(const SearchParams& P, const KState& st, const DevNode& nd, const Prep& pr,
                                uint64_t msub, uint64_t mdel, uint32_t ex, uint32_t xe) {
   LaneExp x{-1, -1, false, msub, mdel, 0u};
-  if (ex != 0xFFFFu) {
-    x.exact = (int64_t)(P.edges[nd.edge_begin + ex].next & EDGE_NEXT_MASK);
-    x.msub &= ~(1ull << ex);
+  if (ex) {  // exx encodings (expand_units)
+    x.exact = (int64_t)(ex & CHILD26_MASK);
+    x.msub &= ~(1ull << (63u - (ex >> 26)));
   }
-  if (xe != 0xFFFFu) {
-    const DevNode xn = P.nodes[P.edges[nd.edge_begin + xe].next & EDGE_NEXT_MASK];
+  if (xe) {
+    const DevNode xn = P.nodes[xe & CHILD26_MASK];
     for (uint32_t e = xn.edge_begin; e < xn.edge_end; ++e) {
       const DevEdge ed = P.edges[e];
       if (ed.ch == pr.cur_ch) {
@@ -886,18 +884,26 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     const bool in_b = lane < B;
     KState st{EMPTY, 0u, 0.0f, 0u};
     if (in_b) st = q[(head + lane) & (QCAP - 1)];
-    // ---- phase A: dedup (read-only), node ceiling, width
+    // ---- phase A: the state's global reads go out first (node record, own single-byte map,
+    // text at j and j + 1) and overlap the dedup probe; then dedup, node ceiling, width
+    DevNode nd{};
+    uint4 own_sb = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t c0 = 0, c1 = 0;
+    if (in_b) {
+      nd = P.nodes[st.node];
+      own_sb = P.sb_bits[st.node];
+      const uint64_t j = start + (st.jm & 0xFFFFu);
+      if (j < S.n) c0 = text_char(P, S, j, err);
+      if (j + 1 < S.n) c1 = text_char(P, S, j + 1, err);
+    }
     bool found = false;
     uint32_t stored_bits = 0, vslot = EMPTY;
     if constexpr (VCAP > 0)  // VCAP == 0: no dedup (unbeamed only)
       if (in_b) vis_lookup<VCAP>(vis, st, found, stored_bits, vslot);
     const bool skip = in_b && found && __uint_as_float(stored_bits) <= st.pen;  // :620
-    DevNode nd{};
-    bool alive = false;
-    if (in_b && !skip) {
-      nd = P.nodes[st.node];
-      alive = !(st.pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr)));  // :638-642
-    }
+    const bool alive =
+        in_b && !skip && !(st.pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr)));  // :638-642
+    if (!alive) nd = DevNode{};
     const bool wide = alive && (nd.edge_end - nd.edge_begin) > 64u;
     const uint64_t mwide = __ballot(wide);
     PROF_ACC(1, t1);
@@ -922,11 +928,11 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     const bool act = alive && lane < Bc;
     Prep pr{0u, 0u, 0u, 0u, 0.0f};
     PROF_T(tb0);
-    if (act) pr = lane_prep(P, S, st, nd, start, err);
+    if (act) pr = lane_prep(P, S, st, nd, start, c0, c1, own_sb);
     PROF_ACC(9, tb0);
     PROF_T(tb1);
     uint64_t msub = 0, mdel = 0;
-    uint32_t ex = 0xFFFFu, xe = 0xFFFFu;
+    uint32_t ex = 0u, xe = 0u;
     expand_units<FAC_UK>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act, msub, mdel, ex, xe);
     PROF_ACC(10, tb1);
     PROF_T(tb2);
