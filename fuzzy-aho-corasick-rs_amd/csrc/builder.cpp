@@ -211,14 +211,14 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
   e.mef = (e.max_edits_fast >= 1 && e.max_edits_fast <= 6) ? e.max_edits_fast : 255;
 
   // ---- flat tables
-  e.nodes.assign(nn, DevNode{});
+  e.nodes.assign(nn, HostNode{});
   e.edges.clear();
   e.out_pat.clear();
   e.sb_bits.assign(nn, uint4{0, 0, 0, 0});
   e.max_degree = 0;
   e.max_degree_nonroot = 0;
   for (size_t i = 0; i < nn; ++i) {
-    DevNode& d = e.nodes[i];
+    HostNode& d = e.nodes[i];
     d.edge_begin = (uint32_t)e.edges.size();
     for (auto& k : kids[i]) {
       const std::u32string& g = gstr[k.first];
@@ -237,7 +237,6 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
     for (uint32_t p : output[i]) e.out_pat.push_back(p);
     d.out_end = (uint32_t)e.out_pat.size();
     d.pidx = pidx[i];
-    d.pad = 0;
   }
   e.sb_edge.resize(e.edges.size());
   for (size_t k = 0; k < e.edges.size(); ++k) e.sb_edge[k] = e.sb_bits[e.edges[k].next & EDGE_NEXT_MASK];
@@ -259,6 +258,20 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
     float len = (float)rl[i];
     e.nodes[i].prune_len = len;
     e.nodes[i].prune_lw = len / rw[i];
+  }
+
+  // ---- device node records (fac_internal.h): 32 B per node + side tables
+  e.dnodes.resize(nn);
+  e.out_range.resize(nn);
+  e.node_pidx.resize(nn);
+  for (size_t i = 0; i < nn; ++i) {
+    const HostNode& h = e.nodes[i];
+    const uint32_t deg = h.edge_end - h.edge_begin;
+    if (deg > NODE_DEG_MASK) { err = "node degree too large"; return FAC_E_UNSUPPORTED; }
+    e.dnodes[i] = DevNode{h.prune_len, h.prune_lw, h.edge_begin, deg | (h.out_end != h.out_begin ? NODE_HAS_OUT : 0u),
+                          e.sb_bits[i]};
+    e.out_range[i] = uint2{h.out_begin, h.out_end};
+    e.node_pidx[i] = h.pidx;
   }
 
   // ---- similarity (structs.rs:30-54)

@@ -4,9 +4,10 @@
 // hash map (structs.rs:249-281). On MI355X the automaton is flattened into structure-of-arrays
 // tables that stay L2-resident (≈1-5 MB at 10K patterns) and are read with wave-uniform loads:
 //
-//   DevNode[N]   32 B  prune_len, prune_len_over_weight, edge range, output range, pattern_index
+//   DevNode[N]   32 B  prune_len, prune_len_over_weight, edge_begin, degree | has-output, and the
+//                      node's single-ASCII-byte edge map (structs.rs:471-493): one load per pop
+//   out_range[N]  8 B  output range (read on emission only); node_pidx[N] 4 B pattern_index
 //   DevEdge[E]    8 B  first code point | target node + (child-has-output, single-byte) flag bits
-//   sb_bits[N]   16 B  128-bit map of the node's single-ASCII-byte edge chars (structs.rs:471-493)
 //   sb_edge[E]   16 B  sb_bits of each edge's child (one parent edge per node: loads in parallel
 //                      with the edge record instead of after it)
 //   out_pat[O]    4 B  output pattern ids (own + fail-merged, builder.rs:235,264-268)
@@ -40,13 +41,24 @@ constexpr uint32_t EDGE_NEXT_MASK = (1u << 30) - 1;
 constexpr uint32_t CHILD26_MASK = (1u << 26) - 1;  // node ids are < 2^26 (builder limit)
 constexpr int32_t LIM_NONE = -1;
 
-struct alignas(16) DevNode {
+// host-side node (builder, host bookkeeping)
+struct HostNode {
   float prune_len;
   float prune_lw;
   uint32_t edge_begin, edge_end;
   uint32_t out_begin, out_end;
   int32_t pidx;  // pattern_index (first pattern touching the node), -1 = None
-  uint32_t pad;
+};
+
+// device node: one 32 B load gives everything a pop needs
+constexpr uint32_t NODE_HAS_OUT = 1u << 31;
+constexpr uint32_t NODE_DEG_MASK = (1u << 24) - 1;
+struct alignas(16) DevNode {
+  float prune_len;
+  float prune_lw;
+  uint32_t edge_begin;
+  uint32_t degf;  // degree | NODE_HAS_OUT
+  uint4 sb;       // 128-bit map of the node's single-ASCII-byte edge chars (structs.rs:471-493)
 };
 static_assert(sizeof(DevNode) == 32, "DevNode layout");
 
@@ -95,7 +107,8 @@ struct SearchParams {
   const DevNode* nodes;
   const DevEdge* edges;
   const uint32_t* out_pat;
-  const uint4* sb_bits;
+  const uint2* out_range;
+  const int32_t* node_pidx;
   const uint4* sb_edge;
   const DevPattern* pats;
   const float* sim_ascii;
@@ -154,7 +167,10 @@ struct Engine {
   uint64_t ab_budget = 0, ab_width = 0;
   float p_ins, p_del, p_sub, p_swp, min_sym;
   // host tables
-  std::vector<DevNode> nodes;
+  std::vector<HostNode> nodes;
+  std::vector<DevNode> dnodes;
+  std::vector<uint2> out_range;
+  std::vector<int32_t> node_pidx;
   std::vector<DevEdge> edges;
   std::vector<uint32_t> out_pat;
   std::vector<uint4> sb_bits;
@@ -183,7 +199,8 @@ struct Engine {
   DevNode* d_nodes = nullptr;
   DevEdge* d_edges = nullptr;
   uint32_t* d_out_pat = nullptr;
-  uint4* d_sb = nullptr;
+  uint2* d_out_range = nullptr;
+  int32_t* d_pidx = nullptr;
   uint4* d_sb_edge = nullptr;
   DevPattern* d_pats = nullptr;
   float* d_sim_ascii = nullptr;

@@ -105,7 +105,7 @@ __device__ __forceinline__ Lim pick_limits(const SearchParams& P, int32_t pi) {
 
 // get_node_limits (search.rs:67-71): the node's pattern, if that pattern has its own limits
 __device__ __forceinline__ int32_t node_limits(const SearchParams& P, uint32_t node) {
-  const int32_t pi = P.nodes[node].pidx;
+  const int32_t pi = P.node_pidx[node];
   if (pi < 0) return -1;
   return P.pats[pi].has_limits ? pi : -1;
 }
@@ -148,9 +148,13 @@ __device__ __forceinline__ uint64_t local_byte(const SearchParams& P, const SegD
 // has_matching_edge_char (structs.rs:471-475) via the node's single-byte edge bitmap
 __device__ __forceinline__ bool sb_has(const SearchParams& P, uint32_t node, uint32_t ch) {
   if (ch >= 128u) return false;
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(P.sb_bits);
-  return (w[node * 4u + (ch >> 5)] >> (ch & 31u)) & 1u;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&P.nodes[node].sb);
+  return (w[ch >> 5] >> (ch & 31u)) & 1u;
 }
+
+__device__ __forceinline__ uint32_t node_deg(const DevNode& n) { return n.degf & NODE_DEG_MASK; }
+__device__ __forceinline__ uint32_t node_end(const DevNode& n) { return n.edge_begin + (n.degf & NODE_DEG_MASK); }
+__device__ __forceinline__ bool node_has_out(const DevNode& n) { return (n.degf & NODE_HAS_OUT) != 0; }
 
 // find_transition_char_no_mappings (structs.rs:512-519): first edge whose first char is `ch`
 __device__ __forceinline__ int64_t goto_char(const SearchParams& P, uint32_t eb, uint32_t ee, uint32_t ch) {
@@ -319,7 +323,9 @@ __device__ __forceinline__ bool visited_check(KState* vis, uint32_t& vcount, con
 // Emission (search.rs:659-737) for one accepted state; lanes spread over the node's output list.
 // Called in FIFO pop order, so the per-window best list keeps the reference's first-found ties.
 __device__ void emit_state(const SearchParams& P, EmitList& EL, uint32_t me_rel, float pen, uint32_t packed,
-                           uint32_t out_begin, uint32_t out_end, unsigned& err) {
+                           uint32_t node, unsigned& err) {
+  const uint2 orr = P.out_range[node];
+  const uint32_t out_begin = orr.x, out_end = orr.y;
   const uint32_t lane = lane_id();
   const bool fast = P.mef != 255u;
   const uint32_t edits = edits_of(packed);
@@ -375,7 +381,7 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
     const uint32_t cur_ch = j < n ? text_char(P, S, j, err) : 0u;
     // Nodes with <= 64 edges (all but the top trie levels) are handled from one register-resident
     // chunk: lane l holds edge l and, at the last edit level, its child's single-byte edge map.
-    const uint32_t deg = nd.edge_end - nd.edge_begin;
+    const uint32_t deg = node_deg(nd);
     const bool small = deg <= 64u;
     uint32_t e_ch = 0, e_next = 0;
     uint4 e_sb = make_uint4(0, 0, 0, 0);
@@ -404,7 +410,7 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
         next_ch = text_char(P, S, j + 1, err);
       }
       // exact transition (:766-798); matched_start stays `start` for every state
-      const int64_t exact_next = small ? small_goto(cur_ch) : goto_char(P, nd.edge_begin, nd.edge_end, cur_ch);
+      const int64_t exact_next = small ? small_goto(cur_ch) : goto_char(P, nd.edge_begin, node_end(nd), cur_ch);
       const uint32_t jm1 = (j_rel + 1u) | ((j_rel + 1u) << 16);
       push_lanes<QCAP>(q, head, tail, lane == 0 && exact_next >= 0,
                        KState{(uint32_t)exact_next, jm1, pen, packed}, err);
@@ -419,7 +425,7 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
                          : (edits == 0 && ((packed >> 16) & 0xFFu) == 0);
       }
       if (subst_ok) {
-        for (uint32_t base = nd.edge_begin; base < nd.edge_end; base += 64) {
+        for (uint32_t base = nd.edge_begin; base < node_end(nd); base += 64) {
           const uint32_t i = base + lane;
           bool keep;
           uint32_t ch, nx;
@@ -428,7 +434,7 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
             ch = e_ch;
             nx = e_next;
           } else {
-            keep = i < nd.edge_end;
+            keep = i < node_end(nd);
             const DevEdge ed = keep ? P.edges[i] : DevEdge{0, 0};
             ch = ed.ch;
             nx = ed.next;
@@ -453,10 +459,10 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
       // swap (:935-989)
       if (j + 1 < n && P.p_swp <= remaining && (!fast || edits < P.mef)) {
         const uint32_t nch = have_next ? next_ch : text_char(P, S, j + 1, err);
-        const int64_t x = small ? small_goto(nch) : goto_char(P, nd.edge_begin, nd.edge_end, nch);
+        const int64_t x = small ? small_goto(nch) : goto_char(P, nd.edge_begin, node_end(nd), nch);
         if (x >= 0) {
           const DevNode nx = P.nodes[(uint32_t)x];
-          const int64_t node2 = goto_char(P, nx.edge_begin, nx.edge_end, cur_ch);
+          const int64_t node2 = goto_char(P, nx.edge_begin, node_end(nx), cur_ch);
           bool ok = node2 >= 0;
           if (ok && !fast) {  // within_limits_swap_ahead with node2's limits (:962-967)
             const Lim m = pick_limits(P, node_limits(P, (uint32_t)node2));
@@ -477,7 +483,7 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
           const Lim m = pick_limits(P, nlim);
           ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.ins, packed & 0xFFu)) : false;
         }
-        if (ok && is_last_edit && nd.out_begin == nd.out_end && !(have_next && sb_has(P, st.node, next_ch)))
+        if (ok && is_last_edit && !node_has_out(nd) && !(have_next && sb_has(P, st.node, next_ch)))
           ok = false;
         const uint32_t jmi = (j_rel + 1u) | (me_rel << 16);
         push_lanes<QCAP>(q, head, tail, lane == 0 && ok, KState{st.node, jmi, __fadd_rn(pen, P.p_ins), packed + 1u},
@@ -497,7 +503,7 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
       if (ok) {
         const bool have_cur = is_last_edit && j < n;
         const float npen = __fadd_rn(pen, P.p_del);
-        for (uint32_t base = nd.edge_begin; base < nd.edge_end; base += 64) {
+        for (uint32_t base = nd.edge_begin; base < node_end(nd); base += 64) {
           const uint32_t i = base + lane;
           bool keep;
           uint32_t nx;
@@ -505,7 +511,7 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
             keep = e_valid;
             nx = e_next;
           } else {
-            keep = i < nd.edge_end;
+            keep = i < node_end(nd);
             nx = keep ? P.edges[i].next : 0u;
           }
           const uint32_t child = nx & EDGE_NEXT_MASK;
@@ -594,7 +600,7 @@ __device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState&
         const Lim m = pick_limits(P, nlim);
         ins_ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.ins, packed & 0xFFu)) : false;
       }
-      if (ins_ok && is_last_edit && nd.out_begin == nd.out_end) ins_ok = have_next && sb_word_bit(own_sb, r.next_ch);
+      if (ins_ok && is_last_edit && !node_has_out(nd)) ins_ok = have_next && sb_word_bit(own_sb, r.next_ch);
     }
   }
   if (P.p_del <= r.remaining) {  // :1035-1045
@@ -606,7 +612,12 @@ __device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState&
     }
   }
   r.flags = (in_text && subst_ok ? PF_SUB : 0u) | (del_ok ? PF_DEL : 0u) | (is_last_edit ? PF_LAST : 0u) |
-            (is_last_edit && (subst_ok || del_ok) ? PF_CSB : 0u) | (have_next ? PF_NEXT : 0u) |
+            // the child's map is only read when the tested char is ASCII (a bit test on >= 128 is false)
+            (is_last_edit && ((in_text && subst_ok && have_next && r.next_ch < 128u) ||
+                              (del_ok && in_text && r.cur_ch < 128u))
+                 ? PF_CSB
+                 : 0u) |
+            (have_next ? PF_NEXT : 0u) |
             (is_last_edit && in_text ? PF_CUR : 0u) | (swap_ok ? PF_SWAP : 0u) | (in_text ? PF_EX : 0u) |
             (ins_ok ? PF_INS : 0u);
   return r;
@@ -658,7 +669,7 @@ template <uint32_t UK>
 __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode& nd, const Prep& pr, bool act,
                              uint64_t& msub, uint64_t& mdel, uint32_t& ex, uint32_t& xe) {
   const uint32_t lane = lane_id();
-  const uint32_t deg = act ? nd.edge_end - nd.edge_begin : 0u;
+  const uint32_t deg = act ? node_deg(nd) : 0u;
   const uint32_t nunit = (deg + UK - 1) / UK;
   const uint32_t uincl = wave_inclusive_sum(nunit);
   const uint32_t ubase = uincl - nunit;
@@ -728,7 +739,7 @@ __device__ LaneExp lane_finish(const SearchParams& P, const KState& st, const De
   }
   if (xe) {
     const DevNode xn = P.nodes[xe & CHILD26_MASK];
-    for (uint32_t e = xn.edge_begin; e < xn.edge_end; ++e) {
+    for (uint32_t e = xn.edge_begin; e < node_end(xn); ++e) {
       const DevEdge ed = P.edges[e];
       if (ed.ch == pr.cur_ch) {
         x.swap = ed.next & EDGE_NEXT_MASK;
@@ -887,11 +898,9 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     // ---- phase A: the state's global reads go out first (node record, own single-byte map,
     // text at j and j + 1) and overlap the dedup probe; then dedup, node ceiling, width
     DevNode nd{};
-    uint4 own_sb = make_uint4(0u, 0u, 0u, 0u);
     uint32_t c0 = 0, c1 = 0;
     if (in_b) {
       nd = P.nodes[st.node];
-      own_sb = P.sb_bits[st.node];
       const uint64_t j = start + (st.jm & 0xFFFFu);
       if (j < S.n) c0 = text_char(P, S, j, err);
       if (j + 1 < S.n) c1 = text_char(P, S, j + 1, err);
@@ -904,7 +913,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     const bool alive =
         in_b && !skip && !(st.pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr)));  // :638-642
     if (!alive) nd = DevNode{};
-    const bool wide = alive && (nd.edge_end - nd.edge_begin) > 64u;
+    const bool wide = alive && node_deg(nd) > 64u;
     const uint64_t mwide = __ballot(wide);
     PROF_ACC(1, t1);
     if (mwide & 1ull) {  // first state alone, edge-parallel
@@ -915,7 +924,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
       if constexpr (VCAP > 0)
         if (visited_check<VCAP>(vis, vcount, s0, P.beam != 0, err)) continue;
       const DevNode n0 = P.nodes[s0.node];
-      if (n0.out_begin != n0.out_end) emit_state(P, EL, s0.jm >> 16, s0.pen, s0.packed, n0.out_begin, n0.out_end, err);
+      if (node_has_out(n0)) emit_state(P, EL, s0.jm >> 16, s0.pen, s0.packed, s0.node, err);
       expand_wide<QCAP>(P, S, q, head, tail, s0, n0, start, err);
       PROF_ACC(2, t2);
       if (any_err(err)) break;
@@ -928,7 +937,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     const bool act = alive && lane < Bc;
     Prep pr{0u, 0u, 0u, 0u, 0.0f};
     PROF_T(tb0);
-    if (act) pr = lane_prep(P, S, st, nd, start, c0, c1, own_sb);
+    if (act) pr = lane_prep(P, S, st, nd, start, c0, c1, nd.sb);
     PROF_ACC(9, tb0);
     PROF_T(tb1);
     uint64_t msub = 0, mdel = 0;
@@ -1028,12 +1037,12 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     PROF_ACC(4, t4);
     PROF_T(t5);
     // ---- phase D: emissions (FIFO order), then pushes at tail + exclusive prefix
-    uint64_t mem = __ballot(alive && lane < Bc && nd.out_begin != nd.out_end);
+    uint64_t mem = __ballot(alive && lane < Bc && node_has_out(nd));
     while (mem) {
       const int l = first_lane(mem);
       mem &= mem - 1;
-      emit_state(P, EL, shfl_u32(st.jm, l) >> 16, shfl_f32(st.pen, l), shfl_u32(st.packed, l),
-                 shfl_u32(nd.out_begin, l), shfl_u32(nd.out_end, l), err);
+      emit_state(P, EL, shfl_u32(st.jm, l) >> 16, shfl_f32(st.pen, l), shfl_u32(st.packed, l), shfl_u32(st.node, l),
+                 err);
     }
     PROF_ACC(5, t5);
     PROF_T(t6);
@@ -1386,10 +1395,11 @@ int upload_engine(Engine& e, std::string& err) {
   HIP_TRY(hipSetDevice(e.device));
   if (!e.stream) HIP_TRY(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
   int rc;
-  if ((rc = upload(e.nodes, &e.d_nodes, err))) return rc;
+  if ((rc = upload(e.dnodes, &e.d_nodes, err))) return rc;
+  if ((rc = upload(e.out_range, &e.d_out_range, err))) return rc;
+  if ((rc = upload(e.node_pidx, &e.d_pidx, err))) return rc;
   if ((rc = upload(e.edges, &e.d_edges, err))) return rc;
   if ((rc = upload(e.out_pat, &e.d_out_pat, err))) return rc;
-  if ((rc = upload(e.sb_bits, &e.d_sb, err))) return rc;
   if ((rc = upload(e.sb_edge, &e.d_sb_edge, err))) return rc;
   if ((rc = upload(e.pats, &e.d_pats, err))) return rc;
   if ((rc = upload(e.sim_ascii, &e.d_sim_ascii, err))) return rc;
@@ -1414,7 +1424,7 @@ int upload_engine(Engine& e, std::string& err) {
 void free_engine_device(Engine& e) {
   if (e.d_nodes == nullptr && e.stream == nullptr) return;
   (void)hipSetDevice(e.device);
-  void* ptrs[] = {e.d_nodes, e.d_edges, e.d_out_pat, e.d_sb, e.d_sb_edge, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
+  void* ptrs[] = {e.d_nodes, e.d_out_range, e.d_pidx, e.d_edges, e.d_out_pat, e.d_sb_edge, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
                   e.d_sim_vals, e.d_bp_mask, e.d_ascii_id};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -1503,7 +1513,8 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
   P.nodes = e.d_nodes;
   P.edges = e.d_edges;
   P.out_pat = e.d_out_pat;
-  P.sb_bits = e.d_sb;
+  P.out_range = e.d_out_range;
+  P.node_pidx = e.d_pidx;
   P.sb_edge = e.d_sb_edge;
   P.pats = e.d_pats;
   P.sim_ascii = e.d_sim_ascii;
