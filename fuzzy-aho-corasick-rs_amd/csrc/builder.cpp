@@ -335,6 +335,62 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
     }
   }
 
+  // ---- O(1) expansion tables: (node, char) goto entries and child single-byte maps for nodes of
+  // degree <= 64, plus each node's child-has-output mask (used by the kernels' fast path)
+  {
+    e.cout.assign(nn, 0ull);
+    std::vector<std::pair<uint64_t, uint64_t>> ent;  // (kv, val)
+    std::unordered_map<uint64_t, size_t> at;         // kv -> index in ent
+    auto put = [&](uint64_t kv) -> uint64_t& {
+      auto it = at.find(kv);
+      if (it != at.end()) return ent[it->second].second;
+      at.emplace(kv, ent.size());
+      ent.push_back({kv, 0ull});
+      return ent.back().second;
+    };
+    for (size_t i = 0; i < nn; ++i) {
+      const HostNode& h = e.nodes[i];
+      const uint32_t deg = h.edge_end - h.edge_begin;
+      for (uint32_t k = 0; k < deg; ++k) {  // goto entries for every node (swap resolution)
+        const DevEdge& ed = e.edges[h.edge_begin + k];
+        const uint32_t child = ed.next & EDGE_NEXT_MASK;
+        const uint64_t key = ((uint64_t)i << 21) | ed.ch;
+        const bool existed = at.count(GT_VALID | GT_GOTO | key) != 0;
+        uint64_t& g = put(GT_VALID | GT_GOTO | key);
+        if (!existed) g = child | ((uint64_t)std::min<uint32_t>(k, 255) << 32);  // first edge, this first char
+        if (ed.next & EDGE_SINGLE_BYTE) g |= 1ull << 40;
+        if (deg > 64) continue;  // child maps only for the fast path's nodes
+        if (ed.next & EDGE_CHILD_OUTPUT) e.cout[i] |= 1ull << k;
+        const HostNode& c = e.nodes[child];
+        for (uint32_t m = c.edge_begin; m < c.edge_end; ++m) {
+          const DevEdge& ce = e.edges[m];
+          if ((ce.next & EDGE_SINGLE_BYTE) && ce.ch < 128) put(GT_VALID | GT_SB | ((uint64_t)i << 21) | ce.ch) |= 1ull << k;
+        }
+      }
+    }
+    uint32_t nb = 1;
+    while (nb * 2 < ent.size() + 1) nb <<= 1;  // <= 2 entries per 4-slot bucket on average
+    e.gt.assign((size_t)nb * 8, 0ull);
+    e.gt_mask = nb - 1;
+    for (auto& kvv : ent) {
+      uint32_t b = gt_hash(kvv.first, e.gt_mask);
+      for (;;) {
+        size_t t = 0;
+        while (t < 4 && e.gt[(size_t)b * 8 + t] != 0) ++t;
+        if (t < 4) {
+          e.gt[(size_t)b * 8 + t] = kvv.first;
+          e.gt[(size_t)b * 8 + 4 + t] = kvv.second;
+          break;
+        }
+        b = (b + 1) & e.gt_mask;
+      }
+    }
+    bool sims01 = true;  // every similarity in [0, 1]: p_sub * (1 - sim) in [0, p_sub]
+    for (float v : e.sim_ascii) sims01 = sims01 && v >= 0.0f && v <= 1.0f;
+    for (float v : e.sim_vals) sims01 = sims01 && v >= 0.0f && v <= 1.0f;
+    e.gt_fast = sims01 && e.min_sym <= 0.0f && e.p_sub >= 0.0f;
+  }
+
   // ---- bitap pre-filter tables (prefilter.rs:161-245)
   e.bitap_ok = false;
   do {

@@ -39,6 +39,15 @@ constexpr uint32_t EDGE_SINGLE_BYTE = 1u << 31;
 constexpr uint32_t EDGE_CHILD_OUTPUT = 1u << 30;
 constexpr uint32_t EDGE_NEXT_MASK = (1u << 30) - 1;
 constexpr uint32_t CHILD26_MASK = (1u << 26) - 1;  // node ids are < 2^26 (builder limit)
+
+// goto table entry: kv = GT_VALID | kind << 47 | node << 21 | char; val by kind:
+//   GT_GOTO: first edge of `node` whose first char is `char`: child | edge index << 32 | own-single-byte << 40
+//   GT_SB:   bit i = child of edge i has a single-byte edge labelled `char` (char < 128)
+constexpr uint64_t GT_VALID = 1ull << 63;
+constexpr uint64_t GT_GOTO = 0, GT_SB = 1ull << 47;
+__host__ __device__ inline uint32_t gt_hash(uint64_t kv, uint32_t mask) {
+  return (uint32_t)((kv * 0x9E3779B97F4A7C15ull) >> 40) & mask;
+}
 constexpr int32_t LIM_NONE = -1;
 
 // host-side node (builder, host bookkeeping)
@@ -109,6 +118,11 @@ struct SearchParams {
   const uint32_t* out_pat;
   const uint2* out_range;
   const int32_t* node_pidx;
+  // O(1) expansion tables (builder.cpp "goto table"): (node, char) -> first edge / child maps
+  const unsigned long long* gt;  // 64 B buckets: 4 keys, then their 4 values
+  uint32_t gt_mask;           // bucket count - 1
+  int32_t gt_fast;            // similarity can never drop a substitution when p_sub <= remaining
+  const unsigned long long* cout;  // per node: bit i = child of edge i has output (degree <= 64)
   const uint4* sb_edge;
   const DevPattern* pats;
   const float* sim_ascii;
@@ -175,6 +189,10 @@ struct Engine {
   std::vector<uint32_t> out_pat;
   std::vector<uint4> sb_bits;
   std::vector<uint4> sb_edge;
+  std::vector<unsigned long long> gt;  // goto table: per bucket 4 keys then 4 values
+  uint32_t gt_mask = 0;
+  bool gt_fast = false;
+  std::vector<unsigned long long> cout;
   std::vector<DevPattern> pats;
   std::vector<float> sim_ascii;
   std::vector<uint64_t> sim_keys;
@@ -202,6 +220,8 @@ struct Engine {
   uint2* d_out_range = nullptr;
   int32_t* d_pidx = nullptr;
   uint4* d_sb_edge = nullptr;
+  unsigned long long* d_gt = nullptr;
+  unsigned long long* d_cout = nullptr;
   DevPattern* d_pats = nullptr;
   float* d_sim_ascii = nullptr;
   uint64_t* d_sim_keys = nullptr;

@@ -156,6 +156,49 @@ __device__ __forceinline__ uint32_t node_deg(const DevNode& n) { return n.degf &
 __device__ __forceinline__ uint32_t node_end(const DevNode& n) { return n.edge_begin + (n.degf & NODE_DEG_MASK); }
 __device__ __forceinline__ bool node_has_out(const DevNode& n) { return (n.degf & NODE_HAS_OUT) != 0; }
 
+// goto-table lookups (fac_internal.h), two keys probed together: a probe reads one bucket's 4
+// keys (32 B), a hit then reads its value from the same 64 B line; absent keys end at an empty slot.
+__device__ __forceinline__ int gt_match(uint4 k01, uint4 k23, uint64_t kv, bool& empty) {
+  const uint32_t lo = (uint32_t)kv, hi = (uint32_t)(kv >> 32);
+  empty = (k01.x == 0u && k01.y == 0u) | (k01.z == 0u && k01.w == 0u) | (k23.x == 0u && k23.y == 0u) |
+          (k23.z == 0u && k23.w == 0u);
+  return (k01.x == lo && k01.y == hi) ? 0 : (k01.z == lo && k01.w == hi) ? 1 : (k23.x == lo && k23.y == hi) ? 2
+         : (k23.z == lo && k23.w == hi)                                    ? 3 : -1;
+}
+
+__device__ __forceinline__ void gt_find2(const SearchParams& P, uint64_t kva, bool la, uint64_t kvb, bool lb,
+                                         bool& ha, uint64_t& va, bool& hb, uint64_t& vb) {
+  uint32_t ba = gt_hash(kva, P.gt_mask), bb = gt_hash(kvb, P.gt_mask);
+  bool da = !la, db = !lb;
+  ha = hb = false;
+  uint32_t sa = 0, sb = 0;
+  while (!(da && db)) {
+    const uint4* pa = reinterpret_cast<const uint4*>(P.gt + (size_t)(da ? 0u : ba) * 8u);
+    const uint4* pb = reinterpret_cast<const uint4*>(P.gt + (size_t)(db ? 0u : bb) * 8u);
+    const uint4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+    bool ea, eb;
+    const int ta = gt_match(a0, a1, kva, ea), tb = gt_match(b0, b1, kvb, eb);
+    if (!da) {
+      if (ta >= 0) {
+        ha = true;
+        sa = ba * 8u + 4u + (uint32_t)ta;
+      }
+      da = ta >= 0 || ea;
+      ba = (ba + 1u) & P.gt_mask;
+    }
+    if (!db) {
+      if (tb >= 0) {
+        hb = true;
+        sb = bb * 8u + 4u + (uint32_t)tb;
+      }
+      db = tb >= 0 || eb;
+      bb = (bb + 1u) & P.gt_mask;
+    }
+  }
+  va = ha ? P.gt[sa] : 0ull;
+  vb = hb ? P.gt[sb] : 0ull;
+}
+
 // find_transition_char_no_mappings (structs.rs:512-519): first edge whose first char is `ch`
 __device__ __forceinline__ int64_t goto_char(const SearchParams& P, uint32_t eb, uint32_t ee, uint32_t ch) {
   const uint32_t lane = lane_id();
@@ -728,6 +771,35 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
   __builtin_amdgcn_wave_barrier();
 }
 
+// O(1) expansion of one state (deg <= 64) when similarity cannot drop a substitution
+// (gt_fast && p_sub <= remaining, see builder.cpp): every edge is a substitution and deletion
+// candidate, filtered at the last edit by "child has output" (cout) and "child has a single-byte
+// edge for the tested char" (GT_SB maps), exactly the per-edge tests of expand_units; the exact and
+// swap edges are the goto entries of text[j] and text[j+1].
+__device__ void expand_fast(const SearchParams& P, const KState& st, const DevNode& nd, const Prep& pr, uint64_t cout,
+                            uint64_t& msub, uint64_t& mdel, uint32_t& ex, uint32_t& xe) {
+  const uint32_t deg = node_deg(nd);
+  const uint64_t dm = deg >= 64u ? ~0ull : ((1ull << deg) - 1ull);
+  const bool is_last = pr.flags & PF_LAST, in_text = pr.flags & PF_EX, sub_on = pr.flags & PF_SUB;
+  const bool del_ok = pr.flags & PF_DEL, swap_ok = pr.flags & PF_SWAP;
+  const uint64_t nk = GT_VALID | ((uint64_t)st.node << 21);
+  bool h0, h1, hs0, hs1;
+  uint64_t g0, g1, s0, s1;
+  gt_find2(P, nk | GT_GOTO | pr.cur_ch, in_text, nk | GT_GOTO | pr.nch, swap_ok, h0, g0, h1, g1);
+  const bool ns0 = is_last && del_ok && (pr.flags & PF_CUR) && pr.cur_ch < 128u;
+  const bool ns1 = is_last && sub_on && (pr.flags & PF_NEXT) && pr.next_ch < 128u;
+  gt_find2(P, nk | GT_SB | pr.cur_ch, ns0, nk | GT_SB | pr.next_ch, ns1, hs0, s0, hs1, s1);
+  uint64_t exbit = 0;
+  if (h0) {
+    const uint32_t k = (uint32_t)(g0 >> 32) & 0xFFu;
+    ex = ((63u - k) << 26) | (uint32_t)(g0 & CHILD26_MASK);
+    exbit = 1ull << k;
+  }
+  if (h1) xe = ((63u - ((uint32_t)(g1 >> 32) & 0xFFu)) << 26) | (uint32_t)(g1 & CHILD26_MASK);
+  msub = sub_on ? (dm & ~exbit & (is_last ? (cout | s1) : ~0ull)) : 0ull;
+  mdel = del_ok ? (dm & (is_last ? (cout | s0) : ~0ull)) : 0ull;
+}
+
 // Per-state completion: exact successor, the exact edge leaves the substitution set, swap target
 // goto(goto(node, text[j+1]), text[j]) (:945-967), push count.
 __device__ LaneExp lane_finish(const SearchParams& P, const KState& st, const DevNode& nd, const Prep& pr,
@@ -737,15 +809,11 @@ __device__ LaneExp lane_finish(const SearchParams& P, const KState& st, const De
     x.exact = (int64_t)(ex & CHILD26_MASK);
     x.msub &= ~(1ull << (63u - (ex >> 26)));
   }
-  if (xe) {
-    const DevNode xn = P.nodes[xe & CHILD26_MASK];
-    for (uint32_t e = xn.edge_begin; e < node_end(xn); ++e) {
-      const DevEdge ed = P.edges[e];
-      if (ed.ch == pr.cur_ch) {
-        x.swap = ed.next & EDGE_NEXT_MASK;
-        break;
-      }
-    }
+  if (xe) {  // node2 = goto(xnode, text[j]) through the goto table
+    bool h, hu;
+    uint64_t g, gu;
+    gt_find2(P, GT_VALID | GT_GOTO | ((uint64_t)(xe & CHILD26_MASK) << 21) | pr.cur_ch, true, 0ull, false, h, g, hu, gu);
+    if (h) x.swap = (int64_t)(g & CHILD26_MASK);
     if (x.swap >= 0 && P.mef == 255u) {  // within_limits_swap_ahead with node2's limits (:962-967)
       const uint32_t packed = st.packed, edits = edits_of(packed);
       const Lim m = pick_limits(P, node_limits(P, (uint32_t)x.swap));
@@ -899,8 +967,10 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     // text at j and j + 1) and overlap the dedup probe; then dedup, node ceiling, width
     DevNode nd{};
     uint32_t c0 = 0, c1 = 0;
+    uint64_t cout = 0;
     if (in_b) {
       nd = P.nodes[st.node];
+      cout = P.cout[st.node];
       const uint64_t j = start + (st.jm & 0xFFFFu);
       if (j < S.n) c0 = text_char(P, S, j, err);
       if (j + 1 < S.n) c1 = text_char(P, S, j + 1, err);
@@ -942,7 +1012,10 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
     PROF_T(tb1);
     uint64_t msub = 0, mdel = 0;
     uint32_t ex = 0u, xe = 0u;
-    expand_units<FAC_UK>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act, msub, mdel, ex, xe);
+    const bool fast = act && P.gt_fast && (!(pr.flags & PF_SUB) || P.p_sub <= pr.remaining);
+    if (__ballot(act && !fast))  // per-edge path for the states similarity can prune
+      expand_units<FAC_UK>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act && !fast, msub, mdel, ex, xe);
+    if (fast) expand_fast(P, st, nd, pr, cout, msub, mdel, ex, xe);
     PROF_ACC(10, tb1);
     PROF_T(tb2);
     if (act) x = lane_finish(P, st, nd, pr, msub, mdel, ex, xe);
@@ -1116,7 +1189,7 @@ __device__ __forceinline__ uint32_t find_seg(const SearchParams& P, uint64_t v) 
 }
 
 template <uint32_t VCAP, uint32_t QCAP>
-__global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
+__device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   __shared__ KState s_vis[VCAP ? VCAP : 1];
   __shared__ KState s_q[QCAP];
   __shared__ __attribute__((aligned(16))) uint32_t s_claim[claim_slots(VCAP)];
@@ -1170,6 +1243,17 @@ __global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
   if (lane == 0) atomicAdd(P.counters + 1, (unsigned long long)popped);
   const unsigned all = wave_or(err);
   if (lane == 0 && all) atomicOr(reinterpret_cast<unsigned int*>(P.counters + 2), all);
+}
+
+// one wavefront per workgroup; the dedup-free variants are held to <= 128 VGPRs (4 waves/SIMD),
+// the dedup variants are bounded by LDS first
+template <uint32_t VCAP, uint32_t QCAP>
+__global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
+  bfs_window_body<VCAP, QCAP>(P);
+}
+template <uint32_t QCAP>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void bfs_window_kernel_nd(SearchParams P) {
+  bfs_window_body<0, QCAP>(P);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1324,6 +1408,11 @@ struct Variant {
   uint32_t vcap, qcap;  // vcap 0: no dedup table (unbeamed engines only)
 };
 
+template <uint32_t Q>
+void launch_nd(uint32_t grid, hipStream_t s, const SearchParams& P) {
+  hipLaunchKernelGGL((bfs_window_kernel_nd<Q>), dim3(grid), dim3(64), 0, s, P);
+}
+
 template <uint32_t V, uint32_t Q>
 void launch_one(uint32_t grid, hipStream_t s, const SearchParams& P) {
   hipLaunchKernelGGL((bfs_window_kernel<V, Q>), dim3(grid), dim3(64), 0, s, P);
@@ -1335,9 +1424,9 @@ constexpr Variant kVariants[] = {{0, 128},   {0, 256},    {0, 512},     {256, 25
 
 hipError_t launch_variant(const Variant& v, uint32_t grid, hipStream_t s, const SearchParams& P) {
   switch (v.vcap * 4096u + v.qcap) {
-    case 0 * 4096u + 128: launch_one<0, 128>(grid, s, P); break;
-    case 0 * 4096u + 256: launch_one<0, 256>(grid, s, P); break;
-    case 0 * 4096u + 512: launch_one<0, 512>(grid, s, P); break;
+    case 0 * 4096u + 128: launch_nd<128>(grid, s, P); break;
+    case 0 * 4096u + 256: launch_nd<256>(grid, s, P); break;
+    case 0 * 4096u + 512: launch_nd<512>(grid, s, P); break;
     case 256 * 4096u + 256: launch_one<256, 256>(grid, s, P); break;
     case 512 * 4096u + 256: launch_one<512, 256>(grid, s, P); break;
     case 512 * 4096u + 512: launch_one<512, 512>(grid, s, P); break;
@@ -1401,6 +1490,8 @@ int upload_engine(Engine& e, std::string& err) {
   if ((rc = upload(e.edges, &e.d_edges, err))) return rc;
   if ((rc = upload(e.out_pat, &e.d_out_pat, err))) return rc;
   if ((rc = upload(e.sb_edge, &e.d_sb_edge, err))) return rc;
+  if ((rc = upload(e.gt, &e.d_gt, err))) return rc;
+  if ((rc = upload(e.cout, &e.d_cout, err))) return rc;
   if ((rc = upload(e.pats, &e.d_pats, err))) return rc;
   if ((rc = upload(e.sim_ascii, &e.d_sim_ascii, err))) return rc;
   if ((rc = upload(e.sim_keys, &e.d_sim_keys, err))) return rc;
@@ -1424,7 +1515,7 @@ int upload_engine(Engine& e, std::string& err) {
 void free_engine_device(Engine& e) {
   if (e.d_nodes == nullptr && e.stream == nullptr) return;
   (void)hipSetDevice(e.device);
-  void* ptrs[] = {e.d_nodes, e.d_out_range, e.d_pidx, e.d_edges, e.d_out_pat, e.d_sb_edge, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
+  void* ptrs[] = {e.d_nodes, e.d_out_range, e.d_pidx, e.d_edges, e.d_out_pat, e.d_sb_edge, e.d_gt, e.d_cout, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
                   e.d_sim_vals, e.d_bp_mask, e.d_ascii_id};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -1516,6 +1607,10 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
   P.out_range = e.d_out_range;
   P.node_pidx = e.d_pidx;
   P.sb_edge = e.d_sb_edge;
+  P.gt = e.d_gt;
+  P.gt_mask = e.gt_mask;
+  P.gt_fast = (e.gt_fast && !std::getenv("FAC_NO_FAST")) ? 1 : 0;  // env: A/B knob
+  P.cout = e.d_cout;
   P.pats = e.d_pats;
   P.sim_ascii = e.d_sim_ascii;
   P.sim_keys = e.d_sim_keys;

@@ -79,11 +79,16 @@ def random_case(rng, vocab, filler, allow_beam=True, allow_limits=True):
     return b, pats, hay, thr
 
 
+@pytest.mark.parametrize("per_edge_only", [False, True])
 @pytest.mark.parametrize("seed,vocab,filler", [
     (0x1234_5678_9abc_def1, ASCII_VOCAB, ASCII_FILLER),
     (0xdead_beef_0bad_f00d, UNI_VOCAB, UNI_FILLER),
 ])
-def test_differential_random(seed, vocab, filler):
+def test_differential_random(seed, vocab, filler, per_edge_only, monkeypatch):
+    """per_edge_only: FAC_NO_FAST disables the O(1) goto-table expansion, so the per-edge unit
+    path is checked on every state as well."""
+    if per_edge_only:
+        monkeypatch.setenv("FAC_NO_FAST", "1")
     rng = Rng(seed)
     total = 0
     for _ in range(150):
