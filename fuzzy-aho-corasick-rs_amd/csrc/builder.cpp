@@ -368,22 +368,49 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
         }
       }
     }
-    uint32_t nb = 1;
-    while (nb * 2 < ent.size() + 1) nb <<= 1;  // <= 2 entries per 4-slot bucket on average
-    e.gt.assign((size_t)nb * 8, 0ull);
-    e.gt_mask = nb - 1;
-    for (auto& kvv : ent) {
-      uint32_t b = gt_hash(kvv.first, e.gt_mask);
-      for (;;) {
-        size_t t = 0;
-        while (t < 4 && e.gt[(size_t)b * 8 + t] != 0) ++t;
-        if (t < 4) {
-          e.gt[(size_t)b * 8 + t] = kvv.first;
-          e.gt[(size_t)b * 8 + 4 + t] = kvv.second;
+    // cuckoo placement (load <= ~0.4): random-walk eviction, reseed / grow on failure
+    uint32_t ns = 16;
+    while (ns * 2 < ent.size() * 5) ns <<= 1;
+    uint64_t rng = 0x2545F4914F6CDD1Dull;
+    auto next_rand = [&]() {
+      rng ^= rng << 13;
+      rng ^= rng >> 7;
+      rng ^= rng << 17;
+      return rng;
+    };
+    for (int attempt = 0;; ++attempt) {
+      if (attempt > 0 && attempt % 4 == 0) ns <<= 1;
+      e.gt_mask = ns - 1;
+      e.gt_seed1 = next_rand();
+      e.gt_seed2 = next_rand();
+      e.gt.assign(ns, uint4{0, 0, 0, 0});
+      bool ok = true;
+      for (auto& kvv : ent) {
+        uint64_t kv = kvv.first, val = kvv.second;
+        uint32_t pos = gt_slot(kv, e.gt_seed1, e.gt_mask);
+        bool placed = false;
+        for (int kick = 0; kick < 500 && !placed; ++kick) {
+          const uint32_t p1 = gt_slot(kv, e.gt_seed1, e.gt_mask), p2 = gt_slot(kv, e.gt_seed2, e.gt_mask);
+          for (uint32_t p : {p1, p2}) {
+            if (e.gt[p].x == 0 && e.gt[p].y == 0) {
+              e.gt[p] = uint4{(uint32_t)kv, (uint32_t)(kv >> 32), (uint32_t)val, (uint32_t)(val >> 32)};
+              placed = true;
+              break;
+            }
+          }
+          if (placed) break;
+          pos = (next_rand() & 1) ? p1 : p2;  // evict one occupant and re-place it
+          const uint4 old = e.gt[pos];
+          e.gt[pos] = uint4{(uint32_t)kv, (uint32_t)(kv >> 32), (uint32_t)val, (uint32_t)(val >> 32)};
+          kv = ((uint64_t)old.y << 32) | old.x;
+          val = ((uint64_t)old.w << 32) | old.z;
+        }
+        if (!placed) {
+          ok = false;
           break;
         }
-        b = (b + 1) & e.gt_mask;
       }
+      if (ok) break;
     }
     bool sims01 = true;  // every similarity in [0, 1]: p_sub * (1 - sim) in [0, p_sub]
     for (float v : e.sim_ascii) sims01 = sims01 && v >= 0.0f && v <= 1.0f;

@@ -45,8 +45,13 @@ constexpr uint32_t CHILD26_MASK = (1u << 26) - 1;  // node ids are < 2^26 (build
 //   GT_SB:   bit i = child of edge i has a single-byte edge labelled `char` (char < 128)
 constexpr uint64_t GT_VALID = 1ull << 63;
 constexpr uint64_t GT_GOTO = 0, GT_SB = 1ull << 47;
-__host__ __device__ inline uint32_t gt_hash(uint64_t kv, uint32_t mask) {
-  return (uint32_t)((kv * 0x9E3779B97F4A7C15ull) >> 40) & mask;
+// 2-choice cuckoo table of 16 B entries {kv, val}: a key lives at gt_slot(kv, seed1) or
+// gt_slot(kv, seed2); lookups read both slots, no probing
+__host__ __device__ inline uint32_t gt_slot(uint64_t kv, uint64_t seed, uint32_t mask) {
+  uint64_t x = (kv ^ seed) * 0x9E3779B97F4A7C15ull;
+  x ^= x >> 29;
+  x *= 0xBF58476D1CE4E5B9ull;
+  return (uint32_t)(x >> 32) & mask;
 }
 constexpr int32_t LIM_NONE = -1;
 
@@ -119,8 +124,9 @@ struct SearchParams {
   const uint2* out_range;
   const int32_t* node_pidx;
   // O(1) expansion tables (builder.cpp "goto table"): (node, char) -> first edge / child maps
-  const unsigned long long* gt;  // 64 B buckets: 4 keys, then their 4 values
-  uint32_t gt_mask;           // bucket count - 1
+  const uint4* gt;            // cuckoo slots {kv lo, kv hi, val lo, val hi}
+  uint32_t gt_mask;           // slot count - 1
+  unsigned long long gt_seed1, gt_seed2;
   int32_t gt_fast;            // similarity can never drop a substitution when p_sub <= remaining
   const unsigned long long* cout;  // per node: bit i = child of edge i has output (degree <= 64)
   const uint4* sb_edge;
@@ -189,8 +195,9 @@ struct Engine {
   std::vector<uint32_t> out_pat;
   std::vector<uint4> sb_bits;
   std::vector<uint4> sb_edge;
-  std::vector<unsigned long long> gt;  // goto table: per bucket 4 keys then 4 values
+  std::vector<uint4> gt;  // goto table (cuckoo slots)
   uint32_t gt_mask = 0;
+  uint64_t gt_seed1 = 0, gt_seed2 = 0;
   bool gt_fast = false;
   std::vector<unsigned long long> cout;
   std::vector<DevPattern> pats;
@@ -220,7 +227,7 @@ struct Engine {
   uint2* d_out_range = nullptr;
   int32_t* d_pidx = nullptr;
   uint4* d_sb_edge = nullptr;
-  unsigned long long* d_gt = nullptr;
+  uint4* d_gt = nullptr;
   unsigned long long* d_cout = nullptr;
   DevPattern* d_pats = nullptr;
   float* d_sim_ascii = nullptr;

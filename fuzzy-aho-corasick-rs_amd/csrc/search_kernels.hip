@@ -156,47 +156,14 @@ __device__ __forceinline__ uint32_t node_deg(const DevNode& n) { return n.degf &
 __device__ __forceinline__ uint32_t node_end(const DevNode& n) { return n.edge_begin + (n.degf & NODE_DEG_MASK); }
 __device__ __forceinline__ bool node_has_out(const DevNode& n) { return (n.degf & NODE_HAS_OUT) != 0; }
 
-// goto-table lookups (fac_internal.h), two keys probed together: a probe reads one bucket's 4
-// keys (32 B), a hit then reads its value from the same 64 B line; absent keys end at an empty slot.
-__device__ __forceinline__ int gt_match(uint4 k01, uint4 k23, uint64_t kv, bool& empty) {
+// goto-table lookup (fac_internal.h): both cuckoo slots read at once, branch-free
+__device__ __forceinline__ bool gt_get(const SearchParams& P, uint64_t kv, bool live, uint64_t& val) {
+  const uint4 a = P.gt[live ? gt_slot(kv, P.gt_seed1, P.gt_mask) : 0u];
+  const uint4 b = P.gt[live ? gt_slot(kv, P.gt_seed2, P.gt_mask) : 0u];
   const uint32_t lo = (uint32_t)kv, hi = (uint32_t)(kv >> 32);
-  empty = (k01.x == 0u && k01.y == 0u) | (k01.z == 0u && k01.w == 0u) | (k23.x == 0u && k23.y == 0u) |
-          (k23.z == 0u && k23.w == 0u);
-  return (k01.x == lo && k01.y == hi) ? 0 : (k01.z == lo && k01.w == hi) ? 1 : (k23.x == lo && k23.y == hi) ? 2
-         : (k23.z == lo && k23.w == hi)                                    ? 3 : -1;
-}
-
-__device__ __forceinline__ void gt_find2(const SearchParams& P, uint64_t kva, bool la, uint64_t kvb, bool lb,
-                                         bool& ha, uint64_t& va, bool& hb, uint64_t& vb) {
-  uint32_t ba = gt_hash(kva, P.gt_mask), bb = gt_hash(kvb, P.gt_mask);
-  bool da = !la, db = !lb;
-  ha = hb = false;
-  uint32_t sa = 0, sb = 0;
-  while (!(da && db)) {
-    const uint4* pa = reinterpret_cast<const uint4*>(P.gt + (size_t)(da ? 0u : ba) * 8u);
-    const uint4* pb = reinterpret_cast<const uint4*>(P.gt + (size_t)(db ? 0u : bb) * 8u);
-    const uint4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
-    bool ea, eb;
-    const int ta = gt_match(a0, a1, kva, ea), tb = gt_match(b0, b1, kvb, eb);
-    if (!da) {
-      if (ta >= 0) {
-        ha = true;
-        sa = ba * 8u + 4u + (uint32_t)ta;
-      }
-      da = ta >= 0 || ea;
-      ba = (ba + 1u) & P.gt_mask;
-    }
-    if (!db) {
-      if (tb >= 0) {
-        hb = true;
-        sb = bb * 8u + 4u + (uint32_t)tb;
-      }
-      db = tb >= 0 || eb;
-      bb = (bb + 1u) & P.gt_mask;
-    }
-  }
-  va = ha ? P.gt[sa] : 0ull;
-  vb = hb ? P.gt[sb] : 0ull;
+  const bool ma = a.x == lo && a.y == hi, mb = b.x == lo && b.y == hi;
+  val = ma ? (((uint64_t)a.w << 32) | a.z) : mb ? (((uint64_t)b.w << 32) | b.z) : 0ull;
+  return live && (ma || mb);
 }
 
 // find_transition_char_no_mappings (structs.rs:512-519): first edge whose first char is `ch`
@@ -783,12 +750,13 @@ __device__ void expand_fast(const SearchParams& P, const KState& st, const DevNo
   const bool is_last = pr.flags & PF_LAST, in_text = pr.flags & PF_EX, sub_on = pr.flags & PF_SUB;
   const bool del_ok = pr.flags & PF_DEL, swap_ok = pr.flags & PF_SWAP;
   const uint64_t nk = GT_VALID | ((uint64_t)st.node << 21);
-  bool h0, h1, hs0, hs1;
-  uint64_t g0, g1, s0, s1;
-  gt_find2(P, nk | GT_GOTO | pr.cur_ch, in_text, nk | GT_GOTO | pr.nch, swap_ok, h0, g0, h1, g1);
   const bool ns0 = is_last && del_ok && (pr.flags & PF_CUR) && pr.cur_ch < 128u;
   const bool ns1 = is_last && sub_on && (pr.flags & PF_NEXT) && pr.next_ch < 128u;
-  gt_find2(P, nk | GT_SB | pr.cur_ch, ns0, nk | GT_SB | pr.next_ch, ns1, hs0, s0, hs1, s1);
+  uint64_t g0, g1, s0, s1;  // all four lookups in flight together
+  const bool h0 = gt_get(P, nk | GT_GOTO | pr.cur_ch, in_text, g0);
+  const bool h1 = gt_get(P, nk | GT_GOTO | pr.nch, swap_ok, g1);
+  gt_get(P, nk | GT_SB | pr.cur_ch, ns0, s0);
+  gt_get(P, nk | GT_SB | pr.next_ch, ns1, s1);
   uint64_t exbit = 0;
   if (h0) {
     const uint32_t k = (uint32_t)(g0 >> 32) & 0xFFu;
@@ -810,10 +778,9 @@ __device__ LaneExp lane_finish(const SearchParams& P, const KState& st, const De
     x.msub &= ~(1ull << (63u - (ex >> 26)));
   }
   if (xe) {  // node2 = goto(xnode, text[j]) through the goto table
-    bool h, hu;
-    uint64_t g, gu;
-    gt_find2(P, GT_VALID | GT_GOTO | ((uint64_t)(xe & CHILD26_MASK) << 21) | pr.cur_ch, true, 0ull, false, h, g, hu, gu);
-    if (h) x.swap = (int64_t)(g & CHILD26_MASK);
+    uint64_t g;
+    if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)(xe & CHILD26_MASK) << 21) | pr.cur_ch, true, g))
+      x.swap = (int64_t)(g & CHILD26_MASK);
     if (x.swap >= 0 && P.mef == 255u) {  // within_limits_swap_ahead with node2's limits (:962-967)
       const uint32_t packed = st.packed, edits = edits_of(packed);
       const Lim m = pick_limits(P, node_limits(P, (uint32_t)x.swap));
@@ -1609,6 +1576,8 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
   P.sb_edge = e.d_sb_edge;
   P.gt = e.d_gt;
   P.gt_mask = e.gt_mask;
+  P.gt_seed1 = e.gt_seed1;
+  P.gt_seed2 = e.gt_seed2;
   P.gt_fast = (e.gt_fast && !std::getenv("FAC_NO_FAST")) ? 1 : 0;  // env: A/B knob
   P.cout = e.d_cout;
   P.pats = e.d_pats;
