@@ -420,7 +420,9 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
         next_ch = text_char(P, S, j + 1, err);
       }
       // exact transition (:766-798); matched_start stays `start` for every state
-      const int64_t exact_next = small ? small_goto(cur_ch) : goto_char(P, nd.edge_begin, node_end(nd), cur_ch);
+      const uint64_t nk = GT_VALID | GT_GOTO | ((uint64_t)st.node << 21);
+      uint64_t gx;
+      const int64_t exact_next = small ? small_goto(cur_ch) : (gt_get(P, nk | cur_ch, true, gx) ? (int64_t)(gx & CHILD26_MASK) : -1);
       const uint32_t jm1 = (j_rel + 1u) | ((j_rel + 1u) << 16);
       push_lanes<QCAP>(q, head, tail, lane == 0 && exact_next >= 0,
                        KState{(uint32_t)exact_next, jm1, pen, packed}, err);
@@ -469,10 +471,10 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
       // swap (:935-989)
       if (j + 1 < n && P.p_swp <= remaining && (!fast || edits < P.mef)) {
         const uint32_t nch = have_next ? next_ch : text_char(P, S, j + 1, err);
-        const int64_t x = small ? small_goto(nch) : goto_char(P, nd.edge_begin, node_end(nd), nch);
+        const int64_t x = small ? small_goto(nch) : (gt_get(P, nk | nch, true, gx) ? (int64_t)(gx & CHILD26_MASK) : -1);
         if (x >= 0) {
-          const DevNode nx = P.nodes[(uint32_t)x];
-          const int64_t node2 = goto_char(P, nx.edge_begin, node_end(nx), cur_ch);
+          const int64_t node2 = gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)x << 21) | cur_ch, true, gx)
+                                    ? (int64_t)(gx & CHILD26_MASK) : -1;
           bool ok = node2 >= 0;
           if (ok && !fast) {  // within_limits_swap_ahead with node2's limits (:962-967)
             const Lim m = pick_limits(P, node_limits(P, (uint32_t)node2));
@@ -793,6 +795,26 @@ __device__ LaneExp lane_finish(const SearchParams& P, const KState& st, const De
   return x;
 }
 
+// position of the r-th (0-based) set bit of m; r < popcount(m)
+__device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t r) {
+  uint32_t w = (uint32_t)m, base = 0;
+  const uint32_t c32 = (uint32_t)__popc(w);
+  if (r >= c32) {
+    r -= c32;
+    w = (uint32_t)(m >> 32);
+    base = 32;
+  }
+#pragma unroll
+  for (uint32_t half = 16; half >= 1; half >>= 1) {
+    const uint32_t c = (uint32_t)__popc(w & ((1u << half) - 1u));
+    const bool up = r >= c;
+    r = up ? r - c : r;
+    w = up ? w >> half : w;
+    base = up ? base + half : base;
+  }
+  return base;
+}
+
 // Pushes of the committed states in the reference's order (search.rs:787-1088): per state exact,
 // substitutions (edge order), swap, insertion, deletions (edge order), written at the state's
 // exclusive-prefix offset. The owner lane writes exact/swap/insertion; substitutions and deletions
@@ -819,42 +841,36 @@ __device__ void push_units(const SearchParams& P, ExpScratch* X, KState* q, uint
       q[(sw_pos + nsw) & (QCAP - 1)] = KState{st.node, jmi, __fadd_rn(pen, P.p_ins), st.packed + 1u};
     }
   }
-  const uint64_t any = act ? (x.msub | x.mdel) : 0ull;
-  const uint32_t span = any ? 64u - (uint32_t)__clzll((long long)any) : 0u;  // edges up to the last push
-  const uint32_t nunit = (span + UK - 1) / UK;
-  const uint32_t uincl = wave_inclusive_sum(nunit);
-  const uint32_t ubase = uincl - nunit;
-  const uint32_t U = (uint32_t)__builtin_amdgcn_readlane((int)uincl, 63);
+  // substitutions and deletions, one push per lane: push k of a state is the k-th set bit of its
+  // msub, then of its mdel
+  const uint32_t nsub = act ? (uint32_t)__popcll(x.msub) : 0u;
+  const uint32_t npush = act ? nsub + (uint32_t)__popcll(x.mdel) : 0u;
+  const uint32_t fincl = wave_inclusive_sum(npush);
+  const uint32_t fbase = fincl - npush;
+  const uint32_t F = (uint32_t)__builtin_amdgcn_readlane((int)fincl, 63);
   uint32_t carry = 0;
-  for (uint32_t R = 0; R < U; R += 64) {
-    const bool valid = R + lane < U;
-    const int o = unit_owner(X, R, nunit, ubase, valid, carry);
-    const uint32_t o_ub = __shfl(ubase, o), o_span = __shfl(span, o), o_eb = __shfl(nd.edge_begin, o);
+  for (uint32_t R = 0; R < F; R += 64) {
+    const bool valid = R + lane < F;
+    const int o = unit_owner(X, R, npush, fbase, valid, carry);
+    const uint32_t o_fb = __shfl(fbase, o), o_ns = __shfl(nsub, o), o_eb = __shfl(nd.edge_begin, o);
     const uint64_t o_ms = shfl_var_u64(x.msub, o), o_md = shfl_var_u64(x.mdel, o);
     const uint32_t o_sb = __shfl(sub_base, o), o_db = __shfl(del_base, o), o_cur = __shfl(cur_ch, o);
     const float o_pen = __shfl(pen, o);
     const uint32_t o_jm = __shfl(st.jm, o), o_packed = __shfl(st.packed, o);
-    const uint32_t e0 = (R + lane - o_ub) * UK;
-    const uint32_t o_j1 = (o_jm & 0xFFFFu) + 1u;
-#pragma unroll
-    for (uint32_t i = 0; i < UK; ++i) {
-      const uint32_t e = e0 + i;
-      const uint64_t bit = 1ull << (e & 63u);
-      const bool ps = valid && e < o_span && (o_ms & bit);
-      const bool pd = valid && e < o_span && (o_md & bit);
-      if (ps || pd) {
-        const DevEdge ed = P.edges[o_eb + e];
-        const uint32_t child = ed.next & EDGE_NEXT_MASK;
-        if (ps) {
-          const float sim = similarity(P, ed.ch, o_cur);
-          const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
-          const uint32_t pos = o_sb + (uint32_t)__popcll(o_ms & (bit - 1ull));
-          q[pos & (QCAP - 1)] = KState{child, o_j1 | (o_j1 << 16), __fadd_rn(o_pen, penalty), o_packed + 0x10000u};
-        }
-        if (pd) {
-          const uint32_t pos = o_db + (uint32_t)__popcll(o_md & (bit - 1ull));
-          q[pos & (QCAP - 1)] = KState{child, o_jm, __fadd_rn(o_pen, P.p_del), o_packed + 0x100u};
-        }
+    if (valid) {
+      const uint32_t k = R + lane - o_fb;
+      const bool is_sub = k < o_ns;
+      const uint32_t r = is_sub ? k : k - o_ns;
+      const uint32_t e = nth_set_bit(is_sub ? o_ms : o_md, r);
+      const DevEdge ed = P.edges[o_eb + e];
+      const uint32_t child = ed.next & EDGE_NEXT_MASK;
+      if (is_sub) {
+        const float sim = similarity(P, ed.ch, o_cur);
+        const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
+        const uint32_t o_j1 = (o_jm & 0xFFFFu) + 1u;
+        q[(o_sb + r) & (QCAP - 1)] = KState{child, o_j1 | (o_j1 << 16), __fadd_rn(o_pen, penalty), o_packed + 0x10000u};
+      } else {
+        q[(o_db + r) & (QCAP - 1)] = KState{child, o_jm, __fadd_rn(o_pen, P.p_del), o_packed + 0x100u};
       }
     }
   }
