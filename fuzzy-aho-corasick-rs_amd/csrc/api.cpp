@@ -201,26 +201,22 @@ int fac_search_raw(const fac_engine* engine, const uint8_t* utf8, uint64_t len, 
   return copy_out(res, out, n_out);
 }
 
-int fac_search_prefiltered(const fac_engine* engine, const uint8_t* utf8, uint64_t len, float threshold,
-                           fac_match** out, uint64_t* n_out, uint64_t* err_graphemes) {
-  if (!engine || !out || !n_out) return fail(FAC_E_INVALID, "NULL argument");
-  const fac::Engine& e = engine->e;
+}  // extern "C"
+
+namespace {
+
+// Prefiltered::raw on a staged haystack (prefilter.rs:304-374): bitap windows on the device, each
+// merged window re-searched as its own sub-haystack, best per (start, end, pattern) by strictly
+// greater similarity, sorted. Falls back to the full search where the reference does (:311-317).
+int prefiltered_staged(const fac::Engine& e, const fac::Haystack& h, float threshold, hipStream_t stream,
+                       std::vector<fac_match>& merged, fac_stats* stats, std::string& err) {
+  merged.clear();
   std::vector<uint32_t> ks;
   if (!e.bitap_ok || !prefilter_ks(e, threshold, ks))  // prefilter.rs:151-155, 311-317
-    return fac_search_raw(engine, utf8, len, threshold, out, n_out, err_graphemes);
-  *out = nullptr;
-  *n_out = 0;
-  fac_haystack* hay = nullptr;
-  int rc = fac_haystack_stage(engine, utf8, len, &hay, err_graphemes);
-  if (rc) return rc;
-  const fac::Haystack& h = hay->h;
-  std::string err;
+    return fac::launch_search(e, h, {whole(h)}, threshold, stream, merged, stats, err);
   std::vector<std::pair<uint64_t, uint64_t>> windows;
-  rc = fac::prefilter_windows(e, h, ks, nullptr, windows, nullptr, err);
-  if (rc) {
-    fac_haystack_free(hay);
-    return fail(rc, err);
-  }
+  int rc = fac::prefilter_windows(e, h, ks, stream, windows, stats, err);
+  if (rc) return rc;
   // Re-search each merged window as its own haystack (prefilter.rs:344-350): the slice re-decides
   // is_ascii, so an all-ASCII slice of a Unicode haystack is searched byte-wise.
   std::vector<fac::SegDesc> segs;
@@ -249,11 +245,10 @@ int fac_search_prefiltered(const fac_engine* engine, const uint8_t* utf8, uint64
     s.w_end = s.n;
     segs.push_back(s);
   }
+  if (segs.empty()) return FAC_OK;
   std::vector<fac_match> res;
-  rc = fac::launch_search(e, h, segs, threshold, nullptr, res, nullptr, err);
-  fac_haystack_free(hay);
-  if (rc) return fail(rc, err);
-  // best per (start, end, pattern) by strictly greater similarity, sorted (prefilter.rs:345-372)
+  rc = fac::launch_search(e, h, segs, threshold, stream, res, stats, err);
+  if (rc) return rc;
   std::map<std::tuple<uint64_t, uint64_t, uint32_t>, fac_match> best;
   for (const fac_match& m : res) {
     auto key = std::make_tuple(m.start, m.end, m.pattern_index);
@@ -261,9 +256,41 @@ int fac_search_prefiltered(const fac_engine* engine, const uint8_t* utf8, uint64
     if (it == best.end()) best.emplace(key, m);
     else if (m.similarity > it->second.similarity) it->second = m;
   }
-  std::vector<fac_match> merged;
   merged.reserve(best.size());
   for (auto& kv : best) merged.push_back(kv.second);
+  return FAC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fac_search_prefiltered(const fac_engine* engine, const uint8_t* utf8, uint64_t len, float threshold,
+                           fac_match** out, uint64_t* n_out, uint64_t* err_graphemes) {
+  if (!engine || !out || !n_out) return fail(FAC_E_INVALID, "NULL argument");
+  *out = nullptr;
+  *n_out = 0;
+  fac_haystack* hay = nullptr;
+  int rc = fac_haystack_stage(engine, utf8, len, &hay, err_graphemes);
+  if (rc) return rc;
+  std::vector<fac_match> merged;
+  std::string err;
+  rc = prefiltered_staged(engine->e, hay->h, threshold, nullptr, merged, nullptr, err);
+  fac_haystack_free(hay);
+  if (rc) return fail(rc, err);
+  return copy_out(merged, out, n_out);
+}
+
+int fac_search_staged_prefiltered(const fac_engine* engine, const fac_haystack* hay, float threshold, void* stream,
+                                  fac_match** out, uint64_t* n_out, fac_stats* stats) {
+  if (!engine || !hay || !out || !n_out) return fail(FAC_E_INVALID, "NULL argument");
+  *out = nullptr;
+  *n_out = 0;
+  std::vector<fac_match> merged;
+  std::string err;
+  const int rc =
+      prefiltered_staged(engine->e, hay->h, threshold, static_cast<hipStream_t>(stream), merged, stats, err);
+  if (rc) return fail(rc, err);
   return copy_out(merged, out, n_out);
 }
 

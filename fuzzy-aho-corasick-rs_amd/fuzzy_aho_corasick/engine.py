@@ -286,6 +286,19 @@ class StagedHaystack:
             _raise(rc)
         return _native.take_matches(out, n.value), st
 
+    def search_prefiltered(self, threshold: float, stream=None):
+        """Prefiltered::raw on the device-resident text (prefilter.rs:146-155, 304-374): raw rows
+        (best per (start, end, pattern), sorted) + fac_stats (prefilter_ms = bitap + merge)."""
+        out = ctypes.POINTER(_native.fac_match)()
+        n = ctypes.c_uint64()
+        st = _native.fac_stats()
+        rc = _native.lib.fac_search_staged_prefiltered(self.engine._h, self._h, f32(threshold),
+                                                       ctypes.c_void_p(stream or 0), ctypes.byref(out),
+                                                       ctypes.byref(n), ctypes.byref(st))
+        if rc:
+            _raise(rc)
+        return _native.take_matches(out, n.value), st
+
 
 class FuzzyReplacer:
     """replacer.rs:9-52"""

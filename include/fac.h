@@ -167,6 +167,13 @@ int fac_search_staged(const fac_engine* engine, const fac_haystack* hay, uint64_
                       uint64_t window_end, float threshold, void* stream, fac_match** out,
                       uint64_t* n_out, fac_stats* stats);
 
+/* Prefiltered::raw on a staged haystack (prefilter.rs:146-155, 304-374): the bitap scan and the
+ * window merge run on the device-resident text, each merged window is re-searched as its own
+ * sub-haystack, results are best-per-(start, end, pattern) and sorted. Falls back to the full
+ * search exactly where the reference does (no bitap filter, or some pattern needs k > 24). */
+int fac_search_staged_prefiltered(const fac_engine* engine, const fac_haystack* hay, float threshold,
+                                  void* stream, fac_match** out, uint64_t* n_out, fac_stats* stats);
+
 /* Diagnostics: the merged candidate windows (grapheme ranges [start, end)) of the bitap
  * pre-filter for `threshold` (prefilter.rs:319-342). Returns the window count (writes up to `cap`
  * pairs into `out`), or -1 if the pre-filter would fall back to a full search. */

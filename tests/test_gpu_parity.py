@@ -200,3 +200,17 @@ def test_every_frontier_variant(monkeypatch, variant):
     text = " ".join(words[rng.next() % 6][: 3 + rng.next() % 6] + "xyzé"[rng.next() % 4] for _ in range(600))
     _staged_vs_oracle(B().fuzzy(L().edits(2)), words, text, 0.6)
     _staged_vs_oracle(B().fuzzy(L().edits(2)).beam_width(8).case_insensitive(True), words, text, 0.6)
+
+
+@pytest.mark.parametrize("seed,vocab,filler", [
+    (0x1234_5678_9abc_def1, ASCII_VOCAB, ASCII_FILLER),
+    (0xdead_beef_0bad_f00d, UNI_VOCAB, UNI_FILLER),
+])
+def test_staged_prefiltered_matches_oracle(seed, vocab, filler):
+    """fac_search_staged_prefiltered (device-resident text) == the oracle's Prefiltered::raw rows."""
+    rng = Rng(seed ^ 0x99)
+    for _ in range(60):
+        b, pats, hay, thr = random_case(rng, vocab, filler, allow_beam=False)
+        got, _ = b.build(pats).stage(hay.encode("utf-8")).search_prefiltered(thr)
+        want = OracleEngine(b, pats).raw_rows(hay, thr, prefilter=True)
+        assert sorted(got) == sorted(want), f"patterns={pats!r} hay={hay!r} thr={thr}"
