@@ -75,10 +75,6 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
     err = "auto_beam width must be >= 1";
     return FAC_E_INVALID;
   }
-  if (e.has_auto_beam && e.beam_width == 0) {  // an explicit beam_width takes precedence (builder.rs:93-106)
-    err = "auto_beam is not implemented on the GPU path yet";
-    return FAC_E_UNSUPPORTED;
-  }
   e.has_limits = cfg->has_limits != 0;
   if (e.has_limits) {
     e.limits = to_dev(cfg->limits);

@@ -167,6 +167,9 @@ struct SearchParams {
   const uint64_t* win_list;  // null: virtual windows 0..total_windows; else list of virtual ids
   uint64_t* spill;           // virtual ids of windows that overflowed this variant's LDS frontier
   uint64_t spill_cap;
+  // auto-beam pass 1 (search.rs:1096-1103): per window queue.len() under exact dedup
+  uint32_t* win_counts;  // null: not recorded
+  int32_t exact_dedup;   // dedup must be exact (beam, or counting for auto-beam)
 };
 
 constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8u, ERR_OUT = 16u, ERR_SPILL = 32u;

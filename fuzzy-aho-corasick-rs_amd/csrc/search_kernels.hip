@@ -921,7 +921,7 @@ __device__ unsigned long long g_prof[16];
 // semantics would diverge: before the first in-batch dedup conflict, before the first pop at which
 // the beam would trigger, and before the first >64-edge node (expanded alone, edge-parallel).
 template <uint32_t VCAP, uint32_t QCAP>
-__device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
+__device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
                            uint32_t& cseq, EmitList& EL, uint64_t start, uint64_t& popped, unsigned& err) {
   const uint32_t lane = lane_id();
 #ifdef FAC_PHASE_PROF
@@ -975,7 +975,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
       head += 1;
       popped += 1;
       if constexpr (VCAP > 0)
-        if (visited_check<VCAP>(vis, vcount, s0, P.beam != 0, err)) continue;
+        if (visited_check<VCAP>(vis, vcount, s0, P.exact_dedup != 0, err)) continue;
       const DevNode n0 = P.nodes[s0.node];
       if (node_has_out(n0)) emit_state(P, EL, s0.jm >> 16, s0.pen, s0.packed, s0.node, err);
       expand_wide<QCAP>(P, S, q, head, tail, s0, n0, start, err);
@@ -1075,7 +1075,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
           kt.jm = shfl_u32(st.jm, l);
           kt.pen = shfl_f32(st.pen, l);
           kt.packed = shfl_u32(st.packed, l);
-          visited_check<VCAP>(vis, vcount, kt, P.beam != 0, err);
+          visited_check<VCAP>(vis, vcount, kt, P.exact_dedup != 0, err);
         }
       } else {  // near-full table: the reference order, one state at a time
         for (uint32_t t = 0; t < Bc; ++t) {
@@ -1085,7 +1085,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
           kt.jm = shfl_u32(st.jm, t);
           kt.pen = shfl_f32(st.pen, t);
           kt.packed = shfl_u32(st.packed, t);
-          visited_check<VCAP>(vis, vcount, kt, P.beam != 0, err);
+          visited_check<VCAP>(vis, vcount, kt, P.exact_dedup != 0, err);
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -1147,6 +1147,7 @@ __device__ void run_window(const SearchParams& P, const SegDesc& S, KState* vis,
   if (lane == 0)
     for (int i = 0; i < 12; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof_acc[i]);
 #endif
+  return tail;  // states pushed this window, the root included: the reference's queue.len()
 }
 
 // 2-gram window skip (search.rs:535-553)
@@ -1207,8 +1208,10 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         const uint32_t seg = shfl_u32(kl, l);
         const uint64_t st = shfl_u64(start, l);
         const SegDesc S = P.segs[seg];
-        run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, popped, err);
-        if (wave_or(err) & (ERR_QUEUE | ERR_VISITED)) {  // frontier overflow: spill the window
+        const uint32_t qlen = run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, popped, err);
+        const bool overflow = (wave_or(err) & (ERR_QUEUE | ERR_VISITED)) != 0;
+        if (P.win_counts && !overflow && lane == 0) P.win_counts[shfl_u64(vid, l)] = qlen;
+        if (overflow) {  // frontier overflow: spill the window
           const uint64_t id = shfl_u64(vid, l);
           if (lane == 0) {
             const unsigned long long k = atomicAdd(P.counters + 3, 1ull);
@@ -1566,8 +1569,12 @@ void free_haystack(Haystack& h) {
   h.d_off = nullptr;
 }
 
-int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs_in, float thr,
-                  hipStream_t stream, std::vector<fac_match>& out, fac_stats* stats, std::string& err) {
+// One search over the windows of `segs_in` with a given beam (0 = none). exact_dedup: the dedup
+// must be exact (beam, or auto-beam counting); counts (optional): per virtual window (non-empty
+// segments concatenated) the number of states pushed, the reference's queue.len().
+int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs_in, float thr,
+                hipStream_t stream, uint32_t beam, bool exact_dedup, std::vector<uint32_t>* counts,
+                std::vector<fac_match>& out, fac_stats* stats, std::string& err) {
   out.clear();
   HIP_TRY(hipSetDevice(e.device));
   if (!stream) stream = e.stream;
@@ -1621,7 +1628,8 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
   P.has_glim = e.has_limits;
   P.glim = e.limits;
   P.has_pattern_limits = e.has_pattern_limits;
-  P.beam = (uint32_t)std::min<uint64_t>(e.beam_width, 0xFFFFFFFFull);
+  P.beam = beam;
+  P.exact_dedup = exact_dedup ? 1 : 0;
   P.window_skip = e.window_skip;
   std::memcpy(P.first_bits, e.first_bits, sizeof(P.first_bits));
   std::memcpy(P.second_bits, e.second_bits, sizeof(P.second_bits));
@@ -1637,15 +1645,16 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
   const uint64_t fan_nr = 3ull + 2ull * e.max_degree_nonroot;
   auto fits = [&](const Variant& v) {
     if (P.beam) return v.vcap > 0 && fan_root + 1 <= v.qcap && 2ull * P.beam + fan_nr + 1 <= v.qcap;
-    return fan_root + 1 <= v.qcap && fan_nr + 1 <= v.qcap;
+    return (v.vcap > 0 || !exact_dedup) && fan_root + 1 <= v.qcap && fan_nr + 1 <= v.qcap;
   };
   const size_t nv = sizeof(kVariants) / sizeof(kVariants[0]);
   size_t vi = nv;
   // defaults (measured on MI355X): beamed -> 512-entry table + 256-entry ring
   // (12.8 KB LDS); unbeamed -> no table + 512-entry ring (a 128 ring cuts batches too often)
   for (size_t i = 0; i < nv && vi == nv; ++i)
-    if (fits(kVariants[i]) && (P.beam ? kVariants[i].vcap >= default_beam_vcap()
-                                      : kVariants[i].vcap == 0 && kVariants[i].qcap >= 512))
+    if (fits(kVariants[i]) && (P.beam          ? kVariants[i].vcap >= default_beam_vcap()
+                               : exact_dedup ? kVariants[i].vcap >= 512 && kVariants[i].qcap >= 512
+                                             : kVariants[i].vcap == 0 && kVariants[i].qcap >= 512))
       vi = i;
   for (size_t i = 0; i < nv && vi == nv; ++i)
     if (fits(kVariants[i])) vi = i;
@@ -1678,6 +1687,13 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
   HIP_TRY(d_cnt.alloc(4 * sizeof(unsigned long long), stream));
   HIP_TRY(d_out.alloc(out_cap * sizeof(fac_match), stream));
   HIP_TRY(d_spill.alloc(spill_cap * sizeof(uint64_t), stream));
+  DevBuf d_counts;
+  P.win_counts = nullptr;
+  if (counts) {
+    HIP_TRY(d_counts.alloc(windows * sizeof(uint32_t), stream));
+    HIP_TRY(hipMemsetAsync(d_counts.p, 0, windows * sizeof(uint32_t), stream));  // skipped windows: 0
+    P.win_counts = static_cast<uint32_t*>(d_counts.p);
+  }
   Events ev;
   HIP_TRY(hipEventCreate(&ev.a));
   HIP_TRY(hipEventCreate(&ev.b));
@@ -1783,6 +1799,11 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
     P.win_list = static_cast<const uint64_t*>(d_list.p);
     ++retries;
   }
+  if (counts && rc == FAC_OK) {
+    counts->resize(windows);
+    HIP_TRY(hipMemcpyAsync(counts->data(), d_counts.p, windows * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+  }
   if (stats) {
     stats->kernel_ms += ms_total;
     stats->kernel_launches += launches;
@@ -1793,6 +1814,72 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
     stats->retries += retries;
   }
   return rc;
+}
+
+// search_unsorted_impl for a list of (sub)haystacks (search.rs:418-1119). With auto_beam and no
+// explicit beam (search.rs:1096-1103) the beam switches on after the first window at which the
+// running total of queue.len() exceeds the budget; the total runs per search_raw call, i.e. per
+// segment (the pre-filter re-searches every merged window with its own call). Two passes
+// reproduce it exactly: pass 1 searches every window unbeamed with exact dedup and records each
+// window's queue.len(); per segment the switch window w* is the first whose running total exceeds
+// the budget; pass-1 matches of windows <= w* are kept and the windows after w* are re-searched
+// with the auto-beam width.
+int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs_in, float thr,
+                  hipStream_t stream, std::vector<fac_match>& out, fac_stats* stats, std::string& err) {
+  const uint32_t beam = (uint32_t)std::min<uint64_t>(e.beam_width, 0xFFFFFFFFull);
+  if (!(e.has_auto_beam && e.beam_width == 0))
+    return launch_pass(e, h, segs_in, thr, stream, beam, beam != 0, nullptr, out, stats, err);
+  std::vector<SegDesc> segs;
+  for (const SegDesc& s : segs_in) {
+    SegDesc c = s;
+    c.w_end = std::min(c.w_end, c.n);
+    if (c.w_begin < c.w_end) segs.push_back(c);
+  }
+  std::vector<uint32_t> counts;
+  std::vector<fac_match> pass1;
+  int rc = launch_pass(e, h, segs, thr, stream, 0, true, &counts, pass1, stats, err);
+  if (rc) return rc;
+  std::vector<SegDesc> tails;          // windows after each segment's switch window
+  std::vector<std::pair<uint64_t, uint64_t>> keep;  // per segment: [byte_base, cut byte) of pass 1
+  uint64_t v = 0;
+  for (const SegDesc& c : segs) {
+    uint64_t total = 0, cut_w = c.w_end;  // first window searched with the beam
+    for (uint64_t w = c.w_begin; w < c.w_end; ++w, ++v) {
+      total += counts[v];
+      if (cut_w == c.w_end && total > e.ab_budget) cut_w = w + 1;
+    }
+    const uint64_t cut_local = cut_w >= c.n ? c.hay_len
+                               : c.ascii    ? cut_w
+                                            : h.starts[c.text_base + cut_w] - c.byte_base;
+    keep.push_back({c.byte_base, c.byte_base + cut_local});
+    if (cut_w < c.w_end) {
+      SegDesc t = c;
+      t.w_begin = cut_w;
+      tails.push_back(t);
+    }
+  }
+  // segments cover disjoint byte ranges: attribute each pass-1 match by its start byte
+  std::vector<size_t> order(segs.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return segs[a].byte_base < segs[b].byte_base; });
+  out.clear();
+  for (const fac_match& m : pass1) {
+    size_t lo = 0, hi = order.size();
+    while (hi - lo > 1) {
+      const size_t mid = (lo + hi) / 2;
+      if (segs[order[mid]].byte_base <= m.start) lo = mid;
+      else hi = mid;
+    }
+    const auto& k = keep[order[lo]];
+    if (m.start >= k.first && m.start < k.second) out.push_back(m);
+  }
+  if (tails.empty()) return FAC_OK;
+  std::vector<fac_match> pass2;
+  rc = launch_pass(e, h, tails, thr, stream, (uint32_t)std::min<uint64_t>(e.ab_width, 0xFFFFFFFFull), true,
+                   nullptr, pass2, stats, err);
+  if (rc) return rc;
+  out.insert(out.end(), pass2.begin(), pass2.end());
+  return FAC_OK;
 }
 
 int prefilter_windows(const Engine& e, const Haystack& h, const std::vector<uint32_t>& ks, hipStream_t stream,

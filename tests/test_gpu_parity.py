@@ -214,3 +214,15 @@ def test_staged_prefiltered_matches_oracle(seed, vocab, filler):
         got, _ = b.build(pats).stage(hay.encode("utf-8")).search_prefiltered(thr)
         want = OracleEngine(b, pats).raw_rows(hay, thr, prefilter=True)
         assert sorted(got) == sorted(want), f"patterns={pats!r} hay={hay!r} thr={thr}"
+
+
+@pytest.mark.parametrize("budget,width", [(0, 2), (5, 4), (40, 8), (300, 3), (2 ** 64 - 1, 8)])
+def test_auto_beam_matches_oracle(budget, width):
+    """auto_beam (search.rs:1096-1103): GPU two-pass (exact counting pass, beamed tail) == the
+    oracle's sequential budget, per search_raw call, incl. the pre-filter's per-window calls."""
+    rng = Rng(0xab ^ budget)
+    for _ in range(40):
+        b, pats, hay, thr = random_case(rng, ASCII_VOCAB + UNI_VOCAB, ASCII_FILLER + UNI_FILLER, allow_beam=False)
+        b = b.auto_beam(budget, width)
+        compare(b, pats, hay, thr)
+        compare(b, pats, hay, thr, prefilter=True)

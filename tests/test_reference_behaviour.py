@@ -377,3 +377,30 @@ def test_mappings_are_refused_not_diverged():  # builder.rs:108-132 are outside 
     from fuzzy_aho_corasick import UnsupportedConfiguration
     with pytest.raises(UnsupportedConfiguration):
         B().fuzzy(L().edits(1)).mapping("ks", "x").build(["alexandr"])
+
+
+def _spans_patterns(ms):
+    return [(m.start, m.end, m.pattern_index, m.sim_bits()) for m in ms]
+
+
+def test_auto_beam_exact_below_budget_and_bounded_above(make_engine):  # tests.rs:867-917
+    pats = ["saddam", "hussein", "tincidunt", "porta", "vestibulum", "accumsan"]
+    text = "this is a saddamhu example with multiple saddam and tincidutn matches"
+    b = lambda: B().fuzzy(L().edits(2)).case_insensitive(True)
+    opts = O().threshold(0.6).sorted()
+    exact = make_engine(b(), pats).search(text, opts)
+    huge = make_engine(b().auto_beam(2 ** 64 - 1, 8), pats).search(text, opts)
+    assert _spans_patterns(exact) == _spans_patterns(huge)  # never engages: exact
+    beamed = make_engine(b().auto_beam(1, 16), pats).search(text, opts)
+    assert "saddam" in [pats[m.pattern_index] for m in beamed]
+
+
+def test_deterministic_search_auto_beam(make_engine):  # tests.rs:1458-1500 (beam-sort path)
+    e = make_engine(B().fuzzy(L().edits(4)).auto_beam(100, 500),
+                    ["hello", "world", "help", "held", "shell", "yellow", "algorithms", "automaton",
+                     "abbreviations"])
+    for hay in ["hello world", "helo world", "She sells sea shells by the sea shore",
+                "Why did the yellow bird help the shell?", "The quick brown fox jumps over the lazy dog",
+                "algorithmic automata and abbreviated forms"]:
+        a = _spans_patterns(e.search(hay, O().threshold(0.5).sorted()))
+        assert a == _spans_patterns(e.search(hay, O().threshold(0.5).sorted()))
