@@ -294,6 +294,19 @@ int fac_search_staged_prefiltered(const fac_engine* engine, const fac_haystack* 
   return copy_out(merged, out, n_out);
 }
 
+int fac_matches_apply(const fac_engine* engine, fac_match* matches, uint64_t n, int32_t order, int32_t overlap,
+                      const uint64_t* unique_ids, uint64_t* n_out) {
+  if (!engine || (!matches && n) || !n_out) return fail(FAC_E_INVALID, "NULL argument");
+  if (order < 0 || order > 3 || overlap < 0 || overlap > 2) return fail(FAC_E_INVALID, "bad order/overlap");
+  std::vector<fac_match> v(matches, matches + n);
+  std::string err;
+  const int rc = fac::apply_matches(engine->e, v, order, overlap, unique_ids, err);
+  if (rc) return fail(rc, err);
+  if (!v.empty()) std::memcpy(matches, v.data(), v.size() * sizeof(fac_match));
+  *n_out = v.size();
+  return FAC_OK;
+}
+
 int64_t fac_prefilter_windows(const fac_engine* engine, const uint8_t* utf8, uint64_t len, float threshold,
                               uint64_t* out, uint64_t cap) {
   if (!engine) return fail(FAC_E_INVALID, "NULL argument"), -1;

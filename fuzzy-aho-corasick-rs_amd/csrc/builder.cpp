@@ -93,9 +93,11 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
   e.pats.resize(np);
   std::vector<uint64_t> starts;
   std::u32string folded;
+  e.pat_bytes.assign(np, 0);
   for (uint64_t i = 0; i < np; ++i) {
     const uint8_t* s = reinterpret_cast<const uint8_t*>(pats[i].utf8);
     uint64_t len = pats[i].len;
+    e.pat_bytes[i] = (uint32_t)std::min<uint64_t>(len, 0xFFFFFFFFull);
     if (len && !s) { err = "NULL pattern"; return FAC_E_INVALID; }
     if (!utf8_valid(s, len)) { err = "pattern is not valid UTF-8"; return FAC_E_INVALID; }
     segment_graphemes(s, len, starts);

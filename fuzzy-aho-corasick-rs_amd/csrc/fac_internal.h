@@ -203,6 +203,7 @@ struct Engine {
   uint64_t gt_seed1 = 0, gt_seed2 = 0;
   bool gt_fast = false;
   std::vector<unsigned long long> cout;
+  std::vector<uint32_t> pat_bytes;  // Pattern::len (bytes, structs.rs:628-630) for ranking
   std::vector<DevPattern> pats;
   std::vector<float> sim_ascii;
   std::vector<uint64_t> sim_keys;
@@ -232,6 +233,7 @@ struct Engine {
   uint4* d_sb_edge = nullptr;
   uint4* d_gt = nullptr;
   unsigned long long* d_cout = nullptr;
+  uint32_t* d_pat_bytes = nullptr;
   DevPattern* d_pats = nullptr;
   float* d_sim_ascii = nullptr;
   uint64_t* d_sim_keys = nullptr;
@@ -260,6 +262,8 @@ int build_engine(const fac_pattern* pats, uint64_t n, const fac_config* cfg, Eng
 int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs, float thr,
                   hipStream_t stream, std::vector<fac_match>& out, fac_stats* stats, std::string& err);
 // bitap pre-filter: candidate windows (grapheme ranges, merged) for a staged haystack
+int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,
+                  std::string& err);
 int prefilter_windows(const Engine& e, const Haystack& h, const std::vector<uint32_t>& ks, hipStream_t stream,
                       std::vector<std::pair<uint64_t, uint64_t>>& windows, fac_stats* stats, std::string& err);
 int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack& h, std::string& err);

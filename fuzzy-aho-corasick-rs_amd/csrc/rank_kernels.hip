@@ -1,0 +1,336 @@
+// rank_kernels.hip — ranking and overlap resolution of raw matches on the MI355X
+// (FuzzyMatches::apply, src/matches.rs:7-149), the step right after the search path.
+//
+// * Orders (matches.rs:23-81) are total orders over (start, end, pattern_index)-unique records, so
+//   a device merge sort (rocPRIM) with the same comparator reproduces the reference's
+//   sort_unstable_by exactly.
+// * non_overlapping (matches.rs:83-112) walks the ranked list and accepts a match iff it does not
+//   intersect an accepted one (binary search on accepted starts). Two matches can only influence
+//   each other's test if their spans touch, so the matches split — in start order, at every point
+//   where a start lies strictly beyond all earlier ends — into clusters that are resolved
+//   independently, one thread per cluster, each walking its members in rank order with the
+//   reference's own test. Kept matches are re-sorted by start (ties: rank order).
+// * non_overlapping_unique (matches.rs:114-149) adds a global "pattern used once" constraint, so it
+//   runs on the host over the device-ranked list (O(n log n)).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include <rocprim/device/device_merge_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <set>
+#include <unordered_set>
+#include <vector>
+
+#include "fac_internal.h"
+
+namespace fac {
+namespace {
+
+// f32 total_cmp as an unsigned key (ascending key order == total order)
+__device__ inline uint32_t total_key(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+struct RankCmp {  // "a before b" for Order::{Default, Greedy, CoverageWeighted}
+  const uint32_t* plen;  // pattern byte length (structs.rs:628-630: Pattern::len is bytes)
+  int order;             // 1 default, 2 greedy, 3 coverage-weighted
+  __device__ bool operator()(const fac_match& a, const fac_match& b) const {
+    const uint32_t sa = total_key(a.similarity), sb = total_key(b.similarity);
+    const uint32_t la = plen[a.pattern_index], lb = plen[b.pattern_index];
+    if (order == 1) {  // matches.rs:24-38
+      if (sa != sb) return sa > sb;
+      if (la != lb) return la > lb;
+      const uint64_t ta = a.end - a.start, tb = b.end - b.start;
+      if (ta != tb) return ta > tb;
+    } else if (order == 2) {  // matches.rs:43-57
+      if (la != lb) return la > lb;
+      if (sa != sb) return sa > sb;
+    } else {  // matches.rs:63-81: similarity * similarity * len as f32, left to right
+      const float ca = __fmul_rn(__fmul_rn(a.similarity, a.similarity), (float)la);
+      const float cb = __fmul_rn(__fmul_rn(b.similarity, b.similarity), (float)lb);
+      const uint32_t ka = total_key(ca), kb = total_key(cb);
+      if (ka != kb) return ka > kb;
+      if (sa != sb) return sa > sb;
+    }
+    if (a.start != b.start) return a.start < b.start;
+    if (a.end != b.end) return a.end < b.end;
+    return a.pattern_index < b.pattern_index;
+  }
+};
+
+struct Span {
+  uint64_t start, end;
+  uint32_t rank;     // position in the ranked list
+  uint32_t cluster;  // filled after the start-order pass
+};
+
+struct SpanByStart {
+  __host__ __device__ bool operator()(const Span& a, const Span& b) const {
+    if (a.start != b.start) return a.start < b.start;
+    if (a.end != b.end) return a.end < b.end;
+    return a.rank < b.rank;
+  }
+};
+
+struct SpanByClusterRank {
+  __host__ __device__ bool operator()(const Span& a, const Span& b) const {
+    if (a.cluster != b.cluster) return a.cluster < b.cluster;
+    return a.rank < b.rank;
+  }
+};
+
+struct KeptByStart {  // final sort_unstable_by_key(start); ties kept in acceptance (rank) order
+  __host__ __device__ bool operator()(const Span& a, const Span& b) const {
+    if (a.start != b.start) return a.start < b.start;
+    return a.rank < b.rank;
+  }
+};
+
+__global__ void spans_kernel(const fac_match* m, uint64_t n, Span* s) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) s[i] = Span{m[i].start, m[i].end, (uint32_t)i, 0u};
+}
+
+// cluster id = number of strict gaps before the element, in start order (max end by a scan)
+__global__ void cluster_flags_kernel(const Span* s, const uint64_t* max_end_incl, uint64_t n, uint32_t* flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) flag[i] = (i > 0 && s[i].start > max_end_incl[i - 1]) ? 1u : 0u;
+}
+
+__global__ void ends_kernel(const Span* s, uint64_t n, uint64_t* e) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) e[i] = s[i].end;
+}
+
+__global__ void assign_cluster_kernel(Span* s, const uint32_t* cid, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) s[i].cluster = cid[i];
+}
+
+// first member index of every cluster (members ordered by (cluster, rank))
+__global__ void cluster_heads_kernel(const Span* s, uint64_t n, uint64_t* head) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && (i == 0 || s[i].cluster != s[i - 1].cluster)) head[s[i].cluster] = i;
+}
+
+// One thread per cluster: the reference's walk (matches.rs:87-110) over the cluster's members in
+// rank order; `occ` holds the cluster's accepted (start, end) sorted by start in the same index
+// range as its members.
+__global__ void resolve_kernel(const Span* s, const uint64_t* head, uint64_t n_clusters, uint64_t n, uint2* occ_lo,
+                               uint2* occ_hi, uint8_t* keep) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_clusters) return;
+  const uint64_t b = head[c], e = (c + 1 < n_clusters) ? head[c + 1] : n;
+  uint64_t k = 0;  // accepted so far
+  for (uint64_t i = b; i < e; ++i) {
+    const uint64_t ms = s[i].start, me = s[i].end;
+    uint64_t lo = 0, hi = k;  // bisect_left on accepted starts
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      const uint64_t st = ((uint64_t)occ_hi[b + mid].x << 32) | occ_lo[b + mid].x;
+      if (st < ms) lo = mid + 1;
+      else hi = mid;
+    }
+    const uint64_t pos = lo;
+    const bool prev_ok = pos == 0 || ((((uint64_t)occ_hi[b + pos - 1].y << 32) | occ_lo[b + pos - 1].y) <= ms);
+    const bool next_ok = pos == k || ((((uint64_t)occ_hi[b + pos].x << 32) | occ_lo[b + pos].x) >= me);
+    if (prev_ok && next_ok) {
+      for (uint64_t t = k; t > pos; --t) {
+        occ_lo[b + t] = occ_lo[b + t - 1];
+        occ_hi[b + t] = occ_hi[b + t - 1];
+      }
+      occ_lo[b + pos] = make_uint2((uint32_t)ms, (uint32_t)me);
+      occ_hi[b + pos] = make_uint2((uint32_t)(ms >> 32), (uint32_t)(me >> 32));
+      ++k;
+      keep[s[i].rank] = 1;
+    }
+  }
+}
+
+__global__ void kept_spans_kernel(const fac_match* m, const uint8_t* keep, const uint32_t* pos, uint64_t n, Span* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && keep[i]) out[pos[i] - 1] = Span{m[i].start, m[i].end, (uint32_t)i, 0u};
+}
+
+__global__ void gather_kernel(const fac_match* m, const Span* order, uint64_t n, fac_match* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = m[order[i].rank];
+}
+
+#define RK_TRY(x)                                                   \
+  do {                                                              \
+    hipError_t _e = (x);                                            \
+    if (_e != hipSuccess) {                                         \
+      err = std::string(#x ": ") + hipGetErrorString(_e);           \
+      return FAC_E_HIP;                                             \
+    }                                                               \
+  } while (0)
+
+struct Buf {
+  void* p = nullptr;
+  ~Buf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t alloc(size_t bytes) { return hipMalloc(&p, std::max<size_t>(bytes, 16)); }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+template <class T, class Cmp>
+hipError_t dev_sort(T* in, T* out, uint64_t n, Cmp cmp, hipStream_t s) {
+  size_t bytes = 0;
+  hipError_t e = rocprim::merge_sort(nullptr, bytes, in, out, n, cmp, s);
+  if (e != hipSuccess) return e;
+  Buf tmp;
+  if ((e = tmp.alloc(bytes)) != hipSuccess) return e;
+  return rocprim::merge_sort(tmp.p, bytes, in, out, n, cmp, s);
+}
+
+constexpr uint64_t kMaxCluster = 1u << 14;  // larger clusters: the host walk (O(n log n))
+
+// The reference's non_overlapping(_unique) walk (matches.rs:83-149) on the host.
+void walk_host(std::vector<fac_match>& v, const uint64_t* unique_ids, bool unique) {
+  std::multiset<std::pair<uint64_t, uint64_t>> occ;  // (start, end) by start
+  std::unordered_set<uint64_t> used;
+  std::vector<std::pair<uint64_t, uint32_t>> kept;  // (start, rank)
+  for (uint32_t r = 0; r < v.size(); ++r) {
+    const fac_match& m = v[r];
+    const uint64_t uid = unique_ids ? unique_ids[m.pattern_index] : m.pattern_index;
+    if (unique && used.count(uid)) continue;
+    auto it = occ.lower_bound({m.start, 0});  // bisect_left on starts
+    const bool next_ok = it == occ.end() || it->first >= m.end;
+    const bool prev_ok = it == occ.begin() || std::prev(it)->second <= m.start;
+    if (prev_ok && next_ok) {
+      occ.insert(it, {m.start, m.end});
+      if (unique) used.insert(uid);
+      kept.push_back({m.start, r});
+    }
+  }
+  std::stable_sort(kept.begin(), kept.end(), [](auto& a, auto& b) { return a.first < b.first; });
+  std::vector<fac_match> out;
+  out.reserve(kept.size());
+  for (auto& k : kept) out.push_back(v[k.second]);
+  v.swap(out);
+}
+
+}  // namespace
+
+int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,
+                  std::string& err) {
+  const uint64_t n = v.size();
+  if (n == 0 || (order == 0 && overlap == 0)) return FAC_OK;
+  RK_TRY(hipSetDevice(e.device));
+  hipStream_t s = e.stream;
+  const uint32_t T = 256;
+  const uint32_t G = (uint32_t)((n + T - 1) / T);
+  Buf d_a, d_b;
+  RK_TRY(d_a.alloc(n * sizeof(fac_match)));
+  RK_TRY(d_b.alloc(n * sizeof(fac_match)));
+  RK_TRY(hipMemcpyAsync(d_a.p, v.data(), n * sizeof(fac_match), hipMemcpyHostToDevice, s));
+  fac_match* ranked = d_a.as<fac_match>();
+  if (order != 0) {
+    RK_TRY(dev_sort(d_a.as<fac_match>(), d_b.as<fac_match>(), n, RankCmp{e.d_pat_bytes, order}, s));
+    ranked = d_b.as<fac_match>();
+  }
+  if (overlap == 0 || overlap == 2) {  // keep, or the unique walk on the host
+    RK_TRY(hipMemcpyAsync(v.data(), ranked, n * sizeof(fac_match), hipMemcpyDeviceToHost, s));
+    RK_TRY(hipStreamSynchronize(s));
+    if (overlap == 2) walk_host(v, unique_ids, true);
+    return FAC_OK;
+  }
+  // ---- non_overlapping: clusters in start order, resolved one thread per cluster
+  Buf d_sp, d_sp2, d_ends, d_maxe, d_flag, d_cid, d_head, d_lo, d_hi, d_keep, d_pos, d_kept;
+  RK_TRY(d_sp.alloc(n * sizeof(Span)));
+  RK_TRY(d_sp2.alloc(n * sizeof(Span)));
+  hipLaunchKernelGGL(spans_kernel, dim3(G), dim3(T), 0, s, ranked, n, d_sp.as<Span>());
+  RK_TRY(dev_sort(d_sp.as<Span>(), d_sp2.as<Span>(), n, SpanByStart{}, s));
+  RK_TRY(d_ends.alloc(n * 8));
+  RK_TRY(d_maxe.alloc(n * 8));
+  hipLaunchKernelGGL(ends_kernel, dim3(G), dim3(T), 0, s, d_sp2.as<Span>(), n, d_ends.as<uint64_t>());
+  {
+    size_t bytes = 0;
+    RK_TRY(rocprim::inclusive_scan(nullptr, bytes, d_ends.as<uint64_t>(), d_maxe.as<uint64_t>(), n,
+                                   rocprim::maximum<uint64_t>(), s));
+    Buf tmp;
+    RK_TRY(tmp.alloc(bytes));
+    RK_TRY(rocprim::inclusive_scan(tmp.p, bytes, d_ends.as<uint64_t>(), d_maxe.as<uint64_t>(), n,
+                                   rocprim::maximum<uint64_t>(), s));
+  }
+  RK_TRY(d_flag.alloc(n * 4));
+  RK_TRY(d_cid.alloc(n * 4));
+  hipLaunchKernelGGL(cluster_flags_kernel, dim3(G), dim3(T), 0, s, d_sp2.as<Span>(), d_maxe.as<uint64_t>(), n,
+                     d_flag.as<uint32_t>());
+  {
+    size_t bytes = 0;
+    RK_TRY(rocprim::inclusive_scan(nullptr, bytes, d_flag.as<uint32_t>(), d_cid.as<uint32_t>(), n,
+                                   rocprim::plus<uint32_t>(), s));
+    Buf tmp;
+    RK_TRY(tmp.alloc(bytes));
+    RK_TRY(rocprim::inclusive_scan(tmp.p, bytes, d_flag.as<uint32_t>(), d_cid.as<uint32_t>(), n,
+                                   rocprim::plus<uint32_t>(), s));
+  }
+  hipLaunchKernelGGL(assign_cluster_kernel, dim3(G), dim3(T), 0, s, d_sp2.as<Span>(), d_cid.as<uint32_t>(), n);
+  RK_TRY(dev_sort(d_sp2.as<Span>(), d_sp.as<Span>(), n, SpanByClusterRank{}, s));
+  uint32_t last_cid = 0;
+  RK_TRY(hipMemcpyAsync(&last_cid, d_cid.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
+  RK_TRY(hipStreamSynchronize(s));
+  const uint64_t n_clusters = (uint64_t)last_cid + 1;
+  RK_TRY(d_head.alloc(n_clusters * 8));
+  hipLaunchKernelGGL(cluster_heads_kernel, dim3(G), dim3(T), 0, s, d_sp.as<Span>(), n, d_head.as<uint64_t>());
+  {  // largest cluster: a thread's walk is quadratic in its cluster, keep it bounded
+    std::vector<uint64_t> heads(n_clusters);
+    RK_TRY(hipMemcpyAsync(heads.data(), d_head.p, n_clusters * 8, hipMemcpyDeviceToHost, s));
+    RK_TRY(hipStreamSynchronize(s));
+    uint64_t biggest = 0;
+    for (uint64_t c = 0; c < n_clusters; ++c) biggest = std::max(biggest, (c + 1 < n_clusters ? heads[c + 1] : n) - heads[c]);
+    if (biggest > kMaxCluster) {
+      RK_TRY(hipMemcpyAsync(v.data(), ranked, n * sizeof(fac_match), hipMemcpyDeviceToHost, s));
+      RK_TRY(hipStreamSynchronize(s));
+      walk_host(v, nullptr, false);
+      return FAC_OK;
+    }
+  }
+  RK_TRY(d_lo.alloc(n * sizeof(uint2)));
+  RK_TRY(d_hi.alloc(n * sizeof(uint2)));
+  RK_TRY(d_keep.alloc(n));
+  RK_TRY(hipMemsetAsync(d_keep.p, 0, n, s));
+  hipLaunchKernelGGL(resolve_kernel, dim3((uint32_t)((n_clusters + T - 1) / T)), dim3(T), 0, s, d_sp.as<Span>(),
+                     d_head.as<uint64_t>(), n_clusters, n, d_lo.as<uint2>(), d_hi.as<uint2>(), d_keep.as<uint8_t>());
+  // compact the kept matches (rank order), then order them by start
+  RK_TRY(d_pos.alloc(n * 4));
+  {
+    size_t bytes = 0;
+    RK_TRY(rocprim::inclusive_scan(nullptr, bytes, d_keep.as<uint8_t>(), d_pos.as<uint32_t>(), n,
+                                   rocprim::plus<uint32_t>(), s));
+    Buf tmp;
+    RK_TRY(tmp.alloc(bytes));
+    RK_TRY(rocprim::inclusive_scan(tmp.p, bytes, d_keep.as<uint8_t>(), d_pos.as<uint32_t>(), n,
+                                   rocprim::plus<uint32_t>(), s));
+  }
+  uint32_t kept = 0;
+  RK_TRY(hipMemcpyAsync(&kept, d_pos.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
+  RK_TRY(hipStreamSynchronize(s));
+  if (kept == 0) {
+    v.clear();
+    return FAC_OK;
+  }
+  RK_TRY(d_kept.alloc((uint64_t)kept * sizeof(Span)));
+  hipLaunchKernelGGL(kept_spans_kernel, dim3(G), dim3(T), 0, s, ranked, d_keep.as<uint8_t>(), d_pos.as<uint32_t>(), n,
+                     d_kept.as<Span>());
+  RK_TRY(dev_sort(d_kept.as<Span>(), d_sp2.as<Span>(), kept, KeptByStart{}, s));
+  fac_match* out = (ranked == d_a.as<fac_match>()) ? d_b.as<fac_match>() : d_a.as<fac_match>();
+  hipLaunchKernelGGL(gather_kernel, dim3((kept + T - 1) / T), dim3(T), 0, s, ranked, d_sp2.as<Span>(), (uint64_t)kept,
+                     out);
+  RK_TRY(hipGetLastError());
+  v.resize(kept);
+  RK_TRY(hipMemcpyAsync(v.data(), out, (uint64_t)kept * sizeof(fac_match), hipMemcpyDeviceToHost, s));
+  RK_TRY(hipStreamSynchronize(s));
+  return FAC_OK;
+}
+
+}  // namespace fac

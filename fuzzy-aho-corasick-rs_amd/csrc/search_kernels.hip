@@ -1478,6 +1478,7 @@ int upload_engine(Engine& e, std::string& err) {
   if ((rc = upload(e.sb_edge, &e.d_sb_edge, err))) return rc;
   if ((rc = upload(e.gt, &e.d_gt, err))) return rc;
   if ((rc = upload(e.cout, &e.d_cout, err))) return rc;
+  if ((rc = upload(e.pat_bytes, &e.d_pat_bytes, err))) return rc;
   if ((rc = upload(e.pats, &e.d_pats, err))) return rc;
   if ((rc = upload(e.sim_ascii, &e.d_sim_ascii, err))) return rc;
   if ((rc = upload(e.sim_keys, &e.d_sim_keys, err))) return rc;
@@ -1501,7 +1502,7 @@ int upload_engine(Engine& e, std::string& err) {
 void free_engine_device(Engine& e) {
   if (e.d_nodes == nullptr && e.stream == nullptr) return;
   (void)hipSetDevice(e.device);
-  void* ptrs[] = {e.d_nodes, e.d_out_range, e.d_pidx, e.d_edges, e.d_out_pat, e.d_sb_edge, e.d_gt, e.d_cout, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
+  void* ptrs[] = {e.d_nodes, e.d_out_range, e.d_pidx, e.d_edges, e.d_out_pat, e.d_sb_edge, e.d_gt, e.d_cout, e.d_pat_bytes, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
                   e.d_sim_vals, e.d_bp_mask, e.d_ascii_id};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);

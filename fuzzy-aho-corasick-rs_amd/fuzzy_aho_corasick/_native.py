@@ -95,6 +95,8 @@ SIGNATURES = {
                                          _P(fac_stats)]),
     "fac_search_staged_prefiltered": (ctypes.c_int, [_engine_p, _hay_p, ctypes.c_float, ctypes.c_void_p,
                                                      _P(_P(fac_match)), _u64p, _P(fac_stats)]),
+    "fac_matches_apply": (ctypes.c_int, [_engine_p, _P(fac_match), ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
+                                         _u64p, _u64p]),
     "fac_prefilter_windows": (ctypes.c_int64, [_engine_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_float,
                                                _u64p, ctypes.c_uint64]),
     "fac_engine_num_nodes": (ctypes.c_uint64, [_engine_p]),

@@ -190,15 +190,64 @@ class FuzzyAhoCorasick:
             _raise(rc, eg.value)
         return self._to_matches(haystack, data, _native.take_matches(out, n.value))
 
+    def _unique_ids(self):
+        """Uniqueness key per pattern for NonOverlappingUnique (matches.rs:118-122): custom ids and
+        automatic (index) ids never compare equal."""
+        if getattr(self, "_uid", None) is None:
+            keys = [(1 << 63) | p.custom_unique_id_ if p.custom_unique_id_ is not None else i
+                    for i, p in enumerate(self.patterns_)]
+            self._uid = (ctypes.c_uint64 * max(1, len(keys)))(*keys)
+        return self._uid
+
+    def _search_ranked(self, haystack: str, threshold: float, order: Order, overlap: Overlap,
+                       prefilter: bool = False) -> FuzzyMatches:
+        """search_raw + FuzzyMatches::apply, the ranking / overlap resolution on the device
+        (fac_matches_apply, matches.rs:7-149) before any Python object is built."""
+        data = haystack.encode("utf-8")
+        out = ctypes.POINTER(_native.fac_match)()
+        n = ctypes.c_uint64()
+        eg = ctypes.c_uint64()
+        fn = _native.lib.fac_search_prefiltered if prefilter else _native.lib.fac_search_raw
+        rc = fn(self._h, data, len(data), f32(threshold), ctypes.byref(out), ctypes.byref(n), ctypes.byref(eg))
+        if rc:
+            _raise(rc, eg.value)
+        count = n.value
+        if count and (order != Order.Unsorted or overlap != Overlap.Keep):
+            kept = ctypes.c_uint64()
+            rc = _native.lib.fac_matches_apply(self._h, out, count, order.value, overlap.value, self._unique_ids(),
+                                               ctypes.byref(kept))
+            if rc:
+                _native.lib.fac_matches_free(out)
+                _raise(rc)
+            count = kept.value
+        return self._to_matches(haystack, data, _native.take_matches(out, count))
+
+    def apply_on_device(self, matches: FuzzyMatches, order: Order, overlap: Overlap) -> FuzzyMatches:
+        """FuzzyMatches::apply of an existing match list through fac_matches_apply (same input
+        order in, so Unsorted + NonOverlapping walks the same sequence as the host)."""
+        n = len(matches.inner)
+        arr = (_native.fac_match * max(1, n))()
+        for i, m in enumerate(matches.inner):
+            arr[i] = _native.fac_match(m.start, m.end, m.pattern_index, m.similarity, m.insertions, m.deletions,
+                                       m.substitutions, m.swaps, m.edits)
+        kept = ctypes.c_uint64()
+        rc = _native.lib.fac_matches_apply(self._h, arr, n, order.value, overlap.value, self._unique_ids(),
+                                           ctypes.byref(kept))
+        if rc:
+            _raise(rc)
+        rows = [(a.start, a.end, a.pattern_index, a.similarity, a.insertions, a.deletions, a.substitutions, a.swaps,
+                 a.edits) for a in arr[:kept.value]]
+        return self._to_matches(matches.haystack, matches.haystack.encode("utf-8"), rows)
+
     # -- query.rs
     def search(self, haystack: str, opts: SearchOptions = None) -> FuzzyMatches:
         opts = opts or SearchOptions()
-        return self.search_raw(haystack, opts.threshold_).apply(opts.order_, opts.overlap_)
+        return self._search_ranked(haystack, opts.threshold_, opts.order_, opts.overlap_)
 
     def _segmented(self, haystack: str, opts: SearchOptions) -> FuzzyMatches:
         order = Order.Default if opts.order_ == Order.Unsorted else opts.order_
         overlap = Overlap.NonOverlapping if opts.overlap_ == Overlap.Keep else opts.overlap_
-        return self.search_raw(haystack, opts.threshold_).apply(order, overlap)
+        return self._search_ranked(haystack, opts.threshold_, order, overlap)
 
     def replace(self, text: str, opts: SearchOptions, callback) -> str:
         return self._segmented(text, opts).replace(callback)
@@ -238,7 +287,7 @@ class Prefiltered:
 
     def search(self, haystack: str, opts: SearchOptions = None) -> FuzzyMatches:
         opts = opts or SearchOptions()
-        return self.engine.search_raw(haystack, opts.threshold_, prefilter=True).apply(opts.order_, opts.overlap_)
+        return self.engine._search_ranked(haystack, opts.threshold_, opts.order_, opts.overlap_, prefilter=True)
 
 
 def prefilter_windows(engine: "FuzzyAhoCorasick", haystack: str, threshold: float):

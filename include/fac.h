@@ -174,6 +174,15 @@ int fac_search_staged(const fac_engine* engine, const fac_haystack* hay, uint64_
 int fac_search_staged_prefiltered(const fac_engine* engine, const fac_haystack* hay, float threshold,
                                   void* stream, fac_match** out, uint64_t* n_out, fac_stats* stats);
 
+/* FuzzyMatches::apply (matches.rs:7-149) on the device: rank `n` raw records in place by `order`
+ * (0 Unsorted, 1 Default, 2 Greedy, 3 CoverageWeighted; matches.rs:23-81) and resolve overlaps by
+ * `overlap` (0 Keep, 1 NonOverlapping, 2 NonOverlappingUnique; matches.rs:83-149). `unique_ids`
+ * (NULL = the pattern index) maps a pattern index to its uniqueness key for overlap 2 (distinct keys
+ * for custom_unique_id and automatic ids). The surviving records are compacted to the front of
+ * `matches`, their count written to `n_out`. */
+int fac_matches_apply(const fac_engine* engine, fac_match* matches, uint64_t n, int32_t order, int32_t overlap,
+                      const uint64_t* unique_ids, uint64_t* n_out);
+
 /* Diagnostics: the merged candidate windows (grapheme ranges [start, end)) of the bitap
  * pre-filter for `threshold` (prefilter.rs:319-342). Returns the window count (writes up to `cap`
  * pairs into `out`), or -1 if the pre-filter would fall back to a full search. */

@@ -226,3 +226,34 @@ def test_auto_beam_matches_oracle(budget, width):
         b = b.auto_beam(budget, width)
         compare(b, pats, hay, thr)
         compare(b, pats, hay, thr, prefilter=True)
+
+
+def _keyrows(ms):
+    return [(m.start, m.end, m.pattern_index, m.sim_bits()) for m in ms]
+
+
+def test_device_apply_matches_host_apply():
+    """fac_matches_apply (ranking + overlap resolution on the device, matches.rs:7-149) == the
+    host FuzzyMatches.apply the translated reference tests pin, for every order x overlap."""
+    from fuzzy_aho_corasick import Order, Overlap
+    from fuzzy_aho_corasick import workloads
+    rng = Rng(0x5151)
+    cases = []
+    for _ in range(40):
+        b, pats, hay, thr = random_case(rng, ASCII_VOCAB + UNI_VOCAB, ASCII_FILLER + UNI_FILLER)
+        pats = [Pattern.from_(p) if isinstance(p, str) else p for p in pats]
+        if rng.next() % 2:  # custom unique ids shared between patterns (matches.rs:118-122)
+            pats = [p.custom_unique_id(rng.next() % 2) if rng.next() % 2 else p for p in pats]
+        cases.append((b, pats, hay, thr))
+    w = workloads.config("c2", 48 << 10, 7)  # dense: thousands of overlapping candidates
+    cases.append((workloads.builder_for(w), w.patterns, w.haystack.decode(), 0.6))
+    for b, pats, hay, thr in cases:
+        eng = b.build(pats)
+        for order in Order:
+            for overlap in Overlap:
+                raw = eng.search_raw(hay, thr)  # one raw list in, both sides see the same order
+                dev = eng.apply_on_device(raw, order, overlap)
+                host = raw.apply(order, overlap)
+                assert _keyrows(dev) == _keyrows(host), (order, overlap, hay[:80])
+                if order != Order.Unsorted:  # the search path ranks on the device too
+                    assert _keyrows(eng._search_ranked(hay, thr, order, overlap)) == _keyrows(host)
