@@ -165,6 +165,13 @@ int fac_haystack_stage(const fac_engine* engine, const uint8_t* utf8, uint64_t l
 
 uint64_t fac_haystack_graphemes(const fac_haystack* hay) { return hay ? hay->h.n : 0; }
 
+uint64_t fac_haystack_grapheme_starts(const fac_haystack* hay, uint64_t* out, uint64_t cap) {
+  if (!hay) return 0;
+  const fac::Haystack& h = hay->h;
+  for (uint64_t g = 0; g < h.n && g < cap; ++g) out[g] = h.ascii ? g : h.starts[g];
+  return h.n;
+}
+
 void fac_haystack_free(fac_haystack* hay) {
   if (!hay) return;
   fac::free_haystack(hay->h);

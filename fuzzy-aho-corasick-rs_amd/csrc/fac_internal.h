@@ -252,7 +252,8 @@ struct Haystack {
   uint64_t* d_off = nullptr;     // Unicode only
   std::vector<uint8_t> utf8;     // host copy (prefilter slices re-decide is_ascii)
   std::vector<uint64_t> starts;  // grapheme byte starts (Unicode only)
-  std::vector<uint8_t> sym;      // prefilter symbol ids per grapheme (Unicode only)
+  mutable std::vector<uint8_t> sym;  // prefilter symbol ids per grapheme (Unicode only, lazy)
+  mutable bool sym_ready = false;
   int device = 0;
 };
 
@@ -262,6 +263,8 @@ int build_engine(const fac_pattern* pats, uint64_t n, const fac_config* cfg, Eng
 int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs, float thr,
                   hipStream_t stream, std::vector<fac_match>& out, fac_stats* stats, std::string& err);
 // bitap pre-filter: candidate windows (grapheme ranges, merged) for a staged haystack
+int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err);
+void ensure_symbols(const Engine& e, const Haystack& h);
 int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,
                   std::string& err);
 int prefilter_windows(const Engine& e, const Haystack& h, const std::vector<uint32_t>& ks, hipStream_t stream,

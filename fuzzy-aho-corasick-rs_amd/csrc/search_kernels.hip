@@ -1521,43 +1521,36 @@ int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack&
       break;
     }
   h.utf8.assign(utf8, utf8 + len);
-  if (h.ascii) {
-    h.n = len;
-  } else {
-    segment_graphemes(utf8, len, h.starts);  // search.rs:398-416
-    h.n = h.starts.size();
-  }
-  if (h.n > 0xFFFFFFFFull) return FAC_E_HAYSTACK_TOO_LARGE;
+  h.n = h.ascii ? len : 0;
   HIP_TRY(hipSetDevice(e.device));
   // All uploads go through the engine's stream and are synchronized before returning, so kernels
   // on any stream see complete data (pageable copies may otherwise still be in flight).
   hipStream_t st = e.stream;
   HIP_TRY(hipMalloc((void**)&h.d_utf8, std::max<uint64_t>(len, 16)));
   if (len) HIP_TRY(hipMemcpyAsync(h.d_utf8, utf8, len, hipMemcpyHostToDevice, st));
-  if (!h.ascii) {
-    std::vector<uint32_t> tc(h.n);
-    for (uint64_t g = 0; g < h.n; ++g) {
-      const uint64_t b = h.starts[g], en = g + 1 < h.n ? h.starts[g + 1] : len;
-      tc[g] = fold_first_char(utf8, b, en, e.case_insensitive);
-    }
-    HIP_TRY(hipMalloc((void**)&h.d_text32, std::max<uint64_t>(h.n * 4, 16)));
-    HIP_TRY(hipMemcpyAsync(h.d_text32, tc.data(), h.n * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMalloc((void**)&h.d_off, std::max<uint64_t>(h.n * 8, 16)));
-    HIP_TRY(hipMemcpyAsync(h.d_off, h.starts.data(), h.n * 8, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipStreamSynchronize(st));  // `tc` is a local buffer
-    if (e.bitap_ok) {  // transcode, grapheme path (prefilter.rs:262-280)
-      h.sym.assign(h.n, 0);
-      std::u32string g;
-      for (uint64_t i = 0; i < h.n; ++i) {
-        const uint64_t b = h.starts[i], en = i + 1 < h.n ? h.starts[i + 1] : len;
-        fold_grapheme(utf8, b, en, e.case_insensitive, g);
-        auto it = std::lower_bound(e.symbol_ids.begin(), e.symbol_ids.end(), std::make_pair(g, 0u));
-        if (it != e.symbol_ids.end() && it->first == g) h.sym[i] = (uint8_t)it->second;
-      }
-    }
+  if (!h.ascii) {  // UAX #29 segmentation + folding on the device (stage_kernels.hip)
+    const int rc = stage_unicode_device(e, h, st, err);
+    if (rc) return rc;
   }
+  if (h.n > 0xFFFFFFFFull) return FAC_E_HAYSTACK_TOO_LARGE;
   HIP_TRY(hipStreamSynchronize(st));
   return FAC_OK;
+}
+
+// Bit-parallel pre-filter transcode of a Unicode haystack (prefilter.rs:262-280): symbol id of
+// every folded grapheme, computed on first use (only pre-filtered searches need it).
+void ensure_symbols(const Engine& e, const Haystack& h) {
+  if (h.ascii || h.sym_ready) return;
+  h.sym.assign(h.n, 0);
+  std::u32string g;
+  const uint8_t* utf8 = h.utf8.data();
+  for (uint64_t i = 0; i < h.n; ++i) {
+    const uint64_t b = h.starts[i], en = i + 1 < h.n ? h.starts[i + 1] : h.len;
+    fold_grapheme(utf8, b, en, e.case_insensitive, g);
+    auto it = std::lower_bound(e.symbol_ids.begin(), e.symbol_ids.end(), std::make_pair(g, 0u));
+    if (it != e.symbol_ids.end() && it->first == g) h.sym[i] = (uint8_t)it->second;
+  }
+  h.sym_ready = true;
 }
 
 void free_haystack(Haystack& h) {
@@ -1899,6 +1892,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const std::vector<uint
                        e.d_ascii_id, static_cast<uint8_t*>(d_ids.p));
     HIP_TRY(hipGetLastError());
   } else {
+    ensure_symbols(e, h);
     HIP_TRY(hipMemcpyAsync(d_ids.p, h.sym.data(), n, hipMemcpyHostToDevice, stream));
   }
   HIP_TRY(d_m.alloc(np * 4, stream));

@@ -19,7 +19,9 @@ struct GcbRange { uint32_t lo, hi; uint8_t prop; };
 struct CpRange { uint32_t lo, hi; };
 struct LowerMap { uint32_t cp; uint32_t out[3]; uint8_t n; };
 
+#define FAC_UNICODE_QUAL
 #include "unicode_data.inc"
+#undef FAC_UNICODE_QUAL
 
 enum Gcb : uint8_t {
   GCB_Other = 0, GCB_CR, GCB_LF, GCB_Control, GCB_Extend, GCB_ZWJ, GCB_RI, GCB_Prepend,

@@ -90,6 +90,7 @@ SIGNATURES = {
                                           _P(_hay_p), _u64p]),
     "fac_haystack_graphemes": (ctypes.c_uint64, [_hay_p]),
     "fac_haystack_free": (None, [_hay_p]),
+    "fac_haystack_grapheme_starts": (ctypes.c_uint64, [_hay_p, _u64p, ctypes.c_uint64]),
     "fac_search_staged": (ctypes.c_int, [_engine_p, _hay_p, ctypes.c_uint64, ctypes.c_uint64,
                                          ctypes.c_float, ctypes.c_void_p, _P(_P(fac_match)), _u64p,
                                          _P(fac_stats)]),

@@ -157,6 +157,9 @@ uint64_t fac_max_match_graphemes(const fac_engine* engine);
 int fac_haystack_stage(const fac_engine* engine, const uint8_t* utf8, uint64_t len,
                        fac_haystack** out, uint64_t* err_graphemes);
 uint64_t fac_haystack_graphemes(const fac_haystack* hay);
+/* Byte start of every staged grapheme (the device segmentation's result, for tests / hosts that
+ * map windows to bytes). Writes up to `cap` entries, returns the grapheme count. */
+uint64_t fac_haystack_grapheme_starts(const fac_haystack* hay, uint64_t* out, uint64_t cap);
 void fac_haystack_free(fac_haystack* hay);
 
 /* Search start windows [window_begin, window_end) of a staged haystack (window_end is clamped

@@ -257,3 +257,34 @@ def test_device_apply_matches_host_apply():
                 assert _keyrows(dev) == _keyrows(host), (order, overlap, hay[:80])
                 if order != Order.Unsorted:  # the search path ranks on the device too
                     assert _keyrows(eng._search_ranked(hay, thr, order, overlap)) == _keyrows(host)
+
+
+def test_device_segmentation_matches_regex():
+    """Device UAX #29 staging (stage_kernels.hip) == the regex module's \\X on text with combining
+    marks, ZWJ emoji, flags, Hangul, Indic conjuncts, CRLF — incl. runs longer than the 1 KiB
+    resync lookback (the sequential path) and chunk boundaries inside multi-byte code points."""
+    import ctypes
+    import regex
+    from fuzzy_aho_corasick import _native
+    pieces = ["a", "é", "é", "क्ष", "क्‍ष", "👩‍💻", "🇫🇷", "🇫",
+              "\r\n", "\n", "\r", "가", "각", " ", "Ω", "̈", "‍", "ẍ́",
+              "ü", "Σ", "؀", "ः", "😀́", "👍🏽", "­", "0", "\t"]
+    rng = Rng(0x5e9)
+    texts = []
+    for _ in range(200):
+        texts.append("".join(pieces[rng.next() % len(pieces)] for _ in range(rng.next() % 1500)))
+    texts += ["a" + "́" * 3000 + "b" * 700, "🇫" * 2001 + "x", "👩‍" * 900 + "💻",
+              "क्" * 1200 + "ष ok", "é" * 5000]
+    eng = B().case_insensitive(True).build(["x"])
+    for t in texts:
+        data = t.encode("utf-8")
+        want = []
+        pos = 0
+        for g in regex.findall(r"\X", t):
+            want.append(pos)
+            pos += len(g.encode("utf-8"))
+        staged = eng.stage(data)
+        buf = (ctypes.c_uint64 * (len(data) + 1))()
+        n = _native.lib.fac_haystack_grapheme_starts(staged._h, buf, len(data) + 1)
+        got = list(buf[:n]) if not data.isascii() else list(range(len(data)))
+        assert got == want, t[:60]
