@@ -153,7 +153,7 @@ class FuzzyAhoCorasick:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h:
+        if h and _native.lib is not None:  # the module may already be torn down at exit
             _native.lib.fac_engine_free(h)
             self._h = None
 
@@ -317,7 +317,7 @@ class StagedHaystack:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h:
+        if h and _native.lib is not None:
             _native.lib.fac_haystack_free(h)
             self._h = None
 
