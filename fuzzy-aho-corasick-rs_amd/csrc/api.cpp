@@ -23,6 +23,9 @@ struct fac_engine {
 struct fac_haystack {
   fac::Haystack h;
 };
+struct fac_stream {
+  fac::StreamCore* s = nullptr;
+};
 
 namespace {
 
@@ -313,6 +316,47 @@ int fac_matches_apply(const fac_engine* engine, fac_match* matches, uint64_t n, 
   *n_out = v.size();
   return FAC_OK;
 }
+
+int fac_stream_open(const fac_engine* engine, float threshold, uint64_t window_bytes, fac_stream** out) {
+  if (!engine || !out) return fail(FAC_E_INVALID, "NULL argument");
+  fac_stream* fs = new (std::nothrow) fac_stream();
+  if (!fs) return fail(FAC_E_OOM, "out of host memory");
+  fs->s = fac::stream_open(engine->e, threshold, window_bytes);
+  *out = fs;
+  return FAC_OK;
+}
+
+int fac_stream_feed(fac_stream* stream, const uint8_t* data, uint64_t len, int32_t eof, fac_match** out,
+                    uint64_t* n_out, uint8_t** text, uint64_t* text_len) {
+  if (!stream || !out || !n_out || !text || !text_len || (len && !data)) return fail(FAC_E_INVALID, "NULL argument");
+  *out = nullptr;
+  *n_out = 0;
+  *text = nullptr;
+  *text_len = 0;
+  std::string err;
+  fac::StreamCore& s = *stream->s;
+  const int rc = fac::stream_feed(s, data, len, eof != 0, err);
+  if (rc) return fail(rc, err);
+  int r = copy_out(s.ready, out, n_out);
+  if (r) return r;
+  *text_len = s.ready_text.size();
+  *text = static_cast<uint8_t*>(std::malloc(std::max<size_t>(s.ready_text.size(), 1)));
+  if (!*text) return fail(FAC_E_OOM, "out of host memory");
+  if (!s.ready_text.empty()) std::memcpy(*text, s.ready_text.data(), s.ready_text.size());
+  s.ready.clear();
+  s.ready_text.clear();
+  return FAC_OK;
+}
+
+uint64_t fac_stream_total(const fac_stream* stream) { return stream ? stream->s->total : 0; }
+
+void fac_stream_close(fac_stream* stream) {
+  if (!stream) return;
+  fac::stream_close(stream->s);
+  delete stream;
+}
+
+void fac_buffer_free(void* p) { std::free(p); }
 
 int64_t fac_prefilter_windows(const fac_engine* engine, const uint8_t* utf8, uint64_t len, float threshold,
                               uint64_t* out, uint64_t cap) {

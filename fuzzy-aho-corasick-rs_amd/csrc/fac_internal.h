@@ -29,6 +29,7 @@ namespace fac {
 // ---------------------------------------------------------------- unicode.cpp
 uint32_t utf8_decode(const uint8_t* s, uint64_t n, uint64_t& i);
 bool utf8_valid(const uint8_t* s, uint64_t n);
+uint64_t utf8_valid_prefix(const uint8_t* s, uint64_t n);
 void segment_graphemes(const uint8_t* s, uint64_t n, std::vector<uint64_t>& starts);
 int lower_full(uint32_t cp, uint32_t out[3]);
 void fold_grapheme(const uint8_t* s, uint64_t b, uint64_t e, bool ci, std::u32string& out);
@@ -241,6 +242,11 @@ struct Engine {
   uint64_t* d_bp_mask = nullptr;
   uint8_t* d_ascii_id = nullptr;
   std::mutex mu;  // guards lazily grown scratch below
+  // per-engine device scratch of the search launcher, reused across calls by whichever call holds
+  // scratch_mu (a concurrent call on the same engine allocates its own)
+  mutable std::mutex scratch_mu;
+  mutable void* scratch_p[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  mutable size_t scratch_n[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 struct Haystack {
@@ -263,6 +269,22 @@ int build_engine(const fac_pattern* pats, uint64_t n, const fac_config* cfg, Eng
 int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs, float thr,
                   hipStream_t stream, std::vector<fac_match>& out, fac_stats* stats, std::string& err);
 // bitap pre-filter: candidate windows (grapheme ranges, merged) for a staged haystack
+// stream.cpp: the WindowReader state (stream.rs:77-159) and the matches ready to hand out
+struct StreamCore {
+  const Engine* e = nullptr;
+  float threshold = 0.f;
+  uint64_t window = 256 * 1024;  // DEFAULT_WINDOW (stream.rs:61)
+  uint64_t overlap = 1;
+  std::vector<uint8_t> buf;
+  uint64_t base = 0, total = 0;
+  bool done = false;
+  std::vector<fac_match> ready;
+  std::vector<uint8_t> ready_text;  // matched bytes of `ready`, concatenated
+};
+
+StreamCore* stream_open(const Engine& e, float threshold, uint64_t window);
+int stream_feed(StreamCore& s, const uint8_t* data, uint64_t len, bool eof, std::string& err);
+void stream_close(StreamCore* s);
 int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err);
 void ensure_symbols(const Engine& e, const Haystack& h);
 int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,

@@ -1442,17 +1442,47 @@ bool debug_poison() {
 struct DevBuf {
   void* p = nullptr;
   hipStream_t s = nullptr;
+  void** slot = nullptr;  // engine scratch slot (kept across calls) or null (owned, freed here)
+  size_t* slot_n = nullptr;
   ~DevBuf() { release(); }
+  void bind(void** sp, size_t* sn) {
+    slot = sp;
+    slot_n = sn;
+  }
   void release() {
     if (!p) return;
+    if (slot) {  // the engine keeps it; the next user orders after us on its own stream
+      (void)hipStreamSynchronize(s);
+      p = nullptr;
+      return;
+    }
     (void)hipStreamSynchronize(s);
     (void)hipFree(p);
     p = nullptr;
   }
   hipError_t alloc(size_t bytes, hipStream_t stream) {
+    bytes = std::max<size_t>(bytes, 16);
+    if (slot) {
+      p = nullptr;
+      s = stream;
+      if (*slot_n < bytes) {
+        if (*slot) {
+          (void)hipStreamSynchronize(stream);
+          (void)hipFree(*slot);
+          *slot = nullptr;
+          *slot_n = 0;
+        }
+        const size_t want = bytes + bytes / 4;
+        const hipError_t err = hipMalloc(slot, want);
+        if (err != hipSuccess) return err;
+        *slot_n = want;
+      }
+      p = *slot;
+      return hipSuccess;
+    }
     release();
     s = stream;
-    return hipMalloc(&p, std::max<size_t>(bytes, 16));
+    return hipMalloc(&p, bytes);
   }
 };
 
@@ -1506,6 +1536,12 @@ void free_engine_device(Engine& e) {
                   e.d_sim_vals, e.d_bp_mask, e.d_ascii_id};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (int i = 0; i < 8; ++i)
+    if (e.scratch_p[i]) {
+      (void)hipFree(e.scratch_p[i]);
+      e.scratch_p[i] = nullptr;
+      e.scratch_n[i] = 0;
+    }
   if (e.stream) (void)hipStreamDestroy(e.stream);
   e.stream = nullptr;
   e.d_nodes = nullptr;
@@ -1670,6 +1706,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   };
 
   DevBuf d_segs, d_prefix, d_out, d_ebuf, d_cnt, d_list, d_spill;
+  std::unique_lock<std::mutex> lease(e.scratch_mu, std::try_to_lock);
+  if (lease.owns_lock()) {  // reuse the engine's scratch (no per-call hipMalloc of the 64 MB lists)
+    DevBuf* bufs[7] = {&d_segs, &d_prefix, &d_out, &d_ebuf, &d_cnt, &d_list, &d_spill};
+    for (int i = 0; i < 7; ++i) bufs[i]->bind(&e.scratch_p[i], &e.scratch_n[i]);
+  }
   HIP_TRY(d_segs.alloc(segs.size() * sizeof(SegDesc), stream));
   HIP_TRY(d_prefix.alloc(prefix.size() * sizeof(uint64_t), stream));
   HIP_TRY(hipMemcpyAsync(d_segs.p, segs.data(), segs.size() * sizeof(SegDesc), hipMemcpyHostToDevice, stream));
@@ -1786,6 +1827,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     pass_windows = cnt[3];
     std::swap(d_list.p, d_spill.p);
     std::swap(d_list.s, d_spill.s);
+    std::swap(d_list.slot, d_spill.slot);
+    std::swap(d_list.slot_n, d_spill.slot_n);
     if (!d_spill.p || spill_cap < pass_windows) {
       HIP_TRY(d_spill.alloc(std::max<uint64_t>(spill_cap, pass_windows) * sizeof(uint64_t), stream));
       spill_cap = std::max<uint64_t>(spill_cap, pass_windows);

@@ -94,6 +94,29 @@ uint32_t utf8_decode(const uint8_t* s, uint64_t n, uint64_t& i) {
   return 0xFFFD;
 }
 
+// Length of the longest valid UTF-8 prefix (Rust's Utf8Error::valid_up_to).
+uint64_t utf8_valid_prefix(const uint8_t* s, uint64_t n) {
+  uint64_t i = 0;
+  while (i < n) {
+    uint8_t b = s[i];
+    if (b < 0x80) { ++i; continue; }
+    int len;
+    uint32_t min;
+    if ((b & 0xE0) == 0xC0) { len = 2; min = 0x80; }
+    else if ((b & 0xF0) == 0xE0) { len = 3; min = 0x800; }
+    else if ((b & 0xF8) == 0xF0) { len = 4; min = 0x10000; }
+    else return i;
+    if (i + len > n) return i;
+    for (int k = 1; k < len; ++k)
+      if ((s[i + k] & 0xC0) != 0x80) return i;
+    uint64_t j = i;
+    uint32_t cp = utf8_decode(s, n, j);
+    if (cp < min || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) return i;
+    i += len;
+  }
+  return n;
+}
+
 bool utf8_valid(const uint8_t* s, uint64_t n) {
   uint64_t i = 0;
   while (i < n) {

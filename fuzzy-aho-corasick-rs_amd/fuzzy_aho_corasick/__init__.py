@@ -5,14 +5,14 @@ FuzzyLimits, FuzzyPenalties, Pattern, SearchOptions, Order, Overlap, FuzzyMatch,
 Segment, Similarity, SearchError. The search itself runs in HIP kernels (libfac.so).
 """
 from .engine import (FuzzyAhoCorasick, FuzzyAhoCorasickBuilder, FuzzyReplacer, Prefiltered,
-                     StagedHaystack)
+                     StagedHaystack, StreamMatch)
 from .matches import FuzzyMatch, FuzzyMatches, Segment, UnmatchedSegment
 from .structs import (DEFAULT_THRESHOLD, DeviceError, FuzzyLimits, FuzzyPenalties, HaystackTooLarge,
                       Order, Overlap, Pattern, SearchError, SearchOptions, Similarity,
                       UnsupportedConfiguration)
 
 __all__ = [
-    "FuzzyAhoCorasick", "FuzzyAhoCorasickBuilder", "FuzzyReplacer", "Prefiltered", "StagedHaystack",
+    "FuzzyAhoCorasick", "FuzzyAhoCorasickBuilder", "FuzzyReplacer", "Prefiltered", "StagedHaystack", "StreamMatch",
     "FuzzyMatch", "FuzzyMatches", "Segment", "UnmatchedSegment", "DEFAULT_THRESHOLD", "DeviceError",
     "FuzzyLimits", "FuzzyPenalties", "HaystackTooLarge", "Order", "Overlap", "Pattern", "SearchError",
     "SearchOptions", "Similarity", "UnsupportedConfiguration",

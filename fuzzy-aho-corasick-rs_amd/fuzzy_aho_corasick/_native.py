@@ -98,6 +98,12 @@ SIGNATURES = {
                                                      _P(_P(fac_match)), _u64p, _P(fac_stats)]),
     "fac_matches_apply": (ctypes.c_int, [_engine_p, _P(fac_match), ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
                                          _u64p, _u64p]),
+    "fac_stream_open": (ctypes.c_int, [_engine_p, ctypes.c_float, ctypes.c_uint64, _P(ctypes.c_void_p)]),
+    "fac_stream_feed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int32,
+                                       _P(_P(fac_match)), _u64p, _P(_P(ctypes.c_uint8)), _u64p]),
+    "fac_stream_total": (ctypes.c_uint64, [ctypes.c_void_p]),
+    "fac_stream_close": (None, [ctypes.c_void_p]),
+    "fac_buffer_free": (None, [ctypes.c_void_p]),
     "fac_prefilter_windows": (ctypes.c_int64, [_engine_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_float,
                                                _u64p, ctypes.c_uint64]),
     "fac_engine_num_nodes": (ctypes.c_uint64, [_engine_p]),

@@ -222,6 +222,27 @@ class FuzzyAhoCorasick:
             count = kept.value
         return self._to_matches(haystack, data, _native.take_matches(out, count))
 
+    # -- stream.rs
+    def search_stream(self, reader, threshold: float, on_match, window: int = 0) -> int:
+        """stream.rs:299-328: search a byte stream (anything with .read(n)) in overlapping windows,
+        calling `on_match(StreamMatch)` with absolute offsets; returns the bytes read."""
+        st = _Stream(self, threshold, window)
+        while True:
+            chunk = reader.read(READ_CHUNK)
+            for m in st.feed(chunk or b"", eof=not chunk):
+                on_match(m)
+            if not chunk:
+                return st.total()
+
+    def stream_matches(self, reader, threshold: float, window: int = 0):
+        """stream.rs:330-352: the same, lazily, as an iterator of StreamMatch."""
+        st = _Stream(self, threshold, window)
+        while True:
+            chunk = reader.read(READ_CHUNK)
+            yield from st.feed(chunk or b"", eof=not chunk)
+            if not chunk:
+                return
+
     def apply_on_device(self, matches: FuzzyMatches, order: Order, overlap: Overlap) -> FuzzyMatches:
         """FuzzyMatches::apply of an existing match list through fac_matches_apply (same input
         order in, so Unsorted + NonOverlapping walks the same sequence as the host)."""
@@ -299,6 +320,62 @@ def prefilter_windows(engine: "FuzzyAhoCorasick", haystack: str, threshold: floa
     if n < 0:
         return None
     return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
+
+
+READ_CHUNK = 64 * 1024  # WindowReader's read() size (stream.rs:94)
+
+
+class StreamMatch:
+    """stream.rs:33-59: a match with absolute (stream-wide) byte offsets and its owned text."""
+    __slots__ = ("start", "end", "pattern_index", "similarity", "insertions", "deletions", "substitutions",
+                 "swaps", "edits", "text")
+
+    def __init__(self, row, text: str):
+        (self.start, self.end, self.pattern_index, self.similarity, self.insertions, self.deletions,
+         self.substitutions, self.swaps, self.edits) = row
+        self.text = text
+
+    def __repr__(self):
+        return f"StreamMatch({self.start}..{self.end} p{self.pattern_index} {self.similarity:.4f} {self.text!r})"
+
+
+class _Stream:
+    """fac_stream: WindowReader + per-window search on the GPU (stream.rs:77-297)."""
+
+    def __init__(self, engine: "FuzzyAhoCorasick", threshold: float, window: int = 0):
+        h = ctypes.c_void_p()
+        rc = _native.lib.fac_stream_open(engine._h, f32(threshold), window, ctypes.byref(h))
+        if rc:
+            _raise(rc)
+        self._h = h
+        self.engine = engine
+
+    def feed(self, data: bytes, eof: bool = False) -> List[StreamMatch]:
+        out = ctypes.POINTER(_native.fac_match)()
+        n = ctypes.c_uint64()
+        text = ctypes.POINTER(ctypes.c_uint8)()
+        tlen = ctypes.c_uint64()
+        rc = _native.lib.fac_stream_feed(self._h, data, len(data), int(eof), ctypes.byref(out), ctypes.byref(n),
+                                         ctypes.byref(text), ctypes.byref(tlen))
+        if rc:
+            _raise(rc)
+        raw = ctypes.string_at(text, tlen.value) if tlen.value else b""
+        _native.lib.fac_buffer_free(text)
+        res, pos = [], 0
+        for row in _native.take_matches(out, n.value):
+            k = row[1] - row[0]
+            res.append(StreamMatch(row, raw[pos:pos + k].decode("utf-8")))
+            pos += k
+        return res
+
+    def total(self) -> int:
+        return int(_native.lib.fac_stream_total(self._h))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _native.lib is not None:
+            _native.lib.fac_stream_close(h)
+            self._h = None
 
 
 class StagedHaystack:

@@ -186,6 +186,20 @@ int fac_search_staged_prefiltered(const fac_engine* engine, const fac_haystack* 
 int fac_matches_apply(const fac_engine* engine, fac_match* matches, uint64_t n, int32_t order, int32_t overlap,
                       const uint64_t* unique_ids, uint64_t* n_out);
 
+/* Streaming search (stream.rs:77-297): feed the input in the reader's read() pieces; windows
+ * of `window_bytes` (0 = the crate's 256 KiB) are cut, searched (sorted + non-overlapping) and
+ * their owned matches returned with absolute byte offsets, exactly like search_stream. Each feed
+ * returns the matches completed so far (`*out`, free with fac_matches_free) and their matched
+ * bytes concatenated in the same order (`*text`, match i has end - start bytes; free with
+ * fac_buffer_free). Pass eof = 1 (data may be empty) once the input has ended. */
+typedef struct fac_stream fac_stream;
+int fac_stream_open(const fac_engine* engine, float threshold, uint64_t window_bytes, fac_stream** out);
+int fac_stream_feed(fac_stream* stream, const uint8_t* data, uint64_t len, int32_t eof, fac_match** out,
+                    uint64_t* n_out, uint8_t** text, uint64_t* text_len);
+uint64_t fac_stream_total(const fac_stream* stream);
+void fac_stream_close(fac_stream* stream);
+void fac_buffer_free(void* p);
+
 /* Diagnostics: the merged candidate windows (grapheme ranges [start, end)) of the bitap
  * pre-filter for `threshold` (prefilter.rs:319-342). Returns the window count (writes up to `cap`
  * pairs into `out`), or -1 if the pre-filter would fall back to a full search. */

@@ -288,3 +288,47 @@ def test_device_segmentation_matches_regex():
         n = _native.lib.fac_haystack_grapheme_starts(staged._h, buf, len(data) + 1)
         got = list(buf[:n]) if not data.isascii() else list(range(len(data)))
         assert got == want, t[:60]
+
+
+def _srows(ms):
+    import struct
+    return [(m.start, m.end, m.pattern_index, struct.unpack("<I", struct.pack("<f", m.similarity))[0], m.text)
+            for m in ms]
+
+
+def test_streaming_apis_match_whole_input():  # tests.rs:1058-1141
+    import io
+    eng = B().fuzzy(L().edits(1)).case_insensitive(True).build(["needle"])
+    filler = "the quick brown fox " * 50
+    text = ""
+    while len(text) < 600_000:
+        text += filler + "needle "
+    truth = sorted((m.start, m.end, m.pattern_index)
+                   for m in eng.search(text, O().threshold(0.8).sorted().non_overlapping()))
+    assert len(truth) > 300
+    cb = []
+    n = eng.search_stream(io.BytesIO(text.encode()), 0.8, lambda m: cb.append(m))
+    assert n == len(text.encode())
+    assert sorted((m.start, m.end, m.pattern_index) for m in cb) == truth
+    it = list(eng.stream_matches(io.BytesIO(text.encode()), 0.8))
+    assert sorted((m.start, m.end, m.pattern_index) for m in it) == truth
+    assert all(text.encode()[m.start:m.end].decode() == m.text for m in cb)
+    hits = []
+    assert B().build(["x"]).search_stream(io.BytesIO(b""), 0.8, hits.append) == 0 and not hits  # :1144-1150
+
+
+@pytest.mark.parametrize("window", [300, 1024, 4096])
+def test_stream_windows_match_oracle_emulation(window):
+    """fac_stream (small windows: many cuts, growth, multi-byte boundaries) == the crate's
+    WindowReader + per-window search replayed on the CPU oracle."""
+    import io
+    from stream_emulation import stream_rows
+    rng = Rng(0x57 ^ window)
+    for _ in range(6):
+        b, pats, hay, thr = random_case(rng, ASCII_VOCAB + UNI_VOCAB, ASCII_FILLER + UNI_FILLER, allow_beam=False)
+        hay = (hay + " ") * (1 + rng.next() % 40)
+        eng = b.build(pats)
+        got = _srows(eng.stream_matches(io.BytesIO(hay.encode()), thr, window=window))
+        orc = OracleEngine(b, pats)
+        want = stream_rows(orc, hay.encode(), thr, eng.max_match_graphemes() + 1, window=window)
+        assert got == want, (window, pats, hay[:80])
