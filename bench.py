@@ -62,16 +62,16 @@ def main():
     graphemes = staged.graphemes
     stream = torch.cuda.current_stream().cuda_stream
 
-    from fuzzy_aho_corasick.distributed import gather_rows
+    from fuzzy_aho_corasick.distributed import gather_records
     dev = torch.device("cuda", local)
 
-    def step():
+    def step():  # records stay 32-byte structs (MATCH_DTYPE), as search_raw's Vec<OwnedMatch>
         if wl.prefilter:  # C5: bitap pre-filter + re-search of the merged windows (prefilter.rs:304-374)
-            rows, st = staged.search_prefiltered(wl.threshold, stream=stream)
+            rows, st = staged.search_prefiltered_records(wl.threshold, stream=stream)
         else:
-            rows, st = staged.search_windows(wl.threshold, stream=stream)
+            rows, st = staged.search_windows_records(wl.threshold, stream=stream)
         if world > 1:  # gather the 32 B Match records to rank 0 over RCCL (xGMI)
-            gather_rows(rows, dev)
+            gather_records(rows, dev)
         return rows, st
 
     for _ in range(args.warmup):

@@ -46,6 +46,16 @@ class fac_config(ctypes.Structure):
                 ("n_mappings", ctypes.c_uint64), ("device", ctypes.c_int32)]
 
 
+def _match_dtype():
+    import numpy as np
+    return np.dtype([("start", "<u8"), ("end", "<u8"), ("pattern_index", "<u4"), ("similarity", "<f4"),
+                     ("insertions", "u1"), ("deletions", "u1"), ("substitutions", "u1"), ("swaps", "u1"),
+                     ("edits", "u1"), ("pad", "V3")])
+
+
+MATCH_DTYPE = _match_dtype()  # the 32-byte fac_match / OwnedMatch record
+
+
 class fac_match(ctypes.Structure):
     _fields_ = [("start", ctypes.c_uint64), ("end", ctypes.c_uint64),
                 ("pattern_index", ctypes.c_uint32), ("similarity", ctypes.c_float),
@@ -131,6 +141,19 @@ def grapheme_starts(data: bytes):
     buf = (ctypes.c_uint64 * (n + 1))()
     cnt = lib.fac_segment_graphemes(data, n, buf, n + 1)
     return list(buf[:cnt])
+
+
+def take_records(ptr, n):
+    """Copy a library-allocated fac_match array into a NumPy structured array (32 B records, no
+    per-record Python objects) and free it."""
+    import numpy as np
+    try:
+        if n == 0:
+            return np.zeros(0, dtype=MATCH_DTYPE)
+        raw = ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8))
+        return np.ctypeslib.as_array(raw, shape=(n * 32,)).view(MATCH_DTYPE).copy()
+    finally:
+        lib.fac_matches_free(ptr)
 
 
 def take_matches(ptr, n):

@@ -63,6 +63,28 @@ def gather_rows(rows: Sequence[Row], device: torch.device, dst: int = 0, group=N
     return out
 
 
+def gather_records(recs, device: torch.device, dst: int = 0, group=None):
+    """gather_rows for a NumPy array of 32-byte records (fac_match): the records travel as bytes,
+    rank `dst` receives one concatenated array."""
+    import numpy as np
+    from ._native import MATCH_DTYPE
+    world = dist.get_world_size(group)
+    n = torch.tensor([len(recs)], dtype=torch.int64, device=device)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    cap = max(1, max(counts)) * REC.size
+    mine = torch.zeros(cap, dtype=torch.uint8, device=device)
+    if len(recs):
+        mine[: len(recs) * REC.size] = torch.from_numpy(np.ascontiguousarray(recs).view(np.uint8)).to(device)
+    bufs = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(bufs, mine, group=group)
+    if dist.get_rank(group) != dst:
+        return None
+    parts = [b[: c * REC.size].cpu().numpy().view(MATCH_DTYPE) for b, c in zip(bufs, counts)]
+    return np.concatenate(parts) if parts else np.zeros(0, dtype=MATCH_DTYPE)
+
+
 def sharded_search(staged, threshold: float, device: torch.device, group=None) -> Optional[List[Row]]:
     """Search one staged haystack across the group's ranks; rank 0 receives the full raw result
     (identical to search_raw on the whole haystack)."""

@@ -412,6 +412,32 @@ class StagedHaystack:
             _raise(rc)
         return _native.take_matches(out, n.value), st
 
+    def search_windows_records(self, threshold: float, window_begin: int = 0, window_end: int = None,
+                               stream=None):
+        """search_windows returning a NumPy array of 32-byte match records (MATCH_DTYPE)."""
+        if window_end is None:
+            window_end = self.graphemes
+        out = ctypes.POINTER(_native.fac_match)()
+        n = ctypes.c_uint64()
+        st = _native.fac_stats()
+        rc = _native.lib.fac_search_staged(self.engine._h, self._h, window_begin, window_end, f32(threshold),
+                                           ctypes.c_void_p(stream or 0), ctypes.byref(out), ctypes.byref(n),
+                                           ctypes.byref(st))
+        if rc:
+            _raise(rc)
+        return _native.take_records(out, n.value), st
+
+    def search_prefiltered_records(self, threshold: float, stream=None):
+        out = ctypes.POINTER(_native.fac_match)()
+        n = ctypes.c_uint64()
+        st = _native.fac_stats()
+        rc = _native.lib.fac_search_staged_prefiltered(self.engine._h, self._h, f32(threshold),
+                                                       ctypes.c_void_p(stream or 0), ctypes.byref(out),
+                                                       ctypes.byref(n), ctypes.byref(st))
+        if rc:
+            _raise(rc)
+        return _native.take_records(out, n.value), st
+
     def search_prefiltered(self, threshold: float, stream=None):
         """Prefiltered::raw on the device-resident text (prefilter.rs:146-155, 304-374): raw rows
         (best per (start, end, pattern), sorted) + fac_stats (prefilter_ms = bitap + merge)."""
