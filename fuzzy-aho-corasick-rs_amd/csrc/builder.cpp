@@ -385,10 +385,11 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
       bool ok = true;
       for (auto& kvv : ent) {
         uint64_t kv = kvv.first, val = kvv.second;
-        uint32_t pos = gt_slot(kv, e.gt_seed1, e.gt_mask);
+        uint32_t pos = 0;
         bool placed = false;
         for (int kick = 0; kick < 500 && !placed; ++kick) {
-          const uint32_t p1 = gt_slot(kv, e.gt_seed1, e.gt_mask), p2 = gt_slot(kv, e.gt_seed2, e.gt_mask);
+          uint32_t p1, p2;
+          gt_slots(kv, e.gt_seed1, e.gt_mask, p1, p2);
           for (uint32_t p : {p1, p2}) {
             if (e.gt[p].x == 0 && e.gt[p].y == 0) {
               e.gt[p] = uint4{(uint32_t)kv, (uint32_t)(kv >> 32), (uint32_t)val, (uint32_t)(val >> 32)};

@@ -48,11 +48,19 @@ constexpr uint64_t GT_VALID = 1ull << 63;
 constexpr uint64_t GT_GOTO = 0, GT_SB = 1ull << 47;
 // 2-choice cuckoo table of 16 B entries {kv, val}: a key lives at gt_slot(kv, seed1) or
 // gt_slot(kv, seed2); lookups read both slots, no probing
-__host__ __device__ inline uint32_t gt_slot(uint64_t kv, uint64_t seed, uint32_t mask) {
-  uint64_t x = (kv ^ seed) * 0x9E3779B97F4A7C15ull;
-  x ^= x >> 29;
-  x *= 0xBF58476D1CE4E5B9ull;
-  return (uint32_t)(x >> 32) & mask;
+__host__ __device__ inline uint32_t gt_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+// both cuckoo slots from one 32-bit hash of the 47-bit key: low bits and the 16-bit rotation
+__host__ __device__ inline void gt_slots(uint64_t kv, uint64_t seed, uint32_t mask, uint32_t& s1, uint32_t& s2) {
+  const uint32_t h = gt_mix32((uint32_t)kv ^ gt_mix32((uint32_t)(kv >> 32) ^ (uint32_t)seed));
+  s1 = h & mask;
+  s2 = ((h >> 16) | (h << 16)) & mask;
 }
 constexpr int32_t LIM_NONE = -1;
 

@@ -158,8 +158,10 @@ __device__ __forceinline__ bool node_has_out(const DevNode& n) { return (n.degf 
 
 // goto-table lookup (fac_internal.h): both cuckoo slots read at once, branch-free
 __device__ __forceinline__ bool gt_get(const SearchParams& P, uint64_t kv, bool live, uint64_t& val) {
-  const uint4 a = P.gt[live ? gt_slot(kv, P.gt_seed1, P.gt_mask) : 0u];
-  const uint4 b = P.gt[live ? gt_slot(kv, P.gt_seed2, P.gt_mask) : 0u];
+  uint32_t s1, s2;
+  gt_slots(kv, P.gt_seed1, P.gt_mask, s1, s2);
+  const uint4 a = P.gt[live ? s1 : 0u];
+  const uint4 b = P.gt[live ? s2 : 0u];
   const uint32_t lo = (uint32_t)kv, hi = (uint32_t)(kv >> 32);
   const bool ma = a.x == lo && a.y == hi, mb = b.x == lo && b.y == hi;
   val = ma ? (((uint64_t)a.w << 32) | a.z) : mb ? (((uint64_t)b.w << 32) | b.z) : 0ull;
