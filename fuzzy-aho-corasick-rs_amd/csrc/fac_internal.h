@@ -56,11 +56,21 @@ __host__ __device__ inline uint32_t gt_mix32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-// both cuckoo slots from one 32-bit hash of the 47-bit key: low bits and the 16-bit rotation
-__host__ __device__ inline void gt_slots(uint64_t kv, uint64_t seed, uint32_t mask, uint32_t& s1, uint32_t& s2) {
-  const uint32_t h = gt_mix32((uint32_t)kv ^ gt_mix32((uint32_t)(kv >> 32) ^ (uint32_t)seed));
+// both cuckoo slots from one 32-bit hash: a base hash of (node, char) shared by the GOTO and SB
+// keys of that pair (the SB hash is an affine step away), low bits and the 16-bit rotation
+__host__ __device__ inline uint32_t gt_base(uint32_t node, uint32_t ch, uint64_t seed) {
+  return gt_mix32(((node << 21) | ch) ^ gt_mix32((node >> 11) ^ (uint32_t)seed));
+}
+__host__ __device__ inline uint32_t gt_kind_hash(uint32_t base, bool sb) {
+  return sb ? base * 0x9E3779B1u + 0x7F4A7C15u : base;
+}
+__host__ __device__ inline void gt_slots_h(uint32_t h, uint32_t mask, uint32_t& s1, uint32_t& s2) {
   s1 = h & mask;
   s2 = ((h >> 16) | (h << 16)) & mask;
+}
+__host__ __device__ inline void gt_slots(uint64_t kv, uint64_t seed, uint32_t mask, uint32_t& s1, uint32_t& s2) {
+  const uint32_t node = (uint32_t)((kv >> 21) & ((1u << 26) - 1)), ch = (uint32_t)(kv & ((1u << 21) - 1));
+  gt_slots_h(gt_kind_hash(gt_base(node, ch, seed), (kv & GT_SB) != 0), mask, s1, s2);
 }
 constexpr int32_t LIM_NONE = -1;
 
