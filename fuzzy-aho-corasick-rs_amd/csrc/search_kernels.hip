@@ -967,7 +967,8 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
 
   while (head < tail) {
     PROF_T(t0);
-    if (P.beam && tail - head > beam2) beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
+    if constexpr (VCAP > 0)  // dedup-free variants run unbeamed engines only (launch_pass fits())
+      if (P.beam && tail - head > beam2) beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
     PROF_ACC(0, t0);
     PROF_T(t1);
     const uint32_t B = min(tail - head, 64u);
@@ -1310,7 +1311,7 @@ __global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
   bfs_window_body<VCAP, QCAP>(P);
 }
 template <uint32_t QCAP>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void bfs_window_kernel_nd(SearchParams P) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QCAP <= 512 ? 4 : 1))) void bfs_window_kernel_nd(SearchParams P) {
   bfs_window_body<0, QCAP>(P);
 }
 
@@ -1477,19 +1478,21 @@ void launch_one(uint32_t grid, hipStream_t s, const SearchParams& P) {
 }
 
 // LDS per wave: 16 B x (vcap + qcap) + vcap claim bytes
-constexpr Variant kVariants[] = {{0, 128},   {0, 256},    {0, 512},     {256, 256},
-                                 {512, 256}, {512, 512},  {1024, 1024}, {2048, 2048}};
+constexpr Variant kVariants[] = {{0, 128},   {0, 256},   {0, 512},     {256, 256},   {512, 256},
+                                 {512, 512}, {1024, 1024}, {2048, 2048}, {4096, 4096}, {0, 8192}};
 
 hipError_t launch_variant(const Variant& v, uint32_t grid, hipStream_t s, const SearchParams& P) {
-  switch (v.vcap * 4096u + v.qcap) {
-    case 0 * 4096u + 128: launch_nd<128>(grid, s, P); break;
-    case 0 * 4096u + 256: launch_nd<256>(grid, s, P); break;
-    case 0 * 4096u + 512: launch_nd<512>(grid, s, P); break;
-    case 256 * 4096u + 256: launch_one<256, 256>(grid, s, P); break;
-    case 512 * 4096u + 256: launch_one<512, 256>(grid, s, P); break;
-    case 512 * 4096u + 512: launch_one<512, 512>(grid, s, P); break;
-    case 1024 * 4096u + 1024: launch_one<1024, 1024>(grid, s, P); break;
-    default: launch_one<2048, 2048>(grid, s, P); break;
+  switch (v.vcap * 16384u + v.qcap) {
+    case 0 * 16384u + 128: launch_nd<128>(grid, s, P); break;
+    case 0 * 16384u + 256: launch_nd<256>(grid, s, P); break;
+    case 0 * 16384u + 512: launch_nd<512>(grid, s, P); break;
+    case 256 * 16384u + 256: launch_one<256, 256>(grid, s, P); break;
+    case 512 * 16384u + 256: launch_one<512, 256>(grid, s, P); break;
+    case 512 * 16384u + 512: launch_one<512, 512>(grid, s, P); break;
+    case 1024 * 16384u + 1024: launch_one<1024, 1024>(grid, s, P); break;
+    case 2048 * 16384u + 2048: launch_one<2048, 2048>(grid, s, P); break;
+    case 4096 * 16384u + 4096: launch_one<4096, 4096>(grid, s, P); break;  // 136 KB LDS: one wave per CU
+    default: launch_nd<8192>(grid, s, P); break;                          // 130 KB, dedup-free (unbeamed)
   }
   return hipGetLastError();
 }
@@ -1774,6 +1777,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     const uint32_t want_v = std::max<uint32_t>(kVariants[cur].vcap * 2, 512);
     for (size_t i = cur + 1; i < nv; ++i)
       if (fits(kVariants[i]) && kVariants[i].vcap >= want_v && kVariants[i].qcap >= kVariants[cur].qcap) return i;
+    // past the largest table: an unbeamed, non-exact engine may still trade the table for a
+    // longer ring (dedup never changes unbeamed results)
+    for (size_t i = cur + 1; i < nv; ++i)
+      if (fits(kVariants[i]) && kVariants[i].vcap == 0 && kVariants[i].qcap > kVariants[cur].qcap) return i;
     return nv;
   };
 

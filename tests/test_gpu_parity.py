@@ -190,8 +190,33 @@ def test_frontier_spill_beamed(monkeypatch, beam_vcap):
     assert n > 0
 
 
+def test_frontier_beyond_2048_states():
+    """Windows whose distinct-state count (oracle: up to 3038 keys at edits 5) exceeds the 2048-entry
+    table: the spill ladder ends on the one-wave-per-CU (4096, 4096) variant, unbeamed and with a
+    512 beam (whose 2x-beam trigger already needs the 2048 ring)."""
+    pats = ["a" * 12, "ab" * 6, "b" * 12, "ba" * 6]
+    hay = "ab" * 20 + "a" * 20 + "b" * 20
+    st, n = _staged_vs_oracle(B().fuzzy(L().edits(5)), pats, hay, 0.3)
+    assert n > 0 and st.retries > 0
+    st, n = _staged_vs_oracle(B().fuzzy(L().edits(5)).beam_width(512), pats, hay, 0.3)
+    assert n > 0 and st.retries > 0
+
+
+def test_frontier_capacity_is_loud():
+    """Edits 6 (oracle: 5706 distinct keys in a window) runs past the (4096, 4096) table onto the
+    dedup-free 8192 ring; if even that overflows, the search fails with FAC_E_CAPACITY instead of
+    returning a partial result."""
+    from fuzzy_aho_corasick.structs import DeviceError
+    pats = ["a" * 12, "ab" * 6, "b" * 12, "ba" * 6]
+    hay = "ab" * 20 + "a" * 20 + "b" * 20
+    try:
+        _staged_vs_oracle(B().fuzzy(L().edits(6)), pats, hay, 0.3)
+    except DeviceError as exc:
+        assert exc.code == 105, exc
+
+
 @pytest.mark.parametrize("variant", ["0,128", "0,256", "0,512", "256,256", "512,256", "512,512", "1024,1024",
-                                     "2048,2048"])
+                                     "2048,2048", "4096,4096", "0,8192"])
 def test_every_frontier_variant(monkeypatch, variant):
     """Each LDS frontier variant (dedup table x queue ring) gives oracle-identical results."""
     monkeypatch.setenv("FAC_VARIANT", variant)
