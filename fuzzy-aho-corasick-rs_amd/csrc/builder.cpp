@@ -336,7 +336,10 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
   // ---- O(1) expansion tables: (node, char) goto entries and child single-byte maps for nodes of
   // degree <= 64, plus each node's child-has-output mask (used by the kernels' fast path)
   {
-    e.cout.assign(nn, 0ull);
+    e.aux.assign(nn, uint4{0, 0, 0, 0});
+    for (size_t i = 0; i < nn; ++i)
+      for (uint32_t m = e.nodes[i].edge_begin; m < e.nodes[i].edge_end; ++m)
+        e.aux[i].z |= 1u << ch_filt_bit(e.edges[m].ch);
     std::vector<std::pair<uint64_t, uint64_t>> ent;  // (kv, val)
     std::unordered_map<uint64_t, size_t> at;         // kv -> index in ent
     auto put = [&](uint64_t kv) -> uint64_t& {
@@ -355,14 +358,18 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
         const uint64_t key = ((uint64_t)i << 21) | ed.ch;
         const bool existed = at.count(GT_VALID | GT_GOTO | key) != 0;
         uint64_t& g = put(GT_VALID | GT_GOTO | key);
-        if (!existed) g = child | ((uint64_t)std::min<uint32_t>(k, 255) << 32);  // first edge, this first char
+        if (!existed)  // first edge with this first char; the child's folded char filter on top
+          g = child | ((uint64_t)std::min<uint32_t>(k, 255) << 32) | ((uint64_t)filt_fold16(e.aux[child].z) << 48);
         if (ed.next & EDGE_SINGLE_BYTE) g |= 1ull << 40;
         if (deg > 64) continue;  // child maps only for the fast path's nodes
-        if (ed.next & EDGE_CHILD_OUTPUT) e.cout[i] |= 1ull << k;
+        if (ed.next & EDGE_CHILD_OUTPUT) (k < 32 ? e.aux[i].x : e.aux[i].y) |= 1u << (k & 31u);
         const HostNode& c = e.nodes[child];
         for (uint32_t m = c.edge_begin; m < c.edge_end; ++m) {
           const DevEdge& ce = e.edges[m];
-          if ((ce.next & EDGE_SINGLE_BYTE) && ce.ch < 128) put(GT_VALID | GT_SB | ((uint64_t)i << 21) | ce.ch) |= 1ull << k;
+          if ((ce.next & EDGE_SINGLE_BYTE) && ce.ch < 128) {
+            put(GT_VALID | GT_SB | ((uint64_t)i << 21) | ce.ch) |= 1ull << k;
+            e.aux[i].w |= 1u << ch_filt_bit(ce.ch);
+          }
         }
       }
     }

@@ -61,6 +61,10 @@ __host__ __device__ inline uint32_t gt_mix32(uint32_t x) {
 __host__ __device__ inline uint32_t gt_base(uint32_t node, uint32_t ch, uint64_t seed) {
   return gt_mix32(((node << 21) | ch) ^ gt_mix32((node >> 11) ^ (uint32_t)seed));
 }
+// char filters (Engine::aux, GOTO values bits 48-63): one bit per hashed code point, a clear bit
+// proves the (node, char) lookup would miss
+__host__ __device__ inline uint32_t ch_filt_bit(uint32_t c) { return (c * 0x9E3779B1u) >> 27; }
+__host__ __device__ inline uint32_t filt_fold16(uint32_t f) { return (f | (f >> 16)) & 0xFFFFu; }
 __host__ __device__ inline uint32_t gt_kind_hash(uint32_t base, bool sb) {
   return sb ? base * 0x9E3779B1u + 0x7F4A7C15u : base;
 }
@@ -147,7 +151,9 @@ struct SearchParams {
   uint32_t gt_mask;           // slot count - 1
   unsigned long long gt_seed1, gt_seed2;
   int32_t gt_fast;            // similarity can never drop a substitution when p_sub <= remaining
-  const unsigned long long* cout;  // per node: bit i = child of edge i has output (degree <= 64)
+  // per node {child-has-output mask lo, hi (degree <= 64), child char filter, grandchild single-byte
+  // char filter}: the filters (bit ch_filt_bit(c)) gate goto-table lookups that would miss
+  const uint4* aux;
   const uint4* sb_edge;
   const DevPattern* pats;
   const float* sim_ascii;
@@ -221,7 +227,7 @@ struct Engine {
   uint32_t gt_mask = 0;
   uint64_t gt_seed1 = 0, gt_seed2 = 0;
   bool gt_fast = false;
-  std::vector<unsigned long long> cout;
+  std::vector<uint4> aux;  // SearchParams::aux
   std::vector<uint32_t> pat_bytes;  // Pattern::len (bytes, structs.rs:628-630) for ranking
   std::vector<DevPattern> pats;
   std::vector<float> sim_ascii;
@@ -251,7 +257,7 @@ struct Engine {
   int32_t* d_pidx = nullptr;
   uint4* d_sb_edge = nullptr;
   uint4* d_gt = nullptr;
-  unsigned long long* d_cout = nullptr;
+  uint4* d_aux = nullptr;
   uint32_t* d_pat_bytes = nullptr;
   DevPattern* d_pats = nullptr;
   float* d_sim_ascii = nullptr;

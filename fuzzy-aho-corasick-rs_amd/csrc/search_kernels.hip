@@ -748,25 +748,35 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
 
 // O(1) expansion of one state (deg <= 64) when similarity cannot drop a substitution
 // (gt_fast && p_sub <= remaining, see builder.cpp): every edge is a substitution and deletion
-// candidate, filtered at the last edit by "child has output" (cout) and "child has a single-byte
+// candidate, filtered at the last edit by "child has output" (aux.xy) and "child has a single-byte
 // edge for the tested char" (GT_SB maps), exactly the per-edge tests of expand_units; the exact and
-// swap edges are the goto entries of text[j] and text[j+1].
-__device__ void expand_fast(const SearchParams& P, const KState& st, const DevNode& nd, const Prep& pr, uint64_t cout,
+// swap edges are the goto entries of text[j] and text[j+1]. A lookup whose char filter bit is clear
+// (aux.z: the node's edge chars, aux.w: its children's single-byte chars) is known to miss and is
+// not issued; a swap edge whose child's folded filter rules out text[j] has no swap target.
+__device__ __forceinline__ bool filt_has(uint32_t f, uint32_t c) { return (f >> ch_filt_bit(c)) & 1u; }
+
+__device__ void expand_fast(const SearchParams& P, const KState& st, const DevNode& nd, const Prep& pr, uint4 aux,
                             uint64_t& msub, uint64_t& mdel, uint32_t& ex, uint32_t& xe) {
   const uint32_t deg = node_deg(nd);
   const uint64_t dm = deg >= 64u ? ~0ull : ((1ull << deg) - 1ull);
   const bool is_last = pr.flags & PF_LAST, in_text = pr.flags & PF_EX, sub_on = pr.flags & PF_SUB;
   const bool del_ok = pr.flags & PF_DEL, swap_ok = pr.flags & PF_SWAP;
   const uint64_t nk = GT_VALID | ((uint64_t)st.node << 21);
-  const bool ns0 = is_last && del_ok && (pr.flags & PF_CUR) && pr.cur_ch < 128u;
-  const bool ns1 = is_last && sub_on && (pr.flags & PF_NEXT) && pr.next_ch < 128u;
+  const uint64_t cout = ((uint64_t)aux.y << 32) | aux.x;
+  const bool l0 = in_text && filt_has(aux.z, pr.cur_ch);
+  const bool l1 = swap_ok && filt_has(aux.z, pr.nch);
+  const bool ns0 = is_last && del_ok && (pr.flags & PF_CUR) && pr.cur_ch < 128u && filt_has(aux.w, pr.cur_ch);
+  const bool ns1 = is_last && sub_on && (pr.flags & PF_NEXT) && pr.next_ch < 128u && filt_has(aux.w, pr.next_ch);
   // one base hash per (node, char); c1 serves both the swap edge and the next-char dead-end map
   const uint32_t b0 = gt_base(st.node, pr.cur_ch, P.gt_seed1);
   const uint32_t c1 = (pr.flags & PF_SWAP) ? pr.nch : pr.next_ch;
   const uint32_t b1 = gt_base(st.node, c1, P.gt_seed1);
-  uint64_t g0, g1, s0 = 0, s1 = 0;  // lookups in flight together
-  const bool h0 = gt_get_h(P, nk | GT_GOTO | pr.cur_ch, b0, in_text, g0);
-  const bool h1 = gt_get_h(P, nk | GT_GOTO | pr.nch, b1, swap_ok, g1);
+  uint64_t g0 = 0, g1 = 0, s0 = 0, s1 = 0;  // lookups in flight together
+  bool h0 = false, h1 = false;
+  if (__ballot(l0 || l1)) {
+    h0 = gt_get_h(P, nk | GT_GOTO | pr.cur_ch, b0, l0, g0);
+    h1 = gt_get_h(P, nk | GT_GOTO | pr.nch, b1, l1, g1);
+  }
   if (__ballot(ns0 || ns1)) {  // child single-byte maps: last edit on an ASCII char only
     gt_get_h(P, nk | GT_SB | pr.cur_ch, gt_kind_hash(b0, true), ns0, s0);
     gt_get_h(P, nk | GT_SB | pr.next_ch, gt_kind_hash(b1, true), ns1, s1);
@@ -777,7 +787,8 @@ __device__ void expand_fast(const SearchParams& P, const KState& st, const DevNo
     ex = ((63u - k) << 26) | (uint32_t)(g0 & CHILD26_MASK);
     exbit = 1ull << k;
   }
-  if (h1) xe = ((63u - ((uint32_t)(g1 >> 32) & 0xFFu)) << 26) | (uint32_t)(g1 & CHILD26_MASK);
+  if (h1 && ((uint32_t)(g1 >> 48) >> (ch_filt_bit(pr.cur_ch) & 15u) & 1u))
+    xe = ((63u - ((uint32_t)(g1 >> 32) & 0xFFu)) << 26) | (uint32_t)(g1 & CHILD26_MASK);
   msub = sub_on ? (dm & ~exbit & (is_last ? (cout | s1) : ~0ull)) : 0ull;
   mdel = del_ok ? (dm & (is_last ? (cout | s0) : ~0ull)) : 0ull;
 }
@@ -979,10 +990,10 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     // text at j and j + 1) and overlap the dedup probe; then dedup, node ceiling, width
     DevNode nd{};
     uint32_t c0 = 0, c1 = 0;
-    uint64_t cout = 0;
+    uint4 aux = make_uint4(0, 0, 0, 0);
     if (in_b) {
       nd = P.nodes[st.node];
-      cout = P.cout[st.node];
+      aux = P.aux[st.node];
       const uint64_t j = start + (st.jm & 0xFFFFu);
       if (j < S.n) c0 = text_char(P, S, j, err);
       if (j + 1 < S.n) c1 = text_char(P, S, j + 1, err);
@@ -1037,7 +1048,7 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     const bool fast = act && P.gt_fast && (!(pr.flags & PF_SUB) || P.p_sub <= pr.remaining);
     if (__ballot(act && !fast))  // per-edge path for the states similarity can prune
       expand_units<FAC_UK>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act && !fast, msub, mdel, ex, xe);
-    if (fast) expand_fast(P, st, nd, pr, cout, msub, mdel, ex, xe);
+    if (fast) expand_fast(P, st, nd, pr, aux, msub, mdel, ex, xe);
 #if defined(FAC_DUP) && FAC_DUP == 1
     if (fast) {
       KState s2{opq(st.node), opq(st.jm), opqf(st.pen), opq(st.packed)};
@@ -1046,7 +1057,7 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
       Prep p2{opq(pr.cur_ch), opq(pr.next_ch), opq(pr.nch), opq(pr.flags), opqf(pr.remaining)};
       uint64_t a = 0, b = 0;
       uint32_t c = 0, d = 0;
-      expand_fast(P, s2, n2, p2, opq64(cout), a, b, c, d);
+      expand_fast(P, s2, n2, p2, make_uint4(opq(aux.x), opq(aux.y), opq(aux.z), opq(aux.w)), a, b, c, d);
       sink64(a);
       sink64(b);
       sink(c);
@@ -1582,7 +1593,7 @@ int upload_engine(Engine& e, std::string& err) {
   if ((rc = upload(e.out_pat, &e.d_out_pat, err))) return rc;
   if ((rc = upload(e.sb_edge, &e.d_sb_edge, err))) return rc;
   if ((rc = upload(e.gt, &e.d_gt, err))) return rc;
-  if ((rc = upload(e.cout, &e.d_cout, err))) return rc;
+  if ((rc = upload(e.aux, &e.d_aux, err))) return rc;
   if ((rc = upload(e.pat_bytes, &e.d_pat_bytes, err))) return rc;
   if ((rc = upload(e.pats, &e.d_pats, err))) return rc;
   if ((rc = upload(e.sim_ascii, &e.d_sim_ascii, err))) return rc;
@@ -1607,7 +1618,7 @@ int upload_engine(Engine& e, std::string& err) {
 void free_engine_device(Engine& e) {
   if (e.d_nodes == nullptr && e.stream == nullptr) return;
   (void)hipSetDevice(e.device);
-  void* ptrs[] = {e.d_nodes, e.d_out_range, e.d_pidx, e.d_edges, e.d_out_pat, e.d_sb_edge, e.d_gt, e.d_cout, e.d_pat_bytes, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
+  void* ptrs[] = {e.d_nodes, e.d_out_range, e.d_pidx, e.d_edges, e.d_out_pat, e.d_sb_edge, e.d_gt, e.d_aux, e.d_pat_bytes, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
                   e.d_sim_vals, e.d_bp_mask, e.d_ascii_id};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -1707,7 +1718,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.gt_seed1 = e.gt_seed1;
   P.gt_seed2 = e.gt_seed2;
   P.gt_fast = (e.gt_fast && !std::getenv("FAC_NO_FAST")) ? 1 : 0;  // env: A/B knob
-  P.cout = e.d_cout;
+  P.aux = e.d_aux;
   P.pats = e.d_pats;
   P.sim_ascii = e.d_sim_ascii;
   P.sim_keys = e.d_sim_keys;
