@@ -195,6 +195,15 @@ struct SearchParams {
   // auto-beam pass 1 (search.rs:1096-1103): per window queue.len() under exact dedup
   uint32_t* win_counts;  // null: not recorded
   int32_t exact_dedup;   // dedup must be exact (beam, or counting for auto-beam)
+  // root-pop cache (launch_pass): the root's pushes, and the beam selection right after them, depend
+  // only on (text[start], text[start + 1], start + 1 < n); windows sharing that key copy them
+  int32_t rc_mode;                  // 0 off, 1 use the cache, 2 build it (win_list = rc_rep)
+  const unsigned long long* rc_keys;  // open-addressing table of keys (0 = empty)
+  const uint32_t* rc_val;           // entry of each key slot (EMPTY: not cached)
+  uint32_t rc_mask;                 // table slots - 1
+  uint32_t rc_stride;               // states per entry
+  KState* rc_states;                // [entry][rc_stride]
+  uint32_t* rc_count;               // states of each entry (EMPTY: not cached)
 };
 
 constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8u, ERR_OUT = 16u, ERR_SPILL = 32u;
@@ -269,8 +278,9 @@ struct Engine {
   // per-engine device scratch of the search launcher, reused across calls by whichever call holds
   // scratch_mu (a concurrent call on the same engine allocates its own)
   mutable std::mutex scratch_mu;
-  mutable void* scratch_p[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  mutable size_t scratch_n[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  static constexpr int kScratch = 16;
+  mutable void* scratch_p[kScratch] = {};
+  mutable size_t scratch_n[kScratch] = {};
 };
 
 struct Haystack {

@@ -961,7 +961,8 @@ __device__ unsigned long long g_prof[16];
 // the beam would trigger, and before the first >64-edge node (expanded alone, edge-parallel).
 template <uint32_t VCAP, uint32_t QCAP>
 __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
-                           uint32_t& cseq, EmitList& EL, uint64_t start, uint64_t& popped, unsigned& err) {
+                           uint32_t& cseq, EmitList& EL, uint64_t start, uint32_t rce, uint64_t& popped,
+                           unsigned& err) {
   const uint32_t lane = lane_id();
 #ifdef FAC_PHASE_PROF
   uint64_t prof_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -972,7 +973,16 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
   uint32_t vcount = 0;
   EL.n = 0;
   uint32_t head = 0, tail = 1;
-  if (lane == 0) q[0] = KState{0u, 0u, 0.0f, 0u};
+  if (rce != EMPTY) {  // root-pop cache hit: the root is popped, its (beam-selected) pushes copied
+    const uint32_t cnt = P.rc_count[rce];
+    const KState* src = P.rc_states + (size_t)rce * P.rc_stride;
+    for (uint32_t i = lane; i < cnt; i += 64) q[(1u + i) & (QCAP - 1)] = src[i];
+    head = 1;
+    tail = 1 + cnt;
+    popped += 1;
+  } else if (lane == 0) {
+    q[0] = KState{0u, 0u, 0.0f, 0u};
+  }
   __builtin_amdgcn_wave_barrier();
   const uint32_t beam2 = 2u * P.beam;
 
@@ -980,6 +990,7 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     PROF_T(t0);
     if constexpr (VCAP > 0)  // dedup-free variants run unbeamed engines only (launch_pass fits())
       if (P.beam && tail - head > beam2) beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
+    if (P.rc_mode == 2 && head > 0) break;  // cache build: stop after the root pop (+ selection)
     PROF_ACC(0, t0);
     PROF_T(t1);
     const uint32_t B = min(tail - head, 64u);
@@ -1256,6 +1267,72 @@ __device__ __forceinline__ uint32_t find_seg(const SearchParams& P, uint64_t v) 
   return lo;
 }
 
+// Root-pop cache key of a window: its first two text chars and whether the second exists. 0: the
+// window is not cacheable (second char beyond the resident halo).
+__device__ __forceinline__ uint64_t rc_key(const SearchParams& P, const SegDesc& S, uint64_t s, unsigned& err) {
+  const uint32_t c0 = text_char(P, S, s, err);
+  const bool has1 = s + 1 < S.n;
+  if (has1 && s + 1 >= S.avail) return 0ull;
+  const uint32_t c1 = has1 ? text_char(P, S, s + 1, err) : 0u;
+  return (1ull << 63) | ((uint64_t)has1 << 62) | ((uint64_t)c1 << 21) | c0;
+}
+__device__ __forceinline__ uint32_t rc_hash(uint64_t k) {
+  return gt_mix32((uint32_t)k ^ gt_mix32((uint32_t)(k >> 32) ^ 0x5bd1e995u));
+}
+constexpr uint32_t RC_PROBES = 32;
+
+template <uint32_t QCAP>
+__device__ __forceinline__ uint32_t rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s) {
+  unsigned e2 = 0;
+  const uint64_t k = rc_key(P, S, s, e2);
+  if (!k) return EMPTY;
+  const uint32_t h = rc_hash(k);
+  for (uint32_t p = 0; p < RC_PROBES; ++p) {
+    const uint32_t slot = (h + p) & P.rc_mask;
+    const unsigned long long kk = P.rc_keys[slot];
+    if (kk == k) {
+      const uint32_t ent = P.rc_val[slot];
+      if (ent == EMPTY) return EMPTY;
+      const uint32_t cnt = P.rc_count[ent];
+      return (cnt != EMPTY && cnt + 1u <= QCAP) ? ent : EMPTY;
+    }
+    if (kk == 0ull) return EMPTY;
+  }
+  return EMPTY;
+}
+
+// Root-pop cache keys: every searched window's key is inserted once (plain probe first, CAS only on
+// an empty slot); the inserting window becomes the entry's representative (rc_rep).
+__global__ __launch_bounds__(256) void rc_collect_kernel(SearchParams P, unsigned long long* keys, uint32_t* val,
+                                                         uint64_t* rep, unsigned int* n_ent, uint32_t max_ent) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  unsigned err = 0;
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < P.total_windows; v += stride) {
+    const uint64_t vid = P.win_list ? P.win_list[v] : v;
+    const uint32_t kl = find_seg(P, vid);
+    const SegDesc S = P.segs[kl];
+    const uint64_t start = S.w_begin + (vid - P.seg_prefix[kl]);
+    if (window_skipped(P, S, start, err)) continue;
+    const uint64_t k = rc_key(P, S, start, err);
+    if (!k) continue;
+    const uint32_t h = rc_hash(k);
+    for (uint32_t p = 0; p < RC_PROBES; ++p) {
+      const uint32_t slot = (h + p) & P.rc_mask;
+      unsigned long long kk = keys[slot];
+      if (kk == 0ull) {
+        kk = atomicCAS(&keys[slot], 0ull, (unsigned long long)k);
+        if (kk == 0ull) {
+          const uint32_t ent = atomicAdd(n_ent, 1u);
+          if (ent < max_ent) rep[ent] = vid;
+          val[slot] = ent < max_ent ? ent : EMPTY;
+          break;
+        }
+      }
+      if (kk == k) break;
+    }
+  }
+}
+
 template <uint32_t VCAP, uint32_t QCAP>
 __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   __shared__ KState s_vis[VCAP ? VCAP : 1];
@@ -1285,6 +1362,8 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         start = S.w_begin + (vid - P.seg_prefix[kl]);
         active = !window_skipped(P, S, start, err);
       }
+      uint32_t rce = EMPTY;  // root-pop cache entry of this lane's window
+      if (P.rc_mode == 1 && active) rce = rc_lookup<QCAP>(P, P.segs[kl], start);
       uint64_t m = __ballot(active);
       while (m) {
         const int l = first_lane(m);
@@ -1292,7 +1371,20 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         const uint32_t seg = shfl_u32(kl, l);
         const uint64_t st = shfl_u64(start, l);
         const SegDesc S = P.segs[seg];
-        const uint32_t qlen = run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, popped, err);
+        const uint32_t qlen =
+            run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, shfl_u32(rce, l), popped, err);
+        if (P.rc_mode == 2) {  // cache build: entry = list position; an overflow leaves it uncached
+          const uint32_t ent = (uint32_t)(v0 + (uint64_t)l);
+          const bool bad = (wave_or(err) & (ERR_QUEUE | ERR_VISITED)) != 0 || qlen - 1u > P.rc_stride;
+          if (!bad)
+            for (uint32_t i = lane; i + 1u < qlen; i += 64)
+              P.rc_states[(size_t)ent * P.rc_stride + i] = s_q[(1u + i) & (QCAP - 1)];
+          if (lane == 0) P.rc_count[ent] = bad ? EMPTY : qlen - 1u;
+          err &= ~(ERR_QUEUE | ERR_VISITED);
+          __builtin_amdgcn_wave_barrier();
+          if (any_err(err)) break;
+          continue;
+        }
         const bool overflow = (wave_or(err) & (ERR_QUEUE | ERR_VISITED)) != 0;
         if (P.win_counts && !overflow && lane == 0) P.win_counts[shfl_u64(vid, l)] = qlen;
         if (overflow) {  // frontier overflow: spill the window
@@ -1622,7 +1714,7 @@ void free_engine_device(Engine& e) {
                   e.d_sim_vals, e.d_bp_mask, e.d_ascii_id};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < Engine::kScratch; ++i)
     if (e.scratch_p[i]) {
       (void)hipFree(e.scratch_p[i]);
       e.scratch_p[i] = nullptr;
@@ -1796,10 +1888,12 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   };
 
   DevBuf d_segs, d_prefix, d_out, d_ebuf, d_cnt, d_list, d_spill;
+  DevBuf d_rck, d_rcv, d_rcrep, d_rcs, d_rcc, d_rcn;  // root-pop cache
   std::unique_lock<std::mutex> lease(e.scratch_mu, std::try_to_lock);
   if (lease.owns_lock()) {  // reuse the engine's scratch (no per-call hipMalloc of the 64 MB lists)
-    DevBuf* bufs[7] = {&d_segs, &d_prefix, &d_out, &d_ebuf, &d_cnt, &d_list, &d_spill};
-    for (int i = 0; i < 7; ++i) bufs[i]->bind(&e.scratch_p[i], &e.scratch_n[i]);
+    DevBuf* bufs[13] = {&d_segs, &d_prefix, &d_out, &d_ebuf, &d_cnt, &d_list, &d_spill,
+                        &d_rck,  &d_rcv,    &d_rcrep, &d_rcs, &d_rcc, &d_rcn};
+    for (int i = 0; i < 13; ++i) bufs[i]->bind(&e.scratch_p[i], &e.scratch_n[i]);
   }
   HIP_TRY(d_segs.alloc(segs.size() * sizeof(SegDesc), stream));
   HIP_TRY(d_prefix.alloc(prefix.size() * sizeof(uint64_t), stream));
@@ -1831,6 +1925,68 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   unsigned long long cnt[4] = {0, 0, 0, 0};
   float ms_total = 0.f;
   out.clear();
+
+  // Root-pop cache (rc_collect_kernel, then the window kernel in build mode over one representative
+  // window per key): skipped when the root emits (an empty pattern) or the search is small.
+  P.rc_mode = 0;
+  const bool root_out = !e.nodes.empty() && e.nodes[0].out_end > e.nodes[0].out_begin;
+  const char* rc_min = std::getenv("FAC_RC_MIN");  // env knobs: tests force it on, A/B turns it off
+  if (!root_out && windows >= (rc_min ? std::strtoull(rc_min, nullptr, 10) : 4096ull) && !std::getenv("FAC_NO_RC")) {
+    const uint32_t slots = 1u << 16, max_ent = (uint32_t)std::min<uint64_t>(windows, 16384);
+    const uint32_t stride = (uint32_t)(beam ? std::min<uint64_t>(fan_root, 2ull * beam) : fan_root);
+    HIP_TRY(d_rck.alloc(slots * sizeof(unsigned long long), stream));
+    HIP_TRY(d_rcv.alloc(slots * sizeof(uint32_t), stream));
+    HIP_TRY(d_rcrep.alloc(max_ent * sizeof(uint64_t), stream));
+    HIP_TRY(d_rcs.alloc((size_t)max_ent * stride * sizeof(KState), stream));
+    HIP_TRY(d_rcc.alloc(max_ent * sizeof(uint32_t), stream));
+    HIP_TRY(d_rcn.alloc(sizeof(unsigned int), stream));
+    HIP_TRY(hipMemsetAsync(d_rck.p, 0, slots * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(d_rcv.p, 0xFF, slots * sizeof(uint32_t), stream));
+    HIP_TRY(hipMemsetAsync(d_rcn.p, 0, sizeof(unsigned int), stream));
+    P.rc_keys = static_cast<const unsigned long long*>(d_rck.p);
+    P.rc_val = static_cast<const uint32_t*>(d_rcv.p);
+    P.rc_mask = slots - 1;
+    P.rc_stride = stride;
+    P.rc_states = static_cast<KState*>(d_rcs.p);
+    P.rc_count = static_cast<uint32_t*>(d_rcc.p);
+    HIP_TRY(hipEventRecord(ev.a, stream));
+    const uint32_t cgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256, (uint64_t)cus * 8));
+    hipLaunchKernelGGL(rc_collect_kernel, dim3(cgrid), dim3(256), 0, stream, P,
+                       static_cast<unsigned long long*>(d_rck.p), static_cast<uint32_t*>(d_rcv.p),
+                       static_cast<uint64_t*>(d_rcrep.p), static_cast<unsigned int*>(d_rcn.p), max_ent);
+    HIP_TRY(hipGetLastError());
+    unsigned int n_ent = 0;
+    HIP_TRY(hipMemcpyAsync(&n_ent, d_rcn.p, sizeof(n_ent), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    n_ent = std::min(n_ent, max_ent);
+    if (n_ent) {
+      SearchParams Q = P;
+      Q.rc_mode = 2;
+      Q.win_list = static_cast<const uint64_t*>(d_rcrep.p);
+      Q.total_windows = n_ent;
+      Q.chunk = 1;
+      Q.win_counts = nullptr;
+      Q.ebuf = static_cast<uint4*>(d_ebuf.p);
+      Q.out = static_cast<fac_match*>(d_out.p);
+      Q.out_cap = out_cap;
+      Q.spill = static_cast<uint64_t*>(d_spill.p);
+      Q.spill_cap = spill_cap;
+      Q.counters = static_cast<unsigned long long*>(d_cnt.p);
+      HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 4 * sizeof(unsigned long long), stream));
+      const hipError_t le = launch_variant(kVariants[vi], std::min<uint32_t>(n_ent, max_grid), stream, Q);
+      if (le != hipSuccess) {
+        err = std::string("kernel launch: ") + hipGetErrorString(le);
+        return FAC_E_HIP;
+      }
+      P.rc_mode = 1;
+    }
+    HIP_TRY(hipEventRecord(ev.b, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+    ms_total += ms;
+    launches += n_ent ? 2 : 1;
+  }
   for (;;) {
     P.chunk = P.win_list ? 1u : 256u;  // spilled windows are few and heavy: one per block turn
     P.total_windows = pass_windows;

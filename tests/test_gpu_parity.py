@@ -79,16 +79,19 @@ def random_case(rng, vocab, filler, allow_beam=True, allow_limits=True):
     return b, pats, hay, thr
 
 
+@pytest.mark.parametrize("root_cache", ["off", "forced"])
 @pytest.mark.parametrize("per_edge_only", [False, True])
 @pytest.mark.parametrize("seed,vocab,filler", [
     (0x1234_5678_9abc_def1, ASCII_VOCAB, ASCII_FILLER),
     (0xdead_beef_0bad_f00d, UNI_VOCAB, UNI_FILLER),
 ])
-def test_differential_random(seed, vocab, filler, per_edge_only, monkeypatch):
+def test_differential_random(seed, vocab, filler, per_edge_only, root_cache, monkeypatch):
     """per_edge_only: FAC_NO_FAST disables the O(1) goto-table expansion, so the per-edge unit
-    path is checked on every state as well."""
+    path is checked on every state as well. root_cache: the root-pop cache off, or forced on for
+    every search (it is normally used from 4096 windows on)."""
     if per_edge_only:
         monkeypatch.setenv("FAC_NO_FAST", "1")
+    monkeypatch.setenv(*(("FAC_NO_RC", "1") if root_cache == "off" else ("FAC_RC_MIN", "1")))
     rng = Rng(seed)
     total = 0
     for _ in range(150):
@@ -242,9 +245,11 @@ def test_staged_prefiltered_matches_oracle(seed, vocab, filler):
 
 
 @pytest.mark.parametrize("budget,width", [(0, 2), (5, 4), (40, 8), (300, 3), (2 ** 64 - 1, 8)])
-def test_auto_beam_matches_oracle(budget, width):
+def test_auto_beam_matches_oracle(budget, width, monkeypatch):
     """auto_beam (search.rs:1096-1103): GPU two-pass (exact counting pass, beamed tail) == the
-    oracle's sequential budget, per search_raw call, incl. the pre-filter's per-window calls."""
+    oracle's sequential budget, per search_raw call, incl. the pre-filter's per-window calls
+    (root-pop cache forced on: pass 1 records queue.len() through cached roots too)."""
+    monkeypatch.setenv("FAC_RC_MIN", "1")
     rng = Rng(0xab ^ budget)
     for _ in range(40):
         b, pats, hay, thr = random_case(rng, ASCII_VOCAB + UNI_VOCAB, ASCII_FILLER + UNI_FILLER, allow_beam=False)
