@@ -1417,6 +1417,12 @@ template <uint32_t QCAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QCAP <= 512 ? 4 : 1))) void bfs_window_kernel_nd(SearchParams P) {
   bfs_window_body<0, QCAP>(P);
 }
+// root-pop cache build (P.rc_mode == 2): one representative window per key, root pop + selection
+// only; its own symbol so profiles separate it from the search launches
+template <uint32_t QCAP>
+__global__ __launch_bounds__(64) void rc_build_kernel(SearchParams P) {
+  bfs_window_body<256, QCAP>(P);
+}
 
 // ------------------------------------------------------------------------------------------
 // Bit-parallel pre-filter (prefilter.rs:247-435)
@@ -1583,6 +1589,17 @@ void launch_one(uint32_t grid, hipStream_t s, const SearchParams& P) {
 // LDS per wave: 16 B x (vcap + qcap) + vcap claim bytes
 constexpr Variant kVariants[] = {{0, 128},   {0, 256},   {0, 512},     {256, 256},   {512, 256},
                                  {512, 512}, {1024, 1024}, {2048, 2048}, {4096, 4096}, {0, 8192}};
+
+// ring for the cache build: the root's pushes (fan_root) after the popped root
+bool launch_rc_build(uint64_t fan_root, uint32_t grid, hipStream_t s, const SearchParams& P) {
+  if (fan_root + 1 <= 256) hipLaunchKernelGGL((rc_build_kernel<256>), dim3(grid), dim3(64), 0, s, P);
+  else if (fan_root + 1 <= 512) hipLaunchKernelGGL((rc_build_kernel<512>), dim3(grid), dim3(64), 0, s, P);
+  else if (fan_root + 1 <= 1024) hipLaunchKernelGGL((rc_build_kernel<1024>), dim3(grid), dim3(64), 0, s, P);
+  else if (fan_root + 1 <= 2048) hipLaunchKernelGGL((rc_build_kernel<2048>), dim3(grid), dim3(64), 0, s, P);
+  else if (fan_root + 1 <= 4096) hipLaunchKernelGGL((rc_build_kernel<4096>), dim3(grid), dim3(64), 0, s, P);
+  else return false;
+  return true;
+}
 
 hipError_t launch_variant(const Variant& v, uint32_t grid, hipStream_t s, const SearchParams& P) {
   switch (v.vcap * 16384u + v.qcap) {
@@ -1923,7 +1940,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   int rc = FAC_OK;
   uint64_t retries = 0, launches = 0, popped = 0, pass_windows = windows;
   unsigned long long cnt[4] = {0, 0, 0, 0};
-  float ms_total = 0.f;
+  float ms_total = 0.f, cache_ms = 0.f;
   out.clear();
 
   // Root-pop cache (rc_collect_kernel, then the window kernel in build mode over one representative
@@ -1931,7 +1948,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.rc_mode = 0;
   const bool root_out = !e.nodes.empty() && e.nodes[0].out_end > e.nodes[0].out_begin;
   const char* rc_min = std::getenv("FAC_RC_MIN");  // env knobs: tests force it on, A/B turns it off
-  if (!root_out && windows >= (rc_min ? std::strtoull(rc_min, nullptr, 10) : 4096ull) && !std::getenv("FAC_NO_RC")) {
+  if (!root_out && fan_root + 1 <= 4096 && windows >= (rc_min ? std::strtoull(rc_min, nullptr, 10) : 4096ull) &&
+      !std::getenv("FAC_NO_RC")) {
     const uint32_t slots = 1u << 16, max_ent = (uint32_t)std::min<uint64_t>(windows, 16384);
     const uint32_t stride = (uint32_t)(beam ? std::min<uint64_t>(fan_root, 2ull * beam) : fan_root);
     HIP_TRY(d_rck.alloc(slots * sizeof(unsigned long long), stream));
@@ -1973,7 +1991,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       Q.spill_cap = spill_cap;
       Q.counters = static_cast<unsigned long long*>(d_cnt.p);
       HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 4 * sizeof(unsigned long long), stream));
-      const hipError_t le = launch_variant(kVariants[vi], std::min<uint32_t>(n_ent, max_grid), stream, Q);
+      launch_rc_build(fan_root, std::min<uint32_t>(n_ent, max_grid), stream, Q);
+      const hipError_t le = hipGetLastError();
       if (le != hipSuccess) {
         err = std::string("kernel launch: ") + hipGetErrorString(le);
         return FAC_E_HIP;
@@ -1982,10 +2001,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     }
     HIP_TRY(hipEventRecord(ev.b, stream));
     HIP_TRY(hipStreamSynchronize(stream));
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
-    ms_total += ms;
-    launches += n_ent ? 2 : 1;
+    HIP_TRY(hipEventElapsedTime(&cache_ms, ev.a, ev.b));
   }
   for (;;) {
     P.chunk = P.win_list ? 1u : 256u;  // spilled windows are few and heavy: one per block turn
@@ -2090,6 +2106,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   if (stats) {
     stats->kernel_ms += ms_total;
     stats->kernel_launches += launches;
+    stats->cache_ms += cache_ms;
     stats->windows += windows;
     stats->states_popped += popped;
     stats->graphemes = h.n;

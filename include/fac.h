@@ -112,7 +112,7 @@ typedef struct fac_match {
 
 /* Per-call device statistics (filled when the pointer is non-NULL). */
 typedef struct fac_stats {
-  double kernel_ms;        /* HIP-event time of the search kernel(s) on the call's stream */
+  double kernel_ms;        /* HIP-event time of the window search kernel(s) on the call's stream */
   double prefilter_ms;     /* HIP-event time of the bitap scan + window merge (0 if unused) */
   uint64_t kernel_launches;
   uint64_t windows;        /* start windows searched */
@@ -120,6 +120,7 @@ typedef struct fac_stats {
   uint64_t graphemes;      /* haystack graphemes */
   uint64_t bytes;          /* haystack UTF-8 bytes */
   uint64_t retries;        /* capacity retries */
+  double cache_ms;         /* HIP-event time of the root-pop cache build (key collection + root pops) */
 } fac_stats;
 
 typedef struct fac_engine fac_engine;
