@@ -1576,14 +1576,23 @@ struct Variant {
   uint32_t vcap, qcap;  // vcap 0: no dedup table (unbeamed engines only)
 };
 
+// FAC_LDS_PAD (bytes of unused dynamic LDS per workgroup): occupancy experiments only
+uint32_t lds_pad() {
+  static const uint32_t v = [] {
+    const char* e = std::getenv("FAC_LDS_PAD");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+  }();
+  return v;
+}
+
 template <uint32_t Q>
 void launch_nd(uint32_t grid, hipStream_t s, const SearchParams& P) {
-  hipLaunchKernelGGL((bfs_window_kernel_nd<Q>), dim3(grid), dim3(64), 0, s, P);
+  hipLaunchKernelGGL((bfs_window_kernel_nd<Q>), dim3(grid), dim3(64), lds_pad(), s, P);
 }
 
 template <uint32_t V, uint32_t Q>
 void launch_one(uint32_t grid, hipStream_t s, const SearchParams& P) {
-  hipLaunchKernelGGL((bfs_window_kernel<V, Q>), dim3(grid), dim3(64), 0, s, P);
+  hipLaunchKernelGGL((bfs_window_kernel<V, Q>), dim3(grid), dim3(64), lds_pad(), s, P);
 }
 
 // LDS per wave: 16 B x (vcap + qcap) + vcap claim bytes
