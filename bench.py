@@ -80,11 +80,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kernel_ms, launches, matches, popped, prefilter_ms, cache_ms = 0.0, 0, 0, 0, 0.0, 0.0
+    kernel_ms, launches, matches, popped, prefilter_ms, cache_ms, cached = 0.0, 0, 0, 0, 0.0, 0.0, 0
     for _ in range(args.steps):
         rows, st = step()
         prefilter_ms += st.prefilter_ms
         cache_ms += st.cache_ms
+        cached += st.states_cached
         kernel_ms += st.kernel_ms
         launches += st.kernel_launches
         matches += len(rows)
@@ -172,7 +173,8 @@ def main():
                 "kernel_launches": launches,
                 "search_kernel_ms_per_step": kernel_ms / max(1, args.steps),
                 "prefilter_ms_per_step": prefilter_ms / max(1, args.steps),
-                "root_cache_ms_per_step": cache_ms / max(1, args.steps),
+                "prefix_cache_ms_per_step": cache_ms / max(1, args.steps),
+                "states_from_prefix_cache_per_step": cached / max(1, args.steps),
             },
         }
         print(json.dumps(line))

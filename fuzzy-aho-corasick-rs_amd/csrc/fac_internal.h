@@ -195,15 +195,20 @@ struct SearchParams {
   // auto-beam pass 1 (search.rs:1096-1103): per window queue.len() under exact dedup
   uint32_t* win_counts;  // null: not recorded
   int32_t exact_dedup;   // dedup must be exact (beam, or counting for auto-beam)
-  // root-pop cache (launch_pass): the root's pushes, and the beam selection right after them, depend
-  // only on (text[start], text[start + 1], start + 1 < n); windows sharing that key copy them
+  // prefix cache (launch_pass): a state at j reads text[j] and text[j + 1], so the
+  // pops before the first state with j >= rc_k - 1 depend only on the window's first rc_k chars;
+  // windows sharing them resume from one snapshot (queue, dedup entries, best list, counters)
   int32_t rc_mode;                  // 0 off, 1 use the cache, 2 build it (win_list = rc_rep)
+  uint32_t rc_k;                    // key chars (2 or 3)
   const unsigned long long* rc_keys;  // open-addressing table of keys (0 = empty)
   const uint32_t* rc_val;           // entry of each key slot (EMPTY: not cached)
   uint32_t rc_mask;                 // table slots - 1
-  uint32_t rc_stride;               // states per entry
-  KState* rc_states;                // [entry][rc_stride]
-  uint32_t* rc_count;               // states of each entry (EMPTY: not cached)
+  uint32_t rc_vmax, rc_emax;        // dedup / best-list entries a snapshot may hold
+  uint4* rc_pool;                   // snapshots: header x2, queue, dedup entries, best list
+  unsigned long long rc_pool_cap;   // pool words (uint4)
+  unsigned long long* rc_pool_used; // bump allocator
+  uint32_t* rc_off;                 // snapshot offset of each entry (pool words)
+  uint32_t* rc_count;               // queued states of each entry (EMPTY: not cached)
 };
 
 constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8u, ERR_OUT = 16u, ERR_SPILL = 32u;

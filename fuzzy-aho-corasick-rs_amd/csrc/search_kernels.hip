@@ -962,7 +962,7 @@ __device__ unsigned long long g_prof[16];
 template <uint32_t VCAP, uint32_t QCAP>
 __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
                            uint32_t& cseq, EmitList& EL, uint64_t start, uint32_t rce, uint64_t& popped,
-                           unsigned& err) {
+                           uint64_t& cached, unsigned& err, uint32_t& head_out, uint32_t& vcount_out) {
   const uint32_t lane = lane_id();
 #ifdef FAC_PHASE_PROF
   uint64_t prof_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -973,13 +973,31 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
   uint32_t vcount = 0;
   EL.n = 0;
   uint32_t head = 0, tail = 1;
-  if (rce != EMPTY) {  // root-pop cache hit: the root is popped, its (beam-selected) pushes copied
-    const uint32_t cnt = P.rc_count[rce];
-    const KState* src = P.rc_states + (size_t)rce * P.rc_stride;
-    for (uint32_t i = lane; i < cnt; i += 64) q[(1u + i) & (QCAP - 1)] = src[i];
-    head = 1;
-    tail = 1 + cnt;
-    popped += 1;
+  if (rce != EMPTY) {  // prefix cache hit: resume from the snapshot of the key's representative
+    const uint4* src = P.rc_pool + rce;
+    const uint4 h0 = src[0], h1 = src[1];  // {head, tail, dedup entries, pops}, {best entries}; [2]: chars
+    src += 3;
+    head = h0.x;
+    tail = h0.y;
+    for (uint32_t i = lane; i < tail - head; i += 64) {
+      const uint4 w = src[i];
+      q[(head + i) & (QCAP - 1)] = KState{w.x, w.y, __uint_as_float(w.z), w.w};
+    }
+    if constexpr (VCAP > 0) {  // the popped keys with their stored penalties (slots re-hashed)
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t i = lane; i < h0.z; i += 64) {
+        const uint4 w = src[(tail - head) + i];
+        uint32_t slot = vis_hash(KState{w.x, w.y, 0.f, w.w}) & (VCAP - 1);
+        while (atomicCAS(&vis[slot].node, EMPTY, w.x) != EMPTY) slot = (slot + 1) & (VCAP - 1);
+        vis[slot].jm = w.y;
+        vis[slot].pen = __uint_as_float(w.z);
+        vis[slot].packed = w.w;
+      }
+      vcount = h0.z;
+    }
+    for (uint32_t i = lane; i < h1.x; i += 64) EL.buf[i] = src[(tail - head) + h0.z + i];
+    EL.n = h1.x;
+    cached += h0.w;  // the snapshot's pops (not counted as popped: that is executed work)
   } else if (lane == 0) {
     q[0] = KState{0u, 0u, 0.0f, 0u};
   }
@@ -990,7 +1008,8 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     PROF_T(t0);
     if constexpr (VCAP > 0)  // dedup-free variants run unbeamed engines only (launch_pass fits())
       if (P.beam && tail - head > beam2) beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
-    if (P.rc_mode == 2 && head > 0) break;  // cache build: stop after the root pop (+ selection)
+    // cache build: stop before the first state that reads text past the key
+    if (P.rc_mode == 2 && (q[head & (QCAP - 1)].jm & 0xFFFFu) + 1u >= P.rc_k) break;
     PROF_ACC(0, t0);
     PROF_T(t1);
     const uint32_t B = min(tail - head, 64u);
@@ -1102,7 +1121,8 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     const uint32_t P0 = tail - head;
     const bool trig = lane >= 1 && lane < Bc && P.beam && (P0 - lane + excl > beam2);
     const bool ovf = lane < Bc && (P0 - lane - 1 + incl > QCAP);
-    const uint64_t mcut = __ballot(trig) | __ballot(ovf);
+    const bool past = P.rc_mode == 2 && lane < Bc && (st.jm & 0xFFFFu) + 1u >= P.rc_k;  // cache build
+    const uint64_t mcut = __ballot(trig) | __ballot(ovf) | __ballot(past);
     if (mcut) Bc = min(Bc, (uint32_t)first_lane(mcut));
     if (Bc == 0) {
       err |= ERR_QUEUE;
@@ -1210,10 +1230,13 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     if (any_err(err)) break;
   }
 
+  head_out = head;
+  vcount_out = vcount;
   // flush this window's best map (search.rs:1111-1118)
   wave_mem_fence();
-  // a window that overflowed the frontier is spilled whole (re-run on a larger variant): no flush
-  if (EL.n && !(wave_or(err) & (ERR_EMIT | ERR_QUEUE | ERR_VISITED))) {
+  // a window that overflowed the frontier is spilled whole (re-run on a larger variant): no flush;
+  // a cache build's representative is searched again by the main pass: no flush either
+  if (EL.n && P.rc_mode != 2 && !(wave_or(err) & (ERR_EMIT | ERR_QUEUE | ERR_VISITED))) {
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(P.counters, (unsigned long long)EL.n);
     base = shfl_u64(base, 0);
@@ -1267,25 +1290,36 @@ __device__ __forceinline__ uint32_t find_seg(const SearchParams& P, uint64_t v) 
   return lo;
 }
 
-// Root-pop cache key of a window: its first two text chars and whether the second exists. 0: the
-// window is not cacheable (second char beyond the resident halo).
-__device__ __forceinline__ uint64_t rc_key(const SearchParams& P, const SegDesc& S, uint64_t s, unsigned& err) {
-  const uint32_t c0 = text_char(P, S, s, err);
-  const bool has1 = s + 1 < S.n;
-  if (has1 && s + 1 >= S.avail) return 0ull;
-  const uint32_t c1 = has1 ? text_char(P, S, s + 1, err) : 0u;
-  return (1ull << 63) | ((uint64_t)has1 << 62) | ((uint64_t)c1 << 21) | c0;
+// Prefix-cache key of a window: its first rc_k chars (0x1FFFFF past the end of the text) and a
+// 64-bit hash of them (top bit set: 0 marks an empty table slot). A snapshot stores the chars and a
+// lookup compares them, so hash collisions only cost a cache miss. False: not cacheable (a char
+// inside the text but beyond the resident halo).
+__device__ __forceinline__ bool rc_key(const SearchParams& P, const SegDesc& S, uint64_t s, uint4& ch, uint64_t& key) {
+  unsigned e2 = 0;
+  uint32_t c[4] = {0x1FFFFFu, 0x1FFFFFu, 0x1FFFFFu, 0x1FFFFFu};
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i)
+    if (i < P.rc_k && s + i < S.n) {
+      if (s + i >= S.avail) return false;
+      c[i] = text_char(P, S, s + i, e2);
+    }
+  ch = make_uint4(c[0], c[1], c[2], c[3]);
+  const uint64_t a = ((uint64_t)c[1] << 21) | c[0], b = ((uint64_t)c[3] << 21) | c[2];
+  uint64_t h = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull) * 0xD6E8FEB86659FD93ull;
+  h ^= h >> 32;
+  h *= 0xD6E8FEB86659FD93ull;
+  h ^= h >> 29;
+  key = h | (1ull << 63);
+  return true;
 }
-__device__ __forceinline__ uint32_t rc_hash(uint64_t k) {
-  return gt_mix32((uint32_t)k ^ gt_mix32((uint32_t)(k >> 32) ^ 0x5bd1e995u));
-}
+__device__ __forceinline__ uint32_t rc_hash(uint64_t k) { return (uint32_t)k ^ (uint32_t)(k >> 32); }
 constexpr uint32_t RC_PROBES = 32;
 
 template <uint32_t QCAP>
 __device__ __forceinline__ uint32_t rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s) {
-  unsigned e2 = 0;
-  const uint64_t k = rc_key(P, S, s, e2);
-  if (!k) return EMPTY;
+  uint4 ch;
+  uint64_t k;
+  if (!rc_key(P, S, s, ch, k)) return EMPTY;
   const uint32_t h = rc_hash(k);
   for (uint32_t p = 0; p < RC_PROBES; ++p) {
     const uint32_t slot = (h + p) & P.rc_mask;
@@ -1293,15 +1327,17 @@ __device__ __forceinline__ uint32_t rc_lookup(const SearchParams& P, const SegDe
     if (kk == k) {
       const uint32_t ent = P.rc_val[slot];
       if (ent == EMPTY) return EMPTY;
-      const uint32_t cnt = P.rc_count[ent];
-      return (cnt != EMPTY && cnt + 1u <= QCAP) ? ent : EMPTY;
+      const uint32_t cnt = P.rc_count[ent], off = P.rc_off[ent];
+      if (cnt == EMPTY || cnt + 1u > QCAP) return EMPTY;
+      const uint4 sc = P.rc_pool[off + 2];  // the snapshot's own chars
+      return (sc.x == ch.x && sc.y == ch.y && sc.z == ch.z && sc.w == ch.w) ? off : EMPTY;
     }
     if (kk == 0ull) return EMPTY;
   }
   return EMPTY;
 }
 
-// Root-pop cache keys: every searched window's key is inserted once (plain probe first, CAS only on
+// Prefix-cache keys: every searched window's key is inserted once (plain probe first, CAS only on
 // an empty slot); the inserting window becomes the entry's representative (rc_rep).
 __global__ __launch_bounds__(256) void rc_collect_kernel(SearchParams P, unsigned long long* keys, uint32_t* val,
                                                          uint64_t* rep, unsigned int* n_ent, uint32_t max_ent) {
@@ -1313,8 +1349,9 @@ __global__ __launch_bounds__(256) void rc_collect_kernel(SearchParams P, unsigne
     const SegDesc S = P.segs[kl];
     const uint64_t start = S.w_begin + (vid - P.seg_prefix[kl]);
     if (window_skipped(P, S, start, err)) continue;
-    const uint64_t k = rc_key(P, S, start, err);
-    if (!k) continue;
+    uint4 ch;
+    uint64_t k;
+    if (!rc_key(P, S, start, ch, k)) continue;
     const uint32_t h = rc_hash(k);
     for (uint32_t p = 0; p < RC_PROBES; ++p) {
       const uint32_t slot = (h + p) & P.rc_mask;
@@ -1340,7 +1377,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   __shared__ __attribute__((aligned(16))) uint32_t s_claim[claim_slots(VCAP)];
   const uint32_t lane = lane_id();
   EmitList EL{P.ebuf + (size_t)blockIdx.x * P.ecap, P.ecap, 0};
-  uint64_t popped = 0;
+  uint64_t popped = 0, cached = 0;
   // dedup-commit claim sequence (phase C): fresh claims are >= 128, above any stale word the
   // expansion scratch leaves behind (<= 64)
   uint32_t cseq = 1;
@@ -1362,7 +1399,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         start = S.w_begin + (vid - P.seg_prefix[kl]);
         active = !window_skipped(P, S, start, err);
       }
-      uint32_t rce = EMPTY;  // root-pop cache entry of this lane's window
+      uint32_t rce = EMPTY;  // prefix-cache snapshot (pool offset) of this lane's window
       if (P.rc_mode == 1 && active) rce = rc_lookup<QCAP>(P, P.segs[kl], start);
       uint64_t m = __ballot(active);
       while (m) {
@@ -1371,16 +1408,52 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         const uint32_t seg = shfl_u32(kl, l);
         const uint64_t st = shfl_u64(start, l);
         const SegDesc S = P.segs[seg];
-        const uint32_t qlen =
-            run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, shfl_u32(rce, l), popped, err);
-        if (P.rc_mode == 2) {  // cache build: entry = list position; an overflow leaves it uncached
+        const uint64_t popped0 = popped;
+        uint32_t qhead = 0, vcnt = 0;
+        const uint32_t qlen = run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, shfl_u32(rce, l), popped,
+                                                     cached, err, qhead, vcnt);
+        if (P.rc_mode == 2) {  // cache build: entry = list position; what does not fit stays uncached
           const uint32_t ent = (uint32_t)(v0 + (uint64_t)l);
-          const bool bad = (wave_or(err) & (ERR_QUEUE | ERR_VISITED)) != 0 || qlen - 1u > P.rc_stride;
-          if (!bad)
-            for (uint32_t i = lane; i + 1u < qlen; i += 64)
-              P.rc_states[(size_t)ent * P.rc_stride + i] = s_q[(1u + i) & (QCAP - 1)];
-          if (lane == 0) P.rc_count[ent] = bad ? EMPTY : qlen - 1u;
-          err &= ~(ERR_QUEUE | ERR_VISITED);
+          const uint32_t nq = qlen - qhead;
+          uint32_t nv = 0;  // occupied dedup slots
+          if constexpr (VCAP > 0)
+            for (uint32_t b = 0; b < VCAP; b += 64) nv += (uint32_t)__popcll(__ballot(s_vis[b + lane].node != EMPTY));
+          bool bad = (wave_or(err) & (ERR_QUEUE | ERR_VISITED | ERR_EMIT)) != 0 || EL.n > P.rc_emax || nv > P.rc_vmax;
+          const uint32_t words = 3 + nq + nv + EL.n;
+          unsigned long long off = 0;
+          if (lane == 0 && !bad) off = atomicAdd(P.rc_pool_used, (unsigned long long)words);
+          off = shfl_u64(off, 0);
+          bad = bad || off + words > P.rc_pool_cap || off > 0xFFFFFFF0ull;
+          uint4 kch;
+          uint64_t kkey;
+          bad = bad || !rc_key(P, S, st, kch, kkey);
+          uint4* dst = P.rc_pool + off + 3;  // after the three header words
+          for (uint32_t i = lane; i < nq && !bad; i += 64) {
+            const KState k = s_q[(qhead + i) & (QCAP - 1)];
+            dst[i] = make_uint4(k.node, k.jm, __float_as_uint(k.pen), k.packed);
+          }
+          if constexpr (VCAP > 0) {  // compacted in slot order
+            uint32_t at0 = 0;
+            for (uint32_t b = 0; b < VCAP && !bad; b += 64) {
+              const KState k = s_vis[b + lane];
+              const bool occ = k.node != EMPTY;
+              const uint64_t m = __ballot(occ);
+              if (occ) dst[nq + at0 + prefix_below(m)] = make_uint4(k.node, k.jm, __float_as_uint(k.pen), k.packed);
+              at0 += (uint32_t)__popcll(m);
+            }
+          }
+          for (uint32_t i = lane; i < EL.n && !bad; i += 64) dst[nq + nv + i] = EL.buf[i];
+          if (lane == 0) {
+            if (!bad) {
+              P.rc_pool[off] = make_uint4(qhead, qlen, nv, (uint32_t)(popped - popped0));
+              P.rc_pool[off + 1] = make_uint4(EL.n, 0u, 0u, 0u);
+              P.rc_pool[off + 2] = kch;
+            }
+            P.rc_off[ent] = bad ? EMPTY : (uint32_t)off;
+            P.rc_count[ent] = bad ? EMPTY : nq;
+          }
+          (void)vcnt;
+          err &= ~(ERR_QUEUE | ERR_VISITED | ERR_EMIT);
           __builtin_amdgcn_wave_barrier();
           if (any_err(err)) break;
           continue;
@@ -1403,6 +1476,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
     if (any_err(err)) break;
   }
   if (lane == 0) atomicAdd(P.counters + 1, (unsigned long long)popped);
+  if (lane == 0 && cached) atomicAdd(P.counters + 4, (unsigned long long)cached);
   const unsigned all = wave_or(err);
   if (lane == 0 && all) atomicOr(reinterpret_cast<unsigned int*>(P.counters + 2), all);
 }
@@ -1417,11 +1491,11 @@ template <uint32_t QCAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QCAP <= 512 ? 4 : 1))) void bfs_window_kernel_nd(SearchParams P) {
   bfs_window_body<0, QCAP>(P);
 }
-// root-pop cache build (P.rc_mode == 2): one representative window per key, root pop + selection
-// only; its own symbol so profiles separate it from the search launches
+// prefix-cache build (P.rc_mode == 2): one representative window per key, popped up to the first
+// state past the key; its own symbol so profiles separate it from the search launches
 template <uint32_t QCAP>
 __global__ __launch_bounds__(64) void rc_build_kernel(SearchParams P) {
-  bfs_window_body<256, QCAP>(P);
+  bfs_window_body<512, QCAP>(P);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1599,13 +1673,13 @@ void launch_one(uint32_t grid, hipStream_t s, const SearchParams& P) {
 constexpr Variant kVariants[] = {{0, 128},   {0, 256},   {0, 512},     {256, 256},   {512, 256},
                                  {512, 512}, {1024, 1024}, {2048, 2048}, {4096, 4096}, {0, 8192}};
 
-// ring for the cache build: the root's pushes (fan_root) after the popped root
-bool launch_rc_build(uint64_t fan_root, uint32_t grid, hipStream_t s, const SearchParams& P) {
-  if (fan_root + 1 <= 256) hipLaunchKernelGGL((rc_build_kernel<256>), dim3(grid), dim3(64), 0, s, P);
-  else if (fan_root + 1 <= 512) hipLaunchKernelGGL((rc_build_kernel<512>), dim3(grid), dim3(64), 0, s, P);
-  else if (fan_root + 1 <= 1024) hipLaunchKernelGGL((rc_build_kernel<1024>), dim3(grid), dim3(64), 0, s, P);
-  else if (fan_root + 1 <= 2048) hipLaunchKernelGGL((rc_build_kernel<2048>), dim3(grid), dim3(64), 0, s, P);
-  else if (fan_root + 1 <= 4096) hipLaunchKernelGGL((rc_build_kernel<4096>), dim3(grid), dim3(64), 0, s, P);
+// cache-build ring: at least the root's pushes after the popped root and the main pass's ring
+bool launch_rc_build(uint32_t need_q, uint32_t grid, hipStream_t s, const SearchParams& P) {
+  if (need_q <= 256) hipLaunchKernelGGL((rc_build_kernel<256>), dim3(grid), dim3(64), 0, s, P);
+  else if (need_q <= 512) hipLaunchKernelGGL((rc_build_kernel<512>), dim3(grid), dim3(64), 0, s, P);
+  else if (need_q <= 1024) hipLaunchKernelGGL((rc_build_kernel<1024>), dim3(grid), dim3(64), 0, s, P);
+  else if (need_q <= 2048) hipLaunchKernelGGL((rc_build_kernel<2048>), dim3(grid), dim3(64), 0, s, P);
+  else if (need_q <= 4096) hipLaunchKernelGGL((rc_build_kernel<4096>), dim3(grid), dim3(64), 0, s, P);
   else return false;
   return true;
 }
@@ -1929,7 +2003,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   uint64_t spill_cap = std::max<uint64_t>(4096, windows / 32);
   const uint32_t max_grid = (uint32_t)cus * 16;
   HIP_TRY(d_ebuf.alloc((size_t)max_grid * P.ecap * sizeof(uint4), stream));
-  HIP_TRY(d_cnt.alloc(4 * sizeof(unsigned long long), stream));
+  HIP_TRY(d_cnt.alloc(5 * sizeof(unsigned long long), stream));
   HIP_TRY(d_out.alloc(out_cap * sizeof(fac_match), stream));
   HIP_TRY(d_spill.alloc(spill_cap * sizeof(uint64_t), stream));
   DevBuf d_counts;
@@ -1947,46 +2021,68 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.win_list = nullptr;
 
   int rc = FAC_OK;
-  uint64_t retries = 0, launches = 0, popped = 0, pass_windows = windows;
-  unsigned long long cnt[4] = {0, 0, 0, 0};
+  uint64_t retries = 0, launches = 0, popped = 0, cached_pops = 0, pass_windows = windows;
+  unsigned long long cnt[5] = {0, 0, 0, 0, 0};
   float ms_total = 0.f, cache_ms = 0.f;
   out.clear();
 
-  // Root-pop cache (rc_collect_kernel, then the window kernel in build mode over one representative
-  // window per key): skipped when the root emits (an empty pattern) or the search is small.
+  // Prefix cache (rc_collect_kernel, then rc_build_kernel over one representative window per key),
+  // keys of 4 chars, else 3, else 2, whichever first gives every snapshot at least 8
+  // windows on average (a build costs about one window search); skipped when the root emits (an
+  // empty pattern) or the search is small.
   P.rc_mode = 0;
   const bool root_out = !e.nodes.empty() && e.nodes[0].out_end > e.nodes[0].out_begin;
-  const char* rc_min = std::getenv("FAC_RC_MIN");  // env knobs: tests force it on, A/B turns it off
-  if (!root_out && fan_root + 1 <= 4096 && windows >= (rc_min ? std::strtoull(rc_min, nullptr, 10) : 4096ull) &&
-      !std::getenv("FAC_NO_RC")) {
-    const uint32_t slots = 1u << 16, max_ent = (uint32_t)std::min<uint64_t>(windows, 16384);
-    const uint32_t stride = (uint32_t)(beam ? std::min<uint64_t>(fan_root, 2ull * beam) : fan_root);
+  const char* rc_min = std::getenv("FAC_RC_MIN");  // env knobs: tests force it on / pin K, A/B turns it off
+  const char* kenv = std::getenv("FAC_RC_K");
+  if (!root_out && fan_root + 1 <= 4096 && kVariants[vi].qcap <= 4096 &&
+      windows >= (rc_min ? std::strtoull(rc_min, nullptr, 10) : 4096ull) && !std::getenv("FAC_NO_RC")) {
+    const uint32_t kpin = kenv ? (uint32_t)std::min<unsigned long>(4, std::max<unsigned long>(2, std::strtoul(kenv, nullptr, 10))) : 0u;
+    const uint32_t qmain = kVariants[vi].qcap, vmain = kVariants[vi].vcap;
+    const uint32_t qbuild = std::max<uint32_t>((uint32_t)fan_root + 1, qmain);
+    P.rc_vmax = vmain ? std::min<uint32_t>(256, vmain / 2) : 256;
+    P.rc_emax = 16;
+    const char* eenv = std::getenv("FAC_RC_ENTRIES");
+    const uint64_t ent_cap = eenv ? std::max<uint64_t>(1, std::strtoull(eenv, nullptr, 10)) : (4ull << 20);
+    const uint32_t max_ent = (uint32_t)std::min<uint64_t>(windows, ent_cap);
+    uint32_t slots = 1u << 12;
+    while (slots < 4ull * max_ent && slots < (1u << 24)) slots <<= 1;
     HIP_TRY(d_rck.alloc(slots * sizeof(unsigned long long), stream));
     HIP_TRY(d_rcv.alloc(slots * sizeof(uint32_t), stream));
     HIP_TRY(d_rcrep.alloc(max_ent * sizeof(uint64_t), stream));
-    HIP_TRY(d_rcs.alloc((size_t)max_ent * stride * sizeof(KState), stream));
-    HIP_TRY(d_rcc.alloc(max_ent * sizeof(uint32_t), stream));
-    HIP_TRY(d_rcn.alloc(sizeof(unsigned int), stream));
-    HIP_TRY(hipMemsetAsync(d_rck.p, 0, slots * sizeof(unsigned long long), stream));
-    HIP_TRY(hipMemsetAsync(d_rcv.p, 0xFF, slots * sizeof(uint32_t), stream));
-    HIP_TRY(hipMemsetAsync(d_rcn.p, 0, sizeof(unsigned int), stream));
+    HIP_TRY(d_rcc.alloc(2 * (size_t)max_ent * sizeof(uint32_t), stream));  // counts, then offsets
+    HIP_TRY(d_rcn.alloc(2 * sizeof(unsigned long long), stream));            // keys, pool words used
     P.rc_keys = static_cast<const unsigned long long*>(d_rck.p);
     P.rc_val = static_cast<const uint32_t*>(d_rcv.p);
     P.rc_mask = slots - 1;
-    P.rc_stride = stride;
-    P.rc_states = static_cast<KState*>(d_rcs.p);
     P.rc_count = static_cast<uint32_t*>(d_rcc.p);
+    P.rc_off = static_cast<uint32_t*>(d_rcc.p) + max_ent;
+    P.rc_pool_used = static_cast<unsigned long long*>(d_rcn.p) + 1;
     HIP_TRY(hipEventRecord(ev.a, stream));
     const uint32_t cgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256, (uint64_t)cus * 8));
-    hipLaunchKernelGGL(rc_collect_kernel, dim3(cgrid), dim3(256), 0, stream, P,
-                       static_cast<unsigned long long*>(d_rck.p), static_cast<uint32_t*>(d_rcv.p),
-                       static_cast<uint64_t*>(d_rcrep.p), static_cast<unsigned int*>(d_rcn.p), max_ent);
-    HIP_TRY(hipGetLastError());
-    unsigned int n_ent = 0;
-    HIP_TRY(hipMemcpyAsync(&n_ent, d_rcn.p, sizeof(n_ent), hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    n_ent = std::min(n_ent, max_ent);
-    if (n_ent) {
+    for (uint32_t k = kpin ? kpin : 4u; k >= (kpin ? kpin : 2u); --k) {
+      P.rc_k = k;
+      HIP_TRY(hipMemsetAsync(d_rck.p, 0, slots * sizeof(unsigned long long), stream));
+      HIP_TRY(hipMemsetAsync(d_rcv.p, 0xFF, slots * sizeof(uint32_t), stream));
+      HIP_TRY(hipMemsetAsync(d_rcn.p, 0, 2 * sizeof(unsigned long long), stream));
+      hipLaunchKernelGGL(rc_collect_kernel, dim3(cgrid), dim3(256), 0, stream, P,
+                         static_cast<unsigned long long*>(d_rck.p), static_cast<uint32_t*>(d_rcv.p),
+                         static_cast<uint64_t*>(d_rcrep.p), static_cast<unsigned int*>(d_rcn.p), max_ent);
+      HIP_TRY(hipGetLastError());
+      unsigned int n_keys = 0;
+      HIP_TRY(hipMemcpyAsync(&n_keys, d_rcn.p, sizeof(n_keys), hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (n_keys == 0) break;
+      if (!kpin && 8ull * n_keys > windows) continue;  // too little reuse: fewer chars per key
+      const uint32_t n_ent = std::min(n_keys, max_ent);
+      // snapshot pool: the worst entry for every key, up to a budget; a build that runs out of
+      // pool leaves the remaining keys uncached
+      const uint64_t worst = 3 + std::min(qmain, qbuild) + P.rc_vmax + P.rc_emax;
+      const char* penv = std::getenv("FAC_RC_POOL_MB");
+      const uint64_t budget = (penv ? std::strtoull(penv, nullptr, 10) : 8192ull) << 20;
+      const uint64_t pool_words = std::max<uint64_t>(1024, std::min<uint64_t>(n_ent * worst, budget / sizeof(uint4)));
+      HIP_TRY(d_rcs.alloc(pool_words * sizeof(uint4), stream));
+      P.rc_pool = static_cast<uint4*>(d_rcs.p);
+      P.rc_pool_cap = pool_words;
       SearchParams Q = P;
       Q.rc_mode = 2;
       Q.win_list = static_cast<const uint64_t*>(d_rcrep.p);
@@ -1999,14 +2095,15 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       Q.spill = static_cast<uint64_t*>(d_spill.p);
       Q.spill_cap = spill_cap;
       Q.counters = static_cast<unsigned long long*>(d_cnt.p);
-      HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 4 * sizeof(unsigned long long), stream));
-      launch_rc_build(fan_root, std::min<uint32_t>(n_ent, max_grid), stream, Q);
+      HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 5 * sizeof(unsigned long long), stream));
+      launch_rc_build(qbuild, std::min<uint32_t>(n_ent, max_grid), stream, Q);
       const hipError_t le = hipGetLastError();
       if (le != hipSuccess) {
         err = std::string("kernel launch: ") + hipGetErrorString(le);
         return FAC_E_HIP;
       }
       P.rc_mode = 1;
+      break;
     }
     HIP_TRY(hipEventRecord(ev.b, stream));
     HIP_TRY(hipStreamSynchronize(stream));
@@ -2023,7 +2120,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     P.spill = static_cast<uint64_t*>(d_spill.p);
     P.spill_cap = spill_cap;
     P.counters = static_cast<unsigned long long*>(d_cnt.p);
-    HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 4 * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 5 * sizeof(unsigned long long), stream));
     if (debug_poison()) HIP_TRY(hipMemsetAsync(d_out.p, 0xAB, out_cap * sizeof(fac_match), stream));
     HIP_TRY(hipEventRecord(ev.a, stream));
     const hipError_t le = launch_variant(kVariants[vi], grid, stream, P);
@@ -2033,13 +2130,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       break;
     }
     HIP_TRY(hipEventRecord(ev.b, stream));
-    HIP_TRY(hipMemcpyAsync(cnt, d_cnt.p, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(cnt, d_cnt.p, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
     ms_total += ms;
     launches += 1;
     popped += cnt[1];
+    cached_pops += cnt[4];
 #ifdef FAC_PHASE_PROF
     {
       unsigned long long pr[16];
@@ -2116,6 +2214,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     stats->kernel_ms += ms_total;
     stats->kernel_launches += launches;
     stats->cache_ms += cache_ms;
+    stats->states_cached += cached_pops;
     stats->windows += windows;
     stats->states_popped += popped;
     stats->graphemes = h.n;

@@ -68,7 +68,8 @@ class fac_stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("prefilter_ms", ctypes.c_double),
                 ("kernel_launches", ctypes.c_uint64), ("windows", ctypes.c_uint64),
                 ("states_popped", ctypes.c_uint64), ("graphemes", ctypes.c_uint64),
-                ("bytes", ctypes.c_uint64), ("retries", ctypes.c_uint64), ("cache_ms", ctypes.c_double)]
+                ("bytes", ctypes.c_uint64), ("retries", ctypes.c_uint64), ("cache_ms", ctypes.c_double),
+                ("states_cached", ctypes.c_uint64)]
 
 
 assert ctypes.sizeof(fac_match) == 32

@@ -116,11 +116,12 @@ typedef struct fac_stats {
   double prefilter_ms;     /* HIP-event time of the bitap scan + window merge (0 if unused) */
   uint64_t kernel_launches;
   uint64_t windows;        /* start windows searched */
-  uint64_t states_popped;  /* BFS states popped (work diagnostic) */
+  uint64_t states_popped;  /* BFS states popped by the search kernel (work diagnostic) */
   uint64_t graphemes;      /* haystack graphemes */
   uint64_t bytes;          /* haystack UTF-8 bytes */
   uint64_t retries;        /* capacity retries */
-  double cache_ms;         /* HIP-event time of the root-pop cache build (key collection + root pops) */
+  double cache_ms;         /* HIP-event time of the prefix-cache build (key collection + snapshots) */
+  uint64_t states_cached;  /* pops replayed from prefix-cache snapshots (not in states_popped) */
 } fac_stats;
 
 typedef struct fac_engine fac_engine;

@@ -79,7 +79,7 @@ def random_case(rng, vocab, filler, allow_beam=True, allow_limits=True):
     return b, pats, hay, thr
 
 
-@pytest.mark.parametrize("root_cache", ["off", "forced"])
+@pytest.mark.parametrize("root_cache", ["off", "k4"])
 @pytest.mark.parametrize("per_edge_only", [False, True])
 @pytest.mark.parametrize("seed,vocab,filler", [
     (0x1234_5678_9abc_def1, ASCII_VOCAB, ASCII_FILLER),
@@ -88,10 +88,15 @@ def random_case(rng, vocab, filler, allow_beam=True, allow_limits=True):
 def test_differential_random(seed, vocab, filler, per_edge_only, root_cache, monkeypatch):
     """per_edge_only: FAC_NO_FAST disables the O(1) goto-table expansion, so the per-edge unit
     path is checked on every state as well. root_cache: the root-pop cache off, or forced on for
-    every search (it is normally used from 4096 windows on)."""
+    every search with 4-char keys (it is normally used from 4096 windows on, with the longest key
+    that still gives 8 windows per snapshot)."""
     if per_edge_only:
         monkeypatch.setenv("FAC_NO_FAST", "1")
-    monkeypatch.setenv(*(("FAC_NO_RC", "1") if root_cache == "off" else ("FAC_RC_MIN", "1")))
+    if root_cache == "off":
+        monkeypatch.setenv("FAC_NO_RC", "1")
+    else:
+        monkeypatch.setenv("FAC_RC_MIN", "1")
+        monkeypatch.setenv("FAC_RC_K", "4")
     rng = Rng(seed)
     total = 0
     for _ in range(150):
@@ -248,14 +253,46 @@ def test_staged_prefiltered_matches_oracle(seed, vocab, filler):
 def test_auto_beam_matches_oracle(budget, width, monkeypatch):
     """auto_beam (search.rs:1096-1103): GPU two-pass (exact counting pass, beamed tail) == the
     oracle's sequential budget, per search_raw call, incl. the pre-filter's per-window calls
-    (root-pop cache forced on: pass 1 records queue.len() through cached roots too)."""
+    (prefix cache forced on: pass 1 records queue.len() through cached prefixes too)."""
     monkeypatch.setenv("FAC_RC_MIN", "1")
+    monkeypatch.setenv("FAC_RC_K", "4")
     rng = Rng(0xab ^ budget)
     for _ in range(40):
         b, pats, hay, thr = random_case(rng, ASCII_VOCAB + UNI_VOCAB, ASCII_FILLER + UNI_FILLER, allow_beam=False)
         b = b.auto_beam(budget, width)
         compare(b, pats, hay, thr)
         compare(b, pats, hay, thr, prefilter=True)
+
+
+@pytest.mark.parametrize("k", ["2", "3", "4"])
+def test_prefix_cache_key_lengths(k, monkeypatch):
+    """Every key length of the prefix cache (forced on) == the oracle, beamed and unbeamed, ASCII
+    and Unicode, including windows whose key runs past the end of the text."""
+    monkeypatch.setenv("FAC_RC_MIN", "1")
+    monkeypatch.setenv("FAC_RC_K", k)
+    rng = Rng(0x5eed ^ int(k))
+    for _ in range(60):
+        b, pats, hay, thr = random_case(rng, ASCII_VOCAB + UNI_VOCAB, ASCII_FILLER + UNI_FILLER)
+        compare(b, pats, hay, thr)
+
+
+def test_prefix_cache_default_on_c3_slice(monkeypatch):
+    """A C3-shaped haystack large enough for the default cache (4-char keys): identical records with
+    the cache on and off; a slice with the cache forced on == the oracle."""
+    from fuzzy_aho_corasick import workloads
+    w = workloads.config("c3", 1 << 20, 3)
+    eng = workloads.builder_for(w).build(w.patterns)
+    staged = eng.stage(w.haystack)
+    on, st_on = staged.search_windows_records(w.threshold)
+    monkeypatch.setenv("FAC_NO_RC", "1")
+    off, _ = staged.search_windows_records(w.threshold)
+    assert st_on.states_cached > 0
+    assert len(on) > 0 and sorted(on.tolist()) == sorted(off.tolist())
+    n = 24 << 10  # oracle on a prefix (whole graphemes: the generator's text is valid UTF-8)
+    hay = w.haystack[:n].decode("utf-8", "ignore")
+    monkeypatch.delenv("FAC_NO_RC")
+    monkeypatch.setenv("FAC_RC_MIN", "1")
+    _staged_vs_oracle(workloads.builder_for(w), w.patterns, hay, w.threshold)
 
 
 def _keyrows(ms):
