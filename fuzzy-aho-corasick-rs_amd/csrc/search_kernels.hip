@@ -944,6 +944,10 @@ __device__ __forceinline__ void sink64(uint64_t v) {
 }
 #endif
 
+struct RcHit {  // prefix-cache snapshot of a window (rc_lookup): pool offset and header
+  uint32_t off, head, tail, nv_nel, pops;
+};
+
 constexpr uint32_t claim_slots(uint32_t vcap) { return vcap / 2 < 512 ? 512 : vcap / 2; }  // >= ExpScratch
 
 #ifdef FAC_PHASE_PROF  // diagnostics build (make prof): cycles per phase of run_window
@@ -961,7 +965,7 @@ __device__ unsigned long long g_prof[16];
 // the beam would trigger, and before the first >64-edge node (expanded alone, edge-parallel).
 template <uint32_t VCAP, uint32_t QCAP>
 __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
-                           uint32_t& cseq, EmitList& EL, uint64_t start, uint32_t rce, uint64_t& popped,
+                           uint32_t& cseq, EmitList& EL, uint64_t start, const RcHit& rc, uint64_t& popped,
                            uint64_t& cached, unsigned& err, uint32_t& head_out, uint32_t& vcount_out) {
   const uint32_t lane = lane_id();
 #ifdef FAC_PHASE_PROF
@@ -973,31 +977,41 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
   uint32_t vcount = 0;
   EL.n = 0;
   uint32_t head = 0, tail = 1;
-  if (rce != EMPTY) {  // prefix cache hit: resume from the snapshot of the key's representative
-    const uint4* src = P.rc_pool + rce;
-    const uint4 h0 = src[0], h1 = src[1];  // {head, tail, dedup entries, pops}, {best entries}; [2]: chars
-    src += 3;
-    head = h0.x;
-    tail = h0.y;
-    for (uint32_t i = lane; i < tail - head; i += 64) {
-      const uint4 w = src[i];
-      q[(head + i) & (QCAP - 1)] = KState{w.x, w.y, __uint_as_float(w.z), w.w};
-    }
-    if constexpr (VCAP > 0) {  // the popped keys with their stored penalties (slots re-hashed)
-      __builtin_amdgcn_wave_barrier();
-      for (uint32_t i = lane; i < h0.z; i += 64) {
-        const uint4 w = src[(tail - head) + i];
-        uint32_t slot = vis_hash(KState{w.x, w.y, 0.f, w.w}) & (VCAP - 1);
-        while (atomicCAS(&vis[slot].node, EMPTY, w.x) != EMPTY) slot = (slot + 1) & (VCAP - 1);
-        vis[slot].jm = w.y;
-        vis[slot].pen = __uint_as_float(w.z);
-        vis[slot].packed = w.w;
+  if (rc.off != EMPTY) {  // prefix cache hit: resume from the snapshot of the key's representative
+    const uint4* src = P.rc_pool + rc.off + 3;  // queue, dedup entries, best list (header in rc)
+    head = rc.head;
+    tail = rc.tail;
+    const uint32_t nq = tail - head, nv = rc.nv_nel & 0xFFFFu, ne = rc.nv_nel >> 16, nw = nq + nv + ne;
+    if constexpr (VCAP > 0) __builtin_amdgcn_wave_barrier();  // the table clear above
+    for (uint32_t b = 0; b < nw; b += 256) {  // four loads in flight per lane, then their stores
+      uint4 w[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t i = b + u * 64 + lane;
+        if (i < nw) w[u] = src[i];
       }
-      vcount = h0.z;
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) {
+        const uint32_t i = b + u * 64 + lane;
+        if (i >= nw) continue;
+        if (i < nq) {
+          q[(head + i) & (QCAP - 1)] = KState{w[u].x, w[u].y, __uint_as_float(w[u].z), w[u].w};
+        } else if (i < nq + nv) {
+          if constexpr (VCAP > 0) {  // a live popped key with its stored penalty (slot re-hashed)
+            uint32_t slot = vis_hash(KState{w[u].x, w[u].y, 0.f, w[u].w}) & (VCAP - 1);
+            while (atomicCAS(&vis[slot].node, EMPTY, w[u].x) != EMPTY) slot = (slot + 1) & (VCAP - 1);
+            vis[slot].jm = w[u].y;
+            vis[slot].pen = __uint_as_float(w[u].z);
+            vis[slot].packed = w[u].w;
+          }
+        } else {
+          EL.buf[i - nq - nv] = w[u];
+        }
+      }
     }
-    for (uint32_t i = lane; i < h1.x; i += 64) EL.buf[i] = src[(tail - head) + h0.z + i];
-    EL.n = h1.x;
-    cached += h0.w;  // the snapshot's pops (not counted as popped: that is executed work)
+    if constexpr (VCAP > 0) vcount = nv;
+    EL.n = ne;
+    cached += rc.pops;  // the snapshot's pops (not counted as popped: that is executed work)
   } else if (lane == 0) {
     q[0] = KState{0u, 0u, 0.0f, 0u};
   }
@@ -1315,26 +1329,29 @@ __device__ __forceinline__ bool rc_key(const SearchParams& P, const SegDesc& S, 
 __device__ __forceinline__ uint32_t rc_hash(uint64_t k) { return (uint32_t)k ^ (uint32_t)(k >> 32); }
 constexpr uint32_t RC_PROBES = 32;
 
+// A window's prefix-cache hit (snapshot header, read with the lookup): off = EMPTY on a miss
 template <uint32_t QCAP>
-__device__ __forceinline__ uint32_t rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s) {
+__device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s) {
+  RcHit r{EMPTY, 0u, 0u, 0u, 0u};
   uint4 ch;
   uint64_t k;
-  if (!rc_key(P, S, s, ch, k)) return EMPTY;
+  if (!rc_key(P, S, s, ch, k)) return r;
   const uint32_t h = rc_hash(k);
   for (uint32_t p = 0; p < RC_PROBES; ++p) {
     const uint32_t slot = (h + p) & P.rc_mask;
     const unsigned long long kk = P.rc_keys[slot];
     if (kk == k) {
       const uint32_t ent = P.rc_val[slot];
-      if (ent == EMPTY) return EMPTY;
+      if (ent == EMPTY) return r;
       const uint32_t cnt = P.rc_count[ent], off = P.rc_off[ent];
-      if (cnt == EMPTY || cnt + 1u > QCAP) return EMPTY;
-      const uint4 sc = P.rc_pool[off + 2];  // the snapshot's own chars
-      return (sc.x == ch.x && sc.y == ch.y && sc.z == ch.z && sc.w == ch.w) ? off : EMPTY;
+      if (cnt == EMPTY || cnt + 1u > QCAP) return r;
+      const uint4 h0 = P.rc_pool[off], h1 = P.rc_pool[off + 1], sc = P.rc_pool[off + 2];  // [2]: its chars
+      if (sc.x == ch.x && sc.y == ch.y && sc.z == ch.z && sc.w == ch.w) r = RcHit{off, h0.x, h0.y, h0.z | (h1.x << 16), h0.w};
+      return r;
     }
-    if (kk == 0ull) return EMPTY;
+    if (kk == 0ull) return r;
   }
-  return EMPTY;
+  return r;
 }
 
 // Prefix-cache keys: every searched window's key is inserted once (plain probe first, CAS only on
@@ -1399,8 +1416,8 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         start = S.w_begin + (vid - P.seg_prefix[kl]);
         active = !window_skipped(P, S, start, err);
       }
-      uint32_t rce = EMPTY;  // prefix-cache snapshot (pool offset) of this lane's window
-      if (P.rc_mode == 1 && active) rce = rc_lookup<QCAP>(P, P.segs[kl], start);
+      RcHit hit{EMPTY, 0u, 0u, 0u, 0u};  // prefix-cache snapshot of this lane's window
+      if (P.rc_mode == 1 && active) hit = rc_lookup<QCAP>(P, P.segs[kl], start);
       uint64_t m = __ballot(active);
       while (m) {
         const int l = first_lane(m);
@@ -1410,14 +1427,22 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         const SegDesc S = P.segs[seg];
         const uint64_t popped0 = popped;
         uint32_t qhead = 0, vcnt = 0;
-        const uint32_t qlen = run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, shfl_u32(rce, l), popped,
-                                                     cached, err, qhead, vcnt);
+        const RcHit rc{shfl_u32(hit.off, l), shfl_u32(hit.head, l), shfl_u32(hit.tail, l), shfl_u32(hit.nv_nel, l),
+                       shfl_u32(hit.pops, l)};
+        const uint32_t qlen =
+            run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, rc, popped, cached, err, qhead, vcnt);
         if (P.rc_mode == 2) {  // cache build: entry = list position; what does not fit stays uncached
           const uint32_t ent = (uint32_t)(v0 + (uint64_t)l);
           const uint32_t nq = qlen - qhead;
-          uint32_t nv = 0;  // occupied dedup slots
+          // live dedup entries: a key is only met again at its own j, and every future state's j is
+          // at least the smallest j in the queue (j never decreases along a path)
+          uint32_t jmin = 0xFFFFu;
+          for (uint32_t i = lane; i < nq; i += 64) jmin = min(jmin, s_q[(qhead + i) & (QCAP - 1)].jm & 0xFFFFu);
+          jmin = wave_min_u32(jmin);
+          auto live = [&](const KState& k) { return k.node != EMPTY && (k.jm & 0xFFFFu) >= jmin; };
+          uint32_t nv = 0;
           if constexpr (VCAP > 0)
-            for (uint32_t b = 0; b < VCAP; b += 64) nv += (uint32_t)__popcll(__ballot(s_vis[b + lane].node != EMPTY));
+            for (uint32_t b = 0; b < VCAP; b += 64) nv += (uint32_t)__popcll(__ballot(live(s_vis[b + lane])));
           bool bad = (wave_or(err) & (ERR_QUEUE | ERR_VISITED | ERR_EMIT)) != 0 || EL.n > P.rc_emax || nv > P.rc_vmax;
           const uint32_t words = 3 + nq + nv + EL.n;
           unsigned long long off = 0;
@@ -1436,7 +1461,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
             uint32_t at0 = 0;
             for (uint32_t b = 0; b < VCAP && !bad; b += 64) {
               const KState k = s_vis[b + lane];
-              const bool occ = k.node != EMPTY;
+              const bool occ = live(k);
               const uint64_t m = __ballot(occ);
               if (occ) dst[nq + at0 + prefix_below(m)] = make_uint4(k.node, k.jm, __float_as_uint(k.pen), k.packed);
               at0 += (uint32_t)__popcll(m);
