@@ -67,10 +67,7 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
   e.has_auto_beam = cfg->has_auto_beam != 0;
   e.ab_budget = cfg->auto_beam_budget;
   e.ab_width = cfg->auto_beam_width;
-  if (cfg->n_mappings > 0) {
-    err = "multi-character mappings are not supported on the GPU path";
-    return FAC_E_UNSUPPORTED;
-  }
+  if (cfg->n_mappings > 0 && !cfg->mappings) { err = "NULL mappings"; return FAC_E_INVALID; }
   if (e.has_auto_beam && e.ab_width == 0 && e.beam_width == 0) {
     err = "auto_beam width must be >= 1";
     return FAC_E_INVALID;
@@ -182,6 +179,90 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
     }
   }
 
+  // ---- multi-character mappings (builder.rs:383-442): every rule in both directions; from every
+  // node the pattern side is walked through the trie (whole folded graphemes) and, when it is a
+  // path, a transition consuming the haystack side is recorded. Haystack-side graphemes join the
+  // grapheme dictionary so text graphemes can be compared by id.
+  auto intern = [&](const std::u32string& g) -> uint32_t {
+    auto it = gid_of.find(g);
+    if (it != gid_of.end()) return it->second;
+    const uint32_t id = (uint32_t)gstr.size();
+    gid_of.emplace(g, id);
+    gstr.push_back(g);
+    return id;
+  };
+  e.map_range.assign(nn, uint2{0, 0});
+  e.map_ent.clear();
+  e.map_hay.clear();
+  e.has_map = false;
+  e.max_map = 0;
+  uint32_t max_map_hay = 1;
+  if (cfg->n_mappings > 0) {
+    auto fold_side = [&](const char* p, uint64_t len, std::vector<uint32_t>& out) -> bool {
+      const uint8_t* u = reinterpret_cast<const uint8_t*>(p);
+      if (len && !u) return false;
+      if (!utf8_valid(u, len)) return false;
+      segment_graphemes(u, len, starts);
+      out.clear();
+      for (size_t g = 0; g < starts.size(); ++g) {
+        fold_grapheme(u, starts[g], g + 1 < starts.size() ? starts[g + 1] : len, e.case_insensitive, folded);
+        out.push_back(intern(folded));
+      }
+      return true;
+    };
+    struct Directed { std::vector<uint32_t> pat, hay; float penalty; };
+    std::vector<Directed> directed;
+    std::vector<uint32_t> ga, gb;
+    for (uint64_t r = 0; r < cfg->n_mappings; ++r) {
+      const fac_mapping& m = cfg->mappings[r];
+      if (!fold_side(m.a, m.a_len, ga) || !fold_side(m.b, m.b_len, gb)) {
+        err = "mapping is not valid UTF-8";
+        return FAC_E_INVALID;
+      }
+      if (ga.empty() || gb.empty() || ga == gb) continue;
+      volatile float one_minus = 1.0f - m.score;  // substitution * (1 - score), two rounded ops
+      const float penalty = e.p_sub * one_minus;
+      directed.push_back({ga, gb, penalty});
+      directed.push_back({gb, ga, penalty});
+    }
+    for (size_t start = 0; start < nn; ++start) {
+      e.map_range[start].x = (uint32_t)e.map_ent.size();
+      for (const Directed& d : directed) {
+        uint32_t cur = (uint32_t)start;
+        bool ok = true;
+        for (uint32_t g : d.pat) {
+          auto it = go.find(((uint64_t)cur << 32) | g);
+          if (it == go.end()) { ok = false; break; }
+          cur = it->second;
+        }
+        if (!ok) continue;
+        uint32_t f;
+        std::memcpy(&f, &d.penalty, 4);
+        e.map_ent.push_back(uint4{(uint32_t)e.map_hay.size(), (uint32_t)d.hay.size(), cur, f});
+        for (uint32_t g : d.hay) e.map_hay.push_back(g + 1);
+        max_map_hay = std::max<uint32_t>(max_map_hay, (uint32_t)d.hay.size());
+      }
+      e.map_range[start].y = (uint32_t)e.map_ent.size();
+      e.max_map = std::max(e.max_map, e.map_range[start].y - e.map_range[start].x);
+    }
+    e.has_map = !e.map_ent.empty();
+    if (e.max_map > 64) {
+      err = "more than 64 mapping transitions at one trie node";
+      return FAC_E_UNSUPPORTED;
+    }
+  }
+  e.gid_of.clear();
+  e.edge_gid.clear();
+  std::memset(e.ascii_gid, 0, sizeof(e.ascii_gid));
+  if (e.has_map) {  // ids are 1-based: 0 is "not a known grapheme" and matches no edge
+    for (size_t i = 0; i < gstr.size(); ++i) e.gid_of.emplace(gstr[i], (uint32_t)i + 1);
+    for (uint32_t b = 0; b < 128; ++b) {  // gs_text of an ASCII byte (grapheme.rs:100-109)
+      const uint32_t c = (e.case_insensitive && b >= 'A' && b <= 'Z') ? b + 32 : b;
+      auto it = e.gid_of.find(std::u32string(1, (char32_t)c));
+      e.ascii_gid[b] = it == e.gid_of.end() ? 0u : it->second;
+    }
+  }
+
   // ---- effective limits (builder.rs:289-329), has_pattern_limits, max_edits_fast (:444-468)
   e.has_pattern_limits = false;
   for (auto& p : e.pats) e.has_pattern_limits |= p.has_limits != 0;
@@ -226,6 +307,7 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
       if (!output[nx].empty()) nx |= EDGE_CHILD_OUTPUT;
       if (single) nx |= EDGE_SINGLE_BYTE;
       e.edges.push_back({fc, nx});
+      if (e.has_map) e.edge_gid.push_back(k.first + 1);
       if (single && fc < 128) (&e.sb_bits[i].x)[fc >> 5] |= 1u << (fc & 31);
     }
     d.edge_end = (uint32_t)e.edges.size();
@@ -297,7 +379,7 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
   std::memset(e.first_bits, 0, sizeof(e.first_bits));
   std::memset(e.second_bits, 0, sizeof(e.second_bits));
   e.window_skip = false;
-  if (e.mef == 1 && output[0].empty()) {
+  if (e.mef == 1 && !e.has_map && output[0].empty()) {  // search.rs:505 (WINDOW_SKIP && !MAPPINGS)
     bool child_output = false;
     uint32_t f[4] = {e.sb_bits[0].x, e.sb_bits[0].y, e.sb_bits[0].z, e.sb_bits[0].w};
     uint32_t s2[4] = {0, 0, 0, 0};
@@ -314,7 +396,7 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
     }
   }
 
-  // ---- max_match_graphemes (stream.rs:213-253), no mappings => mapping factor 1
+  // ---- max_match_graphemes (stream.rs:213-253): longest pattern + edits x longest mapping side
   {
     uint64_t max_edits = 0;
     auto edits_of = [](const DevLimits& l) -> uint64_t {
@@ -326,7 +408,7 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
       const DevLimits* l = p.has_limits ? &p.lim : (e.has_limits ? &e.limits : nullptr);
       max_edits = std::max<uint64_t>(max_edits, l ? edits_of(*l) : 0);
     }
-    e.max_match_graphemes = (uint64_t)e.max_glen + max_edits;
+    e.max_match_graphemes = (uint64_t)e.max_glen + max_edits * (uint64_t)max_map_hay;
     if (e.max_match_graphemes + 4 > 0xFFFFu) {
       err = "pattern length + edit budget exceeds the 16-bit window span";
       return FAC_E_UNSUPPORTED;
@@ -421,13 +503,14 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
     bool sims01 = true;  // every similarity in [0, 1]: p_sub * (1 - sim) in [0, p_sub]
     for (float v : e.sim_ascii) sims01 = sims01 && v >= 0.0f && v <= 1.0f;
     for (float v : e.sim_vals) sims01 = sims01 && v >= 0.0f && v <= 1.0f;
-    e.gt_fast = sims01 && e.min_sym <= 0.0f && e.p_sub >= 0.0f;
+    // with mappings the exact/swap transitions compare whole graphemes: per-edge path only
+    e.gt_fast = sims01 && e.min_sym <= 0.0f && e.p_sub >= 0.0f && !e.has_map;
   }
 
   // ---- bitap pre-filter tables (prefilter.rs:161-245)
   e.bitap_ok = false;
   do {
-    if (np == 0) break;
+    if (np == 0 || e.has_map) break;  // prefilter.rs:162-165: mappings are not unit edits
     float max_sim = 0.f;  // structs.rs:61-76
     for (int i = 0; i < 128; ++i)
       for (int j = 0; j < 128; ++j)

@@ -19,6 +19,7 @@
 
 #include <cstdint>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -77,6 +78,14 @@ __host__ __device__ inline void gt_slots(uint64_t kv, uint64_t seed, uint32_t ma
   gt_slots_h(gt_kind_hash(gt_base(node, ch, seed), (kv & GT_SB) != 0), mask, s1, s2);
 }
 constexpr int32_t LIM_NONE = -1;
+
+struct U32StrHash {
+  size_t operator()(const std::u32string& s) const {
+    uint64_t h = 1469598103934665603ull;
+    for (char32_t c : s) h = (h ^ (uint64_t)c) * 1099511628211ull;
+    return (size_t)h;
+  }
+};
 
 // host-side node (builder, host bookkeeping)
 struct HostNode {
@@ -209,6 +218,17 @@ struct SearchParams {
   unsigned long long* rc_pool_used; // bump allocator
   uint32_t* rc_off;                 // snapshot offset of each entry (pool words)
   uint32_t* rc_count;               // queued states of each entry (EMPTY: not cached)
+  // multi-character mappings (search.rs:776-780, 883-922, 945-961; builder.rs:383-442). With
+  // has_map, exact and swap transitions compare whole folded graphemes (ids, 0 = not in the
+  // engine's grapheme dictionary): edge_gid per edge, text gids per grapheme (gid32 for Unicode
+  // segments, ascii_gid[folded byte] for ASCII ones)
+  int32_t has_map;
+  const uint32_t* edge_gid;
+  const uint32_t* gid32;
+  const uint32_t* ascii_gid;  // 128 entries
+  const uint2* map_range;     // per node [begin, end) into map_ent
+  const uint4* map_ent;       // {hay begin (into map_hay), hay length, next node, penalty bits}
+  const uint32_t* map_hay;    // haystack-side grapheme ids
 };
 
 constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8u, ERR_OUT = 16u, ERR_SPILL = 32u;
@@ -258,6 +278,15 @@ struct Engine {
   float edit_cost_mult = 0.f;
   uint8_t ascii_id[128] = {0};
   std::vector<std::pair<std::u32string, uint32_t>> symbol_ids;  // sorted by key
+  // multi-character mappings (builder.rs:383-442); has_map = the precomputed table is non-empty
+  bool has_map = false;
+  std::unordered_map<std::u32string, uint32_t, U32StrHash> gid_of;  // folded grapheme -> id (1-based)
+  std::vector<uint32_t> edge_gid;   // per edge
+  uint32_t ascii_gid[128] = {0};    // id of each (folded) ASCII byte, 0 = none
+  std::vector<uint2> map_range;     // per node
+  std::vector<uint4> map_ent;
+  std::vector<uint32_t> map_hay;
+  uint32_t max_map = 0;             // most mapping transitions at one node (<= 64)
   uint32_t alphabet = 0;
   std::vector<uint32_t> bp_m;
   std::vector<float> bp_weight;
@@ -279,6 +308,11 @@ struct Engine {
   float* d_sim_vals = nullptr;
   uint64_t* d_bp_mask = nullptr;
   uint8_t* d_ascii_id = nullptr;
+  uint32_t* d_edge_gid = nullptr;
+  uint32_t* d_ascii_gid = nullptr;
+  uint2* d_map_range = nullptr;
+  uint4* d_map_ent = nullptr;
+  uint32_t* d_map_hay = nullptr;
   std::mutex mu;  // guards lazily grown scratch below
   // per-engine device scratch of the search launcher, reused across calls by whichever call holds
   // scratch_mu (a concurrent call on the same engine allocates its own)
@@ -299,6 +333,8 @@ struct Haystack {
   std::vector<uint64_t> starts;  // grapheme byte starts (Unicode only)
   mutable std::vector<uint8_t> sym;  // prefilter symbol ids per grapheme (Unicode only, lazy)
   mutable bool sym_ready = false;
+  mutable uint32_t* d_gid = nullptr;  // grapheme ids (Unicode, engines with mappings; lazy)
+  mutable const void* gid_engine = nullptr;
   int device = 0;
 };
 

@@ -139,6 +139,44 @@ __device__ __forceinline__ uint32_t text_char(const SearchParams& P, const SegDe
   return P.text32[S.text_base + j];
 }
 
+// id of the whole folded grapheme at j (gs_text, grapheme.rs:61-63, 100-109), engines with
+// mappings only: 0 = not in the engine's grapheme dictionary (equal to no edge or mapping side)
+__device__ __forceinline__ uint32_t text_gid(const SearchParams& P, const SegDesc& S, uint64_t j, unsigned& err) {
+  if (j >= S.avail) {
+    err |= ERR_HALO;
+    return 0;
+  }
+  if (S.ascii) return P.ascii_gid[P.utf8[S.text_base + j] & 0x7Fu];
+  return P.gid32[S.text_base + j];
+}
+
+// Node::find_transition for a whole grapheme (structs.rs:452-464) by id: the edge whose grapheme
+// is the text grapheme (a one-byte grapheme can only equal a single-byte edge), -1 if none
+__device__ __forceinline__ int64_t find_gid(const SearchParams& P, uint32_t node, uint32_t gid) {
+  if (gid == 0) return -1;
+  const DevNode nd = P.nodes[node];
+  for (uint32_t e = nd.edge_begin; e < nd.edge_begin + (nd.degf & NODE_DEG_MASK); ++e)
+    if (P.edge_gid[e] == gid) return (int64_t)(P.edges[e].next & EDGE_NEXT_MASK);
+  return -1;
+}
+
+// Multi-character mappings applicable at (node, j) (search.rs:883-922): bit t = the node's t-th
+// transition consumes text[j .. j + hlen) and stays within max_penalties
+__device__ uint64_t map_mask(const SearchParams& P, const SegDesc& S, uint32_t node, uint64_t j, float pen,
+                             unsigned& err) {
+  const uint2 r = P.map_range[node];
+  uint64_t m = 0;
+  for (uint32_t t = r.x; t < r.y; ++t) {
+    const uint4 mt = P.map_ent[t];
+    if (j + mt.y > S.n) continue;
+    bool ok = true;
+    for (uint32_t k = 0; k < mt.y && ok; ++k) ok = text_gid(P, S, j + k, err) == P.map_hay[mt.x + k];
+    if (!ok || __fadd_rn(pen, __uint_as_float(mt.w)) > P.max_penalties) continue;
+    m |= 1ull << (t - r.x);
+  }
+  return m;
+}
+
 // gs_byte_offset, relative to the (sub)haystack (grapheme.rs:59-61, 95-97)
 __device__ __forceinline__ uint64_t local_byte(const SearchParams& P, const SegDesc& S, uint64_t g) {
   if (S.ascii) return g;
@@ -380,7 +418,20 @@ __device__ void emit_state(const SearchParams& P, EmitList& EL, uint32_t me_rel,
 // Edge-parallel expansion of ONE accepted state (dedup and ceiling passed, emission done): the
 // exact / substitution / swap / insertion / deletion pushes with the 64 lanes spread over the
 // node's edges (search.rs:742-1089). Used for nodes with more than 64 edges.
-template <uint32_t QCAP>
+// find_gid, edge-parallel over the wave (every lane calls it with the same arguments)
+__device__ __forceinline__ int64_t wave_find_gid(const SearchParams& P, uint32_t node, uint32_t gid) {
+  if (gid == 0) return -1;
+  const DevNode nd = P.nodes[node];
+  const uint32_t end = node_end(nd);
+  for (uint32_t base = nd.edge_begin; base < end; base += 64) {
+    const uint32_t i = base + lane_id();
+    const uint64_t m = __ballot(i < end && P.edge_gid[i] == gid);
+    if (m) return (int64_t)(P.edges[base + first_lane(m)].next & EDGE_NEXT_MASK);
+  }
+  return -1;
+}
+
+template <uint32_t QCAP, bool MAP>
 __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, uint32_t head, uint32_t& tail,
                             const KState& st, const DevNode& nd, uint64_t start, unsigned& err) {
   const uint32_t lane = lane_id();
@@ -428,7 +479,10 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
       // exact transition (:766-798); matched_start stays `start` for every state
       const uint64_t nk = GT_VALID | GT_GOTO | ((uint64_t)st.node << 21);
       uint64_t gx;
-      const int64_t exact_next = small ? small_goto(cur_ch) : (gt_get(P, nk | cur_ch, true, gx) ? (int64_t)(gx & CHILD26_MASK) : -1);
+      const int64_t exact_next =
+          MAP ? wave_find_gid(P, st.node, text_gid(P, S, j, err))  // :776-780 with MAPPINGS
+          : small   ? small_goto(cur_ch)
+                    : (gt_get(P, nk | cur_ch, true, gx) ? (int64_t)(gx & CHILD26_MASK) : -1);
       const uint32_t jm1 = (j_rel + 1u) | ((j_rel + 1u) << 16);
       push_lanes<QCAP>(q, head, tail, lane == 0 && exact_next >= 0,
                        KState{(uint32_t)exact_next, jm1, pen, packed}, err);
@@ -472,14 +526,29 @@ __device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, 
           }
           push_lanes<QCAP>(q, head, tail, keep, st2, err);
         }
+        if constexpr (MAP) {  // 1b) multi-character mappings (:883-922), one transition per lane
+          const uint2 r = P.map_range[st.node];
+          const uint64_t mm = map_mask(P, S, st.node, j, pen, err);  // wave-uniform
+          const bool keep = lane < r.y - r.x && ((mm >> lane) & 1ull);
+          KState st2{};
+          if (keep) {
+            const uint4 mt = P.map_ent[r.x + lane];
+            const uint32_t jh = j_rel + mt.y;
+            st2 = KState{mt.z, jh | (jh << 16), __fadd_rn(pen, __uint_as_float(mt.w)), packed + 0x10000u};
+          }
+          push_lanes<QCAP>(q, head, tail, keep, st2, err);
+        }
       }
 
       // swap (:935-989)
       if (j + 1 < n && P.p_swp <= remaining && (!fast || edits < P.mef)) {
         const uint32_t nch = have_next ? next_ch : text_char(P, S, j + 1, err);
-        const int64_t x = small ? small_goto(nch) : (gt_get(P, nk | nch, true, gx) ? (int64_t)(gx & CHILD26_MASK) : -1);
+        const int64_t x = MAP ? wave_find_gid(P, st.node, text_gid(P, S, j + 1, err))  // :945-961
+                          : small   ? small_goto(nch)
+                                    : (gt_get(P, nk | nch, true, gx) ? (int64_t)(gx & CHILD26_MASK) : -1);
         if (x >= 0) {
-          const int64_t node2 = gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)x << 21) | cur_ch, true, gx)
+          const int64_t node2 = MAP ? wave_find_gid(P, (uint32_t)x, text_gid(P, S, j, err))
+                                : gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)x << 21) | cur_ch, true, gx)
                                     ? (int64_t)(gx & CHILD26_MASK) : -1;
           bool ok = node2 >= 0;
           if (ok && !fast) {  // within_limits_swap_ahead with node2's limits (:962-967)
@@ -550,6 +619,7 @@ struct LaneExp {
   bool ins;          // insertion successor
   uint64_t msub, mdel;
   uint32_t count;    // pushes of this state
+  uint64_t mmap;     // MAP: applicable mapping transitions of the node (bit t = its t-th)
 };
 
 __device__ __forceinline__ bool sb_word_bit(uint4 m, uint32_t ch) {  // branch-free (no stack indexing)
@@ -577,6 +647,7 @@ struct Prep {
   uint32_t cur_ch, next_ch, nch;
   uint32_t flags;  // PF_* bits
   float remaining;
+  uint32_t gcur, gnx;  // MAP: grapheme ids at j and j + 1 (0 otherwise)
 };
 constexpr uint32_t PF_SUB = 1u, PF_DEL = 2u, PF_LAST = 4u, PF_CSB = 8u, PF_NEXT = 16u, PF_CUR = 32u, PF_SWAP = 64u,
                    PF_EX = 128u, PF_INS = 256u;
@@ -683,7 +754,7 @@ __device__ __forceinline__ int unit_owner(ExpScratch* X, uint32_t R, uint32_t nu
 // the units of all states are dealt to lanes in rounds of 64 (a lane-per-state loop would run
 // for the batch's largest degree). Per edge: the exact/swap first-char match (structs.rs:512-519),
 // substitution (:814-874) and deletion (:1055-1088) keep tests incl. the last-edit dead-end filter.
-template <uint32_t UK>
+template <uint32_t UK, bool MAP>
 __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode& nd, const Prep& pr, bool act,
                              uint64_t& msub, uint64_t& mdel, uint32_t& ex, uint32_t& xe) {
   const uint32_t lane = lane_id();
@@ -704,6 +775,11 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
     const uint32_t o_pk = __shfl(pk, o), o_eb = __shfl(nd.edge_begin, o);
     const uint32_t cur = __shfl(pr.cur_ch, o), nxt = __shfl(pr.next_ch, o), nc = __shfl(pr.nch, o);
     const float rem = __shfl(pr.remaining, o);
+    uint32_t gc = 0, gn = 0;
+    if constexpr (MAP) {
+      gc = __shfl(pr.gcur, o);
+      gn = __shfl(pr.gnx, o);
+    }
     const uint32_t o_deg = (o_pk >> 9) & 0x7Fu, e0 = (R + lane - (o_pk >> 16)) * UK;
     const bool sub_on = o_pk & PF_SUB, del_ok = o_pk & PF_DEL, is_last = o_pk & PF_LAST, need_csb = o_pk & PF_CSB;
     const bool have_next = o_pk & PF_NEXT, have_cur = o_pk & PF_CUR, swap_ok = o_pk & PF_SWAP, ex_on = o_pk & PF_EX;
@@ -716,8 +792,17 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
       const bool child_out = (ed.next & EDGE_CHILD_OUTPUT) != 0;
       const uint4 csb = P.sb_edge[(ok && need_csb) ? o_eb + e : 0u];  // parallel with the edge load
       const uint32_t enc = ((63u - e) << 26) | (ed.next & CHILD26_MASK);  // child ids < 2^26 (builder)
-      fe = (ok && ex_on && fe == 0u && ed.ch == cur) ? enc : fe;
-      fx = (ok && swap_ok && fx == 0u && ed.ch == nc) ? enc : fx;
+      bool mex, msw;
+      if constexpr (MAP) {  // whole-grapheme transitions (structs.rs:452-464)
+        const uint32_t eg = P.edge_gid[ok ? o_eb + e : 0u];
+        mex = eg == gc;
+        msw = eg == gn;
+      } else {  // first-char transitions (structs.rs:512-519)
+        mex = ed.ch == cur;
+        msw = ed.ch == nc;
+      }
+      fe = (ok && ex_on && fe == 0u && mex) ? enc : fe;
+      fx = (ok && swap_ok && fx == 0u && msw) ? enc : fx;
       const float sim = similarity(P, ed.ch, cur);
       const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
       const bool sb_next = child_out || (have_next && sb_word_bit(csb, nxt));
@@ -795,17 +880,23 @@ __device__ void expand_fast(const SearchParams& P, const KState& st, const DevNo
 
 // Per-state completion: exact successor, the exact edge leaves the substitution set, swap target
 // goto(goto(node, text[j+1]), text[j]) (:945-967), push count.
-__device__ LaneExp lane_finish(const SearchParams& P, const KState& st, const DevNode& nd, const Prep& pr,
-                               uint64_t msub, uint64_t mdel, uint32_t ex, uint32_t xe) {
-  LaneExp x{-1, -1, false, msub, mdel, 0u};
+template <bool MAP>
+__device__ LaneExp lane_finish(const SearchParams& P, const SegDesc& S, uint64_t start, const KState& st,
+                               const DevNode& nd, const Prep& pr, uint64_t msub, uint64_t mdel, uint32_t ex,
+                               uint32_t xe, unsigned& err) {
+  LaneExp x{-1, -1, false, msub, mdel, 0u, 0ull};
   if (ex) {  // exx encodings (expand_units)
     x.exact = (int64_t)(ex & CHILD26_MASK);
     x.msub &= ~(1ull << (63u - (ex >> 26)));
   }
   if (xe) {  // node2 = goto(xnode, text[j]) through the goto table
-    uint64_t g;
-    if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)(xe & CHILD26_MASK) << 21) | pr.cur_ch, true, g))
-      x.swap = (int64_t)(g & CHILD26_MASK);
+    if constexpr (MAP) {
+      x.swap = find_gid(P, xe & CHILD26_MASK, pr.gcur);
+    } else {
+      uint64_t g;
+      if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)(xe & CHILD26_MASK) << 21) | pr.cur_ch, true, g))
+        x.swap = (int64_t)(g & CHILD26_MASK);
+    }
     if (x.swap >= 0 && P.mef == 255u) {  // within_limits_swap_ahead with node2's limits (:962-967)
       const uint32_t packed = st.packed, edits = edits_of(packed);
       const Lim m = pick_limits(P, node_limits(P, (uint32_t)x.swap));
@@ -813,8 +904,10 @@ __device__ LaneExp lane_finish(const SearchParams& P, const KState& st, const De
     }
   }
   x.ins = (pr.flags & PF_INS) != 0;
+  if constexpr (MAP)  // inside the substitution block (:883), i.e. j < n and subst_ok
+    if (pr.flags & PF_SUB) x.mmap = map_mask(P, S, st.node, start + (st.jm & 0xFFFFu), st.pen, err);
   x.count = (x.exact >= 0 ? 1u : 0u) + (uint32_t)__popcll(x.msub) + (x.swap >= 0 ? 1u : 0u) + (x.ins ? 1u : 0u) +
-            (uint32_t)__popcll(x.mdel);
+            (uint32_t)__popcll(x.mdel) + (uint32_t)__popcll(x.mmap);
   return x;
 }
 
@@ -842,7 +935,7 @@ __device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t r) {
 // substitutions (edge order), swap, insertion, deletions (edge order), written at the state's
 // exclusive-prefix offset. The owner lane writes exact/swap/insertion; substitutions and deletions
 // are written by the units that cover their edges (balanced like expand_units).
-template <uint32_t QCAP, uint32_t UK>
+template <uint32_t QCAP, uint32_t UK, bool MAP>
 __device__ void push_units(const SearchParams& P, ExpScratch* X, KState* q, uint32_t base, const KState& st,
                            const DevNode& nd, const LaneExp& x, uint32_t cur_ch, bool act) {
   const uint32_t lane = lane_id();
@@ -851,7 +944,8 @@ __device__ void push_units(const SearchParams& P, ExpScratch* X, KState* q, uint
   const uint32_t jm1 = (j_rel + 1u) | ((j_rel + 1u) << 16);
   const uint32_t nex = x.exact >= 0 ? 1u : 0u, nsw = x.swap >= 0 ? 1u : 0u, nins = x.ins ? 1u : 0u;
   const uint32_t sub_base = base + nex;
-  const uint32_t sw_pos = sub_base + (uint32_t)__popcll(x.msub);
+  const uint32_t map_pos = sub_base + (uint32_t)__popcll(x.msub);
+  const uint32_t sw_pos = map_pos + (uint32_t)__popcll(x.mmap);
   const uint32_t del_base = sw_pos + nsw + nins;
   if (act) {
     if (nex) q[base & (QCAP - 1)] = KState{(uint32_t)x.exact, jm1, pen, st.packed};
@@ -863,6 +957,19 @@ __device__ void push_units(const SearchParams& P, ExpScratch* X, KState* q, uint
       const uint32_t jmi = (j_rel + 1u) | ((st.jm >> 16) << 16);
       q[(sw_pos + nsw) & (QCAP - 1)] = KState{st.node, jmi, __fadd_rn(pen, P.p_ins), st.packed + 1u};
     }
+    if constexpr (MAP)
+      if (x.mmap) {  // mapping pushes, after the substitutions (:883-922)
+        const uint32_t mb = P.map_range[st.node].x;
+        uint64_t mm = x.mmap;
+        uint32_t pos = map_pos;
+        while (mm) {
+          const uint32_t t = (uint32_t)__ffsll((unsigned long long)mm) - 1u;
+          mm &= mm - 1;
+          const uint4 mt = P.map_ent[mb + t];
+          const uint32_t jh = j_rel + mt.y;
+          q[(pos++) & (QCAP - 1)] = KState{mt.z, jh | (jh << 16), __fadd_rn(pen, __uint_as_float(mt.w)), st.packed + 0x10000u};
+        }
+      }
   }
   // substitutions and deletions, one push per lane: push k of a state is the k-th set bit of its
   // msub, then of its mdel
@@ -963,7 +1070,7 @@ __device__ unsigned long long g_prof[16];
 // batches of up to 64 (one state per lane); a batch is cut exactly where the reference's sequential
 // semantics would diverge: before the first in-batch dedup conflict, before the first pop at which
 // the beam would trigger, and before the first >64-edge node (expanded alone, edge-parallel).
-template <uint32_t VCAP, uint32_t QCAP>
+template <uint32_t VCAP, uint32_t QCAP, bool MAP>
 __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
                            uint32_t& cseq, EmitList& EL, uint64_t start, const RcHit& rc, uint64_t& popped,
                            uint64_t& cached, unsigned& err, uint32_t& head_out, uint32_t& vcount_out) {
@@ -1042,6 +1149,13 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
       if (j < S.n) c0 = text_char(P, S, j, err);
       if (j + 1 < S.n) c1 = text_char(P, S, j + 1, err);
     }
+    uint32_t g0 = 0, g1 = 0;
+    if constexpr (MAP)
+      if (in_b) {
+        const uint64_t j = start + (st.jm & 0xFFFFu);
+        if (j < S.n) g0 = text_gid(P, S, j, err);
+        if (j + 1 < S.n) g1 = text_gid(P, S, j + 1, err);
+      }
     bool found = false;
     uint32_t stored_bits = 0, vslot = EMPTY;
     if constexpr (VCAP > 0)  // VCAP == 0: no dedup (unbeamed only)
@@ -1072,7 +1186,7 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
         if (visited_check<VCAP>(vis, vcount, s0, P.exact_dedup != 0, err)) continue;
       const DevNode n0 = P.nodes[s0.node];
       if (node_has_out(n0)) emit_state(P, EL, s0.jm >> 16, s0.pen, s0.packed, s0.node, err);
-      expand_wide<QCAP>(P, S, q, head, tail, s0, n0, start, err);
+      expand_wide<QCAP, MAP>(P, S, q, head, tail, s0, n0, start, err);
       PROF_ACC(2, t2);
       if (any_err(err)) break;
       continue;
@@ -1080,18 +1194,22 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     PROF_T(t3);
     uint32_t Bc = mwide ? (uint32_t)first_lane(mwide) : B;
     // ---- phase B: per-lane expansion decisions and push counts
-    LaneExp x{-1, -1, false, 0ull, 0ull, 0u};
+    LaneExp x{-1, -1, false, 0ull, 0ull, 0u, 0ull};
     const bool act = alive && lane < Bc;
     Prep pr{0u, 0u, 0u, 0u, 0.0f};
     PROF_T(tb0);
     if (act) pr = lane_prep(P, S, st, nd, start, c0, c1, nd.sb);
+    if constexpr (MAP) {
+      pr.gcur = g0;
+      pr.gnx = g1;
+    }
     PROF_ACC(9, tb0);
     PROF_T(tb1);
     uint64_t msub = 0, mdel = 0;
     uint32_t ex = 0u, xe = 0u;
     const bool fast = act && P.gt_fast && (!(pr.flags & PF_SUB) || P.p_sub <= pr.remaining);
     if (__ballot(act && !fast))  // per-edge path for the states similarity can prune
-      expand_units<FAC_UK>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act && !fast, msub, mdel, ex, xe);
+      expand_units<FAC_UK, MAP>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act && !fast, msub, mdel, ex, xe);
     if (fast) expand_fast(P, st, nd, pr, aux, msub, mdel, ex, xe);
 #if defined(FAC_DUP) && FAC_DUP == 1
     if (fast) {
@@ -1110,14 +1228,14 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
 #endif
     PROF_ACC(10, tb1);
     PROF_T(tb2);
-    if (act) x = lane_finish(P, st, nd, pr, msub, mdel, ex, xe);
+    if (act) x = lane_finish<MAP>(P, S, start, st, nd, pr, msub, mdel, ex, xe, err);
 #if defined(FAC_DUP) && FAC_DUP == 2
     if (act) {
       KState s2{opq(st.node), opq(st.jm), opqf(st.pen), opq(st.packed)};
       DevNode n2{opqf(nd.prune_len), opqf(nd.prune_lw), opq(nd.edge_begin), opq(nd.degf),
                  make_uint4(opq(nd.sb.x), opq(nd.sb.y), opq(nd.sb.z), opq(nd.sb.w))};
       const Prep p2 = lane_prep(P, S, s2, n2, start, opq(c0), opq(c1), n2.sb);
-      const LaneExp x2 = lane_finish(P, s2, n2, p2, opq64(msub), opq64(mdel), opq(ex), opq(xe));
+      const LaneExp x2 = lane_finish<MAP>(P, S, start, s2, n2, p2, opq64(msub), opq64(mdel), opq(ex), opq(xe), err);
       sink(p2.flags);
       sink(p2.cur_ch);
       sink(x2.count);
@@ -1227,10 +1345,10 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     }
     PROF_ACC(5, t5);
     PROF_T(t6);
-    push_units<QCAP, FAC_UK>(P, reinterpret_cast<ExpScratch*>(claim), q, tail + excl, st, nd, x, pr.cur_ch,
-                             alive && lane < Bc && x.count != 0);
+    push_units<QCAP, FAC_UK, MAP>(P, reinterpret_cast<ExpScratch*>(claim), q, tail + excl, st, nd, x, pr.cur_ch,
+                                  alive && lane < Bc && x.count != 0);
 #if defined(FAC_DUP) && FAC_DUP == 4
-    push_units<QCAP, FAC_UK>(P, reinterpret_cast<ExpScratch*>(claim), q, opq(tail + excl), st, nd, x, opq(pr.cur_ch),
+    push_units<QCAP, FAC_UK, MAP>(P, reinterpret_cast<ExpScratch*>(claim), q, opq(tail + excl), st, nd, x, opq(pr.cur_ch),
                              alive && lane < Bc && x.count != 0);  // same entries rewritten
 #endif
     __builtin_amdgcn_wave_barrier();
@@ -1387,7 +1505,7 @@ __global__ __launch_bounds__(256) void rc_collect_kernel(SearchParams P, unsigne
   }
 }
 
-template <uint32_t VCAP, uint32_t QCAP>
+template <uint32_t VCAP, uint32_t QCAP, bool MAP>
 __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   __shared__ KState s_vis[VCAP ? VCAP : 1];
   __shared__ KState s_q[QCAP];
@@ -1430,7 +1548,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         const RcHit rc{shfl_u32(hit.off, l), shfl_u32(hit.head, l), shfl_u32(hit.tail, l), shfl_u32(hit.nv_nel, l),
                        shfl_u32(hit.pops, l)};
         const uint32_t qlen =
-            run_window<VCAP, QCAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, rc, popped, cached, err, qhead, vcnt);
+            run_window<VCAP, QCAP, MAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, rc, popped, cached, err, qhead, vcnt);
         if (P.rc_mode == 2) {  // cache build: entry = list position; what does not fit stays uncached
           const uint32_t ent = (uint32_t)(v0 + (uint64_t)l);
           const uint32_t nq = qlen - qhead;
@@ -1508,19 +1626,19 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
 
 // one wavefront per workgroup; the dedup-free variants are held to <= 128 VGPRs (4 waves/SIMD),
 // the dedup variants are bounded by LDS first
-template <uint32_t VCAP, uint32_t QCAP>
+template <uint32_t VCAP, uint32_t QCAP, bool MAP>
 __global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
-  bfs_window_body<VCAP, QCAP>(P);
+  bfs_window_body<VCAP, QCAP, MAP>(P);
 }
-template <uint32_t QCAP>
+template <uint32_t QCAP, bool MAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QCAP <= 512 ? 4 : 1))) void bfs_window_kernel_nd(SearchParams P) {
-  bfs_window_body<0, QCAP>(P);
+  bfs_window_body<0, QCAP, MAP>(P);
 }
 // prefix-cache build (P.rc_mode == 2): one representative window per key, popped up to the first
 // state past the key; its own symbol so profiles separate it from the search launches
 template <uint32_t QCAP>
 __global__ __launch_bounds__(64) void rc_build_kernel(SearchParams P) {
-  bfs_window_body<512, QCAP>(P);
+  bfs_window_body<512, QCAP, false>(P);  // the prefix cache is off with mappings
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1686,12 +1804,14 @@ uint32_t lds_pad() {
 
 template <uint32_t Q>
 void launch_nd(uint32_t grid, hipStream_t s, const SearchParams& P) {
-  hipLaunchKernelGGL((bfs_window_kernel_nd<Q>), dim3(grid), dim3(64), lds_pad(), s, P);
+  if (P.has_map) hipLaunchKernelGGL((bfs_window_kernel_nd<Q, true>), dim3(grid), dim3(64), lds_pad(), s, P);
+  else hipLaunchKernelGGL((bfs_window_kernel_nd<Q, false>), dim3(grid), dim3(64), lds_pad(), s, P);
 }
 
 template <uint32_t V, uint32_t Q>
 void launch_one(uint32_t grid, hipStream_t s, const SearchParams& P) {
-  hipLaunchKernelGGL((bfs_window_kernel<V, Q>), dim3(grid), dim3(64), lds_pad(), s, P);
+  if (P.has_map) hipLaunchKernelGGL((bfs_window_kernel<V, Q, true>), dim3(grid), dim3(64), lds_pad(), s, P);
+  else hipLaunchKernelGGL((bfs_window_kernel<V, Q, false>), dim3(grid), dim3(64), lds_pad(), s, P);
 }
 
 // LDS per wave: 16 B x (vcap + qcap) + vcap claim bytes
@@ -1816,6 +1936,14 @@ int upload_engine(Engine& e, std::string& err) {
   if ((rc = upload(e.sim_ascii, &e.d_sim_ascii, err))) return rc;
   if ((rc = upload(e.sim_keys, &e.d_sim_keys, err))) return rc;
   if ((rc = upload(e.sim_vals, &e.d_sim_vals, err))) return rc;
+  if (e.has_map) {
+    if ((rc = upload(e.edge_gid, &e.d_edge_gid, err))) return rc;
+    std::vector<uint32_t> ag(e.ascii_gid, e.ascii_gid + 128);
+    if ((rc = upload(ag, &e.d_ascii_gid, err))) return rc;
+    if ((rc = upload(e.map_range, &e.d_map_range, err))) return rc;
+    if ((rc = upload(e.map_ent, &e.d_map_ent, err))) return rc;
+    if ((rc = upload(e.map_hay, &e.d_map_hay, err))) return rc;
+  }
   if (e.bitap_ok) {
     // transposed masks [(alphabet+1)][P] so the lanes of a wave (consecutive patterns) coalesce
     const size_t np = e.bp_m.size(), A = e.alphabet + 1;
@@ -1836,7 +1964,8 @@ void free_engine_device(Engine& e) {
   if (e.d_nodes == nullptr && e.stream == nullptr) return;
   (void)hipSetDevice(e.device);
   void* ptrs[] = {e.d_nodes, e.d_out_range, e.d_pidx, e.d_edges, e.d_out_pat, e.d_sb_edge, e.d_gt, e.d_aux, e.d_pat_bytes, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
-                  e.d_sim_vals, e.d_bp_mask, e.d_ascii_id};
+                  e.d_sim_vals, e.d_bp_mask, e.d_ascii_id, e.d_edge_gid, e.d_ascii_gid, e.d_map_range,
+                  e.d_map_ent, e.d_map_hay};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int i = 0; i < Engine::kScratch; ++i)
@@ -1897,9 +2026,33 @@ void free_haystack(Haystack& h) {
   if (h.d_utf8) (void)hipFree(h.d_utf8);
   if (h.d_text32) (void)hipFree(h.d_text32);
   if (h.d_off) (void)hipFree(h.d_off);
+  if (h.d_gid) (void)hipFree(h.d_gid);
   h.d_utf8 = nullptr;
   h.d_text32 = nullptr;
   h.d_off = nullptr;
+  h.d_gid = nullptr;
+}
+
+// Grapheme ids of a Unicode haystack for an engine with mappings (gs_text compared as whole
+// folded graphemes, grapheme.rs:61-63): computed on the host on first use and uploaded.
+int ensure_gids(const Engine& e, const Haystack& h, std::string& err) {
+  if (h.ascii || (h.d_gid && h.gid_engine == &e)) return FAC_OK;
+  std::vector<uint32_t> gid(h.n, 0);
+  std::u32string g;
+  const uint8_t* utf8 = h.utf8.data();
+  for (uint64_t i = 0; i < h.n; ++i) {
+    const uint64_t b = h.starts[i], en = i + 1 < h.n ? h.starts[i + 1] : h.len;
+    fold_grapheme(utf8, b, en, e.case_insensitive, g);
+    auto it = e.gid_of.find(g);
+    if (it != e.gid_of.end()) gid[i] = it->second;
+  }
+  HIP_TRY(hipSetDevice(h.device));
+  if (h.d_gid) HIP_TRY(hipFree(h.d_gid));
+  h.d_gid = nullptr;
+  HIP_TRY(hipMalloc((void**)&h.d_gid, std::max<size_t>(gid.size() * sizeof(uint32_t), 16)));
+  if (!gid.empty()) HIP_TRY(hipMemcpy(h.d_gid, gid.data(), gid.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  h.gid_engine = &e;
+  return FAC_OK;
 }
 
 // One search over the windows of `segs_in` with a given beam (0 = none). exact_dedup: the dedup
@@ -1964,6 +2117,17 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.beam = beam;
   P.exact_dedup = exact_dedup ? 1 : 0;
   P.window_skip = e.window_skip;
+  P.has_map = e.has_map ? 1 : 0;
+  if (e.has_map) {  // multi-character mappings: whole-grapheme ids (ensure_gids for Unicode text)
+    const int grc = ensure_gids(e, h, err);
+    if (grc) return grc;
+    P.edge_gid = e.d_edge_gid;
+    P.gid32 = h.d_gid;
+    P.ascii_gid = e.d_ascii_gid;
+    P.map_range = e.d_map_range;
+    P.map_ent = e.d_map_ent;
+    P.map_hay = e.d_map_hay;
+  }
   std::memcpy(P.first_bits, e.first_bits, sizeof(P.first_bits));
   std::memcpy(P.second_bits, e.second_bits, sizeof(P.second_bits));
   P.chunk = 256;
@@ -1974,8 +2138,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   // Variant ladder. A variant fits when one state's fan-out always fits the ring: for a beam,
   // after the selection (<= 2 bw pending, search.rs:577-589) plus one non-root state's pushes;
   // without one, only the single-state bound (overflowing windows spill to the next variant).
-  const uint64_t fan_root = 3ull + 2ull * (e.nodes.empty() ? 0u : e.nodes[0].edge_end - e.nodes[0].edge_begin);
-  const uint64_t fan_nr = 3ull + 2ull * e.max_degree_nonroot;
+  const uint64_t fan_root = 3ull + e.max_map + 2ull * (e.nodes.empty() ? 0u : e.nodes[0].edge_end - e.nodes[0].edge_begin);
+  const uint64_t fan_nr = 3ull + e.max_map + 2ull * e.max_degree_nonroot;
   auto fits = [&](const Variant& v) {
     if (P.beam) return v.vcap > 0 && fan_root + 1 <= v.qcap && 2ull * P.beam + fan_nr + 1 <= v.qcap;
     return (v.vcap > 0 || !exact_dedup) && fan_root + 1 <= v.qcap && fan_nr + 1 <= v.qcap;
@@ -2059,7 +2223,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   const bool root_out = !e.nodes.empty() && e.nodes[0].out_end > e.nodes[0].out_begin;
   const char* rc_min = std::getenv("FAC_RC_MIN");  // env knobs: tests force it on / pin K, A/B turns it off
   const char* kenv = std::getenv("FAC_RC_K");
-  if (!root_out && fan_root + 1 <= 4096 && kVariants[vi].qcap <= 4096 &&
+  if (!root_out && !e.has_map && fan_root + 1 <= 4096 && kVariants[vi].qcap <= 4096 &&
       windows >= (rc_min ? std::strtoull(rc_min, nullptr, 10) : 4096ull) && !std::getenv("FAC_NO_RC")) {
     const uint32_t kpin = kenv ? (uint32_t)std::min<unsigned long>(4, std::max<unsigned long>(2, std::strtoul(kenv, nullptr, 10))) : 0u;
     const uint32_t qmain = kVariants[vi].qcap, vmain = kVariants[vi].vcap;

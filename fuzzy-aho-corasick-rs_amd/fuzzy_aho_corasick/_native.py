@@ -32,6 +32,11 @@ class fac_pattern(ctypes.Structure):
                 ("has_limits", ctypes.c_int32), ("limits", fac_limits)]
 
 
+class fac_mapping(ctypes.Structure):
+    _fields_ = [("a", ctypes.c_char_p), ("a_len", ctypes.c_uint64), ("b", ctypes.c_char_p),
+                ("b_len", ctypes.c_uint64), ("score", ctypes.c_float)]
+
+
 class fac_config(ctypes.Structure):
     _fields_ = [("case_insensitive", ctypes.c_int32), ("has_limits", ctypes.c_int32),
                 ("limits", fac_limits), ("penalty_insertion", ctypes.c_float),
@@ -43,7 +48,8 @@ class fac_config(ctypes.Structure):
                 ("n_similarity_pairs", ctypes.c_uint64),
                 ("similarity_pairs", ctypes.POINTER(ctypes.c_uint32)),
                 ("similarity_pair_values", ctypes.POINTER(ctypes.c_float)),
-                ("n_mappings", ctypes.c_uint64), ("device", ctypes.c_int32)]
+                ("n_mappings", ctypes.c_uint64), ("mappings", ctypes.POINTER(fac_mapping)),
+                ("device", ctypes.c_int32)]
 
 
 def _match_dtype():

@@ -133,6 +133,14 @@ class FuzzyAhoCorasick:
             cfg.similarity_pair_values = vals
             self._keep += [tab, ab, vals]
         cfg.n_mappings = len(builder._mappings)
+        if builder._mappings:  # builder.rs:116-132
+            maps = (_native.fac_mapping * len(builder._mappings))()
+            for i, (a, b, score) in enumerate(builder._mappings):
+                ea, eb = a.encode("utf-8"), b.encode("utf-8")
+                self._keep += [ea, eb]
+                maps[i].a, maps[i].a_len, maps[i].b, maps[i].b_len, maps[i].score = ea, len(ea), eb, len(eb), score
+            cfg.mappings = maps
+            self._keep.append(maps)
         cfg.device = builder._device
         arr = (_native.fac_pattern * max(1, len(patterns)))()
         enc = []

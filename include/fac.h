@@ -18,8 +18,8 @@
  *   FAC_OK                      0
  *   FAC_E_HAYSTACK_TOO_LARGE    1   SearchError::HaystackTooLarge{graphemes} (search.rs:198-201)
  *   FAC_E_INVALID             100   bad argument (NULL, invalid UTF-8, beam_width == 0, ...)
- *   FAC_E_UNSUPPORTED         101   configuration outside the GPU path (mappings) — never a
- *                                   silent CPU fallback
+ *   FAC_E_UNSUPPORTED         101   configuration outside the GPU path (> 64 mapping transitions
+ *                                   at one node, > 2^26 nodes, ...) — never a silent CPU fallback
  *   FAC_E_HIP                 102   HIP runtime error (fac_last_error() has the text)
  *   FAC_E_NO_DEVICE           103   no usable MI355X (gfx950) device
  *   FAC_E_OOM                 104   host or device allocation failure
@@ -67,6 +67,16 @@ typedef struct fac_pattern {
   fac_limits limits; /* per-pattern limits, finalized; used iff has_limits */
 } fac_pattern;
 
+/* One multi-character mapping rule (a, b, score), builder.rs:30-31, 116-132: either side may
+ * stand in for the other at penalty substitution * (1 - score), counted as one substitution. */
+typedef struct fac_mapping {
+  const char* a; /* UTF-8 */
+  uint64_t a_len;
+  const char* b; /* UTF-8 */
+  uint64_t b_len;
+  float score;
+} fac_mapping;
+
 /* Builder state (src/builder.rs:22-33, FuzzyPenalties structs.rs:370-393). */
 typedef struct fac_config {
   int32_t case_insensitive;
@@ -88,9 +98,10 @@ typedef struct fac_config {
   uint64_t n_similarity_pairs;
   const uint32_t* similarity_pairs; /* 2*n code points (a, b) */
   const float* similarity_pair_values;
-  /* Multi-character mappings (builder.rs:108-132): not on the GPU path; n_mappings > 0 makes
-   * fac_build return FAC_E_UNSUPPORTED. */
+  /* Multi-character mappings (builder.rs:108-132, mapping / mapping_scored): applied
+   * bidirectionally; precomputed per trie node like builder.rs:383-442. */
   uint64_t n_mappings;
+  const struct fac_mapping* mappings;
   int32_t device; /* HIP device ordinal for this engine's tables */
 } fac_config;
 

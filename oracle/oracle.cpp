@@ -91,8 +91,19 @@ struct Similarity {  // structs.rs:9-14, 30-54, 82-92
   }
 };
 
+struct MapT {  // MappingTransition (structs.rs:235-242)
+  std::vector<std::u32string> hay;  // haystack graphemes to consume (folded)
+  uint32_t next;                    // node reached by the pattern-side walk
+  float penalty;                    // substitution * (1 - score)
+};
+
 struct Engine {
   std::vector<Node> nodes;
+  // multi-character mappings: rules as configured (folded sides, score), and the precomputed
+  // per-node transitions (builder.rs:383-442); has_mappings = !self.mappings.is_empty()
+  std::vector<std::tuple<std::vector<std::u32string>, std::vector<std::u32string>, float>> map_rules;
+  std::vector<std::vector<MapT>> mappings;
+  bool has_mappings = false;
   std::vector<Pattern> patterns;
   Similarity sim;
   bool has_limits = false;
@@ -154,8 +165,9 @@ size_t k_from_limits(const Limits& l, bool& bounded) {  // prefilter.rs:388-405
   return (size_t)l.ins + l.del + l.sub + 2 * (size_t)l.swp;
 }
 
-void build_bitap(Engine& e) {  // prefilter.rs:161-245 (mappings never configured in the oracle)
+void build_bitap(Engine& e) {  // prefilter.rs:161-245
   e.bitap_ok = false;
+  if (e.has_mappings) return;  // :162-165
   if (e.patterns.empty()) return;
   float max_sim = e.sim.max_off_diagonal();
   float p_sub_min = e.p_sub * (1.0f - max_sim);
@@ -320,6 +332,35 @@ void build(Engine& e) {
     else
       e.max_edits_fast = 255;
   }
+  // multi-character mapping transitions (builder.rs:383-442): each rule in both directions; from
+  // every node, walk the pattern side through the trie and record a jump consuming the haystack side
+  e.mappings.assign(nn, {});
+  e.has_mappings = false;
+  if (!e.map_rules.empty()) {
+    std::vector<std::tuple<std::vector<std::u32string>, std::vector<std::u32string>, float>> directed;
+    for (auto& r : e.map_rules) {
+      const auto& ga = std::get<0>(r);
+      const auto& gb = std::get<1>(r);
+      if (ga.empty() || gb.empty() || ga == gb) continue;
+      const float penalty = e.p_sub * (1.0f - std::get<2>(r));
+      directed.emplace_back(ga, gb, penalty);
+      directed.emplace_back(gb, ga, penalty);
+    }
+    for (size_t start = 0; start < nn; ++start)
+      for (auto& d : directed) {
+        size_t cur = start;
+        bool ok = true;
+        for (auto& g : std::get<0>(d)) {
+          auto it = nodes[cur].transitions.find(g);
+          if (it == nodes[cur].transitions.end()) { ok = false; break; }
+          cur = it->second;
+        }
+        if (ok) {
+          e.mappings[start].push_back({std::get<1>(d), (uint32_t)cur, std::get<2>(d)});
+          e.has_mappings = true;
+        }
+      }
+  }
   build_bitap(e);
 }
 
@@ -376,6 +417,17 @@ struct Searcher {
       if (ed.first_char == ch) return ed.next;
     return -1;
   }
+  // Node::find_transition (structs.rs:452-464): a one-byte grapheme takes the first single-byte
+  // edge with that char; anything longer is a transitions-map lookup of the whole grapheme
+  static int64_t find_transition(const Node& n, const std::u32string& g) {
+    if (g.size() == 1 && g[0] < 0x80) {
+      for (auto& ed : n.edges)
+        if (ed.first_char == g[0] && ed.single_byte) return ed.next;
+      return -1;
+    }
+    auto it = n.transitions.find(g);
+    return it == n.transitions.end() ? -1 : (int64_t)it->second;
+  }
   static bool has_matching_edge_char(const Node& n, uint32_t ch) {  // structs.rs:471-475
     for (auto& ed : n.edges)
       if (ed.first_char == ch && ed.single_byte) return true;
@@ -414,10 +466,12 @@ struct Searcher {
   // `text_chars`, grapheme byte offsets (nullptr = identity), haystack byte length.
   uint32_t w_begin = 0, w_end = 0xFFFFFFFFu;  // start-window range (sharding diagnostics)
 
+  // gt: the folded grapheme strings (gs_text), required when the engine has mappings
   void run(const uint32_t* tc, const uint64_t* off, uint32_t n, uint64_t hay_len, float thr,
-           std::vector<Match>& out) {
+           std::vector<Match>& out, const std::u32string* gt = nullptr) {
     out.clear();
     if (n == 0) return;
+    const bool MAPPINGS = e.has_mappings;  // search.rs:204, 303
     const uint32_t mef = e.max_edits_fast == 0 || e.max_edits_fast > 6 ? 255 : e.max_edits_fast;
     const bool fast = mef != 255;
     const uint32_t text_len = n;
@@ -435,7 +489,7 @@ struct Searcher {
 
     bool ws = false;  // :504-521
     __uint128_t first_bits = 0, second_bits = 0;
-    if (mef == 1 && root.output.empty()) {
+    if (mef == 1 && !MAPPINGS && root.output.empty()) {  // :505 (WINDOW_SKIP && !MAPPINGS)
       first_bits = single_char_edge_bits(root);
       bool child_output = false;
       for (auto& ed : root.edges) {
@@ -527,7 +581,8 @@ struct Searcher {
           uint32_t next_ch = 0;
           if (is_last_edit && (!fast || edits < mef) && j + 1 < text_len) { have_next = true; next_ch = tc[j + 1]; }
           const uint32_t ms_next = st.me == st.ms ? j : st.ms;
-          int64_t exact_next = find_no_mappings(nd, current_ch);  // :776-780 (MAPPINGS=false)
+          int64_t exact_next = MAPPINGS ? find_transition(nd, gt[j])           // :776-780
+                                        : find_no_mappings(nd, current_ch);
           if (exact_next >= 0) {
             queue.push_back({(uint32_t)exact_next, j + 1, ms_next, j + 1, st.pen, edits, pc});
             ++states_pushed;
@@ -547,12 +602,26 @@ struct Searcher {
               queue.push_back({ed.next, j + 1, ms_next, j + 1, st.pen + penalty, (uint8_t)(edits + 1), pc + 0x10000});
               ++states_pushed;
             }
+            if (MAPPINGS)  // 1b) multi-character mappings (:883-922)
+              for (const MapT& mt : e.mappings[st.node]) {
+                const uint32_t hlen = (uint32_t)mt.hay.size();
+                if ((uint64_t)j + hlen > text_len) continue;
+                bool hay_matches = true;
+                for (uint32_t k = 0; k < hlen && hay_matches; ++k) hay_matches = gt[j + k] == mt.hay[k];
+                if (!hay_matches) continue;
+                const float np = st.pen + mt.penalty;
+                if (np > max_penalties) continue;
+                queue.push_back({mt.next, j + hlen, ms_next, j + hlen, np, (uint8_t)(edits + 1), pc + 0x10000});
+                ++states_pushed;
+              }
           }
           // swap :935-989
           if (j + 1 < text_len && e.p_swp <= remaining && (!fast || edits < mef)) {
             uint32_t nch = have_next ? next_ch : tc[j + 1];
-            int64_t x = find_no_mappings(nd, nch);
-            int64_t node2 = x >= 0 ? find_no_mappings(e.nodes[(size_t)x], current_ch) : -1;
+            int64_t x = MAPPINGS ? find_transition(nd, gt[j + 1]) : find_no_mappings(nd, nch);  // :945-961
+            int64_t node2 = x < 0 ? -1
+                            : MAPPINGS ? find_transition(e.nodes[(size_t)x], gt[j])
+                                       : find_no_mappings(e.nodes[(size_t)x], current_ch);
             if (node2 >= 0 && (fast || swp_ahead(node_limits((uint32_t)node2), edits, (uint8_t)(pc >> 24)))) {
               queue.push_back({(uint32_t)node2, j + 2, st.ms, j + 2, st.pen + e.p_swp, (uint8_t)(edits + 1), pc + 0x1000000});
               ++states_pushed;
@@ -642,6 +711,7 @@ uint64_t g_deg_hist[80];  // diagnostics only (degree / edits histogram of expan
 // Staging for a (sub)haystack: ASCII fast path or caller-provided global graphemes.
 struct Staged {
   std::vector<uint32_t> tc;
+  std::vector<std::u32string> gt;  // folded grapheme strings (engines with mappings only)
   std::vector<uint64_t> off;  // empty = identity
   uint64_t len = 0;
 };
@@ -674,6 +744,8 @@ void search_raw_slice(const Engine& e, const Text& t, uint64_t b0, uint64_t b1, 
       if (e.case_insensitive && b >= 'A' && b <= 'Z') b += 32;
       s.tc[i] = b;
     }
+    if (e.has_mappings)  // gs_text (grapheme.rs:100-109)
+      for (uint64_t i = 0; i < s.len; ++i) s.gt.emplace_back(1, (char32_t)s.tc[i]);
   } else {  // search.rs:296-302 (global segmentation restricted to the slice)
     uint32_t n = g1 - g0;
     s.tc.resize(n);
@@ -682,6 +754,7 @@ void search_raw_slice(const Engine& e, const Text& t, uint64_t b0, uint64_t b1, 
       uint32_t g = g0 + i;
       s.tc[i] = t.goff[g + 1] > t.goff[g] ? t.cps[t.goff[g]] : 0;
       s.off[i] = t.boff[g] - b0;
+      if (e.has_mappings) s.gt.emplace_back(t.cps + t.goff[g], t.cps + t.goff[g + 1]);  // grapheme.rs:61-63
     }
   }
   if (s.tc.size() > 0xFFFFFFFFull) { out.clear(); return; }
@@ -689,7 +762,8 @@ void search_raw_slice(const Engine& e, const Text& t, uint64_t b0, uint64_t b1, 
   S.deg_hist = g_deg_hist;
   S.w_begin = w_begin;
   S.w_end = w_end;
-  S.run(s.tc.data(), s.off.empty() ? nullptr : s.off.data(), (uint32_t)s.tc.size(), s.len, thr, out);
+  S.run(s.tc.data(), s.off.empty() ? nullptr : s.off.data(), (uint32_t)s.tc.size(), s.len, thr, out,
+        s.gt.empty() ? nullptr : s.gt.data());
   if (popped) *popped += S.states_popped;
   for (auto& m : out) { m.start += b0; m.end += b0; }
 }
@@ -715,6 +789,13 @@ struct orc_config {
   uint64_t n_sim_pairs;
   const uint32_t* sim_pair_ab;    // 2*n
   const float* sim_pair_val;      // n
+  // mapping rules (builder.rs:116-132), sides already segmented + folded by the caller:
+  // rule r's side a = graphemes [side_off[2r], side_off[2r+1]), side b = [side_off[2r+1], side_off[2r+2])
+  uint64_t n_map;
+  const uint32_t* map_side_off;  // 2*n_map + 1
+  const uint32_t* map_g_off;     // graphemes + 1, into map_cps
+  const uint32_t* map_cps;
+  const float* map_score;        // n_map
 };
 
 struct orc_match {
@@ -761,6 +842,13 @@ void* orc_build(const orc_config* cfg, uint64_t n_patterns, const uint32_t* glen
     }
     for (uint32_t g = pg_off[i]; g < pg_off[i + 1]; ++g)
       p.graphemes.emplace_back(cps + g_off[g], cps + g_off[g + 1]);
+  }
+  for (uint64_t r = 0; r < cfg->n_map; ++r) {
+    std::vector<std::u32string> side[2];
+    for (int k = 0; k < 2; ++k)
+      for (uint32_t g = cfg->map_side_off[2 * r + k]; g < cfg->map_side_off[2 * r + k + 1]; ++g)
+        side[k].emplace_back(cfg->map_cps + cfg->map_g_off[g], cfg->map_cps + cfg->map_g_off[g + 1]);
+    e->map_rules.emplace_back(side[0], side[1], cfg->map_score[r]);
   }
   build(*e);
   return e;

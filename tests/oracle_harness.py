@@ -39,7 +39,9 @@ class orc_config(ctypes.Structure):
                 ("ab_width", ctypes.c_uint64), ("min_symbol_similarity", ctypes.c_float),
                 ("custom_similarity", ctypes.c_int32), ("sim_ascii", ctypes.POINTER(ctypes.c_float)),
                 ("n_sim_pairs", ctypes.c_uint64), ("sim_pair_ab", ctypes.POINTER(ctypes.c_uint32)),
-                ("sim_pair_val", ctypes.POINTER(ctypes.c_float))]
+                ("sim_pair_val", ctypes.POINTER(ctypes.c_float)), ("n_map", ctypes.c_uint64),
+                ("map_side_off", ctypes.POINTER(ctypes.c_uint32)), ("map_g_off", ctypes.POINTER(ctypes.c_uint32)),
+                ("map_cps", ctypes.POINTER(ctypes.c_uint32)), ("map_score", ctypes.POINTER(ctypes.c_float))]
 
 
 class orc_match(ctypes.Structure):
@@ -123,8 +125,20 @@ class OracleEngine:
             cfg.custom_similarity = 1
             cfg.sim_ascii, cfg.n_sim_pairs, cfg.sim_pair_ab, cfg.sim_pair_val = tab, len(extra), ab, vals
             self._keep += [tab, ab, vals]
-        if b._mappings:
-            raise NotImplementedError("mappings are outside the restated hot path")
+        if b._mappings:  # builder.rs:392-402: both sides grapheme-split and folded like patterns
+            side_off, m_goff, m_cps, scores = [0], [0], [], []
+            for a, c, score in b._mappings:
+                for side in (a, c):
+                    for g in graphemes(side):
+                        m_cps += [ord(ch) for ch in fold(g, self.ci)]
+                        m_goff.append(len(m_cps))
+                    side_off.append(len(m_goff) - 1)
+                scores.append(score)
+            arrs = [(ctypes.c_uint32 * len(side_off))(*side_off), (ctypes.c_uint32 * len(m_goff))(*m_goff),
+                    (ctypes.c_uint32 * max(1, len(m_cps)))(*m_cps), (ctypes.c_float * len(scores))(*scores)]
+            cfg.n_map = len(b._mappings)
+            cfg.map_side_off, cfg.map_g_off, cfg.map_cps, cfg.map_score = arrs
+            self._keep += arrs
         n = len(self.patterns_)
         glen, weight, flag, lim, pg_off, g_off, cps = [], [], [], [], [0], [0], []
         for p in self.patterns_:

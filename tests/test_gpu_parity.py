@@ -399,3 +399,42 @@ def test_stream_windows_match_oracle_emulation(window):
         orc = OracleEngine(b, pats)
         want = stream_rows(orc, hay.encode(), thr, eng.max_match_graphemes() + 1, window=window)
         assert got == want, (window, pats, hay[:80])
+
+
+MAP_RULES = [("æ", "ae"), ("ks", "x"), ("ß", "ss"), ("œ", "oe"), ("ph", "f"), ("c", "k"), ("é", "é"),
+             ("ω", "o"), ("ll", "l"), ("AE", "Æ")]
+MAP_VOCAB_ASCII = ["encyclopaedia", "alexandr", "strasse", "phone", "cell", "oeuvre", "kafe", "ab"]
+MAP_FILLER_ASCII = ["a", "e", "x", "ks", "s", "ph", "f", " ", "k", "c", "l", "oe", "A", "E"]
+MAP_VOCAB_UNI = ["encyclopædia", "straße", "cœur", "café", "Ωμέγα", "alexandr", "phone"]
+MAP_FILLER_UNI = ["æ", "ae", "ß", "ss", "œ", "é", "é", "ω", "o", " ", "x", "ks", "Æ", "\r\n"]
+
+
+@pytest.mark.parametrize("seed,vocab,filler", [
+    (0x5EED_0001, MAP_VOCAB_ASCII, MAP_FILLER_ASCII),
+    (0x5EED_0002, MAP_VOCAB_UNI, MAP_FILLER_UNI),
+    (0x5EED_0003, MAP_VOCAB_UNI + MAP_VOCAB_ASCII, MAP_FILLER_UNI + MAP_FILLER_ASCII),
+])
+def test_mappings_differential(seed, vocab, filler):
+    """Multi-character mappings (builder.rs:383-442, search.rs:776-780, 883-922, 945-961): random
+    rule sets (scores 1.0 / 0.8 / 0.5), ASCII and Unicode text, every option the hot path has; the
+    pre-filter must fall back to the full search (prefilter.rs:162-165)."""
+    rng = Rng(seed)
+    total = 0
+    for i in range(120):
+        b, pats, hay, thr = random_case(rng, vocab, filler)
+        for _ in range(1 + rng.next() % 3):
+            a, c = MAP_RULES[rng.next() % len(MAP_RULES)]
+            score = [1.0, 0.8, 0.5][rng.next() % 3]
+            b = b.mapping(a, c) if score == 1.0 else b.mapping_scored(a, c, score)
+        total += compare(b, pats, hay, thr, prefilter=(i % 5 == 0))
+    assert total > 0
+
+
+def test_mappings_widen_stream_overlap():
+    """max_match_graphemes (stream.rs:213-253): longest pattern + max edits x longest mapping side."""
+    e = B().fuzzy(L().edits(2)).mapping("x", "kss").build(["alexandr", "ab"])
+    assert e.max_match_graphemes() == 8 + 2 * 3
+    # a rule that applies nowhere leaves the engine without mappings (self.mappings is empty)
+    e2 = B().fuzzy(L().edits(2)).mapping("q", "zzzz").build(["alexandr"])
+    assert e2.max_match_graphemes() == 8 + 2
+    assert e2.with_prefilter().is_active()

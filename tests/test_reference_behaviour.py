@@ -2,8 +2,7 @@
 
 Each test runs twice: on the CPU oracle (`oracle`, checks the restatement against the reference's
 own assertions) and on the GPU engine (`gpu`, marked `gpu`). Test names and line numbers follow
-/root/reference/src/tests.rs. Streaming (stream.rs) and multi-character mappings are outside the
-accelerated path; mappings are checked to be refused (never silently diverging).
+/root/reference/src/tests.rs (streaming equivalence lives in test_gpu_parity.py).
 """
 import pytest
 
@@ -372,11 +371,47 @@ def test_prefilter_falls_back_when_not_reducible(make_engine):  # prefilter.rs:5
     assert e.with_prefilter().is_active()
 
 
-@pytest.mark.gpu
-def test_mappings_are_refused_not_diverged():  # builder.rs:108-132 are outside the GPU path
-    from fuzzy_aho_corasick import UnsupportedConfiguration
-    with pytest.raises(UnsupportedConfiguration):
-        B().fuzzy(L().edits(1)).mapping("ks", "x").build(["alexandr"])
+def _mapped(make_engine, edits, rules, patterns):
+    b = B().case_insensitive(True).fuzzy(L().edits(edits))
+    for r in rules:
+        b = b.mapping_scored(*r) if len(r) == 3 else b.mapping(*r)
+    return make_engine(b, patterns)
+
+
+def test_multi_char_mapping_bidirectional(make_engine):  # tests.rs:919-960
+    ae = _mapped(make_engine, 1, [("æ", "ae")], ["encyclopaedia"])
+    m = ae.search("encyclopædia", O().threshold(0.95).sorted())
+    assert len(m) == 1, "æ in the haystack should match the 'ae' pattern"
+    assert m[0].substitutions == 1
+    assert m[0].similarity > 0.999, "score-1.0 mapping should be penalty-free"
+    ea = _mapped(make_engine, 1, [("æ", "ae")], ["encyclopædia"])
+    assert len(ea.search("encyclopaedia", O().threshold(0.95).sorted())) == 1
+
+
+def test_multi_char_mapping_many_to_one(make_engine):  # tests.rs:962-986
+    mk = lambda pats: _mapped(make_engine, 1, [("ks", "x")], pats)  # noqa: E731
+    assert len(mk(["alexandr"]).search("aleksandr", O().threshold(0.95).sorted())) == 1
+    assert len(mk(["aleksandr"]).search("alexandr", O().threshold(0.95).sorted())) == 1
+
+
+def test_multi_char_mapping_counts_as_edit(make_engine):  # tests.rs:988-1012
+    build = lambda edits: _mapped(make_engine, edits, [("ß", "ss")], ["strasse"])  # noqa: E731
+    assert len(build(0).search("straße", O().threshold(0.9).sorted())) == 0
+    assert len(build(1).search("straße", O().threshold(0.9).sorted())) == 1
+
+
+def test_multi_char_mapping_scored_penalty(make_engine):  # tests.rs:1014-1039
+    exact = _mapped(make_engine, 1, [("ks", "x")], ["alexandr"])
+    scored = _mapped(make_engine, 1, [("ks", "x", 0.8)], ["alexandr"])
+    se = exact.search("aleksandr", O().threshold(0.5).sorted())[0].similarity
+    ss = scored.search("aleksandr", O().threshold(0.5).sorted())[0].similarity
+    assert se > 0.999
+    assert ss < se
+
+
+def test_no_mapping_is_unaffected(make_engine):  # tests.rs:1041-1056
+    e = make_engine(B().case_insensitive(True).fuzzy(L().edits(1)), ["encyclopaedia"])
+    assert len(e.search("encyclopædia", O().threshold(0.9).sorted())) == 0
 
 
 def _spans_patterns(ms):
