@@ -148,6 +148,16 @@ struct SegDesc {
   uint32_t pad;
 };
 
+// one prefix-cache level: open-addressing table of key hashes -> entry -> snapshot
+struct RcTable {
+  uint32_t k;                        // key chars
+  uint32_t mask;                     // slots - 1
+  const unsigned long long* keys;    // 0 = empty slot
+  const uint32_t* val;               // entry of each slot (EMPTY: not cached)
+  const uint32_t* off;               // snapshot offset of each entry (pool words)
+  const uint32_t* count;             // queued states of each entry (EMPTY: not cached)
+};
+
 struct SearchParams {
   // automaton
   const DevNode* nodes;
@@ -207,17 +217,19 @@ struct SearchParams {
   // prefix cache (launch_pass): a state at j reads text[j] and text[j + 1], so the
   // pops before the first state with j >= rc_k - 1 depend only on the window's first rc_k chars;
   // windows sharing them resume from one snapshot (queue, dedup entries, best list, counters)
-  int32_t rc_mode;                  // 0 off, 1 use the cache, 2 build it (win_list = rc_rep)
-  uint32_t rc_k;                    // key chars (2 or 3)
-  const unsigned long long* rc_keys;  // open-addressing table of keys (0 = empty)
-  const uint32_t* rc_val;           // entry of each key slot (EMPTY: not cached)
-  uint32_t rc_mask;                 // table slots - 1
+  // Two levels: short keys for every window, long keys for the frequent prefixes only; a lookup
+  // takes the deepest hit (rc_tab[0] first). A level-2 build resumes its representatives from
+  // level-1 snapshots.
+  int32_t rc_mode;                  // 0 off, 1 use the cache, 2 build it (win_list = representatives)
+  uint32_t rc_k;                    // key chars of the level being collected / built (2..8)
+  uint32_t rc_ntab;                 // tables a lookup consults (0..2)
+  RcTable rc_tab[2];
   uint32_t rc_vmax, rc_emax;        // dedup / best-list entries a snapshot may hold
-  uint4* rc_pool;                   // snapshots: header x2, queue, dedup entries, best list
+  uint4* rc_pool;                   // snapshots: header x4, queue, dedup entries, best list
   unsigned long long rc_pool_cap;   // pool words (uint4)
   unsigned long long* rc_pool_used; // bump allocator
-  uint32_t* rc_off;                 // snapshot offset of each entry (pool words)
-  uint32_t* rc_count;               // queued states of each entry (EMPTY: not cached)
+  uint32_t* rc_off;                 // build: snapshot offset of each entry (pool words)
+  uint32_t* rc_count;               // build: queued states of each entry (EMPTY: not cached)
   // multi-character mappings (search.rs:776-780, 883-922, 945-961; builder.rs:383-442). With
   // has_map, exact and swap transitions compare whole folded graphemes (ids, 0 = not in the
   // engine's grapheme dictionary): edge_gid per edge, text gids per grapheme (gid32 for Unicode
@@ -317,7 +329,7 @@ struct Engine {
   // per-engine device scratch of the search launcher, reused across calls by whichever call holds
   // scratch_mu (a concurrent call on the same engine allocates its own)
   mutable std::mutex scratch_mu;
-  static constexpr int kScratch = 16;
+  static constexpr int kScratch = 24;
   mutable void* scratch_p[kScratch] = {};
   mutable size_t scratch_n[kScratch] = {};
 };

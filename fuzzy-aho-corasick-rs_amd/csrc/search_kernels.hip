@@ -1051,6 +1051,7 @@ __device__ __forceinline__ void sink64(uint64_t v) {
 }
 #endif
 
+constexpr uint32_t RC_HDR = 4;  // snapshot header words: {head, tail, nv, pops}, {ne}, chars 0-3, chars 4-7
 struct RcHit {  // prefix-cache snapshot of a window (rc_lookup): pool offset and header
   uint32_t off, head, tail, nv_nel, pops;
 };
@@ -1085,7 +1086,7 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
   EL.n = 0;
   uint32_t head = 0, tail = 1;
   if (rc.off != EMPTY) {  // prefix cache hit: resume from the snapshot of the key's representative
-    const uint4* src = P.rc_pool + rc.off + 3;  // queue, dedup entries, best list (header in rc)
+    const uint4* src = P.rc_pool + rc.off + RC_HDR;  // queue, dedup entries, best list (header in rc)
     head = rc.head;
     tail = rc.tail;
     const uint32_t nq = tail - head, nv = rc.nv_nel & 0xFFFFu, ne = rc.nv_nel >> 16, nw = nq + nv + ne;
@@ -1422,52 +1423,69 @@ __device__ __forceinline__ uint32_t find_seg(const SearchParams& P, uint64_t v) 
   return lo;
 }
 
-// Prefix-cache key of a window: its first rc_k chars (0x1FFFFF past the end of the text) and a
-// 64-bit hash of them (top bit set: 0 marks an empty table slot). A snapshot stores the chars and a
-// lookup compares them, so hash collisions only cost a cache miss. False: not cacheable (a char
-// inside the text but beyond the resident halo).
-__device__ __forceinline__ bool rc_key(const SearchParams& P, const SegDesc& S, uint64_t s, uint4& ch, uint64_t& key) {
+// Prefix-cache key of a window: its first k (<= 8) chars (0x1FFFFF past the end of the text and
+// in unused positions) and a 64-bit hash of them (top bit set: 0 marks an empty table slot). A
+// snapshot stores the chars and a lookup compares them, so hash collisions only cost a cache miss.
+// False: not cacheable (a char inside the text but beyond the resident halo).
+struct RcChars {
+  uint4 a, b;
+};
+__device__ __forceinline__ bool rc_key(const SearchParams& P, const SegDesc& S, uint64_t s, uint32_t k, RcChars& ch,
+                                       uint64_t& key) {
   unsigned e2 = 0;
-  uint32_t c[4] = {0x1FFFFFu, 0x1FFFFFu, 0x1FFFFFu, 0x1FFFFFu};
+  uint32_t c[8];
 #pragma unroll
-  for (uint32_t i = 0; i < 4; ++i)
-    if (i < P.rc_k && s + i < S.n) {
+  for (uint32_t i = 0; i < 8; ++i) {
+    c[i] = 0x1FFFFFu;
+    if (i < k && s + i < S.n) {
       if (s + i >= S.avail) return false;
       c[i] = text_char(P, S, s + i, e2);
     }
-  ch = make_uint4(c[0], c[1], c[2], c[3]);
-  const uint64_t a = ((uint64_t)c[1] << 21) | c[0], b = ((uint64_t)c[3] << 21) | c[2];
-  uint64_t h = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull) * 0xD6E8FEB86659FD93ull;
-  h ^= h >> 32;
+  }
+  ch.a = make_uint4(c[0], c[1], c[2], c[3]);
+  ch.b = make_uint4(c[4], c[5], c[6], c[7]);
+  uint64_t h = 0x632BE59BD9B4E019ull ^ k;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; i += 2) {
+    const uint64_t w = ((uint64_t)c[i + 1] << 21) | c[i];
+    h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+  }
   h *= 0xD6E8FEB86659FD93ull;
-  h ^= h >> 29;
+  h ^= h >> 32;
   key = h | (1ull << 63);
   return true;
 }
 __device__ __forceinline__ uint32_t rc_hash(uint64_t k) { return (uint32_t)k ^ (uint32_t)(k >> 32); }
 constexpr uint32_t RC_PROBES = 32;
 
-// A window's prefix-cache hit (snapshot header, read with the lookup): off = EMPTY on a miss
+// A window's prefix-cache hit (snapshot header, read with the lookup): off = EMPTY on a miss.
+// Tables are consulted deepest first; the first verified hit wins.
 template <uint32_t QCAP>
 __device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s) {
   RcHit r{EMPTY, 0u, 0u, 0u, 0u};
-  uint4 ch;
-  uint64_t k;
-  if (!rc_key(P, S, s, ch, k)) return r;
-  const uint32_t h = rc_hash(k);
-  for (uint32_t p = 0; p < RC_PROBES; ++p) {
-    const uint32_t slot = (h + p) & P.rc_mask;
-    const unsigned long long kk = P.rc_keys[slot];
-    if (kk == k) {
-      const uint32_t ent = P.rc_val[slot];
-      if (ent == EMPTY) return r;
-      const uint32_t cnt = P.rc_count[ent], off = P.rc_off[ent];
-      if (cnt == EMPTY || cnt + 1u > QCAP) return r;
-      const uint4 h0 = P.rc_pool[off], h1 = P.rc_pool[off + 1], sc = P.rc_pool[off + 2];  // [2]: its chars
-      if (sc.x == ch.x && sc.y == ch.y && sc.z == ch.z && sc.w == ch.w) r = RcHit{off, h0.x, h0.y, h0.z | (h1.x << 16), h0.w};
-      return r;
+  for (uint32_t t = 0; t < P.rc_ntab; ++t) {
+    const RcTable& T = P.rc_tab[t];
+    RcChars ch;
+    uint64_t k;
+    if (!rc_key(P, S, s, T.k, ch, k)) continue;
+    const uint32_t h = rc_hash(k);
+    for (uint32_t p = 0; p < RC_PROBES; ++p) {
+      const uint32_t slot = (h + p) & T.mask;
+      const unsigned long long kk = T.keys[slot];
+      if (kk == k) {
+        const uint32_t ent = T.val[slot];
+        if (ent == EMPTY) break;
+        const uint32_t cnt = T.count[ent], off = T.off[ent];
+        if (cnt == EMPTY || cnt + 1u > QCAP) break;
+        const uint4 h0 = P.rc_pool[off], h1 = P.rc_pool[off + 1], sa = P.rc_pool[off + 2], sb = P.rc_pool[off + 3];
+        if (sa.x == ch.a.x && sa.y == ch.a.y && sa.z == ch.a.z && sa.w == ch.a.w && sb.x == ch.b.x &&
+            sb.y == ch.b.y && sb.z == ch.b.z && sb.w == ch.b.w)
+          return RcHit{off, h0.x, h0.y, h0.z | (h1.x << 16), h0.w};
+        break;
+      }
+      if (kk == 0ull) break;
     }
-    if (kk == 0ull) return r;
   }
   return r;
 }
@@ -1475,7 +1493,8 @@ __device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc&
 // Prefix-cache keys: every searched window's key is inserted once (plain probe first, CAS only on
 // an empty slot); the inserting window becomes the entry's representative (rc_rep).
 __global__ __launch_bounds__(256) void rc_collect_kernel(SearchParams P, unsigned long long* keys, uint32_t* val,
-                                                         uint64_t* rep, unsigned int* n_ent, uint32_t max_ent) {
+                                                         uint64_t* rep, unsigned int* n_ent, uint32_t max_ent,
+                                                         uint32_t mask) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   unsigned err = 0;
   for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < P.total_windows; v += stride) {
@@ -1484,12 +1503,12 @@ __global__ __launch_bounds__(256) void rc_collect_kernel(SearchParams P, unsigne
     const SegDesc S = P.segs[kl];
     const uint64_t start = S.w_begin + (vid - P.seg_prefix[kl]);
     if (window_skipped(P, S, start, err)) continue;
-    uint4 ch;
+    RcChars ch;
     uint64_t k;
-    if (!rc_key(P, S, start, ch, k)) continue;
+    if (!rc_key(P, S, start, P.rc_k, ch, k)) continue;
     const uint32_t h = rc_hash(k);
     for (uint32_t p = 0; p < RC_PROBES; ++p) {
-      const uint32_t slot = (h + p) & P.rc_mask;
+      const uint32_t slot = (h + p) & mask;
       unsigned long long kk = keys[slot];
       if (kk == 0ull) {
         kk = atomicCAS(&keys[slot], 0ull, (unsigned long long)k);
@@ -1502,6 +1521,61 @@ __global__ __launch_bounds__(256) void rc_collect_kernel(SearchParams P, unsigne
       }
       if (kk == k) break;
     }
+  }
+}
+
+// Level-2 keys (long prefixes): a sample of the windows (every `stride`-th) is counted per key;
+// the first inserter of a key is its representative.
+__global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, unsigned long long* keys, uint32_t* cnt,
+                                                       uint64_t* rep, uint32_t mask, uint32_t stride) {
+  const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+  unsigned err = 0;
+  const uint64_t ns = (P.total_windows + stride - 1) / stride;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gstride) {
+    const uint64_t vid = i * stride;
+    const uint32_t kl = find_seg(P, vid);
+    const SegDesc S = P.segs[kl];
+    const uint64_t start = S.w_begin + (vid - P.seg_prefix[kl]);
+    if (window_skipped(P, S, start, err)) continue;
+    RcChars ch;
+    uint64_t k;
+    if (!rc_key(P, S, start, P.rc_k, ch, k)) continue;
+    const uint32_t h = rc_hash(k);
+    for (uint32_t p = 0; p < RC_PROBES; ++p) {
+      const uint32_t slot = (h + p) & mask;
+      unsigned long long kk = keys[slot];
+      if (kk == 0ull) {
+        kk = atomicCAS(&keys[slot], 0ull, (unsigned long long)k);
+        if (kk == 0ull) {
+          rep[slot] = vid;
+          atomicAdd(&cnt[slot], 1u);
+          break;
+        }
+      }
+      if (kk == k) {
+        atomicAdd(&cnt[slot], 1u);
+        break;
+      }
+    }
+  }
+}
+
+// Level-2 entries: the keys counted at least `thr` times, numbered in slot order of arrival;
+// every other slot maps to EMPTY (not cached: the lookup falls through to level 1).
+__global__ __launch_bounds__(256) void rc_select_kernel(const unsigned long long* keys, const uint32_t* cnt,
+                                                        const uint64_t* rep_slot, uint32_t* val, uint64_t* rep,
+                                                        unsigned int* n_ent, uint32_t n_slots, uint32_t thr,
+                                                        uint32_t max_ent) {
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += gridDim.x * blockDim.x) {
+    uint32_t v = EMPTY;
+    if (keys[s] != 0ull && cnt[s] >= thr) {
+      const uint32_t ent = atomicAdd(n_ent, 1u);
+      if (ent < max_ent) {
+        rep[ent] = rep_slot[s];
+        v = ent;
+      }
+    }
+    val[s] = v;
   }
 }
 
@@ -1535,7 +1609,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         active = !window_skipped(P, S, start, err);
       }
       RcHit hit{EMPTY, 0u, 0u, 0u, 0u};  // prefix-cache snapshot of this lane's window
-      if (P.rc_mode == 1 && active) hit = rc_lookup<QCAP>(P, P.segs[kl], start);
+      if (P.rc_mode != 0 && P.rc_ntab && active) hit = rc_lookup<QCAP>(P, P.segs[kl], start);
       uint64_t m = __ballot(active);
       while (m) {
         const int l = first_lane(m);
@@ -1562,15 +1636,15 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           if constexpr (VCAP > 0)
             for (uint32_t b = 0; b < VCAP; b += 64) nv += (uint32_t)__popcll(__ballot(live(s_vis[b + lane])));
           bool bad = (wave_or(err) & (ERR_QUEUE | ERR_VISITED | ERR_EMIT)) != 0 || EL.n > P.rc_emax || nv > P.rc_vmax;
-          const uint32_t words = 3 + nq + nv + EL.n;
+          const uint32_t words = RC_HDR + nq + nv + EL.n;
           unsigned long long off = 0;
           if (lane == 0 && !bad) off = atomicAdd(P.rc_pool_used, (unsigned long long)words);
           off = shfl_u64(off, 0);
           bad = bad || off + words > P.rc_pool_cap || off > 0xFFFFFFF0ull;
-          uint4 kch;
+          RcChars kch;
           uint64_t kkey;
-          bad = bad || !rc_key(P, S, st, kch, kkey);
-          uint4* dst = P.rc_pool + off + 3;  // after the three header words
+          bad = bad || !rc_key(P, S, st, P.rc_k, kch, kkey);
+          uint4* dst = P.rc_pool + off + RC_HDR;  // after the header words
           for (uint32_t i = lane; i < nq && !bad; i += 64) {
             const KState k = s_q[(qhead + i) & (QCAP - 1)];
             dst[i] = make_uint4(k.node, k.jm, __float_as_uint(k.pen), k.packed);
@@ -1588,9 +1662,11 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           for (uint32_t i = lane; i < EL.n && !bad; i += 64) dst[nq + nv + i] = EL.buf[i];
           if (lane == 0) {
             if (!bad) {
-              P.rc_pool[off] = make_uint4(qhead, qlen, nv, (uint32_t)(popped - popped0));
+              // pops: those of the parent snapshot this build resumed from, plus its own
+              P.rc_pool[off] = make_uint4(qhead, qlen, nv, (uint32_t)(popped - popped0) + rc.pops);
               P.rc_pool[off + 1] = make_uint4(EL.n, 0u, 0u, 0u);
-              P.rc_pool[off + 2] = kch;
+              P.rc_pool[off + 2] = kch.a;
+              P.rc_pool[off + 3] = kch.b;
             }
             P.rc_off[ent] = bad ? EMPTY : (uint32_t)off;
             P.rc_count[ent] = bad ? EMPTY : nq;
@@ -1626,8 +1702,12 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
 
 // one wavefront per workgroup; the dedup-free variants are held to <= 128 VGPRs (4 waves/SIMD),
 // the dedup variants are bounded by LDS first
+#ifndef FAC_BEAM_WAVES  // waves/SIMD the dedup variants are compiled for (VGPR budget); 0 = unbounded
+#define FAC_BEAM_WAVES 0
+#endif
 template <uint32_t VCAP, uint32_t QCAP, bool MAP>
-__global__ __launch_bounds__(64) void bfs_window_kernel(SearchParams P) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((FAC_BEAM_WAVES && VCAP <= 512) ? FAC_BEAM_WAVES : 1)))
+void bfs_window_kernel(SearchParams P) {
   bfs_window_body<VCAP, QCAP, MAP>(P);
 }
 template <uint32_t QCAP, bool MAP>
@@ -2177,12 +2257,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   };
 
   DevBuf d_segs, d_prefix, d_out, d_ebuf, d_cnt, d_list, d_spill;
-  DevBuf d_rck, d_rcv, d_rcrep, d_rcs, d_rcc, d_rcn;  // root-pop cache
+  DevBuf d_rck, d_rcv, d_rcrep, d_rcs, d_rcc, d_rcn;  // prefix cache, level 1 + pool
+  DevBuf d_rck2, d_rcv2, d_rcslot2, d_rcrep2, d_rcc2;  // prefix cache, level 2
   std::unique_lock<std::mutex> lease(e.scratch_mu, std::try_to_lock);
   if (lease.owns_lock()) {  // reuse the engine's scratch (no per-call hipMalloc of the 64 MB lists)
-    DevBuf* bufs[13] = {&d_segs, &d_prefix, &d_out, &d_ebuf, &d_cnt, &d_list, &d_spill,
-                        &d_rck,  &d_rcv,    &d_rcrep, &d_rcs, &d_rcc, &d_rcn};
-    for (int i = 0; i < 13; ++i) bufs[i]->bind(&e.scratch_p[i], &e.scratch_n[i]);
+    DevBuf* bufs[18] = {&d_segs, &d_prefix, &d_out,   &d_ebuf, &d_cnt,     &d_list,   &d_spill, &d_rck,  &d_rcv,
+                        &d_rcrep, &d_rcs,   &d_rcc,   &d_rcn,  &d_rck2,    &d_rcv2,   &d_rcslot2, &d_rcrep2, &d_rcc2};
+    static_assert(Engine::kScratch >= 18, "engine scratch slots");
+    for (int i = 0; i < 18; ++i) bufs[i]->bind(&e.scratch_p[i], &e.scratch_n[i]);
   }
   HIP_TRY(d_segs.alloc(segs.size() * sizeof(SegDesc), stream));
   HIP_TRY(d_prefix.alloc(prefix.size() * sizeof(uint64_t), stream));
@@ -2215,23 +2297,30 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   float ms_total = 0.f, cache_ms = 0.f;
   out.clear();
 
-  // Prefix cache (rc_collect_kernel, then rc_build_kernel over one representative window per key),
-  // keys of 4 chars, else 3, else 2, whichever first gives every snapshot at least 8
-  // windows on average (a build costs about one window search); skipped when the root emits (an
-  // empty pattern) or the search is small.
+  // Prefix cache. Level 1: every window's key of K0 chars (4, else 3, else 2,
+  // whichever first gives every snapshot at least 8 windows on average); rc_collect_kernel numbers
+  // the keys, rc_build_kernel searches one representative per key up to the first state that reads
+  // past the key. Level 2: keys of K1 (> K0) chars, counted on a sample of the windows; keys seen at
+  // least T times get a snapshot built by resuming their representative from its level-1 snapshot.
+  // A window resumes from the deepest snapshot its prefix has. Skipped when the root emits (an empty
+  // pattern), with mappings (whole-grapheme keys), or when the search is small.
   P.rc_mode = 0;
+  P.rc_ntab = 0;
   const bool root_out = !e.nodes.empty() && e.nodes[0].out_end > e.nodes[0].out_begin;
   const char* rc_min = std::getenv("FAC_RC_MIN");  // env knobs: tests force it on / pin K, A/B turns it off
   const char* kenv = std::getenv("FAC_RC_K");
   if (!root_out && !e.has_map && fan_root + 1 <= 4096 && kVariants[vi].qcap <= 4096 &&
       windows >= (rc_min ? std::strtoull(rc_min, nullptr, 10) : 4096ull) && !std::getenv("FAC_NO_RC")) {
+    auto env_u = [](const char* name, uint64_t dflt) {
+      const char* v = std::getenv(name);
+      return v ? std::strtoull(v, nullptr, 10) : dflt;
+    };
     const uint32_t kpin = kenv ? (uint32_t)std::min<unsigned long>(4, std::max<unsigned long>(2, std::strtoul(kenv, nullptr, 10))) : 0u;
     const uint32_t qmain = kVariants[vi].qcap, vmain = kVariants[vi].vcap;
     const uint32_t qbuild = std::max<uint32_t>((uint32_t)fan_root + 1, qmain);
     P.rc_vmax = vmain ? std::min<uint32_t>(256, vmain / 2) : 256;
-    P.rc_emax = 16;
-    const char* eenv = std::getenv("FAC_RC_ENTRIES");
-    const uint64_t ent_cap = eenv ? std::max<uint64_t>(1, std::strtoull(eenv, nullptr, 10)) : (4ull << 20);
+    P.rc_emax = 64;
+    const uint64_t ent_cap = std::max<uint64_t>(1, env_u("FAC_RC_ENTRIES", 4ull << 20));
     const uint32_t max_ent = (uint32_t)std::min<uint64_t>(windows, ent_cap);
     uint32_t slots = 1u << 12;
     while (slots < 4ull * max_ent && slots < (1u << 24)) slots <<= 1;
@@ -2239,64 +2328,145 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     HIP_TRY(d_rcv.alloc(slots * sizeof(uint32_t), stream));
     HIP_TRY(d_rcrep.alloc(max_ent * sizeof(uint64_t), stream));
     HIP_TRY(d_rcc.alloc(2 * (size_t)max_ent * sizeof(uint32_t), stream));  // counts, then offsets
-    HIP_TRY(d_rcn.alloc(2 * sizeof(unsigned long long), stream));            // keys, pool words used
-    P.rc_keys = static_cast<const unsigned long long*>(d_rck.p);
-    P.rc_val = static_cast<const uint32_t*>(d_rcv.p);
-    P.rc_mask = slots - 1;
-    P.rc_count = static_cast<uint32_t*>(d_rcc.p);
-    P.rc_off = static_cast<uint32_t*>(d_rcc.p) + max_ent;
+    HIP_TRY(d_rcn.alloc(4 * sizeof(unsigned long long), stream));  // keys, pool words used, level-2 entries
+    RcTable L1{0u, slots - 1, static_cast<const unsigned long long*>(d_rck.p), static_cast<const uint32_t*>(d_rcv.p),
+               static_cast<uint32_t*>(d_rcc.p) + max_ent, static_cast<uint32_t*>(d_rcc.p)};
     P.rc_pool_used = static_cast<unsigned long long*>(d_rcn.p) + 1;
     HIP_TRY(hipEventRecord(ev.a, stream));
+    HIP_TRY(hipMemsetAsync(d_rcn.p, 0, 4 * sizeof(unsigned long long), stream));
     const uint32_t cgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256, (uint64_t)cus * 8));
+    uint32_t n_ent1 = 0;
     for (uint32_t k = kpin ? kpin : 4u; k >= (kpin ? kpin : 2u); --k) {
       P.rc_k = k;
       HIP_TRY(hipMemsetAsync(d_rck.p, 0, slots * sizeof(unsigned long long), stream));
       HIP_TRY(hipMemsetAsync(d_rcv.p, 0xFF, slots * sizeof(uint32_t), stream));
-      HIP_TRY(hipMemsetAsync(d_rcn.p, 0, 2 * sizeof(unsigned long long), stream));
+      HIP_TRY(hipMemsetAsync(d_rcn.p, 0, sizeof(unsigned long long), stream));
       hipLaunchKernelGGL(rc_collect_kernel, dim3(cgrid), dim3(256), 0, stream, P,
                          static_cast<unsigned long long*>(d_rck.p), static_cast<uint32_t*>(d_rcv.p),
-                         static_cast<uint64_t*>(d_rcrep.p), static_cast<unsigned int*>(d_rcn.p), max_ent);
+                         static_cast<uint64_t*>(d_rcrep.p), static_cast<unsigned int*>(d_rcn.p), max_ent, slots - 1);
       HIP_TRY(hipGetLastError());
       unsigned int n_keys = 0;
       HIP_TRY(hipMemcpyAsync(&n_keys, d_rcn.p, sizeof(n_keys), hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
       if (n_keys == 0) break;
       if (!kpin && 8ull * n_keys > windows) continue;  // too little reuse: fewer chars per key
-      const uint32_t n_ent = std::min(n_keys, max_ent);
-      // snapshot pool: the worst entry for every key, up to a budget; a build that runs out of
-      // pool leaves the remaining keys uncached
-      const uint64_t worst = 3 + std::min(qmain, qbuild) + P.rc_vmax + P.rc_emax;
-      const char* penv = std::getenv("FAC_RC_POOL_MB");
-      const uint64_t budget = (penv ? std::strtoull(penv, nullptr, 10) : 8192ull) << 20;
-      const uint64_t pool_words = std::max<uint64_t>(1024, std::min<uint64_t>(n_ent * worst, budget / sizeof(uint4)));
+      n_ent1 = std::min(n_keys, max_ent);
+      L1.k = k;
+      break;
+    }
+    // level 2: frequent long prefixes (FAC_RC_K2 = 0 turns it off)
+    const uint32_t k2 = (uint32_t)std::min<uint64_t>(8, env_u("FAC_RC_K2", 6));
+    const uint32_t stride2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_STRIDE2", 8));
+    const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", 2));
+    uint32_t n_ent2 = 0;
+    RcTable L2{};
+    if (n_ent1 && k2 > L1.k && windows >= env_u("FAC_RC_MIN2", 1ull << 20)) {
+      const uint64_t samples = (windows + stride2 - 1) / stride2;
+      uint32_t slots2 = 1u << 12;
+      while (slots2 < 2ull * samples && slots2 < (1u << 27)) slots2 <<= 1;
+      const uint32_t max_ent2 = (uint32_t)std::min<uint64_t>(samples, ent_cap);
+      HIP_TRY(d_rck2.alloc(slots2 * sizeof(unsigned long long), stream));
+      HIP_TRY(d_rcv2.alloc(slots2 * sizeof(uint32_t), stream));  // sample counts, then entries
+      HIP_TRY(d_rcslot2.alloc(slots2 * sizeof(uint64_t), stream));
+      HIP_TRY(d_rcrep2.alloc(max_ent2 * sizeof(uint64_t), stream));
+      HIP_TRY(d_rcc2.alloc(2 * (size_t)max_ent2 * sizeof(uint32_t), stream));
+      HIP_TRY(hipMemsetAsync(d_rck2.p, 0, slots2 * sizeof(unsigned long long), stream));
+      HIP_TRY(hipMemsetAsync(d_rcv2.p, 0, slots2 * sizeof(uint32_t), stream));
+      SearchParams C = P;
+      C.rc_k = k2;
+      hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, C,
+                         static_cast<unsigned long long*>(d_rck2.p), static_cast<uint32_t*>(d_rcv2.p),
+                         static_cast<uint64_t*>(d_rcslot2.p), slots2 - 1, stride2);
+      HIP_TRY(hipGetLastError());
+      // counts are read and replaced by entries in place: a slot is only touched by its own thread
+      hipLaunchKernelGGL(rc_select_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>(slots2 / 256, cus * 8))),
+                         dim3(256), 0, stream, static_cast<const unsigned long long*>(d_rck2.p),
+                         static_cast<const uint32_t*>(d_rcv2.p), static_cast<const uint64_t*>(d_rcslot2.p),
+                         static_cast<uint32_t*>(d_rcv2.p), static_cast<uint64_t*>(d_rcrep2.p),
+                         reinterpret_cast<unsigned int*>(static_cast<unsigned long long*>(d_rcn.p) + 2), slots2, thr2,
+                         max_ent2);
+      HIP_TRY(hipGetLastError());
+      unsigned int nk2 = 0;
+      HIP_TRY(hipMemcpyAsync(&nk2, static_cast<unsigned long long*>(d_rcn.p) + 2, sizeof(nk2), hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      n_ent2 = std::min(nk2, max_ent2);
+      L2 = RcTable{k2, slots2 - 1, static_cast<const unsigned long long*>(d_rck2.p), static_cast<const uint32_t*>(d_rcv2.p),
+                   static_cast<uint32_t*>(d_rcc2.p) + max_ent2, static_cast<uint32_t*>(d_rcc2.p)};
+      if (n_ent2 == 0) L2.k = 0;
+    }
+    if (n_ent1) {
+      // snapshot pool: the worst entry for every key of both levels, up to a budget; a build that
+      // runs out of pool leaves the remaining keys uncached
+      const uint64_t worst = RC_HDR + std::min(qmain, qbuild) + P.rc_vmax + P.rc_emax;
+      const uint64_t budget = env_u("FAC_RC_POOL_MB", 16384ull) << 20;
+      const uint64_t pool_words =
+          std::max<uint64_t>(1024, std::min<uint64_t>((uint64_t)(n_ent1 + n_ent2) * worst, budget / sizeof(uint4)));
       HIP_TRY(d_rcs.alloc(pool_words * sizeof(uint4), stream));
       P.rc_pool = static_cast<uint4*>(d_rcs.p);
       P.rc_pool_cap = pool_words;
-      SearchParams Q = P;
-      Q.rc_mode = 2;
-      Q.win_list = static_cast<const uint64_t*>(d_rcrep.p);
-      Q.total_windows = n_ent;
-      Q.chunk = 1;
-      Q.win_counts = nullptr;
-      Q.ebuf = static_cast<uint4*>(d_ebuf.p);
-      Q.out = static_cast<fac_match*>(d_out.p);
-      Q.out_cap = out_cap;
-      Q.spill = static_cast<uint64_t*>(d_spill.p);
-      Q.spill_cap = spill_cap;
-      Q.counters = static_cast<unsigned long long*>(d_cnt.p);
-      HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 5 * sizeof(unsigned long long), stream));
-      launch_rc_build(qbuild, std::min<uint32_t>(n_ent, max_grid), stream, Q);
-      const hipError_t le = hipGetLastError();
-      if (le != hipSuccess) {
-        err = std::string("kernel launch: ") + hipGetErrorString(le);
-        return FAC_E_HIP;
+      auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, const RcTable* parent) -> int {
+        SearchParams Q = P;
+        Q.rc_mode = 2;
+        Q.rc_k = T.k;
+        Q.rc_ntab = parent ? 1u : 0u;
+        if (parent) Q.rc_tab[0] = *parent;
+        Q.rc_off = const_cast<uint32_t*>(T.off);
+        Q.rc_count = const_cast<uint32_t*>(T.count);
+        Q.win_list = reps;
+        Q.total_windows = n_ent;
+        Q.chunk = 1;
+        Q.win_counts = nullptr;
+        Q.ebuf = static_cast<uint4*>(d_ebuf.p);
+        Q.out = static_cast<fac_match*>(d_out.p);
+        Q.out_cap = out_cap;
+        Q.spill = static_cast<uint64_t*>(d_spill.p);
+        Q.spill_cap = spill_cap;
+        Q.counters = static_cast<unsigned long long*>(d_cnt.p);
+        HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 5 * sizeof(unsigned long long), stream));
+        launch_rc_build(qbuild, std::min<uint32_t>(n_ent, max_grid), stream, Q);
+        const hipError_t le = hipGetLastError();
+        if (le != hipSuccess) {
+          err = std::string("kernel launch: ") + hipGetErrorString(le);
+          return FAC_E_HIP;
+        }
+        return FAC_OK;
+      };
+      int brc = build(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p), nullptr);
+      if (brc) return brc;
+      if (n_ent2) {
+        brc = build(L2, n_ent2, static_cast<const uint64_t*>(d_rcrep2.p), &L1);
+        if (brc) return brc;
+        P.rc_tab[0] = L2;
+        P.rc_tab[1] = L1;
+        P.rc_ntab = 2;
+      } else {
+        P.rc_tab[0] = L1;
+        P.rc_ntab = 1;
       }
       P.rc_mode = 1;
-      break;
     }
     HIP_TRY(hipEventRecord(ev.b, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     HIP_TRY(hipEventElapsedTime(&cache_ms, ev.a, ev.b));
+    if (P.rc_mode == 1 && std::getenv("FAC_RC_DEBUG")) {  // diagnostics: keys, pool use, cached entries
+      unsigned long long rcn[3] = {0, 0, 0};
+      HIP_TRY(hipMemcpy(rcn, d_rcn.p, sizeof(rcn), hipMemcpyDeviceToHost));
+      auto cached_of = [&](const RcTable& T, uint32_t ne, uint64_t& qsum) -> uint64_t {
+        std::vector<uint32_t> cntv(ne);
+        if (ne && hipMemcpy(cntv.data(), T.count, ne * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+        uint64_t c = 0;
+        for (uint32_t v : cntv)
+          if (v != EMPTY) ++c, qsum += v;
+        return c;
+      };
+      uint64_t q1 = 0, q2 = 0;
+      const uint64_t c1 = cached_of(L1, n_ent1, q1), c2 = n_ent2 ? cached_of(L2, n_ent2, q2) : 0;
+      std::fprintf(stderr,
+                   "FAC_RC windows=%llu L1 k=%u keys=%llu cached=%llu mean_queue=%.1f | L2 k=%u entries=%u cached=%llu "
+                   "mean_queue=%.1f | pool %.1f MB\n",
+                   (unsigned long long)windows, L1.k, rcn[0], (unsigned long long)c1, c1 ? (double)q1 / c1 : 0.0, L2.k,
+                   n_ent2, (unsigned long long)c2, c2 ? (double)q2 / c2 : 0.0, rcn[1] * 16.0 / 1e6);
+    }
   }
   for (;;) {
     P.chunk = P.win_list ? 1u : 256u;  // spilled windows are few and heavy: one per block turn

@@ -79,7 +79,7 @@ def random_case(rng, vocab, filler, allow_beam=True, allow_limits=True):
     return b, pats, hay, thr
 
 
-@pytest.mark.parametrize("root_cache", ["off", "k4"])
+@pytest.mark.parametrize("root_cache", ["off", "k4", "k2+k4", "k3+k8"])
 @pytest.mark.parametrize("per_edge_only", [False, True])
 @pytest.mark.parametrize("seed,vocab,filler", [
     (0x1234_5678_9abc_def1, ASCII_VOCAB, ASCII_FILLER),
@@ -94,9 +94,16 @@ def test_differential_random(seed, vocab, filler, per_edge_only, root_cache, mon
         monkeypatch.setenv("FAC_NO_FAST", "1")
     if root_cache == "off":
         monkeypatch.setenv("FAC_NO_RC", "1")
-    else:
+    else:  # "kA" one level of A-char keys; "kA+kB": level 2 with B-char keys for every sampled key
+        levels = root_cache.split("+")
         monkeypatch.setenv("FAC_RC_MIN", "1")
-        monkeypatch.setenv("FAC_RC_K", "4")
+        monkeypatch.setenv("FAC_RC_K", levels[0][1:])
+        if len(levels) == 2:
+            for k, v in (("FAC_RC_K2", levels[1][1:]), ("FAC_RC_MIN2", "1"), ("FAC_RC_STRIDE2", "1"),
+                         ("FAC_RC_T2", "1")):
+                monkeypatch.setenv(k, v)
+        else:
+            monkeypatch.setenv("FAC_RC_K2", "0")
     rng = Rng(seed)
     total = 0
     for _ in range(150):
@@ -274,6 +281,25 @@ def test_prefix_cache_key_lengths(k, monkeypatch):
     for _ in range(60):
         b, pats, hay, thr = random_case(rng, ASCII_VOCAB + UNI_VOCAB, ASCII_FILLER + UNI_FILLER)
         compare(b, pats, hay, thr)
+
+
+@pytest.mark.parametrize("k2", ["5", "6", "8"])
+def test_prefix_cache_two_levels_c3_slice(k2, monkeypatch):
+    """Level-2 snapshots (long prefixes, built by resuming level-1 snapshots) on a C3-shaped
+    haystack: identical records with the cache on and off."""
+    from fuzzy_aho_corasick import workloads
+    w = workloads.config("c3", 2 << 20, 3)
+    eng = workloads.builder_for(w).build(w.patterns)
+    staged = eng.stage(w.haystack)
+    monkeypatch.setenv("FAC_RC_MIN2", "1")
+    monkeypatch.setenv("FAC_RC_K2", k2)
+    on, st_on = staged.search_windows_records(w.threshold)
+    monkeypatch.setenv("FAC_RC_K2", "0")
+    one, st_one = staged.search_windows_records(w.threshold)
+    monkeypatch.setenv("FAC_NO_RC", "1")
+    off, _ = staged.search_windows_records(w.threshold)
+    assert st_on.states_cached > st_one.states_cached > 0
+    assert len(on) > 0 and sorted(on.tolist()) == sorted(off.tolist()) == sorted(one.tolist())
 
 
 def test_prefix_cache_default_on_c3_slice(monkeypatch):
