@@ -158,6 +158,9 @@ struct RcTable {
   const uint32_t* count;             // queued states of each entry (EMPTY: not cached)
 };
 
+constexpr int N_COUNTERS = 8;  // SearchParams::counters
+constexpr int kRcLevels = 4;   // prefix-cache levels: level 1 + up to 3 sampled levels
+
 struct SearchParams {
   // automaton
   const DevNode* nodes;
@@ -206,7 +209,12 @@ struct SearchParams {
   uint4* ebuf;              // per-wave emission scratch
   fac_match* out;
   uint64_t out_cap;
-  unsigned long long* counters;  // [0] matches, [1] states popped, [2] error flags, [3] spilled windows
+  unsigned long long* counters;  // [0] matches, [1] states popped, [2] error flags, [3] spilled windows,
+                                 // [4] pops replayed from snapshots, [5] windows resumed from a snapshot,
+                                 // [6] of those, finished by the snapshot alone (empty queue),
+                                 // [7] next window chunk (dynamic chunk hand-out)
+  int32_t rc_lane_flush;         // resumed windows with an empty queue are flushed lane-parallel
+  int32_t dyn_chunks;            // 1: chunks from the work counter; 0: static grid-stride
   // window list mode (re-run of spilled windows) and the spill list of capacity overflows
   const uint64_t* win_list;  // null: virtual windows 0..total_windows; else list of virtual ids
   uint64_t* spill;           // virtual ids of windows that overflowed this variant's LDS frontier
@@ -222,12 +230,13 @@ struct SearchParams {
   // level-1 snapshots.
   int32_t rc_mode;                  // 0 off, 1 use the cache, 2 build it (win_list = representatives)
   uint32_t rc_k;                    // key chars of the level being collected / built (2..8)
-  uint32_t rc_ntab;                 // tables a lookup consults (0..2)
-  RcTable rc_tab[2];
+  uint32_t rc_ntab;                 // tables a lookup consults (0..kRcLevels), deepest first
+  RcTable rc_tab[kRcLevels];
   uint32_t rc_vmax, rc_emax;        // dedup / best-list entries a snapshot may hold
   uint4* rc_pool;                   // snapshots: header x4, queue, dedup entries, best list
   unsigned long long rc_pool_cap;   // pool words (uint4)
   unsigned long long* rc_pool_used; // bump allocator
+  uint32_t rc_pool_chunk;           // pool words a building wave takes at a time
   uint32_t* rc_off;                 // build: snapshot offset of each entry (pool words)
   uint32_t* rc_count;               // build: queued states of each entry (EMPTY: not cached)
   // multi-character mappings (search.rs:776-780, 883-922, 945-961; builder.rs:383-442). With
@@ -329,7 +338,7 @@ struct Engine {
   // per-engine device scratch of the search launcher, reused across calls by whichever call holds
   // scratch_mu (a concurrent call on the same engine allocates its own)
   mutable std::mutex scratch_mu;
-  static constexpr int kScratch = 24;
+  static constexpr int kScratch = 32;
   mutable void* scratch_p[kScratch] = {};
   mutable size_t scratch_n[kScratch] = {};
 };

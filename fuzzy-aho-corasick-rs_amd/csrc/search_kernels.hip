@@ -1051,13 +1051,39 @@ __device__ __forceinline__ void sink64(uint64_t v) {
 }
 #endif
 
+constexpr uint32_t RC_POOL_CHUNK = 4096;  // largest pool chunk (words, 64 KiB) a building wave takes
 constexpr uint32_t RC_HDR = 4;  // snapshot header words: {head, tail, nv, pops}, {ne}, chars 0-3, chars 4-7
 struct RcHit {  // prefix-cache snapshot of a window (rc_lookup): pool offset and header
   uint32_t off, head, tail, nv_nel, pops;
 };
 
+// one best-map entry {me_rel, pattern, similarity bits, packed counts} of the window at `start`
+// as the crate's OwnedMatch record (search.rs:1111-1118); sb = the window's start byte
+__device__ __forceinline__ fac_match match_record(const SearchParams& P, const SegDesc& S, uint64_t start, uint64_t sb,
+                                                  const uint4& ent) {
+  const uint64_t me = start + ent.x;
+  fac_match m;
+  m.start = sb;
+  m.end = S.byte_base + (me < S.n ? local_byte(P, S, me) : S.hay_len);
+  m.pattern_index = ent.y;
+  m.similarity = __uint_as_float(ent.z);
+  m.insertions = ent.w & 0xFFu;
+  m.deletions = (ent.w >> 8) & 0xFFu;
+  m.substitutions = (ent.w >> 16) & 0xFFu;
+  m.swaps = ent.w >> 24;
+  m.edits = (uint8_t)edits_of(ent.w);
+  m.pad[0] = m.pad[1] = m.pad[2] = 0;
+  return m;
+}
+
 constexpr uint32_t claim_slots(uint32_t vcap) { return vcap / 2 < 512 ? 512 : vcap / 2; }  // >= ExpScratch
 
+#ifdef FAC_WIN_HIST  // diagnostics build (make hist): windows, pops and cycles by pops per window
+__device__ unsigned long long g_hist[24];
+__device__ __forceinline__ uint32_t hist_bucket(uint64_t pops) {  // 0, 1-15, 16-63, 64-255, 256-1023, 1024+
+  return pops == 0 ? 0u : pops < 16 ? 1u : pops < 64 ? 2u : pops < 256 ? 3u : pops < 1024 ? 4u : 5u;
+}
+#endif
 #ifdef FAC_PHASE_PROF  // diagnostics build (make prof): cycles per phase of run_window
 __device__ unsigned long long g_prof[16];
 #define PROF_T(t) const uint64_t t = __builtin_amdgcn_s_memtime()
@@ -1374,23 +1400,9 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     if (lane == 0) base = atomicAdd(P.counters, (unsigned long long)EL.n);
     base = shfl_u64(base, 0);
     const uint64_t sb = S.byte_base + local_byte(P, S, start);
-    const uint64_t n = S.n;
     for (uint32_t i = lane; i < EL.n; i += 64) {
       if (base + i >= P.out_cap) break;
-      const uint4 ent = EL.buf[i];
-      const uint64_t me = start + ent.x;
-      fac_match m;
-      m.start = sb;
-      m.end = S.byte_base + (me < n ? local_byte(P, S, me) : S.hay_len);
-      m.pattern_index = ent.y;
-      m.similarity = __uint_as_float(ent.z);
-      m.insertions = ent.w & 0xFFu;
-      m.deletions = (ent.w >> 8) & 0xFFu;
-      m.substitutions = (ent.w >> 16) & 0xFFu;
-      m.swaps = ent.w >> 24;
-      m.edits = (uint8_t)edits_of(ent.w);
-      m.pad[0] = m.pad[1] = m.pad[2] = 0;
-      P.out[base + i] = m;
+      P.out[base + i] = match_record(P, S, start, sb, EL.buf[i]);
     }
   }
 #ifdef FAC_PHASE_PROF
@@ -1430,40 +1442,56 @@ __device__ __forceinline__ uint32_t find_seg(const SearchParams& P, uint64_t v) 
 struct RcChars {
   uint4 a, b;
 };
-__device__ __forceinline__ bool rc_key(const SearchParams& P, const SegDesc& S, uint64_t s, uint32_t k, RcChars& ch,
-                                       uint64_t& key) {
+constexpr uint32_t RC_PAD = 0x1FFFFFu;
+// the window's first k chars (RC_PAD past the end of the text); false: a char inside the text but
+// beyond the resident halo (not cacheable)
+__device__ __forceinline__ bool rc_chars(const SearchParams& P, const SegDesc& S, uint64_t s, uint32_t k, uint32_t c[8]) {
   unsigned e2 = 0;
-  uint32_t c[8];
+  bool ok = true;
 #pragma unroll
   for (uint32_t i = 0; i < 8; ++i) {
-    c[i] = 0x1FFFFFu;
+    c[i] = RC_PAD;
     if (i < k && s + i < S.n) {
-      if (s + i >= S.avail) return false;
-      c[i] = text_char(P, S, s + i, e2);
+      if (s + i >= S.avail) ok = false;
+      else c[i] = text_char(P, S, s + i, e2);
     }
   }
-  ch.a = make_uint4(c[0], c[1], c[2], c[3]);
-  ch.b = make_uint4(c[4], c[5], c[6], c[7]);
+  return ok;
+}
+// key of the first k of the chars c (the rest padded)
+__device__ __forceinline__ uint64_t rc_hash_chars(const uint32_t c[8], uint32_t k, RcChars& ch) {
+  uint32_t d[8];
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) d[i] = i < k ? c[i] : RC_PAD;
+  ch.a = make_uint4(d[0], d[1], d[2], d[3]);
+  ch.b = make_uint4(d[4], d[5], d[6], d[7]);
   uint64_t h = 0x632BE59BD9B4E019ull ^ k;
 #pragma unroll
   for (uint32_t i = 0; i < 8; i += 2) {
-    const uint64_t w = ((uint64_t)c[i + 1] << 21) | c[i];
+    const uint64_t w = ((uint64_t)d[i + 1] << 21) | d[i];
     h = (h ^ w) * 0x9E3779B97F4A7C15ull;
     h ^= h >> 29;
   }
   h *= 0xD6E8FEB86659FD93ull;
   h ^= h >> 32;
-  key = h | (1ull << 63);
+  return h | (1ull << 63);
+}
+__device__ __forceinline__ bool rc_key(const SearchParams& P, const SegDesc& S, uint64_t s, uint32_t k, RcChars& ch,
+                                       uint64_t& key) {
+  uint32_t c[8];
+  if (!rc_chars(P, S, s, k, c)) return false;
+  key = rc_hash_chars(c, k, ch);
   return true;
 }
 __device__ __forceinline__ uint32_t rc_hash(uint64_t k) { return (uint32_t)k ^ (uint32_t)(k >> 32); }
 constexpr uint32_t RC_PROBES = 32;
 
 // A window's prefix-cache hit (snapshot header, read with the lookup): off = EMPTY on a miss.
-// Tables are consulted deepest first; the first verified hit wins.
+// Every level's probe chain (key slot, entry, snapshot count/offset) is issued together; the
+// deepest level whose snapshot header verifies the chars wins.
+#ifdef FAC_RC_SERIAL_LOOKUP
 template <uint32_t QCAP>
 __device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s) {
-  RcHit r{EMPTY, 0u, 0u, 0u, 0u};
   for (uint32_t t = 0; t < P.rc_ntab; ++t) {
     const RcTable& T = P.rc_tab[t];
     RcChars ch;
@@ -1487,47 +1515,67 @@ __device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc&
       if (kk == 0ull) break;
     }
   }
+  return RcHit{EMPTY, 0u, 0u, 0u, 0u};
+}
+#else
+template <uint32_t QCAP>
+__device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s) {
+  RcHit r{EMPTY, 0u, 0u, 0u, 0u};
+  uint32_t kmax = 0;
+  for (uint32_t t = 0; t < P.rc_ntab; ++t) kmax = max(kmax, P.rc_tab[t].k);
+  uint32_t c[8];
+  const bool ok = rc_chars(P, S, s, kmax, c);  // not cacheable past the halo at the deepest level:
+  uint64_t key[kRcLevels];                       // probe the levels whose keys stay inside it
+  uint32_t slot[kRcLevels];
+  unsigned long long kk[kRcLevels];
+  bool live[kRcLevels];
+#pragma unroll
+  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {
+    const RcTable& T = P.rc_tab[t];
+    live[t] = t < P.rc_ntab && (ok || (s + T.k <= S.avail));
+    RcChars ch;
+    key[t] = rc_hash_chars(c, T.k, ch);
+    slot[t] = rc_hash(key[t]) & T.mask;
+    kk[t] = live[t] ? T.keys[slot[t]] : 0ull;
+  }
+  uint32_t ent[kRcLevels];
+#pragma unroll
+  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {
+    const RcTable& T = P.rc_tab[t];
+    for (uint32_t p = 1; live[t] && kk[t] != key[t] && kk[t] != 0ull && p < RC_PROBES; ++p) {  // rare
+      slot[t] = (slot[t] + 1) & T.mask;
+      kk[t] = T.keys[slot[t]];
+    }
+    live[t] = live[t] && kk[t] == key[t];
+    ent[t] = live[t] ? T.val[slot[t]] : EMPTY;
+  }
+  uint32_t cnt[kRcLevels], off[kRcLevels];
+#pragma unroll
+  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {
+    const RcTable& T = P.rc_tab[t];
+    live[t] = live[t] && ent[t] != EMPTY;
+    cnt[t] = live[t] ? T.count[ent[t]] : EMPTY;
+    off[t] = live[t] ? T.off[ent[t]] : 0u;
+  }
+  for (uint32_t t = 0; t < P.rc_ntab; ++t) {  // deepest first; a failed verification (a 64-bit hash
+    if (cnt[t] == EMPTY || cnt[t] + 1u > QCAP) continue;  // collision) falls through
+    const uint32_t o = off[t];
+    RcChars ch;
+    (void)rc_hash_chars(c, P.rc_tab[t].k, ch);
+    const uint4 h0 = P.rc_pool[o], h1 = P.rc_pool[o + 1], sa = P.rc_pool[o + 2], sb = P.rc_pool[o + 3];
+    if (sa.x == ch.a.x && sa.y == ch.a.y && sa.z == ch.a.z && sa.w == ch.a.w && sb.x == ch.b.x && sb.y == ch.b.y &&
+        sb.z == ch.b.z && sb.w == ch.b.w)
+      return RcHit{o, h0.x, h0.y, h0.z | (h1.x << 16), h0.w};
+  }
   return r;
 }
+#endif
 
-// Prefix-cache keys: every searched window's key is inserted once (plain probe first, CAS only on
-// an empty slot); the inserting window becomes the entry's representative (rc_rep).
-__global__ __launch_bounds__(256) void rc_collect_kernel(SearchParams P, unsigned long long* keys, uint32_t* val,
-                                                         uint64_t* rep, unsigned int* n_ent, uint32_t max_ent,
-                                                         uint32_t mask) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  unsigned err = 0;
-  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < P.total_windows; v += stride) {
-    const uint64_t vid = P.win_list ? P.win_list[v] : v;
-    const uint32_t kl = find_seg(P, vid);
-    const SegDesc S = P.segs[kl];
-    const uint64_t start = S.w_begin + (vid - P.seg_prefix[kl]);
-    if (window_skipped(P, S, start, err)) continue;
-    RcChars ch;
-    uint64_t k;
-    if (!rc_key(P, S, start, P.rc_k, ch, k)) continue;
-    const uint32_t h = rc_hash(k);
-    for (uint32_t p = 0; p < RC_PROBES; ++p) {
-      const uint32_t slot = (h + p) & mask;
-      unsigned long long kk = keys[slot];
-      if (kk == 0ull) {
-        kk = atomicCAS(&keys[slot], 0ull, (unsigned long long)k);
-        if (kk == 0ull) {
-          const uint32_t ent = atomicAdd(n_ent, 1u);
-          if (ent < max_ent) rep[ent] = vid;
-          val[slot] = ent < max_ent ? ent : EMPTY;
-          break;
-        }
-      }
-      if (kk == k) break;
-    }
-  }
-}
-
-// Level-2 keys (long prefixes): a sample of the windows (every `stride`-th) is counted per key;
-// the first inserter of a key is its representative.
+// Prefix-cache keys: every `stride`-th window's key is inserted and counted (level 1: every window,
+// sampled levels: a sample); the first inserter of a key is its representative. Counts saturate
+// at `sat` (only "at least thr" is asked), so a frequent key is not one hot atomic per window.
 __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, unsigned long long* keys, uint32_t* cnt,
-                                                       uint64_t* rep, uint32_t mask, uint32_t stride) {
+                                                       uint64_t* rep, uint32_t mask, uint32_t stride, uint32_t sat) {
   const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
   unsigned err = 0;
   const uint64_t ns = (P.total_windows + stride - 1) / stride;
@@ -1553,29 +1601,82 @@ __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, unsigned 
         }
       }
       if (kk == k) {
-        atomicAdd(&cnt[slot], 1u);
+        if (cnt[slot] < sat) atomicAdd(&cnt[slot], 1u);
         break;
       }
     }
   }
 }
 
-// Level-2 entries: the keys counted at least `thr` times, numbered in slot order of arrival;
-// every other slot maps to EMPTY (not cached: the lookup falls through to level 1).
-__global__ __launch_bounds__(256) void rc_select_kernel(const unsigned long long* keys, const uint32_t* cnt,
-                                                        const uint64_t* rep_slot, uint32_t* val, uint64_t* rep,
-                                                        unsigned int* n_ent, uint32_t n_slots, uint32_t thr,
-                                                        uint32_t max_ent) {
-  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += gridDim.x * blockDim.x) {
-    uint32_t v = EMPTY;
-    if (keys[s] != 0ull && cnt[s] >= thr) {
-      const uint32_t ent = atomicAdd(n_ent, 1u);
-      if (ent < max_ent) {
-        rep[ent] = rep_slot[s];
-        v = ent;
-      }
+// Entries of a level: the keys counted at least `thr` times, numbered without a contended counter
+// (one same-address atomic per selected wave serialises at one L2 channel): per-block counts over
+// contiguous slot ranges, an exclusive scan of the block counts, then the assignment. Every other
+// slot maps to EMPTY (not cached: the lookup falls through to the next level).
+__device__ __forceinline__ bool rc_selected(const unsigned long long* keys, const uint32_t* cnt, uint32_t s,
+                                            uint32_t thr) {
+  return keys[s] != 0ull && cnt[s] >= thr;
+}
+__global__ __launch_bounds__(256) void rc_sel_count_kernel(const unsigned long long* keys, const uint32_t* cnt,
+                                                           uint32_t n_slots, uint32_t range, uint32_t thr,
+                                                           uint32_t* bcount) {
+  __shared__ uint32_t tot;
+  if (threadIdx.x == 0) tot = 0;
+  __syncthreads();
+  const uint32_t b0 = blockIdx.x * range, b1 = min(b0 + range, n_slots);
+  uint32_t c = 0;
+  for (uint32_t s = b0 + threadIdx.x; s < b1; s += blockDim.x) c += rc_selected(keys, cnt, s, thr) ? 1u : 0u;
+  c = wave_inclusive_sum(c);
+  if (lane_id() == 63) atomicAdd(&tot, c);
+  __syncthreads();
+  if (threadIdx.x == 0) bcount[blockIdx.x] = tot;
+}
+// one block: exclusive scan of nb (<= 8192) block counts in place; n_ent = the total
+__global__ __launch_bounds__(256) void rc_sel_scan_kernel(uint32_t* bcount, uint32_t nb, unsigned int* n_ent) {
+  __shared__ uint32_t c[8192];
+  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) c[i] = bcount[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (uint32_t i = 0; i < nb; ++i) {
+      const uint32_t v = c[i];
+      c[i] = run;
+      run += v;
     }
-    val[s] = v;
+    *n_ent = run;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) bcount[i] = c[i];
+}
+// counts are read and replaced by entries in place (val may alias cnt: a slot is only touched by
+// its own thread); rep[entry] = the slot's representative window
+__global__ __launch_bounds__(256) void rc_sel_assign_kernel(const unsigned long long* keys, const uint32_t* cnt,
+                                                            const uint64_t* rep_slot, uint32_t* val, uint64_t* rep,
+                                                            const uint32_t* bbase, uint32_t n_slots, uint32_t range,
+                                                            uint32_t thr, uint32_t max_ent) {
+  __shared__ uint32_t run;
+  if (threadIdx.x == 0) run = bbase[blockIdx.x];
+  __syncthreads();
+  const uint32_t b0 = blockIdx.x * range, b1 = min(b0 + range, n_slots);
+  for (uint32_t s0 = b0; s0 < b1; s0 += blockDim.x) {
+    const uint32_t s = s0 + threadIdx.x;
+    const bool sel = s < b1 && rc_selected(keys, cnt, s, thr);
+    const uint64_t m = __ballot(sel);
+    uint32_t base = 0;
+    if (m) {
+      if (lane_id() == (uint32_t)first_lane(m)) base = atomicAdd(&run, (uint32_t)__popcll(m));  // LDS
+      base = shfl_u32(base, first_lane(m));
+    }
+    if (s < b1) {
+      uint32_t v = EMPTY;
+      if (sel) {
+        const uint32_t ent = base + prefix_below(m);
+        if (ent < max_ent) {
+          rep[ent] = rep_slot[s];
+          v = ent;
+        }
+      }
+      val[s] = v;
+    }
   }
 }
 
@@ -1586,15 +1687,27 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   __shared__ __attribute__((aligned(16))) uint32_t s_claim[claim_slots(VCAP)];
   const uint32_t lane = lane_id();
   EmitList EL{P.ebuf + (size_t)blockIdx.x * P.ecap, P.ecap, 0};
-  uint64_t popped = 0, cached = 0;
+  uint64_t popped = 0, cached = 0;     // wave-uniform
+  uint64_t cached_lane = 0;            // per lane: lane-flushed windows' snapshot pops
+  unsigned long long pool_cur = 0, pool_end = 0;  // cache build: this wave's snapshot pool chunk
+  uint32_t res_lane = 0, triv_lane = 0;  // per lane: resumed windows, of those lane-flushed
   // dedup-commit claim sequence (phase C): fresh claims are >= 128, above any stale word the
   // expansion scratch leaves behind (<= 64)
   uint32_t cseq = 1;
   for (uint32_t i = lane_id(); i < claim_slots(VCAP); i += 64) s_claim[i] = 0u;
   __builtin_amdgcn_wave_barrier();
   unsigned err = 0;
+  // chunks are handed out by a global work counter (counters[7]): waves that become resident late,
+  // or draw cheap windows, take more chunks, so the launch ends when the work does (a static
+  // grid-stride split idles every slot of a CU once its first-round workgroups finish)
+  auto next_chunk = [&]() -> uint64_t {
+    unsigned long long c = 0;
+    if (lane == 0) c = atomicAdd(P.counters + 7, (unsigned long long)P.chunk);
+    return shfl_u64(c, 0);
+  };
   const uint64_t stride = (uint64_t)gridDim.x * P.chunk;
-  for (uint64_t cb = (uint64_t)blockIdx.x * P.chunk; cb < P.total_windows; cb += stride) {
+  for (uint64_t cb = P.dyn_chunks ? next_chunk() : (uint64_t)blockIdx.x * P.chunk; cb < P.total_windows;
+       cb = P.dyn_chunks ? next_chunk() : cb + stride) {
     const uint64_t ce = min(cb + (uint64_t)P.chunk, P.total_windows);
     for (uint64_t v0 = cb; v0 < ce; v0 += 64) {
       const uint64_t v = v0 + lane;
@@ -1610,6 +1723,45 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
       }
       RcHit hit{EMPTY, 0u, 0u, 0u, 0u};  // prefix-cache snapshot of this lane's window
       if (P.rc_mode != 0 && P.rc_ntab && active) hit = rc_lookup<QCAP>(P, P.segs[kl], start);
+      if (P.rc_mode == 1) {
+        const bool resumed = active && hit.off != EMPTY;
+        res_lane += resumed ? 1u : 0u;
+        // a snapshot with an empty queue is the window's final best map (no pop is left): each lane
+        // writes its own window's records instead of the wave walking the window
+        const bool triv = resumed && hit.tail == hit.head && P.rc_lane_flush;
+        if (__ballot(triv)) {
+          const uint32_t ne = triv ? (hit.nv_nel >> 16) : 0u;
+          const uint32_t incl = wave_inclusive_sum(ne), tot = shfl_u32(incl, 63);
+          unsigned long long base = 0;
+          if (tot) {
+            if (lane == 0) base = atomicAdd(P.counters, (unsigned long long)tot);
+            base = shfl_u64(base, 0);
+          }
+          if (triv) {
+            const SegDesc S = P.segs[kl];
+            const uint64_t sb = S.byte_base + local_byte(P, S, start);
+            const uint4* src = P.rc_pool + hit.off + RC_HDR + (hit.nv_nel & 0xFFFFu);  // best list (nq == 0)
+            for (uint32_t i = 0; i < ne; ++i) {
+              const uint64_t o = base + incl - ne + i;
+              if (o < P.out_cap) P.out[o] = match_record(P, S, start, sb, src[i]);
+            }
+            if (P.win_counts) P.win_counts[vid] = hit.tail;
+            cached_lane += hit.pops;
+            triv_lane += 1;
+          }
+          active = active && !triv;
+        }
+      }
+      if (P.rc_mode == 2) {
+        // a representative whose parent snapshot has an empty queue ends at the parent: its own
+        // snapshot would hold the same best list, so the key stays uncached (lookups fall through)
+        const bool done = active && hit.off != EMPTY && hit.tail == hit.head;
+        if (done) {
+          P.rc_off[v] = EMPTY;
+          P.rc_count[v] = EMPTY;
+        }
+        active = active && !done;
+      }
       uint64_t m = __ballot(active);
       while (m) {
         const int l = first_lane(m);
@@ -1621,8 +1773,20 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         uint32_t qhead = 0, vcnt = 0;
         const RcHit rc{shfl_u32(hit.off, l), shfl_u32(hit.head, l), shfl_u32(hit.tail, l), shfl_u32(hit.nv_nel, l),
                        shfl_u32(hit.pops, l)};
+#ifdef FAC_WIN_HIST
+        const uint64_t t_w0 = __builtin_amdgcn_s_memtime();
+#endif
         const uint32_t qlen =
             run_window<VCAP, QCAP, MAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, rc, popped, cached, err, qhead, vcnt);
+#ifdef FAC_WIN_HIST
+        if (lane == 0 && P.rc_mode != 2) {
+          const uint32_t b = hist_bucket(popped - popped0);
+          atomicAdd(&g_hist[b], 1ull);
+          atomicAdd(&g_hist[6 + b], (unsigned long long)(popped - popped0));
+          atomicAdd(&g_hist[12 + b], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_w0));
+          atomicAdd(&g_hist[18 + b], rc.off != EMPTY ? 1ull : 0ull);
+        }
+#endif
         if (P.rc_mode == 2) {  // cache build: entry = list position; what does not fit stays uncached
           const uint32_t ent = (uint32_t)(v0 + (uint64_t)l);
           const uint32_t nq = qlen - qhead;
@@ -1637,9 +1801,17 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
             for (uint32_t b = 0; b < VCAP; b += 64) nv += (uint32_t)__popcll(__ballot(live(s_vis[b + lane])));
           bool bad = (wave_or(err) & (ERR_QUEUE | ERR_VISITED | ERR_EMIT)) != 0 || EL.n > P.rc_emax || nv > P.rc_vmax;
           const uint32_t words = RC_HDR + nq + nv + EL.n;
-          unsigned long long off = 0;
-          if (lane == 0 && !bad) off = atomicAdd(P.rc_pool_used, (unsigned long long)words);
-          off = shfl_u64(off, 0);
+          // the wave carves snapshots out of its own pool chunk: one pool atomic per chunk, not per
+          // snapshot (a same-address atomic per entry serialises the build at one L2 channel)
+          if (!bad && pool_cur + words > pool_end) {
+            const unsigned long long want = max((unsigned long long)words, (unsigned long long)P.rc_pool_chunk);
+            unsigned long long c = 0;
+            if (lane == 0) c = atomicAdd(P.rc_pool_used, want);
+            pool_cur = shfl_u64(c, 0);
+            pool_end = pool_cur + want;
+          }
+          const unsigned long long off = pool_cur;
+          if (!bad) pool_cur += words;
           bad = bad || off + words > P.rc_pool_cap || off > 0xFFFFFFF0ull;
           RcChars kch;
           uint64_t kkey;
@@ -1695,7 +1867,10 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
     if (any_err(err)) break;
   }
   if (lane == 0) atomicAdd(P.counters + 1, (unsigned long long)popped);
-  if (lane == 0 && cached) atomicAdd(P.counters + 4, (unsigned long long)cached);
+  if (lane == 0) cached_lane += cached;
+  if (cached_lane) atomicAdd(P.counters + 4, cached_lane);
+  if (res_lane) atomicAdd(P.counters + 5, (unsigned long long)res_lane);
+  if (triv_lane) atomicAdd(P.counters + 6, (unsigned long long)triv_lane);
   const unsigned all = wave_or(err);
   if (lane == 0 && all) atomicOr(reinterpret_cast<unsigned int*>(P.counters + 2), all);
 }
@@ -1703,10 +1878,12 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
 // one wavefront per workgroup; the dedup-free variants are held to <= 128 VGPRs (4 waves/SIMD),
 // the dedup variants are bounded by LDS first
 #ifndef FAC_BEAM_WAVES  // waves/SIMD the dedup variants are compiled for (VGPR budget); 0 = unbounded
-#define FAC_BEAM_WAVES 0
+// 3: <= 168 VGPRs (a few rare-path spills), matching the 11 workgroups/CU their LDS allows; unbounded
+// they take ~175 VGPRs and 2 waves/SIMD (C3 kernel 133 -> 111 ms measured)
+#define FAC_BEAM_WAVES 3
 #endif
 template <uint32_t VCAP, uint32_t QCAP, bool MAP>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((FAC_BEAM_WAVES && VCAP <= 512) ? FAC_BEAM_WAVES : 1)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((FAC_BEAM_WAVES && VCAP <= 512 && QCAP <= 256) ? FAC_BEAM_WAVES : 1)))
 void bfs_window_kernel(SearchParams P) {
   bfs_window_body<VCAP, QCAP, MAP>(P);
 }
@@ -1717,7 +1894,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QCAP <= 512 
 // prefix-cache build (P.rc_mode == 2): one representative window per key, popped up to the first
 // state past the key; its own symbol so profiles separate it from the search launches
 template <uint32_t QCAP>
-__global__ __launch_bounds__(64) void rc_build_kernel(SearchParams P) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((FAC_BEAM_WAVES && QCAP <= 256) ? FAC_BEAM_WAVES : 1)))
+void rc_build_kernel(SearchParams P) {
   bfs_window_body<512, QCAP, false>(P);  // the prefix cache is off with mappings
 }
 
@@ -2257,14 +2435,17 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   };
 
   DevBuf d_segs, d_prefix, d_out, d_ebuf, d_cnt, d_list, d_spill;
-  DevBuf d_rck, d_rcv, d_rcrep, d_rcs, d_rcc, d_rcn;  // prefix cache, level 1 + pool
-  DevBuf d_rck2, d_rcv2, d_rcslot2, d_rcrep2, d_rcc2;  // prefix cache, level 2
+  DevBuf d_rck, d_rcv, d_rcslot, d_rcb, d_rcrep, d_rcs, d_rcc, d_rcn;  // prefix cache, level 1 + pool
+  DevBuf d_xk[kRcLevels - 1], d_xv[kRcLevels - 1], d_xslot[kRcLevels - 1], d_xrep[kRcLevels - 1],
+      d_xc[kRcLevels - 1];  // prefix cache, sampled levels
   std::unique_lock<std::mutex> lease(e.scratch_mu, std::try_to_lock);
   if (lease.owns_lock()) {  // reuse the engine's scratch (no per-call hipMalloc of the 64 MB lists)
-    DevBuf* bufs[18] = {&d_segs, &d_prefix, &d_out,   &d_ebuf, &d_cnt,     &d_list,   &d_spill, &d_rck,  &d_rcv,
-                        &d_rcrep, &d_rcs,   &d_rcc,   &d_rcn,  &d_rck2,    &d_rcv2,   &d_rcslot2, &d_rcrep2, &d_rcc2};
-    static_assert(Engine::kScratch >= 18, "engine scratch slots");
-    for (int i = 0; i < 18; ++i) bufs[i]->bind(&e.scratch_p[i], &e.scratch_n[i]);
+    std::vector<DevBuf*> bufs = {&d_segs, &d_prefix, &d_out, &d_ebuf, &d_cnt, &d_list, &d_spill,
+                                 &d_rck,  &d_rcv,    &d_rcslot, &d_rcb, &d_rcrep, &d_rcs, &d_rcc, &d_rcn};
+    for (int x = 0; x < kRcLevels - 1; ++x)
+      for (DevBuf* b : {&d_xk[x], &d_xv[x], &d_xslot[x], &d_xrep[x], &d_xc[x]}) bufs.push_back(b);
+    static_assert(Engine::kScratch >= 15 + 5 * (kRcLevels - 1), "engine scratch slots");
+    for (size_t i = 0; i < bufs.size(); ++i) bufs[i]->bind(&e.scratch_p[i], &e.scratch_n[i]);
   }
   HIP_TRY(d_segs.alloc(segs.size() * sizeof(SegDesc), stream));
   HIP_TRY(d_prefix.alloc(prefix.size() * sizeof(uint64_t), stream));
@@ -2274,7 +2455,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   uint64_t spill_cap = std::max<uint64_t>(4096, windows / 32);
   const uint32_t max_grid = (uint32_t)cus * 16;
   HIP_TRY(d_ebuf.alloc((size_t)max_grid * P.ecap * sizeof(uint4), stream));
-  HIP_TRY(d_cnt.alloc(5 * sizeof(unsigned long long), stream));
+  HIP_TRY(d_cnt.alloc(N_COUNTERS * sizeof(unsigned long long), stream));
   HIP_TRY(d_out.alloc(out_cap * sizeof(fac_match), stream));
   HIP_TRY(d_spill.alloc(spill_cap * sizeof(uint64_t), stream));
   DevBuf d_counts;
@@ -2293,12 +2474,12 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
 
   int rc = FAC_OK;
   uint64_t retries = 0, launches = 0, popped = 0, cached_pops = 0, pass_windows = windows;
-  unsigned long long cnt[5] = {0, 0, 0, 0, 0};
+  unsigned long long cnt[N_COUNTERS] = {};
   float ms_total = 0.f, cache_ms = 0.f;
   out.clear();
 
   // Prefix cache. Level 1: every window's key of K0 chars (4, else 3, else 2,
-  // whichever first gives every snapshot at least 8 windows on average); rc_collect_kernel numbers
+  // whichever first gives every snapshot at least 8 windows on average); rc_count_kernel inserts
   // the keys, rc_build_kernel searches one representative per key up to the first state that reads
   // past the key. Level 2: keys of K1 (> K0) chars, counted on a sample of the windows; keys seen at
   // least T times get a snapshot built by resuming their representative from its level-1 snapshot.
@@ -2306,6 +2487,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   // pattern), with mappings (whole-grapheme keys), or when the search is small.
   P.rc_mode = 0;
   P.rc_ntab = 0;
+  P.rc_lane_flush = std::getenv("FAC_RC_NO_LANE") ? 0 : 1;
+  P.dyn_chunks = std::getenv("FAC_STATIC_GRID") ? 0 : 1;
   const bool root_out = !e.nodes.empty() && e.nodes[0].out_end > e.nodes[0].out_begin;
   const char* rc_min = std::getenv("FAC_RC_MIN");  // env knobs: tests force it on / pin K, A/B turns it off
   const char* kenv = std::getenv("FAC_RC_K");
@@ -2320,12 +2503,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     const uint32_t qbuild = std::max<uint32_t>((uint32_t)fan_root + 1, qmain);
     P.rc_vmax = vmain ? std::min<uint32_t>(256, vmain / 2) : 256;
     P.rc_emax = 64;
-    const uint64_t ent_cap = std::max<uint64_t>(1, env_u("FAC_RC_ENTRIES", 4ull << 20));
+    const uint64_t ent_cap = std::max<uint64_t>(1, env_u("FAC_RC_ENTRIES", 16ull << 20));
     const uint32_t max_ent = (uint32_t)std::min<uint64_t>(windows, ent_cap);
     uint32_t slots = 1u << 12;
     while (slots < 4ull * max_ent && slots < (1u << 24)) slots <<= 1;
     HIP_TRY(d_rck.alloc(slots * sizeof(unsigned long long), stream));
-    HIP_TRY(d_rcv.alloc(slots * sizeof(uint32_t), stream));
+    HIP_TRY(d_rcv.alloc(slots * sizeof(uint32_t), stream));  // key counts, then entries
+    HIP_TRY(d_rcslot.alloc(slots * sizeof(uint64_t), stream));
+    HIP_TRY(d_rcb.alloc(8192 * sizeof(uint32_t), stream));
     HIP_TRY(d_rcrep.alloc(max_ent * sizeof(uint64_t), stream));
     HIP_TRY(d_rcc.alloc(2 * (size_t)max_ent * sizeof(uint32_t), stream));  // counts, then offsets
     HIP_TRY(d_rcn.alloc(4 * sizeof(unsigned long long), stream));  // keys, pool words used, level-2 entries
@@ -2335,86 +2520,129 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     HIP_TRY(hipEventRecord(ev.a, stream));
     HIP_TRY(hipMemsetAsync(d_rcn.p, 0, 4 * sizeof(unsigned long long), stream));
     const uint32_t cgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256, (uint64_t)cus * 8));
+    // keys counted >= thr -> entries 0..n-1 (slot counts replaced by entries in place), reps by entry;
+    // returns n (all selected keys; entries past max_ent stay uncached)
+    auto number_entries = [&](const DevBuf& keys, const DevBuf& cv, const DevBuf& rslot, const DevBuf& rep,
+                              uint32_t n_slots, uint32_t thr, uint32_t cap, unsigned int& n) -> int {
+      const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(8192, n_slots / 4096));
+      const uint32_t range = (n_slots + nb - 1) / nb;  // n_slots and nb are powers of two: a multiple of 256
+      unsigned int* n_dev = reinterpret_cast<unsigned int*>(static_cast<unsigned long long*>(d_rcn.p) + 2);
+      hipLaunchKernelGGL(rc_sel_count_kernel, dim3(nb), dim3(256), 0, stream,
+                         static_cast<const unsigned long long*>(keys.p), static_cast<const uint32_t*>(cv.p), n_slots,
+                         range, thr, static_cast<uint32_t*>(d_rcb.p));
+      hipLaunchKernelGGL(rc_sel_scan_kernel, dim3(1), dim3(256), 0, stream, static_cast<uint32_t*>(d_rcb.p), nb, n_dev);
+      hipLaunchKernelGGL(rc_sel_assign_kernel, dim3(nb), dim3(256), 0, stream,
+                         static_cast<const unsigned long long*>(keys.p), static_cast<const uint32_t*>(cv.p),
+                         static_cast<const uint64_t*>(rslot.p), static_cast<uint32_t*>(cv.p),
+                         static_cast<uint64_t*>(rep.p), static_cast<const uint32_t*>(d_rcb.p), n_slots, range, thr, cap);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemcpyAsync(&n, n_dev, sizeof(n), hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      return FAC_OK;
+    };
     uint32_t n_ent1 = 0;
+    uint64_t l1_keys = 0;
     for (uint32_t k = kpin ? kpin : 4u; k >= (kpin ? kpin : 2u); --k) {
       P.rc_k = k;
       HIP_TRY(hipMemsetAsync(d_rck.p, 0, slots * sizeof(unsigned long long), stream));
-      HIP_TRY(hipMemsetAsync(d_rcv.p, 0xFF, slots * sizeof(uint32_t), stream));
-      HIP_TRY(hipMemsetAsync(d_rcn.p, 0, sizeof(unsigned long long), stream));
-      hipLaunchKernelGGL(rc_collect_kernel, dim3(cgrid), dim3(256), 0, stream, P,
+      HIP_TRY(hipMemsetAsync(d_rcv.p, 0, slots * sizeof(uint32_t), stream));
+      hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P,
                          static_cast<unsigned long long*>(d_rck.p), static_cast<uint32_t*>(d_rcv.p),
-                         static_cast<uint64_t*>(d_rcrep.p), static_cast<unsigned int*>(d_rcn.p), max_ent, slots - 1);
+                         static_cast<uint64_t*>(d_rcslot.p), slots - 1, 1u, 1u);
       HIP_TRY(hipGetLastError());
       unsigned int n_keys = 0;
-      HIP_TRY(hipMemcpyAsync(&n_keys, d_rcn.p, sizeof(n_keys), hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
+      if (int nrc = number_entries(d_rck, d_rcv, d_rcslot, d_rcrep, slots, 1u, max_ent, n_keys)) return nrc;
+      l1_keys = n_keys;
       if (n_keys == 0) break;
       if (!kpin && 8ull * n_keys > windows) continue;  // too little reuse: fewer chars per key
       n_ent1 = std::min(n_keys, max_ent);
       L1.k = k;
       break;
     }
-    // level 2: frequent long prefixes (FAC_RC_K2 = 0 turns it off)
-    const uint32_t k2 = (uint32_t)std::min<uint64_t>(8, env_u("FAC_RC_K2", 6));
-    const uint32_t stride2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_STRIDE2", 8));
+    // sampled levels: frequent long prefixes, ascending key lengths (FAC_RC_LEVELS, e.g. "6" or
+    // "5,7"; FAC_RC_K2 = k pins one level, 0 turns them off)
+    std::vector<uint32_t> ks;
+    if (const char* k2e = std::getenv("FAC_RC_K2")) {
+      const uint32_t k2 = (uint32_t)std::strtoul(k2e, nullptr, 10);
+      if (k2) ks.push_back(std::min<uint32_t>(8, k2));
+    } else {
+      const char* le = std::getenv("FAC_RC_LEVELS");
+      std::string spec = le ? le : "5,6,8";
+      for (size_t a = 0; a < spec.size();) {
+        const size_t b = spec.find(',', a);
+        const uint32_t k = (uint32_t)std::strtoul(spec.substr(a, b == std::string::npos ? std::string::npos : b - a).c_str(), nullptr, 10);
+        if (k && (ks.empty() || k > ks.back()) && k <= 8 && ks.size() < (size_t)kRcLevels - 1) ks.push_back(k);
+        if (b == std::string::npos) break;
+        a = b + 1;
+      }
+    }
+    const uint32_t stride2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_STRIDE2", 2));
     const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", 2));
-    uint32_t n_ent2 = 0;
-    RcTable L2{};
-    if (n_ent1 && k2 > L1.k && windows >= env_u("FAC_RC_MIN2", 1ull << 20)) {
+    std::vector<RcTable> Lx;        // sampled levels, ascending k
+    std::vector<uint32_t> n_entx;   // their entries
+    if (n_ent1 && windows >= env_u("FAC_RC_MIN2", 1ull << 20)) {
       const uint64_t samples = (windows + stride2 - 1) / stride2;
       uint32_t slots2 = 1u << 12;
       while (slots2 < 2ull * samples && slots2 < (1u << 27)) slots2 <<= 1;
       const uint32_t max_ent2 = (uint32_t)std::min<uint64_t>(samples, ent_cap);
-      HIP_TRY(d_rck2.alloc(slots2 * sizeof(unsigned long long), stream));
-      HIP_TRY(d_rcv2.alloc(slots2 * sizeof(uint32_t), stream));  // sample counts, then entries
-      HIP_TRY(d_rcslot2.alloc(slots2 * sizeof(uint64_t), stream));
-      HIP_TRY(d_rcrep2.alloc(max_ent2 * sizeof(uint64_t), stream));
-      HIP_TRY(d_rcc2.alloc(2 * (size_t)max_ent2 * sizeof(uint32_t), stream));
-      HIP_TRY(hipMemsetAsync(d_rck2.p, 0, slots2 * sizeof(unsigned long long), stream));
-      HIP_TRY(hipMemsetAsync(d_rcv2.p, 0, slots2 * sizeof(uint32_t), stream));
-      SearchParams C = P;
-      C.rc_k = k2;
-      hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, C,
-                         static_cast<unsigned long long*>(d_rck2.p), static_cast<uint32_t*>(d_rcv2.p),
-                         static_cast<uint64_t*>(d_rcslot2.p), slots2 - 1, stride2);
-      HIP_TRY(hipGetLastError());
-      // counts are read and replaced by entries in place: a slot is only touched by its own thread
-      hipLaunchKernelGGL(rc_select_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>(slots2 / 256, cus * 8))),
-                         dim3(256), 0, stream, static_cast<const unsigned long long*>(d_rck2.p),
-                         static_cast<const uint32_t*>(d_rcv2.p), static_cast<const uint64_t*>(d_rcslot2.p),
-                         static_cast<uint32_t*>(d_rcv2.p), static_cast<uint64_t*>(d_rcrep2.p),
-                         reinterpret_cast<unsigned int*>(static_cast<unsigned long long*>(d_rcn.p) + 2), slots2, thr2,
-                         max_ent2);
-      HIP_TRY(hipGetLastError());
-      unsigned int nk2 = 0;
-      HIP_TRY(hipMemcpyAsync(&nk2, static_cast<unsigned long long*>(d_rcn.p) + 2, sizeof(nk2), hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
-      n_ent2 = std::min(nk2, max_ent2);
-      L2 = RcTable{k2, slots2 - 1, static_cast<const unsigned long long*>(d_rck2.p), static_cast<const uint32_t*>(d_rcv2.p),
-                   static_cast<uint32_t*>(d_rcc2.p) + max_ent2, static_cast<uint32_t*>(d_rcc2.p)};
-      if (n_ent2 == 0) L2.k = 0;
+      for (uint32_t k2 : ks) {
+        if (k2 <= L1.k) continue;
+        const size_t x = Lx.size();
+        HIP_TRY(d_xk[x].alloc(slots2 * sizeof(unsigned long long), stream));
+        HIP_TRY(d_xv[x].alloc(slots2 * sizeof(uint32_t), stream));  // sample counts, then entries
+        HIP_TRY(d_xslot[x].alloc(slots2 * sizeof(uint64_t), stream));
+        HIP_TRY(d_xrep[x].alloc(max_ent2 * sizeof(uint64_t), stream));
+        HIP_TRY(d_xc[x].alloc(2 * (size_t)max_ent2 * sizeof(uint32_t), stream));
+        HIP_TRY(hipMemsetAsync(d_xk[x].p, 0, slots2 * sizeof(unsigned long long), stream));
+        HIP_TRY(hipMemsetAsync(d_xv[x].p, 0, slots2 * sizeof(uint32_t), stream));
+        SearchParams C = P;
+        C.rc_k = k2;
+        hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, C,
+                           static_cast<unsigned long long*>(d_xk[x].p), static_cast<uint32_t*>(d_xv[x].p),
+                           static_cast<uint64_t*>(d_xslot[x].p), slots2 - 1, stride2, thr2);
+        HIP_TRY(hipGetLastError());
+        unsigned int nk2 = 0;
+        if (int nrc = number_entries(d_xk[x], d_xv[x], d_xslot[x], d_xrep[x], slots2, thr2, max_ent2, nk2)) return nrc;
+        const uint32_t ne = std::min(nk2, max_ent2);
+        if (ne == 0) continue;
+        Lx.push_back(RcTable{k2, slots2 - 1, static_cast<const unsigned long long*>(d_xk[x].p),
+                             static_cast<const uint32_t*>(d_xv[x].p), static_cast<uint32_t*>(d_xc[x].p) + max_ent2,
+                             static_cast<uint32_t*>(d_xc[x].p)});
+        n_entx.push_back(ne);
+      }
     }
     if (n_ent1) {
-      // snapshot pool: the worst entry for every key of both levels, up to a budget; a build that
+      // snapshot pool: the worst entry for every key of every level, up to a budget; a build that
       // runs out of pool leaves the remaining keys uncached
+      uint64_t n_all = n_ent1;
+      for (uint32_t ne : n_entx) n_all += ne;
       const uint64_t worst = RC_HDR + std::min(qmain, qbuild) + P.rc_vmax + P.rc_emax;
       const uint64_t budget = env_u("FAC_RC_POOL_MB", 16384ull) << 20;
-      const uint64_t pool_words =
-          std::max<uint64_t>(1024, std::min<uint64_t>((uint64_t)(n_ent1 + n_ent2) * worst, budget / sizeof(uint4)));
+      // per-wave pool chunks: about a quarter of the expected pool (~40 words a snapshot) spread over
+      // the building waves, at least one worst snapshot; + one partly used chunk per wave and level
+      uint64_t grids = std::min<uint64_t>(n_ent1, max_grid);
+      for (uint32_t ne : n_entx) grids += std::min<uint64_t>(ne, max_grid);
+      P.rc_pool_chunk = (uint32_t)std::max<uint64_t>(worst, std::min<uint64_t>(RC_POOL_CHUNK, n_all * 40 / (4 * grids)));
+      const uint64_t pool_words = std::max<uint64_t>(1024, std::min<uint64_t>(n_all * worst, budget / sizeof(uint4))) +
+                                  grids * P.rc_pool_chunk;
       HIP_TRY(d_rcs.alloc(pool_words * sizeof(uint4), stream));
       P.rc_pool = static_cast<uint4*>(d_rcs.p);
       P.rc_pool_cap = pool_words;
-      auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, const RcTable* parent) -> int {
+      // tables deepest first: a build resumes its representatives from the levels below it
+      std::vector<RcTable> tabs{L1};
+      auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps) -> int {
         SearchParams Q = P;
         Q.rc_mode = 2;
         Q.rc_k = T.k;
-        Q.rc_ntab = parent ? 1u : 0u;
-        if (parent) Q.rc_tab[0] = *parent;
+        Q.rc_ntab = 0;
+        for (size_t t = tabs.size(); t-- > 0 && T.k > tabs[t].k;)  // levels below T, deepest first
+          if (&tabs[t] != &T) Q.rc_tab[Q.rc_ntab++] = tabs[t];
         Q.rc_off = const_cast<uint32_t*>(T.off);
         Q.rc_count = const_cast<uint32_t*>(T.count);
         Q.win_list = reps;
         Q.total_windows = n_ent;
-        Q.chunk = 1;
+        // list chunks of up to 64 representatives: their parent lookups go out together
+        Q.chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, n_ent / (4ull * max_grid)));
         Q.win_counts = nullptr;
         Q.ebuf = static_cast<uint4*>(d_ebuf.p);
         Q.out = static_cast<fac_match*>(d_out.p);
@@ -2422,7 +2650,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         Q.spill = static_cast<uint64_t*>(d_spill.p);
         Q.spill_cap = spill_cap;
         Q.counters = static_cast<unsigned long long*>(d_cnt.p);
-        HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 5 * sizeof(unsigned long long), stream));
+        HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), stream));
         launch_rc_build(qbuild, std::min<uint32_t>(n_ent, max_grid), stream, Q);
         const hipError_t le = hipGetLastError();
         if (le != hipSuccess) {
@@ -2431,25 +2659,22 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         }
         return FAC_OK;
       };
-      int brc = build(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p), nullptr);
+      int brc = build(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p));
       if (brc) return brc;
-      if (n_ent2) {
-        brc = build(L2, n_ent2, static_cast<const uint64_t*>(d_rcrep2.p), &L1);
+      for (size_t x = 0; x < Lx.size(); ++x) {
+        brc = build(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[x].p));
         if (brc) return brc;
-        P.rc_tab[0] = L2;
-        P.rc_tab[1] = L1;
-        P.rc_ntab = 2;
-      } else {
-        P.rc_tab[0] = L1;
-        P.rc_ntab = 1;
+        tabs.push_back(Lx[x]);
       }
+      P.rc_ntab = 0;
+      for (size_t t = tabs.size(); t-- > 0;) P.rc_tab[P.rc_ntab++] = tabs[t];
       P.rc_mode = 1;
     }
     HIP_TRY(hipEventRecord(ev.b, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     HIP_TRY(hipEventElapsedTime(&cache_ms, ev.a, ev.b));
     if (P.rc_mode == 1 && std::getenv("FAC_RC_DEBUG")) {  // diagnostics: keys, pool use, cached entries
-      unsigned long long rcn[3] = {0, 0, 0};
+      unsigned long long rcn[2] = {0, 0};
       HIP_TRY(hipMemcpy(rcn, d_rcn.p, sizeof(rcn), hipMemcpyDeviceToHost));
       auto cached_of = [&](const RcTable& T, uint32_t ne, uint64_t& qsum) -> uint64_t {
         std::vector<uint32_t> cntv(ne);
@@ -2459,13 +2684,20 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
           if (v != EMPTY) ++c, qsum += v;
         return c;
       };
-      uint64_t q1 = 0, q2 = 0;
-      const uint64_t c1 = cached_of(L1, n_ent1, q1), c2 = n_ent2 ? cached_of(L2, n_ent2, q2) : 0;
-      std::fprintf(stderr,
-                   "FAC_RC windows=%llu L1 k=%u keys=%llu cached=%llu mean_queue=%.1f | L2 k=%u entries=%u cached=%llu "
-                   "mean_queue=%.1f | pool %.1f MB\n",
-                   (unsigned long long)windows, L1.k, rcn[0], (unsigned long long)c1, c1 ? (double)q1 / c1 : 0.0, L2.k,
-                   n_ent2, (unsigned long long)c2, c2 ? (double)q2 / c2 : 0.0, rcn[1] * 16.0 / 1e6);
+      uint64_t q1 = 0;
+      const uint64_t c1 = cached_of(L1, n_ent1, q1);
+      std::string lv;
+      for (size_t x = 0; x < Lx.size(); ++x) {
+        uint64_t q = 0;
+        const uint64_t c = cached_of(Lx[x], n_entx[x], q);
+        char b[160];
+        std::snprintf(b, sizeof(b), " | k=%u entries=%u cached=%llu mean_queue=%.1f", Lx[x].k, n_entx[x],
+                      (unsigned long long)c, c ? (double)q / c : 0.0);
+        lv += b;
+      }
+      std::fprintf(stderr, "FAC_RC windows=%llu L1 k=%u keys=%llu cached=%llu mean_queue=%.1f%s | pool %.1f MB\n",
+                   (unsigned long long)windows, L1.k, (unsigned long long)l1_keys, (unsigned long long)c1, c1 ? (double)q1 / c1 : 0.0,
+                   lv.c_str(), rcn[1] * 16.0 / 1e6);
     }
   }
   for (;;) {
@@ -2479,7 +2711,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     P.spill = static_cast<uint64_t*>(d_spill.p);
     P.spill_cap = spill_cap;
     P.counters = static_cast<unsigned long long*>(d_cnt.p);
-    HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 5 * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), stream));
     if (debug_poison()) HIP_TRY(hipMemsetAsync(d_out.p, 0xAB, out_cap * sizeof(fac_match), stream));
     HIP_TRY(hipEventRecord(ev.a, stream));
     const hipError_t le = launch_variant(kVariants[vi], grid, stream, P);
@@ -2489,7 +2721,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       break;
     }
     HIP_TRY(hipEventRecord(ev.b, stream));
-    HIP_TRY(hipMemcpyAsync(cnt, d_cnt.p, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(cnt, d_cnt.p, N_COUNTERS * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
@@ -2497,6 +2729,20 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     launches += 1;
     popped += cnt[1];
     cached_pops += cnt[4];
+    if (std::getenv("FAC_RC_DEBUG") && P.rc_mode == 1)
+      std::fprintf(stderr, "FAC_RC launch windows=%llu resumed=%llu lane_flushed=%llu popped=%llu\n",
+                   (unsigned long long)pass_windows, cnt[5], cnt[6], cnt[1]);
+#ifdef FAC_WIN_HIST
+    {
+      unsigned long long h[24];
+      HIP_TRY(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_hist), sizeof(h)));
+      for (int b = 0; b < 6; ++b)
+        std::fprintf(stderr, "FAC_HIST variant=%u,%u bucket=%d windows=%llu pops=%llu cycles=%llu resumed=%llu\n",
+                     kVariants[vi].vcap, kVariants[vi].qcap, b, h[b], h[6 + b], h[12 + b], h[18 + b]);
+      std::memset(h, 0, sizeof(h));
+      HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_hist), h, sizeof(h)));
+    }
+#endif
 #ifdef FAC_PHASE_PROF
     {
       unsigned long long pr[16];
