@@ -156,6 +156,11 @@ struct RcTable {
   const uint32_t* val;               // entry of each slot (EMPTY: not cached)
   const uint32_t* off;               // snapshot offset of each entry (pool words)
   const uint32_t* count;             // queued states of each entry (EMPTY: not cached)
+  // lookup table of the built entries (rc_publish_kernel): 32-byte slots {exact key: the k chars as
+  // 16-bit units, padded with 0xFFFF; snapshot offset, head, queue length | best entries << 16,
+  // occupied | dedup entries << 22 | pops}
+  const uint4* ct;
+  uint32_t ct_mask;                  // lookup slots - 1
 };
 
 constexpr int N_COUNTERS = 8;  // SearchParams::counters
@@ -237,6 +242,9 @@ struct SearchParams {
   unsigned long long rc_pool_cap;   // pool words (uint4)
   unsigned long long* rc_pool_used; // bump allocator
   uint32_t rc_pool_chunk;           // pool words a building wave takes at a time
+  uint32_t rc_qcap;                 // main pass ring: snapshots with more queued states are not resumed
+  uint4* rc_hits;                   // main pass: per window {offset | RC_DONE, head, tail, nv | ne << 16}
+  uint32_t* rc_hit_pops;            // ... and the snapshot's pops
   uint32_t* rc_off;                 // build: snapshot offset of each entry (pool words)
   uint32_t* rc_count;               // build: queued states of each entry (EMPTY: not cached)
   // multi-character mappings (search.rs:776-780, 883-922, 945-961; builder.rs:383-442). With
@@ -338,7 +346,7 @@ struct Engine {
   // per-engine device scratch of the search launcher, reused across calls by whichever call holds
   // scratch_mu (a concurrent call on the same engine allocates its own)
   mutable std::mutex scratch_mu;
-  static constexpr int kScratch = 32;
+  static constexpr int kScratch = 48;
   mutable void* scratch_p[kScratch] = {};
   mutable size_t scratch_n[kScratch] = {};
 };

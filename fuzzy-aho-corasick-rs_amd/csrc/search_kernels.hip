@@ -1485,13 +1485,27 @@ __device__ __forceinline__ bool rc_key(const SearchParams& P, const SegDesc& S, 
 }
 __device__ __forceinline__ uint32_t rc_hash(uint64_t k) { return (uint32_t)k ^ (uint32_t)(k >> 32); }
 constexpr uint32_t RC_PROBES = 32;
+constexpr uint32_t RC_OCC = 1u << 31, RC_POPS_MASK = (1u << 22) - 1;
+constexpr uint32_t RC_DONE = 0xFFFFFFFEu;  // rc_hits: window skipped or finished by its snapshot
+// exact lookup key: the first k chars as 16-bit units (0xFFFF pads; chars >= 0xFFFF are not encoded)
+__device__ __forceinline__ uint4 rc_exact_key(const uint32_t c[8], uint32_t k) {
+  uint32_t u[8];
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) u[i] = (i < k && c[i] != RC_PAD) ? (c[i] & 0xFFFFu) : 0xFFFFu;
+  return make_uint4(u[0] | (u[1] << 16), u[2] | (u[3] << 16), u[4] | (u[5] << 16), u[6] | (u[7] << 16));
+}
+__device__ __forceinline__ uint32_t rc_key_hash(uint4 k) {
+  uint64_t h = (((uint64_t)k.y << 32) | k.x) * 0x9E3779B97F4A7C15ull;
+  h ^= (((uint64_t)k.w << 32) | k.z) + 0x632BE59BD9B4E019ull + (h >> 29);
+  h *= 0xD6E8FEB86659FD93ull;
+  return (uint32_t)(h >> 32) ^ (uint32_t)h;
+}
 
 // A window's prefix-cache hit (snapshot header, read with the lookup): off = EMPTY on a miss.
 // Every level's probe chain (key slot, entry, snapshot count/offset) is issued together; the
 // deepest level whose snapshot header verifies the chars wins.
 #ifdef FAC_RC_SERIAL_LOOKUP
-template <uint32_t QCAP>
-__device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s) {
+__device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s, uint32_t QCAP) {
   for (uint32_t t = 0; t < P.rc_ntab; ++t) {
     const RcTable& T = P.rc_tab[t];
     RcChars ch;
@@ -1518,58 +1532,89 @@ __device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc&
   return RcHit{EMPTY, 0u, 0u, 0u, 0u};
 }
 #else
-template <uint32_t QCAP>
-__device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s) {
-  RcHit r{EMPTY, 0u, 0u, 0u, 0u};
+__device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s, uint32_t QCAP) {
   uint32_t kmax = 0;
   for (uint32_t t = 0; t < P.rc_ntab; ++t) kmax = max(kmax, P.rc_tab[t].k);
   uint32_t c[8];
   const bool ok = rc_chars(P, S, s, kmax, c);  // not cacheable past the halo at the deepest level:
-  uint64_t key[kRcLevels];                       // probe the levels whose keys stay inside it
-  uint32_t slot[kRcLevels];
-  unsigned long long kk[kRcLevels];
+  uint32_t enc = 8;                             // probe the levels whose keys stay inside it
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i)  // keys hold 16-bit units: a longer key would contain char i
+    if (enc == 8 && c[i] != RC_PAD && c[i] >= 0xFFFFu) enc = i;
   bool live[kRcLevels];
+  uint4 key[kRcLevels], val[kRcLevels];
+  uint32_t slot[kRcLevels];
 #pragma unroll
-  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {
+  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {  // every level's first probe in flight together
     const RcTable& T = P.rc_tab[t];
-    live[t] = t < P.rc_ntab && (ok || (s + T.k <= S.avail));
-    RcChars ch;
-    key[t] = rc_hash_chars(c, T.k, ch);
-    slot[t] = rc_hash(key[t]) & T.mask;
-    kk[t] = live[t] ? T.keys[slot[t]] : 0ull;
-  }
-  uint32_t ent[kRcLevels];
-#pragma unroll
-  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {
-    const RcTable& T = P.rc_tab[t];
-    for (uint32_t p = 1; live[t] && kk[t] != key[t] && kk[t] != 0ull && p < RC_PROBES; ++p) {  // rare
-      slot[t] = (slot[t] + 1) & T.mask;
-      kk[t] = T.keys[slot[t]];
+    live[t] = t < P.rc_ntab && T.k <= enc && (ok || s + T.k <= S.avail);
+    key[t] = rc_exact_key(c, T.k);
+    slot[t] = rc_key_hash(key[t]) & T.ct_mask;
+    if (live[t]) {
+      const uint4* e = T.ct + 2 * (size_t)slot[t];
+      key[t] = make_uint4(key[t].x ^ e[0].x, key[t].y ^ e[0].y, key[t].z ^ e[0].z, key[t].w ^ e[0].w);  // 0: match
+      val[t] = e[1];
     }
-    live[t] = live[t] && kk[t] == key[t];
-    ent[t] = live[t] ? T.val[slot[t]] : EMPTY;
   }
-  uint32_t cnt[kRcLevels], off[kRcLevels];
+  RcHit r{EMPTY, 0u, 0u, 0u, 0u};
+  bool found = false;
 #pragma unroll
-  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {
+  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {  // deepest first; collisions probe on (rare)
+    if (found || !live[t]) continue;
     const RcTable& T = P.rc_tab[t];
-    live[t] = live[t] && ent[t] != EMPTY;
-    cnt[t] = live[t] ? T.count[ent[t]] : EMPTY;
-    off[t] = live[t] ? T.off[ent[t]] : 0u;
-  }
-  for (uint32_t t = 0; t < P.rc_ntab; ++t) {  // deepest first; a failed verification (a 64-bit hash
-    if (cnt[t] == EMPTY || cnt[t] + 1u > QCAP) continue;  // collision) falls through
-    const uint32_t o = off[t];
-    RcChars ch;
-    (void)rc_hash_chars(c, P.rc_tab[t].k, ch);
-    const uint4 h0 = P.rc_pool[o], h1 = P.rc_pool[o + 1], sa = P.rc_pool[o + 2], sb = P.rc_pool[o + 3];
-    if (sa.x == ch.a.x && sa.y == ch.a.y && sa.z == ch.a.z && sa.w == ch.a.w && sb.x == ch.b.x && sb.y == ch.b.y &&
-        sb.z == ch.b.z && sb.w == ch.b.w)
-      return RcHit{o, h0.x, h0.y, h0.z | (h1.x << 16), h0.w};
+    bool hit = (val[t].w & RC_OCC) && !(key[t].x | key[t].y | key[t].z | key[t].w);
+    if (!hit && (val[t].w & RC_OCC)) {
+      const uint4 want = rc_exact_key(c, T.k);
+      for (uint32_t p = 1; p < RC_PROBES && !hit; ++p) {
+        slot[t] = (slot[t] + 1) & T.ct_mask;
+        const uint4* e = T.ct + 2 * (size_t)slot[t];
+        val[t] = e[1];
+        if (!(val[t].w & RC_OCC)) break;
+        const uint4 k2 = e[0];
+        hit = k2.x == want.x && k2.y == want.y && k2.z == want.z && k2.w == want.w;
+      }
+    }
+    const uint32_t nq = val[t].z & 0xFFFFu;
+    if (hit && nq + 1u <= QCAP) {
+      r = RcHit{val[t].x, val[t].y, val[t].y + nq, ((val[t].w >> 22) & 0x1FFu) | (val[t].z & 0xFFFF0000u),
+                val[t].w & RC_POPS_MASK};
+      found = true;
+    }
   }
   return r;
 }
 #endif
+
+// Lookup table of a built level: every entry with a snapshot is inserted under its exact key (the
+// chars from the snapshot header); keys holding a char >= 0xFFFF stay out (such windows resume
+// from a shorter key).
+__global__ __launch_bounds__(256) void rc_publish_kernel(const uint4* pool, const uint32_t* off, const uint32_t* count,
+                                                         uint32_t n_ent, uint32_t k, uint4* ct, uint32_t mask) {
+  for (uint32_t ent = blockIdx.x * blockDim.x + threadIdx.x; ent < n_ent; ent += gridDim.x * blockDim.x) {
+    if (count[ent] == EMPTY) continue;
+    const uint32_t o = off[ent];
+    const uint4 h0 = pool[o], h1 = pool[o + 1], sa = pool[o + 2], sb = pool[o + 3];
+    const uint32_t c[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+    bool enc = true;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) enc = enc && (i >= k || c[i] == RC_PAD || c[i] < 0xFFFFu);
+    if (!enc) continue;
+    const uint4 key = rc_exact_key(c, k);
+    const uint32_t nq = h0.y - h0.x;  // {head, tail, nv, pops}, {ne}
+    const uint4 val = make_uint4(o, h0.x, nq | (h1.x << 16), RC_OCC | (h0.z << 22) | min(h0.w, RC_POPS_MASK));
+    uint32_t slot = rc_key_hash(key) & mask;
+    for (uint32_t p = 0; p < RC_PROBES; ++p, slot = (slot + 1) & mask) {
+      uint4* e = ct + 2 * (size_t)slot;
+      if (atomicCAS(&e[1].w, 0u, val.w) == 0u) {  // read only by later launches
+        e[0] = key;
+        e[1].x = val.x;
+        e[1].y = val.y;
+        e[1].z = val.z;
+        break;
+      }
+    }
+  }
+}
 
 // Prefix-cache keys: every `stride`-th window's key is inserted and counted (level 1: every window,
 // sampled levels: a sample); the first inserter of a key is its representative. Counts saturate
@@ -1680,7 +1725,76 @@ __global__ __launch_bounds__(256) void rc_sel_assign_kernel(const unsigned long 
   }
 }
 
-template <uint32_t VCAP, uint32_t QCAP, bool MAP>
+// A resumed window whose snapshot has an empty queue is finished: the snapshot's best list is its
+// final best map. Each such lane writes its own window's records (one output atomic per wave);
+// returns true for them.
+__device__ __forceinline__ bool flush_final(const SearchParams& P, bool resumed, const RcHit& hit, uint32_t kl,
+                                            uint64_t start, uint64_t vid, uint64_t& cached_lane,
+                                            uint32_t& triv_lane) {
+  const bool triv = resumed && hit.tail == hit.head && P.rc_lane_flush;
+  if (!__ballot(triv)) return false;
+  const uint32_t ne = triv ? (hit.nv_nel >> 16) : 0u;
+  const uint32_t incl = wave_inclusive_sum(ne), tot = shfl_u32(incl, 63);
+  unsigned long long base = 0;
+  if (tot) {
+    if (lane_id() == 0) base = atomicAdd(P.counters, (unsigned long long)tot);
+    base = shfl_u64(base, 0);
+  }
+  if (triv) {
+    const SegDesc S = P.segs[kl];
+    const uint64_t sb = S.byte_base + local_byte(P, S, start);
+    const uint4* src = P.rc_pool + hit.off + RC_HDR + (hit.nv_nel & 0xFFFFu);  // best list (nq == 0)
+    for (uint32_t i = 0; i < ne; ++i) {
+      const uint64_t o = base + incl - ne + i;
+      if (o < P.out_cap) P.out[o] = match_record(P, S, start, sb, src[i]);
+    }
+    if (P.win_counts) P.win_counts[vid] = hit.tail;
+    cached_lane += hit.pops;
+    triv_lane += 1;
+  }
+  return triv;
+}
+
+// Per-window prefix-cache lookups of a main pass (P.rc_mode == 1), ahead of the search kernel:
+// windows that are skipped or finished by their snapshot are marked RC_DONE (the latter flushed
+// here); every other window's hit (or miss) is stored for the search kernel. Keeps the lookup's
+// registers out of the search kernel.
+__global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
+  const uint32_t lane = lane_id();
+  uint64_t cached_lane = 0;
+  uint32_t res_lane = 0, triv_lane = 0;
+  unsigned err = 0;
+  const uint64_t wstride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); v0 < P.total_windows; v0 += wstride) {
+    const uint64_t v = v0 + lane;  // whole waves iterate together (ballots, DPP scans)
+    bool active = v < P.total_windows;
+    uint32_t kl = 0;
+    uint64_t start = 0;
+    if (active) {
+      kl = find_seg(P, v);
+      const SegDesc S = P.segs[kl];
+      start = S.w_begin + (v - P.seg_prefix[kl]);
+      active = !window_skipped(P, S, start, err);
+    }
+    RcHit hit{EMPTY, 0u, 0u, 0u, 0u};
+    if (active) hit = rc_lookup(P, P.segs[kl], start, P.rc_qcap);
+    const bool resumed = active && hit.off != EMPTY;
+    res_lane += resumed ? 1u : 0u;
+    const bool fin = flush_final(P, resumed, hit, kl, start, v, cached_lane, triv_lane);
+    if (v < P.total_windows) {
+      P.rc_hits[v] = (active && !fin) ? make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel) : make_uint4(RC_DONE, 0u, 0u, 0u);
+      P.rc_hit_pops[v] = hit.pops;
+    }
+  }
+  if (cached_lane) atomicAdd(P.counters + 4, cached_lane);
+  if (res_lane) atomicAdd(P.counters + 5, (unsigned long long)res_lane);
+  if (triv_lane) atomicAdd(P.counters + 6, (unsigned long long)triv_lane);
+  if (err) atomicOr(reinterpret_cast<unsigned int*>(P.counters + 2), err);
+}
+
+// LK: the window prologue looks snapshots up itself (cache builds); otherwise a main pass with the
+// prefix cache reads the hits rc_lookup_kernel stored.
+template <uint32_t VCAP, uint32_t QCAP, bool MAP, bool LK>
 __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   __shared__ KState s_vis[VCAP ? VCAP : 1];
   __shared__ KState s_q[QCAP];
@@ -1714,43 +1828,26 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
       bool active = v < ce;
       uint32_t kl = 0;
       uint64_t start = 0, vid = 0;
+      RcHit hit{EMPTY, 0u, 0u, 0u, 0u};  // prefix-cache snapshot of this lane's window
       if (active) {
         vid = P.win_list ? P.win_list[v] : v;
         kl = find_seg(P, vid);
         const SegDesc S = P.segs[kl];
         start = S.w_begin + (vid - P.seg_prefix[kl]);
-        active = !window_skipped(P, S, start, err);
+        if (!LK && P.rc_mode == 1) {  // skip decision and lookup made by rc_lookup_kernel
+          const uint4 h = P.rc_hits[vid];
+          hit = RcHit{h.x, h.y, h.z, h.w, P.rc_hit_pops[vid]};
+          active = h.x != RC_DONE;
+        } else {
+          active = !window_skipped(P, S, start, err);
+        }
       }
-      RcHit hit{EMPTY, 0u, 0u, 0u, 0u};  // prefix-cache snapshot of this lane's window
-      if (P.rc_mode != 0 && P.rc_ntab && active) hit = rc_lookup<QCAP>(P, P.segs[kl], start);
-      if (P.rc_mode == 1) {
+      if constexpr (LK)
+        if (P.rc_mode != 0 && P.rc_ntab && active) hit = rc_lookup(P, P.segs[kl], start, QCAP);
+      if (LK && P.rc_mode == 1) {
         const bool resumed = active && hit.off != EMPTY;
         res_lane += resumed ? 1u : 0u;
-        // a snapshot with an empty queue is the window's final best map (no pop is left): each lane
-        // writes its own window's records instead of the wave walking the window
-        const bool triv = resumed && hit.tail == hit.head && P.rc_lane_flush;
-        if (__ballot(triv)) {
-          const uint32_t ne = triv ? (hit.nv_nel >> 16) : 0u;
-          const uint32_t incl = wave_inclusive_sum(ne), tot = shfl_u32(incl, 63);
-          unsigned long long base = 0;
-          if (tot) {
-            if (lane == 0) base = atomicAdd(P.counters, (unsigned long long)tot);
-            base = shfl_u64(base, 0);
-          }
-          if (triv) {
-            const SegDesc S = P.segs[kl];
-            const uint64_t sb = S.byte_base + local_byte(P, S, start);
-            const uint4* src = P.rc_pool + hit.off + RC_HDR + (hit.nv_nel & 0xFFFFu);  // best list (nq == 0)
-            for (uint32_t i = 0; i < ne; ++i) {
-              const uint64_t o = base + incl - ne + i;
-              if (o < P.out_cap) P.out[o] = match_record(P, S, start, sb, src[i]);
-            }
-            if (P.win_counts) P.win_counts[vid] = hit.tail;
-            cached_lane += hit.pops;
-            triv_lane += 1;
-          }
-          active = active && !triv;
-        }
+        active = active && !flush_final(P, resumed, hit, kl, start, vid, cached_lane, triv_lane);
       }
       if (P.rc_mode == 2) {
         // a representative whose parent snapshot has an empty queue ends at the parent: its own
@@ -1883,20 +1980,20 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
 #define FAC_BEAM_WAVES 3
 #endif
 template <uint32_t VCAP, uint32_t QCAP, bool MAP>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((FAC_BEAM_WAVES && VCAP <= 512 && QCAP <= 256) ? FAC_BEAM_WAVES : 1)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((FAC_BEAM_WAVES && VCAP <= 512 && QCAP <= 256) ? (VCAP <= 256 ? FAC_BEAM_WAVES + 1 : FAC_BEAM_WAVES) : 1)))
 void bfs_window_kernel(SearchParams P) {
-  bfs_window_body<VCAP, QCAP, MAP>(P);
+  bfs_window_body<VCAP, QCAP, MAP, false>(P);
 }
 template <uint32_t QCAP, bool MAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QCAP <= 512 ? 4 : 1))) void bfs_window_kernel_nd(SearchParams P) {
-  bfs_window_body<0, QCAP, MAP>(P);
+  bfs_window_body<0, QCAP, MAP, false>(P);
 }
 // prefix-cache build (P.rc_mode == 2): one representative window per key, popped up to the first
 // state past the key; its own symbol so profiles separate it from the search launches
 template <uint32_t QCAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((FAC_BEAM_WAVES && QCAP <= 256) ? FAC_BEAM_WAVES : 1)))
 void rc_build_kernel(SearchParams P) {
-  bfs_window_body<512, QCAP, false>(P);  // the prefix cache is off with mappings
+  bfs_window_body<512, QCAP, false, true>(P);  // the prefix cache is off with mappings
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2438,13 +2535,18 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   DevBuf d_rck, d_rcv, d_rcslot, d_rcb, d_rcrep, d_rcs, d_rcc, d_rcn;  // prefix cache, level 1 + pool
   DevBuf d_xk[kRcLevels - 1], d_xv[kRcLevels - 1], d_xslot[kRcLevels - 1], d_xrep[kRcLevels - 1],
       d_xc[kRcLevels - 1];  // prefix cache, sampled levels
+  DevBuf d_ct[kRcLevels];  // prefix cache lookup tables
+  DevBuf d_hits, d_hitp;   // per-window lookups of the main pass
   std::unique_lock<std::mutex> lease(e.scratch_mu, std::try_to_lock);
   if (lease.owns_lock()) {  // reuse the engine's scratch (no per-call hipMalloc of the 64 MB lists)
     std::vector<DevBuf*> bufs = {&d_segs, &d_prefix, &d_out, &d_ebuf, &d_cnt, &d_list, &d_spill,
                                  &d_rck,  &d_rcv,    &d_rcslot, &d_rcb, &d_rcrep, &d_rcs, &d_rcc, &d_rcn};
     for (int x = 0; x < kRcLevels - 1; ++x)
       for (DevBuf* b : {&d_xk[x], &d_xv[x], &d_xslot[x], &d_xrep[x], &d_xc[x]}) bufs.push_back(b);
-    static_assert(Engine::kScratch >= 15 + 5 * (kRcLevels - 1), "engine scratch slots");
+    for (int x = 0; x < kRcLevels; ++x) bufs.push_back(&d_ct[x]);
+    bufs.push_back(&d_hits);
+    bufs.push_back(&d_hitp);
+    static_assert(Engine::kScratch >= 17 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
     for (size_t i = 0; i < bufs.size(); ++i) bufs[i]->bind(&e.scratch_p[i], &e.scratch_n[i]);
   }
   HIP_TRY(d_segs.alloc(segs.size() * sizeof(SegDesc), stream));
@@ -2486,6 +2588,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   // A window resumes from the deepest snapshot its prefix has. Skipped when the root emits (an empty
   // pattern), with mappings (whole-grapheme keys), or when the search is small.
   P.rc_mode = 0;
+  P.rc_hits = nullptr;
+  P.rc_hit_pops = nullptr;
   P.rc_ntab = 0;
   P.rc_lane_flush = std::getenv("FAC_RC_NO_LANE") ? 0 : 1;
   P.dyn_chunks = std::getenv("FAC_STATIC_GRID") ? 0 : 1;
@@ -2659,11 +2763,29 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         }
         return FAC_OK;
       };
+      // after its build a level's entries are published into an exact-key lookup table (4 slots per
+      // entry: a miss usually ends at the first probe)
+      auto publish = [&](RcTable& T, uint32_t n_ent, DevBuf& ct) -> int {
+        uint32_t cs = 1u << 12;
+        while (cs < 4ull * n_ent && cs < (1u << 28)) cs <<= 1;
+        HIP_TRY(ct.alloc((size_t)cs * 2 * sizeof(uint4), stream));
+        HIP_TRY(hipMemsetAsync(ct.p, 0, (size_t)cs * 2 * sizeof(uint4), stream));
+        hipLaunchKernelGGL(rc_publish_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_ent + 255) / 256, cus * 8))),
+                           dim3(256), 0, stream, static_cast<const uint4*>(P.rc_pool), T.off, T.count, n_ent, T.k,
+                           static_cast<uint4*>(ct.p), cs - 1);
+        HIP_TRY(hipGetLastError());
+        T.ct = static_cast<const uint4*>(ct.p);
+        T.ct_mask = cs - 1;
+        return FAC_OK;
+      };
       int brc = build(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p));
       if (brc) return brc;
+      if ((brc = publish(L1, n_ent1, d_ct[0]))) return brc;
+      tabs[0] = L1;
       for (size_t x = 0; x < Lx.size(); ++x) {
         brc = build(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[x].p));
         if (brc) return brc;
+        if ((brc = publish(Lx[x], n_entx[x], d_ct[1 + x]))) return brc;
         tabs.push_back(Lx[x]);
       }
       P.rc_ntab = 0;
@@ -2713,6 +2835,22 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     P.counters = static_cast<unsigned long long*>(d_cnt.p);
     HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), stream));
     if (debug_poison()) HIP_TRY(hipMemsetAsync(d_out.p, 0xAB, out_cap * sizeof(fac_match), stream));
+    if (P.rc_mode == 1 && !P.win_list) {  // every window's lookup (+ flush of finished windows) first
+      HIP_TRY(d_hits.alloc(windows * sizeof(uint4), stream));
+      HIP_TRY(d_hitp.alloc(windows * sizeof(uint32_t), stream));
+      P.rc_hits = static_cast<uint4*>(d_hits.p);
+      P.rc_hit_pops = static_cast<uint32_t*>(d_hitp.p);
+      P.rc_qcap = kVariants[vi].qcap;
+      HIP_TRY(hipEventRecord(ev.a, stream));
+      hipLaunchKernelGGL(rc_lookup_kernel, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256, (uint64_t)cus * 16))),
+                         dim3(256), 0, stream, P);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(ev.b, stream));
+      HIP_TRY(hipEventSynchronize(ev.b));
+      float lms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&lms, ev.a, ev.b));
+      cache_ms += lms;
+    }
     HIP_TRY(hipEventRecord(ev.a, stream));
     const hipError_t le = launch_variant(kVariants[vi], grid, stream, P);
     if (le != hipSuccess) {

@@ -131,7 +131,7 @@ typedef struct fac_stats {
   uint64_t graphemes;      /* haystack graphemes */
   uint64_t bytes;          /* haystack UTF-8 bytes */
   uint64_t retries;        /* capacity retries */
-  double cache_ms;         /* HIP-event time of the prefix-cache build (key collection + snapshots) */
+  double cache_ms;         /* HIP-event time of the prefix cache: key counts, snapshot builds, per-window lookups */
   uint64_t states_cached;  /* pops replayed from prefix-cache snapshots (not in states_popped) */
 } fac_stats;
 
