@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -2416,6 +2417,9 @@ int ensure_gids(const Engine& e, const Haystack& h, std::string& err) {
 int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs_in, float thr,
                 hipStream_t stream, uint32_t beam, bool exact_dedup, std::vector<uint32_t>* counts,
                 std::vector<fac_match>& out, fac_stats* stats, std::string& err) {
+  const auto t_begin = std::chrono::steady_clock::now();
+  auto host_ms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count(); };
+  const bool timing = std::getenv("FAC_TIMING") != nullptr;  // diagnostics: host wall-clock phases
   out.clear();
   HIP_TRY(hipSetDevice(e.device));
   if (!stream) stream = e.stream;
@@ -2822,6 +2826,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
                    lv.c_str(), rcn[1] * 16.0 / 1e6);
     }
   }
+  const double t_cache = host_ms();
+  double t_dev = 0.0;
   for (;;) {
     P.chunk = P.win_list ? 1u : 256u;  // spilled windows are few and heavy: one per block turn
     P.total_windows = pass_windows;
@@ -2923,6 +2929,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       ++retries;
       continue;
     }
+    t_dev = host_ms();
     const size_t have = out.size();
     out.resize(have + cnt[0]);
     if (cnt[0]) HIP_TRY(hipMemcpyAsync(out.data() + have, d_out.p, cnt[0] * sizeof(fac_match), hipMemcpyDeviceToHost, stream));
@@ -2948,6 +2955,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     P.win_list = static_cast<const uint64_t*>(d_list.p);
     ++retries;
   }
+  if (timing)
+    std::fprintf(stderr, "FAC_TIMING setup+cache %.2f ms, search %.2f ms, records D2H %.2f ms (host wall clock)\n", t_cache,
+                 t_dev - t_cache, host_ms() - t_dev);
   if (counts && rc == FAC_OK) {
     counts->resize(windows);
     HIP_TRY(hipMemcpyAsync(counts->data(), d_counts.p, windows * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));

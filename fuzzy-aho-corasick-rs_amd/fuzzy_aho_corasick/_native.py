@@ -151,16 +151,18 @@ def grapheme_starts(data: bytes):
 
 
 def take_records(ptr, n):
-    """Copy a library-allocated fac_match array into a NumPy structured array (32 B records, no
-    per-record Python objects) and free it."""
+    """Hand a library-allocated fac_match array to NumPy without a copy: a structured array of 32 B
+    records (no per-record Python objects) viewing the library buffer, which is freed with
+    fac_matches_free when the last view of it goes away."""
     import numpy as np
-    try:
-        if n == 0:
-            return np.zeros(0, dtype=MATCH_DTYPE)
-        raw = ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8))
-        return np.ctypeslib.as_array(raw, shape=(n * 32,)).view(MATCH_DTYPE).copy()
-    finally:
+    import weakref
+    if n == 0:
         lib.fac_matches_free(ptr)
+        return np.zeros(0, dtype=MATCH_DTYPE)
+    addr = ctypes.cast(ptr, ctypes.c_void_p).value
+    buf = (ctypes.c_uint8 * (n * 32)).from_address(addr)
+    weakref.finalize(buf, lib.fac_matches_free, ctypes.cast(addr, ctypes.POINTER(fac_match)))
+    return np.frombuffer(buf, dtype=MATCH_DTYPE)
 
 
 def take_matches(ptr, n):

@@ -4,9 +4,13 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
+import time
 from typing import Iterable, List, Optional, Tuple
 
 from . import _native
+
+_TIMING = bool(os.environ.get("FAC_TIMING"))  # diagnostics: host-side phase times
 from .matches import FuzzyMatch, FuzzyMatches
 from .structs import (DeviceError, FuzzyLimits, FuzzyPenalties, HaystackTooLarge, Order, Overlap,
                       Pattern, SearchOptions, Similarity, UnsupportedConfiguration, f32)
@@ -428,12 +432,18 @@ class StagedHaystack:
         out = ctypes.POINTER(_native.fac_match)()
         n = ctypes.c_uint64()
         st = _native.fac_stats()
+        t0 = time.perf_counter()
         rc = _native.lib.fac_search_staged(self.engine._h, self._h, window_begin, window_end, f32(threshold),
                                            ctypes.c_void_p(stream or 0), ctypes.byref(out), ctypes.byref(n),
                                            ctypes.byref(st))
         if rc:
             _raise(rc)
-        return _native.take_records(out, n.value), st
+        t1 = time.perf_counter()
+        rows = _native.take_records(out, n.value)
+        if _TIMING:
+            print(f"FAC_TIMING native call {1e3 * (t1 - t0):.2f} ms, records to NumPy {1e3 * (time.perf_counter() - t1):.2f} ms",
+                  file=sys.stderr)
+        return rows, st
 
     def search_prefiltered_records(self, threshold: float, stream=None):
         out = ctypes.POINTER(_native.fac_match)()
