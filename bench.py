@@ -81,12 +81,15 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     kernel_ms, launches, matches, popped, prefilter_ms, cache_ms, cached = 0.0, 0, 0, 0, 0.0, 0.0, 0
+    lane_ms, lane_windows = 0.0, 0
     for _ in range(args.steps):
         rows, st = step()
         prefilter_ms += st.prefilter_ms
         cache_ms += st.cache_ms
         cached += st.states_cached
         kernel_ms += st.kernel_ms
+        lane_ms += st.lane_ms
+        lane_windows += st.lane_windows
         launches += st.kernel_launches
         matches += len(rows)
         popped += st.states_popped
@@ -105,9 +108,11 @@ def main():
         total_graphemes = graphemes * args.steps
 
     value = total_graphemes / elapsed / 1e9
-    avg_kernel_s = kernel_ms / max(1, launches) / 1e3
+    # the search proper: the wave kernel's launches plus the lane-serial kernel that takes the small
+    # resumed windows off it (one launch per step when the prefix cache is on)
+    avg_kernel_s = (kernel_ms + lane_ms) / max(1, launches) / 1e3
     bytes_per_launch = len(wl.haystack) + 32 * (matches / max(1, args.steps))
-    kernel_name = "bfs_window_kernel"
+    kernel_name = "bfs_window_kernel + lane_window_kernel" if lane_ms > 0 else "bfs_window_kernel"
     if prefilter_ms > kernel_ms:  # C5: the bitap scan dominates; 1 B/char in
         kernel_name = "bitap_kernel (+transcode, runs)"
         avg_kernel_s = prefilter_ms / max(1, args.steps) / 1e3
@@ -172,6 +177,8 @@ def main():
                 "states_per_second": popped / max(1e-9, kernel_ms / 1e3),
                 "kernel_launches": launches,
                 "search_kernel_ms_per_step": kernel_ms / max(1, args.steps),
+                "lane_kernel_ms_per_step": lane_ms / max(1, args.steps),
+                "lane_windows_per_step": lane_windows / max(1, args.steps),
                 "prefilter_ms_per_step": prefilter_ms / max(1, args.steps),
                 "prefix_cache_ms_per_step": cache_ms / max(1, args.steps),
                 "states_from_prefix_cache_per_step": cached / max(1, args.steps),

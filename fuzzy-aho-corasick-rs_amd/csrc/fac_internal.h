@@ -163,7 +163,7 @@ struct RcTable {
   uint32_t ct_mask;                  // lookup slots - 1
 };
 
-constexpr int N_COUNTERS = 8;  // SearchParams::counters
+constexpr int N_COUNTERS = 10;  // SearchParams::counters (8: lane-searched windows, 9: lane work counter)
 constexpr int kRcLevels = 4;   // prefix-cache levels: level 1 + up to 3 sampled levels
 
 struct SearchParams {
@@ -220,6 +220,8 @@ struct SearchParams {
                                  // [7] next window chunk (dynamic chunk hand-out)
   int32_t rc_lane_flush;         // resumed windows with an empty queue are flushed lane-parallel
   int32_t dyn_chunks;            // 1: chunks from the work counter; 0: static grid-stride
+  uint32_t lane_popmax;           // lane_window_kernel: pops after which a window goes back to the wave kernel
+  int32_t lane_debug;             // lane_window_kernel: diagnostics counters (FAC_RC_DEBUG)
   // window list mode (re-run of spilled windows) and the spill list of capacity overflows
   const uint64_t* win_list;  // null: virtual windows 0..total_windows; else list of virtual ids
   uint64_t* spill;           // virtual ids of windows that overflowed this variant's LDS frontier

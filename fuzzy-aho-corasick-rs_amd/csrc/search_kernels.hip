@@ -1620,8 +1620,13 @@ __global__ __launch_bounds__(256) void rc_publish_kernel(const uint4* pool, cons
 // Prefix-cache keys: every `stride`-th window's key is inserted and counted (level 1: every window,
 // sampled levels: a sample); the first inserter of a key is its representative. Counts saturate
 // at `sat` (only "at least thr" is asked), so a frequent key is not one hot atomic per window.
+// `seen` (optional, sampled levels): a bitmap of key hashes; a key's first sighting only sets its bit,
+// so keys seen once (most long keys) never reach the table and the table is sized for repeated keys
+// (a count of c then means c + 1 sightings; bitmap collisions only admit a few singletons). A key
+// that finds no slot within `probes` stays uncounted (not cached).
 __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, unsigned long long* keys, uint32_t* cnt,
-                                                       uint64_t* rep, uint32_t mask, uint32_t stride, uint32_t sat) {
+                                                       uint64_t* rep, uint32_t mask, uint32_t stride, uint32_t sat,
+                                                       uint32_t* seen, uint32_t seen_mask, uint32_t probes) {
   const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
   unsigned err = 0;
   const uint64_t ns = (P.total_windows + stride - 1) / stride;
@@ -1634,8 +1639,12 @@ __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, unsigned 
     RcChars ch;
     uint64_t k;
     if (!rc_key(P, S, start, P.rc_k, ch, k)) continue;
+    if (seen) {
+      const uint32_t b = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 32) & seen_mask;
+      if (!(atomicOr(&seen[b >> 5], 1u << (b & 31u)) & (1u << (b & 31u)))) continue;  // first sighting
+    }
     const uint32_t h = rc_hash(k);
-    for (uint32_t p = 0; p < RC_PROBES; ++p) {
+    for (uint32_t p = 0; p < probes; ++p) {
       const uint32_t slot = (h + p) & mask;
       unsigned long long kk = keys[slot];
       if (kk == 0ull) {
@@ -1791,6 +1800,254 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
   if (res_lane) atomicAdd(P.counters + 5, (unsigned long long)res_lane);
   if (triv_lane) atomicAdd(P.counters + 6, (unsigned long long)triv_lane);
   if (err) atomicOr(reinterpret_cast<unsigned int*>(P.counters + 2), err);
+}
+
+// ---- Lane-serial search of small resumed windows ----
+// After the prefix-cache lookups most unfinished windows need only a handful of pops, for which
+// run_window spends a window prologue and whole 64-lane batches holding a few states. Here every
+// lane runs one such window alone, in the reference's sequential order (search.rs:560-1089, the
+// oracle's Searcher::run), resumed from its snapshot: the queue ring and the best list live in LDS
+// (slot i of lane l at i * 64 + l). There is no dedup table: without a beam, dedup cannot change
+// results, and a queue run without dedup is never shorter than the dedup queue at
+// the same pop (every state it adds over the dedup run is pushed before it is popped), so a window
+// whose dedup-free pending count never exceeds 2·beam never beams. A window that would (or that
+// overflows the ring or the best list, reads past the resident halo, or exceeds the pop budget) is
+// left to the wave kernel, which restarts it from its snapshot; finished windows write their
+// records and are marked RC_DONE.
+constexpr uint32_t LANE_RUN = 1u, LANE_OK = 2u, LANE_BAIL = 3u;
+constexpr uint32_t LANE_CHUNK = 4096;
+__device__ unsigned long long g_lane_dbg[8];  // diagnostics (FAC_RC_DEBUG): taken, finished, bailed, lane runs
+__device__ __forceinline__ int64_t lane_goto(const SearchParams& P, const DevNode& nd, uint32_t ch) {
+  const uint32_t ee = node_end(nd);
+  for (uint32_t e = nd.edge_begin; e < ee; ++e) {  // find_transition_char_no_mappings (structs.rs:512-519)
+    const DevEdge ed = P.edges[e];
+    if (ed.ch == ch) return (int64_t)(ed.next & EDGE_NEXT_MASK);
+  }
+  return -1;
+}
+template <uint32_t QL, uint32_t ELN>
+__device__ void lane_run_window(const SearchParams& P, uint4* s_q, uint4* s_e, uint64_t vid, bool have,
+                                uint64_t& popped_lane, uint64_t& cached_lane, uint32_t& done_lane) {
+  const uint32_t lane = lane_id();
+  uint32_t status = have ? LANE_RUN : 0u;
+  uint32_t head = 0, tail = 0, nel = 0, pops = 0, snap_pops = 0;
+  uint64_t start = 0;
+  SegDesc S{};
+  if (have) {
+    const uint4 h = P.rc_hits[vid];
+    snap_pops = P.rc_hit_pops[vid];
+    const uint32_t kl = find_seg(P, vid);
+    S = P.segs[kl];
+    start = S.w_begin + (vid - P.seg_prefix[kl]);
+    const uint32_t nq = h.z - h.y, nv = h.w & 0xFFFFu;
+    nel = h.w >> 16;
+    const uint4* src = P.rc_pool + h.x + RC_HDR;  // queue, dedup entries (unused), best list
+    for (uint32_t i = 0; i < nq; ++i) s_q[i * 64 + lane] = src[i];
+    for (uint32_t i = 0; i < nel; ++i) s_e[i * 64 + lane] = src[nq + nv + i];
+    tail = nq;
+  }
+  const bool fast = P.mef != 255u;
+  unsigned err = 0;
+  uint32_t trips = 0;
+  const uint64_t t_run0 = __builtin_amdgcn_s_memtime();
+  while (__ballot(status == LANE_RUN)) {
+    ++trips;
+    if (status != LANE_RUN) continue;
+    if (head == tail) {
+      status = LANE_OK;
+      continue;
+    }
+    if ((P.beam && tail - head > 2u * P.beam) || pops >= P.lane_popmax) {  // the beam could trigger (:577)
+      status = LANE_BAIL;
+      continue;
+    }
+    const uint4 w = s_q[(head % QL) * 64 + lane];
+    ++head;
+    ++pops;
+    const KState st{w.x, w.y, __uint_as_float(w.z), w.w};
+    const DevNode nd = P.nodes[st.node];
+    if (st.pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr))) continue;  // :638-642
+    const uint32_t packed = st.packed, edits = edits_of(packed);
+    const uint32_t j_rel = st.jm & 0xFFFFu, me_rel = st.jm >> 16;
+    if (node_has_out(nd)) {  // emission (:659-737) into the best list, first-found ties
+      const uint2 orr = P.out_range[st.node];
+      const uint32_t ins = packed & 0xFFu, del = (packed >> 8) & 0xFFu, sub = (packed >> 16) & 0xFFu, swp = packed >> 24;
+      for (uint32_t i = orr.x; i < orr.y && status == LANE_RUN; ++i) {
+        const uint32_t p = P.out_pat[i];
+        const DevPattern pt = P.pats[p];
+        bool ok;
+        if (fast) {
+          ok = edits <= P.mef;
+        } else {  // within_limits (:151-169)
+          const Lim m = pick_limits(P, pt.has_limits ? (int32_t)p : -1);
+          ok = m.has ? (lim_le(m.l.edits, edits) && lim_le(m.l.ins, ins) && lim_le(m.l.del, del) &&
+                        lim_le(m.l.sub, sub) && lim_le(m.l.swp, swp))
+                     : (edits == 0);
+        }
+        if (!ok) continue;
+        const float sim = __fmul_rn(__fdiv_rn(__fsub_rn(pt.glen, st.pen), pt.glen), pt.weight);  // :696-699
+        if (sim < P.thr) continue;                                                              // :701
+        uint32_t at = nel;
+        for (uint32_t k = 0; k < nel; ++k) {
+          const uint4 e = s_e[k * 64 + lane];
+          if (e.x == me_rel && e.y == p) {
+            at = k;
+            if (sim > __uint_as_float(e.z)) s_e[k * 64 + lane] = make_uint4(me_rel, p, __float_as_uint(sim), packed);
+            break;
+          }
+        }
+        if (at == nel) {
+          if (nel == ELN) status = LANE_BAIL;
+          else s_e[(nel++) * 64 + lane] = make_uint4(me_rel, p, __float_as_uint(sim), packed);
+        }
+      }
+      if (status != LANE_RUN) continue;
+    }
+    const uint64_t j = start + j_rel;
+    uint32_t c0 = 0, c1 = 0;
+    if (j < S.n) c0 = text_char(P, S, j, err);
+    if (j + 1 < S.n) c1 = text_char(P, S, j + 1, err);
+    if (err) {
+      status = LANE_BAIL;
+      continue;
+    }
+    const Prep pr = lane_prep(P, S, st, nd, start, c0, c1, nd.sb);
+    auto push = [&](uint32_t node, uint32_t jm, float pen, uint32_t pk) {
+      if (tail - head >= QL) {
+        status = LANE_BAIL;
+        return false;
+      }
+      s_q[(tail % QL) * 64 + lane] = make_uint4(node, jm, __float_as_uint(pen), pk);
+      ++tail;
+      return true;
+    };
+    const uint32_t eb = nd.edge_begin, ee = node_end(nd);
+    const uint32_t j1 = j_rel + 1u, jm1 = j1 | (j1 << 16);
+    int64_t ex = -1;
+    if (pr.flags & PF_EX) {  // exact (:776-800)
+      ex = lane_goto(P, nd, pr.cur_ch);
+      if (ex >= 0 && !push((uint32_t)ex, jm1, st.pen, packed)) continue;
+    }
+    if (pr.flags & PF_SUB) {  // substitutions (:803-874), edge order, the exact edge excluded
+      bool ok = true;
+      for (uint32_t e = eb; e < ee && ok; ++e) {
+        const DevEdge ed = P.edges[e];
+        const uint32_t child = ed.next & EDGE_NEXT_MASK;
+        if (ex >= 0 && child == (uint32_t)ex) continue;
+        const float sim = similarity(P, ed.ch, pr.cur_ch);
+        if (sim < P.min_sym) continue;
+        const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
+        if (penalty > pr.remaining) continue;
+        if ((pr.flags & PF_LAST) && !(ed.next & EDGE_CHILD_OUTPUT) &&
+            (!(pr.flags & PF_NEXT) || !sb_has(P, child, pr.next_ch)))
+          continue;
+        ok = push(child, jm1, __fadd_rn(st.pen, penalty), packed + 0x10000u);
+      }
+      if (!ok) continue;
+    }
+    if (pr.flags & PF_SWAP) {  // swap (:935-989): goto(goto(node, text[j+1]), text[j])
+      const int64_t x = lane_goto(P, nd, pr.nch);
+      int64_t node2 = -1;
+      if (x >= 0) node2 = lane_goto(P, P.nodes[(uint32_t)x], pr.cur_ch);
+      if (node2 >= 0 && !fast) {  // within_limits_swap_ahead with node2's limits (:962-967)
+        const Lim m = pick_limits(P, node_limits(P, (uint32_t)node2));
+        if (!(m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.swp, packed >> 24)) : false)) node2 = -1;
+      }
+      const uint32_t j2 = j_rel + 2u;
+      if (node2 >= 0 && !push((uint32_t)node2, j2 | (j2 << 16), __fadd_rn(st.pen, P.p_swp), packed + 0x1000000u)) continue;
+    }
+    if ((pr.flags & PF_INS) && !push(st.node, j1 | (me_rel << 16), __fadd_rn(st.pen, P.p_ins), packed + 1u)) continue;  // :994-1029
+    if (pr.flags & PF_DEL) {  // deletions (:1035-1089), edge order
+      const float npen = __fadd_rn(st.pen, P.p_del);
+      bool ok = true;
+      for (uint32_t e = eb; e < ee && ok; ++e) {
+        const DevEdge ed = P.edges[e];
+        const uint32_t child = ed.next & EDGE_NEXT_MASK;
+        if ((pr.flags & PF_LAST) && !(ed.next & EDGE_CHILD_OUTPUT) &&
+            (!(pr.flags & PF_CUR) || !sb_has(P, child, pr.cur_ch)))
+          continue;
+        ok = push(child, st.jm, npen, packed + 0x100u);
+      }
+    }
+  }
+  popped_lane += pops;
+  const bool fin = status == LANE_OK;
+  {
+    const uint64_t t_run1 = __builtin_amdgcn_s_memtime();
+    const uint32_t n_have = (uint32_t)__popcll(__ballot(have)), n_fin = (uint32_t)__popcll(__ballot(fin));
+    if (P.lane_debug && lane == 0) {  // diagnostics (FAC_RC_DEBUG), one set of atomics per wave round
+      atomicAdd(&g_lane_dbg[0], (unsigned long long)n_have);
+      atomicAdd(&g_lane_dbg[1], (unsigned long long)n_fin);
+      atomicAdd(&g_lane_dbg[2], (unsigned long long)(n_have - n_fin));
+      atomicAdd(&g_lane_dbg[4], (unsigned long long)trips);
+      atomicAdd(&g_lane_dbg[5], t_run1 - t_run0);
+      atomicAdd(&g_lane_dbg[7], 1ull);
+    }
+  }
+  const uint32_t ne = fin ? nel : 0u;
+  const uint32_t incl = wave_inclusive_sum(ne), tot = shfl_u32(incl, 63);
+  unsigned long long base = 0;
+  if (tot) {
+    if (lane == 0) base = atomicAdd(P.counters, (unsigned long long)tot);
+    base = shfl_u64(base, 0);
+  }
+  if (fin) {
+    const uint64_t sb = S.byte_base + local_byte(P, S, start);
+    for (uint32_t i = 0; i < ne; ++i) {
+      const uint64_t o = base + incl - ne + i;
+      if (o < P.out_cap) P.out[o] = match_record(P, S, start, sb, s_e[i * 64 + lane]);
+    }
+    P.rc_hits[vid] = make_uint4(RC_DONE, 0u, 0u, 0u);
+    cached_lane += snap_pops;
+    done_lane += 1;
+  }
+}
+
+template <uint32_t QL, uint32_t ELN>
+__global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
+  __shared__ uint4 s_q[QL * 64];
+  __shared__ uint4 s_e[ELN * 64];
+  __shared__ uint64_t s_list[128];
+  const uint32_t lane = lane_id();
+  uint64_t popped_lane = 0, cached_lane = 0;
+  uint32_t done_lane = 0, nbuf = 0;  // nbuf: wave-uniform
+  const uint64_t t_k0 = __builtin_amdgcn_s_memtime();
+  for (;;) {
+    unsigned long long c = 0;
+    if (lane == 0) c = atomicAdd(P.counters + 9, (unsigned long long)LANE_CHUNK);
+    const uint64_t cb = shfl_u64(c, 0);
+    if (cb >= P.total_windows) break;
+    const uint64_t ce = min(cb + (uint64_t)LANE_CHUNK, P.total_windows);
+    for (uint64_t v0 = cb; v0 < ce; v0 += 64) {
+      const uint64_t v = v0 + lane;
+      bool take = false;
+      if (v < ce) {  // unfinished resumed windows whose snapshot fits the lane's ring and best list
+        const uint4 h = P.rc_hits[v];
+        take = h.x != RC_DONE && h.x != EMPTY && h.z - h.y <= QL && (h.w >> 16) <= ELN;
+      }
+      const uint64_t m = __ballot(take);
+      if (take) s_list[nbuf + prefix_below(m)] = v;
+      nbuf += (uint32_t)__popcll(m);
+      __builtin_amdgcn_wave_barrier();
+      if (nbuf >= 64) {
+        const uint64_t vid = s_list[lane];
+        const uint64_t rest = lane + 64 < nbuf ? s_list[lane + 64] : 0ull;
+        __builtin_amdgcn_wave_barrier();
+        if (lane + 64 < nbuf) s_list[lane] = rest;
+        nbuf -= 64;
+        __builtin_amdgcn_wave_barrier();
+        lane_run_window<QL, ELN>(P, s_q, s_e, vid, true, popped_lane, cached_lane, done_lane);
+      }
+    }
+  }
+  if (nbuf) {
+    const uint64_t vid = lane < nbuf ? s_list[lane] : 0ull;
+    lane_run_window<QL, ELN>(P, s_q, s_e, vid, lane < nbuf, popped_lane, cached_lane, done_lane);
+  }
+  if (popped_lane) atomicAdd(P.counters + 1, popped_lane);
+  if (cached_lane) atomicAdd(P.counters + 4, cached_lane);
+  if (done_lane) atomicAdd(P.counters + 8, (unsigned long long)done_lane);
+  if (P.lane_debug && lane == 0) atomicAdd(&g_lane_dbg[6], __builtin_amdgcn_s_memtime() - t_k0);
 }
 
 // LK: the window prologue looks snapshots up itself (cache builds); otherwise a main pass with the
@@ -2541,6 +2798,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       d_xc[kRcLevels - 1];  // prefix cache, sampled levels
   DevBuf d_ct[kRcLevels];  // prefix cache lookup tables
   DevBuf d_hits, d_hitp;   // per-window lookups of the main pass
+  DevBuf d_seen;           // prefix cache: sampled levels' first-sighting bitmap
   std::unique_lock<std::mutex> lease(e.scratch_mu, std::try_to_lock);
   if (lease.owns_lock()) {  // reuse the engine's scratch (no per-call hipMalloc of the 64 MB lists)
     std::vector<DevBuf*> bufs = {&d_segs, &d_prefix, &d_out, &d_ebuf, &d_cnt, &d_list, &d_spill,
@@ -2550,7 +2808,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     for (int x = 0; x < kRcLevels; ++x) bufs.push_back(&d_ct[x]);
     bufs.push_back(&d_hits);
     bufs.push_back(&d_hitp);
-    static_assert(Engine::kScratch >= 17 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
+    bufs.push_back(&d_seen);
+    static_assert(Engine::kScratch >= 20 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
     for (size_t i = 0; i < bufs.size(); ++i) bufs[i]->bind(&e.scratch_p[i], &e.scratch_n[i]);
   }
   HIP_TRY(d_segs.alloc(segs.size() * sizeof(SegDesc), stream));
@@ -2581,7 +2840,15 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   int rc = FAC_OK;
   uint64_t retries = 0, launches = 0, popped = 0, cached_pops = 0, pass_windows = windows;
   unsigned long long cnt[N_COUNTERS] = {};
-  float ms_total = 0.f, cache_ms = 0.f;
+  float ms_total = 0.f, cache_ms = 0.f, lane_ms = 0.f;
+  uint64_t lane_windows = 0;
+  hipEvent_t ev_lane = nullptr;  // end of the lane-serial kernel (destroyed on return)
+  struct EvGuard {
+    hipEvent_t& e;
+    ~EvGuard() {
+      if (e) (void)hipEventDestroy(e);
+    }
+  } ev_lane_guard{ev_lane};
   out.clear();
 
   // Prefix cache. Level 1: every window's key of K0 chars (4, else 3, else 2,
@@ -2613,8 +2880,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     P.rc_emax = 64;
     const uint64_t ent_cap = std::max<uint64_t>(1, env_u("FAC_RC_ENTRIES", 16ull << 20));
     const uint32_t max_ent = (uint32_t)std::min<uint64_t>(windows, ent_cap);
+    // count tables: level-1 keys are few (one per distinct k-gram), so the table stays cache-sized
+    const uint32_t cprobes = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(RC_PROBES, env_u("FAC_RC_CPROBES", RC_PROBES)));
+    const uint32_t l1_log2 = (uint32_t)std::min<uint64_t>(24, std::max<uint64_t>(12, env_u("FAC_RC_SLOTS1", 24)));
     uint32_t slots = 1u << 12;
-    while (slots < 4ull * max_ent && slots < (1u << 24)) slots <<= 1;
+    while (slots < 4ull * max_ent && slots < (1u << l1_log2)) slots <<= 1;
     HIP_TRY(d_rck.alloc(slots * sizeof(unsigned long long), stream));
     HIP_TRY(d_rcv.alloc(slots * sizeof(uint32_t), stream));  // key counts, then entries
     HIP_TRY(d_rcslot.alloc(slots * sizeof(uint64_t), stream));
@@ -2656,7 +2926,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       HIP_TRY(hipMemsetAsync(d_rcv.p, 0, slots * sizeof(uint32_t), stream));
       hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P,
                          static_cast<unsigned long long*>(d_rck.p), static_cast<uint32_t*>(d_rcv.p),
-                         static_cast<uint64_t*>(d_rcslot.p), slots - 1, 1u, 1u);
+                         static_cast<uint64_t*>(d_rcslot.p), slots - 1, 1u, 1u, nullptr, 0u, cprobes);
       HIP_TRY(hipGetLastError());
       unsigned int n_keys = 0;
       if (int nrc = number_entries(d_rck, d_rcv, d_rcslot, d_rcrep, slots, 1u, max_ent, n_keys)) return nrc;
@@ -2688,10 +2958,21 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", 2));
     std::vector<RcTable> Lx;        // sampled levels, ascending k
     std::vector<uint32_t> n_entx;   // their entries
+    const uint32_t bloom_log2 = (uint32_t)std::min<uint64_t>(32, env_u("FAC_RC_BLOOM", 0));  // 0: off
     if (n_ent1 && windows >= env_u("FAC_RC_MIN2", 1ull << 20)) {
       const uint64_t samples = (windows + stride2 - 1) / stride2;
+      const uint32_t l2_log2 = (uint32_t)std::min<uint64_t>(27, std::max<uint64_t>(12, env_u("FAC_RC_SLOTS2", 27)));
       uint32_t slots2 = 1u << 12;
-      while (slots2 < 2ull * samples && slots2 < (1u << 27)) slots2 <<= 1;
+      while (slots2 < 2ull * samples && slots2 < (1u << l2_log2)) slots2 <<= 1;
+      uint32_t* seen = nullptr;
+      uint32_t seen_mask = 0;
+      if (bloom_log2 >= 16) {
+        HIP_TRY(d_seen.alloc(((size_t)1 << bloom_log2) / 8, stream));
+        seen = static_cast<uint32_t*>(d_seen.p);
+        seen_mask = (uint32_t)(((uint64_t)1 << bloom_log2) - 1);
+      }
+      // with the bitmap a table count of c means c + 1 sightings
+      const uint32_t thr_t = seen ? std::max<uint32_t>(1, thr2 - 1) : thr2;
       const uint32_t max_ent2 = (uint32_t)std::min<uint64_t>(samples, ent_cap);
       for (uint32_t k2 : ks) {
         if (k2 <= L1.k) continue;
@@ -2703,14 +2984,15 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         HIP_TRY(d_xc[x].alloc(2 * (size_t)max_ent2 * sizeof(uint32_t), stream));
         HIP_TRY(hipMemsetAsync(d_xk[x].p, 0, slots2 * sizeof(unsigned long long), stream));
         HIP_TRY(hipMemsetAsync(d_xv[x].p, 0, slots2 * sizeof(uint32_t), stream));
+        if (seen) HIP_TRY(hipMemsetAsync(seen, 0, ((size_t)seen_mask + 1) / 8, stream));
         SearchParams C = P;
         C.rc_k = k2;
         hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, C,
                            static_cast<unsigned long long*>(d_xk[x].p), static_cast<uint32_t*>(d_xv[x].p),
-                           static_cast<uint64_t*>(d_xslot[x].p), slots2 - 1, stride2, thr2);
+                           static_cast<uint64_t*>(d_xslot[x].p), slots2 - 1, stride2, thr_t, seen, seen_mask, cprobes);
         HIP_TRY(hipGetLastError());
         unsigned int nk2 = 0;
-        if (int nrc = number_entries(d_xk[x], d_xv[x], d_xslot[x], d_xrep[x], slots2, thr2, max_ent2, nk2)) return nrc;
+        if (int nrc = number_entries(d_xk[x], d_xv[x], d_xslot[x], d_xrep[x], slots2, thr_t, max_ent2, nk2)) return nrc;
         const uint32_t ne = std::min(nk2, max_ent2);
         if (ne == 0) continue;
         Lx.push_back(RcTable{k2, slots2 - 1, static_cast<const unsigned long long*>(d_xk[x].p),
@@ -2769,9 +3051,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       };
       // after its build a level's entries are published into an exact-key lookup table (4 slots per
       // entry: a miss usually ends at the first probe)
+      const uint64_t ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", 4)));
       auto publish = [&](RcTable& T, uint32_t n_ent, DevBuf& ct) -> int {
         uint32_t cs = 1u << 12;
-        while (cs < 4ull * n_ent && cs < (1u << 28)) cs <<= 1;
+        while (cs < ct_mult * n_ent && cs < (1u << 28)) cs <<= 1;
         HIP_TRY(ct.alloc((size_t)cs * 2 * sizeof(uint4), stream));
         HIP_TRY(hipMemsetAsync(ct.p, 0, (size_t)cs * 2 * sizeof(uint4), stream));
         hipLaunchKernelGGL(rc_publish_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_ent + 255) / 256, cus * 8))),
@@ -2852,10 +3135,34 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
                          dim3(256), 0, stream, P);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(ev.b, stream));
-      HIP_TRY(hipEventSynchronize(ev.b));
+      // small unfinished windows: one lane each (lane_window_kernel); the rest stay for the wave kernel
+      const bool lane_on = !std::getenv("FAC_NO_LANE") && !P.win_counts && !P.has_map;  // beamed: exact_dedup is set, bail-outs keep it exact
+      if (lane_on) {
+        if (!ev_lane) HIP_TRY(hipEventCreate(&ev_lane));
+        P.lane_debug = std::getenv("FAC_RC_DEBUG") ? 1 : 0;
+        P.lane_popmax = (uint32_t)std::max<unsigned long>(1, std::getenv("FAC_LANE_POPS") ? std::strtoul(std::getenv("FAC_LANE_POPS"), nullptr, 10) : 32ul);
+        const uint32_t lgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + LANE_CHUNK - 1) / LANE_CHUNK, (uint64_t)cus * 12));
+        if (std::getenv("FAC_LANE_Q8")) hipLaunchKernelGGL((lane_window_kernel<8, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+        else hipLaunchKernelGGL((lane_window_kernel<16, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(ev_lane, stream));
+      }
+      HIP_TRY(hipEventSynchronize(lane_on ? ev_lane : ev.b));
       float lms = 0.f;
       HIP_TRY(hipEventElapsedTime(&lms, ev.a, ev.b));
       cache_ms += lms;
+      if (lane_on) {
+        HIP_TRY(hipEventElapsedTime(&lms, ev.b, ev_lane));
+        lane_ms += lms;
+        if (std::getenv("FAC_RC_DEBUG")) {
+          unsigned long long d[8];
+          HIP_TRY(hipMemcpyFromSymbol(d, HIP_SYMBOL(g_lane_dbg), sizeof(d)));
+          std::fprintf(stderr, "FAC_LANE taken=%llu finished=%llu bailed=%llu ms=%.3f popmax=%u trips=%llu run_cycles=%llu "
+                       "wave_cycles=%llu rounds=%llu\n", d[0], d[1], d[2], lms, P.lane_popmax, d[4], d[5], d[6], d[7]);
+          std::memset(d, 0, sizeof(d));
+          HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_lane_dbg), d, sizeof(d)));
+        }
+      }
     }
     HIP_TRY(hipEventRecord(ev.a, stream));
     const hipError_t le = launch_variant(kVariants[vi], grid, stream, P);
@@ -2873,9 +3180,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     launches += 1;
     popped += cnt[1];
     cached_pops += cnt[4];
+    lane_windows += cnt[8];
     if (std::getenv("FAC_RC_DEBUG") && P.rc_mode == 1)
-      std::fprintf(stderr, "FAC_RC launch windows=%llu resumed=%llu lane_flushed=%llu popped=%llu\n",
-                   (unsigned long long)pass_windows, cnt[5], cnt[6], cnt[1]);
+      std::fprintf(stderr, "FAC_RC launch windows=%llu resumed=%llu lane_flushed=%llu lane_searched=%llu popped=%llu\n",
+                   (unsigned long long)pass_windows, cnt[5], cnt[6], cnt[8], cnt[1]);
 #ifdef FAC_WIN_HIST
     {
       unsigned long long h[24];
@@ -2968,6 +3276,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     stats->kernel_launches += launches;
     stats->cache_ms += cache_ms;
     stats->states_cached += cached_pops;
+    stats->lane_ms += lane_ms;
+    stats->lane_windows += lane_windows;
     stats->windows += windows;
     stats->states_popped += popped;
     stats->graphemes = h.n;

@@ -75,7 +75,8 @@ class fac_stats(ctypes.Structure):
                 ("kernel_launches", ctypes.c_uint64), ("windows", ctypes.c_uint64),
                 ("states_popped", ctypes.c_uint64), ("graphemes", ctypes.c_uint64),
                 ("bytes", ctypes.c_uint64), ("retries", ctypes.c_uint64), ("cache_ms", ctypes.c_double),
-                ("states_cached", ctypes.c_uint64)]
+                ("states_cached", ctypes.c_uint64), ("lane_ms", ctypes.c_double),
+                ("lane_windows", ctypes.c_uint64)]
 
 
 assert ctypes.sizeof(fac_match) == 32

@@ -133,6 +133,8 @@ typedef struct fac_stats {
   uint64_t retries;        /* capacity retries */
   double cache_ms;         /* HIP-event time of the prefix cache: key counts, snapshot builds, per-window lookups */
   uint64_t states_cached;  /* pops replayed from prefix-cache snapshots (not in states_popped) */
+  double lane_ms;          /* HIP-event time of the lane-serial search of small resumed windows */
+  uint64_t lane_windows;   /* windows finished by the lane-serial kernel */
 } fac_stats;
 
 typedef struct fac_engine fac_engine;

@@ -321,6 +321,32 @@ def test_prefix_cache_default_on_c3_slice(monkeypatch):
     _staged_vs_oracle(workloads.builder_for(w), w.patterns, hay, w.threshold)
 
 
+@pytest.mark.parametrize("pops", ["1", "4", "32"])
+def test_lane_serial_windows(pops, monkeypatch):
+    """lane_window_kernel (small unfinished windows resumed from their snapshots, one lane each, no
+    dedup table; windows over the pop budget, the ring, the best list or 2*beam go back to the wave
+    kernel) == the wave kernel alone on C3- and C2-shaped slices, and == the oracle on the random
+    differential cases with the prefix cache forced on."""
+    from fuzzy_aho_corasick import workloads
+    monkeypatch.setenv("FAC_LANE_POPS", pops)
+    for cfg, mib in (("c3", 2), ("c2", 4)):
+        w = workloads.config(cfg, mib << 20, 3)
+        staged = workloads.builder_for(w).build(w.patterns).stage(w.haystack)
+        on, st_on = staged.search_windows_records(w.threshold)
+        monkeypatch.setenv("FAC_NO_LANE", "1")
+        off, st_off = staged.search_windows_records(w.threshold)
+        monkeypatch.delenv("FAC_NO_LANE")
+        assert (st_on.lane_windows > 0 or pops == "1") and st_off.lane_windows == 0, cfg
+        assert len(on) > 0 and sorted(on.tolist()) == sorted(off.tolist()), cfg
+    monkeypatch.setenv("FAC_RC_MIN", "1")
+    for k in ("2", "4"):
+        monkeypatch.setenv("FAC_RC_K", k)
+        rng = Rng(0x1a2e ^ int(pops) ^ (int(k) << 8))
+        for _ in range(60):
+            b, pats, hay, thr = random_case(rng, ASCII_VOCAB + UNI_VOCAB, ASCII_FILLER + UNI_FILLER)
+            compare(b, pats, hay, thr)
+
+
 def _keyrows(ms):
     return [(m.start, m.end, m.pattern_index, m.sim_bits()) for m in ms]
 
