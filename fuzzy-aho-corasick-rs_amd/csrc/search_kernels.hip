@@ -1817,14 +1817,6 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
 constexpr uint32_t LANE_RUN = 1u, LANE_OK = 2u, LANE_BAIL = 3u;
 constexpr uint32_t LANE_CHUNK = 4096;
 __device__ unsigned long long g_lane_dbg[8];  // diagnostics (FAC_RC_DEBUG): taken, finished, bailed, lane runs
-__device__ __forceinline__ int64_t lane_goto(const SearchParams& P, const DevNode& nd, uint32_t ch) {
-  const uint32_t ee = node_end(nd);
-  for (uint32_t e = nd.edge_begin; e < ee; ++e) {  // find_transition_char_no_mappings (structs.rs:512-519)
-    const DevEdge ed = P.edges[e];
-    if (ed.ch == ch) return (int64_t)(ed.next & EDGE_NEXT_MASK);
-  }
-  return -1;
-}
 template <uint32_t QL, uint32_t ELN>
 __device__ void lane_run_window(const SearchParams& P, uint4* s_q, uint4* s_e, uint64_t vid, bool have,
                                 uint64_t& popped_lane, uint64_t& cached_lane, uint32_t& done_lane) {
@@ -1865,10 +1857,20 @@ __device__ void lane_run_window(const SearchParams& P, uint4* s_q, uint4* s_e, u
     ++head;
     ++pops;
     const KState st{w.x, w.y, __uint_as_float(w.z), w.w};
+    // the state's reads go out together: node record, char filters, text at j and j + 1
     const DevNode nd = P.nodes[st.node];
-    if (st.pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr))) continue;  // :638-642
-    const uint32_t packed = st.packed, edits = edits_of(packed);
+    const uint4 aux = P.aux[st.node];
     const uint32_t j_rel = st.jm & 0xFFFFu, me_rel = st.jm >> 16;
+    const uint64_t j = start + j_rel;
+    uint32_t c0 = 0, c1 = 0;
+    if (j < S.n) c0 = text_char(P, S, j, err);
+    if (j + 1 < S.n) c1 = text_char(P, S, j + 1, err);
+    if (st.pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr))) continue;  // :638-642
+    if (err) {
+      status = LANE_BAIL;
+      continue;
+    }
+    const uint32_t packed = st.packed, edits = edits_of(packed);
     if (node_has_out(nd)) {  // emission (:659-737) into the best list, first-found ties
       const uint2 orr = P.out_range[st.node];
       const uint32_t ins = packed & 0xFFu, del = (packed >> 8) & 0xFFu, sub = (packed >> 16) & 0xFFu, swp = packed >> 24;
@@ -1903,14 +1905,6 @@ __device__ void lane_run_window(const SearchParams& P, uint4* s_q, uint4* s_e, u
       }
       if (status != LANE_RUN) continue;
     }
-    const uint64_t j = start + j_rel;
-    uint32_t c0 = 0, c1 = 0;
-    if (j < S.n) c0 = text_char(P, S, j, err);
-    if (j + 1 < S.n) c1 = text_char(P, S, j + 1, err);
-    if (err) {
-      status = LANE_BAIL;
-      continue;
-    }
     const Prep pr = lane_prep(P, S, st, nd, start, c0, c1, nd.sb);
     auto push = [&](uint32_t node, uint32_t jm, float pen, uint32_t pk) {
       if (tail - head >= QL) {
@@ -1923,32 +1917,47 @@ __device__ void lane_run_window(const SearchParams& P, uint4* s_q, uint4* s_e, u
     };
     const uint32_t eb = nd.edge_begin, ee = node_end(nd);
     const uint32_t j1 = j_rel + 1u, jm1 = j1 | (j1 << 16);
-    int64_t ex = -1;
-    if (pr.flags & PF_EX) {  // exact (:776-800)
-      ex = lane_goto(P, nd, pr.cur_ch);
-      if (ex >= 0 && !push((uint32_t)ex, jm1, st.pen, packed)) continue;
-    }
+    // exact and swap successors through the goto table (first edge with the char, structs.rs:512-519);
+    // a clear char-filter bit proves the lookup would miss
+    int64_t ex = -1, x = -1;
+    uint64_t gx = 0, gv = 0;
+    const bool want_ex = (pr.flags & PF_EX) && filt_has(aux.z, pr.cur_ch);
+    const bool want_x = (pr.flags & PF_SWAP) && filt_has(aux.z, pr.nch);
+    if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)st.node << 21) | pr.cur_ch, want_ex, gv)) ex = (int64_t)(gv & CHILD26_MASK);
+    if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)st.node << 21) | pr.nch, want_x, gx)) x = (int64_t)(gx & CHILD26_MASK);
+    if (ex >= 0 && !push((uint32_t)ex, jm1, st.pen, packed)) continue;  // exact (:776-800)
     if (pr.flags & PF_SUB) {  // substitutions (:803-874), edge order, the exact edge excluded
       bool ok = true;
-      for (uint32_t e = eb; e < ee && ok; ++e) {
-        const DevEdge ed = P.edges[e];
-        const uint32_t child = ed.next & EDGE_NEXT_MASK;
-        if (ex >= 0 && child == (uint32_t)ex) continue;
-        const float sim = similarity(P, ed.ch, pr.cur_ch);
-        if (sim < P.min_sym) continue;
-        const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
-        if (penalty > pr.remaining) continue;
-        if ((pr.flags & PF_LAST) && !(ed.next & EDGE_CHILD_OUTPUT) &&
-            (!(pr.flags & PF_NEXT) || !sb_has(P, child, pr.next_ch)))
-          continue;
-        ok = push(child, jm1, __fadd_rn(st.pen, penalty), packed + 0x10000u);
+      for (uint32_t e0 = eb; e0 < ee && ok; e0 += 4) {
+        DevEdge ed[4];
+        float sim[4];
+        bool sbn[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) ed[k] = e0 + k < ee ? P.edges[e0 + k] : DevEdge{0u, 0u};
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) sim[k] = similarity(P, ed[k].ch, pr.cur_ch);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+          sbn[k] = (pr.flags & PF_LAST) && (pr.flags & PF_NEXT) && e0 + k < ee && sb_has(P, ed[k].next & EDGE_NEXT_MASK, pr.next_ch);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          if (!ok || e0 + k >= ee) continue;
+          const uint32_t child = ed[k].next & EDGE_NEXT_MASK;
+          if (ex >= 0 && child == (uint32_t)ex) continue;
+          if (sim[k] < P.min_sym) continue;
+          const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim[k]));
+          if (penalty > pr.remaining) continue;
+          if ((pr.flags & PF_LAST) && !(ed[k].next & EDGE_CHILD_OUTPUT) && !sbn[k]) continue;
+          ok = push(child, jm1, __fadd_rn(st.pen, penalty), packed + 0x10000u);
+        }
       }
       if (!ok) continue;
     }
-    if (pr.flags & PF_SWAP) {  // swap (:935-989): goto(goto(node, text[j+1]), text[j])
-      const int64_t x = lane_goto(P, nd, pr.nch);
+    if (x >= 0) {  // swap (:935-989): goto(goto(node, text[j+1]), text[j])
       int64_t node2 = -1;
-      if (x >= 0) node2 = lane_goto(P, P.nodes[(uint32_t)x], pr.cur_ch);
+      uint64_t g2 = 0;
+      const bool want2 = ((gx >> 48) >> (ch_filt_bit(pr.cur_ch) & 15u)) & 1u;  // x's folded char filter
+      if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)x << 21) | pr.cur_ch, want2, g2)) node2 = (int64_t)(g2 & CHILD26_MASK);
       if (node2 >= 0 && !fast) {  // within_limits_swap_ahead with node2's limits (:962-967)
         const Lim m = pick_limits(P, node_limits(P, (uint32_t)node2));
         if (!(m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.swp, packed >> 24)) : false)) node2 = -1;
@@ -1960,13 +1969,20 @@ __device__ void lane_run_window(const SearchParams& P, uint4* s_q, uint4* s_e, u
     if (pr.flags & PF_DEL) {  // deletions (:1035-1089), edge order
       const float npen = __fadd_rn(st.pen, P.p_del);
       bool ok = true;
-      for (uint32_t e = eb; e < ee && ok; ++e) {
-        const DevEdge ed = P.edges[e];
-        const uint32_t child = ed.next & EDGE_NEXT_MASK;
-        if ((pr.flags & PF_LAST) && !(ed.next & EDGE_CHILD_OUTPUT) &&
-            (!(pr.flags & PF_CUR) || !sb_has(P, child, pr.cur_ch)))
-          continue;
-        ok = push(child, st.jm, npen, packed + 0x100u);
+      for (uint32_t e0 = eb; e0 < ee && ok; e0 += 4) {
+        DevEdge ed[4];
+        bool sbc[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) ed[k] = e0 + k < ee ? P.edges[e0 + k] : DevEdge{0u, 0u};
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+          sbc[k] = (pr.flags & PF_LAST) && (pr.flags & PF_CUR) && e0 + k < ee && sb_has(P, ed[k].next & EDGE_NEXT_MASK, pr.cur_ch);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          if (!ok || e0 + k >= ee) continue;
+          if ((pr.flags & PF_LAST) && !(ed[k].next & EDGE_CHILD_OUTPUT) && !sbc[k]) continue;
+          ok = push(ed[k].next & EDGE_NEXT_MASK, st.jm, npen, packed + 0x100u);
+        }
       }
     }
   }
@@ -3142,8 +3158,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         P.lane_debug = std::getenv("FAC_RC_DEBUG") ? 1 : 0;
         P.lane_popmax = (uint32_t)std::max<unsigned long>(1, std::getenv("FAC_LANE_POPS") ? std::strtoul(std::getenv("FAC_LANE_POPS"), nullptr, 10) : 32ul);
         const uint32_t lgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + LANE_CHUNK - 1) / LANE_CHUNK, (uint64_t)cus * 12));
-        if (std::getenv("FAC_LANE_Q8")) hipLaunchKernelGGL((lane_window_kernel<8, 8>), dim3(lgrid), dim3(64), 0, stream, P);
-        else hipLaunchKernelGGL((lane_window_kernel<16, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+        if (std::getenv("FAC_LANE_Q16")) hipLaunchKernelGGL((lane_window_kernel<16, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+        else if (std::getenv("FAC_LANE_Q32")) hipLaunchKernelGGL((lane_window_kernel<32, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+        else hipLaunchKernelGGL((lane_window_kernel<8, 8>), dim3(lgrid), dim3(64), 0, stream, P);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ev_lane, stream));
       }
