@@ -268,6 +268,7 @@ constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8
 struct Engine {
   int device = 0;
   hipStream_t stream = nullptr;
+  mutable hipStream_t aux_stream = nullptr;  // prefix cache: level-1 build beside the sampled-level counts
   fac_config cfg{};
   bool case_insensitive = false;
   bool has_limits = false;

@@ -1818,252 +1818,277 @@ constexpr uint32_t LANE_RUN = 1u, LANE_OK = 2u, LANE_BAIL = 3u;
 constexpr uint32_t LANE_CHUNK = 4096;
 __device__ unsigned long long g_lane_dbg[8];  // diagnostics (FAC_RC_DEBUG): taken, finished, bailed, lane runs
 template <uint32_t QL, uint32_t ELN>
-__device__ void lane_run_window(const SearchParams& P, uint4* s_q, uint4* s_e, uint64_t vid, bool have,
-                                uint64_t& popped_lane, uint64_t& cached_lane, uint32_t& done_lane) {
+__device__ __forceinline__ void lane_step(const SearchParams& P, uint4* s_q, uint4* s_e, const SegDesc& S, uint64_t start,
+                                          uint32_t& status, uint32_t& head, uint32_t& tail, uint32_t& nel, uint32_t& pops,
+                                          unsigned& err) {
   const uint32_t lane = lane_id();
-  uint32_t status = have ? LANE_RUN : 0u;
-  uint32_t head = 0, tail = 0, nel = 0, pops = 0, snap_pops = 0;
-  uint64_t start = 0;
-  SegDesc S{};
-  if (have) {
-    const uint4 h = P.rc_hits[vid];
-    snap_pops = P.rc_hit_pops[vid];
-    const uint32_t kl = find_seg(P, vid);
-    S = P.segs[kl];
-    start = S.w_begin + (vid - P.seg_prefix[kl]);
-    const uint32_t nq = h.z - h.y, nv = h.w & 0xFFFFu;
-    nel = h.w >> 16;
-    const uint4* src = P.rc_pool + h.x + RC_HDR;  // queue, dedup entries (unused), best list
-    for (uint32_t i = 0; i < nq; ++i) s_q[i * 64 + lane] = src[i];
-    for (uint32_t i = 0; i < nel; ++i) s_e[i * 64 + lane] = src[nq + nv + i];
-    tail = nq;
-  }
   const bool fast = P.mef != 255u;
-  unsigned err = 0;
-  uint32_t trips = 0;
-  const uint64_t t_run0 = __builtin_amdgcn_s_memtime();
-  while (__ballot(status == LANE_RUN)) {
-    ++trips;
-    if (status != LANE_RUN) continue;
-    if (head == tail) {
-      status = LANE_OK;
-      continue;
-    }
-    if ((P.beam && tail - head > 2u * P.beam) || pops >= P.lane_popmax) {  // the beam could trigger (:577)
-      status = LANE_BAIL;
-      continue;
-    }
-    const uint4 w = s_q[(head % QL) * 64 + lane];
-    ++head;
-    ++pops;
-    const KState st{w.x, w.y, __uint_as_float(w.z), w.w};
-    // the state's reads go out together: node record, char filters, text at j and j + 1
-    const DevNode nd = P.nodes[st.node];
-    const uint4 aux = P.aux[st.node];
-    const uint32_t j_rel = st.jm & 0xFFFFu, me_rel = st.jm >> 16;
-    const uint64_t j = start + j_rel;
-    uint32_t c0 = 0, c1 = 0;
-    if (j < S.n) c0 = text_char(P, S, j, err);
-    if (j + 1 < S.n) c1 = text_char(P, S, j + 1, err);
-    if (st.pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr))) continue;  // :638-642
-    if (err) {
-      status = LANE_BAIL;
-      continue;
-    }
-    const uint32_t packed = st.packed, edits = edits_of(packed);
-    if (node_has_out(nd)) {  // emission (:659-737) into the best list, first-found ties
-      const uint2 orr = P.out_range[st.node];
-      const uint32_t ins = packed & 0xFFu, del = (packed >> 8) & 0xFFu, sub = (packed >> 16) & 0xFFu, swp = packed >> 24;
-      for (uint32_t i = orr.x; i < orr.y && status == LANE_RUN; ++i) {
-        const uint32_t p = P.out_pat[i];
-        const DevPattern pt = P.pats[p];
-        bool ok;
-        if (fast) {
-          ok = edits <= P.mef;
-        } else {  // within_limits (:151-169)
-          const Lim m = pick_limits(P, pt.has_limits ? (int32_t)p : -1);
-          ok = m.has ? (lim_le(m.l.edits, edits) && lim_le(m.l.ins, ins) && lim_le(m.l.del, del) &&
-                        lim_le(m.l.sub, sub) && lim_le(m.l.swp, swp))
-                     : (edits == 0);
-        }
-        if (!ok) continue;
-        const float sim = __fmul_rn(__fdiv_rn(__fsub_rn(pt.glen, st.pen), pt.glen), pt.weight);  // :696-699
-        if (sim < P.thr) continue;                                                              // :701
-        uint32_t at = nel;
-        for (uint32_t k = 0; k < nel; ++k) {
-          const uint4 e = s_e[k * 64 + lane];
-          if (e.x == me_rel && e.y == p) {
-            at = k;
-            if (sim > __uint_as_float(e.z)) s_e[k * 64 + lane] = make_uint4(me_rel, p, __float_as_uint(sim), packed);
-            break;
-          }
-        }
-        if (at == nel) {
-          if (nel == ELN) status = LANE_BAIL;
-          else s_e[(nel++) * 64 + lane] = make_uint4(me_rel, p, __float_as_uint(sim), packed);
-        }
-      }
-      if (status != LANE_RUN) continue;
-    }
-    const Prep pr = lane_prep(P, S, st, nd, start, c0, c1, nd.sb);
-    auto push = [&](uint32_t node, uint32_t jm, float pen, uint32_t pk) {
-      if (tail - head >= QL) {
-        status = LANE_BAIL;
-        return false;
-      }
-      s_q[(tail % QL) * 64 + lane] = make_uint4(node, jm, __float_as_uint(pen), pk);
-      ++tail;
-      return true;
-    };
-    const uint32_t eb = nd.edge_begin, ee = node_end(nd);
-    const uint32_t j1 = j_rel + 1u, jm1 = j1 | (j1 << 16);
-    // exact and swap successors through the goto table (first edge with the char, structs.rs:512-519);
-    // a clear char-filter bit proves the lookup would miss
-    int64_t ex = -1, x = -1;
-    uint64_t gx = 0, gv = 0;
-    const bool want_ex = (pr.flags & PF_EX) && filt_has(aux.z, pr.cur_ch);
-    const bool want_x = (pr.flags & PF_SWAP) && filt_has(aux.z, pr.nch);
-    if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)st.node << 21) | pr.cur_ch, want_ex, gv)) ex = (int64_t)(gv & CHILD26_MASK);
-    if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)st.node << 21) | pr.nch, want_x, gx)) x = (int64_t)(gx & CHILD26_MASK);
-    if (ex >= 0 && !push((uint32_t)ex, jm1, st.pen, packed)) continue;  // exact (:776-800)
-    if (pr.flags & PF_SUB) {  // substitutions (:803-874), edge order, the exact edge excluded
-      bool ok = true;
-      for (uint32_t e0 = eb; e0 < ee && ok; e0 += 4) {
-        DevEdge ed[4];
-        float sim[4];
-        bool sbn[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) ed[k] = e0 + k < ee ? P.edges[e0 + k] : DevEdge{0u, 0u};
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) sim[k] = similarity(P, ed[k].ch, pr.cur_ch);
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k)
-          sbn[k] = (pr.flags & PF_LAST) && (pr.flags & PF_NEXT) && e0 + k < ee && sb_has(P, ed[k].next & EDGE_NEXT_MASK, pr.next_ch);
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-          if (!ok || e0 + k >= ee) continue;
-          const uint32_t child = ed[k].next & EDGE_NEXT_MASK;
-          if (ex >= 0 && child == (uint32_t)ex) continue;
-          if (sim[k] < P.min_sym) continue;
-          const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim[k]));
-          if (penalty > pr.remaining) continue;
-          if ((pr.flags & PF_LAST) && !(ed[k].next & EDGE_CHILD_OUTPUT) && !sbn[k]) continue;
-          ok = push(child, jm1, __fadd_rn(st.pen, penalty), packed + 0x10000u);
-        }
+  if (head == tail) {
+    status = LANE_OK;
+    return;
+  }
+  if ((P.beam && tail - head > 2u * P.beam) || pops >= P.lane_popmax) {  // the beam could trigger (:577)
+    status = LANE_BAIL;
+    return;
+  }
+  const uint4 w = s_q[(head % QL) * 64 + lane];
+  ++head;
+  ++pops;
+  const KState st{w.x, w.y, __uint_as_float(w.z), w.w};
+  // the state's reads go out together: node record, char filters, text at j and j + 1
+  const DevNode nd = P.nodes[st.node];
+  const uint4 aux = P.aux[st.node];
+  const uint32_t j_rel = st.jm & 0xFFFFu, me_rel = st.jm >> 16;
+  const uint64_t j = start + j_rel;
+  uint32_t c0 = 0, c1 = 0;
+  if (j < S.n) c0 = text_char(P, S, j, err);
+  if (j + 1 < S.n) c1 = text_char(P, S, j + 1, err);
+  if (st.pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr))) return;  // :638-642
+  if (err) {
+    status = LANE_BAIL;
+    return;
+  }
+  const uint32_t packed = st.packed, edits = edits_of(packed);
+  if (node_has_out(nd)) {  // emission (:659-737) into the best list, first-found ties
+    const uint2 orr = P.out_range[st.node];
+    const uint32_t ins = packed & 0xFFu, del = (packed >> 8) & 0xFFu, sub = (packed >> 16) & 0xFFu, swp = packed >> 24;
+    for (uint32_t i = orr.x; i < orr.y && status == LANE_RUN; ++i) {
+      const uint32_t p = P.out_pat[i];
+      const DevPattern pt = P.pats[p];
+      bool ok;
+      if (fast) {
+        ok = edits <= P.mef;
+      } else {  // within_limits (:151-169)
+        const Lim m = pick_limits(P, pt.has_limits ? (int32_t)p : -1);
+        ok = m.has ? (lim_le(m.l.edits, edits) && lim_le(m.l.ins, ins) && lim_le(m.l.del, del) &&
+                      lim_le(m.l.sub, sub) && lim_le(m.l.swp, swp))
+                   : (edits == 0);
       }
       if (!ok) continue;
-    }
-    if (x >= 0) {  // swap (:935-989): goto(goto(node, text[j+1]), text[j])
-      int64_t node2 = -1;
-      uint64_t g2 = 0;
-      const bool want2 = ((gx >> 48) >> (ch_filt_bit(pr.cur_ch) & 15u)) & 1u;  // x's folded char filter
-      if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)x << 21) | pr.cur_ch, want2, g2)) node2 = (int64_t)(g2 & CHILD26_MASK);
-      if (node2 >= 0 && !fast) {  // within_limits_swap_ahead with node2's limits (:962-967)
-        const Lim m = pick_limits(P, node_limits(P, (uint32_t)node2));
-        if (!(m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.swp, packed >> 24)) : false)) node2 = -1;
-      }
-      const uint32_t j2 = j_rel + 2u;
-      if (node2 >= 0 && !push((uint32_t)node2, j2 | (j2 << 16), __fadd_rn(st.pen, P.p_swp), packed + 0x1000000u)) continue;
-    }
-    if ((pr.flags & PF_INS) && !push(st.node, j1 | (me_rel << 16), __fadd_rn(st.pen, P.p_ins), packed + 1u)) continue;  // :994-1029
-    if (pr.flags & PF_DEL) {  // deletions (:1035-1089), edge order
-      const float npen = __fadd_rn(st.pen, P.p_del);
-      bool ok = true;
-      for (uint32_t e0 = eb; e0 < ee && ok; e0 += 4) {
-        DevEdge ed[4];
-        bool sbc[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) ed[k] = e0 + k < ee ? P.edges[e0 + k] : DevEdge{0u, 0u};
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k)
-          sbc[k] = (pr.flags & PF_LAST) && (pr.flags & PF_CUR) && e0 + k < ee && sb_has(P, ed[k].next & EDGE_NEXT_MASK, pr.cur_ch);
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-          if (!ok || e0 + k >= ee) continue;
-          if ((pr.flags & PF_LAST) && !(ed[k].next & EDGE_CHILD_OUTPUT) && !sbc[k]) continue;
-          ok = push(ed[k].next & EDGE_NEXT_MASK, st.jm, npen, packed + 0x100u);
+      const float sim = __fmul_rn(__fdiv_rn(__fsub_rn(pt.glen, st.pen), pt.glen), pt.weight);  // :696-699
+      if (sim < P.thr) continue;                                                              // :701
+      uint32_t at = nel;
+      for (uint32_t k = 0; k < nel; ++k) {
+        const uint4 e = s_e[k * 64 + lane];
+        if (e.x == me_rel && e.y == p) {
+          at = k;
+          if (sim > __uint_as_float(e.z)) s_e[k * 64 + lane] = make_uint4(me_rel, p, __float_as_uint(sim), packed);
+          break;
         }
       }
+      if (at == nel) {
+        if (nel == ELN) status = LANE_BAIL;
+        else s_e[(nel++) * 64 + lane] = make_uint4(me_rel, p, __float_as_uint(sim), packed);
+      }
     }
+    if (status != LANE_RUN) return;
   }
-  popped_lane += pops;
-  const bool fin = status == LANE_OK;
-  {
-    const uint64_t t_run1 = __builtin_amdgcn_s_memtime();
-    const uint32_t n_have = (uint32_t)__popcll(__ballot(have)), n_fin = (uint32_t)__popcll(__ballot(fin));
-    if (P.lane_debug && lane == 0) {  // diagnostics (FAC_RC_DEBUG), one set of atomics per wave round
-      atomicAdd(&g_lane_dbg[0], (unsigned long long)n_have);
-      atomicAdd(&g_lane_dbg[1], (unsigned long long)n_fin);
-      atomicAdd(&g_lane_dbg[2], (unsigned long long)(n_have - n_fin));
-      atomicAdd(&g_lane_dbg[4], (unsigned long long)trips);
-      atomicAdd(&g_lane_dbg[5], t_run1 - t_run0);
-      atomicAdd(&g_lane_dbg[7], 1ull);
+  const Prep pr = lane_prep(P, S, st, nd, start, c0, c1, nd.sb);
+  auto push = [&](uint32_t node, uint32_t jm, float pen, uint32_t pk) {
+    if (tail - head >= QL) {
+      status = LANE_BAIL;
+      return false;
     }
-  }
-  const uint32_t ne = fin ? nel : 0u;
-  const uint32_t incl = wave_inclusive_sum(ne), tot = shfl_u32(incl, 63);
-  unsigned long long base = 0;
-  if (tot) {
-    if (lane == 0) base = atomicAdd(P.counters, (unsigned long long)tot);
-    base = shfl_u64(base, 0);
-  }
-  if (fin) {
-    const uint64_t sb = S.byte_base + local_byte(P, S, start);
-    for (uint32_t i = 0; i < ne; ++i) {
-      const uint64_t o = base + incl - ne + i;
-      if (o < P.out_cap) P.out[o] = match_record(P, S, start, sb, s_e[i * 64 + lane]);
+    s_q[(tail % QL) * 64 + lane] = make_uint4(node, jm, __float_as_uint(pen), pk);
+    ++tail;
+    return true;
+  };
+  const uint32_t eb = nd.edge_begin, ee = node_end(nd);
+  const uint32_t j1 = j_rel + 1u, jm1 = j1 | (j1 << 16);
+  // exact and swap successors through the goto table (first edge with the char, structs.rs:512-519);
+  // a clear char-filter bit proves the lookup would miss
+  int64_t ex = -1, x = -1;
+  uint64_t gx = 0, gv = 0;
+  const bool want_ex = (pr.flags & PF_EX) && filt_has(aux.z, pr.cur_ch);
+  const bool want_x = (pr.flags & PF_SWAP) && filt_has(aux.z, pr.nch);
+  if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)st.node << 21) | pr.cur_ch, want_ex, gv)) ex = (int64_t)(gv & CHILD26_MASK);
+  if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)st.node << 21) | pr.nch, want_x, gx)) x = (int64_t)(gx & CHILD26_MASK);
+  if (ex >= 0 && !push((uint32_t)ex, jm1, st.pen, packed)) return;  // exact (:776-800)
+  if (pr.flags & PF_SUB) {  // substitutions (:803-874), edge order, the exact edge excluded
+    bool ok = true;
+    for (uint32_t e0 = eb; e0 < ee && ok; e0 += 4) {
+      DevEdge ed[4];
+      float sim[4];
+      bool sbn[4];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) ed[k] = e0 + k < ee ? P.edges[e0 + k] : DevEdge{0u, 0u};
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) sim[k] = similarity(P, ed[k].ch, pr.cur_ch);
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k)
+        sbn[k] = (pr.flags & PF_LAST) && (pr.flags & PF_NEXT) && e0 + k < ee && sb_has(P, ed[k].next & EDGE_NEXT_MASK, pr.next_ch);
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        if (!ok || e0 + k >= ee) continue;
+        const uint32_t child = ed[k].next & EDGE_NEXT_MASK;
+        if (ex >= 0 && child == (uint32_t)ex) continue;
+        if (sim[k] < P.min_sym) continue;
+        const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim[k]));
+        if (penalty > pr.remaining) continue;
+        if ((pr.flags & PF_LAST) && !(ed[k].next & EDGE_CHILD_OUTPUT) && !sbn[k]) continue;
+        ok = push(child, jm1, __fadd_rn(st.pen, penalty), packed + 0x10000u);
+      }
     }
-    P.rc_hits[vid] = make_uint4(RC_DONE, 0u, 0u, 0u);
-    cached_lane += snap_pops;
-    done_lane += 1;
+    if (!ok) return;
+  }
+  if (x >= 0) {  // swap (:935-989): goto(goto(node, text[j+1]), text[j])
+    int64_t node2 = -1;
+    uint64_t g2 = 0;
+    const bool want2 = ((gx >> 48) >> (ch_filt_bit(pr.cur_ch) & 15u)) & 1u;  // x's folded char filter
+    if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)x << 21) | pr.cur_ch, want2, g2)) node2 = (int64_t)(g2 & CHILD26_MASK);
+    if (node2 >= 0 && !fast) {  // within_limits_swap_ahead with node2's limits (:962-967)
+      const Lim m = pick_limits(P, node_limits(P, (uint32_t)node2));
+      if (!(m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.swp, packed >> 24)) : false)) node2 = -1;
+    }
+    const uint32_t j2 = j_rel + 2u;
+    if (node2 >= 0 && !push((uint32_t)node2, j2 | (j2 << 16), __fadd_rn(st.pen, P.p_swp), packed + 0x1000000u)) return;
+  }
+  if ((pr.flags & PF_INS) && !push(st.node, j1 | (me_rel << 16), __fadd_rn(st.pen, P.p_ins), packed + 1u)) return;  // :994-1029
+  if (pr.flags & PF_DEL) {  // deletions (:1035-1089), edge order
+    const float npen = __fadd_rn(st.pen, P.p_del);
+    bool ok = true;
+    for (uint32_t e0 = eb; e0 < ee && ok; e0 += 4) {
+      DevEdge ed[4];
+      bool sbc[4];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) ed[k] = e0 + k < ee ? P.edges[e0 + k] : DevEdge{0u, 0u};
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k)
+        sbc[k] = (pr.flags & PF_LAST) && (pr.flags & PF_CUR) && e0 + k < ee && sb_has(P, ed[k].next & EDGE_NEXT_MASK, pr.cur_ch);
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        if (!ok || e0 + k >= ee) continue;
+        if ((pr.flags & PF_LAST) && !(ed[k].next & EDGE_CHILD_OUTPUT) && !sbc[k]) continue;
+        ok = push(ed[k].next & EDGE_NEXT_MASK, st.jm, npen, packed + 0x100u);
+      }
+    }
   }
 }
 
+// Persistent lanes: a lane whose window finishes (or bails) takes the next listed window at once,
+// so a wave is not held by its slowest window; the wave lists unfinished windows from the lookup
+// results chunk by chunk as its idle lanes need them.
 template <uint32_t QL, uint32_t ELN>
 __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
-  __shared__ uint4 s_q[QL * 64];
-  __shared__ uint4 s_e[ELN * 64];
+  __shared__ uint4 s_q[QL * 64];  // ring slot i of lane l at i * 64 + l
+  __shared__ uint4 s_e[ELN * 64];  // best list
   __shared__ uint64_t s_list[128];
   const uint32_t lane = lane_id();
   uint64_t popped_lane = 0, cached_lane = 0;
-  uint32_t done_lane = 0, nbuf = 0;  // nbuf: wave-uniform
+  uint32_t done_lane = 0;
+  uint32_t nbuf = 0;          // wave-uniform: listed windows
+  uint64_t cur = 0, ce = 0;   // wave-uniform: scan position and end of the current chunk
+  bool chunks_done = false;   // wave-uniform
+  uint32_t status = 0, head = 0, tail = 0, nel = 0, pops = 0, snap_pops = 0;
+  uint64_t vid = 0, start = 0;
+  SegDesc S{};
+  unsigned err = 0;
+  uint64_t trips = 0, started = 0;
   const uint64_t t_k0 = __builtin_amdgcn_s_memtime();
   for (;;) {
-    unsigned long long c = 0;
-    if (lane == 0) c = atomicAdd(P.counters + 9, (unsigned long long)LANE_CHUNK);
-    const uint64_t cb = shfl_u64(c, 0);
-    if (cb >= P.total_windows) break;
-    const uint64_t ce = min(cb + (uint64_t)LANE_CHUNK, P.total_windows);
-    for (uint64_t v0 = cb; v0 < ce; v0 += 64) {
-      const uint64_t v = v0 + lane;
+    const uint64_t idle = __ballot(status != LANE_RUN);
+    const uint32_t n_idle = (uint32_t)__popcll(idle);
+    while (nbuf < n_idle && !chunks_done) {  // list unfinished resumed windows whose snapshot fits
+      if (cur >= ce) {
+        unsigned long long c = 0;
+        if (lane == 0) c = atomicAdd(P.counters + 9, (unsigned long long)LANE_CHUNK);
+        const uint64_t cb = shfl_u64(c, 0);
+        if (cb >= P.total_windows) {
+          chunks_done = true;
+          break;
+        }
+        cur = cb;
+        ce = min(cb + (uint64_t)LANE_CHUNK, P.total_windows);
+      }
+      const uint64_t v = cur + lane;
       bool take = false;
-      if (v < ce) {  // unfinished resumed windows whose snapshot fits the lane's ring and best list
+      if (v < ce) {
         const uint4 h = P.rc_hits[v];
         take = h.x != RC_DONE && h.x != EMPTY && h.z - h.y <= QL && (h.w >> 16) <= ELN;
       }
       const uint64_t m = __ballot(take);
       if (take) s_list[nbuf + prefix_below(m)] = v;
       nbuf += (uint32_t)__popcll(m);
+      cur += 64;
       __builtin_amdgcn_wave_barrier();
-      if (nbuf >= 64) {
-        const uint64_t vid = s_list[lane];
-        const uint64_t rest = lane + 64 < nbuf ? s_list[lane + 64] : 0ull;
-        __builtin_amdgcn_wave_barrier();
-        if (lane + 64 < nbuf) s_list[lane] = rest;
-        nbuf -= 64;
-        __builtin_amdgcn_wave_barrier();
-        lane_run_window<QL, ELN>(P, s_q, s_e, vid, true, popped_lane, cached_lane, done_lane);
+    }
+    const uint32_t give = min(nbuf, n_idle);
+    if (give == 0 && !__ballot(status == LANE_RUN)) break;
+    const uint32_t r = prefix_below(idle);
+    const bool starts = status != LANE_RUN && r < give;
+    uint64_t next = 0;
+    if (starts) next = s_list[r];
+    if (give) {  // drop the handed-out entries from the list
+      const uint32_t rest = nbuf - give;
+      __builtin_amdgcn_wave_barrier();
+      const uint64_t a0 = lane < rest ? s_list[give + lane] : 0ull;
+      const uint64_t a1 = lane + 64 < rest ? s_list[give + lane + 64] : 0ull;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < rest) s_list[lane] = a0;
+      if (lane + 64 < rest) s_list[lane + 64] = a1;
+      nbuf = rest;
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (starts) {  // resume the window from its snapshot
+      vid = next;
+      const uint4 h = P.rc_hits[vid];
+      snap_pops = P.rc_hit_pops[vid];
+      const uint32_t kl = find_seg(P, vid);
+      S = P.segs[kl];
+      start = S.w_begin + (vid - P.seg_prefix[kl]);
+      const uint32_t nq = h.z - h.y, nv = h.w & 0xFFFFu;
+      nel = h.w >> 16;
+      const uint4* src = P.rc_pool + h.x + RC_HDR;  // queue, dedup entries (unused), best list
+      for (uint32_t i = 0; i < nq; ++i) s_q[i * 64 + lane] = src[i];
+      for (uint32_t i = 0; i < nel; ++i) s_e[i * 64 + lane] = src[nq + nv + i];
+      head = 0;
+      tail = nq;
+      pops = 0;
+      err = 0;
+      status = LANE_RUN;
+      ++started;
+    }
+    ++trips;
+    if (status == LANE_RUN) lane_step<QL, ELN>(P, s_q, s_e, S, start, status, head, tail, nel, pops, err);
+    const bool fin = status == LANE_OK, bail = status == LANE_BAIL;
+    if (__ballot(fin || bail)) {  // finished windows write their records (one output atomic per wave)
+      const uint32_t ne = fin ? nel : 0u;
+      const uint32_t incl = wave_inclusive_sum(ne), tot = shfl_u32(incl, 63);
+      unsigned long long base = 0;
+      if (tot) {
+        if (lane == 0) base = atomicAdd(P.counters, (unsigned long long)tot);
+        base = shfl_u64(base, 0);
+      }
+      if (fin) {
+        const uint64_t sb = S.byte_base + local_byte(P, S, start);
+        for (uint32_t i = 0; i < ne; ++i) {
+          const uint64_t o = base + incl - ne + i;
+          if (o < P.out_cap) P.out[o] = match_record(P, S, start, sb, s_e[i * 64 + lane]);
+        }
+        P.rc_hits[vid] = make_uint4(RC_DONE, 0u, 0u, 0u);
+        cached_lane += snap_pops;
+        done_lane += 1;
+      }
+      if (fin || bail) {
+        popped_lane += pops;
+        status = 0u;
       }
     }
-  }
-  if (nbuf) {
-    const uint64_t vid = lane < nbuf ? s_list[lane] : 0ull;
-    lane_run_window<QL, ELN>(P, s_q, s_e, vid, lane < nbuf, popped_lane, cached_lane, done_lane);
   }
   if (popped_lane) atomicAdd(P.counters + 1, popped_lane);
   if (cached_lane) atomicAdd(P.counters + 4, cached_lane);
   if (done_lane) atomicAdd(P.counters + 8, (unsigned long long)done_lane);
-  if (P.lane_debug && lane == 0) atomicAdd(&g_lane_dbg[6], __builtin_amdgcn_s_memtime() - t_k0);
+  if (P.lane_debug) {  // diagnostics (FAC_RC_DEBUG): windows started / finished, pop steps, cycles
+    const uint32_t st = (uint32_t)wave_inclusive_sum((uint32_t)started), dn = wave_inclusive_sum(done_lane);
+    if (lane == 63) {
+      atomicAdd(&g_lane_dbg[0], (unsigned long long)st);
+      atomicAdd(&g_lane_dbg[1], (unsigned long long)dn);
+      atomicAdd(&g_lane_dbg[2], (unsigned long long)(st - dn));
+      atomicAdd(&g_lane_dbg[4], trips);
+      atomicAdd(&g_lane_dbg[6], __builtin_amdgcn_s_memtime() - t_k0);
+      atomicAdd(&g_lane_dbg[7], 1ull);
+    }
+  }
 }
 
 // LK: the window prologue looks snapshots up itself (cache builds); otherwise a main pass with the
@@ -2605,6 +2630,8 @@ void free_engine_device(Engine& e) {
     }
   if (e.stream) (void)hipStreamDestroy(e.stream);
   e.stream = nullptr;
+  if (e.aux_stream) (void)hipStreamDestroy(e.aux_stream);
+  e.aux_stream = nullptr;
   e.d_nodes = nullptr;
 }
 
@@ -2961,7 +2988,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (k2) ks.push_back(std::min<uint32_t>(8, k2));
     } else {
       const char* le = std::getenv("FAC_RC_LEVELS");
-      std::string spec = le ? le : "5,6,8";
+      std::string spec = le ? le : "5,6";  // with the lane-serial kernel an 8-char level no longer pays (C3 156 -> 147 ms)
       for (size_t a = 0; a < spec.size();) {
         const size_t b = spec.find(',', a);
         const uint32_t k = (uint32_t)std::strtoul(spec.substr(a, b == std::string::npos ? std::string::npos : b - a).c_str(), nullptr, 10);
@@ -2969,6 +2996,92 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         if (b == std::string::npos) break;
         a = b + 1;
       }
+    }
+    // Snapshot pool and the level-1 build go first: the level-1 build runs on the engine's second
+    // stream while the sampled levels are counted on this one (the counts only need level 1's k).
+    // The pool is sized for every key the levels could select (up to the budget); a build that runs
+    // out of pool leaves the remaining keys uncached.
+    const uint64_t samples_est = windows >= env_u("FAC_RC_MIN2", 1ull << 20) ? (windows + std::max<uint64_t>(1, env_u("FAC_RC_STRIDE2", 2)) - 1) / std::max<uint64_t>(1, env_u("FAC_RC_STRIDE2", 2)) : 0;
+    const uint64_t max_ent2_est = std::min<uint64_t>(samples_est, ent_cap);
+    const uint64_t worst = RC_HDR + std::min(qmain, qbuild) + P.rc_vmax + P.rc_emax;
+    hipStream_t bstream = stream;  // the level-1 build's stream
+    hipEvent_t l1_done = nullptr;
+    struct EvDel {
+      hipEvent_t& e;
+      ~EvDel() {
+        if (e) (void)hipEventDestroy(e);
+      }
+    } l1_done_guard{l1_done};
+    std::vector<RcTable> tabs;  // built levels, ascending k: a build resumes its representatives from them
+    const uint64_t ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", 4)));
+    auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, hipStream_t bs) -> int {
+      SearchParams Q = P;
+      Q.rc_mode = 2;
+      Q.rc_k = T.k;
+      Q.rc_ntab = 0;
+      for (size_t t = tabs.size(); t-- > 0 && T.k > tabs[t].k;)  // levels below T, deepest first
+        Q.rc_tab[Q.rc_ntab++] = tabs[t];
+      Q.rc_off = const_cast<uint32_t*>(T.off);
+      Q.rc_count = const_cast<uint32_t*>(T.count);
+      Q.win_list = reps;
+      Q.total_windows = n_ent;
+      // list chunks of up to 64 representatives: their parent lookups go out together
+      Q.chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, n_ent / (4ull * max_grid)));
+      Q.win_counts = nullptr;
+      Q.ebuf = static_cast<uint4*>(d_ebuf.p);
+      Q.out = static_cast<fac_match*>(d_out.p);
+      Q.out_cap = out_cap;
+      Q.spill = static_cast<uint64_t*>(d_spill.p);
+      Q.spill_cap = spill_cap;
+      Q.counters = static_cast<unsigned long long*>(d_cnt.p);
+      HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), bs));
+      launch_rc_build(qbuild, std::min<uint32_t>(n_ent, max_grid), bs, Q);
+      const hipError_t le = hipGetLastError();
+      if (le != hipSuccess) {
+        err = std::string("kernel launch: ") + hipGetErrorString(le);
+        return FAC_E_HIP;
+      }
+      return FAC_OK;
+    };
+    // after its build a level's entries are published into an exact-key lookup table (4 slots per
+    // entry: a miss usually ends at the first probe)
+    auto publish = [&](RcTable& T, uint32_t n_ent, DevBuf& ct, hipStream_t bs) -> int {
+      uint32_t cs = 1u << 12;
+      while (cs < ct_mult * n_ent && cs < (1u << 28)) cs <<= 1;
+      HIP_TRY(ct.alloc((size_t)cs * 2 * sizeof(uint4), bs));
+      HIP_TRY(hipMemsetAsync(ct.p, 0, (size_t)cs * 2 * sizeof(uint4), bs));
+      hipLaunchKernelGGL(rc_publish_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_ent + 255) / 256, cus * 8))),
+                         dim3(256), 0, bs, static_cast<const uint4*>(P.rc_pool), T.off, T.count, n_ent, T.k,
+                         static_cast<uint4*>(ct.p), cs - 1);
+      HIP_TRY(hipGetLastError());
+      T.ct = static_cast<const uint4*>(ct.p);
+      T.ct_mask = cs - 1;
+      return FAC_OK;
+    };
+    if (n_ent1) {
+      const uint64_t n_all = n_ent1 + (uint64_t)ks.size() * max_ent2_est;
+      const uint64_t budget = env_u("FAC_RC_POOL_MB", 16384ull) << 20;
+      // per-wave pool chunks: about a quarter of the expected pool (~40 words a snapshot) spread over
+      // the building waves, at least one worst snapshot; + one partly used chunk per wave and level
+      const uint64_t grids = std::min<uint64_t>(n_ent1, max_grid) + (uint64_t)ks.size() * std::min<uint64_t>(max_ent2_est, max_grid);
+      P.rc_pool_chunk = (uint32_t)std::max<uint64_t>(worst, std::min<uint64_t>(RC_POOL_CHUNK, n_all * 40 / (4 * grids)));
+      const uint64_t pool_words = std::max<uint64_t>(1024, std::min<uint64_t>(n_all * worst, budget / sizeof(uint4))) +
+                                  grids * P.rc_pool_chunk;
+      HIP_TRY(d_rcs.alloc(pool_words * sizeof(uint4), stream));
+      P.rc_pool = static_cast<uint4*>(d_rcs.p);
+      P.rc_pool_cap = pool_words;
+      if (!std::getenv("FAC_RC_ONE_STREAM")) {
+        if (!e.aux_stream) HIP_TRY(hipStreamCreateWithFlags(&e.aux_stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&l1_done, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(l1_done, stream));  // everything so far (counts, pool) before the build
+        HIP_TRY(hipStreamWaitEvent(e.aux_stream, l1_done, 0));
+        bstream = e.aux_stream;
+      }
+      int brc = build(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p), bstream);
+      if (brc) return brc;
+      if ((brc = publish(L1, n_ent1, d_ct[0], bstream))) return brc;
+      if (bstream != stream) HIP_TRY(hipEventRecord(l1_done, bstream));
+      tabs.push_back(L1);
     }
     const uint32_t stride2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_STRIDE2", 2));
     const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", 2));
@@ -3018,77 +3131,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       }
     }
     if (n_ent1) {
-      // snapshot pool: the worst entry for every key of every level, up to a budget; a build that
-      // runs out of pool leaves the remaining keys uncached
-      uint64_t n_all = n_ent1;
-      for (uint32_t ne : n_entx) n_all += ne;
-      const uint64_t worst = RC_HDR + std::min(qmain, qbuild) + P.rc_vmax + P.rc_emax;
-      const uint64_t budget = env_u("FAC_RC_POOL_MB", 16384ull) << 20;
-      // per-wave pool chunks: about a quarter of the expected pool (~40 words a snapshot) spread over
-      // the building waves, at least one worst snapshot; + one partly used chunk per wave and level
-      uint64_t grids = std::min<uint64_t>(n_ent1, max_grid);
-      for (uint32_t ne : n_entx) grids += std::min<uint64_t>(ne, max_grid);
-      P.rc_pool_chunk = (uint32_t)std::max<uint64_t>(worst, std::min<uint64_t>(RC_POOL_CHUNK, n_all * 40 / (4 * grids)));
-      const uint64_t pool_words = std::max<uint64_t>(1024, std::min<uint64_t>(n_all * worst, budget / sizeof(uint4))) +
-                                  grids * P.rc_pool_chunk;
-      HIP_TRY(d_rcs.alloc(pool_words * sizeof(uint4), stream));
-      P.rc_pool = static_cast<uint4*>(d_rcs.p);
-      P.rc_pool_cap = pool_words;
-      // tables deepest first: a build resumes its representatives from the levels below it
-      std::vector<RcTable> tabs{L1};
-      auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps) -> int {
-        SearchParams Q = P;
-        Q.rc_mode = 2;
-        Q.rc_k = T.k;
-        Q.rc_ntab = 0;
-        for (size_t t = tabs.size(); t-- > 0 && T.k > tabs[t].k;)  // levels below T, deepest first
-          if (&tabs[t] != &T) Q.rc_tab[Q.rc_ntab++] = tabs[t];
-        Q.rc_off = const_cast<uint32_t*>(T.off);
-        Q.rc_count = const_cast<uint32_t*>(T.count);
-        Q.win_list = reps;
-        Q.total_windows = n_ent;
-        // list chunks of up to 64 representatives: their parent lookups go out together
-        Q.chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, n_ent / (4ull * max_grid)));
-        Q.win_counts = nullptr;
-        Q.ebuf = static_cast<uint4*>(d_ebuf.p);
-        Q.out = static_cast<fac_match*>(d_out.p);
-        Q.out_cap = out_cap;
-        Q.spill = static_cast<uint64_t*>(d_spill.p);
-        Q.spill_cap = spill_cap;
-        Q.counters = static_cast<unsigned long long*>(d_cnt.p);
-        HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), stream));
-        launch_rc_build(qbuild, std::min<uint32_t>(n_ent, max_grid), stream, Q);
-        const hipError_t le = hipGetLastError();
-        if (le != hipSuccess) {
-          err = std::string("kernel launch: ") + hipGetErrorString(le);
-          return FAC_E_HIP;
-        }
-        return FAC_OK;
-      };
-      // after its build a level's entries are published into an exact-key lookup table (4 slots per
-      // entry: a miss usually ends at the first probe)
-      const uint64_t ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", 4)));
-      auto publish = [&](RcTable& T, uint32_t n_ent, DevBuf& ct) -> int {
-        uint32_t cs = 1u << 12;
-        while (cs < ct_mult * n_ent && cs < (1u << 28)) cs <<= 1;
-        HIP_TRY(ct.alloc((size_t)cs * 2 * sizeof(uint4), stream));
-        HIP_TRY(hipMemsetAsync(ct.p, 0, (size_t)cs * 2 * sizeof(uint4), stream));
-        hipLaunchKernelGGL(rc_publish_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_ent + 255) / 256, cus * 8))),
-                           dim3(256), 0, stream, static_cast<const uint4*>(P.rc_pool), T.off, T.count, n_ent, T.k,
-                           static_cast<uint4*>(ct.p), cs - 1);
-        HIP_TRY(hipGetLastError());
-        T.ct = static_cast<const uint4*>(ct.p);
-        T.ct_mask = cs - 1;
-        return FAC_OK;
-      };
-      int brc = build(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p));
-      if (brc) return brc;
-      if ((brc = publish(L1, n_ent1, d_ct[0]))) return brc;
-      tabs[0] = L1;
+      if (bstream != stream) HIP_TRY(hipStreamWaitEvent(stream, l1_done, 0));  // level 1 built and published
       for (size_t x = 0; x < Lx.size(); ++x) {
-        brc = build(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[x].p));
+        int brc = build(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[x].p), stream);
         if (brc) return brc;
-        if ((brc = publish(Lx[x], n_entx[x], d_ct[1 + x]))) return brc;
+        if ((brc = publish(Lx[x], n_entx[x], d_ct[1 + x], stream))) return brc;
         tabs.push_back(Lx[x]);
       }
       P.rc_ntab = 0;
