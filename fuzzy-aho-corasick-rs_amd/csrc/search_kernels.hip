@@ -1971,7 +1971,9 @@ __device__ __forceinline__ void lane_step(const SearchParams& P, uint4* s_q, uin
 template <uint32_t QL, uint32_t ELN>
 __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
   __shared__ uint4 s_q[QL * 64];  // ring slot i of lane l at i * 64 + l
-  __shared__ uint4 s_e[ELN * 64];  // best list
+  // best lists in this workgroup's slice of the emit scratch (read only on emissions; keeping them out
+  // of LDS lets more waves share a CU): entry i of lane l at i * 64 + l
+  uint4* s_e = P.ebuf + (size_t)blockIdx.x * P.ecap;
   __shared__ uint64_t s_list[128];
   const uint32_t lane = lane_id();
   uint64_t popped_lane = 0, cached_lane = 0;
@@ -3204,10 +3206,13 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         if (!ev_lane) HIP_TRY(hipEventCreate(&ev_lane));
         P.lane_debug = std::getenv("FAC_RC_DEBUG") ? 1 : 0;
         P.lane_popmax = (uint32_t)std::max<unsigned long>(1, std::getenv("FAC_LANE_POPS") ? std::strtoul(std::getenv("FAC_LANE_POPS"), nullptr, 10) : 32ul);
-        const uint32_t lgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + LANE_CHUNK - 1) / LANE_CHUNK, (uint64_t)cus * 12));
-        if (std::getenv("FAC_LANE_Q16")) hipLaunchKernelGGL((lane_window_kernel<16, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+        // one wave per workgroup; each takes its best lists from its own emit-scratch slice
+        const uint32_t lgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + LANE_CHUNK - 1) / LANE_CHUNK, (uint64_t)max_grid));
+        static_assert(16 * 64 <= 1024, "lane best lists must fit the emit scratch slice (P.ecap >= 1024)");
+        // 16-state rings by default (C3: lane 19 ms + wave kernel 37 ms, against 6 + 58 with 8 states)
+        if (std::getenv("FAC_LANE_Q8")) hipLaunchKernelGGL((lane_window_kernel<8, 8>), dim3(lgrid), dim3(64), 0, stream, P);
         else if (std::getenv("FAC_LANE_Q32")) hipLaunchKernelGGL((lane_window_kernel<32, 8>), dim3(lgrid), dim3(64), 0, stream, P);
-        else hipLaunchKernelGGL((lane_window_kernel<8, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+        else hipLaunchKernelGGL((lane_window_kernel<16, 8>), dim3(lgrid), dim3(64), 0, stream, P);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ev_lane, stream));
       }
