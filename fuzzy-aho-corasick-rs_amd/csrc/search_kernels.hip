@@ -1817,8 +1817,20 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
 constexpr uint32_t LANE_RUN = 1u, LANE_OK = 2u, LANE_BAIL = 3u;
 constexpr uint32_t LANE_CHUNK = 4096;
 __device__ unsigned long long g_lane_dbg[8];  // diagnostics (FAC_RC_DEBUG): taken, finished, bailed, lane runs
+// Lane ring entries are 12 bytes in three LDS planes (node, penalty, position word): the position word
+// packs j_rel and me_rel (8 bits each) and the four edit counts (4 bits each). A state that does not
+// fit sends its window back to the wave kernel.
+__device__ __forceinline__ bool lane_pack(uint32_t jm, uint32_t pk, uint32_t& w) {
+  const uint32_t jr = jm & 0xFFFFu, mr = jm >> 16;
+  w = jr | (mr << 8) | ((pk & 0xFu) << 16) | (((pk >> 8) & 0xFu) << 20) | (((pk >> 16) & 0xFu) << 24) | ((pk >> 24) << 28);
+  return jr < 256u && mr < 256u && ((pk & 0xF0F0F0F0u) == 0u);
+}
+__device__ __forceinline__ void lane_unpack(uint32_t w, uint32_t& jm, uint32_t& pk) {
+  jm = (w & 0xFFu) | (((w >> 8) & 0xFFu) << 16);
+  pk = ((w >> 16) & 0xFu) | (((w >> 20) & 0xFu) << 8) | (((w >> 24) & 0xFu) << 16) | ((w >> 28) << 24);
+}
 template <uint32_t QL, uint32_t ELN>
-__device__ __forceinline__ void lane_step(const SearchParams& P, uint4* s_q, uint4* s_e, const SegDesc& S, uint64_t start,
+__device__ __forceinline__ void lane_step(const SearchParams& P, uint32_t* s_q, uint4* s_e, const SegDesc& S, uint64_t start,
                                           uint32_t& status, uint32_t& head, uint32_t& tail, uint32_t& nel, uint32_t& pops,
                                           unsigned& err) {
   const uint32_t lane = lane_id();
@@ -1831,10 +1843,12 @@ __device__ __forceinline__ void lane_step(const SearchParams& P, uint4* s_q, uin
     status = LANE_BAIL;
     return;
   }
-  const uint4 w = s_q[(head % QL) * 64 + lane];
+  const uint32_t slot = (head % QL) * 64 + lane;
+  uint32_t jm0, pk0;
+  lane_unpack(s_q[2 * QL * 64 + slot], jm0, pk0);
   ++head;
   ++pops;
-  const KState st{w.x, w.y, __uint_as_float(w.z), w.w};
+  const KState st{s_q[slot], jm0, __uint_as_float(s_q[QL * 64 + slot]), pk0};
   // the state's reads go out together: node record, char filters, text at j and j + 1
   const DevNode nd = P.nodes[st.node];
   const uint4 aux = P.aux[st.node];
@@ -1885,11 +1899,15 @@ __device__ __forceinline__ void lane_step(const SearchParams& P, uint4* s_q, uin
   }
   const Prep pr = lane_prep(P, S, st, nd, start, c0, c1, nd.sb);
   auto push = [&](uint32_t node, uint32_t jm, float pen, uint32_t pk) {
-    if (tail - head >= QL) {
+    uint32_t w;
+    if (tail - head >= QL || !lane_pack(jm, pk, w)) {
       status = LANE_BAIL;
       return false;
     }
-    s_q[(tail % QL) * 64 + lane] = make_uint4(node, jm, __float_as_uint(pen), pk);
+    const uint32_t slot = (tail % QL) * 64 + lane;
+    s_q[slot] = node;
+    s_q[QL * 64 + slot] = __float_as_uint(pen);
+    s_q[2 * QL * 64 + slot] = w;
     ++tail;
     return true;
   };
@@ -1970,7 +1988,7 @@ __device__ __forceinline__ void lane_step(const SearchParams& P, uint4* s_q, uin
 // results chunk by chunk as its idle lanes need them.
 template <uint32_t QL, uint32_t ELN>
 __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
-  __shared__ uint4 s_q[QL * 64];  // ring slot i of lane l at i * 64 + l
+  __shared__ uint32_t s_q[3 * QL * 64];  // ring slot i of lane l at i * 64 + l, three planes
   // best lists in this workgroup's slice of the emit scratch (read only on emissions; keeping them out
   // of LDS lets more waves share a CU): entry i of lane l at i * 64 + l
   uint4* s_e = P.ebuf + (size_t)blockIdx.x * P.ecap;
@@ -2041,13 +2059,21 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
       const uint32_t nq = h.z - h.y, nv = h.w & 0xFFFFu;
       nel = h.w >> 16;
       const uint4* src = P.rc_pool + h.x + RC_HDR;  // queue, dedup entries (unused), best list
-      for (uint32_t i = 0; i < nq; ++i) s_q[i * 64 + lane] = src[i];
+      bool fits = true;
+      for (uint32_t i = 0; i < nq; ++i) {
+        const uint4 q = src[i];
+        uint32_t w;
+        fits = lane_pack(q.y, q.w, w) && fits;
+        s_q[i * 64 + lane] = q.x;
+        s_q[QL * 64 + i * 64 + lane] = q.z;
+        s_q[2 * QL * 64 + i * 64 + lane] = w;
+      }
       for (uint32_t i = 0; i < nel; ++i) s_e[i * 64 + lane] = src[nq + nv + i];
       head = 0;
       tail = nq;
       pops = 0;
       err = 0;
-      status = LANE_RUN;
+      status = fits ? LANE_RUN : LANE_BAIL;
       ++started;
     }
     ++trips;
