@@ -3101,20 +3101,31 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (!std::getenv("FAC_RC_ONE_STREAM")) {
         if (!e.aux_stream) HIP_TRY(hipStreamCreateWithFlags(&e.aux_stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&l1_done, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(l1_done, stream));  // everything so far (counts, pool) before the build
-        HIP_TRY(hipStreamWaitEvent(e.aux_stream, l1_done, 0));
         bstream = e.aux_stream;
+      }
+    }
+    // launched once the sampled levels' count tables are cleared (a fill queued behind the build's
+    // persistent waves would hold the counts back)
+    bool l1_launched = false;
+    auto launch_l1 = [&]() -> int {
+      if (l1_launched || !n_ent1) return FAC_OK;
+      l1_launched = true;
+      if (bstream != stream) {
+        HIP_TRY(hipEventRecord(l1_done, stream));  // everything so far (counts, pool, clears) first
+        HIP_TRY(hipStreamWaitEvent(bstream, l1_done, 0));
       }
       int brc = build(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p), bstream);
       if (brc) return brc;
       if ((brc = publish(L1, n_ent1, d_ct[0], bstream))) return brc;
       if (bstream != stream) HIP_TRY(hipEventRecord(l1_done, bstream));
       tabs.push_back(L1);
-    }
+      return FAC_OK;
+    };
     const uint32_t stride2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_STRIDE2", 2));
     const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", 2));
     std::vector<RcTable> Lx;        // sampled levels, ascending k
     std::vector<uint32_t> n_entx;   // their entries
+    std::vector<size_t> xbuf;       // their count-table buffers
     const uint32_t bloom_log2 = (uint32_t)std::min<uint64_t>(32, env_u("FAC_RC_BLOOM", 0));  // 0: off
     if (n_ent1 && windows >= env_u("FAC_RC_MIN2", 1ull << 20)) {
       const uint64_t samples = (windows + stride2 - 1) / stride2;
@@ -3131,9 +3142,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       // with the bitmap a table count of c means c + 1 sightings
       const uint32_t thr_t = seen ? std::max<uint32_t>(1, thr2 - 1) : thr2;
       const uint32_t max_ent2 = (uint32_t)std::min<uint64_t>(samples, ent_cap);
-      for (uint32_t k2 : ks) {
-        if (k2 <= L1.k) continue;
-        const size_t x = Lx.size();
+      std::vector<uint32_t> kk;  // the levels to count; buffers x = position in kk
+      for (uint32_t k2 : ks)
+        if (k2 > L1.k) kk.push_back(k2);
+      for (size_t x = 0; x < kk.size(); ++x) {  // every level's tables cleared before the level-1 build
         HIP_TRY(d_xk[x].alloc(slots2 * sizeof(unsigned long long), stream));
         HIP_TRY(d_xv[x].alloc(slots2 * sizeof(uint32_t), stream));  // sample counts, then entries
         HIP_TRY(d_xslot[x].alloc(slots2 * sizeof(uint64_t), stream));
@@ -3141,6 +3153,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         HIP_TRY(d_xc[x].alloc(2 * (size_t)max_ent2 * sizeof(uint32_t), stream));
         HIP_TRY(hipMemsetAsync(d_xk[x].p, 0, slots2 * sizeof(unsigned long long), stream));
         HIP_TRY(hipMemsetAsync(d_xv[x].p, 0, slots2 * sizeof(uint32_t), stream));
+      }
+      if (int lrc = launch_l1()) return lrc;
+      for (size_t x = 0; x < kk.size(); ++x) {
+        const uint32_t k2 = kk[x];
         if (seen) HIP_TRY(hipMemsetAsync(seen, 0, ((size_t)seen_mask + 1) / 8, stream));
         SearchParams C = P;
         C.rc_k = k2;
@@ -3156,12 +3172,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
                              static_cast<const uint32_t*>(d_xv[x].p), static_cast<uint32_t*>(d_xc[x].p) + max_ent2,
                              static_cast<uint32_t*>(d_xc[x].p)});
         n_entx.push_back(ne);
+        xbuf.push_back(x);
       }
     }
+    if (int lrc = launch_l1()) return lrc;  // no sampled levels
     if (n_ent1) {
       if (bstream != stream) HIP_TRY(hipStreamWaitEvent(stream, l1_done, 0));  // level 1 built and published
       for (size_t x = 0; x < Lx.size(); ++x) {
-        int brc = build(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[x].p), stream);
+        int brc = build(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), stream);
         if (brc) return brc;
         if ((brc = publish(Lx[x], n_entx[x], d_ct[1 + x], stream))) return brc;
         tabs.push_back(Lx[x]);

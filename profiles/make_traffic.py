@@ -5,6 +5,10 @@ for non-streaming reads); WRITE_SIZE as reported. Both counters are in kB, per k
 
 usage: python profiles/make_traffic.py CFG MIB FETCH.csv WRITE.csv [TARGET_MIB [KERNEL_SUBSTR]]
 
+KERNEL_SUBSTR may list several kernels separated by commas (e.g.
+"bfs_window_kernel,lane_window_kernel"): their per-launch averages are summed, matching bench.py's
+roofline, which times the wave kernel and the lane-serial kernel together (one launch each per step).
+
 TARGET_MIB (optional) scales a measurement taken on a smaller launch linearly to the bench launch
 (windows are i.i.d.; checked: 8, 32 and 256 MiB C3 launches give the same bytes per grapheme).
 """
@@ -24,9 +28,16 @@ def per_launch_kb(path, kernel):
 def main():
     cfg, mib, fetch_csv, write_csv = sys.argv[1], float(sys.argv[2]), sys.argv[3], sys.argv[4]
     target = float(sys.argv[5]) if len(sys.argv) > 5 else mib
-    kernel = sys.argv[6] if len(sys.argv) > 6 else "bfs_window_kernel"
-    fetch_kb, name = per_launch_kb(fetch_csv, kernel)
-    write_kb, _ = per_launch_kb(write_csv, kernel)
+    kernels = (sys.argv[6] if len(sys.argv) > 6 else "bfs_window_kernel,lane_window_kernel").split(",")
+    fetch_kb = write_kb = 0.0
+    names = []
+    for kernel in kernels:
+        f, name = per_launch_kb(fetch_csv, kernel)
+        w, _ = per_launch_kb(write_csv, kernel)
+        fetch_kb += f
+        write_kb += w
+        names.append(name)
+    name = " + ".join(names)
     scale = target / mib
     out = {
         "config": cfg,
