@@ -2349,7 +2349,7 @@ __global__ void transcode_ascii_kernel(const uint8_t* __restrict__ utf8, uint64_
 struct BitapParams {
   const uint8_t* ids;
   uint64_t n;
-  const uint64_t* mask_t;  // [(alphabet+1)][P] transposed masks
+  const void* mask_t;      // [(alphabet+1)][P] transposed masks, automaton words (uint32_t or uint64_t)
   const uint32_t* m;       // pattern length (graphemes)
   const uint32_t* k;       // edit budget per pattern
   uint32_t n_pat;
@@ -2362,7 +2362,9 @@ struct BitapParams {
 // initial state, so a segment starts `m + k` symbols early from the reference's initial state and
 // only reports ends inside its own range. Every hit covers [end - m - k, end) in the bitmap;
 // maximal runs of the bitmap are exactly the sorted + merged windows of prefilter.rs:334-342.
-template <int KMAX>
+// W: the automaton word (uint32_t when every pattern has m <= 32: half the VALU work of uint64_t);
+// KMAX: the largest edit budget (levels above a pattern's own k are computed but never read).
+template <int KMAX, typename W>
 __global__ __launch_bounds__(256) void bitap_kernel(BitapParams B) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -2376,40 +2378,59 @@ __global__ __launch_bounds__(256) void bitap_kernel(BitapParams B) {
   const uint32_t m = live ? B.m[p] : 1;
   const uint32_t k = live ? B.k[p] : 0;
   const uint64_t span = (uint64_t)m + k;
-  const uint64_t match_bit = 1ull << (m - 1);
-  uint64_t r[KMAX + 1];
+  const W match_bit = (W)1 << (m - 1);
+  W r[KMAX + 1];
 #pragma unroll
-  for (int d = 0; d <= KMAX; ++d) r[d] = d == 0 ? 0ull : ((1ull << d) - 1);
+  for (int d = 0; d <= KMAX; ++d) r[d] = d == 0 ? (W)0 : (W)(((W)1 << d) - 1);
   // Start 87 = 63 + 24 symbols early: from there on the automaton state equals the one obtained by
   // scanning from the text start (an alignment with <= k errors spans <= m + k symbols).
   const uint64_t warm = 63 + 24;
   const uint64_t s0 = a > warm ? a - warm : 0;
-  for (uint64_t i = s0; i < b; ++i) {
-    const uint32_t c = B.ids[i];  // wave-uniform
-    const uint64_t bc = live ? B.mask_t[(uint64_t)c * B.n_pat + p] : 0ull;
-    uint64_t prev_old = r[0];
-    uint64_t prev_new = ((r[0] << 1) | 1ull) & bc;
-    r[0] = prev_new;
-    uint64_t hit_level = (k == 0) ? prev_new : 0ull;
+  // Symbols come in 64 at a time (lane l loads symbol i0 + l, broadcast by readlane) and each lane
+  // issues the masks of 8 symbols before stepping through them, so the loop waits on one memory
+  // round trip per 8 symbols instead of two per symbol.
+  constexpr uint32_t U = 8;
+  const W* mask_p = static_cast<const W*>(B.mask_t) + (live ? p : 0u);  // this lane's column
+  for (uint64_t i0 = s0; i0 < b; i0 += 64) {
+    const uint32_t cl = i0 + lane < b ? (uint32_t)B.ids[i0 + lane] : 0u;
+    const uint32_t nsym = (uint32_t)min((uint64_t)64, b - i0);
+    for (uint32_t u0 = 0; u0 < nsym; u0 += U) {
+      W bcs[U];
 #pragma unroll
-    for (int d = 1; d <= KMAX; ++d) {
-      const uint64_t old = r[d];
-      const uint64_t nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | 1ull;
-      r[d] = nv;  // levels above k are computed but never read
-      prev_old = old;
-      prev_new = nv;
-      if ((uint32_t)d == k) hit_level = nv;
-    }
-    if (live && i >= a && (hit_level & match_bit)) {  // R[k] subsumes the lower levels
-      const uint64_t end = i + 1;
-      const uint64_t ws = end > span ? end - span : 0;
-      for (uint64_t x = ws; x < end;) {  // set bits [ws, end)
-        const uint64_t word = x >> 5;
-        const uint32_t lo = (uint32_t)(x & 31);
-        const uint32_t cnt = (uint32_t)min((uint64_t)(32 - lo), end - x);
-        const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << lo;
-        atomicOr(B.cover + word, bits);
-        x += cnt;
+      for (uint32_t q = 0; q < U; ++q) {
+        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, (int)(u0 + q));  // u0 + q < 64: wave-uniform
+        bcs[q] = (live && u0 + q < nsym) ? mask_p[(size_t)c * B.n_pat] : (W)0;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < U; ++q) {
+        if (u0 + q >= nsym) break;
+        const uint64_t i = i0 + u0 + q;
+        const W bc = bcs[q];
+        W prev_old = r[0];
+        W prev_new = ((r[0] << 1) | (W)1) & bc;
+        r[0] = prev_new;
+        W hit_level = (k == 0) ? prev_new : (W)0;
+#pragma unroll
+        for (int d = 1; d <= KMAX; ++d) {
+          const W old = r[d];
+          const W nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | (W)1;
+          r[d] = nv;  // levels above k are computed but never read
+          prev_old = old;
+          prev_new = nv;
+          if ((uint32_t)d == k) hit_level = nv;
+        }
+        if (live && i >= a && (hit_level & match_bit)) {  // R[k] subsumes the lower levels
+          const uint64_t end = i + 1;
+          const uint64_t ws = end > span ? end - span : 0;
+          for (uint64_t x = ws; x < end;) {  // set bits [ws, end)
+            const uint64_t word = x >> 5;
+            const uint32_t lo = (uint32_t)(x & 31);
+            const uint32_t cnt = (uint32_t)min((uint64_t)(32 - lo), end - x);
+            const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << lo;
+            atomicOr(B.cover + word, bits);
+            x += cnt;
+          }
+        }
       }
     }
   }
@@ -2633,6 +2654,12 @@ int upload_engine(Engine& e, std::string& err) {
     for (size_t p = 0; p < np; ++p)
       for (size_t c = 0; c < A; ++c) mt[c * np + p] = e.bp_mask[p * A + c];
     if ((rc = upload(mt, &e.d_bp_mask, err))) return rc;
+    // 32-bit copy for engines whose patterns all fit a 32-bit automaton word (half the mask reads)
+    if (!e.bp_m.empty() && *std::max_element(e.bp_m.begin(), e.bp_m.end()) <= 32) {
+      std::vector<uint32_t> mt32(mt.size());
+      for (size_t i = 0; i < mt.size(); ++i) mt32[i] = (uint32_t)mt[i];
+      if ((rc = upload(mt32, &e.d_bp_mask32, err))) return rc;
+    }
     std::vector<uint8_t> aid(e.ascii_id, e.ascii_id + 128);
     if ((rc = upload(aid, &e.d_ascii_id, err))) return rc;
   }
@@ -2646,7 +2673,7 @@ void free_engine_device(Engine& e) {
   if (e.d_nodes == nullptr && e.stream == nullptr) return;
   (void)hipSetDevice(e.device);
   void* ptrs[] = {e.d_nodes, e.d_out_range, e.d_pidx, e.d_edges, e.d_out_pat, e.d_sb_edge, e.d_gt, e.d_aux, e.d_pat_bytes, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
-                  e.d_sim_vals, e.d_bp_mask, e.d_ascii_id, e.d_edge_gid, e.d_ascii_gid, e.d_map_range,
+                  e.d_sim_vals, e.d_bp_mask, e.d_bp_mask32, e.d_ascii_id, e.d_edge_gid, e.d_ascii_gid, e.d_map_range,
                   e.d_map_ent, e.d_map_hay};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -3509,11 +3536,24 @@ int prefilter_windows(const Engine& e, const Haystack& h, const std::vector<uint
   const uint64_t waves = segs * ((np + 63) / 64);
   const uint32_t kmax = ks.empty() ? 0 : *std::max_element(ks.begin(), ks.end());
   const dim3 bgrid((uint32_t)((waves + 3) / 4));
-  if (kmax <= 2) hipLaunchKernelGGL((bitap_kernel<2>), bgrid, dim3(256), 0, stream, B);
-  else if (kmax <= 4) hipLaunchKernelGGL((bitap_kernel<4>), bgrid, dim3(256), 0, stream, B);
-  else if (kmax <= 8) hipLaunchKernelGGL((bitap_kernel<8>), bgrid, dim3(256), 0, stream, B);
-  else if (kmax <= 16) hipLaunchKernelGGL((bitap_kernel<16>), bgrid, dim3(256), 0, stream, B);
-  else hipLaunchKernelGGL((bitap_kernel<24>), bgrid, dim3(256), 0, stream, B);
+  const uint32_t mmax = np ? *std::max_element(e.bp_m.begin(), e.bp_m.begin() + np) : 0u;
+  if (mmax <= 32 && e.d_bp_mask32) {
+    B.mask_t = e.d_bp_mask32;
+    if (kmax == 0) hipLaunchKernelGGL((bitap_kernel<0, uint32_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax == 1) hipLaunchKernelGGL((bitap_kernel<1, uint32_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax == 2) hipLaunchKernelGGL((bitap_kernel<2, uint32_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 4) hipLaunchKernelGGL((bitap_kernel<4, uint32_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 8) hipLaunchKernelGGL((bitap_kernel<8, uint32_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 16) hipLaunchKernelGGL((bitap_kernel<16, uint32_t>), bgrid, dim3(256), 0, stream, B);
+    else hipLaunchKernelGGL((bitap_kernel<24, uint32_t>), bgrid, dim3(256), 0, stream, B);
+  } else {
+    if (kmax <= 1) hipLaunchKernelGGL((bitap_kernel<1, uint64_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 2) hipLaunchKernelGGL((bitap_kernel<2, uint64_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 4) hipLaunchKernelGGL((bitap_kernel<4, uint64_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 8) hipLaunchKernelGGL((bitap_kernel<8, uint64_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 16) hipLaunchKernelGGL((bitap_kernel<16, uint64_t>), bgrid, dim3(256), 0, stream, B);
+    else hipLaunchKernelGGL((bitap_kernel<24, uint64_t>), bgrid, dim3(256), 0, stream, B);
+  }
   HIP_TRY(hipGetLastError());
   uint64_t cap = 1 << 16;
   HIP_TRY(d_cnt.alloc(8, stream));
