@@ -338,8 +338,6 @@ struct Engine {
   float* d_sim_ascii = nullptr;
   uint64_t* d_sim_keys = nullptr;
   float* d_sim_vals = nullptr;
-  uint64_t* d_bp_mask = nullptr;
-  uint32_t* d_bp_mask32 = nullptr;  // the same masks as 32-bit words (every pattern m <= 32)
   uint8_t* d_ascii_id = nullptr;
   uint32_t* d_edge_gid = nullptr;
   uint32_t* d_ascii_gid = nullptr;

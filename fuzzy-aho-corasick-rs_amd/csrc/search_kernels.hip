@@ -2349,39 +2349,62 @@ __global__ void transcode_ascii_kernel(const uint8_t* __restrict__ utf8, uint64_
 struct BitapParams {
   const uint8_t* ids;
   uint64_t n;
-  const void* mask_t;      // [(alphabet+1)][P] transposed masks, automaton words (uint32_t or uint64_t)
-  const uint32_t* m;       // pattern length (graphemes)
-  const uint32_t* k;       // edit budget per pattern
-  uint32_t n_pat;
+  const void* mask_t;      // [(alphabet+1)][n_words] transposed packed masks (uint32_t or uint64_t words)
+  const void* top;         // per word: the top (match) bit of every pattern packed into it
+  const uint32_t* k;       // per word: the edit budget shared by its patterns
+  uint32_t n_words;
   uint32_t seg_len;        // text positions owned by one wave
   uint32_t* cover;         // coverage bitmap, 1 bit per grapheme
 };
 
-// Each lane runs one pattern's shift-AND automaton over the wave's text segment
-// (bitap_windows, prefilter.rs:410-435). The state after `m + k` symbols no longer depends on the
-// initial state, so a segment starts `m + k` symbols early from the reference's initial state and
-// only reports ends inside its own range. Every hit covers [end - m - k, end) in the bitmap;
-// maximal runs of the bitmap are exactly the sorted + merged windows of prefilter.rs:334-342.
+// Shift-AND over several patterns per automaton word: the patterns of one edit budget are packed
+// side by side (pattern f in bits lo_f..top_f). Every recurrence of bitap_windows
+// (prefilter.rs:410-435) only moves bits upwards by one, so a pattern's top bit carries into the next
+// pattern's bit 0 only, and that bit is forced to 1 in every level (the `| 1` of the recurrence,
+// here `| first`) -- level 0 ANDs the carried bit with the same mask bit as the forced one. Bits
+// 0..m-1 of every field therefore evolve exactly as in a word of their own; the reference's bits at
+// and above m never reach below m, so dropping them changes nothing observable.
+template <typename W>
+__device__ __forceinline__ W low_bits(uint32_t n) {
+  return n >= sizeof(W) * 8 ? ~(W)0 : (((W)1 << n) - (W)1);
+}
+
+// Each lane runs one packed word over the wave's text segment. The state after `m + k` symbols no
+// longer depends on the initial state, so a segment starts `m + k` symbols early from the
+// reference's initial state and only reports ends inside its own range. Every hit of pattern f
+// covers [end - m_f - k, end) in the bitmap; maximal runs of the bitmap are exactly the sorted +
+// merged windows of prefilter.rs:334-342.
 // W: the automaton word (uint32_t when every pattern has m <= 32: half the VALU work of uint64_t);
-// KMAX: the largest edit budget (levels above a pattern's own k are computed but never read).
+// KMAX: the largest edit budget (levels above a word's own k are computed but never read).
 template <int KMAX, typename W>
 __global__ __launch_bounds__(256) void bitap_kernel(BitapParams B) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t pat_groups = (B.n_pat + 63) / 64;
-  const uint64_t seg = wave / pat_groups;
-  const uint32_t p = (wave % pat_groups) * 64 + lane;
+  const uint32_t word_groups = (B.n_words + 63) / 64;
+  const uint64_t seg = wave / word_groups;
+  const uint32_t p = (wave % word_groups) * 64 + lane;
   const uint64_t a = seg * B.seg_len;
   if (a >= B.n) return;
   const uint64_t b = min(a + (uint64_t)B.seg_len, B.n);
-  const bool live = p < B.n_pat;
-  const uint32_t m = live ? B.m[p] : 1;
+  const bool live = p < B.n_words;
+  const W top = live ? static_cast<const W*>(B.top)[p] : (W)0;
   const uint32_t k = live ? B.k[p] : 0;
-  const uint64_t span = (uint64_t)m + k;
-  const W match_bit = (W)1 << (m - 1);
+  const W first = (W)(top << 1) | (W)1;  // bit 0 of every field
   W r[KMAX + 1];
+  // initial state R[d] = (1 << d) - 1 per pattern (prefilter.rs:417), clipped to the field
 #pragma unroll
-  for (int d = 0; d <= KMAX; ++d) r[d] = d == 0 ? (W)0 : (W)(((W)1 << d) - 1);
+  for (int d = 0; d <= KMAX; ++d) r[d] = 0;
+  {
+    uint32_t lo = 0;
+    for (W t = top; t;) {
+      const uint32_t hi = (uint32_t)__builtin_ctzll((unsigned long long)t);
+      t &= t - 1;
+      const uint32_t m = hi + 1 - lo;
+#pragma unroll
+      for (int d = 1; d <= KMAX; ++d) r[d] |= low_bits<W>(min((uint32_t)d, m)) << lo;
+      lo = hi + 1;
+    }
+  }
   // Start 87 = 63 + 24 symbols early: from there on the automaton state equals the one obtained by
   // scanning from the text start (an alignment with <= k errors spans <= m + k symbols).
   const uint64_t warm = 63 + 24;
@@ -2399,7 +2422,7 @@ __global__ __launch_bounds__(256) void bitap_kernel(BitapParams B) {
 #pragma unroll
       for (uint32_t q = 0; q < U; ++q) {
         const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, (int)(u0 + q));  // u0 + q < 64: wave-uniform
-        bcs[q] = (live && u0 + q < nsym) ? mask_p[(size_t)c * B.n_pat] : (W)0;
+        bcs[q] = (live && u0 + q < nsym) ? mask_p[(size_t)c * B.n_words] : (W)0;
       }
 #pragma unroll
       for (uint32_t q = 0; q < U; ++q) {
@@ -2407,29 +2430,37 @@ __global__ __launch_bounds__(256) void bitap_kernel(BitapParams B) {
         const uint64_t i = i0 + u0 + q;
         const W bc = bcs[q];
         W prev_old = r[0];
-        W prev_new = ((r[0] << 1) | (W)1) & bc;
+        W prev_new = ((r[0] << 1) | first) & bc;
         r[0] = prev_new;
         W hit_level = (k == 0) ? prev_new : (W)0;
 #pragma unroll
         for (int d = 1; d <= KMAX; ++d) {
           const W old = r[d];
-          const W nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | (W)1;
+          const W nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | first;
           r[d] = nv;  // levels above k are computed but never read
           prev_old = old;
           prev_new = nv;
           if ((uint32_t)d == k) hit_level = nv;
         }
-        if (live && i >= a && (hit_level & match_bit)) {  // R[k] subsumes the lower levels
+        W hits = hit_level & top;  // R[k] subsumes the lower levels
+        if (live && i >= a && hits) {
           const uint64_t end = i + 1;
-          const uint64_t ws = end > span ? end - span : 0;
-          for (uint64_t x = ws; x < end;) {  // set bits [ws, end)
-            const uint64_t word = x >> 5;
-            const uint32_t lo = (uint32_t)(x & 31);
-            const uint32_t cnt = (uint32_t)min((uint64_t)(32 - lo), end - x);
-            const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << lo;
-            atomicOr(B.cover + word, bits);
-            x += cnt;
-          }
+          do {
+            const uint32_t hi = (uint32_t)__builtin_ctzll((unsigned long long)hits);
+            hits &= hits - 1;
+            const W below = top & low_bits<W>(hi);  // tops of the fields under this one
+            const uint32_t lo = below ? 64u - (uint32_t)__builtin_clzll((unsigned long long)below) : 0u;
+            const uint64_t span = (uint64_t)(hi + 1 - lo) + k;
+            const uint64_t ws = end > span ? end - span : 0;
+            for (uint64_t x = ws; x < end;) {  // set bits [ws, end)
+              const uint64_t w = x >> 5;
+              const uint32_t l = (uint32_t)(x & 31);
+              const uint32_t cnt = (uint32_t)min((uint64_t)(32 - l), end - x);
+              const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << l;
+              atomicOr(B.cover + w, bits);
+              x += cnt;
+            }
+          } while (hits);
         }
       }
     }
@@ -2648,18 +2679,7 @@ int upload_engine(Engine& e, std::string& err) {
     if ((rc = upload(e.map_hay, &e.d_map_hay, err))) return rc;
   }
   if (e.bitap_ok) {
-    // transposed masks [(alphabet+1)][P] so the lanes of a wave (consecutive patterns) coalesce
-    const size_t np = e.bp_m.size(), A = e.alphabet + 1;
-    std::vector<uint64_t> mt(A * np);
-    for (size_t p = 0; p < np; ++p)
-      for (size_t c = 0; c < A; ++c) mt[c * np + p] = e.bp_mask[p * A + c];
-    if ((rc = upload(mt, &e.d_bp_mask, err))) return rc;
-    // 32-bit copy for engines whose patterns all fit a 32-bit automaton word (half the mask reads)
-    if (!e.bp_m.empty() && *std::max_element(e.bp_m.begin(), e.bp_m.end()) <= 32) {
-      std::vector<uint32_t> mt32(mt.size());
-      for (size_t i = 0; i < mt.size(); ++i) mt32[i] = (uint32_t)mt[i];
-      if ((rc = upload(mt32, &e.d_bp_mask32, err))) return rc;
-    }
+    // the packed masks depend on the per-call edit budgets: prefilter_windows builds them
     std::vector<uint8_t> aid(e.ascii_id, e.ascii_id + 128);
     if ((rc = upload(aid, &e.d_ascii_id, err))) return rc;
   }
@@ -2673,7 +2693,7 @@ void free_engine_device(Engine& e) {
   if (e.d_nodes == nullptr && e.stream == nullptr) return;
   (void)hipSetDevice(e.device);
   void* ptrs[] = {e.d_nodes, e.d_out_range, e.d_pidx, e.d_edges, e.d_out_pat, e.d_sb_edge, e.d_gt, e.d_aux, e.d_pat_bytes, e.d_pats, e.d_sim_ascii, e.d_sim_keys,
-                  e.d_sim_vals, e.d_bp_mask, e.d_bp_mask32, e.d_ascii_id, e.d_edge_gid, e.d_ascii_gid, e.d_map_range,
+                  e.d_sim_vals, e.d_ascii_id, e.d_edge_gid, e.d_ascii_gid, e.d_map_range,
                   e.d_map_ent, e.d_map_hay};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -3501,7 +3521,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const std::vector<uint
   const uint64_t n = h.n;
   if (n == 0) return FAC_OK;
   const uint32_t np = (uint32_t)e.bp_m.size();
-  DevBuf d_ids, d_m, d_k, d_cover, d_runs, d_cnt;
+  DevBuf d_ids, d_k, d_cover, d_runs, d_cnt;
   HIP_TRY(d_ids.alloc(n + 16, stream));
   if (h.ascii) {
     const uint64_t threads = (n + 15) / 16;
@@ -3512,10 +3532,56 @@ int prefilter_windows(const Engine& e, const Haystack& h, const std::vector<uint
     ensure_symbols(e, h);
     HIP_TRY(hipMemcpyAsync(d_ids.p, h.sym.data(), n, hipMemcpyHostToDevice, stream));
   }
-  HIP_TRY(d_m.alloc(np * 4, stream));
-  HIP_TRY(d_k.alloc(np * 4, stream));
-  HIP_TRY(hipMemcpyAsync(d_m.p, e.bp_m.data(), np * 4, hipMemcpyHostToDevice, stream));
-  HIP_TRY(hipMemcpyAsync(d_k.p, ks.data(), np * 4, hipMemcpyHostToDevice, stream));
+  // Pack the patterns into automaton words: patterns of one edit budget, longest first, each into
+  // the first word with room (first-fit decreasing); 32-bit words when every pattern fits one.
+  const uint32_t mmax = np ? *std::max_element(e.bp_m.begin(), e.bp_m.begin() + np) : 0u;
+  const bool w32 = mmax <= 32;
+  const uint32_t wbits = w32 ? 32u : 64u;
+  std::vector<uint32_t> order(np);
+  for (uint32_t i = 0; i < np; ++i) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+    return ks[x] != ks[y] ? ks[x] < ks[y] : (e.bp_m[x] != e.bp_m[y] ? e.bp_m[x] > e.bp_m[y] : x < y);
+  });
+  std::vector<uint32_t> wk, wused;                   // per word: edit budget, bits used
+  std::vector<std::pair<uint32_t, uint32_t>> place(np);  // pattern -> (word, bit offset)
+  uint32_t k_first_word = 0;                         // words of the current budget start here
+  for (uint32_t idx = 0; idx < np; ++idx) {
+    const uint32_t i = order[idx], m = e.bp_m[i];
+    if (idx && ks[i] != ks[order[idx - 1]]) k_first_word = (uint32_t)wk.size();
+    uint32_t w = k_first_word;
+    while (w < wk.size() && wused[w] + m > wbits) ++w;
+    if (w == wk.size()) {
+      wk.push_back(ks[i]);
+      wused.push_back(0);
+    }
+    place[i] = {w, wused[w]};
+    wused[w] += m;
+  }
+  const uint32_t nw = (uint32_t)wk.size();
+  const uint32_t rows = e.alphabet + 1;
+  std::vector<uint64_t> pmask((size_t)rows * nw, 0), ptop(nw, 0);
+  for (uint32_t i = 0; i < np; ++i) {
+    const uint32_t w = place[i].first, off = place[i].second;
+    ptop[w] |= 1ull << (off + e.bp_m[i] - 1);
+    for (uint32_t c = 0; c < rows; ++c) pmask[(size_t)c * nw + w] |= e.bp_mask[(size_t)i * rows + c] << off;
+  }
+  DevBuf d_pmask, d_ptop;
+  if (w32) {
+    std::vector<uint32_t> m32(pmask.begin(), pmask.end()), t32(ptop.begin(), ptop.end());
+    HIP_TRY(d_pmask.alloc(m32.size() * 4, stream));
+    HIP_TRY(d_ptop.alloc(t32.size() * 4, stream));
+    HIP_TRY(hipMemcpyAsync(d_pmask.p, m32.data(), m32.size() * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_ptop.p, t32.data(), t32.size() * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipStreamSynchronize(stream));  // pageable sources: complete before the vectors go
+  } else {
+    HIP_TRY(d_pmask.alloc(pmask.size() * 8, stream));
+    HIP_TRY(d_ptop.alloc(ptop.size() * 8, stream));
+    HIP_TRY(hipMemcpyAsync(d_pmask.p, pmask.data(), pmask.size() * 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_ptop.p, ptop.data(), ptop.size() * 8, hipMemcpyHostToDevice, stream));
+  }
+  HIP_TRY(d_k.alloc(nw * 4, stream));
+  HIP_TRY(hipMemcpyAsync(d_k.p, wk.data(), nw * 4, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipStreamSynchronize(stream));  // pageable sources: complete before the vectors go
   const uint64_t n_words = (n + 31) / 32;
   HIP_TRY(d_cover.alloc(n_words * 4, stream));
   HIP_TRY(hipMemsetAsync(d_cover.p, 0, n_words * 4, stream));
@@ -3526,19 +3592,17 @@ int prefilter_windows(const Engine& e, const Haystack& h, const std::vector<uint
   BitapParams B{};
   B.ids = static_cast<const uint8_t*>(d_ids.p);
   B.n = n;
-  B.mask_t = e.d_bp_mask;
-  B.m = static_cast<const uint32_t*>(d_m.p);
+  B.mask_t = d_pmask.p;
+  B.top = d_ptop.p;
   B.k = static_cast<const uint32_t*>(d_k.p);
-  B.n_pat = np;
+  B.n_words = nw;
   B.seg_len = 4096;
   B.cover = static_cast<uint32_t*>(d_cover.p);
   const uint64_t segs = (n + B.seg_len - 1) / B.seg_len;
-  const uint64_t waves = segs * ((np + 63) / 64);
+  const uint64_t waves = segs * ((nw + 63) / 64);
   const uint32_t kmax = ks.empty() ? 0 : *std::max_element(ks.begin(), ks.end());
   const dim3 bgrid((uint32_t)((waves + 3) / 4));
-  const uint32_t mmax = np ? *std::max_element(e.bp_m.begin(), e.bp_m.begin() + np) : 0u;
-  if (mmax <= 32 && e.d_bp_mask32) {
-    B.mask_t = e.d_bp_mask32;
+  if (w32) {
     if (kmax == 0) hipLaunchKernelGGL((bitap_kernel<0, uint32_t>), bgrid, dim3(256), 0, stream, B);
     else if (kmax == 1) hipLaunchKernelGGL((bitap_kernel<1, uint32_t>), bgrid, dim3(256), 0, stream, B);
     else if (kmax == 2) hipLaunchKernelGGL((bitap_kernel<2, uint32_t>), bgrid, dim3(256), 0, stream, B);

@@ -148,6 +148,43 @@ def test_bitap_windows_match_reference_merge(seed, vocab, filler):
             assert got == want, f"patterns={pats!r} hay={hay!r} thr={thr}\n gpu={got}\n orc={want}"
 
 
+@pytest.mark.parametrize("long_patterns", [False, True])
+def test_bitap_packed_words_match_reference(long_patterns):
+    """Many patterns packed several to an automaton word (first-fit by edit budget): windows equal
+    the oracle's per-pattern bitap_windows + merge (prefilter.rs:319-342, 410-435). Lengths 1..20
+    (32-bit words) or 1..60 (64-bit words), mixed weights and per-pattern edit limits (several k
+    groups), planted fuzzy copies."""
+    from fuzzy_aho_corasick.engine import prefilter_windows
+    rng = Rng(0x5EED_B17A_9ACC_0001 ^ int(long_patterns))
+    alpha = "abcdefghij"
+    top = 60 if long_patterns else 20
+    pats = []
+    for i in range(300):
+        w = "".join(alpha[rng.next() % len(alpha)] for _ in range(1 + rng.next() % top))
+        p = Pattern(w).with_weight(0.7 + (rng.next() % 7) * 0.1)
+        if rng.next() % 3 == 0:
+            p = p.fuzzy(L().edits(rng.next() % 3))
+        pats.append(p)
+    hay = []
+    for _ in range(400):
+        if rng.next() % 4 == 0:
+            w = list(pats[rng.next() % len(pats)].pattern)
+            if w and rng.next() % 2:
+                w[rng.next() % len(w)] = alpha[rng.next() % len(alpha)]
+            hay.append("".join(w))
+        else:
+            hay.append("".join(alpha[rng.next() % len(alpha)] for _ in range(1 + rng.next() % 12)))
+    hay = " ".join(hay)
+    b = B().fuzzy(L().edits(2))
+    gpu = b.build(pats)
+    orc = OracleEngine(b, pats)
+    for thr in (0.75, 0.85, 0.95):
+        want = orc.prefilter_windows(hay, thr)
+        got = prefilter_windows(gpu, hay, thr)
+        assert got == want, f"thr={thr}: {len(got)} vs {len(want)} windows"
+    compare(b, pats, hay, 0.85, prefilter=True)
+
+
 def test_edge_inputs():
     b = B().fuzzy(L().edits(2))
     compare(b, ["abc"], "", 0.0)                      # empty haystack
