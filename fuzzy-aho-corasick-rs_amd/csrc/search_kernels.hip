@@ -1671,7 +1671,7 @@ __device__ __forceinline__ bool rc_selected(const unsigned long long* keys, cons
                                             uint32_t thr) {
   return keys[s] != 0ull && cnt[s] >= thr;
 }
-__global__ __launch_bounds__(256) void rc_sel_count_kernel(const unsigned long long* keys, const uint32_t* cnt,
+__global__ __launch_bounds__(64) void rc_sel_count_kernel(const unsigned long long* keys, const uint32_t* cnt,
                                                            uint32_t n_slots, uint32_t range, uint32_t thr,
                                                            uint32_t* bcount) {
   __shared__ uint32_t tot;
@@ -1685,26 +1685,26 @@ __global__ __launch_bounds__(256) void rc_sel_count_kernel(const unsigned long l
   __syncthreads();
   if (threadIdx.x == 0) bcount[blockIdx.x] = tot;
 }
-// one block: exclusive scan of nb (<= 8192) block counts in place; n_ent = the total
-__global__ __launch_bounds__(256) void rc_sel_scan_kernel(uint32_t* bcount, uint32_t nb, unsigned int* n_ent) {
-  __shared__ uint32_t c[8192];
-  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) c[i] = bcount[i];
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t run = 0;
-    for (uint32_t i = 0; i < nb; ++i) {
-      const uint32_t v = c[i];
-      c[i] = run;
-      run += v;
-    }
-    *n_ent = run;
+// one wave: exclusive scan of nb (<= 8192) block counts in place; n_ent = the total. Each lane
+// scans 128 consecutive counts. The numbering kernels run while the level-1 build's persistent
+// single-wave workgroups hold the CUs on the second stream, and every freed wave slot goes to the
+// build's next workgroup first: a 4-wave workgroup queued there 10 ms, a 1-wave one does not.
+__global__ __launch_bounds__(64) void rc_sel_scan_kernel(uint32_t* bcount, uint32_t nb, unsigned int* n_ent) {
+  const uint32_t base = lane_id() * 128;
+  uint32_t tot = 0;
+  for (uint32_t i = 0; i < 128; ++i) tot += base + i < nb ? bcount[base + i] : 0u;
+  const uint32_t incl = wave_inclusive_sum(tot);
+  uint32_t run = incl - tot;
+  if (lane_id() == 63) *n_ent = incl;
+  for (uint32_t i = 0; i < 128 && base + i < nb; ++i) {
+    const uint32_t v = bcount[base + i];
+    bcount[base + i] = run;
+    run += v;
   }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) bcount[i] = c[i];
 }
 // counts are read and replaced by entries in place (val may alias cnt: a slot is only touched by
 // its own thread); rep[entry] = the slot's representative window
-__global__ __launch_bounds__(256) void rc_sel_assign_kernel(const unsigned long long* keys, const uint32_t* cnt,
+__global__ __launch_bounds__(64) void rc_sel_assign_kernel(const unsigned long long* keys, const uint32_t* cnt,
                                                             const uint64_t* rep_slot, uint32_t* val, uint64_t* rep,
                                                             const uint32_t* bbase, uint32_t n_slots, uint32_t range,
                                                             uint32_t thr, uint32_t max_ent) {
@@ -2596,6 +2596,30 @@ bool debug_poison() {
 // RAII scratch. Plain hipMalloc/hipFree: with the stream-ordered pool (hipMallocAsync /
 // hipFreeAsync) on ROCm 7.2 the match counter of a recycled block intermittently came back short
 // (reproduced 6/60 calls; 0/60 with hipMalloc), so the pool is not used.
+// One pinned, device-mapped host word per host thread (kept for the thread's lifetime): kernels
+// store small results there directly, with no copy to queue behind other streams' work.
+int pinned_word(unsigned int*& host, unsigned int*& dev, std::string& err) {
+  thread_local unsigned int* h = nullptr;
+  if (!h) {
+    void* p = nullptr;
+    const hipError_t e = hipHostMalloc(&p, 64, hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) {
+      err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
+      return FAC_E_HIP;
+    }
+    h = static_cast<unsigned int*>(p);
+  }
+  void* d = nullptr;
+  const hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+  if (e != hipSuccess) {
+    err = std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e);
+    return FAC_E_HIP;
+  }
+  host = h;
+  dev = static_cast<unsigned int*>(d);
+  return FAC_OK;
+}
+
 struct DevBuf {
   void* p = nullptr;
   hipStream_t s = nullptr;
@@ -3022,18 +3046,24 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
                               uint32_t n_slots, uint32_t thr, uint32_t cap, unsigned int& n) -> int {
       const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(8192, n_slots / 4096));
       const uint32_t range = (n_slots + nb - 1) / nb;  // n_slots and nb are powers of two: a multiple of 256
-      unsigned int* n_dev = reinterpret_cast<unsigned int*>(static_cast<unsigned long long*>(d_rcn.p) + 2);
-      hipLaunchKernelGGL(rc_sel_count_kernel, dim3(nb), dim3(256), 0, stream,
+      // the count comes back through pinned host memory written by the scan kernel: a 4-byte D2H copy
+      // is a blit workgroup that queued 9 ms behind the level-1 build's waves on the second stream
+      unsigned int* n_host = nullptr;
+      unsigned int* n_dev = nullptr;
+      if (int hrc = pinned_word(n_host, n_dev, err)) return hrc;
+      *reinterpret_cast<volatile unsigned int*>(n_host) = 0u;
+      // single-wave workgroups throughout (see rc_sel_scan_kernel)
+      hipLaunchKernelGGL(rc_sel_count_kernel, dim3(nb), dim3(64), 0, stream,
                          static_cast<const unsigned long long*>(keys.p), static_cast<const uint32_t*>(cv.p), n_slots,
                          range, thr, static_cast<uint32_t*>(d_rcb.p));
-      hipLaunchKernelGGL(rc_sel_scan_kernel, dim3(1), dim3(256), 0, stream, static_cast<uint32_t*>(d_rcb.p), nb, n_dev);
-      hipLaunchKernelGGL(rc_sel_assign_kernel, dim3(nb), dim3(256), 0, stream,
+      hipLaunchKernelGGL(rc_sel_scan_kernel, dim3(1), dim3(64), 0, stream, static_cast<uint32_t*>(d_rcb.p), nb, n_dev);
+      hipLaunchKernelGGL(rc_sel_assign_kernel, dim3(nb), dim3(64), 0, stream,
                          static_cast<const unsigned long long*>(keys.p), static_cast<const uint32_t*>(cv.p),
                          static_cast<const uint64_t*>(rslot.p), static_cast<uint32_t*>(cv.p),
                          static_cast<uint64_t*>(rep.p), static_cast<const uint32_t*>(d_rcb.p), n_slots, range, thr, cap);
       HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(&n, n_dev, sizeof(n), hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
+      n = *reinterpret_cast<volatile unsigned int*>(n_host);
       return FAC_OK;
     };
     uint32_t n_ent1 = 0;
@@ -3089,7 +3119,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     } l1_done_guard{l1_done};
     std::vector<RcTable> tabs;  // built levels, ascending k: a build resumes its representatives from them
     const uint64_t ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", 4)));
-    auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, hipStream_t bs) -> int {
+    auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, hipStream_t bs, bool cleared = false) -> int {
       SearchParams Q = P;
       Q.rc_mode = 2;
       Q.rc_k = T.k;
@@ -3109,7 +3139,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       Q.spill = static_cast<uint64_t*>(d_spill.p);
       Q.spill_cap = spill_cap;
       Q.counters = static_cast<unsigned long long*>(d_cnt.p);
-      HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), bs));
+      if (!cleared) HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), bs));
       launch_rc_build(qbuild, std::min<uint32_t>(n_ent, max_grid), bs, Q);
       const hipError_t le = hipGetLastError();
       if (le != hipSuccess) {
@@ -3120,11 +3150,22 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     };
     // after its build a level's entries are published into an exact-key lookup table (4 slots per
     // entry: a miss usually ends at the first probe)
-    auto publish = [&](RcTable& T, uint32_t n_ent, DevBuf& ct, hipStream_t bs) -> int {
+    auto ct_slots = [&](uint32_t n_ent) {
       uint32_t cs = 1u << 12;
       while (cs < ct_mult * n_ent && cs < (1u << 28)) cs <<= 1;
+      return cs;
+    };
+    auto clear_ct = [&](uint32_t n_ent, DevBuf& ct, hipStream_t bs) -> int {
+      const uint32_t cs = ct_slots(n_ent);
       HIP_TRY(ct.alloc((size_t)cs * 2 * sizeof(uint4), bs));
       HIP_TRY(hipMemsetAsync(ct.p, 0, (size_t)cs * 2 * sizeof(uint4), bs));
+      return FAC_OK;
+    };
+    auto publish = [&](RcTable& T, uint32_t n_ent, DevBuf& ct, hipStream_t bs, bool cleared = false) -> int {
+      const uint32_t cs = ct_slots(n_ent);
+      if (!cleared) {
+        if (int crc = clear_ct(n_ent, ct, bs)) return crc;
+      }
       hipLaunchKernelGGL(rc_publish_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_ent + 255) / 256, cus * 8))),
                          dim3(256), 0, bs, static_cast<const uint4*>(P.rc_pool), T.off, T.count, n_ent, T.k,
                          static_cast<uint4*>(ct.p), cs - 1);
@@ -3157,13 +3198,17 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     auto launch_l1 = [&]() -> int {
       if (l1_launched || !n_ent1) return FAC_OK;
       l1_launched = true;
+      // the build's counters are cleared here: a fill queued on the second stream behind the
+      // sampled-level count kernel's workgroups started the build 2.6 ms late
+      HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), stream));
+      if (int crc = clear_ct(n_ent1, d_ct[0], stream)) return crc;  // likewise the lookup table
       if (bstream != stream) {
         HIP_TRY(hipEventRecord(l1_done, stream));  // everything so far (counts, pool, clears) first
         HIP_TRY(hipStreamWaitEvent(bstream, l1_done, 0));
       }
-      int brc = build(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p), bstream);
+      int brc = build(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p), bstream, true);
       if (brc) return brc;
-      if ((brc = publish(L1, n_ent1, d_ct[0], bstream))) return brc;
+      if ((brc = publish(L1, n_ent1, d_ct[0], bstream, true))) return brc;
       if (bstream != stream) HIP_TRY(hipEventRecord(l1_done, bstream));
       tabs.push_back(L1);
       return FAC_OK;
