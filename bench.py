@@ -21,7 +21,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "fuzzy-aho-corasick-rs_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-DEFAULT_MIB = {"c1": 1, "c2": 64, "c3": 256, "c4": 128, "c5": 256}
+DEFAULT_MIB = {"c1": 1, "c2": 1024, "c3": 256, "c4": 128, "c5": 256}  # C2: the 1 GB of BASELINE configs[1]
 
 
 def parse():
