@@ -3099,7 +3099,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (k2) ks.push_back(std::min<uint32_t>(8, k2));
     } else {
       const char* le = std::getenv("FAC_RC_LEVELS");
-      std::string spec = le ? le : "5,6";  // with the lane-serial kernel an 8-char level no longer pays (C3 156 -> 147 ms)
+      // with the lane-serial kernel an 8-char level no longer pays (C3 156 -> 147 ms); one-edit
+      // engines finish most windows within 5 chars, and a 6-char level costs them more in counts
+      // and lookup probes than it saves (C2 1 GiB: 266 -> 188 ms per step with "5" alone)
+      std::string spec = le ? le : (e.mef <= 1u ? "5" : "5,6");
       for (size_t a = 0; a < spec.size();) {
         const size_t b = spec.find(',', a);
         const uint32_t k = (uint32_t)std::strtoul(spec.substr(a, b == std::string::npos ? std::string::npos : b - a).c_str(), nullptr, 10);
