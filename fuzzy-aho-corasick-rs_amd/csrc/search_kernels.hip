@@ -1661,8 +1661,8 @@ __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, unsigned 
           break;
         }
       }
-      if (kk == k) {
-        if (cnt[slot] < sat) atomicAdd(&cnt[slot], 1u);
+      if (kk == k) {  // sat == 1 (level 1 keeps every key): the inserter's count is all it needs
+        if (sat > 1u && cnt[slot] < sat) atomicAdd(&cnt[slot], 1u);
         break;
       }
     }
