@@ -2156,7 +2156,29 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   for (uint64_t cb = P.dyn_chunks ? next_chunk() : (uint64_t)blockIdx.x * P.chunk; cb < P.total_windows;
        cb = P.dyn_chunks ? next_chunk() : cb + stride) {
     const uint64_t ce = min(cb + (uint64_t)P.chunk, P.total_windows);
+    // A main pass behind the lookups (and the lane kernel) finds most windows already RC_DONE:
+    // one round of independent loads marks the chunk's 64-window groups that hold live windows,
+    // and the rest are skipped without their dependent segment / hit / pops loads (C2 1 GiB: 6K
+    // live windows out of 1G).
+    uint64_t live_groups = ~0ull;
+    if (!LK && P.rc_mode == 1 && !P.win_list) {
+      live_groups = 0ull;
+      const uint32_t ng = (uint32_t)((ce - cb + 63) / 64);  // P.chunk <= 4096: at most 64 groups
+      const uint32_t* hx = reinterpret_cast<const uint32_t*>(P.rc_hits);
+      for (uint32_t g = 0; g < ng; g += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+          const uint64_t v = cb + (uint64_t)(g + q) * 64 + lane;
+          x[q] = (g + q < ng && v < ce) ? hx[4 * v] : RC_DONE;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q)
+          if (__ballot(x[q] != RC_DONE)) live_groups |= 1ull << (g + q);
+      }
+    }
     for (uint64_t v0 = cb; v0 < ce; v0 += 64) {
+      if (!((live_groups >> ((v0 - cb) >> 6)) & 1ull)) continue;
       const uint64_t v = v0 + lane;
       bool active = v < ce;
       uint32_t kl = 0;
@@ -3321,8 +3343,12 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   }
   const double t_cache = host_ms();
   double t_dev = 0.0;
+  const uint32_t rc_chunk = (uint32_t)std::min<unsigned long>(4096, std::max<unsigned long>(64,
+      std::getenv("FAC_RC_CHUNK") ? std::strtoul(std::getenv("FAC_RC_CHUNK"), nullptr, 10) : 1024ul));
   for (;;) {
-    P.chunk = P.win_list ? 1u : 256u;  // spilled windows are few and heavy: one per block turn
+    // spilled windows are few and heavy: one per block turn; behind the prefix-cache lookups most
+    // windows are done, so chunks are larger (fewer hand-out atomics; the group prescan skips them)
+    P.chunk = P.win_list ? 1u : (P.rc_mode == 1 ? rc_chunk : 256u);
     P.total_windows = pass_windows;
     const uint64_t want = (pass_windows + P.chunk - 1) / P.chunk;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, max_grid));
