@@ -2161,7 +2161,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
     // and the rest are skipped without their dependent segment / hit / pops loads (C2 1 GiB: 6K
     // live windows out of 1G).
     uint64_t live_groups = ~0ull;
-    if (!LK && P.rc_mode == 1 && !P.win_list) {
+    if (!LK && P.rc_mode == 1 && !P.win_list && P.chunk > 256) {
       live_groups = 0ull;
       const uint32_t ng = (uint32_t)((ce - cb + 63) / 64);  // P.chunk <= 4096: at most 64 groups
       const uint32_t* hx = reinterpret_cast<const uint32_t*>(P.rc_hits);
@@ -3343,8 +3343,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   }
   const double t_cache = host_ms();
   double t_dev = 0.0;
+  // Main-pass chunk behind the prefix cache. Unbeamed windows left after the lookups and the lane
+  // kernel are few and cheap, and a wave's turn costs a hand-out atomic plus the group prescan, so
+  // chunks grow to 16 turns per wave (up to 4096 windows; C2 1 GiB: wave kernel 51 -> 4.5 ms).
+  // Beamed searches keep 256: their remaining windows are heavy and balance matters more (C3: 256
+  // -> 2048 costs 0.7 ms).
+  const uint64_t rc_auto = P.beam ? 256ull : std::min<uint64_t>(4096, std::max<uint64_t>(256, pass_windows / (16ull * max_grid)));
   const uint32_t rc_chunk = (uint32_t)std::min<unsigned long>(4096, std::max<unsigned long>(64,
-      std::getenv("FAC_RC_CHUNK") ? std::strtoul(std::getenv("FAC_RC_CHUNK"), nullptr, 10) : 1024ul));
+      std::getenv("FAC_RC_CHUNK") ? std::strtoul(std::getenv("FAC_RC_CHUNK"), nullptr, 10) : rc_auto));
   for (;;) {
     // spilled windows are few and heavy: one per block turn; behind the prefix-cache lookups most
     // windows are done, so chunks are larger (fewer hand-out atomics; the group prescan skips them)
