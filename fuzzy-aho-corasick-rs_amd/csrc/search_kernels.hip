@@ -2452,10 +2452,14 @@ __global__ __launch_bounds__(256) void bitap_kernel(BitapParams B) {
         const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, (int)(u0 + q));  // u0 + q < 64: wave-uniform
         bcs[q] = (live && u0 + q < nsym) ? mask_p[(size_t)c * B.n_words] : (W)0;
       }
+      // the hits of the 8 symbols are kept and only looked at when one of them is set (rare): the
+      // per-symbol path carries no segment-range compare and no divergent branch
+      W hq[U];
+#pragma unroll
+      for (uint32_t q = 0; q < U; ++q) hq[q] = (W)0;
 #pragma unroll
       for (uint32_t q = 0; q < U; ++q) {
         if (u0 + q >= nsym) break;
-        const uint64_t i = i0 + u0 + q;
         const W bc = bcs[q];
         W prev_old = r[0];
         W prev_new = ((r[0] << 1) | first) & bc;
@@ -2470,8 +2474,17 @@ __global__ __launch_bounds__(256) void bitap_kernel(BitapParams B) {
           prev_new = nv;
           if ((uint32_t)d == k) hit_level = nv;
         }
-        W hits = hit_level & top;  // R[k] subsumes the lower levels
-        if (live && i >= a && hits) {
+        hq[q] = hit_level & top;  // R[k] subsumes the lower levels
+      }
+      W any = (W)0;
+#pragma unroll
+      for (uint32_t q = 0; q < U; ++q) any |= hq[q];
+      if (live && any) {
+#pragma unroll
+        for (uint32_t q = 0; q < U; ++q) {
+          W hits = hq[q];
+          const uint64_t i = i0 + u0 + q;
+          if (!hits || i < a) continue;  // ends before the segment belong to the previous wave
           const uint64_t end = i + 1;
           do {
             const uint32_t hi = (uint32_t)__builtin_ctzll((unsigned long long)hits);
