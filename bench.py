@@ -4,16 +4,27 @@
 Workload (default): BASELINE.json configs[2] — edits=2, beam_width=64, 10K patterns,
 case-insensitive Unicode graphemes, one MI355X per rank — on seeded synthetic data
 (fuzzy_aho_corasick/workloads.py, SURVEY.md §8(d) generator). A "step" is one pass of the hot path
-(FuzzyAhoCorasick::search_raw over every start window of the rank's staged haystack, device
-resident) plus, for N > 1, the RCCL gather of the 32-byte Match records to rank 0. Weak scaling:
-each rank owns its own haystack of the same size (the C4 batch layout).
+(FuzzyAhoCorasick::search_raw over every start window of the rank's device-resident haystack) with
+the 32-byte Match records delivered to rank 0's host memory: at N = 1 straight D2H, at N > 1 sent
+from each rank's HBM to rank 0 over RCCL (counts all-gather + point-to-point sends) and then D2H.
 
-    python bench.py [--gpus N --steps K --warmup W --config c3 --mib 16]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+Modes:
+  default (weak scaling, the C4 batch layout): every rank owns its own haystack of the size;
+  --shard (strong scaling): one haystack; every rank stages only its halo-sliced shard;
+  --config c5: the 100 GiB streaming run (100 x a 1 GiB block, pre-filter on): each GPU processes
+    its 1/8 share (12.5 GiB) as device-resident stream windows (stream.rs window_matches).
+
+    python bench.py [--gpus N --steps K --warmup W --config c3 --mib 256 --shard]
+
+`--gpus N` with N > 1 outside torchrun re-launches this script under torch.distributed.run with N
+ranks (before any GPU call); under torchrun, --gpus must equal WORLD_SIZE.
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -21,58 +32,123 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "fuzzy-aho-corasick-rs_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-DEFAULT_MIB = {"c1": 1, "c2": 1024, "c3": 256, "c4": 128, "c5": 256}  # C2: the 1 GB of BASELINE configs[1]
+DEFAULT_MIB = {"c1": 1, "c2": 1024, "c3": 256, "c4": 128, "c5": 1024}  # C2: the 1 GB of BASELINE configs[1]
+# CPU baseline samples: prefixes of the same haystack for the all-cores leg
+CPU_PREFIX_MIB = {"c1": 1, "c2": 64, "c3": 16, "c4": 64, "c5": 64}
+WORKLOAD = {
+    "c1": "exact, 16 ASCII patterns",
+    "c2": "edits=1, 1K ASCII patterns",
+    "c3": "edits=2, beam_width=64, 10K patterns, case-insensitive Unicode graphemes",
+    "c4": "edits=1, 1K ASCII patterns (C2 engine), one 128 MiB haystack per GPU (seeds 40..47)",
+    "c5": "streaming, edits=1, 1K patterns (10-16), threshold 0.85, bitap prefilter, 1/8 of 100 GiB per GPU",
+}
+METRIC = "haystack Gchars/s at edits<=2, 10K patterns; 1/2/4/8 MI355X"
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
-    ap.add_argument("--mib", type=float, default=None, help="haystack MiB per rank per step")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--mib", type=float, default=None, help="haystack MiB per rank (c5: block MiB)")
+    ap.add_argument("--shard", action="store_true", help="strong scaling: shard one haystack over the ranks")
+    ap.add_argument("--end-to-end", action="store_true",
+                    help="time search_raw end to end: host bytes -> staging (UTF-8 check, H2D, segmentation) -> records")
+    ap.add_argument("--gib", type=float, default=100.0, help="c5: total stream GiB (each GPU takes 1/8)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="single-thread CPU baseline sample budget")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="all-cores CPU baseline threads (box share: 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/gather plumbing only (gloo, no GPU, no search): for CPU tests of --gpus N")
     return ap.parse_args()
+
+
+def relaunch(args) -> int:
+    """Run this script under torch.distributed.run with args.gpus ranks (this process has touched no
+    GPU), wait, and return its exit code."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def sources_sha() -> str:
+    """Hash of the kernel and host sources (csrc/): a traffic.json measured on other sources is stale."""
+    h = hashlib.sha256()
+    d = os.path.join(REPO, "fuzzy-aho-corasick-rs_amd", "csrc")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".cpp", ".h", ".inc")):
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
 
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(relaunch(args))
+    world = int(world_env or "1")
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with --nproc-per-node {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")  # RCCL on ROCm
+
+    import torch
+    import torch.distributed as dist
+    if args.dry_run:
+        return run_dry(args, world, rank)
     torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL on ROCm
+    if args.config == "c5":
+        return run_c5(args, world, rank, local)
 
     from fuzzy_aho_corasick import workloads as W
     from fuzzy_aho_corasick.engine import StagedHaystack
+    from fuzzy_aho_corasick.distributed import gather_device
 
     mib = args.mib if args.mib is not None else DEFAULT_MIB[args.config]
     nbytes = int(mib * (1 << 20))
-    base_seed = {"c1": 1, "c2": 2, "c3": 3, "c4": 40, "c5": 5}[args.config]
-    # weak scaling: every rank builds the same engine and owns a different haystack of equal size
-    wl = W.config(args.config, nbytes, seed=base_seed, hay_seed=base_seed + 1000 + 101 * rank)
+    if args.config == "c4":  # C2 engine, haystack seeds 40..47 (SURVEY §8(d))
+        wl = W.config("c4", nbytes, seed=2, hay_seed=40 + (0 if args.shard else rank))
+    else:
+        base_seed = {"c1": 1, "c2": 2, "c3": 3}[args.config]
+        # weak scaling: every rank builds the same engine and owns a different haystack of equal size
+        wl = W.config(args.config, nbytes, seed=base_seed,
+                      hay_seed=base_seed + 1000 + (0 if args.shard else 101 * rank))
     engine = W.builder_for(wl).device(local).build(wl.patterns)
-    staged = StagedHaystack(engine, wl.haystack)
-    graphemes = staged.graphemes
+    if args.shard:
+        staged = StagedHaystack.shard(engine, wl.haystack, world, rank)
+    else:
+        staged = StagedHaystack(engine, wl.haystack)
+    windows = staged.owned_windows  # graphemes this rank searches per step
     stream = torch.cuda.current_stream().cuda_stream
+    host_buf = [None]  # rank 0: pinned landing buffer of the gathered records
 
-    from fuzzy_aho_corasick.distributed import gather_records
-    dev = torch.device("cuda", local)
-
-    def step():  # records stay 32-byte structs (MATCH_DTYPE), as search_raw's Vec<OwnedMatch>
-        if wl.prefilter:  # C5: bitap pre-filter + re-search of the merged windows (prefilter.rs:304-374)
-            rows, st = staged.search_prefiltered_records(wl.threshold, stream=stream)
-        else:
-            rows, st = staged.search_windows_records(wl.threshold, stream=stream)
-        if world > 1:  # gather the 32 B Match records to rank 0 over RCCL (xGMI)
-            gather_records(rows, dev)
-        return rows, st
+    def step():
+        if args.end_to_end:  # search_raw: staging (UTF-8 check, H2D, segmentation + fold) + search
+            hs = StagedHaystack(engine, wl.haystack)
+            rows, st = hs.search_windows_records(wl.threshold, stream=stream)
+            del hs
+            return len(rows), st
+        if world == 1:  # records D2H into the library's pooled pinned buffers
+            rows, st = (staged.search_prefiltered_records(wl.threshold, stream=stream) if wl.prefilter
+                        else staged.search_windows_records(wl.threshold, stream=stream))
+            return len(rows), st
+        recs, n, st = staged.search_device(wl.threshold, stream=stream)
+        got = gather_device(recs, n, 0)  # RCCL: counts all-gather + point-to-point sends to rank 0
+        if got is not None:
+            if host_buf[0] is None or host_buf[0].numel() < got.numel():
+                host_buf[0] = torch.empty(int(got.numel() * 1.25) + 4096, dtype=torch.uint8, pin_memory=True)
+            host_buf[0][: got.numel()].copy_(got)
+            return got.numel() // 32, st
+        return n, st
 
     for _ in range(args.warmup):
         step()
@@ -80,60 +156,61 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kernel_ms, launches, matches, popped, prefilter_ms, cache_ms, cached = 0.0, 0, 0, 0, 0.0, 0.0, 0
-    lane_ms, lane_windows = 0.0, 0
+    acc = dict(kernel_ms=0.0, lane_ms=0.0, cache_ms=0.0, prefilter_ms=0.0, launches=0, popped=0, cached=0,
+               lane_windows=0, matches=0)
     for _ in range(args.steps):
-        rows, st = step()
-        prefilter_ms += st.prefilter_ms
-        cache_ms += st.cache_ms
-        cached += st.states_cached
-        kernel_ms += st.kernel_ms
-        lane_ms += st.lane_ms
-        lane_windows += st.lane_windows
-        launches += st.kernel_launches
-        matches += len(rows)
-        popped += st.states_popped
+        nrec, st = step()
+        acc["kernel_ms"] += st.kernel_ms
+        acc["lane_ms"] += st.lane_ms
+        acc["cache_ms"] += st.cache_ms
+        acc["prefilter_ms"] += st.prefilter_ms
+        acc["launches"] += st.kernel_launches
+        acc["popped"] += st.states_popped
+        acc["cached"] += st.states_cached
+        acc["lane_windows"] += st.lane_windows
+        acc["matches"] += nrec
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    total_graphemes = windows * args.steps
     if world > 1:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        g = torch.tensor([graphemes], device="cuda", dtype=torch.int64)
+        g = torch.tensor([windows], device="cuda", dtype=torch.int64)
         dist.all_reduce(g)
         total_graphemes = int(g.item()) * args.steps
-    else:
-        total_graphemes = graphemes * args.steps
 
     value = total_graphemes / elapsed / 1e9
-    # the search proper: the wave kernel's launches plus the lane-serial kernel that takes the small
-    # resumed windows off it (one launch per step when the prefix cache is on)
-    avg_kernel_s = (kernel_ms + lane_ms) / max(1, launches) / 1e3
-    bytes_per_launch = len(wl.haystack) + 32 * (matches / max(1, args.steps))
-    kernel_name = "bfs_window_kernel + lane_window_kernel" if lane_ms > 0 else "bfs_window_kernel"
-    if prefilter_ms > kernel_ms:  # C5: the bitap scan dominates; 1 B/char in
-        kernel_name = "bitap_kernel (+transcode, runs)"
-        avg_kernel_s = prefilter_ms / max(1, args.steps) / 1e3
-        bytes_per_launch = len(wl.haystack)
-    achieved = bytes_per_launch / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
-    traffic = None
+    K = max(1, args.steps)
+    # Roofline of the whole step: this rank's algorithmic bytes (its haystack's UTF-8
+    # bytes read once + 32 B per record written) over the device time of every kernel of the step —
+    # prefix-cache counts/builds/publishes and lookups, the lane-serial and the wave kernels (HIP events
+    # on the search streams), or the bitap scan + re-search for the pre-filter.
+    step_dev_ms = (acc["cache_ms"] + acc["lane_ms"] + acc["kernel_ms"] + acc["prefilter_ms"]) / K
+    rank_bytes = staged.owned_bytes if args.shard else len(wl.haystack)
+    recs_rank = acc["matches"] / K / (world if world > 1 else 1)
+    bytes_step = rank_bytes + 32 * recs_rank
+    achieved = bytes_step / (step_dev_ms / 1e3) / 1e9 if step_dev_ms > 0 else 0.0
+    traffic, traffic_note = None, "no profiles/traffic.json"
     if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("config") == args.config and abs(tj.get("mib", -1) - mib) < 1e-6:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+        tj = json.load(open(args.traffic_json))
+        if tj.get("sources_sha") != sources_sha():
+            traffic_note = f"profiles/traffic.json is stale (sources {tj.get('sources_sha')} != {sources_sha()})"
+        elif tj.get("config") != args.config or abs(tj.get("mib", -1) - mib) > 1e-6 or args.shard:
+            traffic_note = "profiles/traffic.json was measured on another workload"
+        else:
+            traffic, traffic_note = tj.get("hbm_bytes_per_step"), tj.get("source")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(wl, args.cpu_seconds)
+        cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:
+        wave_ms = acc["kernel_ms"] / K
         line = {
-            "metric": "haystack Gchars/s at edits<=2, 10K patterns; 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": value,
             "unit": "Gchars/s",
             "n_gpus": world,
@@ -141,23 +218,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.shard else "weak",
             "vs_baseline": None,
             "dtype": "u32 code points / f32 penalties",
             "data": "synthetic (seeded xorshift generator, SURVEY.md §8(d)); random words + planted fuzzy patterns",
             "config": {
-                "workload": f"{args.config}: " + {
-                    "c1": "exact, 16 ASCII patterns",
-                    "c2": "edits=1, 1K ASCII patterns",
-                    "c3": "edits=2, beam_width=64, 10K patterns, case-insensitive Unicode graphemes",
-                    "c4": "edits=1, 1K ASCII patterns, one haystack per GPU",
-                    "c5": "edits=1, 1K patterns (10-16), threshold 0.85, bitap prefilter",
-                }[args.config],
+                "workload": f"{args.config}: " + WORKLOAD[args.config],
                 "patterns": len(wl.patterns),
-                "haystack_bytes_per_gpu": len(wl.haystack),
-                "graphemes_per_gpu": graphemes,
+                "haystack_bytes_per_gpu": rank_bytes,
+                "graphemes_per_gpu": windows,
                 "threshold": wl.threshold,
-                "parallelism": f"dp{world} (weak: one haystack per GPU, RCCL gather of Match records)",
+                "end_to_end_search_raw": bool(args.end_to_end),
+                "parallelism": (f"shard{world} (strong: one {len(wl.haystack)}-byte haystack, halo-sliced shards)"
+                                if args.shard else f"dp{world} (weak: one haystack per GPU)")
+                               + (", RCCL gather of Match records to rank 0" if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",
@@ -166,55 +240,213 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": kernel_name,
-                "avg_kernel_ms": avg_kernel_s * 1e3,
-                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "traffic_source": traffic_note,
+                "kernel": "whole search step: prefix-cache count/build/publish + rc_lookup + lane_window + "
+                          "bfs_window kernels" if not wl.prefilter else "bitap_kernel + runs + re-search",
+                "avg_kernel_ms": step_dev_ms,
+                "algorithmic_bytes_per_launch": bytes_step,
+                "wave_kernel_only": {"kernel": "bfs_window_kernel", "avg_ms": wave_ms,
+                                     "frac": (bytes_step / (wave_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if wave_ms > 0 else None},
             },
             "cpu_baseline": cpu,
             "diagnostics": {
-                "matches_per_step": matches / max(1, args.steps),
-                "states_popped_per_step": popped / max(1, args.steps),
-                "states_per_second": popped / max(1e-9, kernel_ms / 1e3),
-                "kernel_launches": launches,
-                "search_kernel_ms_per_step": kernel_ms / max(1, args.steps),
-                "lane_kernel_ms_per_step": lane_ms / max(1, args.steps),
-                "lane_windows_per_step": lane_windows / max(1, args.steps),
-                "prefilter_ms_per_step": prefilter_ms / max(1, args.steps),
-                "prefix_cache_ms_per_step": cache_ms / max(1, args.steps),
-                "states_from_prefix_cache_per_step": cached / max(1, args.steps),
+                "matches_per_step": acc["matches"] / K,
+                "states_popped_per_step": acc["popped"] / K,
+                "states_per_second": acc["popped"] / max(1e-9, acc["kernel_ms"] / 1e3),
+                "kernel_launches": acc["launches"],
+                "search_kernel_ms_per_step": wave_ms,
+                "lane_kernel_ms_per_step": acc["lane_ms"] / K,
+                "lane_windows_per_step": acc["lane_windows"] / K,
+                "prefilter_ms_per_step": acc["prefilter_ms"] / K,
+                "prefix_cache_ms_per_step": acc["cache_ms"] / K,
+                "states_from_prefix_cache_per_step": acc["cached"] / K,
+                "sources_sha": sources_sha(),
             },
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(wl, budget_s):
-    """CPU restatement (oracle/, single thread) timed on a bounded prefix of the same workload."""
+def run_c5(args, world, rank, local):
+    """C5: a 100 GiB stream = 100 x one deterministic 1 GiB block (1 needle per MiB),
+    resident once in HBM as block || block[:halo]. GPU g processes its contiguous 1/8 of the stream
+    as windows cut at block and share boundaries, each searched on the device exactly like
+    stream.rs window_matches: the window's text (its bytes plus max_match_graphemes() + 1 of
+    overlap, stream.rs:256-258) through Prefiltered::search, ranked sorted().non_overlapping(), and
+    the matches starting before the commit point kept, at absolute offsets."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from fuzzy_aho_corasick import workloads as W
+    from fuzzy_aho_corasick.engine import StagedHaystack
+    from fuzzy_aho_corasick.distributed import gather_records
+
+    block_bytes = int((args.mib if args.mib is not None else DEFAULT_MIB["c5"]) * (1 << 20))
+    wl = W.config("c5", block_bytes, seed=5)
+    block = wl.haystack
+    engine = W.builder_for(wl).device(local).build(wl.patterns)
+    overlap = engine.max_match_graphemes() + 1  # stream_overlap (stream.rs:256-258); ASCII: bytes
+    B = len(block)
+    staged = StagedHaystack(engine, block + block[:overlap])
+    total = int(args.gib * (1 << 30)) // B * B  # whole blocks
+    share = total // 8
+    lo, hi = rank * share, (rank + 1) * share  # this GPU's range (1/8 of the stream)
+    windows = []  # (g_begin, g_end, commit, base) in the staged buffer
+    c = lo
+    while c < hi:
+        c1 = min(hi, (c // B + 1) * B)
+        o = c % B
+        end = min(total, c1 + overlap)
+        windows.append((o, o + (end - c), c1 - c, c))
+        c = c1
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        parts, pf_ms, k_ms = [], 0.0, 0.0
+        for (g0, g1, commit, base) in windows:
+            recs, st = staged.stream_window(g0, g1, commit, base, wl.threshold, True, stream=stream)
+            parts.append(recs)
+            pf_ms += st.prefilter_ms
+            k_ms += st.kernel_ms
+        recs = np.concatenate(parts)
+        if world > 1:
+            gathered = gather_records(recs, 0)
+            return (len(gathered) if gathered is not None else 0), pf_ms, k_ms
+        return len(recs), pf_ms, k_ms
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    matches = pf = km = 0
+    for _ in range(args.steps):
+        n, a, b = step()
+        matches += n
+        pf += a
+        km += b
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    processed = (hi - lo) * world * args.steps
+    K = max(1, args.steps)
+    dev_ms = (pf + km) / K
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
+    if rank == 0:
+        bytes_step = (hi - lo) + 32 * matches / K / world
+        achieved = bytes_step / (dev_ms / 1e3) / 1e9 if dev_ms > 0 else 0.0
+        print(json.dumps({
+            "metric": METRIC, "value": processed / elapsed / 1e9, "unit": "Gchars/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8 symbol ids / u32 bitap words",
+            "data": f"synthetic: {total / (1 << 30):g} GiB stream = repeats of one {B}-byte block "
+                    "(SURVEY.md §8(d) generator, 1 planted needle per MiB), resident in HBM",
+            "config": {"workload": "c5: " + WORKLOAD["c5"], "patterns": len(wl.patterns),
+                       "stream_bytes": total, "bytes_per_gpu": hi - lo, "stream_windows_per_gpu": len(windows),
+                       "window_overlap_graphemes": overlap, "threshold": wl.threshold,
+                       "parallelism": f"dp{world} (each GPU its 1/8 of the stream; RCCL gather of Match records)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "bitap_kernel + runs_kernel + re-search of the merged windows",
+                         "avg_kernel_ms": dev_ms, "algorithmic_bytes_per_launch": bytes_step},
+            "cpu_baseline": cpu,
+            "diagnostics": {"matches_per_step": matches / K, "prefilter_ms_per_step": pf / K,
+                            "research_kernel_ms_per_step": km / K, "sources_sha": sources_sha()},
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_dry(args, world, rank):
+    """Plumbing check without a GPU: the same launch, barrier / max-over-ranks timing and record
+    gather to rank 0 (gloo), with every rank contributing synthetic records instead of a search."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from fuzzy_aho_corasick._native import MATCH_DTYPE
+    from fuzzy_aho_corasick.distributed import gather_records
+    if world > 1:
+        dist.init_process_group("gloo")
+    recs = np.zeros(1000 + rank, dtype=MATCH_DTYPE)
+    recs["start"] = np.arange(len(recs)) + (rank << 32)
+    got = 0
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g = gather_records(recs, 0) if world > 1 else recs
+        got = len(g) if g is not None else 0
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "Gchars/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": elapsed / max(1, args.steps) * 1e3,
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "none",
+                          "data": "dry run: launcher and record-gather plumbing only, no search",
+                          "config": {"workload": "dry-run", "records_gathered_per_step": got}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(wl, budget_s, threads):
+    """The CPU restatement (oracle/, test infrastructure) timed on the host cores on bounded prefixes
+    of the same haystack: one thread on a prefix sized to ~budget_s, and `threads` threads
+    (start-range sharding, like search_stream_parallel, stream.rs:378-429) on SURVEY §8(d)'s prefix
+    (C2/C4/C5: 64 MiB, C3: 16 MiB; shortened if it would take more than ~20 s)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
-    from oracle_harness import OracleEngine  # test infrastructure, baseline leg only
+    from oracle_harness import OracleEngine, PreparedText  # test infrastructure, baseline leg only
     from fuzzy_aho_corasick import workloads as W
 
     orc = OracleEngine(W.builder_for(wl), wl.patterns)
-    size = 1 << 14
+
+    def prefix(nbytes):
+        s = wl.haystack[:nbytes]
+        while s and (s[-1] & 0xC0) == 0x80:
+            s = s[:-1]
+        if s and s[-1] >= 0xC0:
+            s = s[:-1]
+        return s
+
+    size, rate = 1 << 14, None
     while True:
-        sample = wl.haystack[:size]
-        while sample and (sample[-1] & 0xC0) == 0x80:
-            sample = sample[:-1]
-        if sample and sample[-1] >= 0xC0:
-            sample = sample[:-1]
-        text = sample.decode("utf-8")
-        from oracle_harness import graphemes as segs
-        n_g = len(sample) if sample.isascii() else len(segs(text))
+        pt = PreparedText(orc, prefix(size))
         t = time.perf_counter()
-        orc.raw_rows(sample, wl.threshold, prefilter=wl.prefilter)
+        pt.search(wl.threshold, prefilter=wl.prefilter)
         dt = time.perf_counter() - t
+        rate = pt.n / dt
         if dt * 4 > budget_s or size >= len(wl.haystack):
             break
         size = min(len(wl.haystack), int(size * min(8.0, max(2.0, budget_s / max(dt, 1e-3) / 2))))
-    return {"value": n_g / dt / 1e9, "unit": "Gchars/s", "cores": 1, "kind": "port",
-            "sample": f"first {len(sample)} bytes ({n_g} graphemes) of the same haystack, {dt:.1f} s, "
-                      f"oracle/ CPU restatement, single thread"}
+    one = {"value": rate / 1e9, "unit": "Gchars/s", "cores": 1, "kind": "port",
+           "sample": f"first {len(pt.data)} bytes ({pt.n} graphemes) of the same haystack, {dt:.1f} s, "
+                     "oracle/ CPU restatement of the reference algorithm, single thread"}
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    want = CPU_PREFIX_MIB[wl.name] << 20
+    est = want / max(1.0, len(pt.data) / dt) / threads  # seconds at linear scaling
+    nbytes = int(want if est <= 20 else want * 20 / est)
+    big = PreparedText(orc, prefix(nbytes))
+    t = time.perf_counter()
+    big.search(wl.threshold, prefilter=wl.prefilter, threads=threads)
+    dt_all = time.perf_counter() - t
+    one["all_cores"] = {"value": big.n / dt_all / 1e9, "unit": "Gchars/s", "cores": threads, "kind": "port",
+                        "sample": f"first {len(big.data)} bytes ({big.n} graphemes), {dt_all:.1f} s, {threads} threads, "
+                                  "start windows split into contiguous ranges (prefilter: whole-text per thread "
+                                  "slices)" if wl.prefilter else
+                                  f"first {len(big.data)} bytes ({big.n} graphemes), {dt_all:.1f} s, {threads} threads, "
+                                  "start windows split into contiguous ranges"}
+    return one
 
 
 if __name__ == "__main__":

@@ -27,6 +27,147 @@ struct fac_stream {
   fac::StreamCore* s = nullptr;
 };
 
+namespace fac {
+
+const char* diag_env(const char* name) {
+  static const bool on = [] {
+    const char* d = std::getenv("FAC_DIAGNOSTICS");
+    return d && *d && std::strcmp(d, "0") != 0;
+  }();
+  return on ? std::getenv(name) : nullptr;
+}
+
+uint64_t grapheme_limit() {
+  const char* v = diag_env("FAC_GRAPHEME_LIMIT");
+  return v ? std::strtoull(v, nullptr, 10) : 0xFFFFFFFFull;
+}
+
+namespace {
+// Result buffers handed across the C ABI. A search's records are copied D2H straight into the
+// buffer the caller receives; buffers of >= 1 MiB are pinned and go back to this pool on
+// fac_matches_free, so repeated searches land their records in already-mapped, already-pinned
+// pages (a fresh malloc'd buffer faults every page on first touch: C2's 72 MB of records per call
+// cost 20-40 ms of page faults, varying by box).
+struct PoolBlock {
+  void* p;
+  uint64_t bytes;
+  bool used;
+};
+std::mutex g_pool_mu;
+std::vector<PoolBlock> g_pool;
+constexpr uint64_t kPinnedMin = 1ull << 20;
+constexpr uint64_t kPoolKeep = 4ull << 30;  // pinned bytes kept while unused
+}  // namespace
+
+fac_match* result_alloc(uint64_t n_records) {
+  const uint64_t bytes = std::max<uint64_t>(n_records, 1) * sizeof(fac_match);
+  if (bytes < kPinnedMin) return static_cast<fac_match*>(std::malloc(bytes));
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  PoolBlock* best = nullptr;
+  for (PoolBlock& b : g_pool)
+    if (!b.used && b.bytes >= bytes && b.bytes <= 4 * bytes && (!best || b.bytes < best->bytes)) best = &b;
+  if (best) {
+    best->used = true;
+    return static_cast<fac_match*>(best->p);
+  }
+  const uint64_t want = bytes + bytes / 4;  // headroom: the next call's count differs a little
+  void* p = nullptr;
+  if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess || !p)
+    return static_cast<fac_match*>(std::malloc(bytes));  // unpinned: result_free recognises it
+  g_pool.push_back({p, want, true});
+  return static_cast<fac_match*>(p);
+}
+
+void result_free(void* p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    for (size_t i = 0; i < g_pool.size(); ++i)
+      if (g_pool[i].p == p) {
+        g_pool[i].used = false;
+        uint64_t idle = 0;
+        for (const PoolBlock& b : g_pool)
+          if (!b.used) idle += b.bytes;
+        // trim the largest idle blocks beyond the keep budget
+        while (idle > kPoolKeep) {
+          size_t big = g_pool.size();
+          for (size_t k = 0; k < g_pool.size(); ++k)
+            if (!g_pool[k].used && (big == g_pool.size() || g_pool[k].bytes > g_pool[big].bytes)) big = k;
+          if (big == g_pool.size()) break;
+          (void)hipHostFree(g_pool[big].p);
+          idle -= g_pool[big].bytes;
+          g_pool.erase(g_pool.begin() + (std::ptrdiff_t)big);
+        }
+        return;
+      }
+  }
+  std::free(p);
+}
+
+namespace {
+int grow_pinned(MatchSink& s, uint64_t need, std::string& err) {
+  if (need <= s.pinned_cap) return FAC_OK;
+  const uint64_t cap = std::max<uint64_t>(need, 2 * s.pinned_cap);
+  fac_match* p = result_alloc(cap);
+  if (!p) {
+    err = "out of host memory";
+    return FAC_E_OOM;
+  }
+  if (s.n) std::memcpy(p, s.pinned, s.n * sizeof(fac_match));
+  result_free(s.pinned);
+  s.pinned = p;
+  s.pinned_cap = cap;
+  return FAC_OK;
+}
+}  // namespace
+
+int sink_append_device(MatchSink& s, const fac_match* d_src, uint64_t cnt, hipStream_t stream, std::string& err) {
+  if (!cnt) return FAC_OK;
+  hipError_t he = hipSuccess;
+  if (s.dev) {
+    const uint64_t fit = s.n >= s.dev_cap ? 0 : std::min(cnt, s.dev_cap - s.n);
+    if (fit) he = hipMemcpyAsync(s.dev + s.n, d_src, fit * sizeof(fac_match), hipMemcpyDeviceToDevice, stream);
+  } else if (s.vec) {
+    s.vec->resize(s.n + cnt);
+    he = hipMemcpyAsync(s.vec->data() + s.n, d_src, cnt * sizeof(fac_match), hipMemcpyDeviceToHost, stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(stream);  // pageable destination
+  } else {
+    if (int rc = grow_pinned(s, s.n + cnt, err)) return rc;
+    he = hipMemcpyAsync(s.pinned + s.n, d_src, cnt * sizeof(fac_match), hipMemcpyDeviceToHost, stream);
+  }
+  if (he != hipSuccess) {
+    err = std::string("record copy: ") + hipGetErrorString(he);
+    return FAC_E_HIP;
+  }
+  s.n += cnt;
+  return FAC_OK;
+}
+
+int sink_append_host(MatchSink& s, const fac_match* src, uint64_t cnt, hipStream_t stream, std::string& err) {
+  if (!cnt) return FAC_OK;
+  if (s.dev) {
+    const uint64_t fit = s.n >= s.dev_cap ? 0 : std::min(cnt, s.dev_cap - s.n);
+    if (fit) {
+      hipError_t he = hipMemcpyAsync(s.dev + s.n, src, fit * sizeof(fac_match), hipMemcpyHostToDevice, stream);
+      if (he == hipSuccess) he = hipStreamSynchronize(stream);  // pageable source
+      if (he != hipSuccess) {
+        err = std::string("record copy: ") + hipGetErrorString(he);
+        return FAC_E_HIP;
+      }
+    }
+  } else if (s.vec) {
+    s.vec->resize(s.n + cnt);
+    std::memcpy(s.vec->data() + s.n, src, cnt * sizeof(fac_match));
+  } else {
+    if (int rc = grow_pinned(s, s.n + cnt, err)) return rc;
+    std::memcpy(s.pinned + s.n, src, cnt * sizeof(fac_match));
+  }
+  s.n += cnt;
+  return FAC_OK;
+}
+
+}  // namespace fac
+
 namespace {
 
 thread_local std::string g_err;
@@ -34,6 +175,18 @@ thread_local std::string g_err;
 int fail(int rc, const std::string& msg) {
   g_err = msg;
   return rc;
+}
+
+// hands a pinned sink's buffer to the C ABI caller (freed by fac_matches_free)
+int hand_out(fac::MatchSink& s, fac_match** out, uint64_t* n_out) {
+  if (!s.pinned) {
+    s.pinned = fac::result_alloc(1);
+    if (!s.pinned) return fail(FAC_E_OOM, "out of host memory");
+  }
+  *out = s.pinned;
+  *n_out = s.n;
+  s.pinned = nullptr;
+  return FAC_OK;
 }
 
 int check_device(int device) {
@@ -56,15 +209,19 @@ int copy_out(const std::vector<fac_match>& v, fac_match** out, uint64_t* n_out) 
   return FAC_OK;
 }
 
+// The staged haystack as search_raw's text: a shard whose text continues past its resident halo
+// (open_end) has no end inside the resident bytes (the kernels flag any window that would read
+// past them), and only its owned start windows are searched.
+constexpr uint64_t kOpenEnd = 1ull << 62;
 fac::SegDesc whole(const fac::Haystack& h) {
   fac::SegDesc s{};
   s.text_base = 0;
-  s.n = h.n;
+  s.n = h.open_end ? kOpenEnd : h.n;
   s.avail = h.n;
-  s.hay_len = h.len;
+  s.hay_len = h.open_end ? kOpenEnd : h.len;
   s.byte_base = 0;
   s.w_begin = 0;
-  s.w_end = h.n;
+  s.w_end = std::min(h.n, h.owned);
   s.ascii = h.ascii ? 1u : 0u;
   return s;
 }
@@ -94,10 +251,10 @@ bool prefilter_ks(const fac::Engine& e, float threshold, std::vector<uint32_t>& 
 }
 
 int search_staged_all(const fac::Engine& e, const fac::Haystack& h, float thr, hipStream_t stream,
-                      std::vector<fac_match>& res, fac_stats* stats) {
+                      fac::MatchSink& res, fac_stats* stats) {
   std::string err;
   std::vector<fac::SegDesc> segs{whole(h)};
-  int rc = fac::launch_search(e, h, segs, thr, stream, res, stats, err);
+  int rc = fac::launch_search_sink(e, h, segs, thr, stream, 0, res, stats, err);
   if (rc) return fail(rc, err);
   return FAC_OK;
 }
@@ -140,31 +297,108 @@ uint32_t fac_engine_max_edits_fast(const fac_engine* engine) { return engine ? e
 uint64_t fac_max_match_graphemes(const fac_engine* engine) { return engine ? engine->e.max_match_graphemes : 0; }
 int fac_prefilter_active(const fac_engine* engine) { return engine && engine->e.bitap_ok ? 1 : 0; }
 
-void fac_matches_free(fac_match* matches) { std::free(matches); }
+void fac_matches_free(fac_match* matches) { fac::result_free(matches); }
+
+static int stage_common(const fac_engine* engine, const uint8_t* utf8, uint64_t len, int force_ascii, fac_haystack** out,
+                 uint64_t* err_graphemes, fac_haystack*& fh) {
+  fh = new (std::nothrow) fac_haystack();
+  if (!fh) return fail(FAC_E_OOM, "out of host memory");
+  std::string err;
+  int rc = fac::stage_haystack(engine->e, utf8, len, fh->h, err, force_ascii);
+  if (rc == FAC_E_HAYSTACK_TOO_LARGE) {
+    if (err_graphemes) *err_graphemes = fh->h.n;
+    fac::free_haystack(fh->h);
+    delete fh;
+    fh = nullptr;
+    return fail(rc, "haystack has more than u32::MAX grapheme clusters");
+  }
+  if (rc) {
+    fac::free_haystack(fh->h);
+    delete fh;
+    fh = nullptr;
+    return fail(rc, err);
+  }
+  *out = fh;
+  return FAC_OK;
+}
 
 int fac_haystack_stage(const fac_engine* engine, const uint8_t* utf8, uint64_t len, fac_haystack** out,
                        uint64_t* err_graphemes) {
   if (!engine || !out || (len && !utf8)) return fail(FAC_E_INVALID, "NULL argument");
   *out = nullptr;
   if (!fac::utf8_valid(utf8, len)) return fail(FAC_E_INVALID, "haystack is not valid UTF-8");
-  fac_haystack* fh = new (std::nothrow) fac_haystack();
-  if (!fh) return fail(FAC_E_OOM, "out of host memory");
-  std::string err;
-  int rc = fac::stage_haystack(engine->e, utf8, len, fh->h, err);
-  if (rc == FAC_E_HAYSTACK_TOO_LARGE) {
-    if (err_graphemes) *err_graphemes = fh->h.n;
-    fac::free_haystack(fh->h);
-    delete fh;
-    return fail(rc, "haystack has more than u32::MAX grapheme clusters");
+  fac_haystack* fh = nullptr;
+  return stage_common(engine, utf8, len, -1, out, err_graphemes, fh);
+}
+
+int fac_shard_plan(uint64_t max_match_graphemes, const uint8_t* utf8, uint64_t len, int32_t is_ascii, uint64_t n_shards,
+                   uint64_t shard, uint64_t plan[4]) {
+  if (!plan || (len && !utf8) || n_shards == 0 || shard >= n_shards) return fail(FAC_E_INVALID, "bad argument");
+  const bool ascii = is_ascii < 0 ? fac::ascii_only(utf8, len) : is_ascii != 0;
+  // cut r: the first safe cut at or after r * len / n (ASCII text: graphemes are bytes, any byte)
+  auto cut = [&](uint64_t r) -> uint64_t {
+    if (r == 0) return 0;
+    if (r >= n_shards) return len;
+    uint64_t p = (uint64_t)((unsigned __int128)len * r / n_shards);
+    if (ascii) return p;
+    while (p < len && !fac::safe_cut(utf8, len, p)) ++p;
+    return p;
+  };
+  const uint64_t a = cut(shard), b = std::max(a, cut(shard + 1));
+  // halo: max_match_graphemes() + 2 graphemes past b (the +1 of stream_overlap, stream.rs:256-258,
+  // and the text[j + 1] lookahead of the last owned window's deepest state)
+  const uint64_t halo = max_match_graphemes + 2;
+  uint64_t e = b;
+  if (ascii) {
+    e = std::min<uint64_t>(len, b + halo);
+  } else if (b < len) {
+    // segment forward from b (a safe cut, or the text end) until `halo` graphemes are complete:
+    // boundaries before the last character of the segmented piece are exact (UAX #29 rules look
+    // at most one character ahead)
+    std::vector<uint64_t> st;
+    for (uint64_t span = 16 * halo + 64;; span *= 2) {
+      const uint64_t end = std::min(len, b + span);
+      uint64_t endc = end;
+      while (endc < len && (utf8[endc] & 0xC0) == 0x80) ++endc;  // whole code points
+      fac::segment_graphemes(utf8 + b, endc - b, st);
+      if (st.size() > halo + 1) {
+        e = b + st[halo];
+        break;
+      }
+      if (endc >= len) {
+        e = len;
+        break;
+      }
+    }
   }
-  if (rc) {
-    fac::free_haystack(fh->h);
-    delete fh;
-    return fail(rc, err);
-  }
-  *out = fh;
+  plan[0] = a;
+  plan[1] = b;
+  plan[2] = e;
+  plan[3] = (ascii ? 1u : 0u) | (e < len ? 2u : 0u);
   return FAC_OK;
 }
+
+int fac_haystack_stage_shard(const fac_engine* engine, const uint8_t* utf8, uint64_t len, uint64_t owned_bytes,
+                             int32_t global_ascii, int32_t open_end, uint64_t base, fac_haystack** out,
+                             uint64_t* err_graphemes) {
+  if (!engine || !out || (len && !utf8) || owned_bytes > len) return fail(FAC_E_INVALID, "bad argument");
+  *out = nullptr;
+  if (!fac::utf8_valid(utf8, len)) return fail(FAC_E_INVALID, "shard is not valid UTF-8 (cut inside a code point)");
+  fac_haystack* fh = nullptr;
+  int rc = stage_common(engine, utf8, len, global_ascii ? 1 : 0, out, err_graphemes, fh);
+  if (rc) return rc;
+  fac::Haystack& h = fh->h;
+  h.base = base;
+  h.open_end = open_end != 0;
+  if (h.ascii) {
+    h.owned = owned_bytes;
+  } else {
+    h.owned = (uint64_t)(std::lower_bound(h.starts.begin(), h.starts.end(), owned_bytes) - h.starts.begin());
+  }
+  return FAC_OK;
+}
+
+uint64_t fac_haystack_owned_windows(const fac_haystack* hay) { return hay ? std::min(hay->h.n, hay->h.owned) : 0; }
 
 uint64_t fac_haystack_graphemes(const fac_haystack* hay) { return hay ? hay->h.n : 0; }
 
@@ -185,15 +419,53 @@ int fac_search_staged(const fac_engine* engine, const fac_haystack* hay, uint64_
                       uint64_t window_end, float threshold, void* stream, fac_match** out, uint64_t* n_out,
                       fac_stats* stats) {
   if (!engine || !hay || !out || !n_out) return fail(FAC_E_INVALID, "NULL argument");
+  fac_search_args a{};
+  a.window_begin = window_begin;
+  a.window_end = window_end;
+  a.threshold = threshold;
+  a.stream = stream;
+  return fac_search_staged_ex(engine, hay, &a, out, n_out, stats);
+}
+
+int fac_search_staged_ex(const fac_engine* engine, const fac_haystack* hay, const fac_search_args* args,
+                         fac_match** out, uint64_t* n_out, fac_stats* stats) {
+  if (!engine || !hay || !args || !n_out || (!out && !args->device_out)) return fail(FAC_E_INVALID, "NULL argument");
+  if (out) *out = nullptr;
+  *n_out = 0;
   const fac::Haystack& h = hay->h;
   fac::SegDesc s = whole(h);
-  s.w_begin = std::min(window_begin, h.n);
-  s.w_end = std::min(window_end, h.n);
-  std::vector<fac_match> res;
+  s.w_begin = std::min(args->window_begin, s.w_end);
+  s.w_end = std::min(args->window_end, s.w_end);
+  fac::MatchSink sink;
+  sink.dev = static_cast<fac_match*>(args->device_out);
+  sink.dev_cap = args->device_cap;
   std::string err;
-  int rc = fac::launch_search(engine->e, h, {s}, threshold, static_cast<hipStream_t>(stream), res, stats, err);
+  int rc = fac::launch_search_sink(engine->e, h, {s}, args->threshold, static_cast<hipStream_t>(args->stream),
+                                   args->auto_beam_prefix, sink, stats, err);
+  if (rc) {
+    fac::result_free(sink.pinned);
+    return fail(rc, err);
+  }
+  if (sink.dev) {
+    *n_out = sink.n;
+    if (sink.n > sink.dev_cap) return fail(FAC_E_OUTPUT_CAPACITY, "device output buffer too small (*n_out = records needed)");
+    return FAC_OK;
+  }
+  return hand_out(sink, out, n_out);
+}
+
+int fac_auto_beam_total(const fac_engine* engine, const fac_haystack* hay, uint64_t window_begin, uint64_t window_end,
+                        float threshold, void* stream, uint64_t* total) {
+  if (!engine || !hay || !total) return fail(FAC_E_INVALID, "NULL argument");
+  *total = 0;
+  const fac::Haystack& h = hay->h;
+  fac::SegDesc s = whole(h);
+  s.w_begin = std::min(window_begin, s.w_end);
+  s.w_end = std::min(window_end, s.w_end);
+  std::string err;
+  const int rc = fac::auto_beam_total(engine->e, h, {s}, threshold, static_cast<hipStream_t>(stream), *total, err);
   if (rc) return fail(rc, err);
-  return copy_out(res, out, n_out);
+  return FAC_OK;
 }
 
 int fac_search_raw(const fac_engine* engine, const uint8_t* utf8, uint64_t len, float threshold, fac_match** out,
@@ -204,56 +476,71 @@ int fac_search_raw(const fac_engine* engine, const uint8_t* utf8, uint64_t len, 
   fac_haystack* hay = nullptr;
   int rc = fac_haystack_stage(engine, utf8, len, &hay, err_graphemes);
   if (rc) return rc;
-  std::vector<fac_match> res;
-  rc = search_staged_all(engine->e, hay->h, threshold, nullptr, res, nullptr);
+  fac::MatchSink sink;
+  rc = search_staged_all(engine->e, hay->h, threshold, nullptr, sink, nullptr);
   fac_haystack_free(hay);
-  if (rc) return rc;
-  return copy_out(res, out, n_out);
+  if (rc) {
+    fac::result_free(sink.pinned);
+    return rc;
+  }
+  return hand_out(sink, out, n_out);
 }
 
 }  // extern "C"
 
 namespace {
 
-// Prefiltered::raw on a staged haystack (prefilter.rs:304-374): bitap windows on the device, each
-// merged window re-searched as its own sub-haystack, best per (start, end, pattern) by strictly
-// greater similarity, sorted. Falls back to the full search where the reference does (:311-317).
-int prefiltered_staged(const fac::Engine& e, const fac::Haystack& h, float threshold, hipStream_t stream,
-                       std::vector<fac_match>& merged, fac_stats* stats, std::string& err) {
+// The staged bytes [bs, be) = graphemes [g0, g1) searched as a text of their own (search_raw on a
+// slice: is_ascii is re-decided on the slice, search.rs:196, prefilter.rs:349-350).
+fac::SegDesc slice_view(const fac::Haystack& h, uint64_t g0, uint64_t g1) {
+  const uint64_t bs = h.ascii ? g0 : (g0 < h.n ? h.starts[g0] : h.len);
+  const uint64_t be = h.ascii ? g1 : (g1 < h.n ? h.starts[g1] : h.len);
+  const bool asc = h.ascii || fac::ascii_only(h.utf8.data() + bs, be - bs);
+  fac::SegDesc s{};
+  s.ascii = asc ? 1u : 0u;
+  s.text_base = asc ? bs : g0;
+  s.n = asc ? be - bs : g1 - g0;
+  s.avail = s.n;
+  s.hay_len = be - bs;
+  s.byte_base = bs;
+  s.w_begin = 0;
+  s.w_end = s.n;
+  return s;
+}
+
+// Prefiltered::raw on a text view of a staged haystack (prefilter.rs:304-374): bitap windows on the
+// device, each merged window re-searched as its own sub-haystack, best per (start, end, pattern) by
+// strictly greater similarity, sorted. Falls back to the full search of the view where the
+// reference does (:311-317).
+int prefiltered_view(const fac::Engine& e, const fac::Haystack& h, const fac::SegDesc& view, float threshold,
+                     hipStream_t stream, std::vector<fac_match>& merged, fac_stats* stats, std::string& err) {
   merged.clear();
   std::vector<uint32_t> ks;
   if (!e.bitap_ok || !prefilter_ks(e, threshold, ks))  // prefilter.rs:151-155, 311-317
-    return fac::launch_search(e, h, {whole(h)}, threshold, stream, merged, stats, err);
+    return fac::launch_search(e, h, {view}, threshold, stream, merged, stats, err);
   std::vector<std::pair<uint64_t, uint64_t>> windows;
-  int rc = fac::prefilter_windows(e, h, ks, stream, windows, stats, err);
+  int rc = fac::prefilter_windows(e, h, view, ks, stream, windows, stats, err);
   if (rc) return rc;
   // Re-search each merged window as its own haystack (prefilter.rs:344-350): the slice re-decides
   // is_ascii, so an all-ASCII slice of a Unicode haystack is searched byte-wise.
   std::vector<fac::SegDesc> segs;
   segs.reserve(windows.size());
   for (auto& w : windows) {
-    const uint64_t gs = w.first, ge = std::min<uint64_t>(w.second, h.n);
-    const uint64_t bs = h.ascii ? gs : h.starts[gs];
-    const uint64_t be = h.ascii ? ge : (ge < h.n ? h.starts[ge] : h.len);
-    fac::SegDesc s{};
-    bool sub_ascii = h.ascii;
-    if (!sub_ascii) {
-      sub_ascii = true;
-      for (uint64_t i = bs; i < be; ++i)
-        if (h.utf8[i] & 0x80) {
-          sub_ascii = false;
-          break;
-        }
+    const uint64_t gs = w.first, ge = std::min<uint64_t>(w.second, view.n);
+    if (view.ascii) {  // byte-wise view: windows are bytes of h.d_utf8 from view.text_base
+      fac::SegDesc s{};
+      s.ascii = 1u;
+      s.text_base = view.text_base + gs;
+      s.n = ge - gs;
+      s.avail = s.n;
+      s.hay_len = s.n;
+      s.byte_base = view.text_base + gs;
+      s.w_begin = 0;
+      s.w_end = s.n;
+      segs.push_back(s);
+    } else {
+      segs.push_back(slice_view(h, view.text_base + gs, view.text_base + ge));
     }
-    s.ascii = sub_ascii ? 1u : 0u;
-    s.text_base = sub_ascii ? bs : gs;
-    s.n = sub_ascii ? be - bs : ge - gs;
-    s.avail = s.n;
-    s.hay_len = be - bs;
-    s.byte_base = bs;
-    s.w_begin = 0;
-    s.w_end = s.n;
-    segs.push_back(s);
   }
   if (segs.empty()) return FAC_OK;
   std::vector<fac_match> res;
@@ -269,6 +556,15 @@ int prefiltered_staged(const fac::Engine& e, const fac::Haystack& h, float thres
   merged.reserve(best.size());
   for (auto& kv : best) merged.push_back(kv.second);
   return FAC_OK;
+}
+
+int prefiltered_staged(const fac::Engine& e, const fac::Haystack& h, float threshold, hipStream_t stream,
+                       std::vector<fac_match>& merged, fac_stats* stats, std::string& err) {
+  if (h.open_end) {
+    err = "the pre-filtered search needs a whole haystack, not an open-ended shard";
+    return FAC_E_INVALID;
+  }
+  return prefiltered_view(e, h, whole(h), threshold, stream, merged, stats, err);
 }
 
 }  // namespace
@@ -302,6 +598,41 @@ int fac_search_staged_prefiltered(const fac_engine* engine, const fac_haystack* 
       prefiltered_staged(engine->e, hay->h, threshold, static_cast<hipStream_t>(stream), merged, stats, err);
   if (rc) return fail(rc, err);
   return copy_out(merged, out, n_out);
+}
+
+int fac_stream_window_staged(const fac_engine* engine, const fac_haystack* hay, uint64_t g_begin, uint64_t g_end,
+                             uint64_t commit_bytes, uint64_t base, float threshold, int32_t prefilter, void* stream,
+                             fac_match** out, uint64_t* n_out, fac_stats* stats) {
+  if (!engine || !hay || !out || !n_out) return fail(FAC_E_INVALID, "NULL argument");
+  *out = nullptr;
+  *n_out = 0;
+  const fac::Haystack& h = hay->h;
+  if (h.open_end || h.base) return fail(FAC_E_INVALID, "stream windows are cut from a whole staged haystack");
+  g_end = std::min(g_end, h.n);
+  g_begin = std::min(g_begin, g_end);
+  const fac::SegDesc view = slice_view(h, g_begin, g_end);
+  const fac::Engine& e = engine->e;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  std::vector<fac_match> v;
+  std::string err;
+  int rc = prefilter ? prefiltered_view(e, h, view, threshold, st, v, stats, err)
+                     : fac::launch_search(e, h, {view}, threshold, st, v, stats, err);
+  if (rc) return fail(rc, err);
+  // window_matches (stream.rs:262-297): sorted().non_overlapping() within the window, then the
+  // matches the window owns (start < commit), at absolute offsets
+  if (!v.empty() && (rc = fac::apply_matches(e, v, 1, 1, nullptr, err))) return fail(rc, err);
+  std::vector<fac_match> owned;
+  owned.reserve(v.size());
+  for (fac_match m : v) {
+    m.start -= view.byte_base;
+    m.end -= view.byte_base;
+    if (m.start < commit_bytes) {
+      m.start += base;
+      m.end += base;
+      owned.push_back(m);
+    }
+  }
+  return copy_out(owned, out, n_out);
 }
 
 int fac_matches_apply(const fac_engine* engine, fac_match* matches, uint64_t n, int32_t order, int32_t overlap,
@@ -368,7 +699,7 @@ int64_t fac_prefilter_windows(const fac_engine* engine, const uint8_t* utf8, uin
   if (fac_haystack_stage(engine, utf8, len, &hay, nullptr)) return -1;
   std::string err;
   std::vector<std::pair<uint64_t, uint64_t>> windows;
-  int rc = fac::prefilter_windows(e, hay->h, ks, nullptr, windows, nullptr, err);
+  int rc = fac::prefilter_windows(e, hay->h, whole(hay->h), ks, nullptr, windows, nullptr, err);
   fac_haystack_free(hay);
   if (rc) return fail(rc, err), -1;
   for (size_t i = 0; i < windows.size() && i < cap; ++i) {

@@ -214,6 +214,7 @@ struct SearchParams {
   uint4* ebuf;              // per-wave emission scratch
   fac_match* out;
   uint64_t out_cap;
+  uint64_t out_shift;       // added to every record's start/end (global byte of a shard's byte 0)
   unsigned long long* counters;  // [0] matches, [1] states popped, [2] error flags, [3] spilled windows,
                                  // [4] pops replayed from snapshots, [5] windows resumed from a snapshot,
                                  // [6] of those, finished by the snapshot alone (empty queue),
@@ -357,6 +358,12 @@ struct Haystack {
   bool ascii = true;
   uint64_t len = 0;  // bytes
   uint64_t n = 0;    // graphemes
+  // shard of a larger haystack (fac_haystack_stage_shard): output offsets are shifted by `base`
+  // (global byte of local byte 0); `open_end`: the text continues past the resident bytes, which
+  // hold only the halo (j == n / end-of-text logic never applies); start windows [0, owned)
+  uint64_t base = 0;
+  bool open_end = false;
+  uint64_t owned = UINT64_MAX;
   uint8_t* d_utf8 = nullptr;
   uint32_t* d_text32 = nullptr;  // Unicode only
   uint64_t* d_off = nullptr;     // Unicode only
@@ -369,11 +376,44 @@ struct Haystack {
   int device = 0;
 };
 
+// Where a search delivers its records: a host vector (internal callers), a pooled pinned host
+// buffer handed to the C ABI caller (fac_search_staged / fac_search_raw: no page faults on the
+// D2H, result_alloc below), or the caller's device buffer (fac_search_staged_device: records stay
+// in HBM for the RCCL gather). `n` counts every record; with a device buffer only the first
+// dev_cap are written.
+struct MatchSink {
+  std::vector<fac_match>* vec = nullptr;
+  fac_match* pinned = nullptr;
+  uint64_t pinned_cap = 0;
+  fac_match* dev = nullptr;
+  uint64_t dev_cap = 0;
+  uint64_t n = 0;
+};
+// result buffers (api.cpp): large ones come from a pool of pinned host buffers that
+// fac_matches_free returns to the pool; small ones are malloc'd. result_free takes either.
+fac_match* result_alloc(uint64_t n_records);
+void result_free(void* p);
+int sink_append_device(MatchSink& s, const fac_match* d_src, uint64_t cnt, hipStream_t stream, std::string& err);
+int sink_append_host(MatchSink& s, const fac_match* src, uint64_t cnt, hipStream_t stream, std::string& err);
+
 // builder.cpp
 int build_engine(const fac_pattern* pats, uint64_t n, const fac_config* cfg, Engine& e, std::string& err);
 // search_kernels.hip
 int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs, float thr,
                   hipStream_t stream, std::vector<fac_match>& out, fac_stats* stats, std::string& err);
+// ab_prefix: the running auto-beam total (queue.len() summed) of the windows before this call's
+// first window, for a shard of one haystack (search.rs:1096-1103); 0 for a whole search
+int launch_search_sink(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs, float thr,
+                       hipStream_t stream, uint64_t ab_prefix, MatchSink& sink, fac_stats* stats, std::string& err);
+// auto-beam pass 1 alone: sum of queue.len() over the windows of `segs` searched unbeamed
+int auto_beam_total(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs, float thr,
+                    hipStream_t stream, uint64_t& total, std::string& err);
+// diagnostics knobs: FAC_* environment variables are honoured only with FAC_DIAGNOSTICS=1 set, so
+// a stray variable in a user's environment never changes the search path
+const char* diag_env(const char* name);
+// largest grapheme count a haystack may have (u32::MAX, search.rs:198-201; lowered only by the
+// diagnostics knob FAC_GRAPHEME_LIMIT so tests can reach SearchError::HaystackTooLarge)
+uint64_t grapheme_limit();
 // bitap pre-filter: candidate windows (grapheme ranges, merged) for a staged haystack
 // stream.cpp: the WindowReader state (stream.rs:77-159) and the matches ready to hand out
 struct StreamCore {
@@ -395,9 +435,21 @@ int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::stri
 void ensure_symbols(const Engine& e, const Haystack& h);
 int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,
                   std::string& err);
-int prefilter_windows(const Engine& e, const Haystack& h, const std::vector<uint32_t>& ks, hipStream_t stream,
-                      std::vector<std::pair<uint64_t, uint64_t>>& windows, fac_stats* stats, std::string& err);
-int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack& h, std::string& err);
+// merged bitap windows (prefilter.rs:319-342) of a text view of a staged haystack (view.ascii:
+// bytes [text_base, text_base + n) of h.d_utf8; else graphemes [text_base, text_base + n)); windows
+// in the view's local grapheme coordinates
+int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, const std::vector<uint32_t>& ks,
+                      hipStream_t stream, std::vector<std::pair<uint64_t, uint64_t>>& windows, fac_stats* stats,
+                      std::string& err);
+// force_ascii: -1 decide from the bytes (search.rs:196), 0 Unicode graphemes, 1 ASCII bytes (a
+// shard of a haystack whose global is_ascii is already known)
+int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack& h, std::string& err,
+                   int force_ascii = -1);
+// shard planning (unicode.cpp): p is a grapheme boundary whose segmentation does not depend on
+// anything before it (previous char ASCII and not CR, char at p neither Extend, ZWJ nor SpacingMark)
+bool safe_cut(const uint8_t* s, uint64_t n, uint64_t p);
+// str::is_ascii (search.rs:196), eight bytes at a time
+bool ascii_only(const uint8_t* s, uint64_t n);
 void free_haystack(Haystack& h);
 int upload_engine(Engine& e, std::string& err);
 void free_engine_device(Engine& e);

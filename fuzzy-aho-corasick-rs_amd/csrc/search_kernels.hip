@@ -1064,8 +1064,8 @@ __device__ __forceinline__ fac_match match_record(const SearchParams& P, const S
                                                   const uint4& ent) {
   const uint64_t me = start + ent.x;
   fac_match m;
-  m.start = sb;
-  m.end = S.byte_base + (me < S.n ? local_byte(P, S, me) : S.hay_len);
+  m.start = P.out_shift + sb;
+  m.end = P.out_shift + S.byte_base + (me < S.n ? local_byte(P, S, me) : S.hay_len);
   m.pattern_index = ent.y;
   m.similarity = __uint_as_float(ent.z);
   m.insertions = ent.w & 0xFFu;
@@ -2571,7 +2571,7 @@ struct Variant {
 // FAC_LDS_PAD (bytes of unused dynamic LDS per workgroup): occupancy experiments only
 uint32_t lds_pad() {
   static const uint32_t v = [] {
-    const char* e = std::getenv("FAC_LDS_PAD");
+    const char* e = diag_env("FAC_LDS_PAD");
     return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
   }();
   return v;
@@ -2622,13 +2622,13 @@ hipError_t launch_variant(const Variant& v, uint32_t grid, hipStream_t s, const 
 
 // first dedup-table size tried for beamed engines (FAC_BEAM_VCAP overrides; 256 / 512 / ...)
 uint32_t default_beam_vcap() {
-  const char* e = std::getenv("FAC_BEAM_VCAP");
+  const char* e = diag_env("FAC_BEAM_VCAP");
   return e ? (uint32_t)std::atoi(e) : 512u;
 }
 
 bool debug_poison() {
   static const bool v = [] {
-    const char* e = std::getenv("FAC_DEBUG_POISON");
+    const char* e = diag_env("FAC_DEBUG_POISON");
     return e && e[0] == '1';
   }();
   return v;
@@ -2775,15 +2775,11 @@ void free_engine_device(Engine& e) {
   e.d_nodes = nullptr;
 }
 
-int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack& h, std::string& err) {
+int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack& h, std::string& err,
+                   int force_ascii) {
   h.device = e.device;
   h.len = len;
-  h.ascii = true;
-  for (uint64_t i = 0; i < len; ++i)
-    if (utf8[i] & 0x80) {
-      h.ascii = false;
-      break;
-    }
+  h.ascii = force_ascii < 0 ? ascii_only(utf8, len) : force_ascii != 0;
   h.utf8.assign(utf8, utf8 + len);
   h.n = h.ascii ? len : 0;
   HIP_TRY(hipSetDevice(e.device));
@@ -2796,7 +2792,7 @@ int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack&
     const int rc = stage_unicode_device(e, h, st, err);
     if (rc) return rc;
   }
-  if (h.n > 0xFFFFFFFFull) return FAC_E_HAYSTACK_TOO_LARGE;
+  if (h.n > grapheme_limit()) return FAC_E_HAYSTACK_TOO_LARGE;
   HIP_TRY(hipStreamSynchronize(st));
   return FAC_OK;
 }
@@ -2856,11 +2852,10 @@ int ensure_gids(const Engine& e, const Haystack& h, std::string& err) {
 // segments concatenated) the number of states pushed, the reference's queue.len().
 int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs_in, float thr,
                 hipStream_t stream, uint32_t beam, bool exact_dedup, std::vector<uint32_t>* counts,
-                std::vector<fac_match>& out, fac_stats* stats, std::string& err) {
+                MatchSink& out, fac_stats* stats, std::string& err) {
   const auto t_begin = std::chrono::steady_clock::now();
   auto host_ms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count(); };
-  const bool timing = std::getenv("FAC_TIMING") != nullptr;  // diagnostics: host wall-clock phases
-  out.clear();
+  const bool timing = diag_env("FAC_TIMING") != nullptr;  // diagnostics: host wall-clock phases
   HIP_TRY(hipSetDevice(e.device));
   if (!stream) stream = e.stream;
   std::vector<SegDesc> segs;
@@ -2886,7 +2881,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.gt_mask = e.gt_mask;
   P.gt_seed1 = e.gt_seed1;
   P.gt_seed2 = e.gt_seed2;
-  P.gt_fast = (e.gt_fast && !std::getenv("FAC_NO_FAST")) ? 1 : 0;  // env: A/B knob
+  P.gt_fast = (e.gt_fast && !diag_env("FAC_NO_FAST")) ? 1 : 0;  // env: A/B knob
   P.aux = e.d_aux;
   P.pats = e.d_pats;
   P.sim_ascii = e.d_sim_ascii;
@@ -2900,6 +2895,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.total_windows = windows;
   P.case_insensitive = e.case_insensitive;
   P.thr = thr;
+  P.out_shift = h.base;
   {  // search.rs:486-487, evaluated as two rounded f32 operations like the reference
     volatile float prod = e.nodes[0].prune_lw * thr;
     P.max_penalties = e.nodes[0].prune_len - prod;
@@ -2954,7 +2950,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       vi = i;
   for (size_t i = 0; i < nv && vi == nv; ++i)
     if (fits(kVariants[i])) vi = i;
-  if (const char* fv = std::getenv("FAC_VARIANT")) {  // tuning override "vcap,qcap"
+  if (const char* fv = diag_env("FAC_VARIANT")) {  // tuning override "vcap,qcap"
     unsigned a = 0, b = 0;
     if (std::sscanf(fv, "%u,%u", &a, &b) == 2)
       for (size_t i = 0; i < nv; ++i)
@@ -3032,7 +3028,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (e) (void)hipEventDestroy(e);
     }
   } ev_lane_guard{ev_lane};
-  out.clear();
 
   // Prefix cache. Level 1: every window's key of K0 chars (4, else 3, else 2,
   // whichever first gives every snapshot at least 8 windows on average); rc_count_kernel inserts
@@ -3045,15 +3040,15 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.rc_hits = nullptr;
   P.rc_hit_pops = nullptr;
   P.rc_ntab = 0;
-  P.rc_lane_flush = std::getenv("FAC_RC_NO_LANE") ? 0 : 1;
-  P.dyn_chunks = std::getenv("FAC_STATIC_GRID") ? 0 : 1;
+  P.rc_lane_flush = diag_env("FAC_RC_NO_LANE") ? 0 : 1;
+  P.dyn_chunks = diag_env("FAC_STATIC_GRID") ? 0 : 1;
   const bool root_out = !e.nodes.empty() && e.nodes[0].out_end > e.nodes[0].out_begin;
-  const char* rc_min = std::getenv("FAC_RC_MIN");  // env knobs: tests force it on / pin K, A/B turns it off
-  const char* kenv = std::getenv("FAC_RC_K");
+  const char* rc_min = diag_env("FAC_RC_MIN");  // env knobs: tests force it on / pin K, A/B turns it off
+  const char* kenv = diag_env("FAC_RC_K");
   if (!root_out && !e.has_map && fan_root + 1 <= 4096 && kVariants[vi].qcap <= 4096 &&
-      windows >= (rc_min ? std::strtoull(rc_min, nullptr, 10) : 4096ull) && !std::getenv("FAC_NO_RC")) {
+      windows >= (rc_min ? std::strtoull(rc_min, nullptr, 10) : 4096ull) && !diag_env("FAC_NO_RC")) {
     auto env_u = [](const char* name, uint64_t dflt) {
-      const char* v = std::getenv(name);
+      const char* v = diag_env(name);
       return v ? std::strtoull(v, nullptr, 10) : dflt;
     };
     const uint32_t kpin = kenv ? (uint32_t)std::min<unsigned long>(4, std::max<unsigned long>(2, std::strtoul(kenv, nullptr, 10))) : 0u;
@@ -3129,11 +3124,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     // sampled levels: frequent long prefixes, ascending key lengths (FAC_RC_LEVELS, e.g. "6" or
     // "5,7"; FAC_RC_K2 = k pins one level, 0 turns them off)
     std::vector<uint32_t> ks;
-    if (const char* k2e = std::getenv("FAC_RC_K2")) {
+    if (const char* k2e = diag_env("FAC_RC_K2")) {
       const uint32_t k2 = (uint32_t)std::strtoul(k2e, nullptr, 10);
       if (k2) ks.push_back(std::min<uint32_t>(8, k2));
     } else {
-      const char* le = std::getenv("FAC_RC_LEVELS");
+      const char* le = diag_env("FAC_RC_LEVELS");
       // with the lane-serial kernel an 8-char level no longer pays (C3 156 -> 147 ms); one-edit
       // engines finish most windows within 5 chars, and a 6-char level costs them more in counts
       // and lookup probes than it saves (C2 1 GiB: 266 -> 188 ms per step with "5" alone)
@@ -3230,7 +3225,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       HIP_TRY(d_rcs.alloc(pool_words * sizeof(uint4), stream));
       P.rc_pool = static_cast<uint4*>(d_rcs.p);
       P.rc_pool_cap = pool_words;
-      if (!std::getenv("FAC_RC_ONE_STREAM")) {
+      if (!diag_env("FAC_RC_ONE_STREAM")) {
         if (!e.aux_stream) HIP_TRY(hipStreamCreateWithFlags(&e.aux_stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&l1_done, hipEventDisableTiming));
         bstream = e.aux_stream;
@@ -3327,7 +3322,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     HIP_TRY(hipEventRecord(ev.b, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     HIP_TRY(hipEventElapsedTime(&cache_ms, ev.a, ev.b));
-    if (P.rc_mode == 1 && std::getenv("FAC_RC_DEBUG")) {  // diagnostics: keys, pool use, cached entries
+    if (P.rc_mode == 1 && diag_env("FAC_RC_DEBUG")) {  // diagnostics: keys, pool use, cached entries
       unsigned long long rcn[2] = {0, 0};
       HIP_TRY(hipMemcpy(rcn, d_rcn.p, sizeof(rcn), hipMemcpyDeviceToHost));
       auto cached_of = [&](const RcTable& T, uint32_t ne, uint64_t& qsum) -> uint64_t {
@@ -3363,7 +3358,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   // -> 2048 costs 0.7 ms).
   const uint64_t rc_auto = P.beam ? 256ull : std::min<uint64_t>(4096, std::max<uint64_t>(256, pass_windows / (16ull * max_grid)));
   const uint32_t rc_chunk = (uint32_t)std::min<unsigned long>(4096, std::max<unsigned long>(64,
-      std::getenv("FAC_RC_CHUNK") ? std::strtoul(std::getenv("FAC_RC_CHUNK"), nullptr, 10) : rc_auto));
+      diag_env("FAC_RC_CHUNK") ? std::strtoul(diag_env("FAC_RC_CHUNK"), nullptr, 10) : rc_auto));
   for (;;) {
     // spilled windows are few and heavy: one per block turn; behind the prefix-cache lookups most
     // windows are done, so chunks are larger (fewer hand-out atomics; the group prescan skips them)
@@ -3391,17 +3386,17 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(ev.b, stream));
       // small unfinished windows: one lane each (lane_window_kernel); the rest stay for the wave kernel
-      const bool lane_on = !std::getenv("FAC_NO_LANE") && !P.win_counts && !P.has_map;  // beamed: exact_dedup is set, bail-outs keep it exact
+      const bool lane_on = !diag_env("FAC_NO_LANE") && !P.win_counts && !P.has_map;  // beamed: exact_dedup is set, bail-outs keep it exact
       if (lane_on) {
         if (!ev_lane) HIP_TRY(hipEventCreate(&ev_lane));
-        P.lane_debug = std::getenv("FAC_RC_DEBUG") ? 1 : 0;
-        P.lane_popmax = (uint32_t)std::max<unsigned long>(1, std::getenv("FAC_LANE_POPS") ? std::strtoul(std::getenv("FAC_LANE_POPS"), nullptr, 10) : 32ul);
+        P.lane_debug = diag_env("FAC_RC_DEBUG") ? 1 : 0;
+        P.lane_popmax = (uint32_t)std::max<unsigned long>(1, diag_env("FAC_LANE_POPS") ? std::strtoul(diag_env("FAC_LANE_POPS"), nullptr, 10) : 32ul);
         // one wave per workgroup; each takes its best lists from its own emit-scratch slice
         const uint32_t lgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + LANE_CHUNK - 1) / LANE_CHUNK, (uint64_t)max_grid));
         static_assert(16 * 64 <= 1024, "lane best lists must fit the emit scratch slice (P.ecap >= 1024)");
         // 16-state rings by default (C3: lane 19 ms + wave kernel 37 ms, against 6 + 58 with 8 states)
-        if (std::getenv("FAC_LANE_Q8")) hipLaunchKernelGGL((lane_window_kernel<8, 8>), dim3(lgrid), dim3(64), 0, stream, P);
-        else if (std::getenv("FAC_LANE_Q32")) hipLaunchKernelGGL((lane_window_kernel<32, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+        if (diag_env("FAC_LANE_Q8")) hipLaunchKernelGGL((lane_window_kernel<8, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+        else if (diag_env("FAC_LANE_Q32")) hipLaunchKernelGGL((lane_window_kernel<32, 8>), dim3(lgrid), dim3(64), 0, stream, P);
         else hipLaunchKernelGGL((lane_window_kernel<16, 8>), dim3(lgrid), dim3(64), 0, stream, P);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(ev_lane, stream));
@@ -3413,7 +3408,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (lane_on) {
         HIP_TRY(hipEventElapsedTime(&lms, ev.b, ev_lane));
         lane_ms += lms;
-        if (std::getenv("FAC_RC_DEBUG")) {
+        if (diag_env("FAC_RC_DEBUG")) {
           unsigned long long d[8];
           HIP_TRY(hipMemcpyFromSymbol(d, HIP_SYMBOL(g_lane_dbg), sizeof(d)));
           std::fprintf(stderr, "FAC_LANE taken=%llu finished=%llu bailed=%llu ms=%.3f popmax=%u trips=%llu run_cycles=%llu "
@@ -3440,7 +3435,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     popped += cnt[1];
     cached_pops += cnt[4];
     lane_windows += cnt[8];
-    if (std::getenv("FAC_RC_DEBUG") && P.rc_mode == 1)
+    if (diag_env("FAC_RC_DEBUG") && P.rc_mode == 1)
       std::fprintf(stderr, "FAC_RC launch windows=%llu resumed=%llu lane_flushed=%llu lane_searched=%llu popped=%llu\n",
                    (unsigned long long)pass_windows, cnt[5], cnt[6], cnt[8], cnt[1]);
 #ifdef FAC_WIN_HIST
@@ -3497,9 +3492,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       continue;
     }
     t_dev = host_ms();
-    const size_t have = out.size();
-    out.resize(have + cnt[0]);
-    if (cnt[0]) HIP_TRY(hipMemcpyAsync(out.data() + have, d_out.p, cnt[0] * sizeof(fac_match), hipMemcpyDeviceToHost, stream));
+    if (cnt[0]) {
+      const int arc = sink_append_device(out, static_cast<const fac_match*>(d_out.p), cnt[0], stream, err);
+      if (arc) return arc;
+    }
     HIP_TRY(hipStreamSynchronize(stream));
     if (cnt[3] == 0) break;
     // windows that overflowed this variant's frontier: re-run just those on the next one
@@ -3554,11 +3550,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
 // window's queue.len(); per segment the switch window w* is the first whose running total exceeds
 // the budget; pass-1 matches of windows <= w* are kept and the windows after w* are re-searched
 // with the auto-beam width.
-int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs_in, float thr,
-                  hipStream_t stream, std::vector<fac_match>& out, fac_stats* stats, std::string& err) {
+int launch_search_sink(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs_in, float thr,
+                       hipStream_t stream, uint64_t ab_prefix, MatchSink& out, fac_stats* stats, std::string& err) {
   const uint32_t beam = (uint32_t)std::min<uint64_t>(e.beam_width, 0xFFFFFFFFull);
   if (!(e.has_auto_beam && e.beam_width == 0))
     return launch_pass(e, h, segs_in, thr, stream, beam, beam != 0, nullptr, out, stats, err);
+  const uint32_t ab_beam = (uint32_t)std::min<uint64_t>(e.ab_width, 0xFFFFFFFFull);
+  // a shard whose earlier shards already crossed the budget is beamed from its first window
+  if (ab_prefix > e.ab_budget) return launch_pass(e, h, segs_in, thr, stream, ab_beam, true, nullptr, out, stats, err);
   std::vector<SegDesc> segs;
   for (const SegDesc& s : segs_in) {
     SegDesc c = s;
@@ -3567,13 +3566,15 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
   }
   std::vector<uint32_t> counts;
   std::vector<fac_match> pass1;
-  int rc = launch_pass(e, h, segs, thr, stream, 0, true, &counts, pass1, stats, err);
+  MatchSink s1;
+  s1.vec = &pass1;
+  int rc = launch_pass(e, h, segs, thr, stream, 0, true, &counts, s1, stats, err);
   if (rc) return rc;
   std::vector<SegDesc> tails;          // windows after each segment's switch window
   std::vector<std::pair<uint64_t, uint64_t>> keep;  // per segment: [byte_base, cut byte) of pass 1
   uint64_t v = 0;
   for (const SegDesc& c : segs) {
-    uint64_t total = 0, cut_w = c.w_end;  // first window searched with the beam
+    uint64_t total = ab_prefix, cut_w = c.w_end;  // first window searched with the beam
     for (uint64_t w = c.w_begin; w < c.w_end; ++w, ++v) {
       total += counts[v];
       if (cut_w == c.w_end && total > e.ab_budget) cut_w = w + 1;
@@ -3588,48 +3589,67 @@ int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>
       tails.push_back(t);
     }
   }
-  // segments cover disjoint byte ranges: attribute each pass-1 match by its start byte
+  // segments cover disjoint byte ranges: attribute each pass-1 match by its start byte (records
+  // carry the shard's global shift h.base)
   std::vector<size_t> order(segs.size());
   for (size_t i = 0; i < order.size(); ++i) order[i] = i;
   std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return segs[a].byte_base < segs[b].byte_base; });
-  out.clear();
+  std::vector<fac_match> kept;
   for (const fac_match& m : pass1) {
+    const uint64_t st = m.start - h.base;
     size_t lo = 0, hi = order.size();
     while (hi - lo > 1) {
       const size_t mid = (lo + hi) / 2;
-      if (segs[order[mid]].byte_base <= m.start) lo = mid;
+      if (segs[order[mid]].byte_base <= st) lo = mid;
       else hi = mid;
     }
     const auto& k = keep[order[lo]];
-    if (m.start >= k.first && m.start < k.second) out.push_back(m);
+    if (st >= k.first && st < k.second) kept.push_back(m);
   }
+  if ((rc = sink_append_host(out, kept.data(), kept.size(), stream, err))) return rc;
   if (tails.empty()) return FAC_OK;
-  std::vector<fac_match> pass2;
-  rc = launch_pass(e, h, tails, thr, stream, (uint32_t)std::min<uint64_t>(e.ab_width, 0xFFFFFFFFull), true,
-                   nullptr, pass2, stats, err);
-  if (rc) return rc;
-  out.insert(out.end(), pass2.begin(), pass2.end());
-  return FAC_OK;
+  return launch_pass(e, h, tails, thr, stream, ab_beam, true, nullptr, out, stats, err);
 }
 
-int prefilter_windows(const Engine& e, const Haystack& h, const std::vector<uint32_t>& ks, hipStream_t stream,
-                      std::vector<std::pair<uint64_t, uint64_t>>& windows, fac_stats* stats, std::string& err) {
+int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs, float thr,
+                  hipStream_t stream, std::vector<fac_match>& out, fac_stats* stats, std::string& err) {
+  out.clear();
+  MatchSink s;
+  s.vec = &out;
+  return launch_search_sink(e, h, segs, thr, stream, 0, s, stats, err);
+}
+
+int auto_beam_total(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs, float thr,
+                    hipStream_t stream, uint64_t& total, std::string& err) {
+  std::vector<uint32_t> counts;
+  std::vector<fac_match> recs;
+  MatchSink s;
+  s.vec = &recs;
+  const int rc = launch_pass(e, h, segs, thr, stream, 0, true, &counts, s, nullptr, err);
+  total = 0;
+  for (uint32_t c : counts) total += c;
+  return rc;
+}
+
+int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, const std::vector<uint32_t>& ks,
+                      hipStream_t stream, std::vector<std::pair<uint64_t, uint64_t>>& windows, fac_stats* stats,
+                      std::string& err) {
   windows.clear();
   HIP_TRY(hipSetDevice(e.device));
   if (!stream) stream = e.stream;
-  const uint64_t n = h.n;
+  const uint64_t n = view.n;
   if (n == 0) return FAC_OK;
   const uint32_t np = (uint32_t)e.bp_m.size();
   DevBuf d_ids, d_k, d_cover, d_runs, d_cnt;
   HIP_TRY(d_ids.alloc(n + 16, stream));
-  if (h.ascii) {
+  if (view.ascii) {  // transcode, ASCII text (prefilter.rs:253-258): one byte per grapheme
     const uint64_t threads = (n + 15) / 16;
-    hipLaunchKernelGGL(transcode_ascii_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, stream, h.d_utf8, n,
-                       e.d_ascii_id, static_cast<uint8_t*>(d_ids.p));
+    hipLaunchKernelGGL(transcode_ascii_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, stream,
+                       h.d_utf8 + view.text_base, n, e.d_ascii_id, static_cast<uint8_t*>(d_ids.p));
     HIP_TRY(hipGetLastError());
   } else {
     ensure_symbols(e, h);
-    HIP_TRY(hipMemcpyAsync(d_ids.p, h.sym.data(), n, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_ids.p, h.sym.data() + view.text_base, n, hipMemcpyHostToDevice, stream));
   }
   // Pack the patterns into automaton words: patterns of one edit budget, longest first, each into
   // the first word with room (first-fit decreasing); 32-bit words when every pattern fits one.

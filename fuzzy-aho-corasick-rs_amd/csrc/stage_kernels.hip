@@ -285,9 +285,11 @@ int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::stri
   ST_TRY(hipMemcpyAsync(scal_h + 1, scal + 1, 8, hipMemcpyDeviceToHost, st));
   ST_TRY(hipStreamSynchronize(st));
   h.n = scal_h[1];
-  if (h.n > 0xFFFFFFFFull) return FAC_E_HAYSTACK_TOO_LARGE;
-  // grapheme starts = positions with brk set
-  ST_TRY(hipMalloc((void**)&h.d_off, std::max<uint64_t>(h.n * 8, 16)));
+  if (h.n > grapheme_limit()) return FAC_E_HAYSTACK_TOO_LARGE;
+  // grapheme starts = positions with brk set, plus off[n] = len (a shard's halo end: an emission
+  // at j == n of an open-ended shard reads it before the halo check flags the window)
+  ST_TRY(hipMalloc((void**)&h.d_off, (h.n + 1) * 8));
+  ST_TRY(hipMemcpyAsync(h.d_off + h.n, &h.len, 8, hipMemcpyHostToDevice, st));
   {
     size_t bytes = 0;
     rocprim::counting_iterator<uint64_t> idx(0);

@@ -184,6 +184,33 @@ void segment_graphemes(const uint8_t* s, uint64_t n, std::vector<uint64_t>& star
   }
 }
 
+// A shard cut at byte p: the previous character is ASCII and not CR, so no rule of
+// segment_graphemes above keeps p inside a cluster unless the character at p is Extend, ZWJ or
+// SpacingMark (GB9, GB9a); and after an ASCII character every piece of state (ri_run, pict, gb11,
+// incb_state) depends on the character at p alone, so segmenting from p reproduces exactly the
+// boundaries the whole text has from p on.
+bool ascii_only(const uint8_t* s, uint64_t n) {
+  uint64_t i = 0, acc = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    std::memcpy(&w, s + i, 8);
+    acc |= w;
+    if ((i & 4095) == 0 && (acc & 0x8080808080808080ull)) return false;
+  }
+  for (; i < n; ++i) acc |= s[i];
+  return (acc & 0x8080808080808080ull) == 0;
+}
+
+bool safe_cut(const uint8_t* s, uint64_t n, uint64_t p) {
+  if (p == 0 || p >= n) return true;
+  const uint8_t prev = s[p - 1];
+  if (prev >= 0x80 || prev == '\r') return false;
+  if ((s[p] & 0xC0) == 0x80) return false;  // not a code point start
+  uint64_t i = p;
+  const uint8_t g = gcb(utf8_decode(s, n, i));
+  return g != GCB_Extend && g != GCB_ZWJ && g != GCB_SpacingMark;
+}
+
 int lower_full(uint32_t cp, uint32_t out[3]) {
   if (cp < 0x80) {
     out[0] = (cp >= 'A' && cp <= 'Z') ? cp + 32 : cp;

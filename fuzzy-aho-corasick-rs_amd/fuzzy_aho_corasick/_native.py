@@ -18,6 +18,7 @@ FAC_E_HIP = 102
 FAC_E_NO_DEVICE = 103
 FAC_E_OOM = 104
 FAC_E_CAPACITY = 105
+FAC_E_OUTPUT_CAPACITY = 106
 LIMIT_NONE = -1
 
 
@@ -79,6 +80,12 @@ class fac_stats(ctypes.Structure):
                 ("lane_windows", ctypes.c_uint64)]
 
 
+class fac_search_args(ctypes.Structure):
+    _fields_ = [("window_begin", ctypes.c_uint64), ("window_end", ctypes.c_uint64), ("threshold", ctypes.c_float),
+                ("stream", ctypes.c_void_p), ("auto_beam_prefix", ctypes.c_uint64), ("device_out", ctypes.c_void_p),
+                ("device_cap", ctypes.c_uint64)]
+
+
 assert ctypes.sizeof(fac_match) == 32
 
 if not os.path.exists(LIB_PATH):
@@ -112,6 +119,18 @@ SIGNATURES = {
     "fac_search_staged": (ctypes.c_int, [_engine_p, _hay_p, ctypes.c_uint64, ctypes.c_uint64,
                                          ctypes.c_float, ctypes.c_void_p, _P(_P(fac_match)), _u64p,
                                          _P(fac_stats)]),
+    "fac_search_staged_ex": (ctypes.c_int, [_engine_p, _hay_p, _P(fac_search_args), _P(_P(fac_match)), _u64p,
+                                            _P(fac_stats)]),
+    "fac_auto_beam_total": (ctypes.c_int, [_engine_p, _hay_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float,
+                                           ctypes.c_void_p, _u64p]),
+    "fac_shard_plan": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint64,
+                                      ctypes.c_uint64, _P(ctypes.c_uint64)]),
+    "fac_haystack_stage_shard": (ctypes.c_int, [_engine_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, _P(_hay_p), _u64p]),
+    "fac_haystack_owned_windows": (ctypes.c_uint64, [_hay_p]),
+    "fac_stream_window_staged": (ctypes.c_int, [_engine_p, _hay_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                ctypes.c_uint64, ctypes.c_float, ctypes.c_int32, ctypes.c_void_p,
+                                                _P(_P(fac_match)), _u64p, _P(fac_stats)]),
     "fac_search_staged_prefiltered": (ctypes.c_int, [_engine_p, _hay_p, ctypes.c_float, ctypes.c_void_p,
                                                      _P(_P(fac_match)), _u64p, _P(fac_stats)]),
     "fac_matches_apply": (ctypes.c_int, [_engine_p, _P(fac_match), ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
@@ -139,6 +158,16 @@ for _name, (_res, _args) in SIGNATURES.items():
 
 def last_error() -> str:
     return lib.fac_last_error().decode("utf-8", "replace")
+
+
+def shard_plan(max_match_graphemes: int, data: bytes, n_shards: int, shard: int, is_ascii: int = -1):
+    """fac_shard_plan (host only): (a, b, e, global_ascii, open_end) — the shard owns the start
+    windows of bytes [a, b) and stages bytes [a, e)."""
+    plan = (ctypes.c_uint64 * 4)()
+    rc = lib.fac_shard_plan(max_match_graphemes, data, len(data), is_ascii, n_shards, shard, plan)
+    if rc:
+        raise ValueError(last_error())
+    return int(plan[0]), int(plan[1]), int(plan[2]), bool(plan[3] & 1), bool(plan[3] & 2)
 
 
 def grapheme_starts(data: bytes):

@@ -3,21 +3,29 @@
 Start windows are independent and the best-map key holds the start byte (search.rs:444, 694), so
 the path shards with no data-path collective; the only exchange is the final gather of the
 32-byte Match records (the crate's OwnedMatch POD, stream.rs:719-745) to rank 0:
-  * batch mode  (C4): every rank searches its own haystack;
-  * shard mode (C2/C3 on N GPUs): every rank searches the start windows [a_r, b_r) of one
-    haystack (`shard_bounds`), keeping the global length so `j == n` / end-byte logic is unchanged.
+  * batch mode (C4): every rank searches its own haystack;
+  * shard mode (C2/C3 on N GPUs): every rank stages only its slice of one haystack — the bytes
+    whose start windows it owns plus a halo of max_match_graphemes() + 2 graphemes, cut at
+    context-free grapheme boundaries (fac_shard_plan) — and keeps the global is_ascii, so the
+    union of the shards' records is search_raw's result on the whole haystack.
+
+The gather (`gather_device`) is an all_gather of the u64 record counts followed by point-to-point
+sends of each rank's count x 32 B straight from its HBM record buffer to rank 0's (batched
+isend/irecv: each peer has a direct xGMI link to rank 0). No rank receives records it does not
+need and nothing is padded. The reference's parallel analogue is search_stream_parallel
+(stream.rs:378-429), which fans windows out to threads and funnels their matches to one callback.
 """
 from __future__ import annotations
 
-import struct
 from typing import List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
-REC = struct.Struct("<QQIf5B3x")  # fac_match, 32 bytes
-assert REC.size == 32
+from ._native import MATCH_DTYPE
 
+REC_BYTES = 32
 Row = Tuple[int, int, int, float, int, int, int, int, int]
 
 
@@ -28,67 +36,114 @@ def shard_bounds(n_windows: int, world: int, rank: int) -> Tuple[int, int]:
     return a, a + base + (1 if rank < extra else 0)
 
 
-def pack_rows(rows: Sequence[Row]) -> torch.Tensor:
-    buf = bytearray(REC.size * len(rows))
-    for i, r in enumerate(rows):
-        REC.pack_into(buf, i * REC.size, *r)
-    return torch.frombuffer(buf, dtype=torch.uint8) if buf else torch.zeros(0, dtype=torch.uint8)
+def _wire_device(group) -> torch.device:
+    """Where collective buffers live: HBM for RCCL, host memory for gloo (CPU tests)."""
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
 
 
-def unpack_rows(t: torch.Tensor, n: int) -> List[Row]:
-    data = bytes(t[: n * REC.size].cpu().numpy().tobytes())
-    return [REC.unpack_from(data, i * REC.size) for i in range(n)]
-
-
-def gather_rows(rows: Sequence[Row], device: torch.device, dst: int = 0, group=None) -> Optional[List[Row]]:
-    """Gather every rank's Match records to `dst`: all_gather of the counts, then an all_gather of
-    the records padded to the largest count (the volume is KBs-MBs; one collective each)."""
+def gather_device(recs: torch.Tensor, n: int, dst: int = 0, group=None) -> Optional[torch.Tensor]:
+    """Gather every rank's `n` records (a uint8 tensor of >= n * 32 bytes, in HBM for RCCL) to
+    rank `dst`: all_gather of the counts, then one batched isend/irecv per peer carrying exactly
+    count * 32 bytes. Returns the concatenation in rank order on `dst` (a uint8 tensor on the wire
+    device), None elsewhere."""
     world = dist.get_world_size(group)
-    n = torch.tensor([len(rows)], dtype=torch.int64, device=device)
-    counts = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(counts, n, group=group)
+    rank = dist.get_rank(group)
+    wire = _wire_device(group)
+    cnt = torch.tensor([n], dtype=torch.int64, device=wire)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
     counts = [int(c.item()) for c in counts]
-    cap = max(1, max(counts)) * REC.size
-    mine = torch.zeros(cap, dtype=torch.uint8, device=device)
-    packed = pack_rows(rows)
-    if packed.numel():
-        mine[: packed.numel()] = packed.to(device)
-    bufs = [torch.empty_like(mine) for _ in range(world)]
-    dist.all_gather(bufs, mine, group=group)
-    if dist.get_rank(group) != dst:
+    mine = recs[: n * REC_BYTES]
+    if mine.device != wire:
+        mine = mine.to(wire)
+    if rank != dst:
+        if n:
+            dist.batch_isend_irecv([dist.P2POp(dist.isend, mine.contiguous(), dist.get_global_rank(group, dst)
+                                               if group is not None else dst, group)])[0].wait()
         return None
-    out: List[Row] = []
-    for b, c in zip(bufs, counts):
-        out.extend(unpack_rows(b, c))
+    offs = np.concatenate([[0], np.cumsum(counts)]) * REC_BYTES
+    out = torch.empty(int(offs[-1]), dtype=torch.uint8, device=wire)
+    if n:
+        out[offs[rank]: offs[rank] + n * REC_BYTES].copy_(mine)
+    ops = []
+    for r in range(world):
+        if r == rank or counts[r] == 0:
+            continue
+        src = dist.get_global_rank(group, r) if group is not None else r
+        ops.append(dist.P2POp(dist.irecv, out[offs[r]: offs[r + 1]], src, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
     return out
 
 
-def gather_records(recs, device: torch.device, dst: int = 0, group=None):
-    """gather_rows for a NumPy array of 32-byte records (fac_match): the records travel as bytes,
-    rank `dst` receives one concatenated array."""
-    import numpy as np
-    from ._native import MATCH_DTYPE
-    world = dist.get_world_size(group)
-    n = torch.tensor([len(recs)], dtype=torch.int64, device=device)
-    counts = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(counts, n, group=group)
-    counts = [int(c.item()) for c in counts]
-    cap = max(1, max(counts)) * REC.size
-    mine = torch.zeros(cap, dtype=torch.uint8, device=device)
-    if len(recs):
-        mine[: len(recs) * REC.size] = torch.from_numpy(np.ascontiguousarray(recs).view(np.uint8)).to(device)
-    bufs = [torch.empty_like(mine) for _ in range(world)]
-    dist.all_gather(bufs, mine, group=group)
-    if dist.get_rank(group) != dst:
+def records_to_tensor(recs: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(recs).view(np.uint8).reshape(-1))
+
+
+def tensor_to_records(t: torch.Tensor) -> np.ndarray:
+    return t.cpu().numpy().view(MATCH_DTYPE)
+
+
+def gather_records(recs: np.ndarray, dst: int = 0, group=None) -> Optional[np.ndarray]:
+    """gather_device for a host NumPy array of 32-byte records (MATCH_DTYPE)."""
+    t = records_to_tensor(recs)
+    got = gather_device(t, len(recs), dst, group)
+    return None if got is None else tensor_to_records(got)
+
+
+def gather_rows(rows: Sequence[Row], dst: int = 0, group=None) -> Optional[List[Row]]:
+    """gather_records for row tuples (start, end, pattern, sim, ins, del, sub, swp, edits)."""
+    recs = np.zeros(len(rows), dtype=MATCH_DTYPE)
+    if rows:
+        cols = list(zip(*rows))
+        for name, col in zip(("start", "end", "pattern_index", "similarity", "insertions", "deletions",
+                              "substitutions", "swaps", "edits"), cols):
+            recs[name] = col
+    got = gather_records(recs, dst, group)
+    if got is None:
         return None
-    parts = [b[: c * REC.size].cpu().numpy().view(MATCH_DTYPE) for b, c in zip(bufs, counts)]
-    return np.concatenate(parts) if parts else np.zeros(0, dtype=MATCH_DTYPE)
+    return [(int(r["start"]), int(r["end"]), int(r["pattern_index"]), float(r["similarity"]), int(r["insertions"]),
+             int(r["deletions"]), int(r["substitutions"]), int(r["swaps"]), int(r["edits"])) for r in got]
 
 
-def sharded_search(staged, threshold: float, device: torch.device, group=None) -> Optional[List[Row]]:
-    """Search one staged haystack across the group's ranks; rank 0 receives the full raw result
-    (identical to search_raw on the whole haystack)."""
+def check_grapheme_total(owned_graphemes: int, group=None) -> None:
+    """search_raw refuses a haystack of more than u32::MAX graphemes (search.rs:198-201); a sharded
+    haystack is refused the same way, on the global count."""
+    from .structs import HaystackTooLarge
+    t = torch.tensor([owned_graphemes], dtype=torch.int64, device=_wire_device(group))
+    dist.all_reduce(t, group=group)
+    total = int(t.item())
+    if total > 0xFFFFFFFF:
+        raise HaystackTooLarge(total)
+
+
+def auto_beam_prefix(staged, threshold: float, group=None) -> int:
+    """Running auto-beam total (search.rs:1096-1103) of every window before this rank's shard: each
+    rank counts its own windows unbeamed (fac_auto_beam_total), the totals are all-gathered and the
+    exclusive prefix is this rank's starting total."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    a, b = shard_bounds(staged.graphemes, world, rank)
-    rows, _ = staged.search_windows(threshold, a, b)
-    return gather_rows(rows, device, 0, group)
+    t = torch.tensor([staged.auto_beam_total(threshold)], dtype=torch.int64, device=_wire_device(group))
+    totals = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(totals, t, group=group)
+    return int(sum(int(x.item()) for x in totals[:rank]))
+
+
+def sharded_search(engine, data: bytes, threshold: float, group=None, staged=None, is_ascii: int = -1):
+    """search_raw of one haystack across the group's ranks (one GPU each): every rank stages its
+    halo-sliced shard, searches its start windows with the records left in HBM and sends them to
+    rank 0, which returns the full raw result as a NumPy record array (None on other ranks)."""
+    from .engine import StagedHaystack
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if staged is None:
+        staged = StagedHaystack.shard(engine, data, world, rank, is_ascii)
+    check_grapheme_total(staged.owned_windows, group)
+    prefix = 0
+    b = engine.builder
+    if b._auto_beam is not None and b._beam_width is None:
+        prefix = auto_beam_prefix(staged, threshold, group)
+    recs, n, _ = staged.search_device(threshold, auto_beam_prefix=prefix)
+    got = gather_device(recs, n, 0, group)
+    return None if got is None else tensor_to_records(got)

@@ -391,18 +391,87 @@ class _Stream:
 
 
 class StagedHaystack:
-    """A haystack staged into HBM once (fac_haystack_stage) and searched many times."""
+    """A haystack staged into HBM once (fac_haystack_stage) and searched many times.
 
-    def __init__(self, engine: FuzzyAhoCorasick, data: bytes):
+    `StagedHaystack.shard(engine, data, n, r)` stages only shard r of n of `data` (its owned bytes
+    plus the halo, fac_shard_plan): searching it yields search_raw's records for the shard's start
+    windows at global byte offsets."""
+
+    def __init__(self, engine: FuzzyAhoCorasick, data: bytes, _shard=None):
         self.engine = engine
         self.data = data
         h = ctypes.c_void_p()
         eg = ctypes.c_uint64()
-        rc = _native.lib.fac_haystack_stage(engine._h, data, len(data), ctypes.byref(h), ctypes.byref(eg))
+        if _shard is None:
+            rc = _native.lib.fac_haystack_stage(engine._h, data, len(data), ctypes.byref(h), ctypes.byref(eg))
+            self.base, self.owned_bytes, self.open_end, self.plan = 0, len(data), False, None
+        else:
+            a, b, e, asc, open_end = _shard
+            piece = data[a:e]
+            rc = _native.lib.fac_haystack_stage_shard(engine._h, piece, len(piece), b - a, int(asc), int(open_end), a,
+                                                      ctypes.byref(h), ctypes.byref(eg))
+            self.base, self.owned_bytes, self.open_end, self.plan = a, b - a, open_end, _shard
         if rc:
             _raise(rc, eg.value)
         self._h = h
         self.graphemes = int(_native.lib.fac_haystack_graphemes(h))
+        self.owned_windows = int(_native.lib.fac_haystack_owned_windows(h))
+        self._dev_out = None  # growable device record buffer (search_device)
+
+    @classmethod
+    def shard(cls, engine: FuzzyAhoCorasick, data: bytes, n_shards: int, shard: int, is_ascii: int = -1):
+        plan = _native.shard_plan(engine.max_match_graphemes(), data, n_shards, shard, is_ascii)
+        return cls(engine, data, _shard=plan)
+
+    def search_device(self, threshold: float, window_begin: int = 0, window_end: int = None, stream=None,
+                      auto_beam_prefix: int = 0, torch_device=None):
+        """fac_search_staged_ex with the records left in HBM: (uint8 tensor of n * 32 bytes on the
+        engine's device, n, fac_stats). The buffer is reused across calls and grown on demand."""
+        import torch
+        dev = torch_device or torch.device("cuda", self.engine.device)
+        if window_end is None:
+            window_end = self.graphemes
+        while True:
+            if self._dev_out is None:
+                self._dev_out = torch.empty(max(4096, self.owned_windows // 64) * 32, dtype=torch.uint8, device=dev)
+            a = _native.fac_search_args(window_begin, window_end, f32(threshold), ctypes.c_void_p(stream or 0),
+                                        auto_beam_prefix, ctypes.c_void_p(self._dev_out.data_ptr()),
+                                        self._dev_out.numel() // 32)
+            n = ctypes.c_uint64()
+            st = _native.fac_stats()
+            rc = _native.lib.fac_search_staged_ex(self.engine._h, self._h, ctypes.byref(a), None, ctypes.byref(n),
+                                                  ctypes.byref(st))
+            if rc == _native.FAC_E_OUTPUT_CAPACITY:
+                self._dev_out = torch.empty(int(n.value * 1.25 + 1024) * 32, dtype=torch.uint8, device=dev)
+                continue
+            if rc:
+                _raise(rc)
+            return self._dev_out[: n.value * 32], int(n.value), st
+
+    def auto_beam_total(self, threshold: float, window_begin: int = 0, window_end: int = None, stream=None) -> int:
+        """fac_auto_beam_total: sum of queue.len() over the windows searched unbeamed."""
+        if window_end is None:
+            window_end = self.graphemes
+        t = ctypes.c_uint64()
+        rc = _native.lib.fac_auto_beam_total(self.engine._h, self._h, window_begin, window_end, f32(threshold),
+                                             ctypes.c_void_p(stream or 0), ctypes.byref(t))
+        if rc:
+            _raise(rc)
+        return int(t.value)
+
+    def stream_window(self, g_begin: int, g_end: int, commit_bytes: int, base: int, threshold: float,
+                      prefilter: bool, stream=None):
+        """fac_stream_window_staged (stream.rs:262-297 window_matches on a device-resident window):
+        NumPy records (MATCH_DTYPE) of the window's owned matches at absolute offsets + fac_stats."""
+        out = ctypes.POINTER(_native.fac_match)()
+        n = ctypes.c_uint64()
+        st = _native.fac_stats()
+        rc = _native.lib.fac_stream_window_staged(self.engine._h, self._h, g_begin, g_end, commit_bytes, base,
+                                                  f32(threshold), int(prefilter), ctypes.c_void_p(stream or 0),
+                                                  ctypes.byref(out), ctypes.byref(n), ctypes.byref(st))
+        if rc:
+            _raise(rc)
+        return _native.take_records(out, n.value), st
 
     def __del__(self):
         h = getattr(self, "_h", None)

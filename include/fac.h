@@ -25,6 +25,12 @@
  *   FAC_E_OOM                 104   host or device allocation failure
  *   FAC_E_CAPACITY            105   a per-window device work buffer overflowed even after the
  *                                   automatic retries (pathological input)
+ *   FAC_E_OUTPUT_CAPACITY     106   the caller's device output buffer is too small; *n_out holds
+ *                                   the record count needed (fac_search_staged_ex)
+ *
+ * Diagnostics: the library reads FAC_* environment knobs (kernel variants, prefix-cache levels,
+ * FAC_GRAPHEME_LIMIT, ...) only when FAC_DIAGNOSTICS=1 is set; otherwise the search path depends
+ * on the arguments alone.
  */
 #ifndef FAC_H
 #define FAC_H
@@ -44,6 +50,7 @@ extern "C" {
 #define FAC_E_NO_DEVICE 103
 #define FAC_E_OOM 104
 #define FAC_E_CAPACITY 105
+#define FAC_E_OUTPUT_CAPACITY 106
 
 #define FAC_LIMIT_NONE (-1)
 
@@ -184,6 +191,58 @@ void fac_haystack_free(fac_haystack* hay);
 int fac_search_staged(const fac_engine* engine, const fac_haystack* hay, uint64_t window_begin,
                       uint64_t window_end, float threshold, void* stream, fac_match** out,
                       uint64_t* n_out, fac_stats* stats);
+
+/* Extended staged search. Records go to the host (*out, fac_matches_free) or, with device_out set,
+ * straight into that device buffer of device_cap records on the engine's device (no host copy: the
+ * multi-GPU gather sends them over RCCL from there); *n_out is the record count either way, and
+ * FAC_E_OUTPUT_CAPACITY means the buffer was too small (grow it to *n_out and search again).
+ * auto_beam_prefix: for a shard of one haystack, the running auto-beam total (sum of queue.len())
+ * of every window before this shard (search.rs:1096-1103; fac_auto_beam_total), 0 otherwise. */
+typedef struct fac_search_args {
+  uint64_t window_begin;
+  uint64_t window_end;
+  float threshold;
+  void* stream;
+  uint64_t auto_beam_prefix;
+  void* device_out;
+  uint64_t device_cap;
+} fac_search_args;
+int fac_search_staged_ex(const fac_engine* engine, const fac_haystack* hay, const fac_search_args* args,
+                         fac_match** out, uint64_t* n_out, fac_stats* stats);
+
+/* Auto-beam pass 1 alone (search.rs:1096-1103): the sum of queue.len() over the start windows
+ * [window_begin, window_end) searched unbeamed. A sharded search of an auto-beam engine exchanges
+ * these totals so every shard switches the beam on at the same global window as search_raw. */
+int fac_auto_beam_total(const fac_engine* engine, const fac_haystack* hay, uint64_t window_begin, uint64_t window_end,
+                        float threshold, void* stream, uint64_t* total);
+
+/* Sharding one haystack over n_shards GPUs. fac_shard_plan cuts the bytes into
+ * contiguous shards at grapheme boundaries whose segmentation needs no left context (any byte of
+ * an ASCII haystack; otherwise after an ASCII non-CR character, before a character that is not
+ * Extend/ZWJ/SpacingMark; host-only, no device needed) and returns plan = {a, b, e, flags}: the shard owns the start windows of
+ * bytes [a, b) and must stage bytes [a, e), e = b plus max_match_graphemes() + 2 graphemes (the
+ * stream overlap of stream.rs:256-258 and the text[j+1] lookahead; max_match_graphemes is
+ * fac_max_match_graphemes(engine)), flags bit 0 = global is_ascii,
+ * bit 1 = the text continues past e. is_ascii: the haystack's is_ascii if known, -1 to compute it.
+ * fac_haystack_stage_shard stages such a slice: searched with fac_search_staged[_ex] it yields
+ * exactly the records search_raw of the whole haystack yields for the owned start windows, at
+ * global byte offsets (slice offset + base). */
+int fac_shard_plan(uint64_t max_match_graphemes, const uint8_t* utf8, uint64_t len, int32_t is_ascii, uint64_t n_shards,
+                   uint64_t shard, uint64_t plan[4]);
+int fac_haystack_stage_shard(const fac_engine* engine, const uint8_t* utf8, uint64_t len, uint64_t owned_bytes,
+                             int32_t global_ascii, int32_t open_end, uint64_t base, fac_haystack** out,
+                             uint64_t* err_graphemes);
+/* start windows a staged haystack owns (all of them unless it is a shard) */
+uint64_t fac_haystack_owned_windows(const fac_haystack* hay);
+
+/* One streaming window on the device (stream.rs:262-297 window_matches): the graphemes
+ * [g_begin, g_end) of a staged haystack are searched as the window's text (Prefiltered::search if
+ * `prefilter`, else search), ranked sorted().non_overlapping() (matches.rs), and the matches the
+ * window owns (start byte < commit_bytes, relative to the window) are returned at absolute offsets
+ * base + window offset. */
+int fac_stream_window_staged(const fac_engine* engine, const fac_haystack* hay, uint64_t g_begin, uint64_t g_end,
+                             uint64_t commit_bytes, uint64_t base, float threshold, int32_t prefilter, void* stream,
+                             fac_match** out, uint64_t* n_out, fac_stats* stats);
 
 /* Prefiltered::raw on a staged haystack (prefilter.rs:146-155, 304-374): the bitap scan and the
  * window merge run on the device-resident text, each merged window is re-searched as its own

@@ -706,7 +706,7 @@ void bitap_windows(const std::vector<uint64_t>& mask, size_t m, size_t k, const 
   }
 }
 
-uint64_t g_deg_hist[80];  // diagnostics only (degree / edits histogram of expanded states)
+thread_local uint64_t g_deg_hist[80];  // diagnostics only (degree / edits histogram of expanded states); per thread: the CPU baseline runs the oracle on several threads
 
 // Staging for a (sub)haystack: ASCII fast path or caller-provided global graphemes.
 struct Staged {

@@ -9,6 +9,10 @@ for p in (REPO, PKG_DIR, os.path.join(REPO, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# The library honours its FAC_* tuning / test knobs only in diagnostics mode (fac.h); the tests use
+# them (monkeypatch.setenv) to force kernel paths.
+os.environ["FAC_DIAGNOSTICS"] = "1"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 (MI355X) GPU; run on the GPU box")

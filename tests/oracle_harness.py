@@ -198,6 +198,9 @@ class OracleEngine:
         self.states_popped = popped.value
         return rows
 
+    def prepare(self, data: bytes) -> "PreparedText":
+        return PreparedText(self, data)
+
     def prefilter_windows(self, haystack, threshold):
         data = haystack.encode("utf-8")
         goff, cps = [0], []
@@ -269,6 +272,106 @@ class OracleReplacer:
 
     def replace(self, text, opts):
         return self.engine.replace(text, opts, lambda m: self.replacements[m.pattern_index])
+
+
+class PreparedText:
+    """A haystack staged once for the oracle (regex \\X segmentation + str.lower folding, as in
+    raw_rows, but into NumPy arrays so large prefixes stage in seconds) and searched with one or
+    several threads. ctypes releases the GIL around the oracle call, so `threads` > 1 runs the
+    oracle on that many cores at once: the start windows are split into contiguous ranges (the
+    union is search_raw's result, like search_stream_parallel, stream.rs:378-429); with the
+    pre-filter every thread searches its own slice of the text (stream windows with
+    max_match_graphemes() + 1 of overlap, each keeping the matches that start in its slice)."""
+
+    def __init__(self, engine: "OracleEngine", data: bytes):
+        import numpy as np
+        self.engine, self.data = engine, data
+        text = data.decode("utf-8")
+        self.ascii = data.isascii()
+        if self.ascii:
+            self.n = len(data)
+            goff = np.zeros(1, np.uint32)
+            cps = np.zeros(1, np.uint32)
+            boff = np.zeros(1, np.uint64)
+        else:
+            gs = graphemes(text)
+            self.n = len(gs)
+            cp = np.frombuffer(text.encode("utf-32-le"), dtype=np.uint32)
+            simple = len(cp) == len(gs)
+            if simple and engine.ci:
+                uniq = np.unique(cp)
+                low = [chr(int(c)).lower() for c in uniq]
+                simple = all(len(x) == 1 for x in low)
+                if simple:
+                    cp = np.array([ord(x) for x in low], np.uint32)[np.searchsorted(uniq, cp)]
+            if simple:  # one code point per grapheme, folding keeps it one code point
+                cps = cp.astype(np.uint32)
+                goff = np.arange(self.n + 1, dtype=np.uint32)
+                raw = np.frombuffer(text.encode("utf-32-le"), dtype=np.uint32)
+                ln = 1 + (raw >= 0x80) + (raw >= 0x800) + (raw >= 0x10000)
+                boff = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.uint64)
+            else:
+                c, go, bo, pos = [], [0], [], 0
+                for g in gs:
+                    bo.append(pos)
+                    pos += len(g.encode("utf-8"))
+                    c += [ord(ch) for ch in fold(g, engine.ci)]
+                    go.append(len(c))
+                cps, goff, boff = (np.array(c or [0], np.uint32), np.array(go, np.uint32),
+                                   np.array(bo or [0], np.uint64))
+        self._arrs = (goff, cps, boff)
+
+    def _run(self, threshold, prefilter, w0, w1, data=None, arrs=None, n=None):
+        data = self.data if data is None else data
+        goff, cps, boff = self._arrs if arrs is None else arrs
+        n = (0 if self.ascii else self.n) if n is None else n
+        P = ctypes.POINTER
+        out = P(orc_match)()
+        cnt = ctypes.c_uint64()
+        popped = ctypes.c_uint64()
+        rc = _lib.orc_search_windows(self.engine._h, data, len(data), n,
+                                     goff.ctypes.data_as(_U32P), cps.ctypes.data_as(_U32P),
+                                     boff.ctypes.data_as(P(ctypes.c_uint64)), f32(threshold), int(prefilter),
+                                     ctypes.byref(out), ctypes.byref(cnt), ctypes.byref(popped), w0, w1)
+        if rc:
+            raise RuntimeError(f"oracle error {rc}")
+        rows = [(out[i].start, out[i].end, out[i].pattern) for i in range(cnt.value)]
+        _lib.orc_matches_free(out)
+        return rows
+
+    def search(self, threshold, prefilter=False, threads=1):
+        """Raw (start, end, pattern) triples of search_raw / Prefiltered::raw."""
+        if threads <= 1:
+            return self._run(threshold, prefilter, 0, 0xFFFFFFFF)
+        import threading
+        res = [None] * threads
+        if not prefilter:
+            def work(t):
+                a, b = self.n * t // threads, self.n * (t + 1) // threads
+                res[t] = self._run(threshold, False, a, b)
+        else:
+            # stream windows: byte slices cut at spaces (ASCII) with max_match + 1 of overlap
+            over = 64 + 4 * max(len(p.pattern) for p in self.engine.patterns_)
+            cuts = [0]
+            for t in range(1, threads):
+                c = len(self.data) * t // threads
+                while c < len(self.data) and self.data[c - 1] != 0x20:
+                    c += 1
+                cuts.append(c)
+            cuts.append(len(self.data))
+
+            def work(t):
+                a, b = cuts[t], cuts[t + 1]
+                piece = self.data[a:min(len(self.data), b + over)]
+                sub = PreparedText(self.engine, piece)
+                res[t] = [(s + a, e + a, p) for (s, e, p) in sub._run(threshold, True, 0, 0xFFFFFFFF)
+                          if s < b - a]
+        ts = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+        for th in ts:
+            th.start()
+        for th in ts:
+            th.join()
+        return [r for part in res for r in part]
 
 
 def bitap_ends(pattern: bytes, text: bytes, k: int):

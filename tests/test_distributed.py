@@ -1,9 +1,16 @@
-"""World-size-2 tests of the multi-rank path: shard the start windows of one haystack across two
-processes, gather the 32-byte Match records to rank 0 with torch.distributed, and check the union
-equals the single-process search. CPU variant: gloo + the oracle as the per-rank compute; GPU
-variant: gloo for the exchange, both ranks' searches on cuda:0 through the C ABI."""
+"""Multi-rank paths: shard planning, halo-sliced shards, the record gather to rank 0
+and the bench launcher.
+
+CPU tests use gloo with world sizes 2 and 4 and the oracle as each rank's compute: every rank
+searches only its staged slice (owned bytes + halo, as cut by the C ABI's fac_shard_plan) and the
+union gathered on rank 0 must equal the oracle's search_raw of the whole haystack. GPU tests run
+the product's sharded_search (both ranks on cuda:0, gloo for the exchange) against the same
+whole-haystack oracle, including an auto-beam engine whose budget is crossed inside rank 0's shard.
+"""
+import json
 import os
 import socket
+import subprocess
 import sys
 import tempfile
 
@@ -13,7 +20,8 @@ import torch.multiprocessing as mp
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 PATTERNS = ["needle", "haystack", "fuzzy", "automaton", "école", "Москва"]
-HAY = ("a needle in a haystakc, fuzzy automatn; ecole Москва école nedle " * 40).strip()
+HAY_UNI = ("a needle in a haystakc, fuzzy automatn; ecole Москва école nedle " * 40).strip()
+HAY_ASCII = ("a needle in a haystakc, fuzzy automatn; nedle hasytack autmaton fuzyz " * 40).strip()
 
 
 def _free_port():
@@ -24,46 +32,71 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, use_gpu, out_path):
+def _builder(kind):
+    from fuzzy_aho_corasick import FuzzyAhoCorasickBuilder, FuzzyLimits
+    b = FuzzyAhoCorasickBuilder().case_insensitive(True).device(0)
+    if kind == "e1":
+        return b.fuzzy(FuzzyLimits().edits(1))
+    if kind == "e2beam":
+        return b.fuzzy(FuzzyLimits().edits(2)).beam_width(8)
+    if kind == "autobeam":  # the budget is crossed a few dozen windows into the haystack
+        return b.fuzzy(FuzzyLimits().edits(2)).auto_beam(400, 4)
+    raise ValueError(kind)
+
+
+def _mmg(patterns, edits):
+    from oracle_harness import graphemes
+    return max(len(graphemes(p)) for p in patterns) + edits
+
+
+def _worker(rank, world, port, use_gpu, kind, hay, out_path):
     sys.path[:0] = [os.path.join(REPO, "fuzzy-aho-corasick-rs_amd"), os.path.join(REPO, "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    import torch
     import torch.distributed as dist
-    from fuzzy_aho_corasick import FuzzyAhoCorasickBuilder, FuzzyLimits
-    from fuzzy_aho_corasick.distributed import gather_rows, shard_bounds
+    from fuzzy_aho_corasick import _native
+    from fuzzy_aho_corasick.distributed import gather_rows, sharded_search
+    from oracle_harness import OracleEngine
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    b = FuzzyAhoCorasickBuilder().fuzzy(FuzzyLimits().edits(1)).case_insensitive(True).device(0)
+    b = _builder(kind)
+    data = hay.encode("utf-8")
+    orc = OracleEngine(b, PATTERNS)
+    full = sorted(orc.raw_rows(hay, 0.7)) if rank == 0 else None
     if use_gpu:
-        staged = b.build(PATTERNS).stage(HAY.encode("utf-8"))
-        a, e = shard_bounds(staged.graphemes, world, rank)
-        rows, _ = staged.search_windows(0.7, a, e)
-        full = staged.search_windows(0.7)[0] if rank == 0 else None
+        recs = sharded_search(b.build(PATTERNS), data, 0.7)
+        got = None if recs is None else sorted(
+            (int(r["start"]), int(r["end"]), int(r["pattern_index"]), float(r["similarity"]), int(r["insertions"]),
+             int(r["deletions"]), int(r["substitutions"]), int(r["swaps"]), int(r["edits"])) for r in recs)
     else:
-        from oracle_harness import OracleEngine, graphemes
-        eng = OracleEngine(b, PATTERNS)
-        n = len(graphemes(HAY))
-        a, e = shard_bounds(n, world, rank)
-        rows = eng.raw_rows(HAY, 0.7, windows=(a, e))
-        full = eng.raw_rows(HAY, 0.7) if rank == 0 else None
-    got = gather_rows(rows, torch.device("cpu"))
+        edits = 2 if kind != "e1" else 1
+        a, bb, e, asc, open_end = _native.shard_plan(_mmg(PATTERNS, edits), data, world, rank)
+        piece = data[a:e]
+        if asc:
+            owned = bb - a
+        else:  # owned start windows = graphemes of the owned bytes
+            from oracle_harness import graphemes
+            owned = len(graphemes(piece[: bb - a].decode("utf-8")))
+        rows = orc.raw_rows(piece, 0.7, windows=(0, owned)) if bb > a else []
+        rows = [(s + a, en + a) + tuple(r) for (s, en, *r) in rows]
+        got = gather_rows(rows)
+        got = None if got is None else sorted(got)
     if rank == 0:
         with open(out_path, "w") as f:
-            f.write(repr((sorted(got), sorted(full))))
+            f.write(repr((got, full)))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(use_gpu):
+def _run(world, use_gpu, kind, hay):
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res.txt")
-        mp.spawn(_worker, args=(2, _free_port(), use_gpu, out), nprocs=2, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), use_gpu, kind, hay, out), nprocs=world, join=True)
         got, full = eval(open(out).read())
-    assert got == full and len(full) > 10
+    assert len(full) > 10
+    assert got == full
 
 
 def test_shard_bounds_partition():
-    sys.path.insert(0, os.path.join(REPO, "fuzzy-aho-corasick-rs_amd"))
     from fuzzy_aho_corasick.distributed import shard_bounds
     for n in (0, 1, 7, 1000, 1001):
         for w in (1, 2, 3, 8):
@@ -72,42 +105,105 @@ def test_shard_bounds_partition():
             assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
 
 
-def test_two_rank_gloo_shard_and_gather_cpu():
-    _run(False)
+@pytest.mark.parametrize("hay", [HAY_ASCII, HAY_UNI, "éé ab‍c 👍🏽x " * 30 + "a\r\nb " * 20])
+def test_shard_plan_cuts_at_context_free_boundaries(hay):
+    """Shards tile the bytes, every cut is a grapheme boundary of the whole text, and the halo holds
+    max_match_graphemes() + 2 complete graphemes past the owned bytes (or reaches the end)."""
+    from fuzzy_aho_corasick import _native
+    from oracle_harness import graphemes
+    data = hay.encode("utf-8")
+    starts, pos = set(), 0
+    for g in graphemes(hay):
+        starts.add(pos)
+        pos += len(g.encode("utf-8"))
+    starts.add(len(data))
+    asc = data.isascii()
+    for world in (1, 2, 3, 4, 8):
+        plans = [_native.shard_plan(7, data, world, r) for r in range(world)]
+        assert plans[0][0] == 0 and plans[-1][1] == len(data)
+        for r, (a, b, e, g_asc, open_end) in enumerate(plans):
+            assert g_asc == asc and a <= b <= e <= len(data)
+            assert open_end == (e < len(data))
+            if r + 1 < world:
+                assert plans[r + 1][0] == b
+            if not asc:
+                assert a in starts and b in starts and e in starts
+            if e < len(data):
+                n_halo = len(data[b:e]) if asc else len(graphemes(data[b:e].decode("utf-8")))
+                assert n_halo == 7 + 2
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("kind,hay", [("e1", HAY_ASCII), ("e1", HAY_UNI), ("e2beam", HAY_UNI)])
+def test_sharded_oracle_equals_whole_cpu(world, kind, hay):
+    """Halo-sliced shards searched as their own texts, gathered over gloo == whole search_raw."""
+    _run(world, False, kind, hay)
 
 
 @pytest.mark.gpu
-def test_two_rank_gloo_shard_and_gather_gpu():
-    _run(True)
+@pytest.mark.parametrize("kind,hay", [("e1", HAY_ASCII), ("e1", HAY_UNI), ("e2beam", HAY_UNI),
+                                      ("autobeam", HAY_UNI)])
+def test_sharded_search_gpu(kind, hay):
+    """sharded_search (halo-sliced staging, device records, gather) on 2 ranks == oracle whole."""
+    _run(2, True, kind, hay)
 
 
 def _rec_worker(rank, world, port, out_path):
     sys.path[:0] = [os.path.join(REPO, "fuzzy-aho-corasick-rs_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import numpy as np
-    import torch
     import torch.distributed as dist
     from fuzzy_aho_corasick._native import MATCH_DTYPE
     from fuzzy_aho_corasick.distributed import gather_records
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    recs = np.zeros(3 + rank, dtype=MATCH_DTYPE)
-    recs["start"] = np.arange(len(recs)) + 100 * rank
+    n = 0 if rank == 1 else 3 + rank  # rank 1 contributes nothing
+    recs = np.zeros(n, dtype=MATCH_DTYPE)
+    recs["start"] = np.arange(n) + 100 * rank
     recs["end"] = recs["start"] + 5
     recs["pattern_index"] = rank
     recs["similarity"] = np.float32(0.5 + rank / 8)
-    got = gather_records(recs, torch.device("cpu"))
+    got = gather_records(recs)
     if rank == 0:
         with open(out_path, "w") as f:
             f.write(repr([(int(r["start"]), int(r["end"]), int(r["pattern_index"]), float(r["similarity"])) for r in got]))
+    else:
+        assert got is None
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_gather_records_cpu():
-    """The bench's record-array gather (32-byte fac_match structs as bytes over the collective)."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_gather_records_to_rank0_cpu(world):
+    """Counts all-gather + point-to-point sends: rank 0 gets every record in rank order, others None."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res.txt")
-        mp.spawn(_rec_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+        mp.spawn(_rec_worker, args=(world, _free_port(), out), nprocs=world, join=True)
         got = eval(open(out).read())
-    want = [(i, i + 5, 0, 0.5) for i in range(3)] + [(100 + i, 105 + i, 1, 0.625) for i in range(4)]
+    want = []
+    for r in range(world):
+        n = 0 if r == 1 else 3 + r
+        want += [(100 * r + i, 100 * r + i + 5, r, 0.5 + r / 8) for i in range(n)]
     assert got == want
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_gpus_flag_launches_ranks(n):
+    """`bench.py --gpus N` outside torchrun launches N ranks itself (dry run: launcher + gather
+    plumbing on gloo, no GPU) and rank 0 reports n_gpus = N."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--dry-run", "--steps", "1"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1
+    j = json.loads(line[0])
+    assert j["n_gpus"] == n
+    assert j["config"]["records_gathered_per_step"] == sum(1000 + k for k in range(n))
+
+
+def test_bench_rejects_mismatched_world():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)
