@@ -135,17 +135,18 @@ class FuzzyMatches:
     # -- overlap resolution (matches.rs:86-149)
     def non_overlapping(self):
         occupied: List[tuple] = []
+        starts: List[int] = []  # occupied's starts, kept beside it (one bisect per match)
         kept = []
         import bisect
         for m in self.inner:
-            starts = [s for s, _ in occupied]
+            # binary_search Ok(idx)/Err(idx): equal starts occur only for empty spans, where every
+            # choice of idx gives the same accept/reject decisions
             pos = bisect.bisect_left(starts, m.start)
-            if pos < len(occupied) and occupied[pos][0] == m.start:
-                pass  # binary_search Ok(idx) -> idx (any equal index; starts are unique here)
             prev_ok = pos == 0 or occupied[pos - 1][1] <= m.start
             next_ok = pos == len(occupied) or occupied[pos][0] >= m.end
             if prev_ok and next_ok:
                 occupied.insert(pos, (m.start, m.end))
+                starts.insert(pos, m.start)
                 kept.append(m)
         kept.sort(key=lambda m: m.start)
         self.inner = kept
@@ -154,19 +155,20 @@ class FuzzyMatches:
         import bisect
         used = set()
         occupied: List[tuple] = []
+        starts: List[int] = []
         kept = []
         for m in self.inner:
             uid = ("custom", m.pattern.custom_unique_id_) if m.pattern.custom_unique_id_ is not None \
                 else ("auto", m.pattern_index)
             if uid in used:
                 continue
-            starts = [s for s, _ in occupied]
             pos = bisect.bisect_left(starts, m.start)
             prev_ok = pos == 0 or occupied[pos - 1][1] <= m.start
             next_ok = pos == len(occupied) or occupied[pos][0] >= m.end
             if prev_ok and next_ok:
                 used.add(uid)
                 occupied.insert(pos, (m.start, m.end))
+                starts.insert(pos, m.start)
                 kept.append(m)
         kept.sort(key=lambda m: m.start)
         self.inner = kept

@@ -35,6 +35,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
 #include <tuple>
 #include <unordered_map>
@@ -770,6 +771,35 @@ void search_raw_slice(const Engine& e, const Text& t, uint64_t b0, uint64_t b1, 
 
 }  // namespace
 
+namespace {
+int total_cmp(float a, float b) {  // f32::total_cmp
+  int32_t x, y;
+  std::memcpy(&x, &a, 4);
+  std::memcpy(&y, &b, 4);
+  x ^= (int32_t)(((uint32_t)(x >> 31)) >> 1);
+  y ^= (int32_t)(((uint32_t)(y >> 31)) >> 1);
+  return x < y ? -1 : (x > y ? 1 : 0);
+}
+template <typename T>
+int cmp3(T a, T b) { return a < b ? -1 : (a > b ? 1 : 0); }
+// <[T]>::binary_search_by as in Rust >= 1.82 (the crate is edition 2024): on equal keys it returns
+// the index the halving loop settles on, not necessarily the first
+template <typename F>
+std::pair<bool, size_t> rust_binary_search_by(size_t len, F f) {
+  size_t size = len;
+  if (size == 0) return {false, 0};
+  size_t base = 0;
+  while (size > 1) {
+    const size_t half = size / 2, mid = base + half;
+    if (f(mid) <= 0) base = mid;  // cmp != Greater
+    size -= half;
+  }
+  const int c = f(base);
+  if (c == 0) return {true, base};
+  return {false, base + (c < 0 ? 1 : 0)};
+}
+}  // namespace
+
 // ==========================================================================================
 // C ABI (ctypes)
 // ==========================================================================================
@@ -963,6 +993,72 @@ int32_t orc_search_windows(void* h, const uint8_t* utf8, uint64_t len, uint32_t 
 }
 
 void orc_matches_free(orc_match* m) { std::free(m); }
+
+// FuzzyMatches::apply (matches.rs:7-19): ranking by `order` (0 Unsorted, 1 Default :24-38, 2 Greedy
+// :43-57, 3 CoverageWeighted :64-81), then overlap resolution by `overlap` (0 Keep, 1 NonOverlapping
+// :86-113, 2 NonOverlappingUnique :117-149). pat_len[p] = Pattern::len() in bytes (structs.rs:628-630);
+// uid[p] = the uniqueness key of pattern p (custom_unique_id or automatic index, never equal across
+// kinds). Kept matches are compacted to the front in the reference's final order; returns the count.
+
+uint64_t orc_apply(orc_match* m, uint64_t n, int32_t order, int32_t overlap, const uint64_t* pat_len,
+                   const uint64_t* uid) {
+  std::vector<orc_match> v(m, m + n);
+  auto tail = [](const orc_match& l, const orc_match& r) {  // .then start, end, pattern_index
+    int c = cmp3(l.start, r.start);
+    if (!c) c = cmp3(l.end, r.end);
+    if (!c) c = cmp3(l.pattern, r.pattern);
+    return c;
+  };
+  if (order == 1) {
+    std::sort(v.begin(), v.end(), [&](const orc_match& l, const orc_match& r) {
+      int c = total_cmp(r.similarity, l.similarity);
+      if (!c) c = cmp3(pat_len[r.pattern], pat_len[l.pattern]);
+      if (!c) c = cmp3(r.end - r.start, l.end - l.start);  // text.len()
+      if (!c) c = tail(l, r);
+      return c < 0;
+    });
+  } else if (order == 2) {
+    std::sort(v.begin(), v.end(), [&](const orc_match& l, const orc_match& r) {
+      int c = cmp3(pat_len[r.pattern], pat_len[l.pattern]);
+      if (!c) c = total_cmp(r.similarity, l.similarity);
+      if (!c) c = tail(l, r);
+      return c < 0;
+    });
+  } else if (order == 3) {
+    auto score = [&](const orc_match& x) {  // similarity * similarity * len as f32, in that order
+      volatile float s2 = x.similarity * x.similarity;
+      return (float)(s2 * (float)pat_len[x.pattern]);
+    };
+    std::sort(v.begin(), v.end(), [&](const orc_match& l, const orc_match& r) {
+      int c = total_cmp(score(r), score(l));
+      if (!c) c = total_cmp(r.similarity, l.similarity);
+      if (!c) c = tail(l, r);
+      return c < 0;
+    });
+  }
+  if (overlap == 1 || overlap == 2) {
+    std::vector<std::pair<uint64_t, uint64_t>> occupied;
+    std::set<uint64_t> used;
+    std::vector<orc_match> kept;
+    for (const orc_match& x : v) {
+      if (overlap == 2 && used.count(uid[x.pattern])) continue;
+      const auto r = rust_binary_search_by(occupied.size(), [&](size_t i) { return cmp3(occupied[i].first, x.start); });
+      const size_t pos = r.second;
+      const bool prev_ok = pos == 0 || occupied[pos - 1].second <= x.start;
+      const bool next_ok = pos == occupied.size() || occupied[pos].first >= x.end;
+      if (prev_ok && next_ok) {
+        if (overlap == 2) used.insert(uid[x.pattern]);
+        occupied.insert(occupied.begin() + (std::ptrdiff_t)pos, {x.start, x.end});
+        kept.push_back(x);
+      }
+    }
+    // sort_unstable_by_key(start): equal starts (empty spans only) keep an unspecified order
+    std::stable_sort(kept.begin(), kept.end(), [](const orc_match& a, const orc_match& b) { return a.start < b.start; });
+    v.swap(kept);
+  }
+  std::copy(v.begin(), v.end(), m);
+  return v.size();
+}
 
 // Merged bitap windows (prefilter.rs:319-342) for diagnostics; -1 = full-search fallback.
 int64_t orc_prefilter_windows(void* h, const uint8_t* utf8, uint64_t len, uint32_t n_graphemes, const uint32_t* goff,

@@ -17,7 +17,9 @@ PKG_DIR = os.path.join(REPO, "fuzzy-aho-corasick-rs_amd")
 if PKG_DIR not in sys.path:
     sys.path.insert(0, PKG_DIR)
 
-from fuzzy_aho_corasick.matches import FuzzyMatch, FuzzyMatches  # noqa: E402  (host post-processing)
+# FuzzyMatch / FuzzyMatches are used only as result containers (and for the out-of-scope replace /
+# split helpers); ranking and overlap resolution come from the oracle's own orc_apply
+from fuzzy_aho_corasick.matches import FuzzyMatch, FuzzyMatches  # noqa: E402
 from fuzzy_aho_corasick.structs import (FuzzyLimits, FuzzyPenalties, Pattern, SearchOptions, f32)  # noqa: E402
 
 ORACLE_DIR = os.path.join(REPO, "oracle")
@@ -74,6 +76,9 @@ _lib.orc_search_windows.argtypes = _lib.orc_search.argtypes + [ctypes.c_uint32, 
 _lib.orc_prefilter_windows.restype = ctypes.c_int64
 _lib.orc_prefilter_windows.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, _U32P, _U32P,
                                        ctypes.c_float, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64]
+_lib.orc_apply.restype = ctypes.c_uint64
+_lib.orc_apply.argtypes = [ctypes.POINTER(orc_match), ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
+                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
 _lib.orc_bitap_ends.restype = ctypes.c_uint64
 _lib.orc_bitap_ends.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
                                 ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
@@ -224,15 +229,38 @@ class OracleEngine:
                  for (s, e, p, sim, ins, dele, sub, swp, ed) in self.raw_rows(haystack, threshold, prefilter)]
         return FuzzyMatches(haystack, inner, data)
 
+    def apply_rows(self, rows, order, overlap):
+        """FuzzyMatches::apply (matches.rs:7-149) on raw rows, by the oracle's own C++ restatement
+        (orc_apply), independent of the product's ranking code. Returns rows in the result order."""
+        n = len(rows)
+        arr = (orc_match * max(1, n))()
+        for i, (s, e, p, sim, ins, dele, sub, swp, ed) in enumerate(rows):
+            arr[i].start, arr[i].end, arr[i].pattern, arr[i].similarity = s, e, p, sim
+            arr[i].ins, arr[i].dele, arr[i].sub, arr[i].swp, arr[i].edits = ins, dele, sub, swp, ed
+        plen = (ctypes.c_uint64 * max(1, len(self.patterns_)))(*[len(p.pattern.encode("utf-8")) for p in self.patterns_])
+        # uniqueness keys: custom ids and automatic (index) ids never compare equal (matches.rs:118-122)
+        uid = (ctypes.c_uint64 * max(1, len(self.patterns_)))(
+            *[(1 << 63) | p.custom_unique_id_ if p.custom_unique_id_ is not None else i
+              for i, p in enumerate(self.patterns_)])
+        k = _lib.orc_apply(arr, n, int(order.value), int(overlap.value), plen, uid)
+        return [(a.start, a.end, a.pattern, a.similarity, a.ins, a.dele, a.sub, a.swp, a.edits) for a in arr[:k]]
+
+    def _applied(self, haystack, threshold, order, overlap, prefilter=False):
+        data = haystack.encode("utf-8")
+        rows = self.apply_rows(self.raw_rows(haystack, threshold, prefilter), order, overlap)
+        inner = [FuzzyMatch(ins, dele, sub, swp, ed, p, self.patterns_[p], s, e, sim, data[s:e].decode("utf-8"))
+                 for (s, e, p, sim, ins, dele, sub, swp, ed) in rows]
+        return FuzzyMatches(haystack, inner, data)
+
     def search(self, haystack, opts=None):
         opts = opts or SearchOptions()
-        return self.search_raw(haystack, opts.threshold_).apply(opts.order_, opts.overlap_)
+        return self._applied(haystack, opts.threshold_, opts.order_, opts.overlap_)
 
     def _segmented(self, haystack, opts):
         from fuzzy_aho_corasick.structs import Order, Overlap
         order = Order.Default if opts.order_ == Order.Unsorted else opts.order_
         overlap = Overlap.NonOverlapping if opts.overlap_ == Overlap.Keep else opts.overlap_
-        return self.search_raw(haystack, opts.threshold_).apply(order, overlap)
+        return self._applied(haystack, opts.threshold_, order, overlap)
 
     def replace(self, text, opts, callback):
         return self._segmented(text, opts).replace(callback)
@@ -262,7 +290,7 @@ class OraclePrefiltered:
 
     def search(self, haystack, opts=None):
         opts = opts or SearchOptions()
-        return self.engine.search_raw(haystack, opts.threshold_, prefilter=True).apply(opts.order_, opts.overlap_)
+        return self.engine._applied(haystack, opts.threshold_, opts.order_, opts.overlap_, prefilter=True)
 
 
 class OracleReplacer:

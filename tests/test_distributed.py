@@ -134,7 +134,8 @@ def test_shard_plan_cuts_at_context_free_boundaries(hay):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("kind,hay", [("e1", HAY_ASCII), ("e1", HAY_UNI), ("e2beam", HAY_UNI)])
+@pytest.mark.parametrize("kind,hay", [("e1", HAY_ASCII), ("e1", HAY_UNI), ("e2beam", HAY_UNI)],
+                         ids=["e1-ascii", "e1-uni", "e2beam-uni"])
 def test_sharded_oracle_equals_whole_cpu(world, kind, hay):
     """Halo-sliced shards searched as their own texts, gathered over gloo == whole search_raw."""
     _run(world, False, kind, hay)
@@ -142,7 +143,7 @@ def test_sharded_oracle_equals_whole_cpu(world, kind, hay):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,hay", [("e1", HAY_ASCII), ("e1", HAY_UNI), ("e2beam", HAY_UNI),
-                                      ("autobeam", HAY_UNI)])
+                                      ("autobeam", HAY_UNI)], ids=["e1-ascii", "e1-uni", "e2beam-uni", "autobeam-uni"])
 def test_sharded_search_gpu(kind, hay):
     """sharded_search (halo-sliced staging, device records, gather) on 2 ranks == oracle whole."""
     _run(2, True, kind, hay)

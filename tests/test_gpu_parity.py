@@ -384,13 +384,21 @@ def test_lane_serial_windows(pops, monkeypatch):
             compare(b, pats, hay, thr)
 
 
+def FuzzyMatch_sim_bits(sim):
+    import struct
+    return struct.unpack("<I", struct.pack("<f", sim))[0]
+
+
 def _keyrows(ms):
     return [(m.start, m.end, m.pattern_index, m.sim_bits()) for m in ms]
 
 
 def test_device_apply_matches_host_apply():
     """fac_matches_apply (ranking + overlap resolution on the device, matches.rs:7-149) == the
-    host FuzzyMatches.apply the translated reference tests pin, for every order x overlap."""
+    oracle's independent C++ restatement (orc_apply) and the host FuzzyMatches.apply, for every
+    order x overlap, on random cases and a dense C2 slice. After an overlap resolution the kept
+    matches are sorted by start alone (sort_unstable_by_key, ties only between empty spans), so
+    those are compared as sets."""
     from fuzzy_aho_corasick import Order, Overlap
     from fuzzy_aho_corasick import workloads
     rng = Rng(0x5151)
@@ -405,10 +413,16 @@ def test_device_apply_matches_host_apply():
     cases.append((workloads.builder_for(w), w.patterns, w.haystack.decode(), 0.6))
     for b, pats, hay, thr in cases:
         eng = b.build(pats)
+        orc = OracleEngine(b, pats)
         for order in Order:
             for overlap in Overlap:
-                raw = eng.search_raw(hay, thr)  # one raw list in, both sides see the same order
+                raw = eng.search_raw(hay, thr)  # one raw list in, every side sees the same order
+                rows_in = [(m.start, m.end, m.pattern_index, m.similarity, m.insertions, m.deletions, m.substitutions,
+                            m.swaps, m.edits) for m in raw.inner]
+                ref = [(r[0], r[1], r[2], FuzzyMatch_sim_bits(r[3])) for r in orc.apply_rows(rows_in, order, overlap)]
                 dev = eng.apply_on_device(raw, order, overlap)
+                norm = (lambda x: sorted(x)) if overlap != Overlap.Keep else (lambda x: x)  # noqa: E731
+                assert norm(_keyrows(dev)) == norm(ref), (order, overlap, hay[:80])
                 host = raw.apply(order, overlap)
                 assert _keyrows(dev) == _keyrows(host), (order, overlap, hay[:80])
                 if order != Order.Unsorted:  # the search path ranks on the device too
