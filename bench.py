@@ -116,7 +116,7 @@ def main():
     mib = args.mib if args.mib is not None else DEFAULT_MIB[args.config]
     nbytes = int(mib * (1 << 20))
     if args.config == "c4":  # C2 engine, haystack seeds 40..47
-        wl = W.config("c4", nbytes, seed=2, hay_seed=40 + (0 if args.shard else rank))
+        wl = W.config("c4", nbytes, hay_seed=40 + (0 if args.shard else rank))
     else:
         base_seed = {"c1": 1, "c2": 2, "c3": 3}[args.config]
         # weak scaling: every rank builds the same engine and owns a different haystack of equal size

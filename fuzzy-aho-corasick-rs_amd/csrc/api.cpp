@@ -680,6 +680,7 @@ int fac_stream_feed(fac_stream* stream, const uint8_t* data, uint64_t len, int32
 }
 
 uint64_t fac_stream_total(const fac_stream* stream) { return stream ? stream->s->total : 0; }
+uint64_t fac_stream_committed(const fac_stream* stream) { return stream ? fac::stream_committed(*stream->s) : 0; }
 
 void fac_stream_close(fac_stream* stream) {
   if (!stream) return;

@@ -414,8 +414,24 @@ const char* diag_env(const char* name);
 // largest grapheme count a haystack may have (u32::MAX, search.rs:198-201; lowered only by the
 // diagnostics knob FAC_GRAPHEME_LIMIT so tests can reach SearchError::HaystackTooLarge)
 uint64_t grapheme_limit();
-// bitap pre-filter: candidate windows (grapheme ranges, merged) for a staged haystack
-// stream.cpp: the WindowReader state (stream.rs:77-159) and the matches ready to hand out
+// A set of lazily grown device scratch buffers for the search launcher. The engine owns one (leased
+// by whichever call gets it first); a streaming search owns one per in-flight window, bound to the
+// worker thread that searches it (scratch_bind) so concurrent windows never hipMalloc per call.
+struct ScratchSet {
+  static constexpr int kSlots = 64;
+  std::mutex mu;
+  void* p[kSlots] = {};
+  size_t n[kSlots] = {};
+};
+void scratch_bind(ScratchSet* s);  // this thread's searches use `s` (nullptr: the engine's)
+void scratch_free(ScratchSet& s);
+
+// stream.cpp: the WindowReader state (stream.rs:77-159), the windows in flight and the matches
+// ready to hand out. Windows are cut on the host and searched by `depth` worker threads, each with
+// its own HIP stream and scratch: window k + 1's upload, segmentation and search overlap window k's
+// (double buffering); results are handed out in window order.
+struct StreamTask;
+struct StreamWorker;
 struct StreamCore {
   const Engine* e = nullptr;
   float threshold = 0.f;
@@ -426,11 +442,18 @@ struct StreamCore {
   bool done = false;
   std::vector<fac_match> ready;
   std::vector<uint8_t> ready_text;  // matched bytes of `ready`, concatenated
+  static constexpr uint32_t depth = 2;
+  StreamWorker* workers[depth] = {};
+  std::vector<StreamTask*> inflight;  // window order
+  uint64_t seq = 0;
+  int failed = 0;
+  std::string fail_msg;
 };
 
 StreamCore* stream_open(const Engine& e, float threshold, uint64_t window);
 int stream_feed(StreamCore& s, const uint8_t* data, uint64_t len, bool eof, std::string& err);
 void stream_close(StreamCore* s);
+uint64_t stream_committed(const StreamCore& s);  // stream bytes committed (every later match starts at or after)
 int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err);
 void ensure_symbols(const Engine& e, const Haystack& h);
 int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,
@@ -444,7 +467,10 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
 // force_ascii: -1 decide from the bytes (search.rs:196), 0 Unicode graphemes, 1 ASCII bytes (a
 // shard of a haystack whose global is_ascii is already known)
 int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack& h, std::string& err,
-                   int force_ascii = -1);
+                   int force_ascii = -1, hipStream_t stream = nullptr);
+// start byte of the n-th grapheme counted from the end of s[0, len) (UAX #29, the whole text's
+// segmentation; stream.rs:134-139 grapheme_indices(true).rev().nth(n - 1)); false if it has fewer
+bool nth_grapheme_from_end(const uint8_t* s, uint64_t len, uint64_t n, uint64_t& off);
 // shard planning (unicode.cpp): p is a grapheme boundary whose segmentation does not depend on
 // anything before it (previous char ASCII and not CR, char at p neither Extend, ZWJ nor SpacingMark)
 bool safe_cut(const uint8_t* s, uint64_t n, uint64_t p);

@@ -2640,7 +2640,13 @@ bool debug_poison() {
 // One pinned, device-mapped host word per host thread (kept for the thread's lifetime): kernels
 // store small results there directly, with no copy to queue behind other streams' work.
 int pinned_word(unsigned int*& host, unsigned int*& dev, std::string& err) {
-  thread_local unsigned int* h = nullptr;
+  thread_local struct Word {  // freed when the thread ends (streaming workers come and go)
+    unsigned int* p = nullptr;
+    ~Word() {
+      if (p) (void)hipHostFree(p);
+    }
+  } word;
+  unsigned int*& h = word.p;
   if (!h) {
     void* p = nullptr;
     const hipError_t e = hipHostMalloc(&p, 64, hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent);
@@ -2716,7 +2722,20 @@ struct Events {
   }
 };
 
+thread_local ScratchSet* t_scratch = nullptr;  // scratch_bind
+
 }  // namespace
+
+void scratch_bind(ScratchSet* s) { t_scratch = s; }
+
+void scratch_free(ScratchSet& s) {
+  for (int i = 0; i < ScratchSet::kSlots; ++i)
+    if (s.p[i]) {
+      (void)hipFree(s.p[i]);
+      s.p[i] = nullptr;
+      s.n[i] = 0;
+    }
+}
 
 int upload_engine(Engine& e, std::string& err) {
   HIP_TRY(hipSetDevice(e.device));
@@ -2776,16 +2795,17 @@ void free_engine_device(Engine& e) {
 }
 
 int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack& h, std::string& err,
-                   int force_ascii) {
+                   int force_ascii, hipStream_t stream) {
   h.device = e.device;
   h.len = len;
   h.ascii = force_ascii < 0 ? ascii_only(utf8, len) : force_ascii != 0;
   h.utf8.assign(utf8, utf8 + len);
   h.n = h.ascii ? len : 0;
   HIP_TRY(hipSetDevice(e.device));
-  // All uploads go through the engine's stream and are synchronized before returning, so kernels
-  // on any stream see complete data (pageable copies may otherwise still be in flight).
-  hipStream_t st = e.stream;
+  // All uploads go through one stream (the engine's, or the caller's) and are synchronized before
+  // returning, so kernels on any stream see complete data (pageable copies may otherwise still be
+  // in flight).
+  hipStream_t st = stream ? stream : e.stream;
   HIP_TRY(hipMalloc((void**)&h.d_utf8, std::max<uint64_t>(len, 16)));
   if (len) HIP_TRY(hipMemcpyAsync(h.d_utf8, utf8, len, hipMemcpyHostToDevice, st));
   if (!h.ascii) {  // UAX #29 segmentation + folding on the device (stage_kernels.hip)
@@ -2978,7 +2998,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   DevBuf d_ct[kRcLevels];  // prefix cache lookup tables
   DevBuf d_hits, d_hitp;   // per-window lookups of the main pass
   DevBuf d_seen;           // prefix cache: sampled levels' first-sighting bitmap
-  std::unique_lock<std::mutex> lease(e.scratch_mu, std::try_to_lock);
+  ScratchSet* bound = t_scratch;  // a streaming worker's own set, else the engine's
+  std::unique_lock<std::mutex> lease(bound ? bound->mu : e.scratch_mu, std::try_to_lock);
+  void** scratch_p = bound ? bound->p : e.scratch_p;
+  size_t* scratch_n = bound ? bound->n : e.scratch_n;
   if (lease.owns_lock()) {  // reuse the engine's scratch (no per-call hipMalloc of the 64 MB lists)
     std::vector<DevBuf*> bufs = {&d_segs, &d_prefix, &d_out, &d_ebuf, &d_cnt, &d_list, &d_spill,
                                  &d_rck,  &d_rcv,    &d_rcslot, &d_rcb, &d_rcrep, &d_rcs, &d_rcc, &d_rcn};
@@ -2989,7 +3012,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     bufs.push_back(&d_hitp);
     bufs.push_back(&d_seen);
     static_assert(Engine::kScratch >= 20 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
-    for (size_t i = 0; i < bufs.size(); ++i) bufs[i]->bind(&e.scratch_p[i], &e.scratch_n[i]);
+    static_assert(ScratchSet::kSlots >= Engine::kScratch, "stream scratch slots");
+    for (size_t i = 0; i < bufs.size(); ++i) bufs[i]->bind(&scratch_p[i], &scratch_n[i]);
   }
   HIP_TRY(d_segs.alloc(segs.size() * sizeof(SegDesc), stream));
   HIP_TRY(d_prefix.alloc(prefix.size() * sizeof(uint64_t), stream));

@@ -189,6 +189,22 @@ void segment_graphemes(const uint8_t* s, uint64_t n, std::vector<uint64_t>& star
 // SpacingMark (GB9, GB9a); and after an ASCII character every piece of state (ri_run, pict, gb11,
 // incb_state) depends on the character at p alone, so segmenting from p reproduces exactly the
 // boundaries the whole text has from p on.
+bool nth_grapheme_from_end(const uint8_t* s, uint64_t len, uint64_t n, uint64_t& off) {
+  if (n == 0) return false;
+  std::vector<uint64_t> st;
+  for (uint64_t span = 8 * n + 64;; span *= 2) {
+    // segment a tail that starts at a context-free cut: its boundaries are the whole text's
+    uint64_t p = span >= len ? 0 : len - span;
+    while (p > 0 && !safe_cut(s, len, p)) --p;
+    segment_graphemes(s + p, len - p, st);
+    if (st.size() >= n) {
+      off = p + st[st.size() - n];
+      return true;
+    }
+    if (p == 0) return false;
+  }
+}
+
 bool ascii_only(const uint8_t* s, uint64_t n) {
   uint64_t i = 0, acc = 0;
   for (; i + 8 <= n; i += 8) {

@@ -139,6 +139,7 @@ SIGNATURES = {
     "fac_stream_feed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int32,
                                        _P(_P(fac_match)), _u64p, _P(_P(ctypes.c_uint8)), _u64p]),
     "fac_stream_total": (ctypes.c_uint64, [ctypes.c_void_p]),
+    "fac_stream_committed": (ctypes.c_uint64, [ctypes.c_void_p]),
     "fac_stream_close": (None, [ctypes.c_void_p]),
     "fac_buffer_free": (None, [ctypes.c_void_p]),
     "fac_prefilter_windows": (ctypes.c_int64, [_engine_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_float,

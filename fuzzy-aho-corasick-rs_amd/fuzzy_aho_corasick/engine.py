@@ -255,6 +255,55 @@ class FuzzyAhoCorasick:
             if not chunk:
                 return
 
+    def search_stream_parallel(self, reader, threshold: float, threads: int, on_match) -> int:
+        """stream.rs:378-429. The device path already searches two windows at a time (one HIP
+        stream each, fac_stream); `threads` is accepted for API parity."""
+        return self.search_stream(reader, threshold, on_match)
+
+    def replace_stream(self, reader, writer, threshold: float, callback, window: int = 0) -> int:
+        """stream.rs:462-503 + ReplaceCursor::emit_window (:645-705): streaming find-and-replace.
+        Every owned match (per window: sorted().non_overlapping(), start < commit, ordered by
+        (start, end)) is replaced by `callback(m)` (a str; None keeps the matched text) unless it
+        starts inside text already written; everything else is copied through. Text before the
+        stream's commit point is written as soon as it is committed. Returns the bytes written."""
+        st = _Stream(self, threshold, window)
+        pending = bytearray()  # stream bytes [emitted, read) not yet written
+        emitted = written = 0
+
+        def out(b: bytes):
+            nonlocal written
+            if b:
+                writer.write(b)
+                written += len(b)
+
+        def emit(ms, upto):
+            nonlocal emitted, pending
+            for m in sorted(ms, key=lambda m: (m.start, m.end)):
+                if m.start < emitted:  # overlaps text an earlier window's match already wrote
+                    continue
+                out(bytes(pending[: m.start - emitted]))
+                repl = callback(m)
+                out(m.text.encode("utf-8") if repl is None else str(repl).encode("utf-8"))
+                del pending[: m.end - emitted]
+                emitted = m.end
+            if emitted < upto:  # verbatim up to the commit point
+                out(bytes(pending[: upto - emitted]))
+                del pending[: upto - emitted]
+                emitted = upto
+
+        while True:
+            chunk = reader.read(READ_CHUNK)
+            pending += chunk or b""
+            ms = st.feed(chunk or b"", eof=not chunk)
+            if not chunk:
+                emit(ms, st.total())
+                return written
+            emit(ms, max(emitted, st.committed()))
+
+    def replace_stream_parallel(self, reader, writer, threads: int, threshold: float, callback) -> int:
+        """stream.rs:533-638: same output as replace_stream (windows are pipelined on the device)."""
+        return self.replace_stream(reader, writer, threshold, callback)
+
     def apply_on_device(self, matches: FuzzyMatches, order: Order, overlap: Overlap) -> FuzzyMatches:
         """FuzzyMatches::apply of an existing match list through fac_matches_apply (same input
         order in, so Unsorted + NonOverlapping walks the same sequence as the host)."""
@@ -382,6 +431,9 @@ class _Stream:
 
     def total(self) -> int:
         return int(_native.lib.fac_stream_total(self._h))
+
+    def committed(self) -> int:
+        return int(_native.lib.fac_stream_committed(self._h))
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -548,3 +600,7 @@ class FuzzyReplacer:
 
     def replace(self, text: str, opts: SearchOptions) -> str:
         return self.engine.replace(text, opts, lambda m: self.replacements[m.pattern_index])
+
+    def replace_stream(self, reader, writer, threshold: float) -> int:
+        """replacer.rs:35-44"""
+        return self.engine.replace_stream(reader, writer, threshold, lambda m: self.replacements[m.pattern_index])

@@ -130,11 +130,11 @@ def config(name: str, nbytes: int = None, seed: int = None, hay_seed: int = None
         hay = _haystack(hs((seed or 1) + 1000), [ASCII_LOWER], pats, nbytes or (1 << 20), 0, 4096)
         return Workload("c1", pats, hay, 0, 0, False, 0.8)
     if name in ("c2", "c4"):
-        base = seed or (2 if name == "c2" else 40)  # C4: seeds 40..47 per haystack
+        base = seed or 2  # C4 runs the C2 engine on haystacks of seeds 40..47
         rng = XorShift(base).numpy()
         pats = _words(rng, [ASCII_LOWER], 1000, 4, 16, True)
         default = (1 << 30) if name == "c2" else (128 << 20)
-        hay = _haystack(hs(base + 1000), [ASCII_LOWER], pats, nbytes or default, 1, 4096)
+        hay = _haystack(hs(base + 1000 if name == "c2" else 40), [ASCII_LOWER], pats, nbytes or default, 1, 4096)
         return Workload(name, pats, hay, 1, 0, False, 0.8)
     if name == "c3":
         rng = XorShift(seed or 3).numpy()

@@ -262,7 +262,9 @@ int fac_matches_apply(const fac_engine* engine, fac_match* matches, uint64_t n, 
 
 /* Streaming search (stream.rs:77-297): feed the input in the reader's read() pieces; windows
  * of `window_bytes` (0 = the crate's 256 KiB) are cut, searched (sorted + non-overlapping) and
- * their owned matches returned with absolute byte offsets, exactly like search_stream. Each feed
+ * their owned matches returned with absolute byte offsets, exactly like search_stream. Two windows
+ * are searched at a time on two HIP streams (the next window's upload and search overlap the
+ * current one's); matches are still returned in stream order. Each feed
  * returns the matches completed so far (`*out`, free with fac_matches_free) and their matched
  * bytes concatenated in the same order (`*text`, match i has end - start bytes; free with
  * fac_buffer_free). Pass eof = 1 (data may be empty) once the input has ended. */
@@ -271,6 +273,9 @@ int fac_stream_open(const fac_engine* engine, float threshold, uint64_t window_b
 int fac_stream_feed(fac_stream* stream, const uint8_t* data, uint64_t len, int32_t eof, fac_match** out,
                     uint64_t* n_out, uint8_t** text, uint64_t* text_len);
 uint64_t fac_stream_total(const fac_stream* stream);
+/* Stream bytes committed so far: every match still to come starts at or after this offset (the
+ * streaming replace copies the text before it through). */
+uint64_t fac_stream_committed(const fac_stream* stream);
 void fac_stream_close(fac_stream* stream);
 void fac_buffer_free(void* p);
 

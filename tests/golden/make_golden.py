@@ -17,8 +17,8 @@ sys.path[:0] = [os.path.join(REPO, "fuzzy-aho-corasick-rs_amd"), os.path.join(RE
 from fuzzy_aho_corasick import workloads as W  # noqa: E402
 from oracle_harness import OracleEngine  # noqa: E402
 
-SIZES = {"c1": 16384, "c2": 16384, "c3": 8192, "c4": 16384, "c5": 65536}
-PATTERN_CAP = {"c3": 2000}  # keep the fixture small; still a deep 2K-pattern trie
+SIZES = {"c1": 16384, "c2": 16384, "c3": 32768, "c4": 16384, "c5": 65536}
+PATTERN_CAP = {}  # every config with its full pattern set (C3: all 10K patterns, beam 64)
 
 
 def main():

@@ -154,3 +154,67 @@ def test_knobs_need_diagnostics_mode():
         assert r.returncode == 0, r.stderr[-2000:]
         out[diag] = int(r.stdout.strip().splitlines()[-1])
     assert out["0"] > 0 and out["1"] == 0
+
+
+# ---- streaming replace (tests.rs:1153-1273), on the double-buffered device stream
+
+def _needle_engine():
+    return B().fuzzy(L().edits(1)).case_insensitive(True).device(0).build(["needle"])
+
+
+def _replace(eng, text, cb, window=0, parallel=False):
+    import io
+    out = io.BytesIO()
+    if parallel:
+        n = eng.replace_stream_parallel(io.BytesIO(text.encode()), out, 4, 0.8, cb)
+    else:
+        n = eng.replace_stream(io.BytesIO(text.encode()), out, 0.8, cb, window=window)
+    s = out.getvalue().decode()
+    assert n == len(out.getvalue())
+    return s
+
+
+@pytest.mark.parametrize("parallel", [False, True])
+def test_replace_stream_small_cases(parallel):  # tests.rs:1153-1183, 1240-1259
+    eng = _needle_engine()
+    x = lambda m: "X"  # noqa: E731
+    assert _replace(eng, "a needle b", x, parallel=parallel) == "a X b"
+    assert _replace(eng, "needle b", x, parallel=parallel) == "X b"
+    assert _replace(eng, "a needle", x, parallel=parallel) == "a X"
+    assert _replace(eng, "needle needle", x, parallel=parallel) == "X X"
+    assert _replace(eng, "a neeedle b", x, parallel=parallel) == "a X b"  # one insertion
+    assert _replace(eng, "nothing here", x, parallel=parallel) == "nothing here"
+    assert _replace(eng, "", x, parallel=parallel) == ""
+    assert _replace(eng, "a needle b", lambda m: None, parallel=parallel) == "a needle b"
+
+
+@pytest.mark.parametrize("window", [0, 4096, 64 << 10])
+def test_replace_stream_matches_whole_input(window):  # tests.rs:1186-1237
+    eng = _needle_engine()
+    filler = "the quick brown fox " * 50
+    text = ""
+    while len(text) < 600_000:
+        text += filler + "needle "
+    truth = eng.replace(text, O().threshold(0.8), lambda m: f"<{m.pattern_index}>")
+    got = _replace(eng, text, lambda m: f"<{m.pattern_index}>", window=window)
+    assert got == truth and "<0>" in got
+    assert _replace(eng, text, lambda m: f"<{m.pattern_index}>", parallel=True) == truth
+
+
+def test_fuzzy_replacer_replace_stream():  # tests.rs:1262-1273
+    import io
+    r = B().case_insensitive(True).fuzzy(L().edits(1)).device(0).build_replacer([("hello", "hi"), ("world", "earth")])
+    out = io.BytesIO()
+    r.replace_stream(io.BytesIO(b"hell0 w0rld!"), out, 0.8)
+    assert out.getvalue().decode() == "hi earth!"
+
+
+def test_stream_many_windows_in_order():
+    """The double-buffered stream hands windows out in stream order: tiny windows (thousands of
+    cuts, two in flight) give the same matches, in the same order, as the whole-input ranking."""
+    import io
+    eng = _needle_engine()
+    text = ("fox needle " + "x" * 40 + " nedle ") * 800
+    truth = [(m.start, m.end) for m in eng.search(text, O().threshold(0.8).sorted().non_overlapping())]
+    got = [(m.start, m.end) for m in eng.stream_matches(io.BytesIO(text.encode()), 0.8, window=512)]
+    assert got == truth and len(got) == 1600
