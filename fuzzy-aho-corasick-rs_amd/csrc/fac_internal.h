@@ -446,6 +446,7 @@ struct StreamCore {
   StreamWorker* workers[depth] = {};
   std::vector<StreamTask*> inflight;  // window order
   uint64_t seq = 0;
+  uint64_t handed = 0;  // commit point of the last window whose matches were handed out
   int failed = 0;
   std::string fail_msg;
 };
@@ -453,7 +454,7 @@ struct StreamCore {
 StreamCore* stream_open(const Engine& e, float threshold, uint64_t window);
 int stream_feed(StreamCore& s, const uint8_t* data, uint64_t len, bool eof, std::string& err);
 void stream_close(StreamCore* s);
-uint64_t stream_committed(const StreamCore& s);  // stream bytes committed (every later match starts at or after)
+uint64_t stream_committed(const StreamCore& s);  // commit point of the windows handed out so far
 int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err);
 void ensure_symbols(const Engine& e, const Haystack& h);
 int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,

@@ -115,6 +115,7 @@ int collect(StreamCore& s, bool all, std::string& err) {
       g_done_cv.wait(lk, [&] { return t->done; });
     }
     s.inflight.erase(s.inflight.begin());
+    s.handed = t->base + t->commit;
     if (t->rc && !s.failed) {
       s.failed = t->rc;
       s.fail_msg = t->err;
@@ -230,6 +231,6 @@ void stream_close(StreamCore* s) {
   delete s;
 }
 
-uint64_t stream_committed(const StreamCore& s) { return s.base; }
+uint64_t stream_committed(const StreamCore& s) { return s.handed; }
 
 }  // namespace fac

@@ -273,8 +273,8 @@ int fac_stream_open(const fac_engine* engine, float threshold, uint64_t window_b
 int fac_stream_feed(fac_stream* stream, const uint8_t* data, uint64_t len, int32_t eof, fac_match** out,
                     uint64_t* n_out, uint8_t** text, uint64_t* text_len);
 uint64_t fac_stream_total(const fac_stream* stream);
-/* Stream bytes committed so far: every match still to come starts at or after this offset (the
- * streaming replace copies the text before it through). */
+/* Commit point of the windows whose matches were handed out so far: every match still to come
+ * starts at or after this offset (the streaming replace copies the text before it through). */
 uint64_t fac_stream_committed(const fac_stream* stream);
 void fac_stream_close(fac_stream* stream);
 void fac_buffer_free(void* p);
