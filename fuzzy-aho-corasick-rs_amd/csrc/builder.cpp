@@ -348,8 +348,18 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
     const HostNode& h = e.nodes[i];
     const uint32_t deg = h.edge_end - h.edge_begin;
     if (deg > NODE_DEG_MASK) { err = "node degree too large"; return FAC_E_UNSUPPORTED; }
-    e.dnodes[i] = DevNode{h.prune_len, h.prune_lw, h.edge_begin, deg | (h.out_end != h.out_begin ? NODE_HAS_OUT : 0u),
-                          e.sb_bits[i]};
+    // edge-set flags for the substitution shortcut: an ASCII first char among the edges, two edges
+    // sharing a first char
+    uint32_t fl = 0;
+    std::vector<uint32_t> chs;
+    for (uint32_t a = h.edge_begin; a < h.edge_end; ++a) {
+      if (e.edges[a].ch < 128u) fl |= NODE_ASCII_EDGE;
+      chs.push_back(e.edges[a].ch);
+    }
+    std::sort(chs.begin(), chs.end());
+    if (std::adjacent_find(chs.begin(), chs.end()) != chs.end()) fl |= NODE_DUP_CH;
+    e.dnodes[i] = DevNode{h.prune_len, h.prune_lw, h.edge_begin,
+                          deg | fl | (h.out_end != h.out_begin ? NODE_HAS_OUT : 0u), e.sb_bits[i]};
     e.out_range[i] = uint2{h.out_begin, h.out_end};
     e.node_pidx[i] = h.pidx;
   }
@@ -373,6 +383,15 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
     }
   } else {
     default_similarity(e.sim_ascii);
+  }
+  // 128 more entries after the table: for each ASCII text char b, the largest similarity any other
+  // ASCII edge char a has to it (table[a][b], a != b): the kernels' no-substitution test
+  e.sim_ascii.resize(128 * 128 + 128, 0.0f);
+  for (uint32_t b = 0; b < 128; ++b) {
+    float m = 0.0f;
+    for (uint32_t a = 0; a < 128; ++a)
+      if (a != b) m = std::fmax(m, e.sim_ascii[a * 128 + b]);
+    e.sim_ascii[128 * 128 + b] = m;
   }
 
   // ---- 2-gram window skip (search.rs:504-521)

@@ -98,6 +98,8 @@ struct HostNode {
 
 // device node: one 32 B load gives everything a pop needs
 constexpr uint32_t NODE_HAS_OUT = 1u << 31;
+constexpr uint32_t NODE_DUP_CH = 1u << 30;     // two of the node's edges share a first char
+constexpr uint32_t NODE_ASCII_EDGE = 1u << 29; // some edge's first char is ASCII
 constexpr uint32_t NODE_DEG_MASK = (1u << 24) - 1;
 struct alignas(16) DevNode {
   float prune_len;

@@ -841,6 +841,19 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
 // not issued; a swap edge whose child's folded filter rules out text[j] has no swap target.
 __device__ __forceinline__ bool filt_has(uint32_t f, uint32_t c) { return (f >> ch_filt_bit(c)) & 1u; }
 
+// A state with P_sub > remaining pushes a substitution only if p_sub * (1 - sim) <= remaining
+// (:864-866), i.e. for a large enough similarity. With no non-ASCII similarity pairs an edge whose
+// first char differs from text[j] has similarity 0 unless both chars are ASCII (structs.rs:82-92),
+// and then at most the table's largest similarity towards text[j] (sim_ascii[16384 + c]); an edge
+// with text[j]'s first char is the exact edge unless two edges share a first char. When none of
+// these can pass, the state has no substitution at all and the O(1) expansion applies (C3: most
+// states past the first edit read a non-ASCII char or a space).
+__device__ __forceinline__ bool no_subs(const SearchParams& P, const DevNode& nd, uint32_t cur, float remaining) {
+  if (P.n_sim != 0 || (nd.degf & NODE_DUP_CH)) return false;
+  if (cur >= 128u || !(nd.degf & NODE_ASCII_EDGE)) return true;
+  return __fmul_rn(P.p_sub, __fsub_rn(1.0f, P.sim_ascii[128u * 128u + cur])) > remaining;
+}
+
 __device__ void expand_fast(const SearchParams& P, const KState& st, const DevNode& nd, const Prep& pr, uint4 aux,
                             uint64_t& msub, uint64_t& mdel, uint32_t& ex, uint32_t& xe) {
   const uint32_t deg = node_deg(nd);
@@ -875,7 +888,7 @@ __device__ void expand_fast(const SearchParams& P, const KState& st, const DevNo
   }
   if (h1 && ((uint32_t)(g1 >> 48) >> (ch_filt_bit(pr.cur_ch) & 15u) & 1u))
     xe = ((63u - ((uint32_t)(g1 >> 32) & 0xFFu)) << 26) | (uint32_t)(g1 & CHILD26_MASK);
-  msub = sub_on ? (dm & ~exbit & (is_last ? (cout | s1) : ~0ull)) : 0ull;
+  msub = (sub_on && P.p_sub <= pr.remaining) ? (dm & ~exbit & (is_last ? (cout | s1) : ~0ull)) : 0ull;  // else no_subs
   mdel = del_ok ? (dm & (is_last ? (cout | s0) : ~0ull)) : 0ull;
 }
 
@@ -1235,7 +1248,8 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     PROF_T(tb1);
     uint64_t msub = 0, mdel = 0;
     uint32_t ex = 0u, xe = 0u;
-    const bool fast = act && P.gt_fast && (!(pr.flags & PF_SUB) || P.p_sub <= pr.remaining);
+    const bool fast =
+        act && P.gt_fast && (!(pr.flags & PF_SUB) || P.p_sub <= pr.remaining || no_subs(P, nd, pr.cur_ch, pr.remaining));
     if (__ballot(act && !fast))  // per-edge path for the states similarity can prune
       expand_units<FAC_UK, MAP>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act && !fast, msub, mdel, ex, xe);
     if (fast) expand_fast(P, st, nd, pr, aux, msub, mdel, ex, xe);
@@ -1928,7 +1942,9 @@ __device__ __forceinline__ void lane_step(const SearchParams& P, uint32_t* s_q, 
   if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)st.node << 21) | pr.cur_ch, want_ex, gv)) ex = (int64_t)(gv & CHILD26_MASK);
   if (gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)st.node << 21) | pr.nch, want_x, gx)) x = (int64_t)(gx & CHILD26_MASK);
   if (ex >= 0 && !push((uint32_t)ex, jm1, st.pen, packed)) return;  // exact (:776-800)
-  if (pr.flags & PF_SUB) {  // substitutions (:803-874), edge order, the exact edge excluded
+  // substitutions (:803-874), edge order, the exact edge excluded; none when similarity must be
+  // positive and no edge can have it (no_subs)
+  if ((pr.flags & PF_SUB) && !(P.p_sub > pr.remaining && no_subs(P, nd, pr.cur_ch, pr.remaining))) {
     bool ok = true;
     for (uint32_t e0 = eb; e0 < ee && ok; e0 += 4) {
       DevEdge ed[4];
