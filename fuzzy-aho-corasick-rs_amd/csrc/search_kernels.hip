@@ -1099,7 +1099,7 @@ __device__ __forceinline__ uint32_t hist_bucket(uint64_t pops) {  // 0, 1-15, 16
 }
 #endif
 #ifdef FAC_PHASE_PROF  // diagnostics build (make prof): cycles per phase of run_window
-__device__ unsigned long long g_prof[16];
+__device__ unsigned long long g_prof[64];  // [0, 32): main passes, [32, 64): cache builds
 #define PROF_T(t) const uint64_t t = __builtin_amdgcn_s_memtime()
 #define PROF_ACC(i, t0) prof_acc[i] += __builtin_amdgcn_s_memtime() - (t0)
 #else
@@ -1117,7 +1117,7 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
                            uint64_t& cached, unsigned& err, uint32_t& head_out, uint32_t& vcount_out) {
   const uint32_t lane = lane_id();
 #ifdef FAC_PHASE_PROF
-  uint64_t prof_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t prof_acc[20] = {};  // 12: per-edge states, 13: fast states, 14: committed, 15: loaded, 16-19: Bc buckets
 #endif
   PROF_T(t_win);
   if constexpr (VCAP > 0)
@@ -1168,8 +1168,16 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
 
   while (head < tail) {
     PROF_T(t0);
-    if constexpr (VCAP > 0)  // dedup-free variants run unbeamed engines only (launch_pass fits())
+    if constexpr (VCAP > 0) {
       if (P.beam && tail - head > beam2) beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
+    } else if (P.beam && tail - head > beam2) {
+      // a beamed window in a dedup-free variant: until its pending count first passes 2·bw the
+      // beam never triggers and dedup cannot change results (a dedup-free queue is
+      // never shorter than the dedup queue at the same pop). Here it would: the window is spilled
+      // and re-run from its start (snapshot) on a dedup variant.
+      err |= ERR_QUEUE;
+      break;
+    }
     // cache build: stop before the first state that reads text past the key
     if (P.rc_mode == 2 && (q[head & (QCAP - 1)].jm & 0xFFFFu) + 1u >= P.rc_k) break;
     PROF_ACC(0, t0);
@@ -1250,6 +1258,10 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     uint32_t ex = 0u, xe = 0u;
     const bool fast =
         act && P.gt_fast && (!(pr.flags & PF_SUB) || P.p_sub <= pr.remaining || no_subs(P, nd, pr.cur_ch, pr.remaining));
+#ifdef FAC_PHASE_PROF
+    prof_acc[12] += (uint64_t)__popcll(__ballot(act && !fast));
+    prof_acc[13] += (uint64_t)__popcll(__ballot(fast));
+#endif
     if (__ballot(act && !fast))  // per-edge path for the states similarity can prune
       expand_units<FAC_UK, MAP>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act && !fast, msub, mdel, ex, xe);
     if (fast) expand_fast(P, st, nd, pr, aux, msub, mdel, ex, xe);
@@ -1400,6 +1412,9 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     PROF_ACC(6, t6);
 #ifdef FAC_PHASE_PROF
     prof_acc[8] += 1;  // batches
+    prof_acc[14] += Bc;
+    prof_acc[15] += B;
+    prof_acc[16 + (Bc <= 4 ? 0 : Bc <= 16 ? 1 : Bc <= 40 ? 2 : 3)] += 1;
 #endif
     if (any_err(err)) break;
   }
@@ -1423,7 +1438,7 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
 #ifdef FAC_PHASE_PROF
   PROF_ACC(7, t_win);
   if (lane == 0)
-    for (int i = 0; i < 12; ++i) atomicAdd(&g_prof[i], (unsigned long long)prof_acc[i]);
+    for (int i = 0; i < 20; ++i) atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + i], (unsigned long long)prof_acc[i]);
 #endif
   return tail;  // states pushed this window, the root included: the reference's queue.len()
 }
@@ -2986,6 +3001,12 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       vi = i;
   for (size_t i = 0; i < nv && vi == nv; ++i)
     if (fits(kVariants[i])) vi = i;
+  // Beamed main passes start dedup-free (no table: more windows per CU, no dedup work) and spill the
+  // windows whose pending count would pass 2·bw to the dedup variants (run_window).
+  // Not for the auto-beam count pass (exact queue.len() per window) or mappings.
+  if (P.beam && !counts && !e.has_map && fan_root + 1 <= 256 && fan_nr + 1 <= 256 && !diag_env("FAC_NO_BEAM_BAIL"))
+    for (size_t i = 0; i < nv; ++i)
+      if (kVariants[i].vcap == 0 && kVariants[i].qcap == 256) vi = i;
   if (const char* fv = diag_env("FAC_VARIANT")) {  // tuning override "vcap,qcap"
     unsigned a = 0, b = 0;
     if (std::sscanf(fv, "%u,%u", &a, &b) == 2)
@@ -3491,12 +3512,17 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
 #endif
 #ifdef FAC_PHASE_PROF
     {
-      unsigned long long pr[16];
+      unsigned long long pr[64];
       HIP_TRY(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_prof), sizeof(pr)));
-      std::fprintf(stderr, "FAC_PROF variant=%u,%u beam_select=%llu phaseA=%llu wide=%llu phaseB=%llu phaseC=%llu "
-                   "emit=%llu push=%llu window_total=%llu batches=%llu popped=%llu [B: prep=%llu units=%llu finish=%llu]\n",
-                   kVariants[vi].vcap, kVariants[vi].qcap, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7], pr[8],
-                   cnt[1], pr[9], pr[10], pr[11]);
+      for (int m = 0; m < 2; ++m) {
+        const unsigned long long* q = pr + 32 * m;
+        std::fprintf(stderr, "FAC_PROF %s variant=%u,%u beam_select=%llu phaseA=%llu wide=%llu phaseB=%llu phaseC=%llu "
+                     "emit=%llu push=%llu window_total=%llu batches=%llu [B: prep=%llu units=%llu finish=%llu] "
+                     "states: per-edge=%llu fast=%llu committed=%llu loaded=%llu Bc<=4:%llu <=16:%llu <=40:%llu >40:%llu "
+                     "main_popped=%llu\n",
+                     m ? "builds" : "main", kVariants[vi].vcap, kVariants[vi].qcap, q[0], q[1], q[2], q[3], q[4], q[5],
+                     q[6], q[7], q[8], q[9], q[10], q[11], q[12], q[13], q[14], q[15], q[16], q[17], q[18], q[19], cnt[1]);
+      }
       std::memset(pr, 0, sizeof(pr));
       HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), pr, sizeof(pr)));
     }
