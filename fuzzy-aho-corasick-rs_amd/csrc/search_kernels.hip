@@ -1066,7 +1066,12 @@ __device__ __forceinline__ void sink64(uint64_t v) {
 #endif
 
 constexpr uint32_t RC_POOL_CHUNK = 4096;  // largest pool chunk (words, 64 KiB) a building wave takes
-constexpr uint32_t RC_HDR = 4;  // snapshot header words: {head, tail, nv, pops}, {ne}, chars 0-3, chars 4-7
+// snapshot header words: {head, tail, nv, pops}, {ne, jcheck | ncheck << 16, jbeam, jp1}, chars 0-3,
+// chars 4-7; jp1 = 1 + the largest j popped in the chain, jbeam = jp1 at the chain's last beam event (0:
+// none), jcheck = min(jbeam, 1 + the largest j of the dedup entries): the entries a resumed dedup-free
+// run must still honour have j < jcheck (the others were popped after every beam: their subtrees are
+// intact); they are the first ncheck dedup entries (0: none)
+constexpr uint32_t RC_HDR = 4;
 struct RcHit {  // prefix-cache snapshot of a window (rc_lookup): pool offset and header
   uint32_t off, head, tail, nv_nel, pops;
 };
@@ -1092,6 +1097,7 @@ __device__ __forceinline__ fac_match match_record(const SearchParams& P, const S
 
 constexpr uint32_t claim_slots(uint32_t vcap) { return vcap / 2 < 512 ? 512 : vcap / 2; }  // >= ExpScratch
 
+__device__ unsigned long long g_live_dbg[8];  // diagnostics (FAC_RC_DEBUG): live-dedup checks / hits
 #ifdef FAC_WIN_HIST  // diagnostics build (make hist): windows, pops and cycles by pops per window
 __device__ unsigned long long g_hist[24];
 __device__ __forceinline__ uint32_t hist_bucket(uint64_t pops) {  // 0, 1-15, 16-63, 64-255, 256-1023, 1024+
@@ -1111,10 +1117,17 @@ __device__ unsigned long long g_prof[64];  // [0, 32): main passes, [32, 64): ca
 // batches of up to 64 (one state per lane); a batch is cut exactly where the reference's sequential
 // semantics would diverge: before the first in-batch dedup conflict, before the first pop at which
 // the beam would trigger, and before the first >64-edge node (expanded alone, edge-parallel).
-template <uint32_t VCAP, uint32_t QCAP, bool MAP>
+// LIVE (dedup-free variants of beamed engines, VCAP == 0): the resumed snapshot's live dedup entries
+// go into a read-only table (live, LIVE_CAP slots) and a popped state equal to one of them with a
+// stored penalty <= its own is skipped as the reference's visited map would (search.rs:618-622): the
+// window itself runs dedup-free, which cannot change results while no beam triggers -- except against
+// states popped before the snapshot, whose subtrees a beam may have pruned (live_dup).
+constexpr uint32_t LIVE_CAP = 256;
+template <uint32_t VCAP, uint32_t QCAP, bool MAP, bool LIVE = false>
 __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
                            uint32_t& cseq, EmitList& EL, uint64_t start, const RcHit& rc, uint64_t& popped,
-                           uint64_t& cached, unsigned& err, uint32_t& head_out, uint32_t& vcount_out) {
+                           uint64_t& cached, unsigned& err, uint32_t& head_out, uint32_t& vcount_out,
+                           KState* live = nullptr, uint32_t* jbeam_out = nullptr) {
   const uint32_t lane = lane_id();
 #ifdef FAC_PHASE_PROF
   uint64_t prof_acc[20] = {};  // 12: per-edge states, 13: fast states, 14: committed, 15: loaded, 16-19: Bc buckets
@@ -1125,6 +1138,25 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
   uint32_t vcount = 0;
   EL.n = 0;
   uint32_t head = 0, tail = 1;
+  // LIVE: the snapshot's entries a popped state may still meet have j < jlive (0: none); the table is
+  // filled on the first batch that holds such a state (live_loaded), most windows never need it
+  uint32_t jlive = 0;
+  bool live_loaded = false;
+  if constexpr (LIVE) {
+    const uint32_t nv = rc.off != EMPTY ? (rc.nv_nel & 0xFFFFu) : 0u;
+    if (nv) jlive = P.rc_pool[rc.off + 1].y;  // jcheck | ncheck << 16
+    if (P.lane_debug && lane == 0) atomicAdd(&g_live_dbg[jlive ? 4 : 5], 1ull);
+  }
+  // cache builds of beamed engines: jbeam = 1 + the largest j popped before the last beam event of the
+  // snapshot chain (0: none). Only dedup entries popped before a beam can have beam-pruned subtrees,
+  // i.e. only they matter to a resumed dedup-free run (run_window LIVE, lane_window_kernel).
+  uint32_t jp1 = 0, jbeam = 0;  // jp1: 1 + the largest j popped in the chain so far (0: none)
+  const bool track_beam = P.rc_mode == 2 && P.beam;
+  if (track_beam && rc.off != EMPTY) {
+    const uint4 h1 = P.rc_pool[rc.off + 1];
+    jbeam = h1.z;
+    jp1 = h1.w;
+  }
   if (rc.off != EMPTY) {  // prefix cache hit: resume from the snapshot of the key's representative
     const uint4* src = P.rc_pool + rc.off + RC_HDR;  // queue, dedup entries, best list (header in rc)
     head = rc.head;
@@ -1169,7 +1201,10 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
   while (head < tail) {
     PROF_T(t0);
     if constexpr (VCAP > 0) {
-      if (P.beam && tail - head > beam2) beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
+      if (P.beam && tail - head > beam2) {
+        beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
+        if (track_beam) jbeam = max(jbeam, jp1);
+      }
     } else if (P.beam && tail - head > beam2) {
       // a beamed window in a dedup-free variant: until its pending count first passes 2·bw the
       // beam never triggers and dedup cannot change results (a dedup-free queue is
@@ -1219,6 +1254,34 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
         sink(b2 + v2 + (f2 ? 1u : 0u));
       }
 #endif
+    if constexpr (LIVE) {  // read-only: the snapshot's popped states (run_window LIVE)
+      const bool chk = jlive && in_b && (st.jm & 0xFFFFu) + 1u <= (jlive & 0xFFFFu);
+      if (__ballot(chk) && !live_loaded) {  // first need: the snapshot's check entries into the table
+        const uint32_t nv = jlive >> 16, nq = rc.tail - rc.head;
+        if (nv > LIVE_CAP - LIVE_CAP / 4) {  // too many for the table: the dedup variant takes the window
+          err |= ERR_QUEUE;
+          break;
+        }
+        for (uint32_t i = lane; i < LIVE_CAP; i += 64) live[i].node = EMPTY;
+        __builtin_amdgcn_wave_barrier();
+        const uint4* src = P.rc_pool + rc.off + RC_HDR + nq;
+        for (uint32_t i = lane; i < nv; i += 64) {
+          const uint4 w = src[i];
+          uint32_t slot = vis_hash(KState{w.x, w.y, 0.f, w.w}) & (LIVE_CAP - 1);
+          while (atomicCAS(&live[slot].node, EMPTY, w.x) != EMPTY) slot = (slot + 1) & (LIVE_CAP - 1);
+          live[slot].jm = w.y;
+          live[slot].pen = __uint_as_float(w.z);
+          live[slot].packed = w.w;
+        }
+        __builtin_amdgcn_wave_barrier();
+        live_loaded = true;
+      }
+      if (chk) vis_lookup<LIVE_CAP>(live, st, found, stored_bits, vslot);
+      if (P.lane_debug && lane == 0) {
+        atomicAdd(&g_live_dbg[2], (unsigned long long)__popcll(__ballot(chk)));
+        atomicAdd(&g_live_dbg[3], (unsigned long long)__popcll(__ballot(found && __uint_as_float(stored_bits) <= st.pen)));
+      }
+    }
     const bool skip = in_b && found && __uint_as_float(stored_bits) <= st.pen;  // :620
     const bool alive =
         in_b && !skip && !(st.pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr)));  // :638-642
@@ -1231,6 +1294,7 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
       const KState s0 = q[head & (QCAP - 1)];
       head += 1;
       popped += 1;
+      if (track_beam) jp1 = max(jp1, (s0.jm & 0xFFFFu) + 1u);
       if constexpr (VCAP > 0)
         if (visited_check<VCAP>(vis, vcount, s0, P.exact_dedup != 0, err)) continue;
       const DevNode n0 = P.nodes[s0.node];
@@ -1407,6 +1471,7 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
 #endif
     __builtin_amdgcn_wave_barrier();
     tail += shfl_u32(incl, Bc - 1);
+    if (track_beam) jp1 = max(jp1, shfl_u32(wave_inclusive_max(lane < Bc ? (st.jm & 0xFFFFu) + 1u : 0u), 63));
     head += Bc;
     popped += Bc;
     PROF_ACC(6, t6);
@@ -1421,6 +1486,10 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
 
   head_out = head;
   vcount_out = vcount;
+  if (jbeam_out) {
+    jbeam_out[0] = jbeam;
+    jbeam_out[1] = jp1;
+  }
   // flush this window's best map (search.rs:1111-1118)
   wave_mem_fence();
   // a window that overflowed the frontier is spilled whole (re-run on a larger variant): no flush;
@@ -1864,10 +1933,42 @@ __device__ __forceinline__ void lane_unpack(uint32_t w, uint32_t& jm, uint32_t& 
   jm = (w & 0xFFu) | (((w >> 8) & 0xFFu) << 16);
   pk = ((w >> 16) & 0xFu) | (((w >> 20) & 0xFu) << 8) | (((w >> 24) & 0xFu) << 16) | ((w >> 28) << 24);
 }
+// Live dedup entries of the snapshot a beamed window resumed from (lv_n entries at pool word lv_off,
+// the largest j below jlive): the window runs dedup-free, which cannot change results while no beam
+// triggers -- except against the states popped before the snapshot, whose subtrees a beam may have
+// pruned there. A popped state equal to such an entry with a stored penalty <= its own is skipped
+// exactly as the reference's visited map would (search.rs:618-622); the entries are not updated (a
+// later duplicate of a state expanded here only mirrors descendants that are all explored).
+struct LiveDedup {
+  uint32_t off, n, jlive;
+};
+__device__ __forceinline__ bool live_dup(const SearchParams& P, const LiveDedup& L, const KState& st) {
+  if (L.n == 0 || (st.jm & 0xFFFFu) + 1u > L.jlive) return false;
+  bool hit = false;
+  for (uint32_t i = 0; i < L.n; i += 4) {  // four entries in flight (the checks are rare: C3 ~0.2 % of pops)
+    uint4 e[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) e[u] = i + u < L.n ? P.rc_pool[L.off + i + u] : make_uint4(EMPTY, 0u, 0u, 0u);
+    bool done = false;
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+      if (!done && e[u].x == st.node && e[u].y == st.jm && e[u].w == st.packed) {
+        hit = __uint_as_float(e[u].z) <= st.pen;
+        done = true;
+      }
+    if (done) break;
+  }
+  if (P.lane_debug) {
+    atomicAdd(&g_live_dbg[0], 1ull);
+    if (hit) atomicAdd(&g_live_dbg[1], 1ull);
+  }
+  return hit;
+}
+
 template <uint32_t QL, uint32_t ELN>
 __device__ __forceinline__ void lane_step(const SearchParams& P, uint32_t* s_q, uint4* s_e, const SegDesc& S, uint64_t start,
-                                          uint32_t& status, uint32_t& head, uint32_t& tail, uint32_t& nel, uint32_t& pops,
-                                          unsigned& err) {
+                                          const LiveDedup& lv, uint32_t& status, uint32_t& head, uint32_t& tail,
+                                          uint32_t& nel, uint32_t& pops, unsigned& err) {
   const uint32_t lane = lane_id();
   const bool fast = P.mef != 255u;
   if (head == tail) {
@@ -1884,6 +1985,7 @@ __device__ __forceinline__ void lane_step(const SearchParams& P, uint32_t* s_q, 
   ++head;
   ++pops;
   const KState st{s_q[slot], jm0, __uint_as_float(s_q[QL * 64 + slot]), pk0};
+  if (live_dup(P, lv, st)) return;  // :618-622 against the snapshot's popped states
   // the state's reads go out together: node record, char filters, text at j and j + 1
   const DevNode nd = P.nodes[st.node];
   const uint4 aux = P.aux[st.node];
@@ -2037,6 +2139,7 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
   uint64_t cur = 0, ce = 0;   // wave-uniform: scan position and end of the current chunk
   bool chunks_done = false;   // wave-uniform
   uint32_t status = 0, head = 0, tail = 0, nel = 0, pops = 0, snap_pops = 0;
+  LiveDedup lv{0u, 0u, 0u};
   uint64_t vid = 0, start = 0;
   SegDesc S{};
   unsigned err = 0;
@@ -2106,6 +2209,9 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
         s_q[2 * QL * 64 + i * 64 + lane] = w;
       }
       for (uint32_t i = 0; i < nel; ++i) s_e[i * 64 + lane] = src[nq + nv + i];
+      // beamed engines: the snapshot's popped states still dedup (live_dup); a long list goes back
+      const uint32_t jc = P.beam && nv ? P.rc_pool[h.x + 1].y : 0u;  // jcheck | ncheck << 16
+      lv = LiveDedup{h.x + RC_HDR + nq, jc >> 16, jc & 0xFFFFu};
       head = 0;
       tail = nq;
       pops = 0;
@@ -2114,7 +2220,7 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
       ++started;
     }
     ++trips;
-    if (status == LANE_RUN) lane_step<QL, ELN>(P, s_q, s_e, S, start, status, head, tail, nel, pops, err);
+    if (status == LANE_RUN) lane_step<QL, ELN>(P, s_q, s_e, S, start, lv, status, head, tail, nel, pops, err);
     const bool fin = status == LANE_OK, bail = status == LANE_BAIL;
     if (__ballot(fin || bail)) {  // finished windows write their records (one output atomic per wave)
       const uint32_t ne = fin ? nel : 0u;
@@ -2158,9 +2264,10 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
 
 // LK: the window prologue looks snapshots up itself (cache builds); otherwise a main pass with the
 // prefix cache reads the hits rc_lookup_kernel stored.
-template <uint32_t VCAP, uint32_t QCAP, bool MAP, bool LK>
+template <uint32_t VCAP, uint32_t QCAP, bool MAP, bool LK, bool LIVE = false>
 __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   __shared__ KState s_vis[VCAP ? VCAP : 1];
+  __shared__ KState s_live[LIVE ? LIVE_CAP : 1];
   __shared__ KState s_q[QCAP];
   __shared__ __attribute__((aligned(16))) uint32_t s_claim[claim_slots(VCAP)];
   const uint32_t lane = lane_id();
@@ -2253,14 +2360,15 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         const uint64_t st = shfl_u64(start, l);
         const SegDesc S = P.segs[seg];
         const uint64_t popped0 = popped;
-        uint32_t qhead = 0, vcnt = 0;
+        uint32_t qhead = 0, vcnt = 0, jbeam[2] = {0u, 0u};
         const RcHit rc{shfl_u32(hit.off, l), shfl_u32(hit.head, l), shfl_u32(hit.tail, l), shfl_u32(hit.nv_nel, l),
                        shfl_u32(hit.pops, l)};
 #ifdef FAC_WIN_HIST
         const uint64_t t_w0 = __builtin_amdgcn_s_memtime();
 #endif
         const uint32_t qlen =
-            run_window<VCAP, QCAP, MAP>(P, S, s_vis, s_q, s_claim, cseq, EL, st, rc, popped, cached, err, qhead, vcnt);
+            run_window<VCAP, QCAP, MAP, LIVE>(P, S, s_vis, s_q, s_claim, cseq, EL, st, rc, popped, cached, err, qhead,
+                                              vcnt, s_live, jbeam);
 #ifdef FAC_WIN_HIST
         if (lane == 0 && P.rc_mode != 2) {
           const uint32_t b = hist_bucket(popped - popped0);
@@ -2279,9 +2387,15 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           for (uint32_t i = lane; i < nq; i += 64) jmin = min(jmin, s_q[(qhead + i) & (QCAP - 1)].jm & 0xFFFFu);
           jmin = wave_min_u32(jmin);
           auto live = [&](const KState& k) { return k.node != EMPTY && (k.jm & 0xFFFFu) >= jmin; };
-          uint32_t nv = 0;
+          uint32_t nv = 0, jlive = 0;  // 1 + the largest j among the live entries (0: none)
           if constexpr (VCAP > 0)
-            for (uint32_t b = 0; b < VCAP; b += 64) nv += (uint32_t)__popcll(__ballot(live(s_vis[b + lane])));
+            for (uint32_t b = 0; b < VCAP; b += 64) {
+              const KState k = s_vis[b + lane];
+              nv += (uint32_t)__popcll(__ballot(live(k)));
+              jlive = max(jlive, live(k) ? (k.jm & 0xFFFFu) + 1u : 0u);
+            }
+          jlive = wave_inclusive_max(jlive);
+          jlive = shfl_u32(jlive, 63);
           bool bad = (wave_or(err) & (ERR_QUEUE | ERR_VISITED | ERR_EMIT)) != 0 || EL.n > P.rc_emax || nv > P.rc_vmax;
           const uint32_t words = RC_HDR + nq + nv + EL.n;
           // the wave carves snapshots out of its own pool chunk: one pool atomic per chunk, not per
@@ -2304,22 +2418,29 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
             const KState k = s_q[(qhead + i) & (QCAP - 1)];
             dst[i] = make_uint4(k.node, k.jm, __float_as_uint(k.pen), k.packed);
           }
-          if constexpr (VCAP > 0) {  // compacted in slot order
+          // compacted in slot order, the entries a resumed dedup-free run must still honour (j < jcheck)
+          // first: ncheck of them
+          const uint32_t jcheck = min(jlive, jbeam[0]);
+          uint32_t ncheck = 0;
+          if constexpr (VCAP > 0) {
             uint32_t at0 = 0;
-            for (uint32_t b = 0; b < VCAP && !bad; b += 64) {
-              const KState k = s_vis[b + lane];
-              const bool occ = live(k);
-              const uint64_t m = __ballot(occ);
-              if (occ) dst[nq + at0 + prefix_below(m)] = make_uint4(k.node, k.jm, __float_as_uint(k.pen), k.packed);
-              at0 += (uint32_t)__popcll(m);
-            }
+            for (uint32_t pass = 0; pass < 2; ++pass)
+              for (uint32_t b = 0; b < VCAP && !bad; b += 64) {
+                const KState k = s_vis[b + lane];
+                const bool occ = live(k) && (((k.jm & 0xFFFFu) + 1u <= jcheck) == (pass == 0));
+                const uint64_t m = __ballot(occ);
+                if (occ) dst[nq + at0 + prefix_below(m)] = make_uint4(k.node, k.jm, __float_as_uint(k.pen), k.packed);
+                at0 += (uint32_t)__popcll(m);
+                if (pass == 0) ncheck = at0;
+              }
           }
           for (uint32_t i = lane; i < EL.n && !bad; i += 64) dst[nq + nv + i] = EL.buf[i];
           if (lane == 0) {
             if (!bad) {
               // pops: those of the parent snapshot this build resumed from, plus its own
               P.rc_pool[off] = make_uint4(qhead, qlen, nv, (uint32_t)(popped - popped0) + rc.pops);
-              P.rc_pool[off + 1] = make_uint4(EL.n, 0u, 0u, 0u);
+              // jcheck: dedup entries a resumed dedup-free run must still honour (j + 1 <= jcheck)
+              P.rc_pool[off + 1] = make_uint4(EL.n, ncheck ? (jcheck | (ncheck << 16)) : 0u, jbeam[0], jbeam[1]);
               P.rc_pool[off + 2] = kch.a;
               P.rc_pool[off + 3] = kch.b;
             }
@@ -2373,6 +2494,15 @@ void bfs_window_kernel(SearchParams P) {
 template <uint32_t QCAP, bool MAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(QCAP <= 512 ? 4 : 1))) void bfs_window_kernel_nd(SearchParams P) {
   bfs_window_body<0, QCAP, MAP, false>(P);
+}
+// dedup-free first pass of a beamed engine (launch_pass): windows that would beam are spilled, the
+// resumed snapshots' popped states still dedup (run_window LIVE)
+#ifndef FAC_LIVE_WAVES  // waves/SIMD bfs_window_kernel_live is compiled for (VGPR budget)
+#define FAC_LIVE_WAVES 4
+#endif
+template <uint32_t QCAP>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAC_LIVE_WAVES))) void bfs_window_kernel_live(SearchParams P) {
+  bfs_window_body<0, QCAP, false, false, true>(P);
 }
 // prefix-cache build (P.rc_mode == 2): one representative window per key, popped up to the first
 // state past the key; its own symbol so profiles separate it from the search launches
@@ -2610,6 +2740,11 @@ uint32_t lds_pad() {
 
 template <uint32_t Q>
 void launch_nd(uint32_t grid, hipStream_t s, const SearchParams& P) {
+  if constexpr (Q == 256)
+    if (P.beam && !P.has_map) {
+      hipLaunchKernelGGL((bfs_window_kernel_live<Q>), dim3(grid), dim3(64), lds_pad(), s, P);
+      return;
+    }
   if (P.has_map) hipLaunchKernelGGL((bfs_window_kernel_nd<Q, true>), dim3(grid), dim3(64), lds_pad(), s, P);
   else hipLaunchKernelGGL((bfs_window_kernel_nd<Q, false>), dim3(grid), dim3(64), lds_pad(), s, P);
 }
@@ -3497,8 +3632,16 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     cached_pops += cnt[4];
     lane_windows += cnt[8];
     if (diag_env("FAC_RC_DEBUG") && P.rc_mode == 1)
+    {
       std::fprintf(stderr, "FAC_RC launch windows=%llu resumed=%llu lane_flushed=%llu lane_searched=%llu popped=%llu\n",
                    (unsigned long long)pass_windows, cnt[5], cnt[6], cnt[8], cnt[1]);
+      unsigned long long d[8];
+      HIP_TRY(hipMemcpyFromSymbol(d, HIP_SYMBOL(g_live_dbg), sizeof(d)));
+      std::fprintf(stderr, "FAC_LIVE lane checks=%llu hits=%llu | wave checks=%llu hits=%llu windows with/without live entries=%llu/%llu\n",
+                   d[0], d[1], d[2], d[3], d[4], d[5]);
+      std::memset(d, 0, sizeof(d));
+      HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_live_dbg), d, sizeof(d)));
+    }
 #ifdef FAC_WIN_HIST
     {
       unsigned long long h[24];

@@ -1,16 +1,32 @@
 """One C3 step's kernels on their queues (start/end/duration ms from the step's first kernel), from a
-rocprofv3 --kernel-trace --output-format csv run: python profiles/step_timeline.py run_kernel_trace.csv"""
-import csv,re,sys
-rows=list(csv.DictReader(open(sys.argv[1])))
-rows.sort(key=lambda r:int(r['Start_Timestamp']))
-names=[r['Kernel_Name'] for r in rows]
-idx=[i for i,n in enumerate(names) if 'bfs_window_kernel' in n]
-seg=rows[idx[-2]+1:idx[-1]+1]
-t0=int(seg[0]['Start_Timestamp'])
+rocprofv3 --kernel-trace --output-format csv run: python profiles/step_timeline.py run_kernel_trace.csv
+A step starts at a level-1 count (rc_count_kernel) that follows a search kernel; the last complete
+step is printed."""
+import csv
+import re
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r['Start_Timestamp']))
+names = [r['Kernel_Name'] for r in rows]
+def prev_kernel(i):  # the last kernel before i that is not a runtime fill / copy
+    for j in range(i - 1, -1, -1):
+        if '__amd_rocclr' not in names[j]:
+            return names[j]
+    return ''
+
+
+starts = [i for i, n in enumerate(names) if 'rc_count_kernel' in n and 'window_kernel' in prev_kernel(i)]
+a, b = (starts[-2], starts[-1]) if len(starts) >= 2 else (starts[-1], len(rows))
+seg = rows[a:b]
+t0 = int(seg[0]['Start_Timestamp'])
 for r in seg:
-    n=r['Kernel_Name'].replace('fac::(anonymous namespace)::','').replace('void ','')
-    n=re.sub(r'\(.*','',n)[:40]
-    if 'copy' in n: continue
-    s=(int(r['Start_Timestamp'])-t0)/1e6; e=(int(r['End_Timestamp'])-t0)/1e6
-    if 'fill' in n and e-s<0.1: continue
-    print(f"{n:40s} q{r['Queue_Id'][-1]} {s:8.2f} {e:8.2f} {e-s:7.2f}")
+    n = r['Kernel_Name'].replace('fac::(anonymous namespace)::', '').replace('void ', '')
+    n = re.sub(r'\(.*', '', n)[:40]
+    if 'copy' in n:
+        continue
+    s = (int(r['Start_Timestamp']) - t0) / 1e6
+    e = (int(r['End_Timestamp']) - t0) / 1e6
+    if 'fill' in n and e - s < 0.1:
+        continue
+    print(f"{n:40s} q{r['Queue_Id'][-1]} {s:8.2f} {e:8.2f} {e - s:7.2f}")
