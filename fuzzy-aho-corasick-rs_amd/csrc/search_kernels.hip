@@ -1124,7 +1124,7 @@ __device__ unsigned long long g_prof[64];  // [0, 32): main passes, [32, 64): ca
 // states popped before the snapshot, whose subtrees a beam may have pruned (live_dup).
 constexpr uint32_t LIVE_CAP = 256;
 template <uint32_t VCAP, uint32_t QCAP, bool MAP, bool LIVE = false>
-__device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
+__device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
                            uint32_t& cseq, EmitList& EL, uint64_t start, const RcHit& rc, uint64_t& popped,
                            uint64_t& cached, unsigned& err, uint32_t& head_out, uint32_t& vcount_out,
                            KState* live = nullptr, uint32_t* jbeam_out = nullptr) {
@@ -1150,7 +1150,9 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
   // cache builds of beamed engines: jbeam = 1 + the largest j popped before the last beam event of the
   // snapshot chain (0: none). Only dedup entries popped before a beam can have beam-pruned subtrees,
   // i.e. only they matter to a resumed dedup-free run (run_window LIVE, lane_window_kernel).
-  uint32_t jp1 = 0, jbeam = 0;  // jp1: 1 + the largest j popped in the chain so far (0: none)
+  // jp1: 1 + the largest j popped in the chain so far (0: none), kept per lane (the lanes' committed
+  // states) and reduced over the wave only at beam events and at the end
+  uint32_t jp1 = 0, jbeam = 0;
   const bool track_beam = P.rc_mode == 2 && P.beam;
   if (track_beam && rc.off != EMPTY) {
     const uint4 h1 = P.rc_pool[rc.off + 1];
@@ -1203,7 +1205,7 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
     if constexpr (VCAP > 0) {
       if (P.beam && tail - head > beam2) {
         beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
-        if (track_beam) jbeam = max(jbeam, jp1);
+        if (track_beam) jbeam = max(jbeam, shfl_u32(wave_inclusive_max(jp1), 63));
       }
     } else if (P.beam && tail - head > beam2) {
       // a beamed window in a dedup-free variant: until its pending count first passes 2·bw the
@@ -1471,7 +1473,7 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
 #endif
     __builtin_amdgcn_wave_barrier();
     tail += shfl_u32(incl, Bc - 1);
-    if (track_beam) jp1 = max(jp1, shfl_u32(wave_inclusive_max(lane < Bc ? (st.jm & 0xFFFFu) + 1u : 0u), 63));
+    if (track_beam && lane < Bc) jp1 = max(jp1, (st.jm & 0xFFFFu) + 1u);
     head += Bc;
     popped += Bc;
     PROF_ACC(6, t6);
@@ -1488,7 +1490,7 @@ __device__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* 
   vcount_out = vcount;
   if (jbeam_out) {
     jbeam_out[0] = jbeam;
-    jbeam_out[1] = jp1;
+    jbeam_out[1] = track_beam ? shfl_u32(wave_inclusive_max(jp1), 63) : 0u;
   }
   // flush this window's best map (search.rs:1111-1118)
   wave_mem_fence();
@@ -2050,6 +2052,46 @@ __device__ __forceinline__ void lane_step(const SearchParams& P, uint32_t* s_q, 
   };
   const uint32_t eb = nd.edge_begin, ee = node_end(nd);
   const uint32_t j1 = j_rel + 1u, jm1 = j1 | (j1 << 16);
+  // O(1) expansion (expand_fast: the wave kernel's decisions for a state whose similarity cannot drop
+  // a substitution): the substitution / deletion sets come as edge masks, so only their set bits are
+  // walked -- at the last edit the dead-end filters leave a few of a node's edges
+  if (P.gt_fast && node_deg(nd) <= 64u &&
+      (!(pr.flags & PF_SUB) || P.p_sub <= pr.remaining || no_subs(P, nd, pr.cur_ch, pr.remaining))) {
+    uint64_t msub = 0, mdel = 0;
+    uint32_t ex = 0u, xe = 0u;
+    expand_fast(P, st, nd, pr, aux, msub, mdel, ex, xe);
+    if (ex) {  // exact (:776-800); the exact edge leaves the substitution set
+      msub &= ~(1ull << (63u - (ex >> 26)));
+      if (!push(ex & CHILD26_MASK, jm1, st.pen, packed)) return;
+    }
+    while (msub) {  // substitutions (:803-874), edge order
+      const uint32_t e = (uint32_t)__ffsll((unsigned long long)msub) - 1u;
+      msub &= msub - 1;
+      const DevEdge ed = P.edges[eb + e];
+      const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, similarity(P, ed.ch, pr.cur_ch)));
+      if (!push(ed.next & EDGE_NEXT_MASK, jm1, __fadd_rn(st.pen, penalty), packed + 0x10000u)) return;
+    }
+    if (xe) {  // swap (:935-989): goto(goto(node, text[j+1]), text[j])
+      uint64_t g2 = 0;
+      bool ok = gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)(xe & CHILD26_MASK) << 21) | pr.cur_ch, true, g2);
+      if (ok && !fast) {  // within_limits_swap_ahead with node2's limits (:962-967)
+        const Lim m = pick_limits(P, node_limits(P, (uint32_t)(g2 & CHILD26_MASK)));
+        ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.swp, packed >> 24)) : false;
+      }
+      if (ok) {
+        const uint32_t j2 = j_rel + 2u;
+        if (!push((uint32_t)(g2 & CHILD26_MASK), j2 | (j2 << 16), __fadd_rn(st.pen, P.p_swp), packed + 0x1000000u)) return;
+      }
+    }
+    if ((pr.flags & PF_INS) && !push(st.node, j1 | (me_rel << 16), __fadd_rn(st.pen, P.p_ins), packed + 1u)) return;
+    const float npen = __fadd_rn(st.pen, P.p_del);
+    while (mdel) {  // deletions (:1035-1089), edge order
+      const uint32_t e = (uint32_t)__ffsll((unsigned long long)mdel) - 1u;
+      mdel &= mdel - 1;
+      if (!push(P.edges[eb + e].next & EDGE_NEXT_MASK, st.jm, npen, packed + 0x100u)) return;
+    }
+    return;
+  }
   // exact and swap successors through the goto table (first edge with the char, structs.rs:512-519);
   // a clear char-filter bit proves the lookup would miss
   int64_t ex = -1, x = -1;

@@ -384,6 +384,36 @@ def test_lane_serial_windows(pops, monkeypatch):
             compare(b, pats, hay, thr)
 
 
+@pytest.mark.parametrize("levels", ["5,6", "6"])
+def test_beamed_dedup_free_first_pass(levels, monkeypatch):
+    """Beamed main passes run dedup-free (bfs_window_kernel_live, lane_window_kernel) and spill the
+    windows that would beam; the snapshots' dedup entries popped before a beam still skip their
+    duplicates (jcheck). Records == the exact dedup variant alone, on a C3-shaped slice with sampled
+    levels, and == the oracle on random beamed cases with the cache forced on."""
+    from fuzzy_aho_corasick import workloads
+    w = workloads.config("c3", 4 << 20, 3)
+    staged = workloads.builder_for(w).build(w.patterns).stage(w.haystack)
+    monkeypatch.setenv("FAC_RC_MIN2", "1")
+    monkeypatch.setenv("FAC_RC_LEVELS", levels)
+    fast, _ = staged.search_windows_records(w.threshold)
+    monkeypatch.setenv("FAC_NO_BEAM_BAIL", "1")
+    monkeypatch.setenv("FAC_NO_LANE", "1")
+    exact, _ = staged.search_windows_records(w.threshold)
+    assert len(fast) > 0 and sorted(fast.tolist()) == sorted(exact.tolist())
+    monkeypatch.delenv("FAC_NO_BEAM_BAIL")
+    monkeypatch.delenv("FAC_NO_LANE")
+    for k, v in (("FAC_RC_MIN", "1"), ("FAC_RC_K", "2"), ("FAC_RC_K2", "4"), ("FAC_RC_STRIDE2", "1"),
+                 ("FAC_RC_T2", "1")):
+        monkeypatch.setenv(k, v)
+    rng = Rng(0xbea3 ^ len(levels))
+    n = 0
+    while n < 60:
+        b, pats, hay, thr = random_case(rng, ASCII_VOCAB + UNI_VOCAB, ASCII_FILLER + UNI_FILLER)
+        if b._beam_width:
+            compare(b, pats, hay, thr)
+            n += 1
+
+
 def FuzzyMatch_sim_bits(sim):
     import struct
     return struct.unpack("<I", struct.pack("<f", sim))[0]
