@@ -2711,6 +2711,182 @@ __global__ __launch_bounds__(256) void bitap_kernel(BitapParams B) {
   }
 }
 
+// ---- Pigeonhole q-gram filter in front of the bitap scan (exact) ----
+// A pattern of m symbols within k Levenshtein edits of a text window keeps at least one of k + 1
+// disjoint pieces of itself untouched, i.e. that piece occurs verbatim in the window. Each piece
+// contributes its first q symbols (q = min(4, shortest piece), >= 3) as a gram; qgram_scan_kernel
+// looks every text position's 3- and 4-gram up in a small cache-resident table and lists the
+// (position, pattern, piece offset) candidates. qgram_verify_kernel runs the pattern's own bitap
+// recurrence (prefilter.rs:410-435) over the only ends the candidate allows -- piece at text t,
+// pattern offset o: end in [t + m - o - k, t + m - o + k] -- starting m + k symbols early, where the
+// automaton state no longer depends on where the scan began (bitap_kernel's warm-up), and sets the
+// same coverage bits as bitap_kernel. Every hit of every gram-eligible pattern is thus found (and no
+// other: the recurrence is exact), so the merged windows equal the full scan's.
+struct QgramParams {
+  const uint8_t* ids;
+  uint64_t n;
+  const uint2* tab;        // open addressing: {gram key, first entry << 8 | entries} (0: empty slot)
+  uint32_t tab_mask;
+  const uint32_t* ent;     // entries: pattern << 8 | piece offset
+  uint32_t use3, use4;     // gram lengths in use
+  unsigned long long* cand;  // candidates: text position << 24 | entry index
+  unsigned long long* n_cand;
+  uint64_t cap;
+  const uint64_t* pmask;   // per pattern: [rows] symbol masks (bit j = the pattern's j-th symbol)
+  const uint32_t* pm;      // per pattern: m | k << 8
+  uint32_t rows;
+  uint32_t* cover;
+};
+__host__ __device__ inline uint32_t qgram_key(uint32_t a, uint32_t b, uint32_t c, uint32_t d, bool q4) {
+  return q4 ? (a | (b << 8) | (c << 16) | (d << 24)) : (a | (b << 8) | (c << 16) | 0xFF000000u);
+}
+__host__ __device__ inline uint32_t qgram_hash(uint32_t h) {  // murmur3 finalizer: every key bit reaches the low bits
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
+
+__device__ __forceinline__ uint32_t qgram_find(const QgramParams& Q, uint32_t key) {  // 0: none
+  uint32_t s = qgram_hash(key) & Q.tab_mask;
+  for (;;) {
+    const uint2 e = Q.tab[s];
+    if (e.y == 0u) return 0u;
+    if (e.x == key) return e.y;
+    s = (s + 1) & Q.tab_mask;
+  }
+}
+
+// Candidates collect in a per-wave LDS buffer and go out 512 at a time (one list atomic per flush: a
+// same-address atomic per wave turn serialised the scan at one L2 channel, 175 ms per GiB)
+constexpr uint32_t QG_BUF = 512;
+// A 64 Kbit LDS bitmap of the grams' hashes (bit = hash >> 16) screens every position first: only
+// the ~3 % that pass (C5) probe the table in global memory.
+__global__ __launch_bounds__(256) void qgram_scan_kernel(QgramParams Q) {
+  __shared__ unsigned long long s_buf[4][QG_BUF];
+  __shared__ uint32_t s_bits[2048];
+  for (uint32_t x = threadIdx.x; x < 2048; x += blockDim.x) s_bits[x] = 0u;
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x <= Q.tab_mask; x += blockDim.x) {
+    const uint2 e = Q.tab[x];
+    if (e.y) {
+      const uint32_t b = qgram_hash(e.x) >> 16;
+      atomicOr(&s_bits[b >> 5], 1u << (b & 31u));
+    }
+  }
+  __syncthreads();
+  auto maybe = [&](uint32_t key) { const uint32_t b = qgram_hash(key) >> 16; return (s_bits[b >> 5] >> (b & 31u)) & 1u; };
+  unsigned long long* buf = s_buf[threadIdx.x / 64];
+  uint32_t nb = 0;  // wave-uniform
+  auto flush = [&]() {
+    unsigned long long b0 = 0;
+    if (lane_id() == 0) b0 = atomicAdd(Q.n_cand, (unsigned long long)nb);
+    b0 = shfl_u64(b0, 0);
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t x = lane_id(); x < nb; x += 64)
+      if (b0 + x < Q.cap) Q.cand[b0 + x] = buf[x];
+    __builtin_amdgcn_wave_barrier();
+    nb = 0;
+  };
+  // a thread takes 4 consecutive positions from two aligned words of symbols (the ids buffer is
+  // padded past n; positions whose gram would cross n are not looked up)
+  const uint32_t* ids32 = reinterpret_cast<const uint32_t*>(Q.ids);
+  const uint64_t nq = (Q.n + 3) / 4;  // position quads
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t base0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t g0 = base0 - threadIdx.x % 64; g0 < nq; g0 += stride) {  // whole waves iterate together
+    const uint64_t g = g0 + (threadIdx.x % 64);
+    uint32_t h[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // [2 j]: 4-gram at 4 g + j, [2 j + 1]: 3-gram
+    if (g < nq) {
+      const uint64_t w = ((uint64_t)ids32[g + 1] << 32) | ids32[g];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint64_t i = 4 * g + j;
+        const uint32_t a = (uint32_t)(w >> (8 * j)) & 0xFFu, b = (uint32_t)(w >> (8 * j + 8)) & 0xFFu;
+        const uint32_t c = (uint32_t)(w >> (8 * j + 16)) & 0xFFu, d = (uint32_t)(w >> (8 * j + 24)) & 0xFFu;
+        const uint32_t k4 = qgram_key(a, b, c, d, true), k3 = qgram_key(a, b, c, 0u, false);
+        if (Q.use4 && i + 4 <= Q.n && maybe(k4)) h[2 * j] = qgram_find(Q, k4);
+        if (Q.use3 && i + 3 <= Q.n && maybe(k3)) h[2 * j + 1] = qgram_find(Q, k3);
+      }
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < 8; ++x) cnt += h[x] & 0xFFu;
+    if (!__ballot(cnt)) continue;
+    const uint32_t incl = wave_inclusive_sum(cnt), tot = shfl_u32(incl, 63);
+    unsigned long long* dst;
+    uint64_t at;
+    if (tot > QG_BUF) {  // grams shared by many patterns: straight to the list
+      unsigned long long b0 = 0;
+      if (lane_id() == 63) b0 = atomicAdd(Q.n_cand, (unsigned long long)tot);
+      dst = Q.cand;
+      at = shfl_u64(b0, 63) + (incl - cnt);
+    } else {
+      if (nb + tot > QG_BUF) flush();
+      dst = buf;
+      at = nb + incl - cnt;
+      nb += tot;
+    }
+#pragma unroll
+    for (uint32_t x = 0; x < 8; ++x)
+      for (uint32_t y = 0; y < (h[x] & 0xFFu); ++y, ++at)
+        if (dst != Q.cand || at < Q.cap) dst[at] = ((4 * g + x / 2) << 24) | ((h[x] >> 8) + y);
+  }
+  if (nb) flush();
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(256) void qgram_verify_kernel(QgramParams Q, uint64_t n_cand) {
+  const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n_cand) return;
+  const unsigned long long cd = Q.cand[x];
+  const uint64_t t = cd >> 24;
+  const uint32_t e = Q.ent[cd & 0xFFFFFFu], p = e >> 8, o = e & 0xFFu;
+  const uint32_t mk = Q.pm[p], m = mk & 0xFFu, k = mk >> 8;
+  // ends the candidate allows, 1-based: [t + m - o - k, t + m - o + k], clipped to the text
+  const int64_t lo = (int64_t)t + m - o - k, hi = (int64_t)t + m - o + k;
+  const uint64_t e_min = (uint64_t)max<int64_t>(1, lo);
+  const uint64_t e_max = (uint64_t)min<int64_t>((int64_t)Q.n, hi);
+  if (e_min > e_max) return;
+  const uint64_t warm = (uint64_t)m + k;
+  const uint64_t s0 = e_min - 1 > warm ? e_min - 1 - warm : 0;
+  const uint64_t* mask = Q.pmask + (size_t)p * Q.rows;
+  const uint64_t top = 1ull << (m - 1);
+  uint64_t r[KMAX + 1];
+#pragma unroll
+  for (int d = 0; d <= KMAX; ++d) r[d] = d ? ((1ull << d) - 1ull) : 0ull;  // prefilter.rs:415-418
+  for (uint64_t i = s0; i < e_max; ++i) {
+    const uint64_t bc = mask[Q.ids[i]];
+    uint64_t prev_old = r[0];
+    uint64_t prev_new = ((r[0] << 1) | 1ull) & bc;
+    r[0] = prev_new;
+    uint64_t hit = (k == 0) ? prev_new : 0ull;
+#pragma unroll
+    for (int d = 1; d <= KMAX; ++d) {
+      const uint64_t old = r[d];
+      const uint64_t nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | 1ull;
+      r[d] = nv;
+      prev_old = old;
+      prev_new = nv;
+      if ((uint32_t)d == k) hit = nv;
+    }
+    const uint64_t end = i + 1;
+    if (end >= e_min && (hit & top)) {  // coverage [end - m - k, end), as bitap_kernel
+      const uint64_t span = (uint64_t)m + k;
+      const uint64_t ws = end > span ? end - span : 0;
+      for (uint64_t y = ws; y < end;) {
+        const uint64_t w = y >> 5;
+        const uint32_t l = (uint32_t)(y & 31);
+        const uint32_t cnt = (uint32_t)min((uint64_t)(32 - l), end - y);
+        const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << l;
+        atomicOr(Q.cover + w, bits);
+        y += cnt;
+      }
+    }
+  }
+}
+
 // Maximal runs of set bits -> [start, end) windows (unordered; the host sorts them).
 __global__ void runs_kernel(const uint32_t* __restrict__ cover, uint64_t n_words, uint64_t n,
                             unsigned long long* __restrict__ out, unsigned long long* __restrict__ count,
@@ -3902,20 +4078,57 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     ensure_symbols(e, h);
     HIP_TRY(hipMemcpyAsync(d_ids.p, h.sym.data() + view.text_base, n, hipMemcpyHostToDevice, stream));
   }
-  // Pack the patterns into automaton words: patterns of one edit budget, longest first, each into
-  // the first word with room (first-fit decreasing); 32-bit words when every pattern fits one.
-  const uint32_t mmax = np ? *std::max_element(e.bp_m.begin(), e.bp_m.begin() + np) : 0u;
+  const uint32_t rows = e.alphabet + 1;
+  // Pigeonhole q-gram path (qgram_scan_kernel / qgram_verify_kernel) for the patterns whose k + 1
+  // pieces are at least 3 symbols long; the rest go through the full bitap scan.
+  std::vector<uint8_t> qlen(np, 0);
+  std::vector<std::pair<uint32_t, uint32_t>> grams;  // (gram key, pattern << 8 | piece offset)
+  if (!diag_env("FAC_NO_QGRAM") && rows <= 256) {
+    std::vector<uint32_t> sym(64);
+    for (uint32_t i = 0; i < np; ++i) {
+      const uint32_t m = e.bp_m[i], k = ks[i], L = m / (k + 1);
+      if (L < 3 || m > 63) continue;
+      bool one = true;  // every pattern position is exactly one symbol
+      for (uint32_t j = 0; j < m; ++j) {
+        uint32_t hits = 0;
+        for (uint32_t c = 0; c < rows; ++c)
+          if ((e.bp_mask[(size_t)i * rows + c] >> j) & 1ull) sym[j] = c, ++hits;
+        one = one && hits == 1;
+      }
+      if (!one) continue;
+      const uint32_t q = std::min<uint32_t>(4, L);
+      qlen[i] = (uint8_t)q;
+      for (uint32_t r = 0; r <= k; ++r) {
+        const uint32_t o = (uint32_t)((uint64_t)r * m / (k + 1));
+        grams.push_back({qgram_key(sym[o], sym[o + 1], sym[o + 2], q == 4 ? sym[o + 3] : 0u, q == 4), (i << 8) | o});
+      }
+    }
+    std::sort(grams.begin(), grams.end());
+    for (size_t a = 0, b; a < grams.size(); a = b) {  // at most 255 entries per gram (table word)
+      for (b = a; b < grams.size() && grams[b].first == grams[a].first; ++b) {}
+      if (b - a > 255) {
+        std::fill(qlen.begin(), qlen.end(), 0);
+        grams.clear();
+        break;
+      }
+    }
+  }
+  // Pack the full-scan patterns into automaton words: patterns of one edit budget, longest first,
+  // each into the first word with room (first-fit decreasing); 32-bit words when every pattern fits.
+  std::vector<uint32_t> order;
+  for (uint32_t i = 0; i < np; ++i)
+    if (!qlen[i]) order.push_back(i);
+  uint32_t mmax = 0;
+  for (uint32_t i : order) mmax = std::max(mmax, e.bp_m[i]);
   const bool w32 = mmax <= 32;
   const uint32_t wbits = w32 ? 32u : 64u;
-  std::vector<uint32_t> order(np);
-  for (uint32_t i = 0; i < np; ++i) order[i] = i;
   std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
     return ks[x] != ks[y] ? ks[x] < ks[y] : (e.bp_m[x] != e.bp_m[y] ? e.bp_m[x] > e.bp_m[y] : x < y);
   });
   std::vector<uint32_t> wk, wused;                   // per word: edit budget, bits used
   std::vector<std::pair<uint32_t, uint32_t>> place(np);  // pattern -> (word, bit offset)
   uint32_t k_first_word = 0;                         // words of the current budget start here
-  for (uint32_t idx = 0; idx < np; ++idx) {
+  for (uint32_t idx = 0; idx < (uint32_t)order.size(); ++idx) {
     const uint32_t i = order[idx], m = e.bp_m[i];
     if (idx && ks[i] != ks[order[idx - 1]]) k_first_word = (uint32_t)wk.size();
     uint32_t w = k_first_word;
@@ -3928,9 +4141,8 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     wused[w] += m;
   }
   const uint32_t nw = (uint32_t)wk.size();
-  const uint32_t rows = e.alphabet + 1;
   std::vector<uint64_t> pmask((size_t)rows * nw, 0), ptop(nw, 0);
-  for (uint32_t i = 0; i < np; ++i) {
+  for (uint32_t i : order) {
     const uint32_t w = place[i].first, off = place[i].second;
     ptop[w] |= 1ull << (off + e.bp_m[i] - 1);
     for (uint32_t c = 0; c < rows; ++c) pmask[(size_t)c * nw + w] |= e.bp_mask[(size_t)i * rows + c] << off;
@@ -3970,9 +4182,12 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
   B.cover = static_cast<uint32_t*>(d_cover.p);
   const uint64_t segs = (n + B.seg_len - 1) / B.seg_len;
   const uint64_t waves = segs * ((nw + 63) / 64);
-  const uint32_t kmax = ks.empty() ? 0 : *std::max_element(ks.begin(), ks.end());
-  const dim3 bgrid((uint32_t)((waves + 3) / 4));
-  if (w32) {
+  uint32_t kmax = 0;
+  for (uint32_t i : order) kmax = std::max(kmax, ks[i]);
+  const dim3 bgrid((uint32_t)std::max<uint64_t>(1, (waves + 3) / 4));
+  if (nw == 0) {
+    // every pattern takes the q-gram path
+  } else if (w32) {
     if (kmax == 0) hipLaunchKernelGGL((bitap_kernel<0, uint32_t>), bgrid, dim3(256), 0, stream, B);
     else if (kmax == 1) hipLaunchKernelGGL((bitap_kernel<1, uint32_t>), bgrid, dim3(256), 0, stream, B);
     else if (kmax == 2) hipLaunchKernelGGL((bitap_kernel<2, uint32_t>), bgrid, dim3(256), 0, stream, B);
@@ -3989,6 +4204,84 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     else hipLaunchKernelGGL((bitap_kernel<24, uint64_t>), bgrid, dim3(256), 0, stream, B);
   }
   HIP_TRY(hipGetLastError());
+  DevBuf d_qtab, d_qent, d_qmask, d_qpm, d_qcand, d_qn;
+  if (!grams.empty()) {
+    std::vector<uint32_t> ent(grams.size());
+    std::vector<std::pair<uint32_t, uint32_t>> keys;  // (key, first entry << 8 | entries)
+    for (size_t a = 0, b; a < grams.size(); a = b) {
+      for (b = a; b < grams.size() && grams[b].first == grams[a].first; ++b) ent[b] = grams[b].second;
+      keys.push_back({grams[a].first, (uint32_t)(a << 8) | (uint32_t)(b - a)});
+    }
+    uint32_t ts = 64;
+    while (ts < 2 * keys.size()) ts <<= 1;
+    std::vector<uint2> tab(ts, make_uint2(0u, 0u));
+    for (const auto& kv : keys) {
+      uint32_t sl = qgram_hash(kv.first) & (ts - 1);
+      while (tab[sl].y) sl = (sl + 1) & (ts - 1);
+      tab[sl] = make_uint2(kv.first, kv.second);
+    }
+    std::vector<uint32_t> pm(np, 0);
+    uint32_t kq = 0;
+    bool use3 = false, use4 = false;
+    for (uint32_t i = 0; i < np; ++i)
+      if (qlen[i]) {
+        pm[i] = e.bp_m[i] | (ks[i] << 8);
+        kq = std::max(kq, ks[i]);
+        (qlen[i] == 4 ? use4 : use3) = true;
+      }
+    HIP_TRY(d_qtab.alloc(tab.size() * sizeof(uint2), stream));
+    HIP_TRY(d_qent.alloc(ent.size() * 4, stream));
+    HIP_TRY(d_qmask.alloc(e.bp_mask.size() * 8, stream));
+    HIP_TRY(d_qpm.alloc(pm.size() * 4, stream));
+    HIP_TRY(hipMemcpyAsync(d_qtab.p, tab.data(), tab.size() * sizeof(uint2), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_qent.p, ent.data(), ent.size() * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_qmask.p, e.bp_mask.data(), e.bp_mask.size() * 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_qpm.p, pm.data(), pm.size() * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(d_qn.alloc(8, stream));
+    QgramParams Q{};
+    Q.ids = static_cast<const uint8_t*>(d_ids.p);
+    Q.n = n;
+    Q.tab = static_cast<const uint2*>(d_qtab.p);
+    Q.tab_mask = ts - 1;
+    Q.ent = static_cast<const uint32_t*>(d_qent.p);
+    Q.use3 = use3;
+    Q.use4 = use4;
+    Q.n_cand = static_cast<unsigned long long*>(d_qn.p);
+    Q.pmask = static_cast<const uint64_t*>(d_qmask.p);
+    Q.pm = static_cast<const uint32_t*>(d_qpm.p);
+    Q.rows = rows;
+    Q.cover = static_cast<uint32_t*>(d_cover.p);
+    int cus = 256;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
+    const uint32_t sgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, (uint64_t)cus * 16));
+    uint64_t qcap = std::max<uint64_t>(1 << 20, n / 16);
+    unsigned long long nc = 0;
+    for (;;) {  // candidates: one scan, again with room for all of them if the list overflowed
+      HIP_TRY(d_qcand.alloc(qcap * 8, stream));
+      Q.cand = static_cast<unsigned long long*>(d_qcand.p);
+      Q.cap = qcap;
+      HIP_TRY(hipMemsetAsync(d_qn.p, 0, 8, stream));
+      hipLaunchKernelGGL(qgram_scan_kernel, dim3(sgrid), dim3(256), 0, stream, Q);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemcpyAsync(&nc, d_qn.p, 8, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (nc <= qcap) break;
+      qcap = nc;
+    }
+    if (nc) {
+      const dim3 vg((uint32_t)((nc + 255) / 256));
+      if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+      else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+      else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+      else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+      else hipLaunchKernelGGL((qgram_verify_kernel<24>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+      HIP_TRY(hipGetLastError());
+    }
+    if (diag_env("FAC_RC_DEBUG"))
+      std::fprintf(stderr, "FAC_QGRAM patterns=%zu/%u grams=%zu keys=%zu candidates=%llu full-scan words=%u\n",
+                   (size_t)std::count_if(qlen.begin(), qlen.end(), [](uint8_t v) { return v != 0; }), np,
+                   grams.size(), keys.size(), nc, nw);
+  }
   uint64_t cap = 1 << 16;
   HIP_TRY(d_cnt.alloc(8, stream));
   for (;;) {

@@ -148,13 +148,18 @@ def test_bitap_windows_match_reference_merge(seed, vocab, filler):
             assert got == want, f"patterns={pats!r} hay={hay!r} thr={thr}\n gpu={got}\n orc={want}"
 
 
+@pytest.mark.parametrize("qgram", [True, False])
 @pytest.mark.parametrize("long_patterns", [False, True])
-def test_bitap_packed_words_match_reference(long_patterns):
+def test_bitap_packed_words_match_reference(long_patterns, qgram, monkeypatch):
     """Many patterns packed several to an automaton word (first-fit by edit budget): windows equal
     the oracle's per-pattern bitap_windows + merge (prefilter.rs:319-342, 410-435). Lengths 1..20
     (32-bit words) or 1..60 (64-bit words), mixed weights and per-pattern edit limits (several k
-    groups), planted fuzzy copies."""
+    groups), planted fuzzy copies. qgram: patterns whose k + 1 pieces hold >= 3 symbols take the
+    pigeonhole q-gram scan + per-candidate verification (the others the packed full scan); off: every
+    pattern the full scan."""
     from fuzzy_aho_corasick.engine import prefilter_windows
+    if not qgram:
+        monkeypatch.setenv("FAC_NO_QGRAM", "1")
     rng = Rng(0x5EED_B17A_9ACC_0001 ^ int(long_patterns))
     alpha = "abcdefghij"
     top = 60 if long_patterns else 20
@@ -183,6 +188,26 @@ def test_bitap_packed_words_match_reference(long_patterns):
         got = prefilter_windows(gpu, hay, thr)
         assert got == want, f"thr={thr}: {len(got)} vs {len(want)} windows"
     compare(b, pats, hay, 0.85, prefilter=True)
+
+
+def test_qgram_prefilter_c5_slice(monkeypatch):
+    """C5-shaped stream block (1K patterns of 10-16, threshold 0.85, k from k_for): merged bitap
+    windows of the q-gram path == the packed full scan (4 MiB) == the oracle's bitap_windows + merge
+    (first 192 KiB), and the pre-filtered search equals on the slice."""
+    from fuzzy_aho_corasick import workloads
+    from fuzzy_aho_corasick.engine import prefilter_windows
+    w = workloads.config("c5", 4 << 20, 5)
+    b = workloads.builder_for(w)
+    gpu = b.build(w.patterns)
+    hay = w.haystack.decode("utf-8")
+    got = prefilter_windows(gpu, hay, w.threshold)
+    monkeypatch.setenv("FAC_NO_QGRAM", "1")
+    full = prefilter_windows(gpu, hay, w.threshold)
+    assert got and got == full
+    small = hay[: 192 << 10]
+    assert prefilter_windows(gpu, small, w.threshold) == OracleEngine(b, w.patterns).prefilter_windows(small, w.threshold)
+    monkeypatch.delenv("FAC_NO_QGRAM")
+    assert prefilter_windows(gpu, small, w.threshold) == OracleEngine(b, w.patterns).prefilter_windows(small, w.threshold)
 
 
 def test_edge_inputs():
