@@ -242,7 +242,8 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_note,
                 "kernel": "whole search step: prefix-cache count/build/publish + rc_lookup + lane_window + "
-                          "bfs_window kernels" if not wl.prefilter else "bitap_kernel + runs + re-search",
+                          "bfs_window kernels" if not wl.prefilter else
+                          "pre-filter (q-gram scan + verify / packed bitap) + runs + re-search",
                 "avg_kernel_ms": step_dev_ms,
                 "algorithmic_bytes_per_launch": bytes_step,
                 "wave_kernel_only": {"kernel": "bfs_window_kernel", "avg_ms": wave_ms,
@@ -356,7 +357,8 @@ def run_c5(args, world, rank, local):
                        "parallelism": f"dp{world} (each GPU its 1/8 of the stream; RCCL gather of Match records)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "bitap_kernel + runs_kernel + re-search of the merged windows",
+                         "kernel": "pre-filter (q-gram scan + per-candidate bitap verify; packed bitap scan for "
+                                   "patterns with pieces < 3 symbols) + runs_kernel + re-search of the merged windows",
                          "avg_kernel_ms": dev_ms, "algorithmic_bytes_per_launch": bytes_step},
             "cpu_baseline": cpu,
             "diagnostics": {"matches_per_step": matches / K, "prefilter_ms_per_step": pf / K,
