@@ -393,6 +393,12 @@ int fac_haystack_stage_shard(const fac_engine* engine, const uint8_t* utf8, uint
   if (h.ascii) {
     h.owned = owned_bytes;
   } else {
+    std::string err;
+    if (int hrc = fac::ensure_host(h, err)) {
+      fac_haystack_free(fh);
+      *out = nullptr;
+      return fail(hrc, err);
+    }
     h.owned = (uint64_t)(std::lower_bound(h.starts.begin(), h.starts.end(), owned_bytes) - h.starts.begin());
   }
   return FAC_OK;
@@ -405,6 +411,8 @@ uint64_t fac_haystack_graphemes(const fac_haystack* hay) { return hay ? hay->h.n
 uint64_t fac_haystack_grapheme_starts(const fac_haystack* hay, uint64_t* out, uint64_t cap) {
   if (!hay) return 0;
   const fac::Haystack& h = hay->h;
+  std::string err;
+  if (!h.ascii && fac::ensure_host(h, err)) return 0;
   for (uint64_t g = 0; g < h.n && g < cap; ++g) out[g] = h.ascii ? g : h.starts[g];
   return h.n;
 }
@@ -491,7 +499,8 @@ int fac_search_raw(const fac_engine* engine, const uint8_t* utf8, uint64_t len, 
 namespace {
 
 // The staged bytes [bs, be) = graphemes [g0, g1) searched as a text of their own (search_raw on a
-// slice: is_ascii is re-decided on the slice, search.rs:196, prefilter.rs:349-350).
+// slice: is_ascii is re-decided on the slice, search.rs:196, prefilter.rs:349-350). A Unicode
+// haystack's host copies must be fetched first (ensure_host).
 fac::SegDesc slice_view(const fac::Haystack& h, uint64_t g0, uint64_t g1) {
   const uint64_t bs = h.ascii ? g0 : (g0 < h.n ? h.starts[g0] : h.len);
   const uint64_t be = h.ascii ? g1 : (g1 < h.n ? h.starts[g1] : h.len);
@@ -521,6 +530,7 @@ int prefiltered_view(const fac::Engine& e, const fac::Haystack& h, const fac::Se
   std::vector<std::pair<uint64_t, uint64_t>> windows;
   int rc = fac::prefilter_windows(e, h, view, ks, stream, windows, stats, err);
   if (rc) return rc;
+  if (!view.ascii && (rc = fac::ensure_host(h, err))) return rc;  // slice_view reads the host copies
   // Re-search each merged window as its own haystack (prefilter.rs:344-350): the slice re-decides
   // is_ascii, so an all-ASCII slice of a Unicode haystack is searched byte-wise.
   std::vector<fac::SegDesc> segs;
@@ -610,6 +620,9 @@ int fac_stream_window_staged(const fac_engine* engine, const fac_haystack* hay, 
   if (h.open_end || h.base) return fail(FAC_E_INVALID, "stream windows are cut from a whole staged haystack");
   g_end = std::min(g_end, h.n);
   g_begin = std::min(g_begin, g_end);
+  std::string herr;
+  if (!h.ascii)
+    if (int hrc = fac::ensure_host(h, herr)) return fail(hrc, herr);
   const fac::SegDesc view = slice_view(h, g_begin, g_end);
   const fac::Engine& e = engine->e;
   hipStream_t st = static_cast<hipStream_t>(stream);

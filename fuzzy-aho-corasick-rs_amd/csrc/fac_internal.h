@@ -369,8 +369,12 @@ struct Haystack {
   uint8_t* d_utf8 = nullptr;
   uint32_t* d_text32 = nullptr;  // Unicode only
   uint64_t* d_off = nullptr;     // Unicode only
-  std::vector<uint8_t> utf8;     // host copy (prefilter slices re-decide is_ascii)
-  std::vector<uint64_t> starts;  // grapheme byte starts (Unicode only)
+  // host copies, fetched from the device on first use (ensure_host): the UTF-8 bytes (pre-filter
+  // slices re-decide is_ascii; host transcodes) and the grapheme byte starts (Unicode only)
+  mutable std::vector<uint8_t> utf8;
+  mutable std::vector<uint64_t> starts;
+  mutable bool host_ready = false;
+  mutable std::mutex host_mu;
   mutable std::vector<uint8_t> sym;  // prefilter symbol ids per grapheme (Unicode only, lazy)
   mutable bool sym_ready = false;
   mutable uint32_t* d_gid = nullptr;  // grapheme ids (Unicode, engines with mappings; lazy)
@@ -413,6 +417,8 @@ int auto_beam_total(const Engine& e, const Haystack& h, const std::vector<SegDes
 // diagnostics knobs: FAC_* environment variables are honoured only with FAC_DIAGNOSTICS=1 set, so
 // a stray variable in a user's environment never changes the search path
 const char* diag_env(const char* name);
+// the host copies of a staged haystack (Haystack::utf8, ::starts), fetched once from the device
+int ensure_host(const Haystack& h, std::string& err);
 // largest grapheme count a haystack may have (u32::MAX, search.rs:198-201; lowered only by the
 // diagnostics knob FAC_GRAPHEME_LIMIT so tests can reach SearchError::HaystackTooLarge)
 uint64_t grapheme_limit();

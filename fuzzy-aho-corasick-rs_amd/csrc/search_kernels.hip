@@ -3183,7 +3183,6 @@ int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack&
   h.device = e.device;
   h.len = len;
   h.ascii = force_ascii < 0 ? ascii_only(utf8, len) : force_ascii != 0;
-  h.utf8.assign(utf8, utf8 + len);
   h.n = h.ascii ? len : 0;
   HIP_TRY(hipSetDevice(e.device));
   // All uploads go through one stream (the engine's, or the caller's) and are synchronized before
@@ -3203,8 +3202,24 @@ int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack&
 
 // Bit-parallel pre-filter transcode of a Unicode haystack (prefilter.rs:262-280): symbol id of
 // every folded grapheme, computed on first use (only pre-filtered searches need it).
+int ensure_host(const Haystack& h, std::string& err) {
+  std::lock_guard<std::mutex> lk(h.host_mu);
+  if (h.host_ready) return FAC_OK;
+  HIP_TRY(hipSetDevice(h.device));
+  h.utf8.resize(h.len);
+  if (h.len) HIP_TRY(hipMemcpy(h.utf8.data(), h.d_utf8, h.len, hipMemcpyDeviceToHost));
+  if (!h.ascii) {
+    h.starts.resize(h.n);
+    if (h.n) HIP_TRY(hipMemcpy(h.starts.data(), h.d_off, h.n * 8, hipMemcpyDeviceToHost));
+  }
+  h.host_ready = true;
+  return FAC_OK;
+}
+
 void ensure_symbols(const Engine& e, const Haystack& h) {
   if (h.ascii || h.sym_ready) return;
+  std::string err;
+  if (ensure_host(h, err)) return;
   h.sym.assign(h.n, 0);
   std::u32string g;
   const uint8_t* utf8 = h.utf8.data();
@@ -3233,6 +3248,7 @@ void free_haystack(Haystack& h) {
 // folded graphemes, grapheme.rs:61-63): computed on the host on first use and uploaded.
 int ensure_gids(const Engine& e, const Haystack& h, std::string& err) {
   if (h.ascii || (h.d_gid && h.gid_engine == &e)) return FAC_OK;
+  if (int hrc = ensure_host(h, err)) return hrc;
   std::vector<uint32_t> gid(h.n, 0);
   std::u32string g;
   const uint8_t* utf8 = h.utf8.data();
@@ -3999,6 +4015,8 @@ int launch_search_sink(const Engine& e, const Haystack& h, const std::vector<Seg
   if (rc) return rc;
   std::vector<SegDesc> tails;          // windows after each segment's switch window
   std::vector<std::pair<uint64_t, uint64_t>> keep;  // per segment: [byte_base, cut byte) of pass 1
+  if (!h.ascii)
+    if (int hrc = ensure_host(h, err)) return hrc;
   uint64_t v = 0;
   for (const SegDesc& c : segs) {
     uint64_t total = ab_prefix, cut_w = c.w_end;  // first window searched with the beam

@@ -249,7 +249,7 @@ __global__ void fold_kernel(const uint8_t* s, uint64_t len, const uint64_t* off,
 
 // Device staging of a valid, non-ASCII UTF-8 haystack already resident at h.d_utf8: fills
 // h.n, h.d_off (grapheme byte starts), h.d_text32 (folded first code points) and the host copy of
-// the starts (h.starts: pre-filter slices and auto-beam cuts are computed on the host).
+// the starts (fetched to the host only on demand: ensure_host).
 int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err) {
   const uint64_t len = h.len;
   uint8_t* brk = nullptr;
@@ -306,8 +306,6 @@ int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::stri
                        e.case_insensitive ? 1 : 0, h.d_text32);
     ST_TRY(hipGetLastError());
   }
-  h.starts.resize(h.n);
-  if (h.n) ST_TRY(hipMemcpyAsync(h.starts.data(), h.d_off, h.n * 8, hipMemcpyDeviceToHost, st));
   ST_TRY(hipStreamSynchronize(st));
   return FAC_OK;
 }

@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fac_internal.h"
@@ -117,9 +118,20 @@ uint64_t utf8_valid_prefix(const uint8_t* s, uint64_t n) {
   return n;
 }
 
-bool utf8_valid(const uint8_t* s, uint64_t n) {
+namespace {
+// Rust's str::from_utf8 acceptance (no overlongs, surrogates or code points past U+10FFFF); ASCII
+// runs are skipped eight bytes at a time
+bool utf8_valid_serial(const uint8_t* s, uint64_t n) {
   uint64_t i = 0;
   while (i < n) {
+    if (i + 8 <= n) {
+      uint64_t w;
+      std::memcpy(&w, s + i, 8);
+      if (!(w & 0x8080808080808080ull)) {
+        i += 8;
+        continue;
+      }
+    }
     uint8_t b = s[i];
     if (b < 0x80) { ++i; continue; }
     int len;
@@ -137,6 +149,30 @@ bool utf8_valid(const uint8_t* s, uint64_t n) {
     i += len;
   }
   return true;
+}
+}  // namespace
+
+// Large inputs are validated in up to 16 pieces on host threads, cut in front of a byte that is
+// not a continuation byte: every sequence then lies inside one piece (a sequence truncated by a
+// cut is invalid anyway, and so is a run of four continuation bytes that leaves no cut point).
+bool utf8_valid(const uint8_t* s, uint64_t n) {
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const uint64_t T = std::min<uint64_t>(std::min<uint64_t>(16, hw), n >> 22);  // >= 4 MiB a piece
+  if (T <= 1) return utf8_valid_serial(s, n);
+  std::vector<uint64_t> cut(T + 1);
+  cut[0] = 0;
+  cut[T] = n;
+  for (uint64_t t = 1; t < T; ++t) {
+    uint64_t p = n * t / T;
+    for (int k = 0; k < 4 && p < n && (s[p] & 0xC0) == 0x80; ++k) ++p;
+    cut[t] = std::max(cut[t - 1], p);
+  }
+  std::vector<char> ok(T, 1);
+  std::vector<std::thread> th;
+  for (uint64_t t = 0; t < T; ++t)
+    th.emplace_back([&, t] { ok[t] = utf8_valid_serial(s + cut[t], cut[t + 1] - cut[t]) ? 1 : 0; });
+  for (auto& x : th) x.join();
+  return std::all_of(ok.begin(), ok.end(), [](char v) { return v != 0; });
 }
 
 // UAX #29 extended grapheme cluster boundaries (rules GB3-GB13, GB999, with GB9c InCB).
