@@ -1871,6 +1871,20 @@ __device__ __forceinline__ bool flush_final(const SearchParams& P, bool resumed,
   return triv;
 }
 
+// Spilled windows of a dedup-free first pass restart on the exact variant, which needs an exact
+// snapshot: their hits are looked up again in the levels built by the exact kernel (P.rc_tab).
+__global__ __launch_bounds__(256) void rc_relookup_kernel(SearchParams P, uint64_t n) {
+  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t vid = P.win_list[x];
+    const uint32_t kl = find_seg(P, vid);
+    const SegDesc S = P.segs[kl];
+    const uint64_t start = S.w_begin + (vid - P.seg_prefix[kl]);
+    const RcHit hit = rc_lookup(P, S, start, P.rc_qcap);
+    P.rc_hits[vid] = make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel);
+    P.rc_hit_pops[vid] = hit.pops;
+  }
+}
+
 // Per-window prefix-cache lookups of a main pass (P.rc_mode == 1), ahead of the search kernel:
 // windows that are skipped or finished by their snapshot are marked RC_DONE (the latter flushed
 // here); every other window's hit (or miss) is stored for the search kernel. Keeps the lookup's
@@ -2436,6 +2450,26 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
               nv += (uint32_t)__popcll(__ballot(live(k)));
               jlive = max(jlive, live(k) ? (k.jm & 0xFFFFu) + 1u : 0u);
             }
+          // LIVE (dedup-free) build: no table of its own; the snapshot carries the parent's check
+          // entries that a later pop can still meet (jmin <= j < the parent's jcheck) -- no beam ran
+          // in this build, so they remain the only entries popped before a beam (run_window LIVE)
+          const uint4* carry = nullptr;
+          uint32_t ncarry = 0, jcp = 0;
+          if constexpr (VCAP == 0 && LIVE) {
+            if (rc.off != EMPTY) {
+              const uint32_t pj = P.rc_pool[rc.off + 1].y;
+              jcp = pj & 0xFFFFu;
+              ncarry = pj >> 16;
+              carry = P.rc_pool + rc.off + RC_HDR + (rc.tail - rc.head);
+            }
+            for (uint32_t b = 0; b < ncarry; b += 64) {
+              const uint4 d = b + lane < ncarry ? carry[b + lane] : make_uint4(EMPTY, 0u, 0u, 0u);
+              const uint32_t dj = d.y & 0xFFFFu;
+              const bool keep = d.x != EMPTY && dj >= jmin && dj + 1u <= jcp;
+              nv += (uint32_t)__popcll(__ballot(keep));
+              jlive = max(jlive, keep ? dj + 1u : 0u);
+            }
+          }
           jlive = wave_inclusive_max(jlive);
           jlive = shfl_u32(jlive, 63);
           bool bad = (wave_or(err) & (ERR_QUEUE | ERR_VISITED | ERR_EMIT)) != 0 || EL.n > P.rc_emax || nv > P.rc_vmax;
@@ -2475,6 +2509,17 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
                 at0 += (uint32_t)__popcll(m);
                 if (pass == 0) ncheck = at0;
               }
+          } else if constexpr (LIVE) {  // every carried entry is a check entry
+            uint32_t at0 = 0;
+            for (uint32_t b = 0; b < ncarry && !bad; b += 64) {
+              const uint4 d = b + lane < ncarry ? carry[b + lane] : make_uint4(EMPTY, 0u, 0u, 0u);
+              const uint32_t dj = d.y & 0xFFFFu;
+              const bool keep = d.x != EMPTY && dj >= jmin && dj + 1u <= jcp;
+              const uint64_t m = __ballot(keep);
+              if (keep) dst[nq + at0 + prefix_below(m)] = d;
+              at0 += (uint32_t)__popcll(m);
+            }
+            ncheck = at0;
           }
           for (uint32_t i = lane; i < EL.n && !bad; i += 64) dst[nq + nv + i] = EL.buf[i];
           if (lane == 0) {
@@ -2552,6 +2597,12 @@ template <uint32_t QCAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((FAC_BEAM_WAVES && QCAP <= 256) ? FAC_BEAM_WAVES : 1)))
 void rc_build_kernel(SearchParams P) {
   bfs_window_body<512, QCAP, false, true>(P);  // the prefix cache is off with mappings
+}
+// dedup-free build of a sampled level of a beamed engine (launch_pass): resumes from the parent
+// snapshot, honours its check entries (run_window LIVE); a key that would beam (or overflow) is left
+// uncached, its windows resume from the shallower level
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void rc_build_kernel_live(SearchParams P) {
+  bfs_window_body<0, 256, false, true, true>(P);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3466,6 +3517,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   // least T times get a snapshot built by resuming their representative from its level-1 snapshot.
   // A window resumes from the deepest snapshot its prefix has. Skipped when the root emits (an empty
   // pattern), with mappings (whole-grapheme keys), or when the search is small.
+  RcTable exact_tab[kRcLevels];  // levels whose snapshots are exact (deepest first)
+  uint32_t n_exact_tabs = 0;
+  bool any_inexact = false;
   P.rc_mode = 0;
   P.rc_hits = nullptr;
   P.rc_hit_pops = nullptr;
@@ -3587,6 +3641,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       }
     } l1_done_guard{l1_done};
     std::vector<RcTable> tabs;  // built levels, ascending k: a build resumes its representatives from them
+    std::vector<bool> tab_exact;  // built by the exact kernel (else dedup-free: rc_build_kernel_live)
+    // sampled levels of beamed engines are built dedup-free (not for the auto-beam count pass, which
+    // needs every window's exact queue.len(), nor with mappings)
+    const bool live_builds = P.beam && !counts && !e.has_map && qbuild <= 256 && !diag_env("FAC_NO_LIVE_BUILD");
     const uint64_t ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", 4)));
     auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, hipStream_t bs, bool cleared = false) -> int {
       SearchParams Q = P;
@@ -3609,7 +3667,15 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       Q.spill_cap = spill_cap;
       Q.counters = static_cast<unsigned long long*>(d_cnt.p);
       if (!cleared) HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), bs));
-      launch_rc_build(qbuild, std::min<uint32_t>(n_ent, max_grid), bs, Q);
+      uint32_t grid = std::min<uint32_t>(n_ent, max_grid);
+      if (bs != stream && !diag_env("FAC_L1_PERSIST")) {
+        // beside the sampled-level counts: one chunk per workgroup, so workgroup slots free up all
+        // along the build and the counts (higher-priority stream) are not held back to its end
+        Q.dyn_chunks = 0;
+        grid = (uint32_t)std::min<uint64_t>((n_ent + Q.chunk - 1) / Q.chunk, 0x7FFFFFFFull);
+      }
+      if (live_builds && Q.rc_ntab > 0) hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
+      else launch_rc_build(qbuild, grid, bs, Q);
       const hipError_t le = hipGetLastError();
       if (le != hipSuccess) {
         err = std::string("kernel launch: ") + hipGetErrorString(le);
@@ -3656,7 +3722,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       P.rc_pool = static_cast<uint4*>(d_rcs.p);
       P.rc_pool_cap = pool_words;
       if (!diag_env("FAC_RC_ONE_STREAM")) {
-        if (!e.aux_stream) HIP_TRY(hipStreamCreateWithFlags(&e.aux_stream, hipStreamNonBlocking));
+        if (!e.aux_stream) {  // the lowest priority: the sampled-level counts beside it come first
+          int least = 0, greatest = 0;
+          HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+          HIP_TRY(hipStreamCreateWithPriority(&e.aux_stream, hipStreamNonBlocking, least));
+        }
         HIP_TRY(hipEventCreateWithFlags(&l1_done, hipEventDisableTiming));
         bstream = e.aux_stream;
       }
@@ -3680,6 +3750,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if ((brc = publish(L1, n_ent1, d_ct[0], bstream, true))) return brc;
       if (bstream != stream) HIP_TRY(hipEventRecord(l1_done, bstream));
       tabs.push_back(L1);
+      tab_exact.push_back(true);
       return FAC_OK;
     };
     const uint32_t stride2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_STRIDE2", 2));
@@ -3744,10 +3815,15 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         if (brc) return brc;
         if ((brc = publish(Lx[x], n_entx[x], d_ct[1 + x], stream))) return brc;
         tabs.push_back(Lx[x]);
+        tab_exact.push_back(!live_builds);
       }
       P.rc_ntab = 0;
       for (size_t t = tabs.size(); t-- > 0;) P.rc_tab[P.rc_ntab++] = tabs[t];
       P.rc_mode = 1;
+      n_exact_tabs = 0;
+      for (size_t t = tabs.size(); t-- > 0;)
+        if (tab_exact[t]) exact_tab[n_exact_tabs++] = tabs[t];
+      any_inexact = n_exact_tabs < tabs.size();
     }
     HIP_TRY(hipEventRecord(ev.b, stream));
     HIP_TRY(hipStreamSynchronize(stream));
@@ -3959,6 +4035,17 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       spill_cap = std::max<uint64_t>(spill_cap, pass_windows);
     }
     P.win_list = static_cast<const uint64_t*>(d_list.p);
+    if (P.rc_mode == 1 && any_inexact && kVariants[vi].vcap > 0) {
+      // the exact variant restarts the spilled windows from exact snapshots
+      SearchParams R = P;
+      R.rc_ntab = n_exact_tabs;
+      for (uint32_t t = 0; t < n_exact_tabs; ++t) R.rc_tab[t] = exact_tab[t];
+      R.rc_qcap = kVariants[vi].qcap;
+      hipLaunchKernelGGL(rc_relookup_kernel, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((pass_windows + 255) / 256, (uint64_t)cus * 16))),
+                         dim3(256), 0, stream, R, pass_windows);
+      HIP_TRY(hipGetLastError());
+      any_inexact = false;  // those hits are exact now
+    }
     ++retries;
   }
   if (timing)
