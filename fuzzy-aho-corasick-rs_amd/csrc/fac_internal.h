@@ -166,7 +166,7 @@ struct RcTable {
 };
 
 constexpr int N_COUNTERS = 10;  // SearchParams::counters (8: lane-searched windows, 9: lane work counter)
-constexpr int kRcLevels = 4;   // prefix-cache levels: level 1 + up to 3 sampled levels
+constexpr int kRcLevels = 5;   // prefix-cache levels: level 0 (under level 1), level 1, up to 3 sampled levels
 
 struct SearchParams {
   // automaton
@@ -252,6 +252,8 @@ struct SearchParams {
   uint32_t* rc_hit_pops;            // ... and the snapshot's pops
   uint32_t* rc_off;                 // build: snapshot offset of each entry (pool words)
   uint32_t* rc_count;               // build: queued states of each entry (EMPTY: not cached)
+  int32_t rc_keep_final;            // build: snapshot a key whose parent is final too (its level is
+                                    // looked up without the parent's: level 1 over level 0)
   // multi-character mappings (search.rs:776-780, 883-922, 945-961; builder.rs:383-442). With
   // has_map, exact and swap transitions compare whole folded graphemes (ids, 0 = not in the
   // engine's grapheme dictionary): edge_gid per edge, text gids per grapheme (gid32 for Unicode
@@ -351,7 +353,7 @@ struct Engine {
   // per-engine device scratch of the search launcher, reused across calls by whichever call holds
   // scratch_mu (a concurrent call on the same engine allocates its own)
   mutable std::mutex scratch_mu;
-  static constexpr int kScratch = 48;
+  static constexpr int kScratch = 64;
   mutable void* scratch_p[kScratch] = {};
   mutable size_t scratch_n[kScratch] = {};
 };

@@ -1098,6 +1098,7 @@ __device__ __forceinline__ fac_match match_record(const SearchParams& P, const S
 constexpr uint32_t claim_slots(uint32_t vcap) { return vcap / 2 < 512 ? 512 : vcap / 2; }  // >= ExpScratch
 
 __device__ unsigned long long g_live_dbg[8];  // diagnostics (FAC_RC_DEBUG): live-dedup checks / hits
+__device__ unsigned long long g_bad[8];       // diagnostics (FAC_RC_DEBUG): uncached keys by reason
 #ifdef FAC_WIN_HIST  // diagnostics build (make hist): windows, pops and cycles by pops per window
 __device__ unsigned long long g_hist[24];
 __device__ __forceinline__ uint32_t hist_bucket(uint64_t pops) {  // 0, 1-15, 16-63, 64-255, 256-1023, 1024+
@@ -1730,9 +1731,39 @@ __global__ __launch_bounds__(256) void rc_publish_kernel(const uint4* pool, cons
 // so keys seen once (most long keys) never reach the table and the table is sized for repeated keys
 // (a count of c then means c + 1 sightings; bitmap collisions only admit a few singletons). A key
 // that finds no slot within `probes` stays uncounted (not cached).
-__global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, unsigned long long* keys, uint32_t* cnt,
-                                                       uint64_t* rep, uint32_t mask, uint32_t stride, uint32_t sat,
-                                                       uint32_t* seen, uint32_t seen_mask, uint32_t probes) {
+// One level's count table (rc_count_kernel): keys of k chars, open addressing with `probes` slots
+struct RcCountTarget {
+  unsigned long long* keys;
+  uint32_t* cnt;
+  uint64_t* rep;
+  uint32_t mask;
+  uint32_t k;  // 0: no table
+};
+__device__ __forceinline__ void rc_count_insert(const RcCountTarget& T, uint64_t k, uint64_t vid, uint32_t sat,
+                                                uint32_t probes) {
+  const uint32_t h = rc_hash(k);
+  for (uint32_t p = 0; p < probes; ++p) {
+    const uint32_t slot = (h + p) & T.mask;
+    unsigned long long kk = T.keys[slot];
+    if (kk == 0ull) {
+      kk = atomicCAS(&T.keys[slot], 0ull, (unsigned long long)k);
+      if (kk == 0ull) {
+        T.rep[slot] = vid;
+        atomicAdd(&T.cnt[slot], 1u);
+        return;
+      }
+    }
+    if (kk == k) {  // sat == 1 (level 1 keeps every key): the inserter's count is all it needs
+      if (sat > 1u && T.cnt[slot] < sat) atomicAdd(&T.cnt[slot], 1u);
+      return;
+    }
+  }
+}
+// Two levels are counted in one pass over the windows (levels 1 and 0; the two sampled levels):
+// their inserts go out together.
+__global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, RcCountTarget t0, RcCountTarget t1,
+                                                       uint32_t stride, uint32_t sat, uint32_t* seen, uint32_t seen_mask,
+                                                       uint32_t probes) {
   const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
   unsigned err = 0;
   const uint64_t ns = (P.total_windows + stride - 1) / stride;
@@ -1742,29 +1773,18 @@ __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, unsigned 
     const SegDesc S = P.segs[kl];
     const uint64_t start = S.w_begin + (vid - P.seg_prefix[kl]);
     if (window_skipped(P, S, start, err)) continue;
-    RcChars ch;
-    uint64_t k;
-    if (!rc_key(P, S, start, P.rc_k, ch, k)) continue;
-    if (seen) {
-      const uint32_t b = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 32) & seen_mask;
-      if (!(atomicOr(&seen[b >> 5], 1u << (b & 31u)) & (1u << (b & 31u)))) continue;  // first sighting
-    }
-    const uint32_t h = rc_hash(k);
-    for (uint32_t p = 0; p < probes; ++p) {
-      const uint32_t slot = (h + p) & mask;
-      unsigned long long kk = keys[slot];
-      if (kk == 0ull) {
-        kk = atomicCAS(&keys[slot], 0ull, (unsigned long long)k);
-        if (kk == 0ull) {
-          rep[slot] = vid;
-          atomicAdd(&cnt[slot], 1u);
-          break;
-        }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const RcCountTarget& T = t ? t1 : t0;
+      if (!T.k) continue;
+      RcChars ch;
+      uint64_t k;
+      if (!rc_key(P, S, start, T.k, ch, k)) continue;
+      if (seen) {
+        const uint32_t b = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 32) & seen_mask;
+        if (!(atomicOr(&seen[b >> 5], 1u << (b & 31u)) & (1u << (b & 31u)))) continue;  // first sighting
       }
-      if (kk == k) {  // sat == 1 (level 1 keeps every key): the inserter's count is all it needs
-        if (sat > 1u && cnt[slot] < sat) atomicAdd(&cnt[slot], 1u);
-        break;
-      }
+      rc_count_insert(T, k, vid, sat, probes);
     }
   }
 }
@@ -2401,7 +2421,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
       if (P.rc_mode == 2) {
         // a representative whose parent snapshot has an empty queue ends at the parent: its own
         // snapshot would hold the same best list, so the key stays uncached (lookups fall through)
-        const bool done = active && hit.off != EMPTY && hit.tail == hit.head;
+        const bool done = active && hit.off != EMPTY && hit.tail == hit.head && !P.rc_keep_final;
         if (done) {
           P.rc_off[v] = EMPTY;
           P.rc_count[v] = EMPTY;
@@ -2473,6 +2493,10 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           jlive = wave_inclusive_max(jlive);
           jlive = shfl_u32(jlive, 63);
           bool bad = (wave_or(err) & (ERR_QUEUE | ERR_VISITED | ERR_EMIT)) != 0 || EL.n > P.rc_emax || nv > P.rc_vmax;
+          if (bad && lane == 0) {  // diagnostics (FAC_RC_DEBUG): why keys stay uncached
+            const unsigned we = wave_or(err);
+            atomicAdd(&g_bad[(we & ERR_QUEUE) ? 0 : (we & ERR_VISITED) ? 1 : (we & ERR_EMIT) ? 2 : EL.n > P.rc_emax ? 3 : 4], 1ull);
+          }
           const uint32_t words = RC_HDR + nq + nv + EL.n;
           // the wave carves snapshots out of its own pool chunk: one pool atomic per chunk, not per
           // snapshot (a same-address atomic per entry serialises the build at one L2 channel)
@@ -3452,7 +3476,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   DevBuf d_rck, d_rcv, d_rcslot, d_rcb, d_rcrep, d_rcs, d_rcc, d_rcn;  // prefix cache, level 1 + pool
   DevBuf d_xk[kRcLevels - 1], d_xv[kRcLevels - 1], d_xslot[kRcLevels - 1], d_xrep[kRcLevels - 1],
       d_xc[kRcLevels - 1];  // prefix cache, sampled levels
-  DevBuf d_ct[kRcLevels];  // prefix cache lookup tables
+  DevBuf d_ct[kRcLevels];  // prefix cache lookup tables ([kRcLevels - 1]: level 0)
+  DevBuf d_l0k, d_l0v, d_l0slot, d_l0rep, d_l0c;  // prefix cache, level 0
   DevBuf d_hits, d_hitp;   // per-window lookups of the main pass
   DevBuf d_seen;           // prefix cache: sampled levels' first-sighting bitmap
   ScratchSet* bound = t_scratch;  // a streaming worker's own set, else the engine's
@@ -3465,10 +3490,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     for (int x = 0; x < kRcLevels - 1; ++x)
       for (DevBuf* b : {&d_xk[x], &d_xv[x], &d_xslot[x], &d_xrep[x], &d_xc[x]}) bufs.push_back(b);
     for (int x = 0; x < kRcLevels; ++x) bufs.push_back(&d_ct[x]);
+    for (DevBuf* b : {&d_l0k, &d_l0v, &d_l0slot, &d_l0rep, &d_l0c}) bufs.push_back(b);
     bufs.push_back(&d_hits);
     bufs.push_back(&d_hitp);
     bufs.push_back(&d_seen);
-    static_assert(Engine::kScratch >= 20 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
+    static_assert(Engine::kScratch >= 25 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
     static_assert(ScratchSet::kSlots >= Engine::kScratch, "stream scratch slots");
     for (size_t i = 0; i < bufs.size(); ++i) bufs[i]->bind(&scratch_p[i], &scratch_n[i]);
   }
@@ -3588,13 +3614,35 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     };
     uint32_t n_ent1 = 0;
     uint64_t l1_keys = 0;
+    // Level 0: keys one char shorter than level 1's, every window, built from the root; the level-1
+    // build then resumes its representatives from them and pops only the last key char's states
+    // (the root pop, its beam and the first chars' states are shared by every level-1 key). Counted
+    // in the level-1 pass; used when level 1 keeps its first key length.
+    RcTable L0{0u, 0u, nullptr, nullptr, nullptr, nullptr};
+    uint32_t n_ent0 = 0;
+    const bool want_l0 = !diag_env("FAC_NO_RC_L0");
+    auto target = [](const DevBuf& keys, const DevBuf& cnt, const DevBuf& rep, uint32_t n_slots, uint32_t k) {
+      return RcCountTarget{static_cast<unsigned long long*>(keys.p), static_cast<uint32_t*>(cnt.p),
+                           static_cast<uint64_t*>(rep.p), n_slots - 1, k};
+    };
     for (uint32_t k = kpin ? kpin : 4u; k >= (kpin ? kpin : 2u); --k) {
       P.rc_k = k;
       HIP_TRY(hipMemsetAsync(d_rck.p, 0, slots * sizeof(unsigned long long), stream));
       HIP_TRY(hipMemsetAsync(d_rcv.p, 0, slots * sizeof(uint32_t), stream));
-      hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P,
-                         static_cast<unsigned long long*>(d_rck.p), static_cast<uint32_t*>(d_rcv.p),
-                         static_cast<uint64_t*>(d_rcslot.p), slots - 1, 1u, 1u, nullptr, 0u, cprobes);
+      const uint32_t k0 = std::max<uint64_t>(2, std::min<uint64_t>(k - 1, env_u("FAC_RC_L0K", k - 1)));  // knob: A/B
+      const bool l0 = want_l0 && k >= 3 && L0.k == 0;  // the first key length only
+      RcCountTarget t1{nullptr, nullptr, nullptr, 0u, 0u};
+      if (l0) {
+        HIP_TRY(d_l0k.alloc(slots * sizeof(unsigned long long), stream));
+        HIP_TRY(d_l0v.alloc(slots * sizeof(uint32_t), stream));
+        HIP_TRY(d_l0slot.alloc(slots * sizeof(uint64_t), stream));
+        HIP_TRY(hipMemsetAsync(d_l0k.p, 0, slots * sizeof(unsigned long long), stream));
+        HIP_TRY(hipMemsetAsync(d_l0v.p, 0, slots * sizeof(uint32_t), stream));
+        t1 = target(d_l0k, d_l0v, d_l0slot, slots, k0);
+        L0.k = k0;
+      }
+      hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P, target(d_rck, d_rcv, d_rcslot, slots, k),
+                         t1, 1u, 1u, nullptr, 0u, cprobes);
       HIP_TRY(hipGetLastError());
       unsigned int n_keys = 0;
       if (int nrc = number_entries(d_rck, d_rcv, d_rcslot, d_rcrep, slots, 1u, max_ent, n_keys)) return nrc;
@@ -3603,8 +3651,20 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (!kpin && 8ull * n_keys > windows) continue;  // too little reuse: fewer chars per key
       n_ent1 = std::min(n_keys, max_ent);
       L1.k = k;
+      if (l0) {
+        const uint32_t max_ent0 = std::min<uint32_t>(n_ent1, max_ent);
+        HIP_TRY(d_l0rep.alloc(max_ent0 * sizeof(uint64_t), stream));
+        HIP_TRY(d_l0c.alloc(2 * (size_t)max_ent0 * sizeof(uint32_t), stream));
+        unsigned int n0 = 0;
+        if (int nrc = number_entries(d_l0k, d_l0v, d_l0slot, d_l0rep, slots, 1u, max_ent0, n0)) return nrc;
+        n_ent0 = std::min(n0, max_ent0);
+        L0 = RcTable{k0, slots - 1, static_cast<const unsigned long long*>(d_l0k.p),
+                     static_cast<const uint32_t*>(d_l0v.p), static_cast<uint32_t*>(d_l0c.p) + max_ent0,
+                     static_cast<uint32_t*>(d_l0c.p)};
+      }
       break;
     }
+    if (!n_ent0) L0.k = 0;
     // sampled levels: frequent long prefixes, ascending key lengths (FAC_RC_LEVELS, e.g. "6" or
     // "5,7"; FAC_RC_K2 = k pins one level, 0 turns them off)
     std::vector<uint32_t> ks;
@@ -3620,7 +3680,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       for (size_t a = 0; a < spec.size();) {
         const size_t b = spec.find(',', a);
         const uint32_t k = (uint32_t)std::strtoul(spec.substr(a, b == std::string::npos ? std::string::npos : b - a).c_str(), nullptr, 10);
-        if (k && (ks.empty() || k > ks.back()) && k <= 8 && ks.size() < (size_t)kRcLevels - 1) ks.push_back(k);
+        if (k && (ks.empty() || k > ks.back()) && k <= 8 && ks.size() < (size_t)kRcLevels - 2) ks.push_back(k);
         if (b == std::string::npos) break;
         a = b + 1;
       }
@@ -3646,7 +3706,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     // needs every window's exact queue.len(), nor with mappings)
     const bool live_builds = P.beam && !counts && !e.has_map && qbuild <= 256 && !diag_env("FAC_NO_LIVE_BUILD");
     const uint64_t ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", 4)));
-    auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, hipStream_t bs, bool cleared = false) -> int {
+    auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, hipStream_t bs, bool cleared = false,
+                     bool sampled = false) -> int {
       SearchParams Q = P;
       Q.rc_mode = 2;
       Q.rc_k = T.k;
@@ -3655,6 +3716,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         Q.rc_tab[Q.rc_ntab++] = tabs[t];
       Q.rc_off = const_cast<uint32_t*>(T.off);
       Q.rc_count = const_cast<uint32_t*>(T.count);
+      Q.rc_keep_final = (n_ent0 && T.k == L1.k) ? 1 : 0;  // main lookups skip level 0
       Q.win_list = reps;
       Q.total_windows = n_ent;
       // list chunks of up to 64 representatives: their parent lookups go out together
@@ -3674,7 +3736,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         Q.dyn_chunks = 0;
         grid = (uint32_t)std::min<uint64_t>((n_ent + Q.chunk - 1) / Q.chunk, 0x7FFFFFFFull);
       }
-      if (live_builds && Q.rc_ntab > 0) hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
+      if (live_builds && sampled && Q.rc_ntab > 0) hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
       else launch_rc_build(qbuild, grid, bs, Q);
       const hipError_t le = hipGetLastError();
       if (le != hipSuccess) {
@@ -3710,11 +3772,12 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       return FAC_OK;
     };
     if (n_ent1) {
-      const uint64_t n_all = n_ent1 + (uint64_t)ks.size() * max_ent2_est;
+      const uint64_t n_all = n_ent0 + n_ent1 + (uint64_t)ks.size() * max_ent2_est;
       const uint64_t budget = env_u("FAC_RC_POOL_MB", 16384ull) << 20;
       // per-wave pool chunks: about a quarter of the expected pool (~40 words a snapshot) spread over
       // the building waves, at least one worst snapshot; + one partly used chunk per wave and level
-      const uint64_t grids = std::min<uint64_t>(n_ent1, max_grid) + (uint64_t)ks.size() * std::min<uint64_t>(max_ent2_est, max_grid);
+      const uint64_t grids = std::min<uint64_t>(n_ent0, max_grid) + std::min<uint64_t>(n_ent1, max_grid) +
+                             (uint64_t)ks.size() * std::min<uint64_t>(max_ent2_est, max_grid);
       P.rc_pool_chunk = (uint32_t)std::max<uint64_t>(worst, std::min<uint64_t>(RC_POOL_CHUNK, n_all * 40 / (4 * grids)));
       const uint64_t pool_words = std::max<uint64_t>(1024, std::min<uint64_t>(n_all * worst, budget / sizeof(uint4))) +
                                   grids * P.rc_pool_chunk;
@@ -3741,9 +3804,21 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       // sampled-level count kernel's workgroups started the build 2.6 ms late
       HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), stream));
       if (int crc = clear_ct(n_ent1, d_ct[0], stream)) return crc;  // likewise the lookup table
+      if (n_ent0) {  // level 0 first (same stream), the level-1 build resumes from it
+        HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), stream));
+        if (int crc = clear_ct(n_ent0, d_ct[kRcLevels - 1], stream)) return crc;
+      }
       if (bstream != stream) {
         HIP_TRY(hipEventRecord(l1_done, stream));  // everything so far (counts, pool, clears) first
         HIP_TRY(hipStreamWaitEvent(bstream, l1_done, 0));
+      }
+      if (n_ent0) {
+        int brc = build(L0, n_ent0, static_cast<const uint64_t*>(d_l0rep.p), bstream, true);
+        if (brc) return brc;
+        if ((brc = publish(L0, n_ent0, d_ct[kRcLevels - 1], bstream, true))) return brc;
+        tabs.push_back(L0);
+        tab_exact.push_back(true);
+        HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), bstream));
       }
       int brc = build(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p), bstream, true);
       if (brc) return brc;
@@ -3789,13 +3864,18 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (int lrc = launch_l1()) return lrc;
       for (size_t x = 0; x < kk.size(); ++x) {
         const uint32_t k2 = kk[x];
-        if (seen) HIP_TRY(hipMemsetAsync(seen, 0, ((size_t)seen_mask + 1) / 8, stream));
-        SearchParams C = P;
-        C.rc_k = k2;
-        hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, C,
-                           static_cast<unsigned long long*>(d_xk[x].p), static_cast<uint32_t*>(d_xv[x].p),
-                           static_cast<uint64_t*>(d_xslot[x].p), slots2 - 1, stride2, thr_t, seen, seen_mask, cprobes);
-        HIP_TRY(hipGetLastError());
+        // levels are counted two per pass over the sampled windows (one each with the first-sighting
+        // bitmap, which is per level)
+        if (seen || x % 2 == 0) {
+          if (seen) HIP_TRY(hipMemsetAsync(seen, 0, ((size_t)seen_mask + 1) / 8, stream));
+          const bool pair = !seen && x + 1 < kk.size();
+          const RcCountTarget t1 = pair ? target(d_xk[x + 1], d_xv[x + 1], d_xslot[x + 1], slots2, kk[x + 1])
+                                        : RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u};
+          hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P,
+                             target(d_xk[x], d_xv[x], d_xslot[x], slots2, k2), t1, stride2, thr_t, seen, seen_mask,
+                             cprobes);
+          HIP_TRY(hipGetLastError());
+        }
         unsigned int nk2 = 0;
         if (int nrc = number_entries(d_xk[x], d_xv[x], d_xslot[x], d_xrep[x], slots2, thr_t, max_ent2, nk2)) return nrc;
         const uint32_t ne = std::min(nk2, max_ent2);
@@ -3811,14 +3891,15 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     if (n_ent1) {
       if (bstream != stream) HIP_TRY(hipStreamWaitEvent(stream, l1_done, 0));  // level 1 built and published
       for (size_t x = 0; x < Lx.size(); ++x) {
-        int brc = build(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), stream);
+        int brc = build(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), stream, false, true);
         if (brc) return brc;
         if ((brc = publish(Lx[x], n_entx[x], d_ct[1 + x], stream))) return brc;
         tabs.push_back(Lx[x]);
         tab_exact.push_back(!live_builds);
       }
-      P.rc_ntab = 0;
-      for (size_t t = tabs.size(); t-- > 0;) P.rc_tab[P.rc_ntab++] = tabs[t];
+      P.rc_ntab = 0;  // level 0 only feeds the level-1 build: every window holds a level-1 key
+      for (size_t t = tabs.size(); t-- > 0;)
+        if (!(n_ent0 && tabs[t].k == L0.k)) P.rc_tab[P.rc_ntab++] = tabs[t];
       P.rc_mode = 1;
       n_exact_tabs = 0;
       for (size_t t = tabs.size(); t-- > 0;)
@@ -3850,9 +3931,21 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
                       (unsigned long long)c, c ? (double)q / c : 0.0);
         lv += b;
       }
-      std::fprintf(stderr, "FAC_RC windows=%llu L1 k=%u keys=%llu cached=%llu mean_queue=%.1f%s | pool %.1f MB\n",
-                   (unsigned long long)windows, L1.k, (unsigned long long)l1_keys, (unsigned long long)c1, c1 ? (double)q1 / c1 : 0.0,
-                   lv.c_str(), rcn[1] * 16.0 / 1e6);
+      {
+        unsigned long long gb[8];
+        HIP_TRY(hipMemcpyFromSymbol(gb, HIP_SYMBOL(g_bad), sizeof(gb)));
+        std::fprintf(stderr, "FAC_RC uncached keys: queue %llu visited %llu emit %llu best %llu vmax %llu\n", gb[0], gb[1],
+                     gb[2], gb[3], gb[4]);
+        std::memset(gb, 0, sizeof(gb));
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_bad), gb, sizeof(gb)));
+      }
+      uint64_t q0 = 0;
+      const uint64_t c0 = n_ent0 ? cached_of(L0, n_ent0, q0) : 0;
+      std::fprintf(stderr, "FAC_RC windows=%llu L0 k=%u entries=%u cached=%llu mean_queue=%.1f | L1 k=%u keys=%llu cached=%llu "
+                   "mean_queue=%.1f%s | pool %.1f MB\n",
+                   (unsigned long long)windows, L0.k, n_ent0, (unsigned long long)c0, c0 ? (double)q0 / c0 : 0.0, L1.k,
+                   (unsigned long long)l1_keys, (unsigned long long)c1, c1 ? (double)q1 / c1 : 0.0, lv.c_str(),
+                   rcn[1] * 16.0 / 1e6);
     }
   }
   const double t_cache = host_ms();
