@@ -165,7 +165,7 @@ struct RcTable {
   uint32_t ct_mask;                  // lookup slots - 1
 };
 
-constexpr int N_COUNTERS = 10;  // SearchParams::counters (8: lane-searched windows, 9: lane work counter)
+constexpr int N_COUNTERS = 11;  // SearchParams::counters (8: lane-searched windows, 9: lane work counter, 10: lookup regions)
 constexpr int kRcLevels = 5;   // prefix-cache levels: level 0 (under level 1), level 1, up to 3 sampled levels
 
 struct SearchParams {
@@ -250,6 +250,11 @@ struct SearchParams {
   uint32_t rc_qcap;                 // main pass ring: snapshots with more queued states are not resumed
   uint4* rc_hits;                   // main pass: per window {offset | RC_DONE, head, tail, nv | ne << 16}
   uint32_t* rc_hit_pops;            // ... and the snapshot's pops
+  // main pass: rc_hits / rc_hit_pops hold only the windows the lookups leave open, compacted per
+  // region of RC_REGION windows (entries [r * RC_REGION, + rc_region_cnt[r])); rc_voff = the window
+  // of each entry as its offset in the region
+  uint32_t* rc_voff;
+  uint32_t* rc_region_cnt;
   uint32_t* rc_off;                 // build: snapshot offset of each entry (pool words)
   uint32_t* rc_count;               // build: queued states of each entry (EMPTY: not cached)
   int32_t rc_keep_final;            // build: snapshot a key whose parent is final too (its level is

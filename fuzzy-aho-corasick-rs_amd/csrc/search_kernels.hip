@@ -714,6 +714,13 @@ __device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState&
 }
 
 // Wave-wide inclusive max-scan (DPP), unsigned.
+// adds the wave's sum of v to a global counter with one atomic (every lane of the wave calls it): a
+// per-lane atomic on one address serialises at one L2 channel (1M of them at the end of a lookup)
+__device__ __forceinline__ void wave_add_counter(unsigned long long* c, unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if (lane_id() == 0 && v) atomicAdd(c, v);
+}
 __device__ __forceinline__ uint32_t wave_inclusive_max(uint32_t v) {
   int x = (int)v;
   x = (int)max((uint32_t)x, (uint32_t)__builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false));
@@ -1074,6 +1081,7 @@ constexpr uint32_t RC_POOL_CHUNK = 4096;  // largest pool chunk (words, 64 KiB) 
 constexpr uint32_t RC_HDR = 4;
 struct RcHit {  // prefix-cache snapshot of a window (rc_lookup): pool offset and header
   uint32_t off, head, tail, nv_nel, pops;
+  uint32_t lvl = 0;  // rc_tab index of the hit (diagnostics)
 };
 
 // one best-map entry {me_rel, pattern, similarity bits, packed counts} of the window at `start`
@@ -1099,6 +1107,7 @@ constexpr uint32_t claim_slots(uint32_t vcap) { return vcap / 2 < 512 ? 512 : vc
 
 __device__ unsigned long long g_live_dbg[8];  // diagnostics (FAC_RC_DEBUG): live-dedup checks / hits
 __device__ unsigned long long g_bad[8];       // diagnostics (FAC_RC_DEBUG): uncached keys by reason
+__device__ unsigned long long g_lk_dbg[16];   // diagnostics (FAC_RC_DEBUG): main lookups by level x final, misses, skips
 #ifdef FAC_WIN_HIST  // diagnostics build (make hist): windows, pops and cycles by pops per window
 __device__ unsigned long long g_hist[24];
 __device__ __forceinline__ uint32_t hist_bucket(uint64_t pops) {  // 0, 1-15, 16-63, 64-255, 256-1023, 1024+
@@ -1589,6 +1598,10 @@ __device__ __forceinline__ uint32_t rc_hash(uint64_t k) { return (uint32_t)k ^ (
 constexpr uint32_t RC_PROBES = 32;
 constexpr uint32_t RC_OCC = 1u << 31, RC_POPS_MASK = (1u << 22) - 1;
 constexpr uint32_t RC_DONE = 0xFFFFFFFEu;  // rc_hits: window skipped or finished by its snapshot
+constexpr uint32_t RC_REGION = 1024;       // main pass: windows per region of compacted open entries
+__device__ __forceinline__ uint64_t rc_window_of(const SearchParams& P, uint64_t e) {  // entry -> window
+  return (e / RC_REGION) * RC_REGION + P.rc_voff[e];
+}
 // exact lookup key: the first k chars as 16-bit units (0xFFFF pads; chars >= 0xFFFF are not encoded)
 __device__ __forceinline__ uint4 rc_exact_key(const uint32_t c[8], uint32_t k) {
   uint32_t u[8];
@@ -1643,49 +1656,32 @@ __device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc&
 #pragma unroll
   for (uint32_t i = 0; i < 8; ++i)  // keys hold 16-bit units: a longer key would contain char i
     if (enc == 8 && c[i] != RC_PAD && c[i] >= 0xFFFFu) enc = i;
-  bool live[kRcLevels];
-  uint4 key[kRcLevels], val[kRcLevels];
-  uint32_t slot[kRcLevels];
-  bool sure = false;  // the deepest level's first probe already holds a usable hit
-#pragma unroll
-  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {
-    // The deepest level goes first and the shallower levels' probes only go out for windows it did
-    // not settle (they would lose to it anyway): one random 128-byte line per window instead of one
-    // per level (C3: lookup FETCH 31.8 GB -> see DESIGN.md).
-    const RcTable& T = P.rc_tab[t];
-    live[t] = t < P.rc_ntab && T.k <= enc && (ok || s + T.k <= S.avail) && !sure;
-    key[t] = rc_exact_key(c, T.k);
-    slot[t] = rc_key_hash(key[t]) & T.ct_mask;
-    if (live[t]) {
-      const uint4* e = T.ct + 2 * (size_t)slot[t];
-      key[t] = make_uint4(key[t].x ^ e[0].x, key[t].y ^ e[0].y, key[t].z ^ e[0].z, key[t].w ^ e[0].w);  // 0: match
-      val[t] = e[1];
-      if (t == 0)
-        sure = (val[0].w & RC_OCC) && !(key[0].x | key[0].y | key[0].z | key[0].w) && (val[0].z & 0xFFFFu) + 1u <= QCAP;
-    }
-  }
+  // Levels are probed one at a time, deepest first, and a window stops at its first usable hit: the
+  // lookups are bound by the random 128-byte lines they pull (C3: a window settled by the second
+  // level pulls two lines, not three).
   RcHit r{EMPTY, 0u, 0u, 0u, 0u};
   bool found = false;
 #pragma unroll
-  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {  // deepest first; collisions probe on (rare)
-    if (found || !live[t]) continue;
+  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {
     const RcTable& T = P.rc_tab[t];
-    bool hit = (val[t].w & RC_OCC) && !(key[t].x | key[t].y | key[t].z | key[t].w);
-    if (!hit && (val[t].w & RC_OCC)) {
-      const uint4 want = rc_exact_key(c, T.k);
-      for (uint32_t p = 1; p < RC_PROBES && !hit; ++p) {
-        slot[t] = (slot[t] + 1) & T.ct_mask;
-        const uint4* e = T.ct + 2 * (size_t)slot[t];
-        val[t] = e[1];
-        if (!(val[t].w & RC_OCC)) break;
-        const uint4 k2 = e[0];
-        hit = k2.x == want.x && k2.y == want.y && k2.z == want.z && k2.w == want.w;
+    if (found || !(t < P.rc_ntab && T.k <= enc && (ok || s + T.k <= S.avail))) continue;
+    const uint4 want = rc_exact_key(c, T.k);
+    uint32_t slot = rc_key_hash(want) & T.ct_mask;
+    bool hit = false;
+    uint4 val = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t p = 0; p < RC_PROBES; ++p, slot = (slot + 1) & T.ct_mask) {  // collisions probe on (rare)
+      const uint4* e = T.ct + 2 * (size_t)slot;
+      const uint4 k2 = e[0];
+      val = e[1];
+      if (!(val.w & RC_OCC)) break;
+      if (k2.x == want.x && k2.y == want.y && k2.z == want.z && k2.w == want.w) {
+        hit = true;
+        break;
       }
     }
-    const uint32_t nq = val[t].z & 0xFFFFu;
+    const uint32_t nq = val.z & 0xFFFFu;
     if (hit && nq + 1u <= QCAP) {
-      r = RcHit{val[t].x, val[t].y, val[t].y + nq, ((val[t].w >> 22) & 0x1FFu) | (val[t].z & 0xFFFF0000u),
-                val[t].w & RC_POPS_MASK};
+      r = RcHit{val.x, val.y, val.y + nq, ((val.w >> 22) & 0x1FFu) | (val.z & 0xFFFF0000u), val.w & RC_POPS_MASK, t};
       found = true;
     }
   }
@@ -1895,28 +1891,38 @@ __device__ __forceinline__ bool flush_final(const SearchParams& P, bool resumed,
 // snapshot: their hits are looked up again in the levels built by the exact kernel (P.rc_tab).
 __global__ __launch_bounds__(256) void rc_relookup_kernel(SearchParams P, uint64_t n) {
   for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t vid = P.win_list[x];
-    const uint32_t kl = find_seg(P, vid);
+    const uint64_t vid = P.win_list[x];  // an open entry
+    const uint64_t wid = rc_window_of(P, vid);
+    const uint32_t kl = find_seg(P, wid);
     const SegDesc S = P.segs[kl];
-    const uint64_t start = S.w_begin + (vid - P.seg_prefix[kl]);
+    const uint64_t start = S.w_begin + (wid - P.seg_prefix[kl]);
     const RcHit hit = rc_lookup(P, S, start, P.rc_qcap);
     P.rc_hits[vid] = make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel);
     P.rc_hit_pops[vid] = hit.pops;
   }
 }
 
-// Per-window prefix-cache lookups of a main pass (P.rc_mode == 1), ahead of the search kernel:
-// windows that are skipped or finished by their snapshot are marked RC_DONE (the latter flushed
-// here); every other window's hit (or miss) is stored for the search kernel. Keeps the lookup's
-// registers out of the search kernel.
+// Per-window prefix-cache lookups of a main pass (P.rc_mode == 1), ahead of the search kernels:
+// windows that are skipped or finished by their snapshot (flushed here) are done; the others' hits
+// (or misses) are stored compacted per region of RC_REGION windows (entries rc_hits / rc_hit_pops /
+// rc_voff, counts rc_region_cnt), so the searches read only the open windows (C2: 15 % of them).
+// A wave takes whole regions from a work counter (counters[10]). Keeps the lookup's registers out of
+// the search kernels.
 __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
   const uint32_t lane = lane_id();
   uint64_t cached_lane = 0;
   uint32_t res_lane = 0, triv_lane = 0;
   unsigned err = 0;
-  const uint64_t wstride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); v0 < P.total_windows; v0 += wstride) {
-    const uint64_t v = v0 + lane;  // whole waves iterate together (ballots, DPP scans)
+  const uint64_t n_reg = (P.total_windows + RC_REGION - 1) / RC_REGION;
+  for (;;) {
+    unsigned long long rg = 0;
+    if (lane == 0) rg = atomicAdd(P.counters + 10, 1ull);
+    rg = shfl_u64(rg, 0);
+    if (rg >= n_reg) break;
+    const uint64_t rbase = rg * RC_REGION;
+    uint32_t n_open = 0;  // wave-uniform
+    for (uint32_t it = 0; it < RC_REGION; it += 64) {
+    const uint64_t v = rbase + it + lane;  // whole waves iterate together (ballots, DPP scans)
     bool active = v < P.total_windows;
     uint32_t kl = 0;
     uint64_t start = 0;
@@ -1930,15 +1936,29 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
     if (active) hit = rc_lookup(P, P.segs[kl], start, P.rc_qcap);
     const bool resumed = active && hit.off != EMPTY;
     res_lane += resumed ? 1u : 0u;
-    const bool fin = flush_final(P, resumed, hit, kl, start, v, cached_lane, triv_lane);
-    if (v < P.total_windows) {
-      P.rc_hits[v] = (active && !fin) ? make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel) : make_uint4(RC_DONE, 0u, 0u, 0u);
-      P.rc_hit_pops[v] = hit.pops;
+    if (P.lane_debug) {  // diagnostics: windows by the level they resume from (x final), misses, skips
+      const uint32_t cat = !(v < P.total_windows) ? 15u : !active ? 13u : !resumed ? 12u : hit.lvl * 2u + (hit.tail == hit.head ? 1u : 0u);
+      for (uint32_t c = 0; c < 14; ++c) {
+        const uint64_t m = __ballot(cat == c);
+        if (m && lane == 0) atomicAdd(&g_lk_dbg[c], (unsigned long long)__popcll(m));
+      }
     }
+    const bool fin = flush_final(P, resumed, hit, kl, start, v, cached_lane, triv_lane);
+    const bool open = active && !fin;
+    const uint64_t om = __ballot(open);
+    if (open) {
+      const uint64_t e = rbase + n_open + prefix_below(om);
+      P.rc_hits[e] = make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel);
+      P.rc_hit_pops[e] = hit.pops;
+      P.rc_voff[e] = it + lane;
+    }
+    n_open += (uint32_t)__popcll(om);
+    }
+    if (lane == 0) P.rc_region_cnt[rg] = n_open;
   }
-  if (cached_lane) atomicAdd(P.counters + 4, cached_lane);
-  if (res_lane) atomicAdd(P.counters + 5, (unsigned long long)res_lane);
-  if (triv_lane) atomicAdd(P.counters + 6, (unsigned long long)triv_lane);
+  wave_add_counter(P.counters + 4, cached_lane);
+  wave_add_counter(P.counters + 5, res_lane);
+  wave_add_counter(P.counters + 6, triv_lane);
   if (err) atomicOr(reinterpret_cast<unsigned int*>(P.counters + 2), err);
 }
 
@@ -2212,7 +2232,8 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
   uint64_t popped_lane = 0, cached_lane = 0;
   uint32_t done_lane = 0;
   uint32_t nbuf = 0;          // wave-uniform: listed windows
-  uint64_t cur = 0, ce = 0;   // wave-uniform: scan position and end of the current chunk
+  uint64_t cur = 0, ce = 0;   // wave-uniform: scan position and end of the current region's entries
+  uint64_t rg_next = 0, rg_end = 0;  // wave-uniform: regions left of the current chunk
   bool chunks_done = false;   // wave-uniform
   uint32_t status = 0, head = 0, tail = 0, nel = 0, pops = 0, snap_pops = 0;
   LiveDedup lv{0u, 0u, 0u};
@@ -2225,16 +2246,22 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
     const uint64_t idle = __ballot(status != LANE_RUN);
     const uint32_t n_idle = (uint32_t)__popcll(idle);
     while (nbuf < n_idle && !chunks_done) {  // list unfinished resumed windows whose snapshot fits
-      if (cur >= ce) {
-        unsigned long long c = 0;
-        if (lane == 0) c = atomicAdd(P.counters + 9, (unsigned long long)LANE_CHUNK);
-        const uint64_t cb = shfl_u64(c, 0);
-        if (cb >= P.total_windows) {
-          chunks_done = true;
-          break;
+      if (cur >= ce) {  // the next region's open entries (rc_lookup_kernel)
+        if (rg_next >= rg_end) {  // the next LANE_CHUNK windows' regions
+          unsigned long long c = 0;
+          if (lane == 0) c = atomicAdd(P.counters + 9, (unsigned long long)LANE_CHUNK);
+          const uint64_t cb = shfl_u64(c, 0);
+          if (cb >= P.total_windows) {
+            chunks_done = true;
+            break;
+          }
+          rg_next = cb / RC_REGION;
+          rg_end = (min(cb + (uint64_t)LANE_CHUNK, P.total_windows) + RC_REGION - 1) / RC_REGION;
         }
-        cur = cb;
-        ce = min(cb + (uint64_t)LANE_CHUNK, P.total_windows);
+        cur = rg_next * RC_REGION;
+        ce = cur + P.rc_region_cnt[rg_next];
+        ++rg_next;
+        continue;
       }
       const uint64_t v = cur + lane;
       bool take = false;
@@ -2266,12 +2293,13 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
       __builtin_amdgcn_wave_barrier();
     }
     if (starts) {  // resume the window from its snapshot
-      vid = next;
+      vid = next;  // an open entry
       const uint4 h = P.rc_hits[vid];
       snap_pops = P.rc_hit_pops[vid];
-      const uint32_t kl = find_seg(P, vid);
+      const uint64_t wid = rc_window_of(P, vid);
+      const uint32_t kl = find_seg(P, wid);
       S = P.segs[kl];
-      start = S.w_begin + (vid - P.seg_prefix[kl]);
+      start = S.w_begin + (wid - P.seg_prefix[kl]);
       const uint32_t nq = h.z - h.y, nv = h.w & 0xFFFFu;
       nel = h.w >> 16;
       const uint4* src = P.rc_pool + h.x + RC_HDR;  // queue, dedup entries (unused), best list
@@ -2322,9 +2350,9 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
       }
     }
   }
-  if (popped_lane) atomicAdd(P.counters + 1, popped_lane);
-  if (cached_lane) atomicAdd(P.counters + 4, cached_lane);
-  if (done_lane) atomicAdd(P.counters + 8, (unsigned long long)done_lane);
+  wave_add_counter(P.counters + 1, popped_lane);
+  wave_add_counter(P.counters + 4, cached_lane);
+  wave_add_counter(P.counters + 8, done_lane);
   if (P.lane_debug) {  // diagnostics (FAC_RC_DEBUG): windows started / finished, pop steps, cycles
     const uint32_t st = (uint32_t)wave_inclusive_sum((uint32_t)started), dn = wave_inclusive_sum(done_lane);
     if (lane == 63) {
@@ -2367,9 +2395,20 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
     return shfl_u64(c, 0);
   };
   const uint64_t stride = (uint64_t)gridDim.x * P.chunk;
-  for (uint64_t cb = P.dyn_chunks ? next_chunk() : (uint64_t)blockIdx.x * P.chunk; cb < P.total_windows;
-       cb = P.dyn_chunks ? next_chunk() : cb + stride) {
-    const uint64_t ce = min(cb + (uint64_t)P.chunk, P.total_windows);
+  // behind the lookups a chunk holds the open entries of each region it covers: one sub-range each
+  const bool regions = !LK && P.rc_mode == 1 && !P.win_list;
+  for (uint64_t cb0 = P.dyn_chunks ? next_chunk() : (uint64_t)blockIdx.x * P.chunk; cb0 < P.total_windows;
+       cb0 = P.dyn_chunks ? next_chunk() : cb0 + stride) {
+    const uint64_t ce0 = min(cb0 + (uint64_t)P.chunk, P.total_windows);
+    for (uint64_t cb = cb0, cnext = cb0; cb < ce0 && !any_err(err); cb = cnext) {
+    uint64_t ce = ce0;
+    cnext = ce0;
+    if (regions) {
+      const uint64_t rg = cb / RC_REGION;
+      cnext = min(ce0, (rg + 1) * RC_REGION);
+      ce = min(cnext, rg * RC_REGION + P.rc_region_cnt[rg]);
+      if (cb >= ce) continue;
+    }
     // A main pass behind the lookups (and the lane kernel) finds most windows already RC_DONE:
     // one round of independent loads marks the chunk's 64-window groups that hold live windows,
     // and the rest are skipped without their dependent segment / hit / pops loads (C2 1 GiB: 6K
@@ -2396,13 +2435,14 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
       const uint64_t v = v0 + lane;
       bool active = v < ce;
       uint32_t kl = 0;
-      uint64_t start = 0, vid = 0;
+      uint64_t start = 0, vid = 0, wid = 0;  // list id (an open entry behind the lookups) and window
       RcHit hit{EMPTY, 0u, 0u, 0u, 0u};  // prefix-cache snapshot of this lane's window
       if (active) {
         vid = P.win_list ? P.win_list[v] : v;
-        kl = find_seg(P, vid);
+        wid = (!LK && P.rc_mode == 1) ? rc_window_of(P, vid) : vid;
+        kl = find_seg(P, wid);
         const SegDesc S = P.segs[kl];
-        start = S.w_begin + (vid - P.seg_prefix[kl]);
+        start = S.w_begin + (wid - P.seg_prefix[kl]);
         if (!LK && P.rc_mode == 1) {  // skip decision and lookup made by rc_lookup_kernel
           const uint4 h = P.rc_hits[vid];
           hit = RcHit{h.x, h.y, h.z, h.w, P.rc_hit_pops[vid]};
@@ -2416,7 +2456,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
       if (LK && P.rc_mode == 1) {
         const bool resumed = active && hit.off != EMPTY;
         res_lane += resumed ? 1u : 0u;
-        active = active && !flush_final(P, resumed, hit, kl, start, vid, cached_lane, triv_lane);
+        active = active && !flush_final(P, resumed, hit, kl, start, wid, cached_lane, triv_lane);
       }
       if (P.rc_mode == 2) {
         // a representative whose parent snapshot has an empty queue ends at the parent: its own
@@ -2565,7 +2605,8 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           continue;
         }
         const bool overflow = (wave_or(err) & (ERR_QUEUE | ERR_VISITED)) != 0;
-        if (P.win_counts && !overflow && lane == 0) P.win_counts[shfl_u64(vid, l)] = qlen;
+        const uint64_t w_id = shfl_u64(wid, l);
+        if (P.win_counts && !overflow && lane == 0) P.win_counts[w_id] = qlen;
         if (overflow) {  // frontier overflow: spill the window
           const uint64_t id = shfl_u64(vid, l);
           if (lane == 0) {
@@ -2579,13 +2620,14 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
       }
       if (any_err(err)) break;
     }
+    }  // sub-ranges
     if (any_err(err)) break;
   }
   if (lane == 0) atomicAdd(P.counters + 1, (unsigned long long)popped);
   if (lane == 0) cached_lane += cached;
-  if (cached_lane) atomicAdd(P.counters + 4, cached_lane);
-  if (res_lane) atomicAdd(P.counters + 5, (unsigned long long)res_lane);
-  if (triv_lane) atomicAdd(P.counters + 6, (unsigned long long)triv_lane);
+  wave_add_counter(P.counters + 4, cached_lane);
+  wave_add_counter(P.counters + 5, res_lane);
+  wave_add_counter(P.counters + 6, triv_lane);
   const unsigned all = wave_or(err);
   if (lane == 0 && all) atomicOr(reinterpret_cast<unsigned int*>(P.counters + 2), all);
 }
@@ -3479,6 +3521,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   DevBuf d_ct[kRcLevels];  // prefix cache lookup tables ([kRcLevels - 1]: level 0)
   DevBuf d_l0k, d_l0v, d_l0slot, d_l0rep, d_l0c;  // prefix cache, level 0
   DevBuf d_hits, d_hitp;   // per-window lookups of the main pass
+  DevBuf d_voff, d_rcnt;   // ... their windows and per-region counts
   DevBuf d_seen;           // prefix cache: sampled levels' first-sighting bitmap
   ScratchSet* bound = t_scratch;  // a streaming worker's own set, else the engine's
   std::unique_lock<std::mutex> lease(bound ? bound->mu : e.scratch_mu, std::try_to_lock);
@@ -3494,7 +3537,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     bufs.push_back(&d_hits);
     bufs.push_back(&d_hitp);
     bufs.push_back(&d_seen);
-    static_assert(Engine::kScratch >= 25 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
+    bufs.push_back(&d_voff);
+    bufs.push_back(&d_rcnt);
+    static_assert(Engine::kScratch >= 27 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
     static_assert(ScratchSet::kSlots >= Engine::kScratch, "stream scratch slots");
     for (size_t i = 0; i < bufs.size(); ++i) bufs[i]->bind(&scratch_p[i], &scratch_n[i]);
   }
@@ -3549,6 +3594,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.rc_mode = 0;
   P.rc_hits = nullptr;
   P.rc_hit_pops = nullptr;
+  P.rc_voff = nullptr;
+  P.rc_region_cnt = nullptr;
   P.rc_ntab = 0;
   P.rc_lane_flush = diag_env("FAC_RC_NO_LANE") ? 0 : 1;
   P.dyn_chunks = diag_env("FAC_STATIC_GRID") ? 0 : 1;
@@ -3974,16 +4021,25 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), stream));
     if (debug_poison()) HIP_TRY(hipMemsetAsync(d_out.p, 0xAB, out_cap * sizeof(fac_match), stream));
     if (P.rc_mode == 1 && !P.win_list) {  // every window's lookup (+ flush of finished windows) first
-      HIP_TRY(d_hits.alloc(windows * sizeof(uint4), stream));
-      HIP_TRY(d_hitp.alloc(windows * sizeof(uint32_t), stream));
+      // the open windows' hits, compacted per region (entries: n_reg * RC_REGION at most)
+      const uint64_t n_reg = (windows + RC_REGION - 1) / RC_REGION;
+      HIP_TRY(d_hits.alloc(n_reg * RC_REGION * sizeof(uint4), stream));
+      HIP_TRY(d_hitp.alloc(n_reg * RC_REGION * sizeof(uint32_t), stream));
+      HIP_TRY(d_voff.alloc(n_reg * RC_REGION * sizeof(uint32_t), stream));
+      HIP_TRY(d_rcnt.alloc(n_reg * sizeof(uint32_t), stream));
       P.rc_hits = static_cast<uint4*>(d_hits.p);
       P.rc_hit_pops = static_cast<uint32_t*>(d_hitp.p);
+      P.rc_voff = static_cast<uint32_t*>(d_voff.p);
+      P.rc_region_cnt = static_cast<uint32_t*>(d_rcnt.p);
       P.rc_qcap = kVariants[vi].qcap;
       HIP_TRY(hipEventRecord(ev.a, stream));
-      hipLaunchKernelGGL(rc_lookup_kernel, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256, (uint64_t)cus * 16))),
+      P.lane_debug = diag_env("FAC_RC_DEBUG") ? 1 : 0;
+      // one region per wave turn, up to 32 waves per CU (7 fit: SGPR-bound)
+      hipLaunchKernelGGL(rc_lookup_kernel, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_reg + 3) / 4, (uint64_t)cus * 8))),
                          dim3(256), 0, stream, P);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(ev.b, stream));
+      P.total_windows = n_reg * RC_REGION;  // the searches run over entries
       // small unfinished windows: one lane each (lane_window_kernel); the rest stay for the wave kernel
       const bool lane_on = !diag_env("FAC_NO_LANE") && !P.win_counts && !P.has_map;  // beamed: exact_dedup is set, bail-outs keep it exact
       if (lane_on) {
@@ -4004,6 +4060,19 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       float lms = 0.f;
       HIP_TRY(hipEventElapsedTime(&lms, ev.a, ev.b));
       cache_ms += lms;
+      if (P.lane_debug) {
+        unsigned long long d[16];
+        HIP_TRY(hipMemcpyFromSymbol(d, HIP_SYMBOL(g_lk_dbg), sizeof(d)));
+        std::string lv;
+        for (uint32_t t = 0; t < P.rc_ntab; ++t) {
+          char b[96];
+          std::snprintf(b, sizeof(b), " k=%u: open %llu final %llu |", P.rc_tab[t].k, d[2 * t], d[2 * t + 1]);
+          lv += b;
+        }
+        std::fprintf(stderr, "FAC_LK%s miss %llu skipped %llu\n", lv.c_str(), d[12], d[13]);
+        std::memset(d, 0, sizeof(d));
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_lk_dbg), d, sizeof(d)));
+      }
       if (lane_on) {
         HIP_TRY(hipEventElapsedTime(&lms, ev.b, ev_lane));
         lane_ms += lms;
