@@ -1785,6 +1785,21 @@ __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, RcCountTa
   }
 }
 
+// Level-0 keys are the level-1 keys' prefixes: inserted from the level-1 representatives (one per
+// level-1 key, each the representative of its prefix too) instead of from every window.
+__global__ __launch_bounds__(256) void rc_derive_kernel(SearchParams P, const uint64_t* reps, uint32_t n,
+                                                        RcCountTarget T, uint32_t probes) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t vid = reps[i];
+    const uint32_t kl = find_seg(P, vid);
+    const SegDesc S = P.segs[kl];
+    const uint64_t start = S.w_begin + (vid - P.seg_prefix[kl]);
+    RcChars ch;
+    uint64_t k;
+    if (rc_key(P, S, start, T.k, ch, k)) rc_count_insert(T, k, vid, 1u, probes);
+  }
+}
+
 // Entries of a level: the keys counted at least `thr` times, numbered without a contended counter
 // (one same-address atomic per selected wave serialises at one L2 channel): per-block counts over
 // contiguous slot ranges, an exclusive scan of the block counts, then the assignment. Every other
@@ -3689,7 +3704,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         L0.k = k0;
       }
       hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P, target(d_rck, d_rcv, d_rcslot, slots, k),
-                         t1, 1u, 1u, nullptr, 0u, cprobes);
+                         RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u}, 1u, 1u, nullptr, 0u, cprobes);
       HIP_TRY(hipGetLastError());
       unsigned int n_keys = 0;
       if (int nrc = number_entries(d_rck, d_rcv, d_rcslot, d_rcrep, slots, 1u, max_ent, n_keys)) return nrc;
@@ -3698,7 +3713,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (!kpin && 8ull * n_keys > windows) continue;  // too little reuse: fewer chars per key
       n_ent1 = std::min(n_keys, max_ent);
       L1.k = k;
-      if (l0) {
+      if (l0) {  // level-0 keys from the level-1 representatives
+        hipLaunchKernelGGL(rc_derive_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_ent1 + 255) / 256, cus * 8))), dim3(256),
+                           0, stream, P, static_cast<const uint64_t*>(d_rcrep.p), n_ent1, t1, cprobes);
+        HIP_TRY(hipGetLastError());
         const uint32_t max_ent0 = std::min<uint32_t>(n_ent1, max_ent);
         HIP_TRY(d_l0rep.alloc(max_ent0 * sizeof(uint64_t), stream));
         HIP_TRY(d_l0c.alloc(2 * (size_t)max_ent0 * sizeof(uint32_t), stream));
