@@ -3647,7 +3647,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     P.rc_pool_used = static_cast<unsigned long long*>(d_rcn.p) + 1;
     HIP_TRY(hipEventRecord(ev.a, stream));
     HIP_TRY(hipMemsetAsync(d_rcn.p, 0, 4 * sizeof(unsigned long long), stream));
-    const uint32_t cgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256, (uint64_t)cus * 8));
+    const uint32_t cgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256, (uint64_t)cus * env_u("FAC_RC_CGRID", 8)));
+
     // keys counted >= thr -> entries 0..n-1 (slot counts replaced by entries in place), reps by entry;
     // returns n (all selected keys; entries past max_ent stay uncached)
     auto number_entries = [&](const DevBuf& keys, const DevBuf& cv, const DevBuf& rslot, const DevBuf& rep,
@@ -3853,7 +3854,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         if (!e.aux_stream) {  // the lowest priority: the sampled-level counts beside it come first
           int least = 0, greatest = 0;
           HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-          HIP_TRY(hipStreamCreateWithPriority(&e.aux_stream, hipStreamNonBlocking, least));
+          HIP_TRY(hipStreamCreateWithPriority(&e.aux_stream, hipStreamNonBlocking, diag_env("FAC_L1_HIGH") ? greatest : least));
         }
         HIP_TRY(hipEventCreateWithFlags(&l1_done, hipEventDisableTiming));
         bstream = e.aux_stream;
@@ -3894,6 +3895,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       return FAC_OK;
     };
     const uint32_t stride2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_STRIDE2", 2));
+    // the sampled levels' counts run beside the level-0/1 builds and have slack until the level-1
+    // build ends: fewer workgroups leave the builds more of the CUs. Measured: two sampled levels
+    // (C3) 2 per CU (-2 ms against 8), one level (C2, whose builds are shorter) 4 per CU (-2 ms)
+    const uint32_t cgrid2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256,
+        (uint64_t)cus * env_u("FAC_RC_CGRID2", ks.size() >= 2 ? 2 : 4)));
     const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", 2));
     std::vector<RcTable> Lx;        // sampled levels, ascending k
     std::vector<uint32_t> n_entx;   // their entries
@@ -3936,7 +3942,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
           const bool pair = !seen && x + 1 < kk.size();
           const RcCountTarget t1 = pair ? target(d_xk[x + 1], d_xv[x + 1], d_xslot[x + 1], slots2, kk[x + 1])
                                         : RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u};
-          hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P,
+          hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid2), dim3(256), 0, stream, P,
                              target(d_xk[x], d_xv[x], d_xslot[x], slots2, k2), t1, stride2, thr_t, seen, seen_mask,
                              cprobes);
           HIP_TRY(hipGetLastError());
