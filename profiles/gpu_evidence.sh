@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round evidence on one MI355X (run through gpurun from the repo root):
 #   bash profiles/gpu_evidence.sh TAG [what...]
-# what: tests smoke c3 c2 c5 kt pmc  (default: all). Outputs under gpurun_out/TAG/.
+# what: tests smoke c3 c3e2e c2 c4 c5 kt pmc c3t  (default: tests smoke c3 c2 c5 kt pmc). Outputs under gpurun_out/TAG/.
 # Every GPU step has its own time limit; the script stops at the first failing step.
 set -eo pipefail
 TAG=${1:?tag}
@@ -33,6 +33,10 @@ fi
 if has c2; then
   timeout -k 10 300 python bench.py --config c2 --no-cpu-baseline > "$OUT/bench_c2.json" 2> "$OUT/bench_c2.err"
   cat "$OUT/bench_c2.json"
+fi
+if has c4; then
+  timeout -k 10 300 python bench.py --config c4 --no-cpu-baseline > "$OUT/bench_c4.json" 2> "$OUT/bench_c4.err"
+  cat "$OUT/bench_c4.json"
 fi
 if has c5; then
   timeout -k 10 300 python bench.py --config c5 --gib 8 --steps 2 --no-cpu-baseline > "$OUT/bench_c5.json" 2> "$OUT/bench_c5.err"
