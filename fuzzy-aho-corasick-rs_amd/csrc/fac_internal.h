@@ -29,7 +29,7 @@ namespace fac {
 
 // ---------------------------------------------------------------- unicode.cpp
 uint32_t utf8_decode(const uint8_t* s, uint64_t n, uint64_t& i);
-bool utf8_valid(const uint8_t* s, uint64_t n);
+bool utf8_valid(const uint8_t* s, uint64_t n, bool* ascii = nullptr);  // ascii: also whether every byte < 0x80
 uint64_t utf8_valid_prefix(const uint8_t* s, uint64_t n);
 void segment_graphemes(const uint8_t* s, uint64_t n, std::vector<uint64_t>& starts);
 int lower_full(uint32_t cp, uint32_t out[3]);
@@ -471,6 +471,8 @@ int stream_feed(StreamCore& s, const uint8_t* data, uint64_t len, bool eof, std:
 void stream_close(StreamCore* s);
 uint64_t stream_committed(const StreamCore& s);  // commit point of the windows handed out so far
 int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err);
+// bit 0: invalid UTF-8, bit 1: not ASCII (validate_kernel over the device copy; synchronous)
+int validate_device(const uint8_t* d_utf8, uint64_t len, hipStream_t st, unsigned int& flags, std::string& err);
 void ensure_symbols(const Engine& e, const Haystack& h);
 int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,
                   std::string& err);

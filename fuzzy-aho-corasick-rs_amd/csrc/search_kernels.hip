@@ -3314,7 +3314,9 @@ int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack&
                    int force_ascii, hipStream_t stream) {
   h.device = e.device;
   h.len = len;
-  h.ascii = force_ascii < 0 ? ascii_only(utf8, len) : force_ascii != 0;
+  // force_ascii -2: the bytes are validated and classified on the device after the upload
+  const bool check_on_device = force_ascii == -2;
+  h.ascii = check_on_device ? false : force_ascii < 0 ? ascii_only(utf8, len) : force_ascii != 0;
   h.n = h.ascii ? len : 0;
   HIP_TRY(hipSetDevice(e.device));
   // All uploads go through one stream (the engine's, or the caller's) and are synchronized before
@@ -3323,6 +3325,16 @@ int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack&
   hipStream_t st = stream ? stream : e.stream;
   HIP_TRY(hipMalloc((void**)&h.d_utf8, std::max<uint64_t>(len, 16)));
   if (len) HIP_TRY(hipMemcpyAsync(h.d_utf8, utf8, len, hipMemcpyHostToDevice, st));
+  if (check_on_device) {
+    unsigned int f = 0;
+    if (int vrc = validate_device(h.d_utf8, len, st, f, err)) return vrc;
+    if (f & 1u) {
+      err = "haystack is not valid UTF-8";
+      return FAC_E_INVALID;
+    }
+    h.ascii = !(f & 2u);
+    h.n = h.ascii ? len : 0;
+  }
   if (!h.ascii) {  // UAX #29 segmentation + folding on the device (stage_kernels.hip)
     const int rc = stage_unicode_device(e, h, st, err);
     if (rc) return rc;

@@ -9,14 +9,12 @@
 // thread starts at the last such "resync" code point before its chunk (any letter, digit, space or
 // punctuation of ordinary text) and decides every boundary inside its chunk exactly. Text with no
 // resync point within 1 KiB before a chunk (long emoji / RI / combining runs) is segmented by one
-// sequential device thread instead. Grapheme starts are compacted with rocPRIM select.
+// sequential device thread instead. Grapheme starts are compacted per 16 KiB unit: one wave counts
+// each unit, one workgroup scans the counts, one wave writes each unit's starts in order.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstring>
-
-#include <rocprim/device/device_select.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "fac_internal.h"
 
@@ -206,13 +204,138 @@ __global__ void seg_hard_kernel(const uint8_t* s, uint64_t n, const uint8_t* har
   }
 }
 
-__global__ void count_kernel(const uint8_t* brk, uint64_t n, unsigned long long* total) {
-  unsigned long long local = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    local += brk[i];
-  // wave reduction, one atomic per wave
-  for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, 64);
-  if ((threadIdx.x & 63) == 0 && local) atomicAdd(total, local);
+// The C ABI's UTF-8 check (search_raw takes a &str, always valid) and search.rs:196's is_ascii, on
+// the device: unicode.cpp's utf8_valid_serial (Rust's str::from_utf8 acceptance: no overlongs,
+// surrogates or code points past U+10FFFF) per 256-byte chunk, over the segment from the chunk's first
+// byte that is not a continuation byte to the next chunk's -- every sequence then lies in one segment;
+// four continuation bytes in a row leave no start, and text must not begin with one. flags: bit 0
+// invalid, bit 1 some byte >= 0x80.
+__global__ __launch_bounds__(256) void validate_kernel(const uint8_t* s, uint64_t n, unsigned int* flags) {
+  const uint64_t c0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 256;
+  if (c0 >= n) return;
+  auto cont = [&](uint64_t p) { return (s[p] & 0xC0) == 0x80; };
+  auto seg_start = [&](uint64_t p, bool& bad) {  // first non-continuation byte at or after p
+    uint32_t k = 0;
+    while (p < n && cont(p) && k < 4) ++p, ++k;
+    bad = p < n && cont(p);
+    return p;
+  };
+  bool bad = false, bad2 = false;
+  uint64_t i = seg_start(c0, bad);
+  if (c0 == 0 && i != 0) bad = true;
+  const uint64_t e = c0 + 256 < n ? seg_start(c0 + 256, bad2) : n;
+  uint32_t hi = 0;
+  for (uint64_t p = c0; p < min(n, c0 + 256); ++p) hi |= s[p];
+  while (!bad && i < e) {
+    const uint8_t b = s[i];
+    if (b < 0x80) {
+      ++i;
+      continue;
+    }
+    uint32_t len, mn;
+    if ((b & 0xE0) == 0xC0) len = 2, mn = 0x80;
+    else if ((b & 0xF0) == 0xE0) len = 3, mn = 0x800;
+    else if ((b & 0xF8) == 0xF0) len = 4, mn = 0x10000;
+    else {
+      bad = true;
+      break;
+    }
+    if (i + len > e) {
+      bad = true;
+      break;
+    }
+    for (uint32_t k = 1; k < len; ++k)
+      if (!cont(i + k)) bad = true;
+    if (bad) break;
+    uint64_t j = i;
+    const uint32_t cp = decode(s, n, j);
+    if (cp < mn || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) bad = true;
+    i += len;
+  }
+  const unsigned f = (bad ? 1u : 0u) | ((hi & 0x80u) ? 2u : 0u);
+  if (f) atomicOr(flags, f);
+}
+
+// Grapheme-start compaction (brk bytes are 0/1): unit u = bytes [u * kUnit, (u + 1) * kUnit), one
+// wave each. unit_count_kernel counts, unit_scan_kernel (one workgroup) turns the counts into each
+// unit's first output slot and the total, unit_write_kernel writes the positions in order.
+constexpr uint32_t kUnit = 16384;
+__global__ __launch_bounds__(256) void unit_count_kernel(const uint8_t* brk, uint64_t n, uint32_t* ucnt, uint64_t n_units) {
+  const uint64_t u = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
+  const uint32_t lane = threadIdx.x & 63;
+  if (u >= n_units) return;  // whole waves
+  const uint64_t b = u * kUnit, e = min(n, b + (uint64_t)kUnit);
+  uint32_t c = 0;
+  if (e - b == kUnit) {  // 16-byte aligned (b is a multiple of kUnit, hipMalloc'd base)
+    const uint4* p = reinterpret_cast<const uint4*>(brk + b);
+    for (uint32_t i = lane; i < kUnit / 16; i += 64) {
+      const uint4 v = p[i];
+      c += __popc(v.x & 0x01010101u) + __popc(v.y & 0x01010101u) + __popc(v.z & 0x01010101u) + __popc(v.w & 0x01010101u);
+    }
+  } else {
+    for (uint64_t i = b + lane; i < e; i += 64) c += brk[i];
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+  if (lane == 0) ucnt[u] = c;
+}
+__global__ __launch_bounds__(1024) void unit_scan_kernel(const uint32_t* ucnt, uint64_t* ubase, uint64_t n_units,
+                                                         unsigned long long* total) {
+  __shared__ unsigned long long wsum[16];
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint64_t per = (n_units + 1023) / 1024;
+  const uint64_t a = min(n_units, (uint64_t)t * per), b = min(n_units, a + per);
+  unsigned long long sum = 0;
+  for (uint64_t i = a; i < b; ++i) sum += ucnt[i];
+  unsigned long long x = sum;  // inclusive scan over the wave
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  if (t == 0) {
+    unsigned long long run = 0;
+    for (int i = 0; i < 16; ++i) {
+      const unsigned long long v = wsum[i];
+      wsum[i] = run;
+      run += v;
+    }
+    *total = run;
+  }
+  __syncthreads();
+  unsigned long long run = wsum[w] + x - sum;
+  for (uint64_t i = a; i < b; ++i) {
+    ubase[i] = run;
+    run += ucnt[i];
+  }
+}
+__global__ __launch_bounds__(256) void unit_write_kernel(const uint8_t* brk, uint64_t n, const uint64_t* ubase, uint64_t n_units,
+                                                         uint64_t* off) {
+  const uint64_t u = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
+  const uint32_t lane = threadIdx.x & 63;
+  if (u >= n_units) return;  // whole waves
+  uint64_t base = ubase[u];
+  const uint64_t b = u * kUnit, e = min(n, b + (uint64_t)kUnit);
+  for (uint64_t p0 = b; p0 < e; p0 += 256) {  // four flags per lane, in byte order across the wave
+    const uint64_t p = p0 + 4ull * lane;
+    uint32_t f = 0;
+    if (p + 4 <= e) {
+      f = *reinterpret_cast<const uint32_t*>(brk + p) & 0x01010101u;
+    } else {
+      for (uint32_t k = 0; k < 4; ++k)
+        if (p + k < e && brk[p + k]) f |= 1u << (8 * k);
+    }
+    const uint32_t c = __popc(f);
+    uint32_t x = c;  // inclusive scan of the lanes' counts
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    uint64_t o = base + x - c;
+    for (uint32_t k = 0; k < 4; ++k)
+      if ((f >> (8 * k)) & 1u) off[o++] = p + k;
+    base += __shfl(x, 63, 64);
+  }
 }
 
 __device__ uint32_t lower_first(uint32_t cp) {  // unicode.cpp lower_full, first code point
@@ -247,6 +370,28 @@ __global__ void fold_kernel(const uint8_t* s, uint64_t len, const uint64_t* off,
     }                                                     \
   } while (0)
 
+// flags of validate_kernel over the device copy of a haystack (synchronous): bit 0 invalid UTF-8,
+// bit 1 not ASCII
+int validate_device(const uint8_t* d_utf8, uint64_t len, hipStream_t st, unsigned int& flags_out, std::string& err) {
+  flags_out = 0;
+  if (!len) return FAC_OK;
+  unsigned int* flags = nullptr;
+  ST_TRY(hipMalloc((void**)&flags, 4));
+  struct Free {
+    void* p;
+    ~Free() {
+      if (p) (void)hipFree(p);
+    }
+  } f_flags{flags};
+  ST_TRY(hipMemsetAsync(flags, 0, 4, st));
+  const uint64_t chunks = (len + 255) / 256;
+  hipLaunchKernelGGL(validate_kernel, dim3((uint32_t)((chunks + 255) / 256)), dim3(256), 0, st, d_utf8, len, flags);
+  ST_TRY(hipGetLastError());
+  ST_TRY(hipMemcpyAsync(&flags_out, flags, 4, hipMemcpyDeviceToHost, st));
+  ST_TRY(hipStreamSynchronize(st));
+  return FAC_OK;
+}
+
 // Device staging of a valid, non-ASCII UTF-8 haystack already resident at h.d_utf8: fills
 // h.n, h.d_off (grapheme byte starts), h.d_text32 (folded first code points) and the host copy of
 // the starts (fetched to the host only on demand: ensure_host).
@@ -280,8 +425,19 @@ int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::stri
     hipLaunchKernelGGL(seg_hard_kernel, dim3(1), dim3(64), 0, st, h.d_utf8, len, hard, chunks, brk);
     ST_TRY(hipGetLastError());
   }
-  hipLaunchKernelGGL(count_kernel, dim3(2048), dim3(256), 0, st, brk, len, scal + 1);
-  ST_TRY(hipGetLastError());
+  const uint64_t n_units = (len + kUnit - 1) / kUnit;
+  uint32_t* ucnt = nullptr;
+  uint64_t* ubase = nullptr;
+  ST_TRY(hipMalloc((void**)&ucnt, std::max<uint64_t>(n_units, 1) * 4));
+  Free f_ucnt{ucnt};
+  ST_TRY(hipMalloc((void**)&ubase, std::max<uint64_t>(n_units, 1) * 8));
+  Free f_ubase{ubase};
+  const uint32_t ugrid = (uint32_t)((n_units + 3) / 4);
+  if (n_units) {
+    hipLaunchKernelGGL(unit_count_kernel, dim3(ugrid), dim3(256), 0, st, brk, len, ucnt, n_units);
+    hipLaunchKernelGGL(unit_scan_kernel, dim3(1), dim3(1024), 0, st, ucnt, ubase, n_units, scal + 1);
+    ST_TRY(hipGetLastError());
+  }
   ST_TRY(hipMemcpyAsync(scal_h + 1, scal + 1, 8, hipMemcpyDeviceToHost, st));
   ST_TRY(hipStreamSynchronize(st));
   h.n = scal_h[1];
@@ -290,15 +446,9 @@ int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::stri
   // at j == n of an open-ended shard reads it before the halo check flags the window)
   ST_TRY(hipMalloc((void**)&h.d_off, (h.n + 1) * 8));
   ST_TRY(hipMemcpyAsync(h.d_off + h.n, &h.len, 8, hipMemcpyHostToDevice, st));
-  {
-    size_t bytes = 0;
-    rocprim::counting_iterator<uint64_t> idx(0);
-    ST_TRY(rocprim::select(nullptr, bytes, idx, brk, h.d_off, scal + 1, len, st));
-    void* tmp = nullptr;
-    ST_TRY(hipMalloc(&tmp, std::max<size_t>(bytes, 16)));
-    Free f_tmp{tmp};
-    ST_TRY(rocprim::select(tmp, bytes, idx, brk, h.d_off, scal + 1, len, st));
-    ST_TRY(hipStreamSynchronize(st));
+  if (n_units) {
+    hipLaunchKernelGGL(unit_write_kernel, dim3(ugrid), dim3(256), 0, st, brk, len, ubase, n_units, h.d_off);
+    ST_TRY(hipGetLastError());
   }
   ST_TRY(hipMalloc((void**)&h.d_text32, std::max<uint64_t>(h.n * 4, 16)));
   if (h.n) {

@@ -155,10 +155,14 @@ bool utf8_valid_serial(const uint8_t* s, uint64_t n) {
 // Large inputs are validated in up to 16 pieces on host threads, cut in front of a byte that is
 // not a continuation byte: every sequence then lies inside one piece (a sequence truncated by a
 // cut is invalid anyway, and so is a run of four continuation bytes that leaves no cut point).
-bool utf8_valid(const uint8_t* s, uint64_t n) {
+bool utf8_valid(const uint8_t* s, uint64_t n, bool* ascii) {
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const uint64_t T = std::min<uint64_t>(std::min<uint64_t>(16, hw), n >> 22);  // >= 4 MiB a piece
-  if (T <= 1) return utf8_valid_serial(s, n);
+  if (T <= 1) {
+    const bool v = utf8_valid_serial(s, n);
+    if (ascii) *ascii = v && ascii_only(s, n);
+    return v;
+  }
   std::vector<uint64_t> cut(T + 1);
   cut[0] = 0;
   cut[T] = n;
@@ -167,12 +171,18 @@ bool utf8_valid(const uint8_t* s, uint64_t n) {
     for (int k = 0; k < 4 && p < n && (s[p] & 0xC0) == 0x80; ++k) ++p;
     cut[t] = std::max(cut[t - 1], p);
   }
-  std::vector<char> ok(T, 1);
+  std::vector<char> ok(T, 1), asc(T, 1);
   std::vector<std::thread> th;
   for (uint64_t t = 0; t < T; ++t)
-    th.emplace_back([&, t] { ok[t] = utf8_valid_serial(s + cut[t], cut[t + 1] - cut[t]) ? 1 : 0; });
+    th.emplace_back([&, t] {
+      ok[t] = utf8_valid_serial(s + cut[t], cut[t + 1] - cut[t]) ? 1 : 0;
+      // the ASCII check of search.rs:196 on the same piece (early exit at the first non-ASCII 4 KiB)
+      if (ascii && ok[t]) asc[t] = ascii_only(s + cut[t], cut[t + 1] - cut[t]) ? 1 : 0;
+    });
   for (auto& x : th) x.join();
-  return std::all_of(ok.begin(), ok.end(), [](char v) { return v != 0; });
+  const bool v = std::all_of(ok.begin(), ok.end(), [](char c) { return c != 0; });
+  if (ascii) *ascii = v && std::all_of(asc.begin(), asc.end(), [](char c) { return c != 0; });
+  return v;
 }
 
 // UAX #29 extended grapheme cluster boundaries (rules GB3-GB13, GB999, with GB9c InCB).

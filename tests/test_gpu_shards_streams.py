@@ -218,3 +218,56 @@ def test_stream_many_windows_in_order():
     truth = [(m.start, m.end) for m in eng.search(text, O().threshold(0.8).sorted().non_overlapping())]
     got = [(m.start, m.end) for m in eng.stream_matches(io.BytesIO(text.encode()), 0.8, window=512)]
     assert got == truth and len(got) == 1600
+
+
+@pytest.mark.gpu
+def test_device_utf8_check_matches_python():
+    """fac_haystack_stage checks the bytes on the device (validate_kernel: per 256-byte chunk, from its
+    first non-continuation byte) and decides search.rs:196's is_ascii there: accepted exactly when
+    Python's strict decoder (like Rust's str::from_utf8: no overlongs, surrogates, > U+10FFFF,
+    truncations or stray continuation bytes) accepts, with invalid sequences planted at and around
+    the chunk boundaries; accepted haystacks search like the oracle."""
+    import random
+    from fuzzy_aho_corasick import DeviceError
+    from fuzzy_aho_corasick._native import FAC_E_INVALID
+    rng = random.Random(0x0757)
+    eng = B().fuzzy(L().edits(1)).device(0).build(["héllo", "wörld", "ab"])
+    bad = [b"\x80", b"\xbf\xbf", b"\xc0\x80", b"\xc1\xbf", b"\xe0\x80\x80", b"\xed\xa0\x80", b"\xf0\x80\x80\x80",
+           b"\xf4\x90\x80\x80", b"\xf8\x88\x80\x80\x80", b"\xff", b"\xc3", b"\xe2\x82", b"\xf0\x9f\x98",
+           b"\x80\x80\x80\x80\x80", b"\xc3\xa9\x80"]
+    cps = [0x41, 0x7A, 0x20, 0xE9, 0x3B1, 0x20AC, 0x4E2D, 0xFFFD, 0x1F600, 0x10FFFF, 0xD7FF, 0xE000]
+
+    def text(nbytes):
+        out = bytearray()
+        while len(out) < nbytes:
+            out += chr(rng.choice(cps)).encode("utf-8")
+        return bytes(out)
+
+    checked = 0
+    for trial in range(120):
+        base = text(rng.choice([40, 255, 256, 300, 700, 1500, 5000]))
+        data = base
+        if trial % 4:  # plant an invalid (or, cut mid-sequence, sometimes valid) piece
+            piece = rng.choice(bad)
+            at = rng.choice([0, 1, 255, 256, 257, 511, 512, len(base) - 1, len(base), rng.randrange(len(base) + 1)])
+            at = max(0, min(len(base), at))
+            data = base[:at] + piece + base[at:]
+        try:
+            data.decode("utf-8")
+            ok = True
+        except UnicodeDecodeError:
+            ok = False
+        if ok:
+            st = StagedHaystack(eng, data)
+            assert st.graphemes == len(data.decode("utf-8")) or not data.isascii(), trial
+            checked += 1
+        else:
+            with pytest.raises(DeviceError) as ei:
+                StagedHaystack(eng, data)
+            assert ei.value.code == FAC_E_INVALID, trial
+    assert checked >= 30
+    for hay in ("plain ascii héllo wörld " * 40, "ascii only hello world ab " * 20):
+        want = sorted((m.start, m.end, m.pattern_index) for m in OracleEngine(
+            B().fuzzy(L().edits(1)), ["héllo", "wörld", "ab"]).search_raw(hay, 0.8))
+        got = sorted((m.start, m.end, m.pattern_index) for m in eng.search_raw(hay, 0.8))
+        assert len(got) > 0 and got == want
