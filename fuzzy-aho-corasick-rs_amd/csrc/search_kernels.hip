@@ -2895,9 +2895,12 @@ __device__ __forceinline__ uint32_t qgram_find(const QgramParams& Q, uint32_t ke
 constexpr uint32_t QG_BUF = 512;
 // A 64 Kbit LDS bitmap of the grams' hashes (bit = hash >> 16) screens every position first: only
 // the ~3 % that pass (C5) probe the table in global memory.
+constexpr uint32_t QG_PQ = 128;  // per-wave probe queue (LDS)
 __global__ __launch_bounds__(256) void qgram_scan_kernel(QgramParams Q) {
   __shared__ unsigned long long s_buf[4][QG_BUF];
   __shared__ uint32_t s_bits[2048];
+  __shared__ uint32_t s_pk[4][QG_PQ];
+  __shared__ uint64_t s_pp[4][QG_PQ];
   for (uint32_t x = threadIdx.x; x < 2048; x += blockDim.x) s_bits[x] = 0u;
   __syncthreads();
   for (uint32_t x = threadIdx.x; x <= Q.tab_mask; x += blockDim.x) {
@@ -2921,50 +2924,75 @@ __global__ __launch_bounds__(256) void qgram_scan_kernel(QgramParams Q) {
     __builtin_amdgcn_wave_barrier();
     nb = 0;
   };
+  // Positions whose gram passes the bitmap are queued per wave in LDS and probed 64 at a time, one
+  // per lane: probing each of a thread's 8 grams where it stands cost 8 dependent table round trips
+  // per wave step (some lane of 64 passes almost every one), the scan's whole time.
+  uint32_t* pk = s_pk[threadIdx.x / 64];
+  uint64_t* pp = s_pp[threadIdx.x / 64];
+  uint32_t nq = 0;  // wave-uniform
+  auto drain = [&](bool all) {
+    while (nq >= 64 || (all && nq > 0)) {
+      const uint32_t take = min(nq, 64u), lane = lane_id();
+      uint32_t h = 0;
+      uint64_t pos = 0;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < take) {
+        pos = pp[nq - take + lane];
+        h = qgram_find(Q, pk[nq - take + lane]);
+      }
+      __builtin_amdgcn_wave_barrier();
+      nq -= take;
+      const uint32_t cnt = h & 0xFFu;
+      if (!__ballot(cnt)) continue;
+      const uint32_t incl = wave_inclusive_sum(cnt), tot = shfl_u32(incl, 63);
+      unsigned long long* dst;
+      uint64_t at;
+      if (tot > QG_BUF) {  // grams shared by many patterns: straight to the list
+        unsigned long long b0 = 0;
+        if (lane == 63) b0 = atomicAdd(Q.n_cand, (unsigned long long)tot);
+        dst = Q.cand;
+        at = shfl_u64(b0, 63) + (incl - cnt);
+      } else {
+        if (nb + tot > QG_BUF) flush();
+        dst = buf;
+        at = nb + incl - cnt;
+        nb += tot;
+      }
+      for (uint32_t y = 0; y < cnt; ++y, ++at)
+        if (dst != Q.cand || at < Q.cap) dst[at] = (pos << 24) | ((h >> 8) + y);
+    }
+  };
+  auto push = [&](bool pass, uint32_t key, uint64_t pos) {  // wave-uniform call
+    const uint64_t m = __ballot(pass);
+    if (!m) return;
+    if (nq + 64 > QG_PQ) drain(false);
+    if (pass) {
+      const uint32_t at = nq + prefix_below(m);
+      pk[at] = key;
+      pp[at] = pos;
+    }
+    nq += (uint32_t)__popcll(m);
+  };
   // a thread takes 4 consecutive positions from two aligned words of symbols (the ids buffer is
   // padded past n; positions whose gram would cross n are not looked up)
   const uint32_t* ids32 = reinterpret_cast<const uint32_t*>(Q.ids);
-  const uint64_t nq = (Q.n + 3) / 4;  // position quads
+  const uint64_t nq4 = (Q.n + 3) / 4;  // position quads
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t base0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (uint64_t g0 = base0 - threadIdx.x % 64; g0 < nq; g0 += stride) {  // whole waves iterate together
+  for (uint64_t g0 = base0 - threadIdx.x % 64; g0 < nq4; g0 += stride) {  // whole waves iterate together
     const uint64_t g = g0 + (threadIdx.x % 64);
-    uint32_t h[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // [2 j]: 4-gram at 4 g + j, [2 j + 1]: 3-gram
-    if (g < nq) {
-      const uint64_t w = ((uint64_t)ids32[g + 1] << 32) | ids32[g];
+    const uint64_t w = g < nq4 ? (((uint64_t)ids32[g + 1] << 32) | ids32[g]) : 0ull;
 #pragma unroll
-      for (uint32_t j = 0; j < 4; ++j) {
-        const uint64_t i = 4 * g + j;
-        const uint32_t a = (uint32_t)(w >> (8 * j)) & 0xFFu, b = (uint32_t)(w >> (8 * j + 8)) & 0xFFu;
-        const uint32_t c = (uint32_t)(w >> (8 * j + 16)) & 0xFFu, d = (uint32_t)(w >> (8 * j + 24)) & 0xFFu;
-        const uint32_t k4 = qgram_key(a, b, c, d, true), k3 = qgram_key(a, b, c, 0u, false);
-        if (Q.use4 && i + 4 <= Q.n && maybe(k4)) h[2 * j] = qgram_find(Q, k4);
-        if (Q.use3 && i + 3 <= Q.n && maybe(k3)) h[2 * j + 1] = qgram_find(Q, k3);
-      }
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint64_t i = 4 * g + j;
+      const uint32_t a = (uint32_t)(w >> (8 * j)) & 0xFFu, b = (uint32_t)(w >> (8 * j + 8)) & 0xFFu;
+      const uint32_t c = (uint32_t)(w >> (8 * j + 16)) & 0xFFu, d = (uint32_t)(w >> (8 * j + 24)) & 0xFFu;
+      const uint32_t k4 = qgram_key(a, b, c, d, true), k3 = qgram_key(a, b, c, 0u, false);
+      push(g < nq4 && Q.use4 && i + 4 <= Q.n && maybe(k4), k4, i);
+      push(g < nq4 && Q.use3 && i + 3 <= Q.n && maybe(k3), k3, i);
     }
-    uint32_t cnt = 0;
-#pragma unroll
-    for (uint32_t x = 0; x < 8; ++x) cnt += h[x] & 0xFFu;
-    if (!__ballot(cnt)) continue;
-    const uint32_t incl = wave_inclusive_sum(cnt), tot = shfl_u32(incl, 63);
-    unsigned long long* dst;
-    uint64_t at;
-    if (tot > QG_BUF) {  // grams shared by many patterns: straight to the list
-      unsigned long long b0 = 0;
-      if (lane_id() == 63) b0 = atomicAdd(Q.n_cand, (unsigned long long)tot);
-      dst = Q.cand;
-      at = shfl_u64(b0, 63) + (incl - cnt);
-    } else {
-      if (nb + tot > QG_BUF) flush();
-      dst = buf;
-      at = nb + incl - cnt;
-      nb += tot;
-    }
-#pragma unroll
-    for (uint32_t x = 0; x < 8; ++x)
-      for (uint32_t y = 0; y < (h[x] & 0xFFu); ++y, ++at)
-        if (dst != Q.cand || at < Q.cap) dst[at] = ((4 * g + x / 2) << 24) | ((h[x] >> 8) + y);
   }
+  drain(true);
   if (nb) flush();
 }
 
