@@ -206,12 +206,14 @@ __global__ void seg_hard_kernel(const uint8_t* s, uint64_t n, const uint8_t* har
 
 // The C ABI's UTF-8 check (search_raw takes a &str, always valid) and search.rs:196's is_ascii, on
 // the device: unicode.cpp's utf8_valid_serial (Rust's str::from_utf8 acceptance: no overlongs,
-// surrogates or code points past U+10FFFF) per 256-byte chunk, over the segment from the chunk's first
+// surrogates or code points past U+10FFFF) per 16-byte chunk, over the segment from the chunk's first
 // byte that is not a continuation byte to the next chunk's -- every sequence then lies in one segment;
 // four continuation bytes in a row leave no start, and text must not begin with one. flags: bit 0
-// invalid, bit 1 some byte >= 0x80.
+// invalid, bit 1 some byte >= 0x80. 16-byte chunks keep a wave's reads inside 1 KiB (256-byte ones
+// spread each byte load over 128 lines: 48 GB fetched for 256 MiB).
+constexpr uint32_t kValChunk = 16;
 __global__ __launch_bounds__(256) void validate_kernel(const uint8_t* s, uint64_t n, unsigned int* flags) {
-  const uint64_t c0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 256;
+  const uint64_t c0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kValChunk;
   if (c0 >= n) return;
   auto cont = [&](uint64_t p) { return (s[p] & 0xC0) == 0x80; };
   auto seg_start = [&](uint64_t p, bool& bad) {  // first non-continuation byte at or after p
@@ -223,9 +225,9 @@ __global__ __launch_bounds__(256) void validate_kernel(const uint8_t* s, uint64_
   bool bad = false, bad2 = false;
   uint64_t i = seg_start(c0, bad);
   if (c0 == 0 && i != 0) bad = true;
-  const uint64_t e = c0 + 256 < n ? seg_start(c0 + 256, bad2) : n;
+  const uint64_t e = c0 + kValChunk < n ? seg_start(c0 + kValChunk, bad2) : n;
   uint32_t hi = 0;
-  for (uint64_t p = c0; p < min(n, c0 + 256); ++p) hi |= s[p];
+  for (uint64_t p = c0; p < min(n, c0 + kValChunk); ++p) hi |= s[p];
   while (!bad && i < e) {
     const uint8_t b = s[i];
     if (b < 0x80) {
@@ -384,7 +386,7 @@ int validate_device(const uint8_t* d_utf8, uint64_t len, hipStream_t st, unsigne
     }
   } f_flags{flags};
   ST_TRY(hipMemsetAsync(flags, 0, 4, st));
-  const uint64_t chunks = (len + 255) / 256;
+  const uint64_t chunks = (len + kValChunk - 1) / kValChunk;
   hipLaunchKernelGGL(validate_kernel, dim3((uint32_t)((chunks + 255) / 256)), dim3(256), 0, st, d_utf8, len, flags);
   ST_TRY(hipGetLastError());
   ST_TRY(hipMemcpyAsync(&flags_out, flags, 4, hipMemcpyDeviceToHost, st));

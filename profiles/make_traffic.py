@@ -24,8 +24,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
 # kernels that run once per staged haystack (before the timed loop), not per step
-STAGING = ("seg_chunk_kernel", "seg_hard_kernel", "unit_count_kernel", "unit_scan_kernel", "unit_write_kernel", "fold_kernel",
-           "transcode_ascii_kernel")
+STAGING = ("validate_kernel", "seg_chunk_kernel", "seg_hard_kernel", "unit_count_kernel", "unit_scan_kernel",
+           "unit_write_kernel", "fold_kernel", "transcode_ascii_kernel")
 
 
 def is_staging(name):
