@@ -3728,6 +3728,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       return RcCountTarget{static_cast<unsigned long long*>(keys.p), static_cast<uint32_t*>(cnt.p),
                            static_cast<uint64_t*>(rep.p), n_slots - 1, k};
     };
+    // Level-1 keys are counted on every stride1-th window, about 32 M windows in all (a power of two,
+    // at most 16): a key that only unsampled windows hold stays uncached, and its windows resume from
+    // level 0 (the prefixes of the sampled keys; the lookups reach it last) or from the root. Measured
+    // per step against counting every window: C3 (stride 4; 0.3 M windows fall back) 92.4 -> 89.8 ms,
+    // C2 1 GiB (stride 16) 105.5 -> 88.7 ms; strides 8 / 16 on C3 gave 90.0 / 93.3 ms.
+    uint32_t stride1 = 1;
+    while (stride1 < 16 && windows / (2ull * stride1) >= (1ull << 25)) stride1 *= 2;
+    stride1 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_STRIDE1", stride1));
     for (uint32_t k = kpin ? kpin : 4u; k >= (kpin ? kpin : 2u); --k) {
       P.rc_k = k;
       HIP_TRY(hipMemsetAsync(d_rck.p, 0, slots * sizeof(unsigned long long), stream));
@@ -3745,13 +3753,13 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         L0.k = k0;
       }
       hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P, target(d_rck, d_rcv, d_rcslot, slots, k),
-                         RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u}, 1u, 1u, nullptr, 0u, cprobes);
+                         RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u}, stride1, 1u, nullptr, 0u, cprobes);
       HIP_TRY(hipGetLastError());
       unsigned int n_keys = 0;
       if (int nrc = number_entries(d_rck, d_rcv, d_rcslot, d_rcrep, slots, 1u, max_ent, n_keys)) return nrc;
       l1_keys = n_keys;
       if (n_keys == 0) break;
-      if (!kpin && 8ull * n_keys > windows) continue;  // too little reuse: fewer chars per key
+      if (!kpin && 8ull * n_keys > (windows + stride1 - 1) / stride1) continue;  // too little reuse: fewer chars per key
       n_ent1 = std::min(n_keys, max_ent);
       L1.k = k;
       if (l0) {  // level-0 keys from the level-1 representatives
@@ -4008,9 +4016,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         tabs.push_back(Lx[x]);
         tab_exact.push_back(!live_builds);
       }
-      P.rc_ntab = 0;  // level 0 only feeds the level-1 build: every window holds a level-1 key
-      for (size_t t = tabs.size(); t-- > 0;)
-        if (!(n_ent0 && tabs[t].k == L0.k)) P.rc_tab[P.rc_ntab++] = tabs[t];
+      // the lookups probe deepest first and stop at the first hit: level 0 is reached only by the
+      // windows whose level-1 key the sampled count missed
+      P.rc_ntab = 0;
+      for (size_t t = tabs.size(); t-- > 0;) P.rc_tab[P.rc_ntab++] = tabs[t];
       P.rc_mode = 1;
       n_exact_tabs = 0;
       for (size_t t = tabs.size(); t-- > 0;)
