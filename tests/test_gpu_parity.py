@@ -383,6 +383,26 @@ def test_prefix_cache_default_on_c3_slice(monkeypatch):
     _staged_vs_oracle(workloads.builder_for(w), w.patterns, hay, w.threshold)
 
 
+@pytest.mark.parametrize("stride", ["4", "16"])
+def test_prefix_cache_sampled_level1(stride, monkeypatch):
+    """Level-1 keys counted on every stride-th window (the default from 64 M windows): windows whose
+    key the sample missed resume from level 0 or the root; records == every window counted == the
+    cache off, on C3- and C2-shaped slices (forced on here with FAC_RC_STRIDE1)."""
+    from fuzzy_aho_corasick import workloads
+    for cfg, mib in (("c3", 2), ("c2", 4)):
+        w = workloads.config(cfg, mib << 20, 3)
+        staged = workloads.builder_for(w).build(w.patterns).stage(w.haystack)
+        monkeypatch.setenv("FAC_RC_STRIDE1", stride)
+        sampled, st = staged.search_windows_records(w.threshold)
+        monkeypatch.setenv("FAC_RC_STRIDE1", "1")
+        full, _ = staged.search_windows_records(w.threshold)
+        monkeypatch.setenv("FAC_NO_RC", "1")
+        off, _ = staged.search_windows_records(w.threshold)
+        monkeypatch.delenv("FAC_NO_RC")
+        assert st.states_cached > 0, cfg
+        assert len(sampled) > 0 and sorted(sampled.tolist()) == sorted(full.tolist()) == sorted(off.tolist()), cfg
+
+
 @pytest.mark.parametrize("pops", ["1", "4", "32"])
 def test_lane_serial_windows(pops, monkeypatch):
     """lane_window_kernel (small unfinished windows resumed from their snapshots, one lane each, no
