@@ -3942,13 +3942,21 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       tab_exact.push_back(true);
       return FAC_OK;
     };
-    const uint32_t stride2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_STRIDE2", 2));
+    // Sampled levels: every 2nd window's key, kept when seen twice. With a single sampled level
+    // (one-edit engines, whose windows mostly end within 5 chars) about 32 M windows are sampled
+    // (stride a power of two, at most 32) and every sampled key is kept: C2 1 GiB 88.8 -> 71.0 ms,
+    // C4 18.9 -> 17.6 ms per step with the same lane / wave work (the keys that matter are frequent).
+    // Two levels (C3) stay at 2 / 2: strides 3 / 4 or threshold 1 measured slower.
+    uint32_t s2 = 2;
+    if (ks.size() == 1)
+      while (s2 < 32 && windows / (2ull * s2) >= (1ull << 25)) s2 *= 2;
+    const uint32_t stride2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_STRIDE2", s2));
     // the sampled levels' counts run beside the level-0/1 builds and have slack until the level-1
     // build ends: fewer workgroups leave the builds more of the CUs. Measured: two sampled levels
     // (C3) 2 per CU (-2 ms against 8), one level (C2, whose builds are shorter) 4 per CU (-2 ms)
     const uint32_t cgrid2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256,
         (uint64_t)cus * env_u("FAC_RC_CGRID2", ks.size() >= 2 ? 2 : 4)));
-    const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", 2));
+    const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", s2 > 2 ? 1 : 2));
     std::vector<RcTable> Lx;        // sampled levels, ascending k
     std::vector<uint32_t> n_entx;   // their entries
     std::vector<size_t> xbuf;       // their count-table buffers

@@ -387,13 +387,20 @@ def test_prefix_cache_default_on_c3_slice(monkeypatch):
 def test_prefix_cache_sampled_level1(stride, monkeypatch):
     """Level-1 keys counted on every stride-th window (the default from 64 M windows): windows whose
     key the sample missed resume from level 0 or the root; records == every window counted == the
-    cache off, on C3- and C2-shaped slices (forced on here with FAC_RC_STRIDE1)."""
+    cache off, on C3- and C2-shaped slices (forced on here with FAC_RC_STRIDE1). The C2 slice also
+    samples its single 5-char level sparsely and keeps every sampled key (FAC_RC_STRIDE2, T2 = 1: the
+    one-level default from 128 M windows)."""
     from fuzzy_aho_corasick import workloads
     for cfg, mib in (("c3", 2), ("c2", 4)):
         w = workloads.config(cfg, mib << 20, 3)
         staged = workloads.builder_for(w).build(w.patterns).stage(w.haystack)
         monkeypatch.setenv("FAC_RC_STRIDE1", stride)
+        if cfg == "c2":
+            monkeypatch.setenv("FAC_RC_STRIDE2", stride)
+            monkeypatch.setenv("FAC_RC_T2", "1")
         sampled, st = staged.search_windows_records(w.threshold)
+        for k in ("FAC_RC_STRIDE2", "FAC_RC_T2"):
+            monkeypatch.delenv(k, raising=False)
         monkeypatch.setenv("FAC_RC_STRIDE1", "1")
         full, _ = staged.search_windows_records(w.threshold)
         monkeypatch.setenv("FAC_NO_RC", "1")
