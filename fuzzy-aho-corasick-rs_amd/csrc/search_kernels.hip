@@ -3943,13 +3943,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       return FAC_OK;
     };
     // Sampled levels: every 2nd window's key, kept when seen twice. With a single sampled level
-    // (one-edit engines, whose windows mostly end within 5 chars) about 32 M windows are sampled
+    // (one-edit engines, whose windows mostly end within 5 chars) about 8-16 M windows are sampled
     // (stride a power of two, at most 32) and every sampled key is kept: C2 1 GiB 88.8 -> 71.0 ms,
-    // C4 18.9 -> 17.6 ms per step with the same lane / wave work (the keys that matter are frequent).
+    // C4 18.9 -> 17.6 ms per step with the same lane / wave work (the keys that matter are frequent);
+    // C4 at stride 16 (8 M samples) against 4 (32 M): 17.7 -> 16.6 ms, C2 at stride 64: no change.
     // Two levels (C3) stay at 2 / 2: strides 3 / 4 or threshold 1 measured slower.
     uint32_t s2 = 2;
     if (ks.size() == 1)
-      while (s2 < 32 && windows / (2ull * s2) >= (1ull << 25)) s2 *= 2;
+      while (s2 < 32 && windows / (2ull * s2) >= (1ull << 23)) s2 *= 2;
     const uint32_t stride2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_STRIDE2", s2));
     // the sampled levels' counts run beside the level-0/1 builds and have slack until the level-1
     // build ends: fewer workgroups leave the builds more of the CUs. Measured: two sampled levels
