@@ -54,8 +54,12 @@ def parse():
     ap.add_argument("--mib", type=float, default=None, help="haystack MiB per rank (c5: block MiB)")
     ap.add_argument("--shard", action="store_true", help="strong scaling: shard one haystack over the ranks")
     ap.add_argument("--end-to-end", action="store_true",
-                    help="time search_raw end to end: host bytes -> staging (UTF-8 check, H2D, segmentation) -> records")
+                    help="time search_raw from host bytes: staging (H2D, UTF-8 check, segmentation) -> records")
+    ap.add_argument("--prestaged", action="store_true",
+                    help="diagnostic: stage the haystack once before the timed steps (search only)")
     ap.add_argument("--gib", type=float, default=100.0, help="c5: total stream GiB (each GPU takes 1/8)")
+    ap.add_argument("--vocab", type=int, default=50_000,
+                    help="filler words drawn from a fixed vocabulary of this many random words; 0: fresh random words")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="single-thread CPU baseline sample budget")
     ap.add_argument("--cpu-threads", type=int, default=16, help="all-cores CPU baseline threads (box share: 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -115,33 +119,55 @@ def main():
 
     mib = args.mib if args.mib is not None else DEFAULT_MIB[args.config]
     nbytes = int(mib * (1 << 20))
+    vocab = args.vocab or None
     if args.config == "c4":  # C2 engine, haystack seeds 40..47
-        wl = W.config("c4", nbytes, hay_seed=40 + (0 if args.shard else rank))
+        wl = W.config("c4", nbytes, hay_seed=40 + (0 if args.shard else rank), vocab=vocab)
     else:
         base_seed = {"c1": 1, "c2": 2, "c3": 3}[args.config]
         # weak scaling: every rank builds the same engine and owns a different haystack of equal size
         wl = W.config(args.config, nbytes, seed=base_seed,
-                      hay_seed=base_seed + 1000 + (0 if args.shard else 101 * rank))
+                      hay_seed=base_seed + 1000 + (0 if args.shard else 101 * rank), vocab=vocab)
     engine = W.builder_for(wl).device(local).build(wl.patterns)
-    if args.shard:
+    stream = torch.cuda.current_stream().cuda_stream
+    # default step = search_raw on device-resident input: the UTF-8 bytes are uploaded
+    # once (H2D reported apart); every step stages them on the device (UTF-8 check, is_ascii, UAX #29
+    # segmentation + folding: fac_haystack_stage_device), searches every start window and delivers
+    # the records. --prestaged (diagnostic) stages once outside the timed steps; --shard stages each
+    # rank's halo-sliced shard once from the host.
+    device_staging = not (args.shard or args.prestaged or args.end_to_end)
+    dev_hay, h2d_ms = None, None
+    if device_staging:
+        import numpy as np
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        dev_hay = torch.from_numpy(np.frombuffer(wl.haystack, dtype=np.uint8)).to(torch.device("cuda", local))
+        torch.cuda.synchronize()
+        h2d_ms = (time.perf_counter() - t) * 1e3
+        staged = StagedHaystack.from_device(engine, dev_hay.data_ptr(), len(wl.haystack), stream)
+    elif args.shard:
         staged = StagedHaystack.shard(engine, wl.haystack, world, rank)
     else:
         staged = StagedHaystack(engine, wl.haystack)
     windows = staged.owned_windows  # graphemes this rank searches per step
-    stream = torch.cuda.current_stream().cuda_stream
     host_buf = [None]  # rank 0: pinned landing buffer of the gathered records
+    stage_ms = [0.0]
 
     def step():
-        if args.end_to_end:  # search_raw: staging (UTF-8 check, H2D, segmentation + fold) + search
+        if args.end_to_end:  # search_raw from host bytes: staging (H2D, UTF-8 check, segmentation + fold) + search
             hs = StagedHaystack(engine, wl.haystack)
             rows, st = hs.search_windows_records(wl.threshold, stream=stream)
             del hs
             return len(rows), st
+        hs = staged
+        if device_staging:  # synchronous: its kernels are done on return
+            t = time.perf_counter()
+            hs = StagedHaystack.from_device(engine, dev_hay.data_ptr(), len(wl.haystack), stream, reuse=staged)
+            stage_ms[0] += (time.perf_counter() - t) * 1e3
         if world == 1:  # records D2H into the library's pooled pinned buffers
-            rows, st = (staged.search_prefiltered_records(wl.threshold, stream=stream) if wl.prefilter
-                        else staged.search_windows_records(wl.threshold, stream=stream))
+            rows, st = (hs.search_prefiltered_records(wl.threshold, stream=stream) if wl.prefilter
+                        else hs.search_windows_records(wl.threshold, stream=stream))
             return len(rows), st
-        recs, n, st = staged.search_device(wl.threshold, stream=stream)
+        recs, n, st = hs.search_device(wl.threshold, stream=stream)
         got = gather_device(recs, n, 0)  # RCCL: counts all-gather + point-to-point sends to rank 0
         if got is not None:
             if host_buf[0] is None or host_buf[0].numel() < got.numel():
@@ -155,6 +181,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    stage_ms[0] = 0.0
     t0 = time.perf_counter()
     acc = dict(kernel_ms=0.0, lane_ms=0.0, cache_ms=0.0, prefilter_ms=0.0, launches=0, popped=0, cached=0,
                lane_windows=0, matches=0)
@@ -188,7 +215,7 @@ def main():
     # bytes read once + 32 B per record written) over the device time of every kernel of the step —
     # prefix-cache counts/builds/publishes and lookups, the lane-serial and the wave kernels (HIP events
     # on the search streams), or the bitap scan + re-search for the pre-filter.
-    step_dev_ms = (acc["cache_ms"] + acc["lane_ms"] + acc["kernel_ms"] + acc["prefilter_ms"]) / K
+    step_dev_ms = (acc["cache_ms"] + acc["lane_ms"] + acc["kernel_ms"] + acc["prefilter_ms"] + stage_ms[0]) / K
     rank_bytes = staged.owned_bytes if args.shard else len(wl.haystack)
     recs_rank = acc["matches"] / K / (world if world > 1 else 1)
     bytes_step = rank_bytes + 32 * recs_rank
@@ -221,14 +248,20 @@ def main():
             "scaling": "strong" if args.shard else "weak",
             "vs_baseline": None,
             "dtype": "u32 code points / f32 penalties",
-            "data": "synthetic (seeded xorshift generator, SURVEY.md §8(d)); random words + planted fuzzy patterns",
+            "data": "synthetic (seeded xorshift generator, SURVEY.md §8(d)): random words of 2-12 chars "
+                    + (f"drawn from a fixed {args.vocab}-word random vocabulary" if args.vocab else "(every word fresh)")
+                    + ", separated by ' ', one planted pattern with 0..edits random edits every 4 KiB",
             "config": {
                 "workload": f"{args.config}: " + WORKLOAD[args.config],
                 "patterns": len(wl.patterns),
                 "haystack_bytes_per_gpu": rank_bytes,
                 "graphemes_per_gpu": windows,
                 "threshold": wl.threshold,
-                "end_to_end_search_raw": bool(args.end_to_end),
+                "filler_vocabulary": args.vocab or "fresh",
+                "timed_step": ("search_raw from host bytes (H2D + staging + search + records)" if args.end_to_end else
+                               "search_raw on device-resident bytes: device staging (UTF-8 check, is_ascii, UAX #29 "
+                               "segmentation + folding) + search + records" if device_staging else
+                               "search only (haystack staged before the timed steps)"),
                 "parallelism": (f"shard{world} (strong: one {len(wl.haystack)}-byte haystack, halo-sliced shards)"
                                 if args.shard else f"dp{world} (weak: one haystack per GPU)")
                                + (", RCCL gather of Match records to rank 0" if world > 1 else ""),
@@ -241,8 +274,8 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_note,
-                "kernel": "whole search step: prefix-cache count/build/publish + rc_lookup + lane_window + "
-                          "bfs_window kernels" if not wl.prefilter else
+                "kernel": "whole search_raw step: staging (seg_tile + write_tile, synchronous) + prefix-cache "
+                          "count/build/publish + rc_lookup + lane_window + bfs_window kernels" if not wl.prefilter else
                           "pre-filter (q-gram scan + verify / packed bitap) + runs + re-search",
                 "avg_kernel_ms": step_dev_ms,
                 "algorithmic_bytes_per_launch": bytes_step,
@@ -260,6 +293,8 @@ def main():
                 "lane_windows_per_step": acc["lane_windows"] / K,
                 "prefilter_ms_per_step": acc["prefilter_ms"] / K,
                 "prefix_cache_ms_per_step": acc["cache_ms"] / K,
+                "staging_ms_per_step": stage_ms[0] / K,
+                "h2d_ms_once": h2d_ms,
                 "states_from_prefix_cache_per_step": acc["cached"] / K,
                 "sources_sha": sources_sha(),
             },

@@ -339,6 +339,31 @@ int fac_haystack_stage(const fac_engine* engine, const uint8_t* utf8, uint64_t l
   return rc;
 }
 
+int fac_haystack_stage_device(const fac_engine* engine, const uint8_t* d_utf8, uint64_t len, void* stream,
+                              fac_haystack** hay, uint64_t* err_graphemes) {
+  if (!engine || !hay || (len && !d_utf8)) return fail(FAC_E_INVALID, "NULL argument");
+  fac_haystack* fh = *hay;
+  const bool fresh = fh == nullptr;
+  if (fresh) {
+    fh = new (std::nothrow) fac_haystack();
+    if (!fh) return fail(FAC_E_OOM, "out of host memory");
+  } else if (fh->h.own_utf8 && fh->h.d_utf8) {
+    return fail(FAC_E_INVALID, "haystack was not staged from device memory");
+  }
+  std::string err;
+  const int rc = fac::stage_haystack_device(engine->e, d_utf8, len, fh->h, err, static_cast<hipStream_t>(stream));
+  if (rc) {
+    if (rc == FAC_E_HAYSTACK_TOO_LARGE && err_graphemes) *err_graphemes = fh->h.n;
+    if (fresh) {
+      fac::free_haystack(fh->h);
+      delete fh;
+    }
+    return fail(rc, rc == FAC_E_HAYSTACK_TOO_LARGE ? std::string("haystack has more than u32::MAX grapheme clusters") : err);
+  }
+  *hay = fh;
+  return FAC_OK;
+}
+
 int fac_shard_plan(uint64_t max_match_graphemes, const uint8_t* utf8, uint64_t len, int32_t is_ascii, uint64_t n_shards,
                    uint64_t shard, uint64_t plan[4]) {
   if (!plan || (len && !utf8) || n_shards == 0 || shard >= n_shards) return fail(FAC_E_INVALID, "bad argument");
@@ -740,6 +765,13 @@ uint64_t fac_segment_graphemes(const uint8_t* utf8, uint64_t len, uint64_t* star
 
 uint32_t fac_fold_first_char(const uint8_t* utf8, uint64_t len, int32_t case_insensitive) {
   return fac::fold_first_char(utf8, 0, len, case_insensitive != 0);
+}
+
+void fac_edge_order(const uint32_t* cps, const uint64_t* off, uint64_t n, uint32_t* order) {
+  std::vector<std::u32string> g(n);
+  for (uint64_t i = 0; i < n; ++i) g[i].assign(cps + off[i], cps + off[i + 1]);
+  const std::vector<uint32_t> o = fac::transitions_order(g);
+  for (uint64_t i = 0; i < n; ++i) order[i] = o[i];
 }
 
 }  // extern "C"

@@ -3,8 +3,9 @@
 // Mirrors FuzzyAhoCorasickBuilder::build (src/builder.rs:181-484) and emits the flat
 // structure-of-arrays layout of fac_internal.h instead of the reference's per-node Vecs/maps:
 //   * graphemes are interned to ids and the trie is one (node, grapheme-id) -> child hash map;
-//   * children keep insertion order (the reference uses hashbrown order, builder.rs:336-342 —
-//     see DESIGN.md §3 for why this only affects tie-breaks);
+//   * each node's children are ordered like the reference's `transitions.iter()` (builder.rs:
+//     336-342): the crate's FxHasher over the grapheme's UTF-8 bytes (structs.rs:95-156) placed by
+//     hashbrown's SSE2 group probing as std's HashMap inserts them (edge_order below);
 //   * fail links exist only to merge suffix-pattern outputs (builder.rs:239-276); they are not
 //     uploaded, because the search never follows them;
 //   * prune coefficients come from the reach-len / reach-weight pass (builder.rs:344-381).
@@ -43,6 +44,94 @@ void default_similarity(std::vector<float>& t) {  // builder.rs:492-526, structs
   }
 }
 
+// Hash of a `String` key under the crate's FxHasher: `Hash for str` writes the bytes, then 0xff
+// (structs.rs:101-156; core::hash::Hasher::write_str).
+uint64_t fx_str_hash(const std::u32string& g) {
+  std::string u;
+  for (char32_t c : g) {  // UTF-8
+    if (c < 0x80) {
+      u.push_back((char)c);
+    } else if (c < 0x800) {
+      u.push_back((char)(0xC0 | (c >> 6)));
+      u.push_back((char)(0x80 | (c & 0x3F)));
+    } else if (c < 0x10000) {
+      u.push_back((char)(0xE0 | (c >> 12)));
+      u.push_back((char)(0x80 | ((c >> 6) & 0x3F)));
+      u.push_back((char)(0x80 | (c & 0x3F)));
+    } else {
+      u.push_back((char)(0xF0 | (c >> 18)));
+      u.push_back((char)(0x80 | ((c >> 12) & 0x3F)));
+      u.push_back((char)(0x80 | ((c >> 6) & 0x3F)));
+      u.push_back((char)(0x80 | (c & 0x3F)));
+    }
+  }
+  uint64_t h = 0;
+  auto mix = [&h](uint64_t word) { h = ((h << 5) | (h >> 59)) ^ word, h *= 0x517cc1b727220a95ull; };
+  size_t i = 0;
+  for (; i + 8 <= u.size(); i += 8) {
+    uint64_t w;
+    std::memcpy(&w, u.data() + i, 8);  // little-endian host, like u64::from_le_bytes
+    mix(w);
+  }
+  if (i + 4 <= u.size()) {
+    uint32_t w;
+    std::memcpy(&w, u.data() + i, 4);
+    mix(w);
+    i += 4;
+  }
+  for (; i < u.size(); ++i) mix((uint8_t)u[i]);
+  mix(0xff);
+  return h;
+}
+
+// Iteration order of an insert-only std HashMap (hashbrown RawTable, x86-64 SSE2: 16 control bytes
+// per group) after inserting `hashes` in order: a table of 2^b buckets holds at most b < 3 ? 2^b - 1 :
+// 2^b * 7 / 8 items; inserting into a full one first moves every item, in bucket order, into the
+// next size (4, 8, 16, ... buckets); an item goes to the first EMPTY control byte along the
+// triangular probe over 16-byte groups from hash & mask (control bytes past the buckets mirror the
+// first 16; a small table's padding bytes are EMPTY, and a hit there falls back to the first EMPTY
+// bucket). Returns item indices in bucket order.
+std::vector<uint32_t> edge_order(const std::vector<uint64_t>& hashes) {
+  std::vector<int32_t> bucket;  // -1 = EMPTY
+  size_t items = 0;
+  auto capacity = [](size_t nb) { return nb < 16 ? nb - 1 : nb / 8 * 7; };  // bucket_mask_to_capacity
+  auto place = [&bucket](uint64_t hsh) -> size_t {
+    const size_t nb = bucket.size(), mask = nb - 1, mirror_at = std::max<size_t>(nb, 16);
+    size_t pos = (size_t)hsh & mask;
+    for (size_t stride = 16;; pos = (pos + stride) & mask, stride += 16)
+      for (size_t k = 0; k < 16; ++k) {
+        const size_t c = pos + k;  // control byte index
+        const bool empty = c < nb ? bucket[c] < 0 : c >= mirror_at ? bucket[c - mirror_at] < 0 : true;
+        if (!empty) continue;
+        size_t idx = c & mask;
+        if (bucket[idx] >= 0)
+          for (idx = 0; bucket[idx] >= 0; ++idx) {}
+        return idx;
+      }
+  };
+  for (size_t it = 0; it < hashes.size(); ++it) {
+    if (bucket.empty() || items == capacity(bucket.size())) {
+      const size_t want = bucket.empty() ? 1 : capacity(bucket.size()) + 1;  // max(items + 1, cap + 1)
+      size_t nb = want < 4 ? 4 : want < 8 ? 8 : 0;
+      if (!nb) {
+        nb = 1;
+        while (nb < want * 8 / 7) nb <<= 1;
+      }
+      std::vector<int32_t> old;
+      old.swap(bucket);
+      bucket.assign(nb, -1);
+      for (int32_t o : old)
+        if (o >= 0) bucket[place(hashes[(size_t)o])] = o;
+    }
+    bucket[place(hashes[it])] = (int32_t)it;
+    ++items;
+  }
+  std::vector<uint32_t> order;
+  for (int32_t b : bucket)
+    if (b >= 0) order.push_back((uint32_t)b);
+  return order;
+}
+
 int32_t lim_max(int32_t acc, int32_t v) {
   if (v == LIM_NONE) return acc;
   return std::max(acc == LIM_NONE ? 0 : acc, v);
@@ -53,6 +142,12 @@ DevLimits to_dev(const fac_limits& l) { return {l.insertions, l.deletions, l.sub
 bool lim_ok(int32_t v) { return v == LIM_NONE || (v >= 0 && v <= 255); }
 
 }  // namespace
+
+std::vector<uint32_t> transitions_order(const std::vector<std::u32string>& children) {
+  std::vector<uint64_t> hs;
+  for (auto& g : children) hs.push_back(fx_str_hash(g));
+  return edge_order(hs);
+}
 
 int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, Engine& e, std::string& err) {
   e.cfg = *cfg;
@@ -156,6 +251,22 @@ int build_engine(const fac_pattern* pats, uint64_t np, const fac_config* cfg, En
   }
   const size_t nn = kids.size();
   if (nn > (size_t)CHILD26_MASK) { err = "automaton too large (more than 2^26 nodes)"; return FAC_E_UNSUPPORTED; }
+  // edges in the reference's transitions-map iteration order (builder.rs:336-342); diagnostics
+  // knob FAC_EDGE_INSERTION keeps insertion order (A/B measurements only)
+  if (!diag_env("FAC_EDGE_INSERTION")) {
+    std::vector<uint64_t> gh(gstr.size());
+    for (size_t g = 0; g < gstr.size(); ++g) gh[g] = fx_str_hash(gstr[g]);
+    std::vector<uint64_t> hs;
+    std::vector<std::pair<uint32_t, uint32_t>> tmp;
+    for (auto& k : kids) {
+      if (k.size() < 2) continue;
+      hs.clear();
+      for (auto& c : k) hs.push_back(gh[c.first]);
+      tmp.clear();
+      for (uint32_t i : edge_order(hs)) tmp.push_back(k[i]);
+      k.swap(tmp);
+    }
+  }
 
   // ---- fail links, used only to merge outputs (builder.rs:239-276); BFS by depth
   {

@@ -213,7 +213,17 @@ struct SearchParams {
   // work distribution / outputs
   uint32_t chunk;
   uint32_t ecap;            // per-wave emission list capacity
-  uint4* ebuf;              // per-wave emission scratch
+  uint4* ebuf;              // per-wave emission scratch (slice = the wave's slot)
+  // wave slots (bfs_window_body): a launch may have more workgroups than resident waves (the
+  // one-chunk-per-workgroup level-1 build), so per-wave global scratch is indexed by a slot taken
+  // from a free ring when the wave starts and returned when it ends (slot_ctr: taken, returned)
+  unsigned int* slot_ring;
+  unsigned int* slot_ctr;
+  uint32_t n_slots;
+  uint4* bsel;              // beamed engines: the beam selection's scratch (bsel_stride per slot)
+  uint32_t bsel_stride;
+  uint32_t sel_limit;       // select.rs partition rounds before median_of_medians (16; tests lower it)
+  int32_t beam_canonical;   // diagnostics (FAC_BEAM_CANONICAL): rounds 1-2's canonical tie rule
   fac_match* out;
   uint64_t out_cap;
   uint64_t out_shift;       // added to every record's start/end (global byte of a shard's byte 0)
@@ -278,7 +288,9 @@ constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8
 struct Engine {
   int device = 0;
   hipStream_t stream = nullptr;
-  mutable hipStream_t aux_stream = nullptr;  // prefix cache: level-1 build beside the sampled-level counts
+  // prefix cache: level-1 build beside the sampled-level counts (lowest priority; created with the
+  // engine's tables; a streaming worker's ScratchSet has its own)
+  hipStream_t aux_stream = nullptr;
   fac_config cfg{};
   bool case_insensitive = false;
   bool has_limits = false;
@@ -374,8 +386,12 @@ struct Haystack {
   bool open_end = false;
   uint64_t owned = UINT64_MAX;
   uint8_t* d_utf8 = nullptr;
+  bool own_utf8 = true;          // false: the caller's device bytes (fac_haystack_stage_device)
   uint32_t* d_text32 = nullptr;  // Unicode only
   uint64_t* d_off = nullptr;     // Unicode only
+  uint64_t off_cap = 0;          // entries d_off / d_text32 hold (kept when staged again)
+  void* d_stage = nullptr;       // staging scratch (stage_device), kept when staged again
+  size_t stage_cap = 0;
   // host copies, fetched from the device on first use (ensure_host): the UTF-8 bytes (pre-filter
   // slices re-decide is_ascii; host transcodes) and the grapheme byte starts (Unicode only)
   mutable std::vector<uint8_t> utf8;
@@ -411,6 +427,8 @@ int sink_append_host(MatchSink& s, const fac_match* src, uint64_t cnt, hipStream
 
 // builder.cpp
 int build_engine(const fac_pattern* pats, uint64_t n, const fac_config* cfg, Engine& e, std::string& err);
+// a node's children (folded graphemes, insertion order) -> their transitions-map iteration order
+std::vector<uint32_t> transitions_order(const std::vector<std::u32string>& children);
 // search_kernels.hip
 int launch_search(const Engine& e, const Haystack& h, const std::vector<SegDesc>& segs, float thr,
                   hipStream_t stream, std::vector<fac_match>& out, fac_stats* stats, std::string& err);
@@ -437,6 +455,7 @@ struct ScratchSet {
   std::mutex mu;
   void* p[kSlots] = {};
   size_t n[kSlots] = {};
+  hipStream_t aux = nullptr;  // this set's low-priority second stream (prefix-cache level-1 build)
 };
 void scratch_bind(ScratchSet* s);  // this thread's searches use `s` (nullptr: the engine's)
 void scratch_free(ScratchSet& s);
@@ -470,9 +489,9 @@ StreamCore* stream_open(const Engine& e, float threshold, uint64_t window);
 int stream_feed(StreamCore& s, const uint8_t* data, uint64_t len, bool eof, std::string& err);
 void stream_close(StreamCore* s);
 uint64_t stream_committed(const StreamCore& s);  // commit point of the windows handed out so far
-int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err);
-// bit 0: invalid UTF-8, bit 1: not ASCII (validate_kernel over the device copy; synchronous)
-int validate_device(const uint8_t* d_utf8, uint64_t len, hipStream_t st, unsigned int& flags, std::string& err);
+// staging of the bytes at h.d_utf8 on the device (stage_kernels.hip): mode -2 checks the UTF-8 and
+// decides is_ascii, 0 stages Unicode graphemes, 1 ASCII (asynchronous after its count sync)
+int stage_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err, int mode);
 void ensure_symbols(const Engine& e, const Haystack& h);
 int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,
                   std::string& err);
@@ -486,6 +505,10 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
 // shard of a haystack whose global is_ascii is already known)
 int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack& h, std::string& err,
                    int force_ascii = -1, hipStream_t stream = nullptr);
+// search_raw's staging of bytes already in device memory (borrowed, not copied): the UTF-8 check,
+// is_ascii, segmentation and folding on the device; h may hold buffers of an earlier staging
+int stage_haystack_device(const Engine& e, const uint8_t* d_utf8, uint64_t len, Haystack& h, std::string& err,
+                          hipStream_t stream);
 // start byte of the n-th grapheme counted from the end of s[0, len) (UAX #29, the whole text's
 // segmentation; stream.rs:134-139 grapheme_indices(true).rev().nth(n - 1)); false if it has fewer
 bool nth_grapheme_from_end(const uint8_t* s, uint64_t len, uint64_t n, uint64_t& off);

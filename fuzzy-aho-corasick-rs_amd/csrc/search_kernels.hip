@@ -260,12 +260,284 @@ __device__ void emit_update(EmitList& L, uint32_t me_rel, uint32_t p, float sim,
   wave_mem_fence();
 }
 
-// Canonical beam: keep the `bw` smallest pending states by (penalty total order,
-// queue position), in queue order — one legal outcome of the reference's
-// `select_nth_unstable_by(bw - 1, total_cmp)` + `truncate(q_idx + bw)` (search.rs:584-587).
+// ---- Beam (search.rs:577-589): queue[q_idx..].select_nth_unstable_by(bw - 1, total_cmp) +
+// truncate(q_idx + bw), restated from core (Rust >= 1.81: core/src/slice/select.rs, the ipnsort
+// partition of core/src/slice/sort/unstable/quicksort.rs and the pivot of sort/shared/pivot.rs) so
+// the survivors AND their order are the reference's. The wave runs the introselect loop on a copy of
+// the pending slice in its global scratch slice (A), partitions through a second slice (T), and
+// writes the first bw states back to the ring. oracle/oracle.cpp (rsel) is the CPU restatement.
+//
+// Scratch per wave (uint4 units): A[QCAP], T[QCAP], W[48] (per 64 partition positions: the "is less"
+// mask as two words, then the exclusive prefix counts).
+__host__ __device__ constexpr uint32_t bsel_stride(uint32_t qcap) { return 2u * qcap + 48u; }
+
+__device__ __forceinline__ uint32_t sel_key(const uint4& s) { return total_order_key(__uint_as_float(s.z)); }
+
+// median3 (sort/shared/pivot.rs) on (position, key) pairs
+__device__ __forceinline__ void sel_median3(uint32_t pa, uint32_t ka, uint32_t pb, uint32_t kb, uint32_t pc, uint32_t kc,
+                                            uint32_t& p, uint32_t& k) {
+  const bool x = ka < kb, y = ka < kc;
+  if (x == y) {
+    const bool z = kb < kc;
+    if (z ^ x) { p = pc; k = kc; } else { p = pb; k = kb; }
+  } else {
+    p = pa;
+    k = ka;
+  }
+}
+
+// choose_pivot (len >= 17 here): median3 of v[0], v[4 len/8], v[7 len/8] below 64 elements, else the
+// recursive pseudo-median median3_rec. The recursion tree is evaluated bottom-up: one lane per leaf
+// triple (3^D of them, D <= 3 for len <= 4096), then groups of three lanes per level.
+__device__ uint32_t sel_pivot(const uint4* v, uint32_t len) {
+  const uint32_t lane = lane_id();
+  uint32_t s[4] = {len / 8, 0u, 0u, 0u};
+  uint32_t D = 0;
+  if (len >= 64)
+    while (D < 3 && s[D] >= 8) {  // median3_rec recurses while n * 8 >= 64
+      s[D + 1] = s[D] / 8;
+      ++D;
+    }
+  uint32_t nleaf = 1;
+  for (uint32_t d = 0; d < D; ++d) nleaf *= 3;
+  uint32_t p = 0, k = 0;
+  if (lane < nleaf) {
+    uint32_t base = 0, rem = lane, div = nleaf;
+    for (uint32_t d = 0; d < D; ++d) {  // digit d (most significant first) picks a, b or c at level d
+      div /= 3;
+      const uint32_t dig = rem / div;
+      rem -= dig * div;
+      base += (dig == 0 ? 0u : dig == 1 ? 4u : 7u) * s[d];
+    }
+    const uint32_t pa = base, pb = base + 4u * s[D], pc = base + 7u * s[D];
+    sel_median3(pa, sel_key(v[pa]), pb, sel_key(v[pb]), pc, sel_key(v[pc]), p, k);
+  }
+  for (uint32_t n = nleaf; n > 1; n /= 3) {  // one level up: lane g takes lanes 3g, 3g + 1, 3g + 2
+    const int b = (int)(3u * lane) & 63;
+    const uint32_t pa = (uint32_t)__shfl((int)p, b), ka = (uint32_t)__shfl((int)k, b);
+    const uint32_t pb = (uint32_t)__shfl((int)p, (b + 1) & 63), kb = (uint32_t)__shfl((int)k, (b + 1) & 63);
+    const uint32_t pc = (uint32_t)__shfl((int)p, (b + 2) & 63), kc = (uint32_t)__shfl((int)k, (b + 2) & 63);
+    if (lane < n / 3) sel_median3(pa, ka, pb, kb, pc, kc, p, k);
+  }
+  return shfl_u32(p, 0);
+}
+
+// partition (quicksort.rs) of v[0..len) around v[pp] with is_less (le: a <= pivot), through T;
+// returns num_lt. swap(v[0], v[pp]), then partition_lomuto_branchless_cyclic over w = v[1..len): it
+// takes w[1], ..., w[m-1], then w[0] (r = 1..m: e_r) and writes each to w[num_lt], moving the previous
+// occupant into the gap the previous element left. Closed form, lane-parallel (oracle.cpp
+// rsel::lomuto_cyclic is the sequential restatement; tests/test_rust_select.py checks both):
+//   * the lt elements end at w[0..F) in processing order (w position = their exclusive lt count L_r);
+//   * w[p] for p >= F: e_m if p == F and e_m is not lt; else follow r = p + 1: while e_{r-1} is lt,
+//     r = L_r + 1; then e_{r-1};
+// then swap(v[0], v[F]): w[F-1] goes to v[0], the pivot to v[F], every other w[p] to v[p + 1].
+__device__ uint32_t sel_partition(uint4* v, uint4* T, uint32_t* W, uint32_t len, uint32_t pp, bool le) {
+  const uint32_t lane = lane_id();
+  const uint32_t m = len - 1;
+  const uint4 piv = v[pp];
+  const uint32_t pkey = sel_key(piv);
+  auto src = [&](uint32_t r) -> uint32_t {  // e_r's position in v before the pivot swap
+    const uint32_t x = r < m ? r + 1u : 1u;
+    return x == pp ? 0u : x;
+  };
+  uint32_t F = 0;
+  for (uint32_t c = 0; c * 64u < m; ++c) {  // bit b = r - 1
+    const uint32_t b = c * 64u + lane;
+    const bool valid = b < m;
+    uint4 e = make_uint4(0, 0, 0, 0);
+    bool lt = false;
+    if (valid) {
+      e = v[src(b + 1u)];
+      const uint32_t k = sel_key(e);
+      lt = le ? k <= pkey : k < pkey;
+    }
+    const uint64_t mk = __ballot(lt);
+    if (lane == 0) {
+      W[2u * c] = (uint32_t)mk;
+      W[2u * c + 1u] = (uint32_t)(mk >> 32);
+      W[128u + c] = F;
+    }
+    if (lt) T[F + prefix_below(mk) + 1u] = e;  // w position L_r, v position + 1 (fixed below for F - 1)
+    F += (uint32_t)__popcll(mk);
+  }
+  wave_mem_fence();
+  if (lane == 0) {
+    if (F) T[0] = T[F];
+    T[F] = piv;
+  }
+  auto bit = [&](uint32_t b) -> bool { return (W[2u * (b >> 6) + ((b >> 5) & 1u)] >> (b & 31u)) & 1u; };
+  auto lcount = [&](uint32_t r) -> uint32_t {  // L_r: lt elements among e_1 .. e_{r-1}
+    const uint32_t b = r - 1u, c = b >> 6, o = b & 63u;
+    const uint64_t mk = ((uint64_t)W[2u * c + 1u] << 32) | W[2u * c];
+    return W[128u + c] + (uint32_t)__popcll(mk & ((1ull << o) - 1ull));
+  };
+  const bool lt_m = m ? bit(m - 1u) : false;
+  for (uint32_t p = F + lane; p < m; p += 64u) {
+    uint32_t sidx;
+    if (p == F && !lt_m) {
+      sidx = m;
+    } else {
+      uint32_t r = p + 1u;
+      while (bit(r - 2u)) r = lcount(r) + 1u;
+      sidx = r - 1u;
+    }
+    T[p + 1u] = v[src(sidx)];
+  }
+  wave_mem_fence();
+  for (uint32_t i = lane; i < len; i += 64u) v[i] = T[i];
+  wave_mem_fence();
+  return F;
+}
+
+// insertion_sort_shift_left(v, 1) for len <= 16: stable by key (rank = smaller keys + equal keys
+// before), in place through the lanes' registers
+__device__ void sel_small_sort(uint4* v, uint32_t len) {
+  const uint32_t lane = lane_id();
+  uint4 e = make_uint4(0, 0, 0, 0);
+  uint32_t k = 0xFFFFFFFFu;
+  if (lane < len) {
+    e = v[lane];
+    k = sel_key(e);
+  }
+  uint32_t rank = 0;
+  for (uint32_t j = 0; j < len; ++j) {
+    const uint32_t kj = shfl_u32(k, (int)j);
+    rank += (kj < k || (kj == k && j < lane)) ? 1u : 0u;
+  }
+  wave_mem_fence();
+  if (lane < len) v[rank] = e;
+  wave_mem_fence();
+}
+
+// ---- median_of_medians fallback (select.rs), taken after 16 partition rounds: one lane, sequential
+__device__ void sel_s_swap(uint4* v, uint32_t a, uint32_t b) {
+  const uint4 t = v[a];
+  v[a] = v[b];
+  v[b] = t;
+}
+__device__ void sel_s_insertion(uint4* v, uint32_t len) {
+  for (uint32_t i = 1; i < len; ++i) {
+    const uint4 tmp = v[i];
+    const uint32_t kt = sel_key(tmp);
+    if (!(kt < sel_key(v[i - 1]))) continue;
+    uint32_t j = i;
+    for (;;) {
+      v[j] = v[j - 1];
+      --j;
+      if (j == 0 || !(kt < sel_key(v[j - 1]))) break;
+    }
+    v[j] = tmp;
+  }
+}
+__device__ uint32_t sel_s_partition(uint4* v, uint32_t len, uint32_t pivot) {  // quicksort.rs partition
+  if (len == 0) return 0;
+  sel_s_swap(v, 0, pivot);
+  const uint32_t pk = sel_key(v[0]);
+  uint4* w = v + 1;
+  const uint32_t m = len - 1;
+  uint32_t num_lt = 0;
+  if (m) {
+    const uint4 gv = w[0];
+    uint32_t gap = 0;
+    for (uint32_t r = 1; r < m; ++r) {
+      const uint4 x = w[r];
+      const bool lt = sel_key(x) < pk;
+      w[gap] = w[num_lt];
+      w[num_lt] = x;
+      gap = r;
+      num_lt += lt ? 1u : 0u;
+    }
+    const bool lt = sel_key(gv) < pk;
+    w[gap] = w[num_lt];
+    w[num_lt] = gv;
+    num_lt += lt ? 1u : 0u;
+  }
+  sel_s_swap(v, 0, num_lt);
+  return num_lt;
+}
+__device__ uint32_t sel_s_median_idx(const uint4* v, uint32_t a, uint32_t b, uint32_t c) {
+  if (sel_key(v[c]) < sel_key(v[a])) {
+    const uint32_t t = a;
+    a = c;
+    c = t;
+  }
+  if (sel_key(v[c]) < sel_key(v[b])) return c;
+  if (sel_key(v[b]) < sel_key(v[a])) return a;
+  return b;
+}
+// ninther (select.rs): the median of the medians of (a, b, c), (d, e, f), (g, h, i), swapped into e
+__device__ void sel_s_ninther(uint4* v, uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e, uint32_t f,
+                              uint32_t g, uint32_t h, uint32_t i) {
+  auto lt = [&](uint32_t x, uint32_t y) { return sel_key(v[x]) < sel_key(v[y]); };
+  b = sel_s_median_idx(v, a, b, c);
+  h = sel_s_median_idx(v, g, h, i);
+  if (lt(h, b)) { const uint32_t t = b; b = h; h = t; }
+  if (lt(f, d)) { const uint32_t t = d; d = f; f = t; }
+  if (lt(e, d)) {
+    // the middle triple's median is d
+  } else if (lt(f, e)) {
+    d = f;
+  } else {
+    if (lt(e, b)) sel_s_swap(v, e, b);
+    else if (lt(h, e)) sel_s_swap(v, e, h);
+    return;
+  }
+  if (lt(d, b)) d = b;
+  else if (lt(h, d)) d = h;
+  sel_s_swap(v, d, e);
+}
+template <int D>
+__device__ void sel_s_mom(uint4* v, uint32_t len, uint32_t k);
+template <int D>
+__device__ uint32_t sel_s_ninthers(uint4* v, uint32_t len) {  // median_of_ninthers
+  const uint32_t frac = len <= 1024u ? len / 12u : (len <= 128u * 1024u ? len / 64u : len / 1024u);
+  const uint32_t pivot = frac / 2u, lo = len / 2u - pivot, hi = frac + lo, gap = (len - 9u * frac) / 4u;
+  uint32_t a = lo - 4u * frac - gap, b = hi + gap;
+  for (uint32_t i = lo; i < hi; ++i) {
+    sel_s_ninther(v, a, i - frac, b, a + 1u, i, b + 1u, a + 2u, i + frac, b + 2u);
+    a += 3u;
+    b += 3u;
+  }
+  sel_s_mom<D - 1>(v + lo, frac, pivot);
+  return sel_s_partition(v, len, lo + pivot);
+}
+template <int D>
+__device__ void sel_s_mom(uint4* v, uint32_t len, uint32_t k) {  // median_of_medians
+  for (;;) {
+    if (len <= 16u) {
+      if (len >= 2u) sel_s_insertion(v, len);
+      return;
+    }
+    if (k == len - 1u || k == 0u) {  // max_index keeps the first maximum, min_index the first minimum
+      uint32_t acc = 0;
+      for (uint32_t i = 1; i < len; ++i)
+        if (k ? sel_key(v[acc]) < sel_key(v[i]) : sel_key(v[i]) < sel_key(v[acc])) acc = i;
+      sel_s_swap(v, acc, k);
+      return;
+    }
+    uint32_t p;
+    if constexpr (D > 0) {
+      p = sel_s_ninthers<D>(v, len);
+    } else {  // unreachable for len <= 4096 (three levels of ninthers reach <= 16 elements)
+      sel_s_insertion(v, len);
+      return;
+    }
+    if (p == k) return;
+    if (p > k) {
+      len = p;
+    } else {
+      v += p + 1u;
+      len -= p + 1u;
+      k -= p + 1u;
+    }
+  }
+}
+
+// Diagnostics only (FAC_BEAM_CANONICAL, rounds 1-2's rule): keep the bw smallest by (penalty,
+// queue position) in queue order -- not the reference's order; for A/B measurements of the tie rule.
 template <uint32_t QCAP>
-__device__ void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t bw) {
-  constexpr int PER = QCAP / 64;  // keys per lane (pending <= QCAP)
+__device__ void beam_select_canonical(KState* q, uint32_t head, uint32_t& tail, uint32_t bw) {
+  constexpr int PER = QCAP / 64;
   const uint32_t lane = lane_id();
   const uint32_t P = tail - head;
   uint32_t key[PER];
@@ -274,8 +546,6 @@ __device__ void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t b
     const uint32_t i = (uint32_t)t * 64 + lane;
     key[t] = i < P ? total_order_key(q[(head + i) & (QCAP - 1)].pen) : 0xFFFFFFFFu;
   }
-  // Walk the distinct penalty keys upwards until `bw` states are covered: T = the bw-th smallest
-  // key, need_eq = how many states with key T survive (the first ones in queue order).
   uint32_t left = bw, T = 0xFFFFFFFFu, need_eq = 0;
   bool have_last = false;
   uint32_t last = 0;
@@ -297,7 +567,7 @@ __device__ void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t b
     last = m;
     have_last = true;
   }
-  uint32_t w = head, eq_seen = 0;  // stable in-place compaction, chunk by chunk
+  uint32_t w = head, eq_seen = 0;
 #pragma unroll
   for (int t = 0; t < PER; ++t) {
     const uint32_t i = (uint32_t)t * 64 + lane;
@@ -307,7 +577,6 @@ __device__ void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t b
     const uint64_t meq = __ballot(eq);
     const bool keep = valid && (k < T || (eq && eq_seen + prefix_below(meq) < need_eq));
     const uint64_t mk = __ballot(keep);
-    // read the whole chunk, then write the survivors (destination slots never exceed sources)
     const uint4 v = keep ? reinterpret_cast<const uint4*>(q)[(head + i) & (QCAP - 1)] : make_uint4(0, 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
     if (keep) reinterpret_cast<uint4*>(q)[(w + prefix_below(mk)) & (QCAP - 1)] = v;
@@ -315,6 +584,75 @@ __device__ void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t b
     w += __popcll(mk);
     eq_seen += __popcll(meq);
   }
+  tail = head + bw;
+}
+
+template <uint32_t QCAP>
+__device__ void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t bw, uint4* scratch, uint32_t limit0) {
+  const uint32_t lane = lane_id();
+  const uint32_t P = tail - head;
+  uint4* qq = reinterpret_cast<uint4*>(q);
+  if (bw == 1) {  // partition_at_index, index == 0: min_index (first minimum), swapped to the front
+    uint32_t best = 0xFFFFFFFFu;
+    for (uint32_t i = lane; i < P; i += 64u) best = min(best, sel_key(qq[(head + i) & (QCAP - 1)]));
+    best = wave_min_u32(best);
+    uint32_t first = 0xFFFFFFFFu;
+    for (uint32_t i = lane; i < P; i += 64u)
+      if (sel_key(qq[(head + i) & (QCAP - 1)]) == best) first = min(first, i);
+    first = wave_min_u32(first);
+    const uint4 e = qq[(head + first) & (QCAP - 1)];
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) qq[head & (QCAP - 1)] = e;
+    __builtin_amdgcn_wave_barrier();
+    tail = head + 1u;
+    return;
+  }
+  uint4* A = scratch;
+  uint4* T = scratch + QCAP;
+  uint32_t* W = reinterpret_cast<uint32_t*>(scratch + 2u * QCAP);
+  for (uint32_t i = lane; i < P; i += 64u) A[i] = qq[(head + i) & (QCAP - 1)];
+  wave_mem_fence();
+  // partition_at_index_loop (bw - 1 is never len - 1 here: P > 2 bw)
+  uint32_t a = 0, len = P, index = bw - 1u, limit = limit0;
+  bool has_anc = false;
+  uint32_t anc = 0;
+  for (;;) {
+    if (len <= 16u) {
+      if (len >= 2u) sel_small_sort(A + a, len);
+      break;
+    }
+    if (limit == 0) {
+      if (lane == 0) sel_s_mom<4>(A + a, len, index);
+      wave_mem_fence();
+      break;
+    }
+    --limit;
+    const uint32_t pp = sel_pivot(A + a, len);
+    const uint32_t pk = sel_key(A[a + pp]);
+    if (has_anc && !(anc < pk)) {  // pivot equal to the ancestor pivot: split off the equal run
+      const uint32_t mid = sel_partition(A + a, T + a, W, len, pp, true) + 1u;
+      if (index <= mid) break;
+      a += mid;
+      len -= mid;
+      index -= mid;
+      has_anc = false;
+      continue;
+    }
+    const uint32_t mid = sel_partition(A + a, T + a, W, len, pp, false);
+    if (mid < index) {
+      has_anc = true;
+      anc = pk;
+      a += mid + 1u;
+      len -= mid + 1u;
+      index -= mid + 1u;
+    } else if (mid > index) {
+      len = mid;
+    } else {
+      break;
+    }
+  }
+  for (uint32_t i = lane; i < bw; i += 64u) qq[(head + i) & (QCAP - 1)] = A[i];
+  __builtin_amdgcn_wave_barrier();
   tail = head + bw;
 }
 
@@ -1123,6 +1461,31 @@ __device__ unsigned long long g_prof[64];  // [0, 32): main passes, [32, 64): ca
 #define PROF_ACC(i, t0)
 #endif
 
+// Wave slots (SearchParams::slot_ring): lane 0 takes the next position of the free ring and waits
+// for the slot returned into it (positions are filled in return order); the ring starts as 0..n-1.
+__device__ uint32_t slot_acquire(const SearchParams& P) {
+  uint32_t s = 0;
+  if (lane_id() == 0) {
+    const unsigned int h = atomicAdd(P.slot_ctr, 1u);
+    unsigned int* cell = P.slot_ring + (h % P.n_slots);
+    while ((s = atomicExch(cell, EMPTY)) == EMPTY) __builtin_amdgcn_s_sleep(2);
+  }
+  return shfl_u32(s, 0);
+}
+__device__ void slot_release(const SearchParams& P, uint32_t s) {
+  if (lane_id() == 0) {
+    const unsigned int t = atomicAdd(P.slot_ctr + 1, 1u);
+    atomicExch(P.slot_ring + (t % P.n_slots), s);
+  }
+}
+__global__ void slot_init_kernel(unsigned int* ring, unsigned int* ctr, uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) ring[i] = i;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ctr[0] = 0u;
+    ctr[1] = n;
+  }
+}
+
 // One start window, explored by one wavefront. States are popped in the reference's FIFO order in
 // batches of up to 64 (one state per lane); a batch is cut exactly where the reference's sequential
 // semantics would diverge: before the first in-batch dedup conflict, before the first pop at which
@@ -1137,7 +1500,7 @@ template <uint32_t VCAP, uint32_t QCAP, bool MAP, bool LIVE = false>
 __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
                            uint32_t& cseq, EmitList& EL, uint64_t start, const RcHit& rc, uint64_t& popped,
                            uint64_t& cached, unsigned& err, uint32_t& head_out, uint32_t& vcount_out,
-                           KState* live = nullptr, uint32_t* jbeam_out = nullptr) {
+                           KState* live = nullptr, uint32_t* jbeam_out = nullptr, uint4* bsel = nullptr) {
   const uint32_t lane = lane_id();
 #ifdef FAC_PHASE_PROF
   uint64_t prof_acc[20] = {};  // 12: per-edge states, 13: fast states, 14: committed, 15: loaded, 16-19: Bc buckets
@@ -1214,7 +1577,8 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     PROF_T(t0);
     if constexpr (VCAP > 0) {
       if (P.beam && tail - head > beam2) {
-        beam_select<QCAP>(q, head, tail, P.beam);  // :577-589
+        if (P.beam_canonical) beam_select_canonical<QCAP>(q, head, tail, P.beam);  // diagnostics
+        else beam_select<QCAP>(q, head, tail, P.beam, bsel, P.sel_limit);         // :577-589
         if (track_beam) jbeam = max(jbeam, shfl_u32(wave_inclusive_max(jp1), 63));
       }
     } else if (P.beam && tail - head > beam2) {
@@ -2390,7 +2754,9 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   __shared__ KState s_q[QCAP];
   __shared__ __attribute__((aligned(16))) uint32_t s_claim[claim_slots(VCAP)];
   const uint32_t lane = lane_id();
-  EmitList EL{P.ebuf + (size_t)blockIdx.x * P.ecap, P.ecap, 0};
+  const uint32_t slot = slot_acquire(P);
+  EmitList EL{P.ebuf + (size_t)slot * P.ecap, P.ecap, 0};
+  uint4* bsel = (VCAP > 0 && P.bsel) ? P.bsel + (size_t)slot * P.bsel_stride : nullptr;
   uint64_t popped = 0, cached = 0;     // wave-uniform
   uint64_t cached_lane = 0;            // per lane: lane-flushed windows' snapshot pops
   unsigned long long pool_cur = 0, pool_end = 0;  // cache build: this wave's snapshot pool chunk
@@ -2499,7 +2865,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
 #endif
         const uint32_t qlen =
             run_window<VCAP, QCAP, MAP, LIVE>(P, S, s_vis, s_q, s_claim, cseq, EL, st, rc, popped, cached, err, qhead,
-                                              vcnt, s_live, jbeam);
+                                              vcnt, s_live, jbeam, bsel);
 #ifdef FAC_WIN_HIST
         if (lane == 0 && P.rc_mode != 2) {
           const uint32_t b = hist_bucket(popped - popped0);
@@ -2645,6 +3011,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   wave_add_counter(P.counters + 6, triv_lane);
   const unsigned all = wave_or(err);
   if (lane == 0 && all) atomicOr(reinterpret_cast<unsigned int*>(P.counters + 2), all);
+  slot_release(P, slot);
 }
 
 // one wavefront per workgroup; the dedup-free variants are held to <= 128 VGPRs (4 waves/SIMD),
@@ -3273,6 +3640,10 @@ thread_local ScratchSet* t_scratch = nullptr;  // scratch_bind
 void scratch_bind(ScratchSet* s) { t_scratch = s; }
 
 void scratch_free(ScratchSet& s) {
+  if (s.aux) {
+    (void)hipStreamDestroy(s.aux);
+    s.aux = nullptr;
+  }
   for (int i = 0; i < ScratchSet::kSlots; ++i)
     if (s.p[i]) {
       (void)hipFree(s.p[i]);
@@ -3281,9 +3652,16 @@ void scratch_free(ScratchSet& s) {
     }
 }
 
+int aux_priority() {
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
+  return diag_env("FAC_L1_HIGH") ? greatest : least;
+}
+
 int upload_engine(Engine& e, std::string& err) {
   HIP_TRY(hipSetDevice(e.device));
   if (!e.stream) HIP_TRY(hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking));
+  if (!e.aux_stream) HIP_TRY(hipStreamCreateWithPriority(&e.aux_stream, hipStreamNonBlocking, aux_priority()));
   int rc;
   if ((rc = upload(e.dnodes, &e.d_nodes, err))) return rc;
   if ((rc = upload(e.out_range, &e.d_out_range, err))) return rc;
@@ -3352,22 +3730,39 @@ int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack&
   // in flight).
   hipStream_t st = stream ? stream : e.stream;
   HIP_TRY(hipMalloc((void**)&h.d_utf8, std::max<uint64_t>(len, 16)));
+  h.own_utf8 = true;
   if (len) HIP_TRY(hipMemcpyAsync(h.d_utf8, utf8, len, hipMemcpyHostToDevice, st));
-  if (check_on_device) {
-    unsigned int f = 0;
-    if (int vrc = validate_device(h.d_utf8, len, st, f, err)) return vrc;
-    if (f & 1u) {
-      err = "haystack is not valid UTF-8";
-      return FAC_E_INVALID;
-    }
-    h.ascii = !(f & 2u);
-    h.n = h.ascii ? len : 0;
-  }
-  if (!h.ascii) {  // UAX #29 segmentation + folding on the device (stage_kernels.hip)
-    const int rc = stage_unicode_device(e, h, st, err);
-    if (rc) return rc;
-  }
+  // UTF-8 check / is_ascii, UAX #29 segmentation + folding on the device (stage_kernels.hip)
+  if (int rc = stage_device(e, h, st, err, check_on_device ? -2 : h.ascii ? 1 : 0)) return rc;
   if (h.n > grapheme_limit()) return FAC_E_HAYSTACK_TOO_LARGE;
+  HIP_TRY(hipStreamSynchronize(st));
+  return FAC_OK;
+}
+
+int stage_haystack_device(const Engine& e, const uint8_t* d_utf8, uint64_t len, Haystack& h, std::string& err,
+                          hipStream_t stream) {
+  HIP_TRY(hipSetDevice(e.device));
+  if (h.d_utf8 && h.own_utf8) HIP_TRY(hipFree(h.d_utf8));
+  h.device = e.device;
+  h.len = len;
+  h.d_utf8 = const_cast<uint8_t*>(d_utf8);
+  h.own_utf8 = false;
+  h.base = 0;
+  h.open_end = false;
+  h.owned = UINT64_MAX;
+  {
+    std::lock_guard<std::mutex> lk(h.host_mu);
+    h.host_ready = false;
+    h.utf8.clear();
+    h.starts.clear();
+  }
+  h.sym_ready = false;
+  h.sym.clear();
+  if (h.d_gid) HIP_TRY(hipFree(h.d_gid));
+  h.d_gid = nullptr;
+  h.gid_engine = nullptr;
+  hipStream_t st = stream ? stream : e.stream;
+  if (int rc = stage_device(e, h, st, err, -2)) return rc;
   HIP_TRY(hipStreamSynchronize(st));
   return FAC_OK;
 }
@@ -3406,14 +3801,18 @@ void ensure_symbols(const Engine& e, const Haystack& h) {
 
 void free_haystack(Haystack& h) {
   (void)hipSetDevice(h.device);
-  if (h.d_utf8) (void)hipFree(h.d_utf8);
+  if (h.d_utf8 && h.own_utf8) (void)hipFree(h.d_utf8);
   if (h.d_text32) (void)hipFree(h.d_text32);
   if (h.d_off) (void)hipFree(h.d_off);
   if (h.d_gid) (void)hipFree(h.d_gid);
+  if (h.d_stage) (void)hipFree(h.d_stage);
   h.d_utf8 = nullptr;
   h.d_text32 = nullptr;
   h.d_off = nullptr;
   h.d_gid = nullptr;
+  h.d_stage = nullptr;
+  h.off_cap = 0;
+  h.stage_cap = 0;
 }
 
 // Grapheme ids of a Unicode haystack for an engine with mappings (gs_text compared as whole
@@ -3578,6 +3977,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   DevBuf d_hits, d_hitp;   // per-window lookups of the main pass
   DevBuf d_voff, d_rcnt;   // ... their windows and per-region counts
   DevBuf d_seen;           // prefix cache: sampled levels' first-sighting bitmap
+  DevBuf d_slots, d_bsel;  // wave-slot rings (one per stream), beam-selection scratch
   ScratchSet* bound = t_scratch;  // a streaming worker's own set, else the engine's
   std::unique_lock<std::mutex> lease(bound ? bound->mu : e.scratch_mu, std::try_to_lock);
   void** scratch_p = bound ? bound->p : e.scratch_p;
@@ -3594,7 +3994,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     bufs.push_back(&d_seen);
     bufs.push_back(&d_voff);
     bufs.push_back(&d_rcnt);
-    static_assert(Engine::kScratch >= 27 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
+    bufs.push_back(&d_slots);
+    bufs.push_back(&d_bsel);
+    static_assert(Engine::kScratch >= 29 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
     static_assert(ScratchSet::kSlots >= Engine::kScratch, "stream scratch slots");
     for (size_t i = 0; i < bufs.size(); ++i) bufs[i]->bind(&scratch_p[i], &scratch_n[i]);
   }
@@ -3607,6 +4009,33 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   const uint32_t max_grid = (uint32_t)cus * 16;
   HIP_TRY(d_ebuf.alloc((size_t)max_grid * P.ecap * sizeof(uint4), stream));
   HIP_TRY(d_cnt.alloc(N_COUNTERS * sizeof(unsigned long long), stream));
+  // wave slots: a ring of max_grid slots per stream a slot-using kernel runs on (this one, the
+  // level-1 build's); beamed engines: each slot's beam-selection scratch, sized for 256-state rings
+  // at max_grid slots (larger rings get fewer slots, still above their LDS-bound residency)
+  HIP_TRY(d_slots.alloc(2 * ((size_t)max_grid + 2) * sizeof(unsigned int), stream));
+  const size_t bsel_cap = P.beam ? (size_t)max_grid * bsel_stride(256) : 0;  // uint4
+  if (P.beam) HIP_TRY(d_bsel.alloc(bsel_cap * sizeof(uint4), stream));
+  P.sel_limit = 16;
+  if (const char* sl = diag_env("FAC_SEL_LIMIT")) P.sel_limit = (uint32_t)std::strtoul(sl, nullptr, 10);
+  P.beam_canonical = diag_env("FAC_BEAM_CANONICAL") ? 1 : 0;
+  // before every bfs_window_body launch: the stream's slot ring reset, the launch's scratch stride
+  auto prep_slots = [&](SearchParams& Q, hipStream_t s, uint32_t qcap, bool select) -> int {
+    const size_t pool = s == stream ? 0 : 1;
+    unsigned int* base = static_cast<unsigned int*>(d_slots.p) + pool * ((size_t)max_grid + 2);
+    Q.slot_ring = base;
+    Q.slot_ctr = base + max_grid;
+    Q.n_slots = max_grid;
+    Q.bsel = nullptr;
+    Q.bsel_stride = 0;
+    if (select && P.beam) {
+      Q.bsel = static_cast<uint4*>(d_bsel.p);
+      Q.bsel_stride = bsel_stride(qcap);
+      Q.n_slots = (uint32_t)std::min<size_t>(max_grid, bsel_cap / Q.bsel_stride);
+    }
+    hipLaunchKernelGGL(slot_init_kernel, dim3(16), dim3(256), 0, s, Q.slot_ring, Q.slot_ctr, Q.n_slots);
+    HIP_TRY(hipGetLastError());
+    return FAC_OK;
+  };
   HIP_TRY(d_out.alloc(out_cap * sizeof(fac_match), stream));
   HIP_TRY(d_spill.alloc(spill_cap * sizeof(uint64_t), stream));
   DevBuf d_counts;
@@ -3850,7 +4279,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         Q.dyn_chunks = 0;
         grid = (uint32_t)std::min<uint64_t>((n_ent + Q.chunk - 1) / Q.chunk, 0x7FFFFFFFull);
       }
-      if (live_builds && sampled && Q.rc_ntab > 0) hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
+      const bool live_build = live_builds && sampled && Q.rc_ntab > 0;
+      uint32_t qk = 256;  // launch_rc_build's ring
+      while (qk < qbuild) qk <<= 1;
+      if (int src = prep_slots(Q, bs, qk, !live_build)) return src;
+      if (live_build) hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
       else launch_rc_build(qbuild, grid, bs, Q);
       const hipError_t le = hipGetLastError();
       if (le != hipSuccess) {
@@ -3899,13 +4332,12 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       P.rc_pool = static_cast<uint4*>(d_rcs.p);
       P.rc_pool_cap = pool_words;
       if (!diag_env("FAC_RC_ONE_STREAM")) {
-        if (!e.aux_stream) {  // the lowest priority: the sampled-level counts beside it come first
-          int least = 0, greatest = 0;
-          HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-          HIP_TRY(hipStreamCreateWithPriority(&e.aux_stream, hipStreamNonBlocking, diag_env("FAC_L1_HIGH") ? greatest : least));
-        }
+        // the lowest priority: the sampled-level counts beside it come first. A streaming worker's
+        // scratch set has its own (only that worker's thread uses it), so two windows in flight do
+        // not queue their builds behind each other; the engine's is created with its tables.
+        if (bound && !bound->aux) HIP_TRY(hipStreamCreateWithPriority(&bound->aux, hipStreamNonBlocking, aux_priority()));
         HIP_TRY(hipEventCreateWithFlags(&l1_done, hipEventDisableTiming));
-        bstream = e.aux_stream;
+        bstream = bound ? bound->aux : e.aux_stream;
       }
     }
     // launched once the sampled levels' count tables are cleared (a fill queued behind the build's
@@ -3943,8 +4375,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       return FAC_OK;
     };
     // Sampled levels: every 2nd window's key, kept when seen twice. With a single sampled level
-    // (one-edit engines, whose windows mostly end within 5 chars) about 8-16 M windows are sampled
-    // (stride a power of two, at most 32) and every sampled key is kept: C2 1 GiB 88.8 -> 71.0 ms,
+    // (one-edit engines, whose windows mostly end within 5 chars) about 8-32 M windows are sampled
+    // (stride a power of two, at most 32: C2's 1 G windows still sample 32 M) and every sampled key
+    // is kept; keys numbered past the entry budget (ent_cap, 16 M) stay uncached, which is exact: C2 1 GiB 88.8 -> 71.0 ms,
     // C4 18.9 -> 17.6 ms per step with the same lane / wave work (the keys that matter are frequent);
     // C4 at stride 16 (8 M samples) against 4 (32 M): 17.7 -> 16.6 ms, C2 at stride 64: no change.
     // Two levels (C3) stay at 2 / 2: strides 3 / 4 or threshold 1 measured slower.
@@ -4167,6 +4600,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
           HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_lane_dbg), d, sizeof(d)));
         }
       }
+    }
+    if (int src = prep_slots(P, stream, kVariants[vi].qcap, kVariants[vi].vcap > 0)) {
+      rc = src;
+      break;
     }
     HIP_TRY(hipEventRecord(ev.a, stream));
     const hipError_t le = launch_variant(kVariants[vi], grid, stream, P);

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 
 #include "fac_internal.h"
 
@@ -35,7 +36,6 @@ enum Gcb : uint8_t {
 };
 enum Incb : uint8_t { INCB_None = 0, INCB_Linker, INCB_Consonant, INCB_Extend };
 
-constexpr uint32_t kChunk = 256;       // bytes decided per thread
 constexpr uint32_t kLookback = 1024;   // bytes searched backwards for a resync code point
 
 template <typename R>
@@ -141,145 +141,245 @@ __device__ bool seg_step(SegState& st, const Props& R) {
   return brk;
 }
 
-// decide the boundaries at code point starts in [a, b), starting from code point q (q <= a)
-__device__ void seg_range(const uint8_t* s, uint64_t n, uint64_t q, uint64_t a, uint64_t b, uint8_t* brk) {
-  uint64_t i = q;
-  SegState st = seg_init(props(decode(s, n, i)));
-  if (q == 0 && a == 0) brk[0] = 1;
-  while (i < b) {
-    const uint64_t pos = i;
-    const Props R = props(decode(s, n, i));
-    const bool br = seg_step(st, R);
-    if (pos >= a) brk[pos] = br ? 1 : 0;
+__device__ uint32_t lower_first(uint32_t cp) {  // unicode.cpp lower_full, first code point
+  if (cp < 0x80) return (cp >= 'A' && cp <= 'Z') ? cp + 32 : cp;
+  uint32_t lo = 0, hi = sizeof(kLowerMap) / sizeof(kLowerMap[0]);
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (kLowerMap[mid].cp < cp) lo = mid + 1;
+    else hi = mid;
   }
+  return (lo < sizeof(kLowerMap) / sizeof(kLowerMap[0]) && kLowerMap[lo].cp == cp) ? kLowerMap[lo].out[0] : cp;
 }
 
-__global__ void seg_chunk_kernel(const uint8_t* s, uint64_t n, uint8_t* brk, uint8_t* hard, unsigned int* any_hard) {
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t a = c * kChunk;
-  if (a >= n) return;
-  const uint64_t b = min(a + kChunk, n);
-  if (a == 0) {
-    seg_range(s, n, 0, 0, b, brk);
-    return;
+// ---- BMP property / lowercase tables (built once per device from the range tables above): one
+// byte per code point (GCB | Extended_Pictographic << 4 | InCB << 5) and the first code point of its
+// full lowercase (0 when it lies outside the BMP: the range search decides then)
+__global__ void bmp_tables_kernel(uint8_t* ptab, uint16_t* ltab) {
+  const uint32_t cp = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cp >= 0x10000u) return;
+  const Props p = props(cp);
+  ptab[cp] = (uint8_t)(p.g | (p.pict ? 16u : 0u) | ((uint32_t)p.ib << 5));
+  const uint32_t l = lower_first(cp);
+  ltab[cp] = l < 0x10000u ? (uint16_t)l : (uint16_t)0;
+}
+
+__device__ __forceinline__ Props props_fast(const uint8_t* __restrict__ ptab, uint32_t cp) {
+  if (cp < 0x80u)
+    return Props{(uint8_t)(cp == '\r' ? GCB_CR : cp == '\n' ? GCB_LF : (cp < 0x20u || cp == 0x7Fu) ? GCB_Control : GCB_Other),
+                 INCB_None, false};
+  if (cp < 0x10000u) {
+    const uint32_t v = ptab[cp];
+    return Props{(uint8_t)(v & 15u), (uint8_t)(v >> 5), (v & 16u) != 0};
   }
-  // latest resync code point strictly before a (code point starts only)
-  uint64_t q = a;
-  bool found = false;
-  while (q > 0 && a - q < kLookback) {
-    do --q;
-    while (q > 0 && (s[q] & 0xC0) == 0x80);
-    uint64_t t = q;
-    if (resync(props(decode(s, n, t)))) {
-      found = true;
-      break;
+  return props(cp);
+}
+
+__device__ __forceinline__ uint32_t fold_fast(const uint16_t* __restrict__ ltab, uint32_t cp) {
+  if (cp < 0x80u) return (cp - 'A' < 26u) ? cp + 32u : cp;
+  if (cp < 0x10000u) {
+    const uint32_t v = ltab[cp];
+    if (v) return v;
+  }
+  return lower_first(cp);
+}
+
+// Per 16 KiB tile (one workgroup, 64 bytes per thread, the tile staged in LDS): the C ABI's UTF-8
+// check (unicode.cpp utf8_valid_serial = Rust's str::from_utf8) over the code points starting in the
+// thread's bytes -- a segment runs from the first byte that is not a continuation byte to the next
+// thread's, so every sequence lies in one segment and stray continuation bytes are caught -- fused
+// with the UAX #29 boundary decisions of those code points (seg_step from the last resync code point
+// before them, usually the previous one). Boundaries go out as one 64-bit mask per thread, the
+// tile's grapheme count to ucnt. A thread without a resync point within kLookback marks its bytes
+// hard (seg_hard_kernel). scal: [0] flags (bit 0 invalid, bit 1 a byte >= 0x80), [1] any hard.
+constexpr uint32_t kTile = 16384;
+__global__ __launch_bounds__(256) void seg_tile_kernel(const uint8_t* __restrict__ s, uint64_t n, int aligned,
+                                                       const uint8_t* __restrict__ ptab, unsigned long long* __restrict__ bits,
+                                                       uint32_t* __restrict__ ucnt, uint8_t* __restrict__ hard,
+                                                       unsigned long long* __restrict__ scal, int skip_if_ascii) {
+  if (skip_if_ascii && !(scal[0] & 2ull)) return;  // ascii_or_kernel found no byte >= 0x80
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kTile];
+  __shared__ uint32_t red[8];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile, t1 = min(n, t0 + (uint64_t)kTile);
+  if (aligned && t1 - t0 == kTile) {
+    for (uint32_t i = threadIdx.x * 16u; i < kTile; i += 256u * 16u)
+      *reinterpret_cast<uint4*>(tile + i) = *reinterpret_cast<const uint4*>(s + t0 + i);
+  } else {
+    for (uint32_t i = threadIdx.x; i < kTile; i += 256u) tile[i] = t0 + i < n ? s[t0 + i] : 0;
+  }
+  __syncthreads();
+  auto at = [&](uint64_t p) -> uint32_t { return (p >= t0 && p < t1) ? tile[p - t0] : s[p]; };
+  auto cont = [&](uint64_t p) { return (at(p) & 0xC0u) == 0x80u; };
+  auto dec = [&](uint64_t& i) -> uint32_t {  // unicode.cpp utf8_decode, bounded by n
+    const uint32_t b0 = at(i);
+    if (b0 < 0x80u) { i += 1; return b0; }
+    if ((b0 & 0xE0u) == 0xC0u && i + 1 < n) { const uint32_t c = ((b0 & 0x1Fu) << 6) | (at(i + 1) & 0x3Fu); i += 2; return c; }
+    if ((b0 & 0xF0u) == 0xE0u && i + 2 < n) {
+      const uint32_t c = ((b0 & 0x0Fu) << 12) | ((at(i + 1) & 0x3Fu) << 6) | (at(i + 2) & 0x3Fu);
+      i += 3;
+      return c;
     }
-  }
-  if (!found && q > 0) {
-    hard[c] = 1;
-    atomicOr(any_hard, 1u);
-    return;
-  }
-  seg_range(s, n, q, a, b, brk);  // q == 0: the text's own initial state
-}
-
-// Chunks with no resync code point within kLookback: one thread walks each maximal run of such
-// chunks once, from the run's own (unbounded) resync point — linear in the text overall.
-__global__ void seg_hard_kernel(const uint8_t* s, uint64_t n, const uint8_t* hard, uint64_t chunks, uint8_t* brk) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  for (uint64_t c = 0; c < chunks; ++c) {
-    if (!hard[c]) continue;
-    uint64_t e = c;
-    while (e + 1 < chunks && hard[e + 1]) ++e;
-    const uint64_t a = c * kChunk, b = min((e + 1) * kChunk, n);
-    uint64_t q = a;
-    while (q > 0) {
-      do --q;
-      while (q > 0 && (s[q] & 0xC0) == 0x80);
-      uint64_t t = q;
-      if (resync(props(decode(s, n, t)))) break;
+    if ((b0 & 0xF8u) == 0xF0u && i + 3 < n) {
+      const uint32_t c = ((b0 & 0x07u) << 18) | ((at(i + 1) & 0x3Fu) << 12) | ((at(i + 2) & 0x3Fu) << 6) | (at(i + 3) & 0x3Fu);
+      i += 4;
+      return c;
     }
-    seg_range(s, n, q, a, b, brk);
-    c = e;
-  }
-}
-
-// The C ABI's UTF-8 check (search_raw takes a &str, always valid) and search.rs:196's is_ascii, on
-// the device: unicode.cpp's utf8_valid_serial (Rust's str::from_utf8 acceptance: no overlongs,
-// surrogates or code points past U+10FFFF) per 16-byte chunk, over the segment from the chunk's first
-// byte that is not a continuation byte to the next chunk's -- every sequence then lies in one segment;
-// four continuation bytes in a row leave no start, and text must not begin with one. flags: bit 0
-// invalid, bit 1 some byte >= 0x80. 16-byte chunks keep a wave's reads inside 1 KiB (256-byte ones
-// spread each byte load over 128 lines: 48 GB fetched for 256 MiB).
-constexpr uint32_t kValChunk = 16;
-__global__ __launch_bounds__(256) void validate_kernel(const uint8_t* s, uint64_t n, unsigned int* flags) {
-  const uint64_t c0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kValChunk;
-  if (c0 >= n) return;
-  auto cont = [&](uint64_t p) { return (s[p] & 0xC0) == 0x80; };
+    i += 1;
+    return 0xFFFD;
+  };
   auto seg_start = [&](uint64_t p, bool& bad) {  // first non-continuation byte at or after p
     uint32_t k = 0;
     while (p < n && cont(p) && k < 4) ++p, ++k;
     bad = p < n && cont(p);
     return p;
   };
-  bool bad = false, bad2 = false;
-  uint64_t i = seg_start(c0, bad);
-  if (c0 == 0 && i != 0) bad = true;
-  const uint64_t e = c0 + kValChunk < n ? seg_start(c0 + kValChunk, bad2) : n;
+  const uint64_t a = t0 + threadIdx.x * 64ull;
+  unsigned long long mask = 0;
+  bool bad = false, is_hard = false;
   uint32_t hi = 0;
-  for (uint64_t p = c0; p < min(n, c0 + kValChunk); ++p) hi |= s[p];
-  while (!bad && i < e) {
-    const uint8_t b = s[i];
-    if (b < 0x80) {
-      ++i;
-      continue;
+  if (a < n) {
+    const uint64_t b = min(a + 64, n);
+    for (uint64_t p = a; p < b; ++p) hi |= at(p);
+    uint64_t i = seg_start(a, bad);
+    if (a == 0 && i != 0) bad = true;
+    bool bad2 = false;
+    const uint64_t e = b < n ? seg_start(b, bad2) : n;
+    SegState st{};
+    if (!bad && i < e && i > 0) {  // the segmenter's state before the code point at i
+      uint64_t q = i;
+      bool found = false;
+      while (q > 0 && i - q < kLookback) {
+        do --q;
+        while (q > 0 && cont(q));
+        uint64_t t = q;
+        if (resync(props_fast(ptab, dec(t)))) {
+          found = true;
+          break;
+        }
+      }
+      if (!found && q > 0) {
+        is_hard = true;
+      } else {  // from the resync point (or the text's first code point) up to i
+        uint64_t k = q;
+        st = seg_init(props_fast(ptab, dec(k)));
+        while (k < i) seg_step(st, props_fast(ptab, dec(k)));
+      }
     }
-    uint32_t len, mn;
-    if ((b & 0xE0) == 0xC0) len = 2, mn = 0x80;
-    else if ((b & 0xF0) == 0xE0) len = 3, mn = 0x800;
-    else if ((b & 0xF8) == 0xF0) len = 4, mn = 0x10000;
-    else {
-      bad = true;
-      break;
+    for (uint64_t k = i; !bad && !is_hard && k < e;) {
+      const uint64_t pos = k;
+      const uint32_t b0 = at(k);
+      uint32_t cp;
+      if (b0 < 0x80u) {
+        cp = b0;
+        k += 1;
+      } else {
+        uint32_t len, mn;
+        if ((b0 & 0xE0u) == 0xC0u) len = 2, mn = 0x80;
+        else if ((b0 & 0xF0u) == 0xE0u) len = 3, mn = 0x800;
+        else if ((b0 & 0xF8u) == 0xF0u) len = 4, mn = 0x10000;
+        else {
+          bad = true;
+          break;
+        }
+        if (k + len > e) {
+          bad = true;
+          break;
+        }
+        for (uint32_t c = 1; c < len; ++c) bad = bad || !cont(k + c);
+        if (bad) break;
+        cp = dec(k);
+        if (cp < mn || cp > 0x10FFFFu || (cp >= 0xD800u && cp <= 0xDFFFu)) {
+          bad = true;
+          break;
+        }
+      }
+      const Props R = props_fast(ptab, cp);
+      bool br;
+      if (pos == 0) {
+        st = seg_init(R);
+        br = true;
+      } else {
+        br = seg_step(st, R);
+      }
+      if (br) mask |= 1ull << (pos - a);
     }
-    if (i + len > e) {
-      bad = true;
-      break;
-    }
-    for (uint32_t k = 1; k < len; ++k)
-      if (!cont(i + k)) bad = true;
-    if (bad) break;
-    uint64_t j = i;
-    const uint32_t cp = decode(s, n, j);
-    if (cp < mn || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) bad = true;
-    i += len;
+    bits[a >> 6] = is_hard ? 0ull : mask;
+    hard[a >> 6] = is_hard ? 1 : 0;
   }
-  const unsigned f = (bad ? 1u : 0u) | ((hi & 0x80u) ? 2u : 0u);
-  if (f) atomicOr(flags, f);
+  uint32_t c = (uint32_t)__popcll(mask);
+  uint32_t f = (bad ? 1u : 0u) | ((hi & 0x80u) ? 2u : 0u) | (is_hard ? 4u : 0u);
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_down(c, o, 64);
+    f |= (uint32_t)__shfl_down((int)f, o, 64);
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    red[threadIdx.x >> 6] = c;
+    red[4 + (threadIdx.x >> 6)] = f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ucnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    const uint32_t ff = red[4] | red[5] | red[6] | red[7];
+    if (ff & 3u) atomicOr(scal, (unsigned long long)(ff & 3u));
+    if (ff & 4u) atomicOr(scal + 1, 1ull);
+  }
 }
 
-// Grapheme-start compaction (brk bytes are 0/1): unit u = bytes [u * kUnit, (u + 1) * kUnit), one
-// wave each. unit_count_kernel counts, unit_scan_kernel (one workgroup) turns the counts into each
-// unit's first output slot and the total, unit_write_kernel writes the positions in order.
-constexpr uint32_t kUnit = 16384;
-__global__ __launch_bounds__(256) void unit_count_kernel(const uint8_t* brk, uint64_t n, uint32_t* ucnt, uint64_t n_units) {
-  const uint64_t u = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
-  const uint32_t lane = threadIdx.x & 63;
-  if (u >= n_units) return;  // whole waves
-  const uint64_t b = u * kUnit, e = min(n, b + (uint64_t)kUnit);
-  uint32_t c = 0;
-  if (e - b == kUnit) {  // 16-byte aligned (b is a multiple of kUnit, hipMalloc'd base)
-    const uint4* p = reinterpret_cast<const uint4*>(brk + b);
-    for (uint32_t i = lane; i < kUnit / 16; i += 64) {
-      const uint4 v = p[i];
-      c += __popc(v.x & 0x01010101u) + __popc(v.y & 0x01010101u) + __popc(v.z & 0x01010101u) + __popc(v.w & 0x01010101u);
-    }
-  } else {
-    for (uint64_t i = b + lane; i < e; i += 64) c += brk[i];
+// search.rs:196's is_ascii on the device: bit 1 of scal[0] when some byte is >= 0x80
+__global__ __launch_bounds__(256) void ascii_or_kernel(const uint8_t* __restrict__ s, uint64_t n, int aligned,
+                                                       unsigned long long* scal) {
+  uint32_t hi = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t nv = aligned ? n / 16 : 0;
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+    const uint4 w = reinterpret_cast<const uint4*>(s)[v];
+    hi |= w.x | w.y | w.z | w.w;
   }
+  for (uint64_t p = nv * 16 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += stride) hi |= s[p];
+  if (__ballot((hi & 0x80808080u) != 0) && (threadIdx.x & 63u) == 0) atomicOr(scal, 2ull);
+}
+
+// Threads without a resync code point within kLookback (long emoji / RI / combining runs): one
+// thread walks each maximal run of such 64-byte ranges once, from the run's own (unbounded) resync
+// point -- linear in the text overall. Then every tile is recounted.
+__global__ void seg_hard_kernel(const uint8_t* s, uint64_t n, const uint8_t* ptab, const uint8_t* hard, uint64_t ranges,
+                                unsigned long long* bits, const unsigned long long* scal) {
+  if (blockIdx.x != 0 || threadIdx.x != 0 || !scal[1]) return;
+  for (uint64_t c = 0; c < ranges; ++c) {
+    if (!hard[c]) continue;
+    uint64_t r = c;
+    while (r + 1 < ranges && hard[r + 1]) ++r;
+    const uint64_t a = c * 64, b = min((r + 1) * 64, n);
+    uint64_t q = a;
+    while (q > 0) {
+      do --q;
+      while (q > 0 && (s[q] & 0xC0) == 0x80);
+      uint64_t t = q;
+      if (resync(props_fast(ptab, decode(s, n, t)))) break;
+    }
+    uint64_t i = q;
+    SegState st = seg_init(props_fast(ptab, decode(s, n, i)));
+    for (uint64_t w = c; w <= r; ++w) bits[w] = 0;
+    while (i < b) {
+      const uint64_t pos = i;
+      const bool br = seg_step(st, props_fast(ptab, decode(s, n, i)));
+      if (pos >= a && br) bits[pos >> 6] |= 1ull << (pos & 63);
+    }
+    c = r;
+  }
+}
+__global__ __launch_bounds__(256) void recount_kernel(const unsigned long long* bits, uint64_t ranges, uint32_t* ucnt,
+                                                      uint64_t n_units, const unsigned long long* scal) {
+  if (!scal[1]) return;
+  const uint64_t u = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
+  const uint32_t lane = threadIdx.x & 63u;
+  if (u >= n_units) return;
+  uint32_t c = 0;
+  for (uint64_t w = u * (kTile / 64) + lane; w < min(ranges, (u + 1) * (kTile / 64)); w += 64) c += __popcll(bits[w]);
   for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
   if (lane == 0) ucnt[u] = c;
 }
+
 __global__ __launch_bounds__(1024) void unit_scan_kernel(const uint32_t* ucnt, uint64_t* ubase, uint64_t n_units,
                                                          unsigned long long* total) {
   __shared__ unsigned long long wsum[16];
@@ -311,54 +411,44 @@ __global__ __launch_bounds__(1024) void unit_scan_kernel(const uint32_t* ucnt, u
     run += ucnt[i];
   }
 }
-__global__ __launch_bounds__(256) void unit_write_kernel(const uint8_t* brk, uint64_t n, const uint64_t* ubase, uint64_t n_units,
-                                                         uint64_t* off) {
+
+// Grapheme starts (h.d_off) and text_chars (h.d_text32: the folded first code point per grapheme,
+// search.rs:406-412, grapheme.rs:112-119), one wave per tile in byte order: four boundary bits per
+// lane per step, a wave scan gives each start its slot, so consecutive lanes write consecutive slots.
+__global__ __launch_bounds__(256) void write_tile_kernel(const uint8_t* __restrict__ s, uint64_t n,
+                                                         const unsigned long long* __restrict__ bits,
+                                                         const uint64_t* __restrict__ ubase, uint64_t n_units,
+                                                         const uint16_t* __restrict__ ltab, int ci, uint64_t* __restrict__ off,
+                                                         uint32_t* __restrict__ text32) {
   const uint64_t u = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
-  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t lane = threadIdx.x & 63u;
   if (u >= n_units) return;  // whole waves
   uint64_t base = ubase[u];
-  const uint64_t b = u * kUnit, e = min(n, b + (uint64_t)kUnit);
-  for (uint64_t p0 = b; p0 < e; p0 += 256) {  // four flags per lane, in byte order across the wave
+  const uint64_t b = u * kTile, e = min(n, b + (uint64_t)kTile);
+  for (uint64_t p0 = b; p0 < e; p0 += 256) {
     const uint64_t p = p0 + 4ull * lane;
     uint32_t f = 0;
-    if (p + 4 <= e) {
-      f = *reinterpret_cast<const uint32_t*>(brk + p) & 0x01010101u;
-    } else {
-      for (uint32_t k = 0; k < 4; ++k)
-        if (p + k < e && brk[p + k]) f |= 1u << (8 * k);
+    if (p < e) {
+      f = (uint32_t)(bits[p >> 6] >> (p & 63)) & 0xFu;
+      if (p + 4 > e) f &= (1u << (uint32_t)(e - p)) - 1u;
     }
     const uint32_t c = __popc(f);
-    uint32_t x = c;  // inclusive scan of the lanes' counts
+    uint32_t x = c;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y = __shfl_up(x, o, 64);
       if (lane >= (uint32_t)o) x += y;
     }
     uint64_t o = base + x - c;
     for (uint32_t k = 0; k < 4; ++k)
-      if ((f >> (8 * k)) & 1u) off[o++] = p + k;
+      if ((f >> k) & 1u) {
+        uint64_t i = p + k;
+        off[o] = i;
+        const uint32_t cp = decode(s, n, i);
+        text32[o] = ci ? fold_fast(ltab, cp) : cp;
+        ++o;
+      }
     base += __shfl(x, 63, 64);
   }
-}
-
-__device__ uint32_t lower_first(uint32_t cp) {  // unicode.cpp lower_full, first code point
-  if (cp < 0x80) return (cp >= 'A' && cp <= 'Z') ? cp + 32 : cp;
-  uint32_t lo = 0, hi = sizeof(kLowerMap) / sizeof(kLowerMap[0]);
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (kLowerMap[mid].cp < cp) lo = mid + 1;
-    else hi = mid;
-  }
-  return (lo < sizeof(kLowerMap) / sizeof(kLowerMap[0]) && kLowerMap[lo].cp == cp) ? kLowerMap[lo].out[0] : cp;
-}
-
-// text_chars[g]: the folded first code point of grapheme g (search.rs:406-412, grapheme.rs:112-119)
-__global__ void fold_kernel(const uint8_t* s, uint64_t len, const uint64_t* off, uint64_t ng, int ci, uint32_t* text32) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= ng) return;
-  uint64_t i = off[g];
-  const uint64_t e = g + 1 < ng ? off[g + 1] : len;
-  const uint32_t cp = decode(s, e, i);
-  text32[g] = ci ? lower_first(cp) : cp;
 }
 
 }  // namespace
@@ -372,93 +462,122 @@ __global__ void fold_kernel(const uint8_t* s, uint64_t len, const uint64_t* off,
     }                                                     \
   } while (0)
 
-// flags of validate_kernel over the device copy of a haystack (synchronous): bit 0 invalid UTF-8,
-// bit 1 not ASCII
-int validate_device(const uint8_t* d_utf8, uint64_t len, hipStream_t st, unsigned int& flags_out, std::string& err) {
-  flags_out = 0;
-  if (!len) return FAC_OK;
-  unsigned int* flags = nullptr;
-  ST_TRY(hipMalloc((void**)&flags, 4));
-  struct Free {
-    void* p;
-    ~Free() {
-      if (p) (void)hipFree(p);
-    }
-  } f_flags{flags};
-  ST_TRY(hipMemsetAsync(flags, 0, 4, st));
-  const uint64_t chunks = (len + kValChunk - 1) / kValChunk;
-  hipLaunchKernelGGL(validate_kernel, dim3((uint32_t)((chunks + 255) / 256)), dim3(256), 0, st, d_utf8, len, flags);
-  ST_TRY(hipGetLastError());
-  ST_TRY(hipMemcpyAsync(&flags_out, flags, 4, hipMemcpyDeviceToHost, st));
-  ST_TRY(hipStreamSynchronize(st));
+namespace {
+struct BmpTabs {
+  uint8_t* p = nullptr;
+  uint16_t* l = nullptr;
+};
+// the BMP tables of `device`, built on first use (kept for the process)
+int bmp_tables(int device, hipStream_t st, BmpTabs& out, std::string& err) {
+  static std::mutex mu;
+  static BmpTabs tabs[64];
+  if (device < 0 || device >= 64) {
+    err = "device ordinal out of range";
+    return FAC_E_INVALID;
+  }
+  std::lock_guard<std::mutex> lk(mu);
+  BmpTabs& t = tabs[device];
+  if (!t.p) {
+    ST_TRY(hipMalloc((void**)&t.p, 0x10000));
+    ST_TRY(hipMalloc((void**)&t.l, 0x10000 * sizeof(uint16_t)));
+    hipLaunchKernelGGL(bmp_tables_kernel, dim3(256), dim3(256), 0, st, t.p, t.l);
+    ST_TRY(hipGetLastError());
+    ST_TRY(hipStreamSynchronize(st));
+  }
+  out = t;
   return FAC_OK;
 }
+}  // namespace
 
-// Device staging of a valid, non-ASCII UTF-8 haystack already resident at h.d_utf8: fills
-// h.n, h.d_off (grapheme byte starts), h.d_text32 (folded first code points) and the host copy of
-// the starts (fetched to the host only on demand: ensure_host).
-int stage_unicode_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err) {
+// Device staging of a haystack whose bytes are resident at h.d_utf8 (search.rs:196-203, 296-302):
+// mode -2 checks the UTF-8 and decides is_ascii on the device, 0 stages Unicode graphemes (the caller
+// checked the bytes / decided is_ascii for the whole text), 1 is an ASCII haystack (nothing to do).
+// Unicode: h.n, h.d_off (grapheme byte starts + off[n] = len) and h.d_text32 (folded first code
+// points); the scratch and the grapheme arrays are kept in h and reused when it is staged again.
+int stage_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err, int mode) {
   const uint64_t len = h.len;
-  uint8_t* brk = nullptr;
-  ST_TRY(hipMalloc((void**)&brk, std::max<uint64_t>(len, 16)));
-  struct Free {
-    void* p;
-    ~Free() {
-      if (p) (void)hipFree(p);
+  if (mode == 1 || len == 0) {
+    h.ascii = mode != 0;
+    h.n = h.ascii ? len : 0;
+    if (!h.ascii) {
+      if (h.off_cap < 1) {
+        if (h.d_off) ST_TRY(hipFree(h.d_off));
+        h.d_off = nullptr;
+        ST_TRY(hipMalloc((void**)&h.d_off, 16));
+        if (h.d_text32) ST_TRY(hipFree(h.d_text32));
+        h.d_text32 = nullptr;
+        ST_TRY(hipMalloc((void**)&h.d_text32, 16));
+        h.off_cap = 1;
+      }
+      ST_TRY(hipMemcpyAsync(h.d_off, &h.len, 8, hipMemcpyHostToDevice, st));
     }
-  } f_brk{brk};
-  const uint64_t chunks = (len + kChunk - 1) / kChunk;
-  uint8_t* hard = nullptr;
-  ST_TRY(hipMalloc((void**)&hard, std::max<uint64_t>(chunks, 16)));
-  Free f_hard{hard};
-  unsigned long long* scal = nullptr;  // [0] any hard chunk, [1] grapheme count
-  ST_TRY(hipMalloc((void**)&scal, 16));
-  Free f_scal{scal};
-  ST_TRY(hipMemsetAsync(brk, 0, len, st));
-  ST_TRY(hipMemsetAsync(hard, 0, chunks, st));
-  ST_TRY(hipMemsetAsync(scal, 0, 16, st));
-  hipLaunchKernelGGL(seg_chunk_kernel, dim3((uint32_t)((chunks + 255) / 256)), dim3(256), 0, st, h.d_utf8, len, brk,
-                     hard, reinterpret_cast<unsigned int*>(scal));
+    return FAC_OK;
+  }
+  BmpTabs tabs;
+  if (int trc = bmp_tables(h.device, st, tabs, err)) return trc;
+  const uint64_t ranges = (len + 63) / 64, n_units = (len + kTile - 1) / kTile;
+  // scratch: scal[4] | bits[ranges] | ubase[n_units] | ucnt[n_units] | hard[ranges]
+  const size_t need = 32 + ranges * 8 + n_units * 8 + n_units * 4 + ranges + 16;
+  if (h.stage_cap < need) {
+    if (h.d_stage) ST_TRY(hipFree(h.d_stage));
+    h.d_stage = nullptr;
+    h.stage_cap = 0;
+    ST_TRY(hipMalloc(&h.d_stage, need));
+    h.stage_cap = need;
+  }
+  unsigned long long* scal = static_cast<unsigned long long*>(h.d_stage);
+  unsigned long long* bits = scal + 4;
+  uint64_t* ubase = reinterpret_cast<uint64_t*>(bits + ranges);
+  uint32_t* ucnt = reinterpret_cast<uint32_t*>(ubase + n_units);
+  uint8_t* hard = reinterpret_cast<uint8_t*>(ucnt + n_units);
+  const int aligned = (reinterpret_cast<uintptr_t>(h.d_utf8) & 15u) == 0 ? 1 : 0;
+  ST_TRY(hipMemsetAsync(scal, 0, 32, st));
+  if (mode == -2) {
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h.device);
+    const uint64_t want = (len / 16 + 255) / 256;
+    hipLaunchKernelGGL(ascii_or_kernel, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)cus * 8))),
+                       dim3(256), 0, st, h.d_utf8, len, aligned, scal);
+    ST_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(seg_tile_kernel, dim3((uint32_t)n_units), dim3(256), 0, st, h.d_utf8, len, aligned, tabs.p, bits,
+                     ucnt, hard, scal, mode == -2 ? 1 : 0);
+  hipLaunchKernelGGL(seg_hard_kernel, dim3(1), dim3(64), 0, st, h.d_utf8, len, tabs.p, hard, ranges, bits, scal);
+  hipLaunchKernelGGL(recount_kernel, dim3((uint32_t)((n_units + 3) / 4)), dim3(256), 0, st, bits, ranges, ucnt, n_units,
+                     scal);
+  hipLaunchKernelGGL(unit_scan_kernel, dim3(1), dim3(1024), 0, st, ucnt, ubase, n_units, scal + 2);
   ST_TRY(hipGetLastError());
-  unsigned long long scal_h[2] = {0, 0};
-  ST_TRY(hipMemcpyAsync(scal_h, scal, 8, hipMemcpyDeviceToHost, st));
+  unsigned long long sc[4] = {0, 0, 0, 0};
+  ST_TRY(hipMemcpyAsync(sc, scal, sizeof(sc), hipMemcpyDeviceToHost, st));
   ST_TRY(hipStreamSynchronize(st));
-  if (scal_h[0]) {
-    hipLaunchKernelGGL(seg_hard_kernel, dim3(1), dim3(64), 0, st, h.d_utf8, len, hard, chunks, brk);
-    ST_TRY(hipGetLastError());
+  if (mode == -2) {
+    if (sc[0] & 1ull) {
+      err = "haystack is not valid UTF-8";
+      return FAC_E_INVALID;
+    }
+    h.ascii = !(sc[0] & 2ull);
+    if (h.ascii) {
+      h.n = len;
+      return FAC_OK;
+    }
   }
-  const uint64_t n_units = (len + kUnit - 1) / kUnit;
-  uint32_t* ucnt = nullptr;
-  uint64_t* ubase = nullptr;
-  ST_TRY(hipMalloc((void**)&ucnt, std::max<uint64_t>(n_units, 1) * 4));
-  Free f_ucnt{ucnt};
-  ST_TRY(hipMalloc((void**)&ubase, std::max<uint64_t>(n_units, 1) * 8));
-  Free f_ubase{ubase};
-  const uint32_t ugrid = (uint32_t)((n_units + 3) / 4);
-  if (n_units) {
-    hipLaunchKernelGGL(unit_count_kernel, dim3(ugrid), dim3(256), 0, st, brk, len, ucnt, n_units);
-    hipLaunchKernelGGL(unit_scan_kernel, dim3(1), dim3(1024), 0, st, ucnt, ubase, n_units, scal + 1);
-    ST_TRY(hipGetLastError());
-  }
-  ST_TRY(hipMemcpyAsync(scal_h + 1, scal + 1, 8, hipMemcpyDeviceToHost, st));
-  ST_TRY(hipStreamSynchronize(st));
-  h.n = scal_h[1];
+  h.ascii = false;
+  h.n = sc[2];
   if (h.n > grapheme_limit()) return FAC_E_HAYSTACK_TOO_LARGE;
-  // grapheme starts = positions with brk set, plus off[n] = len (a shard's halo end: an emission
-  // at j == n of an open-ended shard reads it before the halo check flags the window)
-  ST_TRY(hipMalloc((void**)&h.d_off, (h.n + 1) * 8));
+  if (h.off_cap < h.n + 1) {  // grapheme starts + off[n] = len (a shard's halo end), folded first chars
+    if (h.d_off) ST_TRY(hipFree(h.d_off));
+    if (h.d_text32) ST_TRY(hipFree(h.d_text32));
+    h.d_off = nullptr;
+    h.d_text32 = nullptr;
+    h.off_cap = 0;
+    ST_TRY(hipMalloc((void**)&h.d_off, (h.n + 1) * 8));
+    ST_TRY(hipMalloc((void**)&h.d_text32, std::max<uint64_t>(h.n * 4, 16)));
+    h.off_cap = h.n + 1;
+  }
   ST_TRY(hipMemcpyAsync(h.d_off + h.n, &h.len, 8, hipMemcpyHostToDevice, st));
-  if (n_units) {
-    hipLaunchKernelGGL(unit_write_kernel, dim3(ugrid), dim3(256), 0, st, brk, len, ubase, n_units, h.d_off);
-    ST_TRY(hipGetLastError());
-  }
-  ST_TRY(hipMalloc((void**)&h.d_text32, std::max<uint64_t>(h.n * 4, 16)));
-  if (h.n) {
-    hipLaunchKernelGGL(fold_kernel, dim3((uint32_t)((h.n + 255) / 256)), dim3(256), 0, st, h.d_utf8, len, h.d_off, h.n,
-                       e.case_insensitive ? 1 : 0, h.d_text32);
-    ST_TRY(hipGetLastError());
-  }
-  ST_TRY(hipStreamSynchronize(st));
+  hipLaunchKernelGGL(write_tile_kernel, dim3((uint32_t)((n_units + 3) / 4)), dim3(256), 0, st, h.d_utf8, len, bits, ubase,
+                     n_units, tabs.l, e.case_insensitive ? 1 : 0, h.d_off, h.d_text32);
+  ST_TRY(hipGetLastError());
   return FAC_OK;
 }
 

@@ -20,6 +20,8 @@
 #include <deque>
 #include <mutex>
 #include <string>
+#include <new>
+#include <stdexcept>
 #include <thread>
 #include <vector>
 
@@ -95,7 +97,15 @@ void worker_loop(const StreamCore* s, StreamWorker* w) {
       t = w->q.front();
       w->q.pop_front();
     }
-    run_window_task(*s, *w, *t);
+    try {  // an allocation failure becomes the window's error code, not std::terminate
+      run_window_task(*s, *w, *t);
+    } catch (const std::bad_alloc&) {
+      t->rc = FAC_E_OOM;
+      t->err = "out of host memory while searching a stream window";
+    } catch (const std::exception& ex) {
+      t->rc = FAC_E_OOM;
+      t->err = std::string("stream window: ") + ex.what();
+    }
     {
       std::lock_guard<std::mutex> lk(g_done_mu);
       t->done = true;

@@ -149,6 +149,9 @@ SIGNATURES = {
     "fac_segment_graphemes": (ctypes.c_uint64, [ctypes.c_char_p, ctypes.c_uint64, _u64p,
                                                 ctypes.c_uint64]),
     "fac_fold_first_char": (ctypes.c_uint32, [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int32]),
+    "fac_haystack_stage_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                 ctypes.POINTER(ctypes.c_void_p), _u64p]),
+    "fac_edge_order": (None, [ctypes.POINTER(ctypes.c_uint32), _u64p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32)]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

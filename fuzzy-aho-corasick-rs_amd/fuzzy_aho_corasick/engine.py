@@ -471,6 +471,29 @@ class StagedHaystack:
         self._dev_out = None  # growable device record buffer (search_device)
 
     @classmethod
+    def from_device(cls, engine: FuzzyAhoCorasick, d_utf8: int, length: int, stream=None,
+                    reuse: "StagedHaystack" = None) -> "StagedHaystack":
+        """fac_haystack_stage_device: search_raw's staging (UTF-8 check, is_ascii, UAX #29 segmentation
+        and folding, search.rs:196-203/296-302) of `length` bytes already in HBM at device address
+        `d_utf8` (borrowed: keep the buffer alive). `reuse`: a haystack staged this way before, whose
+        device buffers are reused (it is restaged in place and returned)."""
+        h = ctypes.c_void_p(reuse._h.value if reuse is not None else None)
+        eg = ctypes.c_uint64()
+        rc = _native.lib.fac_haystack_stage_device(engine._h, ctypes.c_void_p(d_utf8), length, ctypes.c_void_p(stream or 0),
+                                                   ctypes.byref(h), ctypes.byref(eg))
+        if rc:
+            _raise(rc, eg.value)
+        obj = reuse
+        if obj is None:
+            obj = cls.__new__(cls)
+            obj.engine, obj.data, obj._h, obj._dev_out = engine, None, h, None
+            obj.base, obj.open_end, obj.plan = 0, False, None
+        obj.owned_bytes = length
+        obj.graphemes = int(_native.lib.fac_haystack_graphemes(obj._h))
+        obj.owned_windows = int(_native.lib.fac_haystack_owned_windows(obj._h))
+        return obj
+
+    @classmethod
     def shard(cls, engine: FuzzyAhoCorasick, data: bytes, n_shards: int, shard: int, is_ascii: int = -1):
         plan = _native.shard_plan(engine.max_match_graphemes(), data, n_shards, shard, is_ascii)
         return cls(engine, data, _shard=plan)

@@ -178,6 +178,16 @@ uint64_t fac_max_match_graphemes(const fac_engine* engine);
  * repeatedly with no host->device traffic. */
 int fac_haystack_stage(const fac_engine* engine, const uint8_t* utf8, uint64_t len,
                        fac_haystack** out, uint64_t* err_graphemes);
+/* search_raw's staging of UTF-8 bytes that are already in device memory (`d_utf8`, a device
+ * pointer on the engine's device; borrowed, not copied: keep it alive and unchanged while the
+ * haystack is used): the UTF-8 check (the C ABI's stand-in for `&str`), is_ascii, UAX #29
+ * segmentation and folding, all on the device (search.rs:196-203, 296-302), ordered on `stream`
+ * (a hipStream_t; NULL = the engine's) and complete on return. `*hay`: NULL to create a haystack,
+ * or one returned earlier by this function for the same engine, whose device buffers are then
+ * reused (staging again per search costs no allocation). Errors as fac_haystack_stage; on error
+ * `*hay` is left as passed. */
+int fac_haystack_stage_device(const fac_engine* engine, const uint8_t* d_utf8, uint64_t len, void* stream,
+                              fac_haystack** hay, uint64_t* err_graphemes);
 uint64_t fac_haystack_graphemes(const fac_haystack* hay);
 /* Byte start of every staged grapheme (the device segmentation's result, for tests / hosts that
  * map windows to bytes). Writes up to `cap` entries, returns the grapheme count. */
@@ -293,6 +303,12 @@ uint32_t fac_engine_max_edits_fast(const fac_engine* engine);
  * (UAX #29) and per-grapheme first-code-point folding. Writes up to `cap` entries. */
 uint64_t fac_segment_graphemes(const uint8_t* utf8, uint64_t len, uint64_t* starts, uint64_t cap);
 uint32_t fac_fold_first_char(const uint8_t* utf8, uint64_t len, int32_t case_insensitive);
+
+/* Host-side builder helper exposed for tests: the order in which the reference iterates a trie
+ * node's `transitions: FxHashMap<String, u32>` (builder.rs:336-342; FxHasher structs.rs:95-156 +
+ * std's hashbrown) given the children's graphemes in insertion order (code points: grapheme i is
+ * cps[off[i] .. off[i+1])). Writes the n insertion indices in iteration order to `order`. */
+void fac_edge_order(const uint32_t* cps, const uint64_t* off, uint64_t n, uint32_t* order);
 
 #ifdef __cplusplus
 }

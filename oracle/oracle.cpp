@@ -116,6 +116,7 @@ struct Engine {
   size_t beam_width = 0;  // 0 = None
   bool has_auto_beam = false;
   size_t ab_budget = 0, ab_width = 0;
+  int beam_rule = 2;  // g_beam_rule at build time
   float min_symbol_similarity = 0.f;
   // prefilter (prefilter.rs:69-93)
   bool bitap_ok = false;
@@ -132,6 +133,334 @@ struct Match {
   float similarity;
   uint8_t ins, del, sub, swp, edits;
 };
+
+// Restatement modes (orc_set_modes). Edge order: 0 = insertion order, 1 = the iteration order of
+// the reference's `FxHashMap<String, u32>` transitions (FxHasher + hashbrown, below). Beam rule:
+// 0 = canonical (penalty, queue position), 1 = the same with ties at the cut broken towards the
+// LATEST queue position (tie-sensitivity diagnostic only), 2 = core's select_nth_unstable_by.
+int g_edge_order = 1;
+int g_beam_rule = 2;
+int g_sel_limit = 16;  // select.rs partition_at_index_loop's round limit (tests lower it to reach median_of_medians)
+
+// ------------------------------------------------------------------------------------------
+// FxHashMap<String, u32> iteration order (builder.rs:208-214 inserts, :336-342 iterates)
+// ------------------------------------------------------------------------------------------
+// The crate's own FxHasher (structs.rs:95-156) over `impl Hash for str` = write(bytes) then
+// write_u8(0xff) (core::hash::Hasher::write_str).
+uint64_t fx_hash_str(const std::string& s) {
+  const uint64_t K = 0x517cc1b727220a95ull;
+  uint64_t h = 0;
+  auto add = [&](uint64_t i) { h = (((h << 5) | (h >> 59)) ^ i) * K; };
+  const unsigned char* p = reinterpret_cast<const unsigned char*>(s.data());
+  size_t n = s.size();
+  while (n >= 8) {
+    uint64_t w = 0;
+    for (int b = 0; b < 8; ++b) w |= (uint64_t)p[b] << (8 * b);
+    add(w);
+    p += 8;
+    n -= 8;
+  }
+  if (n >= 4) {
+    uint32_t w = 0;
+    for (int b = 0; b < 4; ++b) w |= (uint32_t)p[b] << (8 * b);
+    add(w);
+    p += 4;
+    n -= 4;
+  }
+  for (size_t b = 0; b < n; ++b) add(p[b]);
+  add(0xff);
+  return h;
+}
+
+std::string utf8_of(const std::u32string& g) {
+  std::string o;
+  for (char32_t c : g) {
+    if (c < 0x80) o += (char)c;
+    else if (c < 0x800) { o += (char)(0xC0 | (c >> 6)); o += (char)(0x80 | (c & 0x3F)); }
+    else if (c < 0x10000) {
+      o += (char)(0xE0 | (c >> 12)); o += (char)(0x80 | ((c >> 6) & 0x3F)); o += (char)(0x80 | (c & 0x3F));
+    } else {
+      o += (char)(0xF0 | (c >> 18)); o += (char)(0x80 | ((c >> 12) & 0x3F));
+      o += (char)(0x80 | ((c >> 6) & 0x3F)); o += (char)(0x80 | (c & 0x3F));
+    }
+  }
+  return o;
+}
+
+// hashbrown's RawTable as std's HashMap uses it on x86-64 (SSE2 groups of 16 control bytes),
+// restricted to what an insert-only map does: `insert` = reserve(1) (grow when growth_left == 0,
+// to capacity max(items + 1, full_capacity + 1), re-inserting the old buckets in index order) then
+// the first EMPTY control byte along the triangular group probe from h1 = hash & bucket_mask
+// (fix_insert_slot for tables smaller than a group). Iteration visits full buckets in index order.
+struct SwissOrder {
+  std::vector<int> slot;       // bucket -> item (-1 = EMPTY)
+  std::vector<uint64_t> hash;  // item -> hash
+  size_t items = 0, growth_left = 0;
+  size_t buckets() const { return slot.size(); }
+  static size_t cap_of_mask(size_t mask) { return mask < 8 ? mask : ((mask + 1) / 8) * 7; }
+  static size_t buckets_for(size_t cap) {
+    if (cap < 8) return cap < 4 ? 4 : 8;  // (String, u32) entries: hashbrown's small-table minimum is 3
+    size_t adj = cap * 8 / 7, b = 1;
+    while (b < adj) b <<= 1;
+    return b;
+  }
+  bool ctrl_empty(size_t i) const {  // control byte i of [0, buckets + 16): real, padding or mirror
+    const size_t nb = buckets(), m = std::max<size_t>(nb, 16);
+    if (i < nb) return slot[i] < 0;
+    if (i >= m) return slot[i - m] < 0;
+    return true;  // the EMPTY padding of a table smaller than one group
+  }
+  size_t find_insert_slot(uint64_t h) const {
+    const size_t mask = buckets() - 1;
+    size_t pos = (size_t)h & mask, stride = 0;
+    for (;;) {
+      for (size_t bit = 0; bit < 16; ++bit)
+        if (ctrl_empty(pos + bit)) {
+          size_t idx = (pos + bit) & mask;
+          if (slot[idx] >= 0)  // fix_insert_slot: first EMPTY of the aligned group at 0
+            for (idx = 0; slot[idx] >= 0; ++idx) {}
+          return idx;
+        }
+      stride += 16;
+      pos = (pos + stride) & mask;
+    }
+  }
+  void insert(uint64_t h) {
+    const int id = (int)hash.size();
+    hash.push_back(h);
+    if (growth_left == 0) {
+      const size_t full_cap = slot.empty() ? 0 : cap_of_mask(buckets() - 1);
+      const size_t nb = buckets_for(std::max(items + 1, full_cap + 1));
+      std::vector<int> old;
+      old.swap(slot);
+      slot.assign(nb, -1);
+      for (int it : old)
+        if (it >= 0) slot[find_insert_slot(hash[(size_t)it])] = it;
+      growth_left = cap_of_mask(nb - 1) - items;
+    }
+    slot[find_insert_slot(h)] = id;
+    --growth_left;
+    ++items;
+  }
+  std::vector<int> iteration_order() const {
+    std::vector<int> o;
+    for (int it : slot)
+      if (it >= 0) o.push_back(it);
+    return o;
+  }
+};
+
+// The children of one node in the reference's `transitions.iter()` order, given their insertion order.
+std::vector<std::u32string> hashbrown_order(const std::vector<std::u32string>& inserted) {
+  SwissOrder t;
+  for (auto& g : inserted) t.insert(fx_hash_str(utf8_of(g)));
+  std::vector<std::u32string> o;
+  for (int it : t.iteration_order()) o.push_back(inserted[(size_t)it]);
+  return o;
+}
+
+// ------------------------------------------------------------------------------------------
+// core::slice::select_nth_unstable_by (Rust >= 1.81: introselect with the ipnsort partition),
+// restated for the beam (search.rs:584-587). is_less(a, b) = a.penalties.total_cmp(&b.penalties)
+// == Less. core/src/slice/select.rs: partition_at_index, partition_at_index_loop,
+// median_of_medians, median_of_ninthers, ninther, median_idx, min_index, max_index;
+// core/src/slice/sort/shared/pivot.rs: choose_pivot, median3_rec, median3;
+// core/src/slice/sort/unstable/quicksort.rs: partition, partition_lomuto_branchless_cyclic
+// (State is 28 bytes <= 96); core/src/slice/sort/shared/smallsort.rs: insertion_sort_shift_left.
+// ------------------------------------------------------------------------------------------
+namespace rsel {
+template <typename T, typename L>
+void insertion_sort_shift_left(T* v, size_t len, size_t offset, L& is_less) {
+  for (size_t i = offset; i < len; ++i) {
+    if (!is_less(v[i], v[i - 1])) continue;
+    T tmp = v[i];
+    size_t j = i;
+    for (;;) {
+      v[j] = v[j - 1];
+      --j;
+      if (j == 0 || !is_less(tmp, v[j - 1])) break;
+    }
+    v[j] = tmp;
+  }
+}
+template <typename T, typename L>
+size_t median3(const T* v, size_t a, size_t b, size_t c, L& is_less) {
+  const bool x = is_less(v[a], v[b]), y = is_less(v[a], v[c]);
+  if (x == y) {
+    const bool z = is_less(v[b], v[c]);
+    return (z ^ x) ? c : b;
+  }
+  return a;
+}
+template <typename T, typename L>
+size_t median3_rec(const T* v, size_t a, size_t b, size_t c, size_t n, L& is_less) {
+  if (n * 8 >= 64) {
+    const size_t n8 = n / 8;
+    a = median3_rec(v, a, a + n8 * 4, a + n8 * 7, n8, is_less);
+    b = median3_rec(v, b, b + n8 * 4, b + n8 * 7, n8, is_less);
+    c = median3_rec(v, c, c + n8 * 4, c + n8 * 7, n8, is_less);
+  }
+  return median3(v, a, b, c, is_less);
+}
+template <typename T, typename L>
+size_t choose_pivot(const T* v, size_t len, L& is_less) {  // len >= 8
+  const size_t d8 = len / 8, a = 0, b = d8 * 4, c = d8 * 7;
+  if (len < 64) return median3(v, a, b, c, is_less);
+  return median3_rec(v, a, b, c, d8, is_less);
+}
+// partition_lomuto_branchless_cyclic over w[0..m) against `pivot`: elements are taken in the order
+// w[1], ..., w[m-1], w[0] (w[0] is held in the gap value); each is written to w[num_lt] and the
+// previous occupant of w[num_lt] moves into the gap left by the previous element.
+template <typename T, typename L>
+size_t lomuto_cyclic(T* w, size_t m, const T& pivot, L& is_less) {
+  if (m == 0) return 0;
+  const T gap_value = w[0];
+  size_t gap = 0, num_lt = 0;
+  for (size_t r = 1; r < m; ++r) {
+    const bool lt = is_less(w[r], pivot);
+    w[gap] = w[num_lt];
+    w[num_lt] = w[r];
+    gap = r;
+    num_lt += lt;
+  }
+  const bool lt = is_less(gap_value, pivot);
+  w[gap] = w[num_lt];
+  w[num_lt] = gap_value;
+  return num_lt + lt;
+}
+template <typename T, typename L>
+size_t partition(T* v, size_t len, size_t pivot, L& is_less) {
+  if (len == 0) return 0;
+  std::swap(v[0], v[pivot]);
+  const T p = v[0];
+  const size_t num_lt = lomuto_cyclic(v + 1, len - 1, p, is_less);
+  std::swap(v[0], v[num_lt]);
+  return num_lt;
+}
+template <typename T, typename L>
+size_t min_index(const T* v, size_t len, L& is_less) {
+  size_t acc = 0;
+  for (size_t i = 1; i < len; ++i)
+    if (is_less(v[i], v[acc])) acc = i;
+  return acc;
+}
+template <typename T, typename L>
+size_t max_index(const T* v, size_t len, L& is_less) {
+  size_t acc = 0;
+  for (size_t i = 1; i < len; ++i)
+    if (is_less(v[acc], v[i])) acc = i;
+  return acc;
+}
+template <typename T, typename L>
+size_t median_idx(const T* v, L& is_less, size_t a, size_t b, size_t c) {
+  if (is_less(v[c], v[a])) std::swap(a, c);
+  if (is_less(v[c], v[b])) return c;
+  if (is_less(v[b], v[a])) return a;
+  return b;
+}
+template <typename T, typename L>
+void ninther(T* v, L& is_less, size_t a, size_t b, size_t c, size_t d, size_t e, size_t f, size_t g, size_t h,
+             size_t i) {
+  b = median_idx(v, is_less, a, b, c);
+  h = median_idx(v, is_less, g, h, i);
+  if (is_less(v[h], v[b])) std::swap(b, h);
+  if (is_less(v[f], v[d])) std::swap(d, f);
+  if (is_less(v[e], v[d])) {
+    // the middle triple's median is d
+  } else if (is_less(v[f], v[e])) {
+    d = f;
+  } else {
+    if (is_less(v[e], v[b])) std::swap(v[e], v[b]);
+    else if (is_less(v[h], v[e])) std::swap(v[e], v[h]);
+    return;
+  }
+  if (is_less(v[d], v[b])) d = b;
+  else if (is_less(v[h], v[d])) d = h;
+  std::swap(v[d], v[e]);
+}
+template <typename T, typename L>
+void median_of_medians(T* v, size_t len, L& is_less, size_t k);
+template <typename T, typename L>
+size_t median_of_ninthers(T* v, size_t len, L& is_less) {
+  const size_t frac = len <= 1024 ? len / 12 : (len <= 128 * 1024 ? len / 64 : len / 1024);
+  const size_t pivot = frac / 2, lo = len / 2 - pivot, hi = frac + lo, gap = (len - 9 * frac) / 4;
+  size_t a = lo - 4 * frac - gap, b = hi + gap;
+  for (size_t i = lo; i < hi; ++i) {
+    ninther(v, is_less, a, i - frac, b, a + 1, i, b + 1, a + 2, i + frac, b + 2);
+    a += 3;
+    b += 3;
+  }
+  median_of_medians(v + lo, frac, is_less, pivot);
+  return partition(v, len, lo + pivot, is_less);
+}
+template <typename T, typename L>
+void median_of_medians(T* v, size_t len, L& is_less, size_t k) {
+  for (;;) {
+    if (len <= 16) {
+      if (len >= 2) insertion_sort_shift_left(v, len, 1, is_less);
+      return;
+    }
+    if (k == len - 1) { std::swap(v[max_index(v, len, is_less)], v[k]); return; }
+    if (k == 0) { std::swap(v[min_index(v, len, is_less)], v[k]); return; }
+    const size_t p = median_of_ninthers(v, len, is_less);
+    if (p == k) return;
+    if (p > k) {
+      len = p;
+    } else {
+      v += p + 1;
+      len -= p + 1;
+      k -= p + 1;
+    }
+  }
+}
+template <typename T, typename L>
+void partition_at_index_loop(T* v, size_t len, size_t index, L& is_less) {
+  int limit = g_sel_limit;
+  const T* ancestor = nullptr;
+  T anc_copy{};
+  for (;;) {
+    if (len <= 16) {
+      if (len >= 2) insertion_sort_shift_left(v, len, 1, is_less);
+      return;
+    }
+    if (limit == 0) {
+      median_of_medians(v, len, is_less, index);
+      return;
+    }
+    --limit;
+    const size_t pivot_pos = choose_pivot(v, len, is_less);
+    if (ancestor && !is_less(*ancestor, v[pivot_pos])) {
+      auto le = [&](const T& a, const T& b) { return !is_less(b, a); };
+      const size_t mid = partition(v, len, pivot_pos, le) + 1;
+      if (index <= mid) return;
+      v += mid;
+      len -= mid;
+      index -= mid;
+      ancestor = nullptr;
+      continue;
+    }
+    const size_t mid = partition(v, len, pivot_pos, is_less);
+    if (mid < index) {
+      anc_copy = v[mid];  // the pivot stays at v[mid] for the rest of the call
+      ancestor = &anc_copy;
+      v += mid + 1;
+      len -= mid + 1;
+      index -= mid + 1;
+    } else if (mid > index) {
+      len = mid;
+    } else {
+      return;
+    }
+  }
+}
+template <typename T, typename L>
+void select_nth_unstable_by(T* v, size_t len, size_t index, L is_less) {  // partition_at_index
+  if (index >= len) std::abort();
+  if (index == len - 1) std::swap(v[max_index(v, len, is_less)], v[index]);
+  else if (index == 0) std::swap(v[min_index(v, len, is_less)], v[index]);
+  else partition_at_index_loop(v, len, index, is_less);
+}
+}  // namespace rsel
 
 // ------------------------------------------------------------------------------------------
 // Builder (builder.rs:181-484)
@@ -286,9 +615,11 @@ void build(Engine& e) {
     if (any) { e.has_limits = true; e.limits = m; }
   }
   for (auto& p : e.patterns) e.has_pattern_limits |= p.has_limits;
-  // edges (builder.rs:336-342) — insertion order (see header)
+  // edges (builder.rs:336-342): the transitions map's iteration order (or insertion order, mode 0)
+  e.beam_rule = g_beam_rule;
   for (auto& nd : nodes) {
     nd.edges.clear();
+    if (g_edge_order == 1) nd.order = hashbrown_order(nd.order);
     for (auto& g : nd.order) {
       uint32_t fc = g.empty() ? 0 : g[0];
       bool single = g.size() == 1 && g[0] < 0x80;  // g.len() == 1 (UTF-8 bytes)
@@ -523,10 +854,19 @@ struct Searcher {
       queue.push_back({0, start, start, start, 0.f, 0, 0});
       size_t q_idx = 0;
       while (q_idx < queue.size()) {
-        if (effective_beam) {  // :577-589, canonical tie rule (see header)
+        if (effective_beam) {  // :577-589
           size_t bw = effective_beam;
           size_t remaining = queue.size() - q_idx;
-          if (remaining > bw * 2) beam_select(queue, q_idx, bw);
+          if (remaining > bw * 2) {
+            if (e.beam_rule == 2) {
+              rsel::select_nth_unstable_by(queue.data() + q_idx, remaining, bw - 1, [](const State& a, const State& b) {
+                return total_order_bits(a.pen) < total_order_bits(b.pen);
+              });
+              queue.resize(q_idx + bw);
+            } else {
+              beam_select(queue, q_idx, bw, e.beam_rule == 1);
+            }
+          }
         }
         State st = queue[q_idx];
         if (deg_hist) deg_hist[73] = std::max<uint64_t>(deg_hist[73], queue.size() - q_idx);
@@ -672,11 +1012,13 @@ struct Searcher {
     std::memcpy(&u, &f, 4);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
   }
-  // Canonical beam: keep the bw smallest by (penalty total order, position), stable.
-  static void beam_select(std::vector<State>& q, size_t q_idx, size_t bw) {
+  // Canonical beam: keep the bw smallest by (penalty total order, position), stable; `latest`
+  // breaks ties at the cut towards the latest positions instead (diagnostic).
+  static void beam_select(std::vector<State>& q, size_t q_idx, size_t bw, bool latest) {
     size_t n = q.size() - q_idx;
     std::vector<uint64_t> keys(n);
-    for (size_t i = 0; i < n; ++i) keys[i] = ((uint64_t)total_order_bits(q[q_idx + i].pen) << 32) | (uint64_t)i;
+    for (size_t i = 0; i < n; ++i)
+      keys[i] = ((uint64_t)total_order_bits(q[q_idx + i].pen) << 32) | (uint64_t)(latest ? n - 1 - i : i);
     std::vector<uint64_t> tmp = keys;
     std::nth_element(tmp.begin(), tmp.begin() + (bw - 1), tmp.end());
     uint64_t cut = tmp[bw - 1];
@@ -885,6 +1227,34 @@ void* orc_build(const orc_config* cfg, uint64_t n_patterns, const uint32_t* glen
 }
 
 void orc_free(void* h) { delete static_cast<Engine*>(h); }
+
+// Restatement modes for engines built afterwards (see g_edge_order / g_beam_rule); -1 keeps a mode.
+// The oracle's transitions-map order for one node's children (see hashbrown_order), for tests.
+void orc_edge_order(const uint32_t* cps, const uint64_t* off, uint64_t n, uint32_t* order) {
+  SwissOrder t;
+  for (uint64_t i = 0; i < n; ++i) t.insert(fx_hash_str(utf8_of(std::u32string(cps + off[i], cps + off[i + 1]))));
+  std::vector<int> o = t.iteration_order();
+  for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)o[i];
+}
+
+// rsel::select_nth_unstable_by over n f32 keys (total_cmp), for tests: perm[i] = the original index
+// of the element at position i afterwards.
+void orc_select_nth(const float* keys, uint64_t n, uint64_t index, uint32_t* perm) {
+  struct E { float k; uint32_t i; };
+  std::vector<E> v(n);
+  for (uint64_t i = 0; i < n; ++i) v[i] = {keys[i], (uint32_t)i};
+  rsel::select_nth_unstable_by(v.data(), (size_t)n, (size_t)index, [](const E& a, const E& b) {
+    return Searcher::total_order_bits(a.k) < Searcher::total_order_bits(b.k);
+  });
+  for (uint64_t i = 0; i < n; ++i) perm[i] = v[i].i;
+}
+
+// sel_limit: select.rs's 16 partition rounds before median_of_medians (tests only).
+void orc_set_modes(int32_t edge_order, int32_t beam_rule, int32_t sel_limit) {
+  if (edge_order >= 0) g_edge_order = edge_order;
+  if (beam_rule >= 0) g_beam_rule = beam_rule;
+  if (sel_limit >= 0) g_sel_limit = sel_limit;
+}
 uint64_t* orc_deg_hist() { return g_deg_hist; }
 
 uint64_t orc_num_nodes(void* h) { return static_cast<Engine*>(h)->nodes.size(); }

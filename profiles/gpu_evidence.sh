@@ -14,7 +14,7 @@ cd "$ROOT"
 has() { [[ " $WHAT " == *" $1 "* ]]; }
 
 if has tests; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 900 --timeout-method thread \
     > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
   tail -3 "$OUT/pytest_gpu.log"
 fi

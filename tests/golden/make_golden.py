@@ -4,7 +4,8 @@ expected raw matches computed by the CPU oracle (oracle/, itself pinned by the r
 assertions in tests/test_reference_behaviour.py and tests/test_host_and_oracle.py).
 
 The reference (Rust) cannot run here, so these vectors are oracle outputs: they pin the GPU engine
-and guard the oracle against regressions. Run from the repo root:  python tests/golden/make_golden.py
+and guard the oracle against regressions. The oracle's default restatement modes apply (edge order
+= the transitions map's FxHasher + hashbrown order, beam = core's select_nth_unstable_by). Run from the repo root:  python tests/golden/make_golden.py
 """
 import json
 import os

@@ -79,11 +79,21 @@ _lib.orc_prefilter_windows.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.
 _lib.orc_apply.restype = ctypes.c_uint64
 _lib.orc_apply.argtypes = [ctypes.POINTER(orc_match), ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
                            ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+_lib.orc_set_modes.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
 _lib.orc_bitap_ends.restype = ctypes.c_uint64
 _lib.orc_bitap_ends.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64,
                                 ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
 
 _GRAPHEME = regex.compile(r"\X")
+
+
+def set_modes(edge_order: int = -1, beam_rule: int = -1, sel_limit: int = -1):
+    """Oracle restatement modes for engines built afterwards (oracle.cpp g_edge_order / g_beam_rule):
+    edge order 0 = insertion, 1 = the reference's FxHashMap iteration order (default); beam rule
+    0 = canonical ties, 1 = ties towards the latest queue position, 2 = select_nth_unstable_by
+    (default); sel_limit = select.rs's 16 partition rounds before median_of_medians (tests lower it).
+    Diagnostics only: the defaults are what the GPU path implements."""
+    _lib.orc_set_modes(edge_order, beam_rule, sel_limit)
 
 
 def graphemes(s: str):
@@ -349,7 +359,7 @@ class PreparedText:
                                    np.array(bo or [0], np.uint64))
         self._arrs = (goff, cps, boff)
 
-    def _run(self, threshold, prefilter, w0, w1, data=None, arrs=None, n=None):
+    def _run(self, threshold, prefilter, w0, w1, data=None, arrs=None, n=None, full=False):
         data = self.data if data is None else data
         goff, cps, boff = self._arrs if arrs is None else arrs
         n = (0 if self.ascii else self.n) if n is None else n
@@ -363,20 +373,25 @@ class PreparedText:
                                      ctypes.byref(out), ctypes.byref(cnt), ctypes.byref(popped), w0, w1)
         if rc:
             raise RuntimeError(f"oracle error {rc}")
-        rows = [(out[i].start, out[i].end, out[i].pattern) for i in range(cnt.value)]
+        if full:
+            rows = [(out[i].start, out[i].end, out[i].pattern, out[i].similarity, out[i].ins, out[i].dele,
+                     out[i].sub, out[i].swp, out[i].edits) for i in range(cnt.value)]
+        else:
+            rows = [(out[i].start, out[i].end, out[i].pattern) for i in range(cnt.value)]
         _lib.orc_matches_free(out)
         return rows
 
-    def search(self, threshold, prefilter=False, threads=1):
-        """Raw (start, end, pattern) triples of search_raw / Prefiltered::raw."""
+    def search(self, threshold, prefilter=False, threads=1, full=False):
+        """Raw (start, end, pattern) triples of search_raw / Prefiltered::raw (full=True: every field,
+        without the pre-filter)."""
         if threads <= 1:
-            return self._run(threshold, prefilter, 0, 0xFFFFFFFF)
+            return self._run(threshold, prefilter, 0, 0xFFFFFFFF, full=full)
         import threading
         res = [None] * threads
         if not prefilter:
             def work(t):
                 a, b = self.n * t // threads, self.n * (t + 1) // threads
-                res[t] = self._run(threshold, False, a, b)
+                res[t] = self._run(threshold, False, a, b, full=full)
         else:
             # stream windows: byte slices cut at spaces (ASCII) with max_match + 1 of overlap
             over = 64 + 4 * max(len(p.pattern) for p in self.engine.patterns_)

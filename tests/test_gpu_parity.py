@@ -112,6 +112,34 @@ def test_differential_random(seed, vocab, filler, per_edge_only, root_cache, mon
     assert total > 0
 
 
+@pytest.mark.parametrize("sel_limit", ["16", "1", "0"])
+def test_beam_select_restatement(sel_limit, monkeypatch):
+    """The beam cut is core's select_nth_unstable_by restated (search.rs:584-587; oracle.cpp rsel,
+    search_kernels.hip beam_select): dense ties (many equal penalties), widths 1 (min_index), up to 8
+    (insertion sort of <= 16 pending) and beyond (pivots, partitions, the equal-to-ancestor split),
+    with every window searched from the root and with the prefix cache forced on. sel_limit lowers
+    select.rs's 16 partition rounds on both sides so median_of_medians runs too."""
+    import oracle_harness as OH
+    monkeypatch.setenv("FAC_SEL_LIMIT", sel_limit)
+    OH.set_modes(sel_limit=int(sel_limit))
+    try:
+        rng = Rng(0x5EED0BEA)
+        words = ["abcab", "bacab", "cabba", "abcba", "aabbc", "ccab", "bbca", "acbcab", "cbacbab", "abab"]
+        for t in range(24):
+            pats = [words[rng.next() % len(words)] + "abc"[rng.next() % 3] for _ in range(6 + rng.next() % 20)]
+            hay = "".join("abc "[rng.next() % 4] for _ in range(150 + rng.next() % 250))
+            bw = [1, 2, 3, 5, 8, 9, 13, 21, 40][t % 9]
+            if t % 2:
+                monkeypatch.setenv("FAC_RC_MIN", "1")
+            else:
+                monkeypatch.setenv("FAC_NO_RC", "1")
+            compare(B().fuzzy(L().edits(2 + t % 2)).beam_width(bw), pats, hay, 0.3 + 0.1 * (t % 4))
+            monkeypatch.delenv("FAC_RC_MIN", raising=False)
+            monkeypatch.delenv("FAC_NO_RC", raising=False)
+    finally:
+        OH.set_modes(sel_limit=16)
+
+
 @pytest.mark.parametrize("seed,vocab,filler", [
     (0x1234_5678_9abc_def1, ASCII_VOCAB, ASCII_FILLER),
     (0xdead_beef_0bad_f00d, UNI_VOCAB, UNI_FILLER),
@@ -540,6 +568,55 @@ def test_device_segmentation_matches_regex():
         n = _native.lib.fac_haystack_grapheme_starts(staged._h, buf, len(data) + 1)
         got = list(buf[:n]) if not data.isascii() else list(range(len(data)))
         assert got == want, t[:60]
+
+
+def test_stage_device_restaging_matches_regex_and_oracle():
+    """fac_haystack_stage_device (search_raw's staging of bytes already in HBM, bench.py's timed
+    step): one haystack object restaged over texts of growing and shrinking size -- multi-tile
+    Unicode, combining / emoji / RI runs across 16 KiB tile edges, ASCII, empty -- has the regex
+    module's \\X grapheme starts and searches like the oracle; invalid UTF-8 is refused."""
+    import ctypes
+    import numpy as np
+    import regex
+    import torch
+    from fuzzy_aho_corasick import DeviceError, _native
+    from fuzzy_aho_corasick.engine import StagedHaystack
+    pieces = ["a", "é", "é", "क्ष", "👩‍💻", "🇫🇷", "\r\n", "가", " ", "Ω", "̈", "ẍ́", "Σ", "؀", "😀́",
+              "word ", "naïve ", "Москва ", "hello "]
+    rng = Rng(0xdec0de)
+    texts = []
+    for size in (70_000, 300, 40_000, 0, 120_000, 5):
+        t = "".join(pieces[rng.next() % len(pieces)] for _ in range(size // 3))
+        texts.append(t)
+    texts.insert(2, "x" * 16383 + "́" * 40 + "y" * 20000)  # a combining run across a tile edge
+    texts.insert(4, "a" + "́" * 20000 + "b" * 100)         # the sequential (hard) path across tiles
+    texts.insert(5, "plain ascii hello wolrd " * 2000)
+    b = B().fuzzy(L().edits(1)).case_insensitive(True)
+    pats = ["hello", "naïve", "москва", "word"]
+    eng = b.build(pats)
+    orc = OracleEngine(b, pats)
+    st = None
+    for t in texts:
+        data = t.encode("utf-8")
+        dev = torch.from_numpy(np.frombuffer(data + b"\0", dtype=np.uint8).copy()).to("cuda")
+        st = StagedHaystack.from_device(eng, dev.data_ptr(), len(data), reuse=st)
+        want, pos = [], 0
+        for g in regex.findall(r"\X", t):
+            want.append(pos)
+            pos += len(g.encode("utf-8"))
+        if data.isascii():
+            assert st.graphemes == len(data)
+        else:
+            buf = (ctypes.c_uint64 * (len(data) + 1))()
+            n = _native.lib.fac_haystack_grapheme_starts(st._h, buf, len(data) + 1)
+            assert list(buf[:n]) == want, t[:40]
+        got = sorted((r[0], r[1], r[2], r[3], r[8]) for r in st.search_windows(0.7)[0])
+        exp = sorted((r[0], r[1], r[2], r[3], r[8]) for r in orc.raw_rows(t, 0.7))
+        assert got == exp, t[:40]
+        del dev
+    bad = torch.tensor(list(b"ok \xc3\x28 bad"), dtype=torch.uint8, device="cuda")
+    with pytest.raises(DeviceError):
+        StagedHaystack.from_device(eng, bad.data_ptr(), bad.numel(), reuse=st)
 
 
 def _srows(ms):

@@ -222,7 +222,7 @@ def test_stream_many_windows_in_order():
 
 @pytest.mark.gpu
 def test_device_utf8_check_matches_python():
-    """fac_haystack_stage checks the bytes on the device (validate_kernel: per 256-byte chunk, from its
+    """fac_haystack_stage checks the bytes on the device (validate_kernel: per 16-byte chunk, from its
     first non-continuation byte) and decides search.rs:196's is_ascii there: accepted exactly when
     Python's strict decoder (like Rust's str::from_utf8: no overlongs, surrogates, > U+10FFFF,
     truncations or stray continuation bytes) accepts, with invalid sequences planted at and around
