@@ -316,7 +316,7 @@ def run_c5(args, world, rank, local):
     import torch.distributed as dist
     from fuzzy_aho_corasick import workloads as W
     from fuzzy_aho_corasick.engine import StagedHaystack
-    from fuzzy_aho_corasick.distributed import gather_records
+    from fuzzy_aho_corasick.distributed import gather_device, records_to_tensor, stream_share_windows
 
     block_bytes = int((args.mib if args.mib is not None else DEFAULT_MIB["c5"]) * (1 << 20))
     wl = W.config("c5", block_bytes, seed=5)
@@ -326,16 +326,9 @@ def run_c5(args, world, rank, local):
     B = len(block)
     staged = StagedHaystack(engine, block + block[:overlap])
     total = int(args.gib * (1 << 30)) // B * B  # whole blocks
-    share = total // 8
-    lo, hi = rank * share, (rank + 1) * share  # this GPU's range (1/8 of the stream)
-    windows = []  # (g_begin, g_end, commit, base) in the staged buffer
-    c = lo
-    while c < hi:
-        c1 = min(hi, (c // B + 1) * B)
-        o = c % B
-        end = min(total, c1 + overlap)
-        windows.append((o, o + (end - c), c1 - c, c))
-        c = c1
+    # this GPU's 1/8 of the stream (weak scaling: rank r takes share r)
+    windows = stream_share_windows(total, B, rank, overlap)
+    processed_rank = sum(w[2] for w in windows)
     stream = torch.cuda.current_stream().cuda_stream
 
     def step():
@@ -346,9 +339,10 @@ def run_c5(args, world, rank, local):
             pf_ms += st.prefilter_ms
             k_ms += st.kernel_ms
         recs = np.concatenate(parts)
-        if world > 1:
-            gathered = gather_records(recs, 0)
-            return (len(gathered) if gathered is not None else 0), pf_ms, k_ms
+        if world > 1:  # the window records (host, after the per-window ranking) to HBM, then RCCL
+            dev = records_to_tensor(recs).to(torch.device("cuda", local), non_blocking=False)
+            gathered = gather_device(dev, len(recs), 0)
+            return (gathered.numel() // 32 if gathered is not None else 0), pf_ms, k_ms
         return len(recs), pf_ms, k_ms
 
     for _ in range(args.warmup):
@@ -371,14 +365,17 @@ def run_c5(args, world, rank, local):
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    processed = (hi - lo) * world * args.steps
+    pr = torch.tensor([processed_rank], dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(pr)
+    processed = int(pr.item()) * args.steps
     K = max(1, args.steps)
     dev_ms = (pf + km) / K
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
     if rank == 0:
-        bytes_step = (hi - lo) + 32 * matches / K / world
+        bytes_step = processed_rank + 32 * matches / K / world
         achieved = bytes_step / (dev_ms / 1e3) / 1e9 if dev_ms > 0 else 0.0
         print(json.dumps({
             "metric": METRIC, "value": processed / elapsed / 1e9, "unit": "Gchars/s", "n_gpus": world,
@@ -387,7 +384,7 @@ def run_c5(args, world, rank, local):
             "data": f"synthetic: {total / (1 << 30):g} GiB stream = repeats of one {B}-byte block "
                     "(SURVEY.md §8(d) generator, 1 planted needle per MiB), resident in HBM",
             "config": {"workload": "c5: " + WORKLOAD["c5"], "patterns": len(wl.patterns),
-                       "stream_bytes": total, "bytes_per_gpu": hi - lo, "stream_windows_per_gpu": len(windows),
+                       "stream_bytes": total, "bytes_per_gpu": processed_rank, "stream_windows_per_gpu": len(windows),
                        "window_overlap_graphemes": overlap, "threshold": wl.threshold,
                        "parallelism": f"dp{world} (each GPU its 1/8 of the stream; RCCL gather of Match records)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -405,14 +402,36 @@ def run_c5(args, world, rank, local):
 
 def run_dry(args, world, rank):
     """Plumbing check without a GPU: the same launch, barrier / max-over-ranks timing and record
-    gather to rank 0 (gloo), with every rank contributing synthetic records instead of a search."""
+    gather to rank 0 (gloo). Default: every rank contributes synthetic records. With --shard: the
+    real shard path on a small haystack of the config (--mib, default 1/32 MiB) -- fac_shard_plan
+    cuts it, every rank searches only its owned windows of its halo-sliced piece with the CPU oracle
+    (test infrastructure standing in for the GPU search), the records are gathered to rank 0, which
+    checks the union against the oracle's search of the whole haystack."""
     import numpy as np
     import torch
     import torch.distributed as dist
     from fuzzy_aho_corasick._native import MATCH_DTYPE
-    from fuzzy_aho_corasick.distributed import gather_records
+    from fuzzy_aho_corasick.distributed import gather_records, gather_rows
     if world > 1:
         dist.init_process_group("gloo")
+    parity = None
+    if args.shard:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        from fuzzy_aho_corasick import _native
+        from fuzzy_aho_corasick import workloads as W
+        from oracle_harness import OracleEngine, graphemes  # test infrastructure (dry run only)
+        nbytes = int((args.mib if args.mib is not None else 1 / 32) * (1 << 20))
+        seed = {"c1": 1, "c2": 2, "c3": 3, "c4": 2, "c5": 5}[args.config]
+        wl = W.config(args.config, nbytes, seed=seed, hay_seed=seed + 1000)
+        if args.config == "c3":  # the dry run's oracle is single-threaded: a slice of the 10K patterns
+            wl.patterns = wl.patterns[:500]
+        orc = OracleEngine(W.builder_for(wl), wl.patterns)
+        mmg = max(len(graphemes(p)) for p in wl.patterns) + wl.edits
+        a, b, e, asc, _ = _native.shard_plan(mmg, wl.haystack, world, rank)
+        piece = wl.haystack[a:e]
+        owned = (b - a) if asc else len(graphemes(piece[: b - a].decode("utf-8")))
+        rows = orc.raw_rows(piece, wl.threshold, windows=(0, owned)) if b > a else []
+        mine = [(s + a, en + a) + tuple(r) for (s, en, *r) in rows]
     recs = np.zeros(1000 + rank, dtype=MATCH_DTYPE)
     recs["start"] = np.arange(len(recs)) + (rank << 32)
     got = 0
@@ -420,19 +439,29 @@ def run_dry(args, world, rank):
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        g = gather_records(recs, 0) if world > 1 else recs
+        if args.shard:
+            g = gather_rows(mine) if world > 1 else mine
+        else:
+            g = gather_records(recs, 0) if world > 1 else recs
         got = len(g) if g is not None else 0
     elapsed = time.perf_counter() - t0
+    if args.shard and rank == 0:
+        parity = sorted(g) == sorted(orc.raw_rows(wl.haystack, wl.threshold))
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     if rank == 0:
+        cfg = {"workload": "dry-run", "records_gathered_per_step": got}
+        if args.shard:
+            cfg.update(workload=f"dry-run shard: {args.config} slice of {len(wl.haystack)} bytes, {len(wl.patterns)} patterns, "
+                                "oracle compute", shard_union_equals_whole=parity)
         print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "Gchars/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": elapsed / max(1, args.steps) * 1e3,
-                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "none",
-                          "data": "dry run: launcher and record-gather plumbing only, no search",
-                          "config": {"workload": "dry-run", "records_gathered_per_step": got}}), flush=True)
+                          "higher_is_better": True, "scaling": "strong" if args.shard else "weak", "vs_baseline": None,
+                          "dtype": "none",
+                          "data": "dry run: launcher, shard plan and record-gather plumbing, no GPU search",
+                          "config": cfg}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -513,7 +513,9 @@ int stage_haystack_device(const Engine& e, const uint8_t* d_utf8, uint64_t len, 
 // segmentation; stream.rs:134-139 grapheme_indices(true).rev().nth(n - 1)); false if it has fewer
 bool nth_grapheme_from_end(const uint8_t* s, uint64_t len, uint64_t n, uint64_t& off);
 // shard planning (unicode.cpp): p is a grapheme boundary whose segmentation does not depend on
-// anything before it (previous char ASCII and not CR, char at p neither Extend, ZWJ nor SpacingMark)
+// anything before it (previous char ASCII and not CR, char at p neither Extend, ZWJ nor SpacingMark;
+// or the char at p starts a cluster in every context: GCB Other, not ExtPict, no InCB class, and
+// the previous char is not Prepend)
 bool safe_cut(const uint8_t* s, uint64_t n, uint64_t p);
 // str::is_ascii (search.rs:196), eight bytes at a time
 bool ascii_only(const uint8_t* s, uint64_t n);

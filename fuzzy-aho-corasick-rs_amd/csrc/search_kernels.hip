@@ -409,66 +409,92 @@ __device__ void sel_small_sort(uint4* v, uint32_t len) {
   wave_mem_fence();
 }
 
-// ---- median_of_medians fallback (select.rs), taken after 16 partition rounds: one lane, sequential
-__device__ void sel_s_swap(uint4* v, uint32_t a, uint32_t b) {
-  const uint4 t = v[a];
-  v[a] = v[b];
-  v[b] = t;
+// ---- median_of_medians fallback (select.rs), taken after 16 partition rounds: one lane, sequential,
+// over an element accessor (SelG: states in the global scratch, SelL: (key, position) pairs in LDS)
+struct SelG {
+  uint4* v;
+  using E = uint4;
+  __device__ uint32_t key(uint32_t i) const { return sel_key(v[i]); }
+  __device__ E get(uint32_t i) const { return v[i]; }
+  __device__ void set(uint32_t i, const E& e) const { v[i] = e; }
+  __device__ SelG sub(uint32_t o) const { return SelG{v + o}; }
+};
+struct SelL {
+  uint32_t* K;
+  uint16_t* I;
+  using E = uint2;
+  __device__ uint32_t key(uint32_t i) const { return K[i]; }
+  __device__ E get(uint32_t i) const { return make_uint2(K[i], I[i]); }
+  __device__ void set(uint32_t i, const E& e) const {
+    K[i] = e.x;
+    I[i] = (uint16_t)e.y;
+  }
+  __device__ SelL sub(uint32_t o) const { return SelL{K + o, I + o}; }
+};
+template <typename A>
+__device__ void sel_s_swap(const A& v, uint32_t a, uint32_t b) {
+  const typename A::E t = v.get(a);
+  v.set(a, v.get(b));
+  v.set(b, t);
 }
-__device__ void sel_s_insertion(uint4* v, uint32_t len) {
+template <typename A>
+__device__ void sel_s_insertion(const A& v, uint32_t len) {  // insertion_sort_shift_left(v, 1)
   for (uint32_t i = 1; i < len; ++i) {
-    const uint4 tmp = v[i];
-    const uint32_t kt = sel_key(tmp);
-    if (!(kt < sel_key(v[i - 1]))) continue;
+    const typename A::E tmp = v.get(i);
+    const uint32_t kt = v.key(i);
+    if (!(kt < v.key(i - 1))) continue;
     uint32_t j = i;
     for (;;) {
-      v[j] = v[j - 1];
+      v.set(j, v.get(j - 1));
       --j;
-      if (j == 0 || !(kt < sel_key(v[j - 1]))) break;
+      if (j == 0 || !(kt < v.key(j - 1))) break;
     }
-    v[j] = tmp;
+    v.set(j, tmp);
   }
 }
-__device__ uint32_t sel_s_partition(uint4* v, uint32_t len, uint32_t pivot) {  // quicksort.rs partition
+template <typename A>
+__device__ uint32_t sel_s_partition(const A& v, uint32_t len, uint32_t pivot) {  // quicksort.rs partition
   if (len == 0) return 0;
   sel_s_swap(v, 0, pivot);
-  const uint32_t pk = sel_key(v[0]);
-  uint4* w = v + 1;
+  const uint32_t pk = v.key(0);
+  const A w = v.sub(1);
   const uint32_t m = len - 1;
   uint32_t num_lt = 0;
-  if (m) {
-    const uint4 gv = w[0];
+  if (m) {  // partition_lomuto_branchless_cyclic
+    const typename A::E gv = w.get(0);
+    const bool glt = w.key(0) < pk;
     uint32_t gap = 0;
     for (uint32_t r = 1; r < m; ++r) {
-      const uint4 x = w[r];
-      const bool lt = sel_key(x) < pk;
-      w[gap] = w[num_lt];
-      w[num_lt] = x;
+      const typename A::E x = w.get(r);
+      const bool lt = w.key(r) < pk;
+      w.set(gap, w.get(num_lt));
+      w.set(num_lt, x);
       gap = r;
       num_lt += lt ? 1u : 0u;
     }
-    const bool lt = sel_key(gv) < pk;
-    w[gap] = w[num_lt];
-    w[num_lt] = gv;
-    num_lt += lt ? 1u : 0u;
+    w.set(gap, w.get(num_lt));
+    w.set(num_lt, gv);
+    num_lt += glt ? 1u : 0u;
   }
   sel_s_swap(v, 0, num_lt);
   return num_lt;
 }
-__device__ uint32_t sel_s_median_idx(const uint4* v, uint32_t a, uint32_t b, uint32_t c) {
-  if (sel_key(v[c]) < sel_key(v[a])) {
+template <typename A>
+__device__ uint32_t sel_s_median_idx(const A& v, uint32_t a, uint32_t b, uint32_t c) {
+  if (v.key(c) < v.key(a)) {
     const uint32_t t = a;
     a = c;
     c = t;
   }
-  if (sel_key(v[c]) < sel_key(v[b])) return c;
-  if (sel_key(v[b]) < sel_key(v[a])) return a;
+  if (v.key(c) < v.key(b)) return c;
+  if (v.key(b) < v.key(a)) return a;
   return b;
 }
 // ninther (select.rs): the median of the medians of (a, b, c), (d, e, f), (g, h, i), swapped into e
-__device__ void sel_s_ninther(uint4* v, uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e, uint32_t f,
+template <typename A>
+__device__ void sel_s_ninther(const A& v, uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e, uint32_t f,
                               uint32_t g, uint32_t h, uint32_t i) {
-  auto lt = [&](uint32_t x, uint32_t y) { return sel_key(v[x]) < sel_key(v[y]); };
+  auto lt = [&](uint32_t x, uint32_t y) { return v.key(x) < v.key(y); };
   b = sel_s_median_idx(v, a, b, c);
   h = sel_s_median_idx(v, g, h, i);
   if (lt(h, b)) { const uint32_t t = b; b = h; h = t; }
@@ -486,10 +512,10 @@ __device__ void sel_s_ninther(uint4* v, uint32_t a, uint32_t b, uint32_t c, uint
   else if (lt(h, d)) d = h;
   sel_s_swap(v, d, e);
 }
-template <int D>
-__device__ void sel_s_mom(uint4* v, uint32_t len, uint32_t k);
-template <int D>
-__device__ uint32_t sel_s_ninthers(uint4* v, uint32_t len) {  // median_of_ninthers
+template <int D, typename A>
+__device__ void sel_s_mom(const A& v, uint32_t len, uint32_t k);
+template <int D, typename A>
+__device__ uint32_t sel_s_ninthers(const A& v, uint32_t len) {  // median_of_ninthers
   const uint32_t frac = len <= 1024u ? len / 12u : (len <= 128u * 1024u ? len / 64u : len / 1024u);
   const uint32_t pivot = frac / 2u, lo = len / 2u - pivot, hi = frac + lo, gap = (len - 9u * frac) / 4u;
   uint32_t a = lo - 4u * frac - gap, b = hi + gap;
@@ -498,11 +524,12 @@ __device__ uint32_t sel_s_ninthers(uint4* v, uint32_t len) {  // median_of_ninth
     a += 3u;
     b += 3u;
   }
-  sel_s_mom<D - 1>(v + lo, frac, pivot);
+  sel_s_mom<D - 1>(v.sub(lo), frac, pivot);
   return sel_s_partition(v, len, lo + pivot);
 }
-template <int D>
-__device__ void sel_s_mom(uint4* v, uint32_t len, uint32_t k) {  // median_of_medians
+template <int D, typename A>
+__device__ void sel_s_mom(const A& v0, uint32_t len, uint32_t k) {  // median_of_medians
+  A v = v0;
   for (;;) {
     if (len <= 16u) {
       if (len >= 2u) sel_s_insertion(v, len);
@@ -511,7 +538,7 @@ __device__ void sel_s_mom(uint4* v, uint32_t len, uint32_t k) {  // median_of_me
     if (k == len - 1u || k == 0u) {  // max_index keeps the first maximum, min_index the first minimum
       uint32_t acc = 0;
       for (uint32_t i = 1; i < len; ++i)
-        if (k ? sel_key(v[acc]) < sel_key(v[i]) : sel_key(v[i]) < sel_key(v[acc])) acc = i;
+        if (k ? v.key(acc) < v.key(i) : v.key(i) < v.key(acc)) acc = i;
       sel_s_swap(v, acc, k);
       return;
     }
@@ -526,11 +553,304 @@ __device__ void sel_s_mom(uint4* v, uint32_t len, uint32_t k) {  // median_of_me
     if (p > k) {
       len = p;
     } else {
-      v += p + 1u;
+      v = v.sub(p + 1u);
       len -= p + 1u;
       k -= p + 1u;
     }
   }
+}
+
+template <uint32_t QCAP>
+__device__ void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t bw, uint4* scratch, uint32_t limit0) {
+  const uint32_t lane = lane_id();
+  const uint32_t P = tail - head;
+  uint4* qq = reinterpret_cast<uint4*>(q);
+  if (bw == 1) {  // partition_at_index, index == 0: min_index (first minimum), swapped to the front
+    uint32_t best = 0xFFFFFFFFu;
+    for (uint32_t i = lane; i < P; i += 64u) best = min(best, sel_key(qq[(head + i) & (QCAP - 1)]));
+    best = wave_min_u32(best);
+    uint32_t first = 0xFFFFFFFFu;
+    for (uint32_t i = lane; i < P; i += 64u)
+      if (sel_key(qq[(head + i) & (QCAP - 1)]) == best) first = min(first, i);
+    first = wave_min_u32(first);
+    const uint4 e = qq[(head + first) & (QCAP - 1)];
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) qq[head & (QCAP - 1)] = e;
+    __builtin_amdgcn_wave_barrier();
+    tail = head + 1u;
+    return;
+  }
+  uint4* A = scratch;
+  uint4* T = scratch + QCAP;
+  uint32_t* W = reinterpret_cast<uint32_t*>(scratch + 2u * QCAP);
+  for (uint32_t i = lane; i < P; i += 64u) A[i] = qq[(head + i) & (QCAP - 1)];
+  wave_mem_fence();
+  // partition_at_index_loop (bw - 1 is never len - 1 here: P > 2 bw)
+  uint32_t a = 0, len = P, index = bw - 1u, limit = limit0;
+  bool has_anc = false;
+  uint32_t anc = 0;
+  for (;;) {
+    if (len <= 16u) {
+      if (len >= 2u) sel_small_sort(A + a, len);
+      break;
+    }
+    if (limit == 0) {
+      if (lane == 0) sel_s_mom<4>(SelG{A + a}, len, index);
+      wave_mem_fence();
+      break;
+    }
+    --limit;
+    const uint32_t pp = sel_pivot(A + a, len);
+    const uint32_t pk = sel_key(A[a + pp]);
+    if (has_anc && !(anc < pk)) {  // pivot equal to the ancestor pivot: split off the equal run
+      const uint32_t mid = sel_partition(A + a, T + a, W, len, pp, true) + 1u;
+      if (index <= mid) break;
+      a += mid;
+      len -= mid;
+      index -= mid;
+      has_anc = false;
+      continue;
+    }
+    const uint32_t mid = sel_partition(A + a, T + a, W, len, pp, false);
+    if (mid < index) {
+      has_anc = true;
+      anc = pk;
+      a += mid + 1u;
+      len -= mid + 1u;
+      index -= mid + 1u;
+    } else if (mid > index) {
+      len = mid;
+    } else {
+      break;
+    }
+  }
+  for (uint32_t i = lane; i < bw; i += 64u) qq[(head + i) & (QCAP - 1)] = A[i];
+  __builtin_amdgcn_wave_barrier();
+  tail = head + bw;
+}
+
+// The same select for rings of <= 256 states, on (key, ring position) pairs in the wave's LDS
+// dedup-claim words (free between batches; zeroed again on exit): K[256] keys, I[256] positions
+// (u16), W[8] "is less" masks + W[8..12) their exclusive counts. Each partition reads every moved
+// element into registers (<= 4 per lane) before any is written; the survivors' states are gathered
+// from the ring at the end. Same algorithm and result as beam_select (global scratch, larger rings).
+constexpr uint32_t SEL_LDS_WORDS = 256 + 128 + 8 + 4;
+static_assert(SEL_LDS_WORDS <= 512, "the LDS select must fit the smallest claim region");
+
+__device__ uint32_t sel_pivot_lds(const uint32_t* K, uint32_t a, uint32_t len) {
+  const uint32_t lane = lane_id();
+  uint32_t s[4] = {len / 8, 0u, 0u, 0u};
+  uint32_t D = 0;
+  if (len >= 64)
+    while (D < 3 && s[D] >= 8) {
+      s[D + 1] = s[D] / 8;
+      ++D;
+    }
+  uint32_t nleaf = 1;
+  for (uint32_t d = 0; d < D; ++d) nleaf *= 3;
+  uint32_t p = 0, k = 0;
+  if (lane < nleaf) {
+    uint32_t base = 0, rem = lane, div = nleaf;
+    for (uint32_t d = 0; d < D; ++d) {
+      div /= 3;
+      const uint32_t dig = rem / div;
+      rem -= dig * div;
+      base += (dig == 0 ? 0u : dig == 1 ? 4u : 7u) * s[d];
+    }
+    const uint32_t pa = base, pb = base + 4u * s[D], pc = base + 7u * s[D];
+    sel_median3(pa, K[a + pa], pb, K[a + pb], pc, K[a + pc], p, k);
+  }
+  for (uint32_t n = nleaf; n > 1; n /= 3) {
+    const int b = (int)(3u * lane) & 63;
+    const uint32_t pa = (uint32_t)__shfl((int)p, b), ka = (uint32_t)__shfl((int)k, b);
+    const uint32_t pb = (uint32_t)__shfl((int)p, (b + 1) & 63), kb = (uint32_t)__shfl((int)k, (b + 1) & 63);
+    const uint32_t pc = (uint32_t)__shfl((int)p, (b + 2) & 63), kc = (uint32_t)__shfl((int)k, (b + 2) & 63);
+    if (lane < n / 3) sel_median3(pa, ka, pb, kb, pc, kc, p, k);
+  }
+  return shfl_u32(p, 0);
+}
+
+// partition (see sel_partition) of the elements at [a, a + len), len <= 256
+__device__ uint32_t sel_partition_lds(uint32_t* K, uint16_t* I, uint32_t* W, uint32_t a, uint32_t len, uint32_t pp,
+                                      bool le) {
+  const uint32_t lane = lane_id();
+  const uint32_t m = len - 1;
+  const uint32_t pkey = K[a + pp];
+  const uint16_t pidx = I[a + pp];
+  auto src = [&](uint32_t r) -> uint32_t {
+    const uint32_t x = r < m ? r + 1u : 1u;
+    return a + (x == pp ? 0u : x);
+  };
+  // phase 1: the lt masks; every lane keeps its processing positions' elements and lt destinations
+  uint32_t F = 0, ek[4], ei[4], ed[4];
+#pragma unroll
+  for (uint32_t c = 0; c < 4; ++c) {
+    const uint32_t b = c * 64u + lane;
+    const bool valid = b < m;
+    ek[c] = 0;
+    ei[c] = 0;
+    bool lt = false;
+    if (valid) {
+      const uint32_t sp = src(b + 1u);
+      ek[c] = K[sp];
+      ei[c] = I[sp];
+      lt = le ? ek[c] <= pkey : ek[c] < pkey;
+    }
+    const uint64_t mk = __ballot(lt);
+    ed[c] = lt ? F + prefix_below(mk) : 0xFFFFFFFFu;  // w position L_r
+    if (lane == 0 && c * 64u < m) {
+      W[2u * c] = (uint32_t)mk;
+      W[2u * c + 1u] = (uint32_t)(mk >> 32);
+      W[8u + c] = F;
+    }
+    F += (uint32_t)__popcll(mk);
+  }
+  wave_mem_fence();
+  auto bit = [&](uint32_t b) -> bool { return (W[2u * (b >> 6) + ((b >> 5) & 1u)] >> (b & 31u)) & 1u; };
+  auto lcount = [&](uint32_t r) -> uint32_t {
+    const uint32_t b = r - 1u, c = b >> 6, o = b & 63u;
+    const uint64_t mk = ((uint64_t)W[2u * c + 1u] << 32) | W[2u * c];
+    return W[8u + c] + (uint32_t)__popcll(mk & ((1ull << o) - 1ull));
+  };
+  const bool lt_m = bit(m - 1u);
+  // phase 2: the other positions pull their element (w positions p >= F)
+  uint32_t gk[4], gi[4];
+#pragma unroll
+  for (uint32_t c = 0; c < 4; ++c) {
+    const uint32_t p = F + c * 64u + lane;
+    gk[c] = 0;
+    gi[c] = 0;
+    if (p < m) {
+      uint32_t sidx;
+      if (p == F && !lt_m) {
+        sidx = m;
+      } else {
+        uint32_t r = p + 1u;
+        while (bit(r - 2u)) r = lcount(r) + 1u;
+        sidx = r - 1u;
+      }
+      const uint32_t sp = src(sidx);
+      gk[c] = K[sp];
+      gi[c] = I[sp];
+    }
+  }
+  wave_mem_fence();
+  // phase 3: write back; w position q goes to a + q + 1, except w[F - 1] -> a and the pivot -> a + F
+#pragma unroll
+  for (uint32_t c = 0; c < 4; ++c) {
+    if (ed[c] != 0xFFFFFFFFu) {
+      const uint32_t d = a + (ed[c] == F - 1u ? 0u : ed[c] + 1u);
+      K[d] = ek[c];
+      I[d] = (uint16_t)ei[c];
+    }
+    const uint32_t p = F + c * 64u + lane;
+    if (p < m) {
+      K[a + p + 1u] = gk[c];
+      I[a + p + 1u] = (uint16_t)gi[c];
+    }
+  }
+  if (lane == 0) {
+    K[a + F] = pkey;
+    I[a + F] = pidx;
+  }
+  wave_mem_fence();
+  return F;
+}
+
+template <uint32_t QCAP>
+__device__ void beam_select_lds(KState* q, uint32_t head, uint32_t& tail, uint32_t bw, uint32_t* scratch, uint32_t limit0) {
+  static_assert(QCAP <= 256, "LDS select: rings of up to 256 states");
+  const uint32_t lane = lane_id();
+  const uint32_t P = tail - head;
+  uint4* qq = reinterpret_cast<uint4*>(q);
+  if (bw == 1) {  // partition_at_index, index == 0: min_index (first minimum), swapped to the front
+    uint32_t best = 0xFFFFFFFFu;
+    for (uint32_t i = lane; i < P; i += 64u) best = min(best, sel_key(qq[(head + i) & (QCAP - 1)]));
+    best = wave_min_u32(best);
+    uint32_t first = 0xFFFFFFFFu;
+    for (uint32_t i = lane; i < P; i += 64u)
+      if (sel_key(qq[(head + i) & (QCAP - 1)]) == best) first = min(first, i);
+    first = wave_min_u32(first);
+    const uint4 e = qq[(head + first) & (QCAP - 1)];
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) qq[head & (QCAP - 1)] = e;
+    __builtin_amdgcn_wave_barrier();
+    tail = head + 1u;
+    return;
+  }
+  uint32_t* K = scratch;
+  uint16_t* I = reinterpret_cast<uint16_t*>(scratch + 256);
+  uint32_t* W = scratch + 384;
+  for (uint32_t i = lane; i < P; i += 64u) {
+    K[i] = sel_key(qq[(head + i) & (QCAP - 1)]);
+    I[i] = (uint16_t)i;
+  }
+  wave_mem_fence();
+  uint32_t a = 0, len = P, index = bw - 1u, limit = limit0;
+  bool has_anc = false;
+  uint32_t anc = 0;
+  for (;;) {
+    if (len <= 16u) {
+      if (len >= 2u) {  // insertion_sort_shift_left: stable by key
+        uint32_t k = 0xFFFFFFFFu, ix = 0;
+        if (lane < len) {
+          k = K[a + lane];
+          ix = I[a + lane];
+        }
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < len; ++j) {
+          const uint32_t kj = shfl_u32(k, (int)j);
+          rank += (kj < k || (kj == k && j < lane)) ? 1u : 0u;
+        }
+        wave_mem_fence();
+        if (lane < len) {
+          K[a + rank] = k;
+          I[a + rank] = (uint16_t)ix;
+        }
+        wave_mem_fence();
+      }
+      break;
+    }
+    if (limit == 0) {  // median_of_medians: one lane, sequential
+      if (lane == 0) sel_s_mom<4>(SelL{K + a, I + a}, len, index);
+      wave_mem_fence();
+      break;
+    }
+    --limit;
+    const uint32_t pp = sel_pivot_lds(K, a, len);
+    const uint32_t pk = K[a + pp];
+    if (has_anc && !(anc < pk)) {  // pivot equal to the ancestor pivot: split off the equal run
+      const uint32_t mid = sel_partition_lds(K, I, W, a, len, pp, true) + 1u;
+      if (index <= mid) break;
+      a += mid;
+      len -= mid;
+      index -= mid;
+      has_anc = false;
+      continue;
+    }
+    const uint32_t mid = sel_partition_lds(K, I, W, a, len, pp, false);
+    if (mid < index) {
+      has_anc = true;
+      anc = pk;
+      a += mid + 1u;
+      len -= mid + 1u;
+      index -= mid + 1u;
+    } else if (mid > index) {
+      len = mid;
+    } else {
+      break;
+    }
+  }
+  // the survivors' states, gathered from the ring (every read before any write; bw < 128 here)
+  uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+  if (lane < bw) v0 = qq[(head + I[lane]) & (QCAP - 1)];
+  if (lane + 64u < bw) v1 = qq[(head + I[lane + 64u]) & (QCAP - 1)];
+  wave_mem_fence();
+  if (lane < bw) qq[(head + lane) & (QCAP - 1)] = v0;
+  if (lane + 64u < bw) qq[(head + lane + 64u) & (QCAP - 1)] = v1;
+  for (uint32_t i = lane; i < SEL_LDS_WORDS; i += 64u) scratch[i] = 0u;  // claim words stay <= 64
+  wave_mem_fence();
+  tail = head + bw;
 }
 
 // Diagnostics only (FAC_BEAM_CANONICAL, rounds 1-2's rule): keep the bw smallest by (penalty,
@@ -584,75 +904,6 @@ __device__ void beam_select_canonical(KState* q, uint32_t head, uint32_t& tail, 
     w += __popcll(mk);
     eq_seen += __popcll(meq);
   }
-  tail = head + bw;
-}
-
-template <uint32_t QCAP>
-__device__ void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t bw, uint4* scratch, uint32_t limit0) {
-  const uint32_t lane = lane_id();
-  const uint32_t P = tail - head;
-  uint4* qq = reinterpret_cast<uint4*>(q);
-  if (bw == 1) {  // partition_at_index, index == 0: min_index (first minimum), swapped to the front
-    uint32_t best = 0xFFFFFFFFu;
-    for (uint32_t i = lane; i < P; i += 64u) best = min(best, sel_key(qq[(head + i) & (QCAP - 1)]));
-    best = wave_min_u32(best);
-    uint32_t first = 0xFFFFFFFFu;
-    for (uint32_t i = lane; i < P; i += 64u)
-      if (sel_key(qq[(head + i) & (QCAP - 1)]) == best) first = min(first, i);
-    first = wave_min_u32(first);
-    const uint4 e = qq[(head + first) & (QCAP - 1)];
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) qq[head & (QCAP - 1)] = e;
-    __builtin_amdgcn_wave_barrier();
-    tail = head + 1u;
-    return;
-  }
-  uint4* A = scratch;
-  uint4* T = scratch + QCAP;
-  uint32_t* W = reinterpret_cast<uint32_t*>(scratch + 2u * QCAP);
-  for (uint32_t i = lane; i < P; i += 64u) A[i] = qq[(head + i) & (QCAP - 1)];
-  wave_mem_fence();
-  // partition_at_index_loop (bw - 1 is never len - 1 here: P > 2 bw)
-  uint32_t a = 0, len = P, index = bw - 1u, limit = limit0;
-  bool has_anc = false;
-  uint32_t anc = 0;
-  for (;;) {
-    if (len <= 16u) {
-      if (len >= 2u) sel_small_sort(A + a, len);
-      break;
-    }
-    if (limit == 0) {
-      if (lane == 0) sel_s_mom<4>(A + a, len, index);
-      wave_mem_fence();
-      break;
-    }
-    --limit;
-    const uint32_t pp = sel_pivot(A + a, len);
-    const uint32_t pk = sel_key(A[a + pp]);
-    if (has_anc && !(anc < pk)) {  // pivot equal to the ancestor pivot: split off the equal run
-      const uint32_t mid = sel_partition(A + a, T + a, W, len, pp, true) + 1u;
-      if (index <= mid) break;
-      a += mid;
-      len -= mid;
-      index -= mid;
-      has_anc = false;
-      continue;
-    }
-    const uint32_t mid = sel_partition(A + a, T + a, W, len, pp, false);
-    if (mid < index) {
-      has_anc = true;
-      anc = pk;
-      a += mid + 1u;
-      len -= mid + 1u;
-      index -= mid + 1u;
-    } else if (mid > index) {
-      len = mid;
-    } else {
-      break;
-    }
-  }
-  for (uint32_t i = lane; i < bw; i += 64u) qq[(head + i) & (QCAP - 1)] = A[i];
-  __builtin_amdgcn_wave_barrier();
   tail = head + bw;
 }
 
@@ -1578,7 +1829,8 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     if constexpr (VCAP > 0) {
       if (P.beam && tail - head > beam2) {
         if (P.beam_canonical) beam_select_canonical<QCAP>(q, head, tail, P.beam);  // diagnostics
-        else beam_select<QCAP>(q, head, tail, P.beam, bsel, P.sel_limit);         // :577-589
+        else if constexpr (QCAP <= 256) beam_select_lds<QCAP>(q, head, tail, P.beam, claim, P.sel_limit);  // :577-589
+        else beam_select<QCAP>(q, head, tail, P.beam, bsel, P.sel_limit);
         if (track_beam) jbeam = max(jbeam, shfl_u32(wave_inclusive_max(jp1), 63));
       }
     } else if (P.beam && tail - head > beam2) {
@@ -4005,7 +4257,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   HIP_TRY(hipMemcpyAsync(d_segs.p, segs.data(), segs.size() * sizeof(SegDesc), hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(d_prefix.p, prefix.data(), prefix.size() * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
   uint64_t out_cap = std::max<uint64_t>(4096, windows / 64);
-  uint64_t spill_cap = std::max<uint64_t>(4096, windows / 32);
+  // beamed passes spill every window whose pending count passes 2 bw from the dedup-free first pass
+  // (C3: ~5 % of its windows): a list too short re-runs the whole pass
+  uint64_t spill_cap = std::max<uint64_t>(4096, windows / (P.beam ? 8 : 32));
   const uint32_t max_grid = (uint32_t)cus * 16;
   HIP_TRY(d_ebuf.alloc((size_t)max_grid * P.ecap * sizeof(uint4), stream));
   HIP_TRY(d_cnt.alloc(N_COUNTERS * sizeof(unsigned long long), stream));

@@ -230,11 +230,12 @@ void segment_graphemes(const uint8_t* s, uint64_t n, std::vector<uint64_t>& star
   }
 }
 
-// A shard cut at byte p: the previous character is ASCII and not CR, so no rule of
+// A shard cut at byte p (safe_cut): the previous character is ASCII and not CR, so no rule of
 // segment_graphemes above keeps p inside a cluster unless the character at p is Extend, ZWJ or
 // SpacingMark (GB9, GB9a); and after an ASCII character every piece of state (ri_run, pict, gb11,
 // incb_state) depends on the character at p alone, so segmenting from p reproduces exactly the
-// boundaries the whole text has from p on.
+// boundaries the whole text has from p on. Text without ASCII cuts before a character that starts
+// a cluster in every context (see safe_cut).
 bool nth_grapheme_from_end(const uint8_t* s, uint64_t len, uint64_t n, uint64_t& off) {
   if (n == 0) return false;
   std::vector<uint64_t> st;
@@ -265,12 +266,26 @@ bool ascii_only(const uint8_t* s, uint64_t n) {
 
 bool safe_cut(const uint8_t* s, uint64_t n, uint64_t p) {
   if (p == 0 || p >= n) return true;
-  const uint8_t prev = s[p - 1];
-  if (prev >= 0x80 || prev == '\r') return false;
   if ((s[p] & 0xC0) == 0x80) return false;  // not a code point start
   uint64_t i = p;
-  const uint8_t g = gcb(utf8_decode(s, n, i));
-  return g != GCB_Extend && g != GCB_ZWJ && g != GCB_SpacingMark;
+  const uint32_t r = utf8_decode(s, n, i);
+  const uint8_t g = gcb(r);
+  const uint8_t prev = s[p - 1];
+  if (prev < 0x80) {
+    if (prev == '\r') return false;
+    return g != GCB_Extend && g != GCB_ZWJ && g != GCB_SpacingMark;
+  }
+  // After a non-ASCII character (text with no ASCII, e.g. CJK without spaces): a character that
+  // starts a cluster on its own -- GCB Other or a Hangul LV / LVT syllable (no GB7-GB9a, GB12/13),
+  // not Extended_Pictographic (GB11), no InCB class (GB9c) -- is preceded by a boundary in every
+  // context unless the previous character is Prepend (GB9b) or a leading jamo L (GB6), and it resets
+  // every piece of segmenter state.
+  if ((g != GCB_Other && g != GCB_LV && g != GCB_LVT) || ext_pict(r) || incb(r) != INCB_None) return false;
+  uint64_t q = p - 1;
+  while (q > 0 && (s[q] & 0xC0) == 0x80 && p - q < 4) --q;
+  uint64_t t = q;
+  const uint8_t lg = gcb(utf8_decode(s, n, t));
+  return lg != GCB_Prepend && lg != GCB_L;
 }
 
 int lower_full(uint32_t cp, uint32_t out[3]) {

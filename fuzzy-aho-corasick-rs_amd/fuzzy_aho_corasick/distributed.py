@@ -36,6 +36,30 @@ def shard_bounds(n_windows: int, world: int, rank: int) -> Tuple[int, int]:
     return a, a + base + (1 if rank < extra else 0)
 
 
+def stream_share_windows(total: int, block: int, share_index: int, overlap: int,
+                         n_shares: int = 8) -> List[Tuple[int, int, int, int]]:
+    """C5's cut of a stream of `total` bytes = total / block repeats of one `block`-byte block (SURVEY
+    §8(d)): the stream is split into `n_shares` contiguous shares (one per GPU of the 8-GPU node;
+    GPU g takes share g, so a run on fewer GPUs keeps each GPU's work: weak scaling), and the share
+    into windows cut at block and share boundaries. A window is searched exactly like stream.rs window_matches (:262-297): its text
+    is its bytes plus `overlap` following bytes (max_match_graphemes() + 1 of an ASCII stream,
+    :256-258, clipped at the stream's end), and it owns the matches starting in its bytes. The block
+    is resident once as block || block[:overlap], so every window is a contiguous slice of it:
+    returns (g_begin, g_end, commit, base) = the slice [g_begin, g_end) of that buffer, the owned byte
+    count, the window's stream offset."""
+    share = total // n_shares
+    lo, hi = share_index * share, ((share_index + 1) * share if share_index + 1 < n_shares else total)
+    out = []
+    c = lo
+    while c < hi:
+        c1 = min(hi, (c // block + 1) * block)
+        o = c % block
+        end = min(total, c1 + overlap)
+        out.append((o, o + (end - c), c1 - c, c))
+        c = c1
+    return out
+
+
 def _wire_device(group) -> torch.device:
     """Where collective buffers live: HBM for RCCL, host memory for gloo (CPU tests)."""
     if dist.get_backend(group) == "nccl":

@@ -853,6 +853,8 @@ struct Searcher {
       size_t window_first_out = out.size();
       queue.push_back({0, start, start, start, 0.f, 0, 0});
       size_t q_idx = 0;
+      size_t horizon[3] = {SIZE_MAX, SIZE_MAX, SIZE_MAX};  // diagnostics: pops before the first j + 1 - start >= 4, 5, 6
+      size_t win_pops = 0;
       while (q_idx < queue.size()) {
         if (effective_beam) {  // :577-589
           size_t bw = effective_beam;
@@ -869,7 +871,12 @@ struct Searcher {
           }
         }
         State st = queue[q_idx];
-        if (deg_hist) deg_hist[73] = std::max<uint64_t>(deg_hist[73], queue.size() - q_idx);
+        if (deg_hist) {
+          deg_hist[73] = std::max<uint64_t>(deg_hist[73], queue.size() - q_idx);
+          for (int h = 0; h < 3; ++h)
+            if (horizon[h] == SIZE_MAX && st.j + 1 - start >= (uint32_t)(4 + h)) horizon[h] = win_pops;
+          ++win_pops;
+        }
         ++q_idx;
         ++states_popped;
         Key key{st.node, st.j, st.ms, st.me, st.packed};
@@ -994,6 +1001,7 @@ struct Searcher {
         deg_hist[74] = std::max<uint64_t>(deg_hist[74], visited.size());
         deg_hist[75] += visited.size();
         deg_hist[76] += 1;
+        for (int h = 0; h < 3; ++h) deg_hist[77 + h] += horizon[h] == SIZE_MAX ? win_pops : horizon[h];
       }
       if (e.has_auto_beam && effective_beam == 0) {  // :1096-1103
         states_expanded += queue.size();

@@ -105,10 +105,15 @@ def test_shard_bounds_partition():
             assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
 
 
-@pytest.mark.parametrize("hay", [HAY_ASCII, HAY_UNI, "éé ab‍c 👍🏽x " * 30 + "a\r\nb " * 20])
+HAY_CJK = "漢字仮名交じり文" * 40 + "한국어텍스트ᄀ각" * 30 + "क्षिति" * 10 + "中文؀文本" * 20
+
+
+@pytest.mark.parametrize("hay", [HAY_ASCII, HAY_UNI, "éé ab‍c 👍🏽x " * 30 + "a\r\nb " * 20, HAY_CJK])
 def test_shard_plan_cuts_at_context_free_boundaries(hay):
-    """Shards tile the bytes, every cut is a grapheme boundary of the whole text, and the halo holds
-    max_match_graphemes() + 2 complete graphemes past the owned bytes (or reaches the end)."""
+    """Shards tile the bytes, every cut is a grapheme boundary of the whole text, a shard segmented
+    on its own has the whole text's boundaries, the halo holds max_match_graphemes() + 2 complete
+    graphemes past the owned bytes (or reaches the end); text without ASCII (CJK, Hangul) still
+    splits (cuts before characters that start a cluster in every context)."""
     from fuzzy_aho_corasick import _native
     from oracle_harness import graphemes
     data = hay.encode("utf-8")
@@ -131,6 +136,14 @@ def test_shard_plan_cuts_at_context_free_boundaries(hay):
             if e < len(data):
                 n_halo = len(data[b:e]) if asc else len(graphemes(data[b:e].decode("utf-8")))
                 assert n_halo == 7 + 2
+            if not asc:  # the piece's own segmentation == the whole text's, shifted
+                own, q = [], a
+                for g in graphemes(data[a:e].decode("utf-8")):
+                    own.append(q)
+                    q += len(g.encode("utf-8"))
+                assert own == sorted(x for x in starts if a <= x < e)
+        if world > 1 and hay == HAY_CJK:
+            assert max(p[1] - p[0] for p in plans) <= len(data) // world + 64
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -203,8 +216,76 @@ def test_bench_gpus_flag_launches_ranks(n):
     assert j["config"]["records_gathered_per_step"] == sum(1000 + k for k in range(n))
 
 
+@pytest.mark.parametrize("config", ["c2", "c3"])
+def test_bench_shard_dry_run_plans_and_gathers(config):
+    """`bench.py --gpus 4 --shard --dry-run`: the strong-scaling path end to end without a GPU --
+    fac_shard_plan cuts the config's haystack, each rank searches its owned windows of its
+    halo-sliced piece (the oracle standing in for the device search), the gather brings every record
+    to rank 0, and the union equals the whole-haystack search."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4", "--shard", "--dry-run", "--steps",
+                        "1", "--config", config, "--mib", "0.03"], capture_output=True, text=True, timeout=400, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert j["n_gpus"] == 4 and j["config"]["records_gathered_per_step"] > 0
+    assert j["config"]["shard_union_equals_whole"] is True
+
+
 def test_bench_rejects_mismatched_world():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)
+
+
+def _c5_worker(rank, world, port, blocks, out_path):
+    sys.path[:0] = [os.path.join(REPO, "fuzzy-aho-corasick-rs_amd"), os.path.join(REPO, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import numpy as np
+    import torch.distributed as dist
+    from fuzzy_aho_corasick import workloads as W
+    from fuzzy_aho_corasick.distributed import gather_rows, stream_share_windows
+    from fuzzy_aho_corasick.structs import Order, Overlap
+    from oracle_harness import OracleEngine
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    wl = W.config("c5", 1 << 20, seed=5)
+    rng = np.random.default_rng(55)
+    # a small C5 block: C5's patterns (10-16 chars, edits 1, threshold 0.85, pre-filter), a needle
+    # every 6 KiB instead of every MiB so every share holds several, one planted across a block edge
+    block = W._haystack(rng, [W.ASCII_LOWER], wl.patterns, 48 << 10, 1, 6 << 10)
+    block = block[:-20] + b" " + wl.patterns[3].encode()[:9]  # a needle prefix ending the block ...
+    block = wl.patterns[3].encode()[9:] + b" " + block[len(wl.patterns[3]) - 8:]  # ... continued at its start
+    total = len(block) * blocks
+    orc = OracleEngine(W.builder_for(wl), wl.patterns)
+    overlap = max(len(p) for p in wl.patterns) + 1 + 1  # max_match_graphemes() + 1, ASCII
+    buf = block + block[:overlap]
+    rows = []
+    for (g0, g1, commit, base) in stream_share_windows(total, len(block), rank, overlap, n_shares=world):
+        text = buf[g0:g1]  # stream.rs window_matches: search(sorted, non_overlapping), starts < commit
+        ranked = orc.apply_rows(orc.raw_rows(text, wl.threshold, prefilter=True), Order.Default, Overlap.NonOverlapping)
+        rows += [(s + base, e + base) + tuple(r) for (s, e, *r) in ranked if s < commit]
+    got = gather_rows(rows)
+    if rank == 0:
+        stream = block * blocks
+        full = orc.apply_rows(orc.raw_rows(stream, wl.threshold, prefilter=True), Order.Default, Overlap.NonOverlapping)
+        with open(out_path, "w") as f:
+            f.write(repr((sorted(got), sorted(tuple(r) for r in full))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_c5_stream_shares_equal_whole_stream_cpu(world):
+    """bench.py --config c5's cut (stream_share_windows: one contiguous share per rank, windows at
+    block and share edges with max_match_graphemes() + 1 of overlap, each searched like stream.rs
+    window_matches with the pre-filter and owning the matches that start in it), the oracle as each
+    rank's compute, gathered over gloo == the whole stream searched sorted().non_overlapping()
+    (tests.rs:1058-1142: streaming equals whole input for needles spaced past the overlap)."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res.txt")
+        mp.spawn(_c5_worker, args=(world, _free_port(), 5, out), nprocs=world, join=True)
+        got, full = eval(open(out).read())
+    assert len(full) >= 30
+    assert got == full
