@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="single-thread CPU baseline sample budget")
     ap.add_argument("--cpu-threads", type=int, default=16, help="all-cores CPU baseline threads (box share: 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--traffic-json", default=None, help="default: profiles/traffic_<config>.json")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/gather plumbing only (gloo, no GPU, no search): for CPU tests of --gpus N")
     return ap.parse_args()
@@ -220,15 +220,7 @@ def main():
     recs_rank = acc["matches"] / K / (world if world > 1 else 1)
     bytes_step = rank_bytes + 32 * recs_rank
     achieved = bytes_step / (step_dev_ms / 1e3) / 1e9 if step_dev_ms > 0 else 0.0
-    traffic, traffic_note = None, "no profiles/traffic.json"
-    if os.path.exists(args.traffic_json):
-        tj = json.load(open(args.traffic_json))
-        if tj.get("sources_sha") != sources_sha():
-            traffic_note = f"profiles/traffic.json is stale (sources {tj.get('sources_sha')} != {sources_sha()})"
-        elif tj.get("config") != args.config or abs(tj.get("mib", -1) - mib) > 1e-6 or args.shard:
-            traffic_note = "profiles/traffic.json was measured on another workload"
-        else:
-            traffic, traffic_note = tj.get("hbm_bytes_per_step"), tj.get("source")
+    traffic, traffic_note = load_traffic(args, mib)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -304,6 +296,20 @@ def main():
         dist.destroy_process_group()
 
 
+def load_traffic(args, mib):
+    """PMC traffic per step (profiles/make_traffic.py) if it was measured on this config, size and
+    these sources; else (None, why)."""
+    path = args.traffic_json or os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
+    if not os.path.exists(path):
+        return None, f"no {os.path.relpath(path, REPO)}"
+    tj = json.load(open(path))
+    if tj.get("sources_sha") != sources_sha():
+        return None, f"{os.path.relpath(path, REPO)} is stale (sources {tj.get('sources_sha')} != {sources_sha()})"
+    if tj.get("config") != args.config or abs(tj.get("mib", -1) - mib) > 1e-6 or args.shard or args.vocab != 50_000:
+        return None, f"{os.path.relpath(path, REPO)} was measured on another workload"
+    return tj.get("hbm_bytes_per_step"), tj.get("source")
+
+
 def run_c5(args, world, rank, local):
     """C5: a 100 GiB stream = 100 x one deterministic 1 GiB block (1 needle per MiB),
     resident once in HBM as block || block[:halo]. GPU g processes its contiguous 1/8 of the stream
@@ -369,6 +375,7 @@ def run_c5(args, world, rank, local):
     if world > 1:
         dist.all_reduce(pr)
     processed = int(pr.item()) * args.steps
+    traffic, traffic_note = load_traffic(args, args.gib * 1024)  # c5 traffic is keyed by the stream size
     K = max(1, args.steps)
     dev_ms = (pf + km) / K
     cpu = None
@@ -388,7 +395,7 @@ def run_c5(args, world, rank, local):
                        "window_overlap_graphemes": overlap, "threshold": wl.threshold,
                        "parallelism": f"dp{world} (each GPU its 1/8 of the stream; RCCL gather of Match records)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
                          "kernel": "pre-filter (q-gram scan + per-candidate bitap verify; packed bitap scan for "
                                    "patterns with pieces < 3 symbols) + runs_kernel + re-search of the merged windows",
                          "avg_kernel_ms": dev_ms, "algorithmic_bytes_per_launch": bytes_step},

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round evidence on one MI355X (run through gpurun from the repo root):
 #   bash profiles/gpu_evidence.sh TAG [what...]
-# what: tests smoke c3 c3e2e c2 c4 c5 kt pmc c3t  (default: tests smoke c3 c2 c5 kt pmc). Outputs under gpurun_out/TAG/.
+# what: tests smoke c3 c3e2e c2 c4 c5 c5t kt pmc pmc5 c3t  (default: tests smoke c3 c2 c5 kt pmc). Outputs under gpurun_out/TAG/.
 # Every GPU step has its own time limit; the script stops at the first failing step.
 set -eo pipefail
 TAG=${1:?tag}
@@ -38,9 +38,13 @@ if has c4; then
   timeout -k 10 300 python bench.py --config c4 --no-cpu-baseline > "$OUT/bench_c4.json" 2> "$OUT/bench_c4.err"
   cat "$OUT/bench_c4.json"
 fi
-if has c5; then
-  timeout -k 10 300 python bench.py --config c5 --gib 8 --steps 2 --no-cpu-baseline > "$OUT/bench_c5.json" 2> "$OUT/bench_c5.err"
+if has c5; then  # one GPU's full 12.5 GiB share of the 100 GiB stream, CPU baseline included
+  timeout -k 10 600 python bench.py --config c5 --steps 2 > "$OUT/bench_c5.json" 2> "$OUT/bench_c5.err"
   cat "$OUT/bench_c5.json"
+fi
+if has c5t; then  # after traffic_c5.json exists
+  timeout -k 10 600 python bench.py --config c5 --steps 2 > "$OUT/bench_c5_traffic.json" 2> "$OUT/bench_c5_traffic.err"
+  cat "$OUT/bench_c5_traffic.json"
 fi
 export TMPDIR=/tmp
 if has kt; then
@@ -58,8 +62,18 @@ if has pmc; then
     find "$OUT/pmc_$c" -name '*counter_collection.csv' -exec cp {} "$OUT/c3_pmc_$c.csv" \;
   done
   python3 profiles/make_traffic.py c3 256 2 "$OUT/c3_pmc_FETCH_SIZE.csv" "$OUT/c3_pmc_WRITE_SIZE.csv" "$(python3 -c "import bench; print(bench.sources_sha())")" > "$OUT/traffic.log"
-  cp profiles/traffic.json "$OUT/traffic.json"
+  cp profiles/traffic_c3.json "$OUT/traffic_c3.json"
   head -c 1500 "$OUT/traffic.log"
+fi
+if has pmc5; then  # C5: one GPU's 12.5 GiB share of the 100 GiB stream
+  for c in FETCH_SIZE WRITE_SIZE; do
+    (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc5_$c" -o c5 \
+      -- python3 "$ROOT/bench.py" --config c5 --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pmc5_$c.log" 2>&1)
+    find "$OUT/pmc5_$c" -name '*counter_collection.csv' -exec cp {} "$OUT/c5_pmc_$c.csv" \;
+  done
+  python3 profiles/make_traffic.py c5 102400 1 "$OUT/c5_pmc_FETCH_SIZE.csv" "$OUT/c5_pmc_WRITE_SIZE.csv" "$(python3 -c "import bench; print(bench.sources_sha())")" > "$OUT/traffic5.log"
+  cp profiles/traffic_c5.json "$OUT/traffic_c5.json"
+  head -c 1500 "$OUT/traffic5.log"
 fi
 if has c3t; then  # bench after traffic.json exists: the line carries roofline.traffic
   timeout -k 10 400 python bench.py > "$OUT/bench_c3_traffic.json" 2> "$OUT/bench_c3_traffic.err"
