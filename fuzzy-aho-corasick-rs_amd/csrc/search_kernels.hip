@@ -4473,7 +4473,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       // with the lane-serial kernel an 8-char level no longer pays (C3 156 -> 147 ms); one-edit
       // engines finish most windows within 5 chars, and a 6-char level costs them more in counts
       // and lookup probes than it saves (C2 1 GiB: 266 -> 188 ms per step with "5" alone)
-      std::string spec = le ? le : (e.mef <= 1u ? "5" : "5,6");
+      // beamed engines (the reference's select_nth_unstable_by order): 5 and 7 chars, built exactly
+      // (measured C3: "5,6" 257.7, "5,7" with keys seen >= 4 times 214.9 ms per step;
+      // profiles/r03/sweep_levels.txt)
+      std::string spec = le ? le : (e.mef <= 1u ? "5" : P.beam ? "5,7" : "5,6");
       for (size_t a = 0; a < spec.size();) {
         const size_t b = spec.find(',', a);
         const uint32_t k = (uint32_t)std::strtoul(spec.substr(a, b == std::string::npos ? std::string::npos : b - a).c_str(), nullptr, 10);
@@ -4501,7 +4504,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     std::vector<bool> tab_exact;  // built by the exact kernel (else dedup-free: rc_build_kernel_live)
     // sampled levels of beamed engines are built dedup-free (not for the auto-beam count pass, which
     // needs every window's exact queue.len(), nor with mappings)
-    const bool live_builds = P.beam && !counts && !e.has_map && qbuild <= 256 && !diag_env("FAC_NO_LIVE_BUILD");
+    // Dedup-free ("live") builds of the sampled levels leave every key whose build would beam
+    // uncached, and their snapshots are not exact: a main-pass window that beams after its snapshot
+    // restarts from the deepest exact level. With the reference's beam order (select_nth_unstable_by
+    // scatters the survivors, so the key's horizon comes earlier and more windows beam after it)
+    // that restart dominated (C3: 8.2 M windows restarted from 4-char snapshots, 537 ms per step
+    // against 258 with exact sampled builds). FAC_LIVE_BUILD=1 brings them back (A/B).
+    const bool live_builds = P.beam && !counts && !e.has_map && qbuild <= 256 && diag_env("FAC_LIVE_BUILD") &&
+                             !diag_env("FAC_NO_LIVE_BUILD");
     const uint64_t ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", 4)));
     auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, hipStream_t bs, bool cleared = false,
                      bool sampled = false) -> int {
@@ -4644,7 +4654,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     // (C3) 2 per CU (-2 ms against 8), one level (C2, whose builds are shorter) 4 per CU (-2 ms)
     const uint32_t cgrid2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256,
         (uint64_t)cus * env_u("FAC_RC_CGRID2", ks.size() >= 2 ? 2 : 4)));
-    const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", s2 > 2 ? 1 : 2));
+    const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", s2 > 2 ? 1 : P.beam ? 4 : 2));
     std::vector<RcTable> Lx;        // sampled levels, ascending k
     std::vector<uint32_t> n_entx;   // their entries
     std::vector<size_t> xbuf;       // their count-table buffers
