@@ -1,7 +1,7 @@
 """One C3 step's kernels on their queues (start/end/duration ms from the step's first kernel), from a
 rocprofv3 --kernel-trace --output-format csv run: python profiles/step_timeline.py run_kernel_trace.csv
-A step starts at a level-1 count (rc_count_kernel) that follows a search kernel; the last complete
-step is printed."""
+A step starts at its device staging (ascii_or_kernel), or, for pre-staged runs, at a level-1 count
+(rc_count_kernel) that follows a search kernel; the last complete step is printed."""
 import csv
 import re
 import sys
@@ -16,7 +16,9 @@ def prev_kernel(i):  # the last kernel before i that is not a runtime fill / cop
     return ''
 
 
-starts = [i for i, n in enumerate(names) if 'rc_count_kernel' in n and 'window_kernel' in prev_kernel(i)]
+starts = [i for i, n in enumerate(names) if 'ascii_or_kernel' in n]
+if len(starts) < 2:
+    starts = [i for i, n in enumerate(names) if 'rc_count_kernel' in n and 'window_kernel' in prev_kernel(i)]
 a, b = (starts[-2], starts[-1]) if len(starts) >= 2 else (starts[-1], len(rows))
 seg = rows[a:b]
 t0 = int(seg[0]['Start_Timestamp'])
