@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <vector>
 
 #include "fac_internal.h"
@@ -560,8 +561,15 @@ __device__ void sel_s_mom(const A& v0, uint32_t len, uint32_t k) {  // median_of
   }
 }
 
+// The selects are real calls (not inlined into run_window): inlined, their registers raised the
+// window loop's pressure past the dedup variants' budget and the loop spilled to scratch on every
+// batch (rc_build_kernel<256>: 45 VGPRs spilled, 1168 B/lane scratch). Measured C3: 212.5 -> 162.0 ms
+// per step (prefix cache 79.1 -> 44.8 ms, wave kernels 109.3 -> 93.6 ms; profiles/r03o).
+#ifndef FAC_SEL_ATTR
+#define FAC_SEL_ATTR __attribute__((noinline))
+#endif
 template <uint32_t QCAP>
-__device__ void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t bw, uint4* scratch, uint32_t limit0) {
+__device__ FAC_SEL_ATTR void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t bw, uint4* scratch, uint32_t limit0) {
   const uint32_t lane = lane_id();
   const uint32_t P = tail - head;
   uint4* qq = reinterpret_cast<uint4*>(q);
@@ -758,7 +766,7 @@ __device__ uint32_t sel_partition_lds(uint32_t* K, uint16_t* I, uint32_t* W, uin
 }
 
 template <uint32_t QCAP>
-__device__ void beam_select_lds(KState* q, uint32_t head, uint32_t& tail, uint32_t bw, uint32_t* scratch, uint32_t limit0) {
+__device__ FAC_SEL_ATTR void beam_select_lds(KState* q, uint32_t head, uint32_t& tail, uint32_t bw, uint32_t* scratch, uint32_t limit0) {
   static_assert(QCAP <= 256, "LDS select: rings of up to 256 states");
   const uint32_t lane = lane_id();
   const uint32_t P = tail - head;
@@ -856,7 +864,7 @@ __device__ void beam_select_lds(KState* q, uint32_t head, uint32_t& tail, uint32
 // Diagnostics only (FAC_BEAM_CANONICAL, rounds 1-2's rule): keep the bw smallest by (penalty,
 // queue position) in queue order -- not the reference's order; for A/B measurements of the tie rule.
 template <uint32_t QCAP>
-__device__ void beam_select_canonical(KState* q, uint32_t head, uint32_t& tail, uint32_t bw) {
+__device__ FAC_SEL_ATTR void beam_select_canonical(KState* q, uint32_t head, uint32_t& tail, uint32_t bw) {
   constexpr int PER = QCAP / 64;
   const uint32_t lane = lane_id();
   const uint32_t P = tail - head;
@@ -2530,6 +2538,52 @@ __global__ __launch_bounds__(256) void rc_relookup_kernel(SearchParams P, uint64
     const RcHit hit = rc_lookup(P, S, start, P.rc_qcap);
     P.rc_hits[vid] = make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel);
     P.rc_hit_pops[vid] = hit.pops;
+  }
+}
+
+// Demand level (launch_pass): the keys of the entries still open after the lookups and the lane
+// kernel (the windows the wave kernels would search), counted over exactly those; one wave per
+// region of compacted entries. A key's first inserter (a window) is its representative.
+__global__ __launch_bounds__(256) void rc_count_open_kernel(SearchParams P, RcCountTarget T) {
+  const uint32_t lane = lane_id();
+  const uint64_t n_reg = P.total_windows / RC_REGION;
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
+  for (uint64_t rg = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; rg < n_reg; rg += nw) {
+    const uint32_t n = P.rc_region_cnt[rg];
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint64_t e = rg * RC_REGION + i;
+      if (P.rc_hits[e].x == RC_DONE) continue;
+      const uint64_t wid = rc_window_of(P, e);
+      const uint32_t kl = find_seg(P, wid);
+      const SegDesc S = P.segs[kl];
+      const uint64_t start = S.w_begin + (wid - P.seg_prefix[kl]);
+      RcChars ch;
+      uint64_t k;
+      if (rc_key(P, S, start, T.k, ch, k)) rc_count_insert(T, k, wid, 2u, RC_PROBES);
+    }
+  }
+}
+// ... and the open entries' lookups in the new level (P.rc_tab[0] alone): a hit replaces the entry's
+// snapshot (the level is deeper than every other)
+__global__ __launch_bounds__(256) void rc_relookup_open_kernel(SearchParams P) {
+  const uint32_t lane = lane_id();
+  const uint64_t n_reg = P.total_windows / RC_REGION;
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
+  for (uint64_t rg = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; rg < n_reg; rg += nw) {
+    const uint32_t n = P.rc_region_cnt[rg];
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint64_t e = rg * RC_REGION + i;
+      if (P.rc_hits[e].x == RC_DONE) continue;
+      const uint64_t wid = rc_window_of(P, e);
+      const uint32_t kl = find_seg(P, wid);
+      const SegDesc S = P.segs[kl];
+      const uint64_t start = S.w_begin + (wid - P.seg_prefix[kl]);
+      const RcHit hit = rc_lookup(P, S, start, P.rc_qcap);
+      if (hit.off != EMPTY) {
+        P.rc_hits[e] = make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel);
+        P.rc_hit_pops[e] = hit.pops;
+      }
+    }
   }
 }
 
@@ -4262,7 +4316,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   uint64_t spill_cap = std::max<uint64_t>(4096, windows / (P.beam ? 8 : 32));
   const uint32_t max_grid = (uint32_t)cus * 16;
   HIP_TRY(d_ebuf.alloc((size_t)max_grid * P.ecap * sizeof(uint4), stream));
-  HIP_TRY(d_cnt.alloc(N_COUNTERS * sizeof(unsigned long long), stream));
+  // two counter sets: the pass's, and (second) a cache build's while a pass is open (demand level)
+  HIP_TRY(d_cnt.alloc(2 * N_COUNTERS * sizeof(unsigned long long), stream));
+  size_t build_cnt = 0;  // counter set the cache builds use
   // wave slots: a ring of max_grid slots per stream a slot-using kernel runs on (this one, the
   // level-1 build's); beamed engines: each slot's beam-selection scratch, sized for 256-state rings
   // at max_grid slots (larger rings get fewer slots, still above their LDS-bound residency)
@@ -4340,6 +4396,30 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   const bool root_out = !e.nodes.empty() && e.nodes[0].out_end > e.nodes[0].out_begin;
   const char* rc_min = diag_env("FAC_RC_MIN");  // env knobs: tests force it on / pin K, A/B turns it off
   const char* kenv = diag_env("FAC_RC_K");
+  // prefix-cache state the main pass's demand level shares with the setup below
+  std::vector<RcTable> tabs;      // built levels, ascending k: a build resumes its representatives from them
+  std::vector<bool> tab_exact;    // built by the exact kernel (else dedup-free: rc_build_kernel_live)
+  RcTable L1{0u, 0u, nullptr, nullptr, nullptr, nullptr};
+  uint32_t n_ent0 = 0, qbuild = 0;
+  bool live_builds = false;
+  uint64_t ct_mult = 4;
+  std::function<int(const RcTable&, uint32_t, const uint64_t*, hipStream_t, bool, bool)> rc_build_fn;
+  std::function<int(RcTable&, uint32_t, DevBuf&, hipStream_t, bool)> rc_publish_fn;
+  std::function<int(const DevBuf&, const DevBuf&, const DevBuf&, const DevBuf&, uint32_t, uint32_t, uint32_t, unsigned int&)>
+      rc_number_fn;
+  // after its build a level's entries are published into an exact-key lookup table (4 slots per
+  // entry: a miss usually ends at the first probe)
+  auto ct_slots = [&](uint32_t n_ent) {
+    uint32_t cs = 1u << 12;
+    while (cs < ct_mult * n_ent && cs < (1u << 28)) cs <<= 1;
+    return cs;
+  };
+  auto clear_ct = [&](uint32_t n_ent, DevBuf& ct, hipStream_t bs) -> int {
+    const uint32_t cs = ct_slots(n_ent);
+    HIP_TRY(ct.alloc((size_t)cs * 2 * sizeof(uint4), bs));
+    HIP_TRY(hipMemsetAsync(ct.p, 0, (size_t)cs * 2 * sizeof(uint4), bs));
+    return FAC_OK;
+  };
   if (!root_out && !e.has_map && fan_root + 1 <= 4096 && kVariants[vi].qcap <= 4096 &&
       windows >= (rc_min ? std::strtoull(rc_min, nullptr, 10) : 4096ull) && !diag_env("FAC_NO_RC")) {
     auto env_u = [](const char* name, uint64_t dflt) {
@@ -4348,7 +4428,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     };
     const uint32_t kpin = kenv ? (uint32_t)std::min<unsigned long>(4, std::max<unsigned long>(2, std::strtoul(kenv, nullptr, 10))) : 0u;
     const uint32_t qmain = kVariants[vi].qcap, vmain = kVariants[vi].vcap;
-    const uint32_t qbuild = std::max<uint32_t>((uint32_t)fan_root + 1, qmain);
+    qbuild = std::max<uint32_t>((uint32_t)fan_root + 1, qmain);
     P.rc_vmax = vmain ? std::min<uint32_t>(256, vmain / 2) : 256;
     P.rc_emax = 64;
     const uint64_t ent_cap = std::max<uint64_t>(1, env_u("FAC_RC_ENTRIES", 16ull << 20));
@@ -4365,8 +4445,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     HIP_TRY(d_rcrep.alloc(max_ent * sizeof(uint64_t), stream));
     HIP_TRY(d_rcc.alloc(2 * (size_t)max_ent * sizeof(uint32_t), stream));  // counts, then offsets
     HIP_TRY(d_rcn.alloc(4 * sizeof(unsigned long long), stream));  // keys, pool words used, level-2 entries
-    RcTable L1{0u, slots - 1, static_cast<const unsigned long long*>(d_rck.p), static_cast<const uint32_t*>(d_rcv.p),
-               static_cast<uint32_t*>(d_rcc.p) + max_ent, static_cast<uint32_t*>(d_rcc.p)};
+    L1 = RcTable{0u, slots - 1, static_cast<const unsigned long long*>(d_rck.p), static_cast<const uint32_t*>(d_rcv.p),
+                 static_cast<uint32_t*>(d_rcc.p) + max_ent, static_cast<uint32_t*>(d_rcc.p)};
     P.rc_pool_used = static_cast<unsigned long long*>(d_rcn.p) + 1;
     HIP_TRY(hipEventRecord(ev.a, stream));
     HIP_TRY(hipMemsetAsync(d_rcn.p, 0, 4 * sizeof(unsigned long long), stream));
@@ -4405,7 +4485,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     // (the root pop, its beam and the first chars' states are shared by every level-1 key). Counted
     // in the level-1 pass; used when level 1 keeps its first key length.
     RcTable L0{0u, 0u, nullptr, nullptr, nullptr, nullptr};
-    uint32_t n_ent0 = 0;
+    n_ent0 = 0;
     const bool want_l0 = !diag_env("FAC_NO_RC_L0");
     auto target = [](const DevBuf& keys, const DevBuf& cnt, const DevBuf& rep, uint32_t n_slots, uint32_t k) {
       return RcCountTarget{static_cast<unsigned long long*>(keys.p), static_cast<uint32_t*>(cnt.p),
@@ -4474,8 +4554,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       // engines finish most windows within 5 chars, and a 6-char level costs them more in counts
       // and lookup probes than it saves (C2 1 GiB: 266 -> 188 ms per step with "5" alone)
       // beamed engines (the reference's select_nth_unstable_by order): 5 and 7 chars, built exactly
-      // (measured C3: "5,6" 257.7, "5,7" with keys seen >= 4 times 214.9 ms per step;
-      // profiles/r03/sweep_levels.txt)
+      // (measured C3: "5,6" 257.7, "5,7" with keys seen >= 4 times 214.9 ms per step; after the
+      // selects became calls, "5,7" / "5,6,7" at >= 2 sightings 151.8 / 151.1; profiles/r03/sweep_levels.txt)
       std::string spec = le ? le : (e.mef <= 1u ? "5" : P.beam ? "5,7" : "5,6");
       for (size_t a = 0; a < spec.size();) {
         const size_t b = spec.find(',', a);
@@ -4500,8 +4580,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         if (e) (void)hipEventDestroy(e);
       }
     } l1_done_guard{l1_done};
-    std::vector<RcTable> tabs;  // built levels, ascending k: a build resumes its representatives from them
-    std::vector<bool> tab_exact;  // built by the exact kernel (else dedup-free: rc_build_kernel_live)
     // sampled levels of beamed engines are built dedup-free (not for the auto-beam count pass, which
     // needs every window's exact queue.len(), nor with mappings)
     // Dedup-free ("live") builds of the sampled levels leave every key whose build would beam
@@ -4510,9 +4588,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     // scatters the survivors, so the key's horizon comes earlier and more windows beam after it)
     // that restart dominated (C3: 8.2 M windows restarted from 4-char snapshots, 537 ms per step
     // against 258 with exact sampled builds). FAC_LIVE_BUILD=1 brings them back (A/B).
-    const bool live_builds = P.beam && !counts && !e.has_map && qbuild <= 256 && diag_env("FAC_LIVE_BUILD") &&
+    live_builds = P.beam && !counts && !e.has_map && qbuild <= 256 && diag_env("FAC_LIVE_BUILD") &&
                              !diag_env("FAC_NO_LIVE_BUILD");
-    const uint64_t ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", 4)));
+    ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", 4)));
     auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, hipStream_t bs, bool cleared = false,
                      bool sampled = false) -> int {
       SearchParams Q = P;
@@ -4534,8 +4612,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       Q.out_cap = out_cap;
       Q.spill = static_cast<uint64_t*>(d_spill.p);
       Q.spill_cap = spill_cap;
-      Q.counters = static_cast<unsigned long long*>(d_cnt.p);
-      if (!cleared) HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), bs));
+      Q.counters = static_cast<unsigned long long*>(d_cnt.p) + build_cnt;
+      if (!cleared) HIP_TRY(hipMemsetAsync(Q.counters, 0, N_COUNTERS * sizeof(unsigned long long), bs));
       uint32_t grid = std::min<uint32_t>(n_ent, max_grid);
       if (bs != stream && !diag_env("FAC_L1_PERSIST")) {
         // beside the sampled-level counts: one chunk per workgroup, so workgroup slots free up all
@@ -4556,19 +4634,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       }
       return FAC_OK;
     };
-    // after its build a level's entries are published into an exact-key lookup table (4 slots per
-    // entry: a miss usually ends at the first probe)
-    auto ct_slots = [&](uint32_t n_ent) {
-      uint32_t cs = 1u << 12;
-      while (cs < ct_mult * n_ent && cs < (1u << 28)) cs <<= 1;
-      return cs;
-    };
-    auto clear_ct = [&](uint32_t n_ent, DevBuf& ct, hipStream_t bs) -> int {
-      const uint32_t cs = ct_slots(n_ent);
-      HIP_TRY(ct.alloc((size_t)cs * 2 * sizeof(uint4), bs));
-      HIP_TRY(hipMemsetAsync(ct.p, 0, (size_t)cs * 2 * sizeof(uint4), bs));
-      return FAC_OK;
-    };
     auto publish = [&](RcTable& T, uint32_t n_ent, DevBuf& ct, hipStream_t bs, bool cleared = false) -> int {
       const uint32_t cs = ct_slots(n_ent);
       if (!cleared) {
@@ -4582,6 +4647,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       T.ct_mask = cs - 1;
       return FAC_OK;
     };
+    rc_build_fn = build;  // for the main pass's demand level
+    rc_publish_fn = publish;
+    rc_number_fn = number_entries;
     if (n_ent1) {
       const uint64_t n_all = n_ent0 + n_ent1 + (uint64_t)ks.size() * max_ent2_est;
       const uint64_t budget = env_u("FAC_RC_POOL_MB", 16384ull) << 20;
@@ -4654,7 +4722,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     // (C3) 2 per CU (-2 ms against 8), one level (C2, whose builds are shorter) 4 per CU (-2 ms)
     const uint32_t cgrid2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256,
         (uint64_t)cus * env_u("FAC_RC_CGRID2", ks.size() >= 2 ? 2 : 4)));
-    const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", s2 > 2 ? 1 : P.beam ? 4 : 2));
+    // (beamed engines: keys seen >= 4 times while the selects were inlined into the window loop and
+    // the builds spilled registers; >= 2 since: C3 162.0 -> 151.8 ms, profiles/r03/sweep_levels.txt)
+    const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", s2 > 2 ? 1 : 2));
     std::vector<RcTable> Lx;        // sampled levels, ascending k
     std::vector<uint32_t> n_entx;   // their entries
     std::vector<size_t> xbuf;       // their count-table buffers
@@ -4781,6 +4851,108 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   // chunks grow to 16 turns per wave (up to 4096 windows; C2 1 GiB: wave kernel 51 -> 4.5 ms).
   // Beamed searches keep 256: their remaining windows are heavy and balance matters more (C3: 256
   // -> 2048 costs 0.7 ms).
+  // lane-serial kernel over the open entries (P.total_windows of them, in regions)
+  auto launch_lane = [&]() -> int {
+    // one wave per workgroup; each takes its best lists from its own emit-scratch slice
+    const uint32_t lgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + LANE_CHUNK - 1) / LANE_CHUNK, (uint64_t)max_grid));
+    static_assert(16 * 64 <= 1024, "lane best lists must fit the emit scratch slice (P.ecap >= 1024)");
+    // 16-state rings by default (C3: lane 19 ms + wave kernel 37 ms, against 6 + 58 with 8 states)
+    if (diag_env("FAC_LANE_Q8")) hipLaunchKernelGGL((lane_window_kernel<8, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+    else if (diag_env("FAC_LANE_Q32")) hipLaunchKernelGGL((lane_window_kernel<32, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+    else hipLaunchKernelGGL((lane_window_kernel<16, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+    HIP_TRY(hipGetLastError());
+    return FAC_OK;
+  };
+  auto lane_debug_line = [&](float lms) -> int {
+    if (!diag_env("FAC_RC_DEBUG")) return FAC_OK;
+    unsigned long long d[8];
+    HIP_TRY(hipMemcpyFromSymbol(d, HIP_SYMBOL(g_lane_dbg), sizeof(d)));
+    std::fprintf(stderr, "FAC_LANE taken=%llu finished=%llu bailed=%llu ms=%.3f popmax=%u trips=%llu run_cycles=%llu "
+                 "wave_cycles=%llu rounds=%llu\n", d[0], d[1], d[2], lms, P.lane_popmax, d[4], d[5], d[6], d[7]);
+    std::memset(d, 0, sizeof(d));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_lane_dbg), d, sizeof(d)));
+    return FAC_OK;
+  };
+  // Demand level (FAC_RC_DEMAND = k chars; 0: off). The sampled levels count keys over a sample of
+  // every window, most of which the lookups finish; here the keys are counted over exactly the
+  // windows still open after the lookups and the lane kernel -- the ones the wave kernels would
+  // search -- and every key at least two of them share gets a snapshot, built from its
+  // representative's deepest snapshot. The open windows then look the new level up (a hit replaces
+  // their entry's snapshot) and the lane kernel runs again over those it leaves small.
+  const uint32_t demand_k = (uint32_t)(diag_env("FAC_RC_DEMAND") ? std::strtoul(diag_env("FAC_RC_DEMAND"), nullptr, 10) : 0ul);
+  bool demand_done = false;
+  uint32_t demand_keys = 0;
+  auto demand_stage = [&]() -> int {
+    uint32_t kmax = 0;
+    for (const RcTable& t : tabs) kmax = std::max(kmax, t.k);
+    const size_t n_sampled = tabs.size() - 1 - (n_ent0 ? 1 : 0);
+    if (!rc_build_fn || demand_k <= kmax || demand_k > 8 || P.rc_ntab >= (uint32_t)kRcLevels ||
+        1 + n_sampled > (size_t)kRcLevels - 2)
+      return FAC_OK;
+    const int xi = kRcLevels - 2;  // the count buffers the sampled levels leave free
+    uint32_t slots_d = 1u << 12;
+    while (slots_d < std::min<uint64_t>(windows / 2, 1ull << 26)) slots_d <<= 1;
+    const uint32_t max_entd = std::min<uint32_t>(slots_d / 2, 16u << 20);
+    HIP_TRY(d_xk[xi].alloc(slots_d * sizeof(unsigned long long), stream));
+    HIP_TRY(d_xv[xi].alloc(slots_d * sizeof(uint32_t), stream));
+    HIP_TRY(d_xslot[xi].alloc(slots_d * sizeof(uint64_t), stream));
+    HIP_TRY(d_xrep[xi].alloc(max_entd * sizeof(uint64_t), stream));
+    HIP_TRY(d_xc[xi].alloc(2 * (size_t)max_entd * sizeof(uint32_t), stream));
+    HIP_TRY(hipEventRecord(ev.a, stream));
+    HIP_TRY(hipMemsetAsync(d_xk[xi].p, 0, slots_d * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(d_xv[xi].p, 0, slots_d * sizeof(uint32_t), stream));
+    const uint64_t n_reg = P.total_windows / RC_REGION;
+    const uint32_t rgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_reg + 3) / 4, (uint64_t)cus * 8));
+    hipLaunchKernelGGL(rc_count_open_kernel, dim3(rgrid), dim3(256), 0, stream, P,
+                       RcCountTarget{static_cast<unsigned long long*>(d_xk[xi].p), static_cast<uint32_t*>(d_xv[xi].p),
+                                     static_cast<uint64_t*>(d_xslot[xi].p), slots_d - 1, demand_k});
+    HIP_TRY(hipGetLastError());
+    unsigned int nk = 0;
+    if (int nrc = rc_number_fn(d_xk[xi], d_xv[xi], d_xslot[xi], d_xrep[xi], slots_d, 2u, max_entd, nk)) return nrc;
+    demand_keys = std::min(nk, max_entd);
+    if (demand_keys == 0) return FAC_OK;
+    RcTable D{demand_k, slots_d - 1, static_cast<const unsigned long long*>(d_xk[xi].p),
+              static_cast<const uint32_t*>(d_xv[xi].p), static_cast<uint32_t*>(d_xc[xi].p) + max_entd,
+              static_cast<uint32_t*>(d_xc[xi].p)};
+    build_cnt = N_COUNTERS;  // the pass's counters hold its records so far
+    int brc = rc_build_fn(D, demand_keys, static_cast<const uint64_t*>(d_xrep[xi].p), stream, false, true);
+    build_cnt = 0;
+    if (brc) return brc;
+    if ((brc = rc_publish_fn(D, demand_keys, d_ct[1 + n_sampled], stream, false))) return brc;
+    SearchParams R = P;
+    R.rc_ntab = 1;
+    R.rc_tab[0] = D;
+    hipLaunchKernelGGL(rc_relookup_open_kernel, dim3(rgrid), dim3(256), 0, stream, R);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev.b, stream));
+    HIP_TRY(hipMemsetAsync(static_cast<unsigned long long*>(d_cnt.p) + 9, 0, sizeof(unsigned long long), stream));
+    if (int lrc = launch_lane()) return lrc;
+    HIP_TRY(hipEventRecord(ev_lane, stream));
+    HIP_TRY(hipEventSynchronize(ev_lane));
+    float a = 0.f, b = 0.f;
+    HIP_TRY(hipEventElapsedTime(&a, ev.a, ev.b));
+    HIP_TRY(hipEventElapsedTime(&b, ev.b, ev_lane));
+    cache_ms += a;
+    lane_ms += b;
+    if (int drc = lane_debug_line(b)) return drc;
+    if (diag_env("FAC_RC_DEBUG"))
+      std::fprintf(stderr, "FAC_RC demand level k=%u keys=%u (seen >= 2 among the open windows) %.3f ms, lane again %.3f ms\n",
+                   demand_k, demand_keys, a, b);
+    // a pass run again (buffer growth) looks it up first
+    for (uint32_t t = P.rc_ntab; t > 0; --t) P.rc_tab[t] = P.rc_tab[t - 1];
+    P.rc_tab[0] = D;
+    ++P.rc_ntab;
+    if (!live_builds) {
+      for (uint32_t t = n_exact_tabs; t > 0; --t) exact_tab[t] = exact_tab[t - 1];
+      exact_tab[0] = D;
+      ++n_exact_tabs;
+    } else {
+      any_inexact = true;
+    }
+    tabs.push_back(D);
+    tab_exact.push_back(!live_builds);
+    return FAC_OK;
+  };
   const uint64_t rc_auto = P.beam ? 256ull : std::min<uint64_t>(4096, std::max<uint64_t>(256, pass_windows / (16ull * max_grid)));
   const uint32_t rc_chunk = (uint32_t)std::min<unsigned long>(4096, std::max<unsigned long>(64,
       diag_env("FAC_RC_CHUNK") ? std::strtoul(diag_env("FAC_RC_CHUNK"), nullptr, 10) : rc_auto));
@@ -4825,14 +4997,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         if (!ev_lane) HIP_TRY(hipEventCreate(&ev_lane));
         P.lane_debug = diag_env("FAC_RC_DEBUG") ? 1 : 0;
         P.lane_popmax = (uint32_t)std::max<unsigned long>(1, diag_env("FAC_LANE_POPS") ? std::strtoul(diag_env("FAC_LANE_POPS"), nullptr, 10) : 32ul);
-        // one wave per workgroup; each takes its best lists from its own emit-scratch slice
-        const uint32_t lgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + LANE_CHUNK - 1) / LANE_CHUNK, (uint64_t)max_grid));
-        static_assert(16 * 64 <= 1024, "lane best lists must fit the emit scratch slice (P.ecap >= 1024)");
-        // 16-state rings by default (C3: lane 19 ms + wave kernel 37 ms, against 6 + 58 with 8 states)
-        if (diag_env("FAC_LANE_Q8")) hipLaunchKernelGGL((lane_window_kernel<8, 8>), dim3(lgrid), dim3(64), 0, stream, P);
-        else if (diag_env("FAC_LANE_Q32")) hipLaunchKernelGGL((lane_window_kernel<32, 8>), dim3(lgrid), dim3(64), 0, stream, P);
-        else hipLaunchKernelGGL((lane_window_kernel<16, 8>), dim3(lgrid), dim3(64), 0, stream, P);
-        HIP_TRY(hipGetLastError());
+        if (int lrc = launch_lane()) return lrc;
         HIP_TRY(hipEventRecord(ev_lane, stream));
       }
       HIP_TRY(hipEventSynchronize(lane_on ? ev_lane : ev.b));
@@ -4855,14 +5020,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (lane_on) {
         HIP_TRY(hipEventElapsedTime(&lms, ev.b, ev_lane));
         lane_ms += lms;
-        if (diag_env("FAC_RC_DEBUG")) {
-          unsigned long long d[8];
-          HIP_TRY(hipMemcpyFromSymbol(d, HIP_SYMBOL(g_lane_dbg), sizeof(d)));
-          std::fprintf(stderr, "FAC_LANE taken=%llu finished=%llu bailed=%llu ms=%.3f popmax=%u trips=%llu run_cycles=%llu "
-                       "wave_cycles=%llu rounds=%llu\n", d[0], d[1], d[2], lms, P.lane_popmax, d[4], d[5], d[6], d[7]);
-          std::memset(d, 0, sizeof(d));
-          HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_lane_dbg), d, sizeof(d)));
-        }
+        if (int drc = lane_debug_line(lms)) return drc;
+      }
+      if (demand_k && lane_on && !demand_done) {
+        demand_done = true;
+        if (int drc = demand_stage()) return drc;
       }
     }
     if (int src = prep_slots(P, stream, kVariants[vi].qcap, kVariants[vi].vcap > 0)) {

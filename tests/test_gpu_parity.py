@@ -393,6 +393,27 @@ def test_prefix_cache_two_levels_c3_slice(k2, monkeypatch):
     assert len(on) > 0 and sorted(on.tolist()) == sorted(off.tolist()) == sorted(one.tolist())
 
 
+@pytest.mark.parametrize("demand,levels", [("6", "5"), ("7", "5,6"), ("8", "5,7")])
+def test_prefix_cache_demand_level_c3_slice(demand, levels, monkeypatch):
+    """The demand level (keys counted over the windows still open after the lookups and the lane
+    kernel, built from their deepest snapshots, looked up again, lane kernel re-run): identical
+    records to the cache off on a C3-shaped haystack, with the level actually replaying pops."""
+    from fuzzy_aho_corasick import workloads
+    w = workloads.config("c3", 2 << 20, 3)
+    eng = workloads.builder_for(w).build(w.patterns)
+    staged = eng.stage(w.haystack)
+    monkeypatch.setenv("FAC_RC_MIN2", "1")
+    monkeypatch.setenv("FAC_RC_LEVELS", levels)
+    monkeypatch.setenv("FAC_RC_DEMAND", "0")
+    base, st_base = staged.search_windows_records(w.threshold)
+    monkeypatch.setenv("FAC_RC_DEMAND", demand)
+    on, st_on = staged.search_windows_records(w.threshold)
+    monkeypatch.setenv("FAC_NO_RC", "1")
+    off, _ = staged.search_windows_records(w.threshold)
+    assert st_on.states_cached > st_base.states_cached
+    assert len(on) > 0 and sorted(on.tolist()) == sorted(off.tolist()) == sorted(base.tolist())
+
+
 def test_prefix_cache_default_on_c3_slice(monkeypatch):
     """A C3-shaped haystack large enough for the default cache (4-char keys): identical records with
     the cache on and off; a slice with the cache forced on == the oracle."""

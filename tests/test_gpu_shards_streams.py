@@ -222,11 +222,11 @@ def test_stream_many_windows_in_order():
 
 @pytest.mark.gpu
 def test_device_utf8_check_matches_python():
-    """fac_haystack_stage checks the bytes on the device (validate_kernel: per 16-byte chunk, from its
-    first non-continuation byte) and decides search.rs:196's is_ascii there: accepted exactly when
+    """fac_haystack_stage checks the bytes on the device (seg_tile_kernel: per 64-byte thread range, from
+    its first non-continuation byte) and decides search.rs:196's is_ascii there: accepted exactly when
     Python's strict decoder (like Rust's str::from_utf8: no overlongs, surrogates, > U+10FFFF,
     truncations or stray continuation bytes) accepts, with invalid sequences planted at and around
-    the chunk boundaries; accepted haystacks search like the oracle."""
+    the 64-byte range and 16 KiB tile boundaries; accepted haystacks search like the oracle."""
     import random
     from fuzzy_aho_corasick import DeviceError
     from fuzzy_aho_corasick._native import FAC_E_INVALID
@@ -244,12 +244,13 @@ def test_device_utf8_check_matches_python():
         return bytes(out)
 
     checked = 0
-    for trial in range(120):
-        base = text(rng.choice([40, 255, 256, 300, 700, 1500, 5000]))
+    for trial in range(160):
+        base = text(rng.choice([40, 255, 256, 300, 700, 1500, 5000, 17000]))
         data = base
         if trial % 4:  # plant an invalid (or, cut mid-sequence, sometimes valid) piece
             piece = rng.choice(bad)
-            at = rng.choice([0, 1, 255, 256, 257, 511, 512, len(base) - 1, len(base), rng.randrange(len(base) + 1)])
+            at = rng.choice([0, 1, 63, 64, 65, 127, 128, 255, 256, 257, 511, 512, 16383, 16384, 16385, len(base) - 1, len(base),
+                             rng.randrange(len(base) + 1)])
             at = max(0, min(len(base), at))
             data = base[:at] + piece + base[at:]
         try:
