@@ -1802,7 +1802,8 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u) {
         const uint32_t i = b + u * 64 + lane;
-        if (i < nw) w[u] = src[i];
+        // (a dedup-free variant has no table for the snapshot's dedup entries: not loaded)
+        if (i < nw && (VCAP > 0 || i < nq || i >= nq + nv)) w[u] = src[i];
       }
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u) {
@@ -1876,6 +1877,7 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
         if (j < S.n) g0 = text_gid(P, S, j, err);
         if (j + 1 < S.n) g1 = text_gid(P, S, j + 1, err);
       }
+
     bool found = false;
     uint32_t stored_bits = 0, vslot = EMPTY;
     if constexpr (VCAP > 0)  // VCAP == 0: no dedup (unbeamed only)

@@ -93,6 +93,14 @@ if not os.path.exists(LIB_PATH):
         f"libfac.so not found at {LIB_PATH}; build it with `make -C fuzzy-aho-corasick-rs_amd/csrc` "
         "(or __graft_entry__.build()). There is no fallback implementation.")
 
+# torch (used beside the library for device buffers, streams and torch.distributed) brings up its
+# own HIP runtime first: on some hosts torch's bundled runtime fails to initialise ("No HIP GPUs are
+# available") once another HIP runtime in the process -- this library's -- has made device calls.
+try:
+    import torch as _torch
+    _torch.cuda.is_available()
+except ImportError:
+    pass
 lib = ctypes.CDLL(LIB_PATH)
 
 _P = ctypes.POINTER
