@@ -2242,37 +2242,7 @@ __device__ __forceinline__ uint32_t rc_key_hash(uint4 k) {
   return (uint32_t)(h >> 32) ^ (uint32_t)h;
 }
 
-// A window's prefix-cache hit (snapshot header, read with the lookup): off = EMPTY on a miss.
-// Every level's probe chain (key slot, entry, snapshot count/offset) is issued together; the
-// deepest level whose snapshot header verifies the chars wins.
-#ifdef FAC_RC_SERIAL_LOOKUP
-__device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s, uint32_t QCAP) {
-  for (uint32_t t = 0; t < P.rc_ntab; ++t) {
-    const RcTable& T = P.rc_tab[t];
-    RcChars ch;
-    uint64_t k;
-    if (!rc_key(P, S, s, T.k, ch, k)) continue;
-    const uint32_t h = rc_hash(k);
-    for (uint32_t p = 0; p < RC_PROBES; ++p) {
-      const uint32_t slot = (h + p) & T.mask;
-      const unsigned long long kk = T.keys[slot];
-      if (kk == k) {
-        const uint32_t ent = T.val[slot];
-        if (ent == EMPTY) break;
-        const uint32_t cnt = T.count[ent], off = T.off[ent];
-        if (cnt == EMPTY || cnt + 1u > QCAP) break;
-        const uint4 h0 = P.rc_pool[off], h1 = P.rc_pool[off + 1], sa = P.rc_pool[off + 2], sb = P.rc_pool[off + 3];
-        if (sa.x == ch.a.x && sa.y == ch.a.y && sa.z == ch.a.z && sa.w == ch.a.w && sb.x == ch.b.x &&
-            sb.y == ch.b.y && sb.z == ch.b.z && sb.w == ch.b.w)
-          return RcHit{off, h0.x, h0.y, h0.z | (h1.x << 16), h0.w};
-        break;
-      }
-      if (kk == 0ull) break;
-    }
-  }
-  return RcHit{EMPTY, 0u, 0u, 0u, 0u};
-}
-#else
+// A window's prefix-cache hit (from the levels' exact-key lookup tables): off = EMPTY on a miss.
 __device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s, uint32_t QCAP) {
   uint32_t kmax = 0;
   for (uint32_t t = 0; t < P.rc_ntab; ++t) kmax = max(kmax, P.rc_tab[t].k);
@@ -2313,7 +2283,6 @@ __device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc&
   }
   return r;
 }
-#endif
 
 // Lookup table of a built level: every entry with a snapshot is inserted under its exact key (the
 // chars from the snapshot header); keys holding a char >= 0xFFFF stay out (such windows resume
