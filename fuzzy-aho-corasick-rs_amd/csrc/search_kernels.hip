@@ -1670,12 +1670,12 @@ __device__ __forceinline__ void sink64(uint64_t v) {
 #endif
 
 constexpr uint32_t RC_POOL_CHUNK = 4096;  // largest pool chunk (words, 64 KiB) a building wave takes
-// snapshot header words: {head, tail, nv, pops}, {ne, jcheck | ncheck << 16, jbeam, jp1}, chars 0-3,
-// chars 4-7; jp1 = 1 + the largest j popped in the chain, jbeam = jp1 at the chain's last beam event (0:
+// snapshot header words: {head, tail, nv, pops}, {ne, jcheck | ncheck << 16, jbeam, jp1} (the key's
+// chars are read from the representative's text by rc_publish_kernel); jp1 = 1 + the largest j popped in the chain, jbeam = jp1 at the chain's last beam event (0:
 // none), jcheck = min(jbeam, 1 + the largest j of the dedup entries): the entries a resumed dedup-free
 // run must still honour have j < jcheck (the others were popped after every beam: their subtrees are
 // intact); they are the first ncheck dedup entries (0: none)
-constexpr uint32_t RC_HDR = 4;
+constexpr uint32_t RC_HDR = 2;  // {head, tail, nv, pops}, {ne, jcheck | ncheck << 16, jbeam, jp1}
 struct RcHit {  // prefix-cache snapshot of a window (rc_lookup): pool offset and header
   uint32_t off, head, tail, nv_nel, pops;
   uint32_t lvl = 0;  // rc_tab index of the hit (diagnostics)
@@ -1759,11 +1759,14 @@ template <uint32_t VCAP, uint32_t QCAP, bool MAP, bool LIVE = false>
 __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
                            uint32_t& cseq, EmitList& EL, uint64_t start, const RcHit& rc, uint64_t& popped,
                            uint64_t& cached, unsigned& err, uint32_t& head_out, uint32_t& vcount_out,
-                           KState* live = nullptr, uint32_t* jbeam_out = nullptr, uint4* bsel = nullptr) {
-  const uint32_t lane = lane_id();
+                           KState* live = nullptr, uint32_t* jbeam_out = nullptr, uint4* bsel = nullptr
 #ifdef FAC_PHASE_PROF
-  uint64_t prof_acc[20] = {};  // 12: per-edge states, 13: fast states, 14: committed, 15: loaded, 16-19: Bc buckets
+                           , uint64_t* prof_acc = nullptr  // the wave's accumulators (bfs_window_body), added up at its end
 #endif
+                           ) {
+  const uint32_t lane = lane_id();
+  // FAC_PHASE_PROF slots: 12: per-edge states, 13: fast states, 14: committed, 15: loaded, 16-19: Bc
+  // buckets, 20: prologue (table clear, snapshot load), 21: flush
   PROF_T(t_win);
   if constexpr (VCAP > 0)
     for (uint32_t i = lane; i < VCAP; i += 64) vis[i].node = EMPTY;
@@ -1832,6 +1835,7 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
   }
   __builtin_amdgcn_wave_barrier();
   const uint32_t beam2 = 2u * P.beam;
+  PROF_ACC(20, t_win);
 
   while (head < tail) {
     PROF_T(t0);
@@ -2117,11 +2121,15 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     prof_acc[8] += 1;  // batches
     prof_acc[14] += Bc;
     prof_acc[15] += B;
-    prof_acc[16 + (Bc <= 4 ? 0 : Bc <= 16 ? 1 : Bc <= 40 ? 2 : 3)] += 1;
+    prof_acc[16] += Bc <= 4 ? 1 : 0;  // constant indices: the accumulators stay in registers
+    prof_acc[17] += Bc > 4 && Bc <= 16 ? 1 : 0;
+    prof_acc[18] += Bc > 16 && Bc <= 40 ? 1 : 0;
+    prof_acc[19] += Bc > 40 ? 1 : 0;
 #endif
     if (any_err(err)) break;
   }
 
+  PROF_T(t_fl);
   head_out = head;
   vcount_out = vcount;
   if (jbeam_out) {
@@ -2143,9 +2151,8 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     }
   }
 #ifdef FAC_PHASE_PROF
+  PROF_ACC(21, t_fl);
   PROF_ACC(7, t_win);
-  if (lane == 0)
-    for (int i = 0; i < 20; ++i) atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + i], (unsigned long long)prof_acc[i]);
 #endif
   return tail;  // states pushed this window, the root included: the reference's queue.len()
 }
@@ -2287,13 +2294,19 @@ __device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc&
 // Lookup table of a built level: every entry with a snapshot is inserted under its exact key (the
 // chars from the snapshot header); keys holding a char >= 0xFFFF stay out (such windows resume
 // from a shorter key).
-__global__ __launch_bounds__(256) void rc_publish_kernel(const uint4* pool, const uint32_t* off, const uint32_t* count,
-                                                         uint32_t n_ent, uint32_t k, uint4* ct, uint32_t mask) {
+__global__ __launch_bounds__(256) void rc_publish_kernel(SearchParams P, const uint64_t* reps, const uint4* pool,
+                                                         const uint32_t* off, const uint32_t* count, uint32_t n_ent,
+                                                         uint32_t k, uint4* ct, uint32_t mask) {
   for (uint32_t ent = blockIdx.x * blockDim.x + threadIdx.x; ent < n_ent; ent += gridDim.x * blockDim.x) {
     if (count[ent] == EMPTY) continue;
     const uint32_t o = off[ent];
-    const uint4 h0 = pool[o], h1 = pool[o + 1], sa = pool[o + 2], sb = pool[o + 3];
-    const uint32_t c[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+    const uint4 h0 = pool[o], h1 = pool[o + 1];
+    // the key: the first k chars of the representative window (the build's own window)
+    const uint64_t wid = reps[ent];
+    const uint32_t kl = find_seg(P, wid);
+    const SegDesc S = P.segs[kl];
+    uint32_t c[8];
+    if (!rc_chars(P, S, S.w_begin + (wid - P.seg_prefix[kl]), k, c)) continue;
     bool enc = true;
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) enc = enc && (i >= k || c[i] == RC_PAD || c[i] < 0xFFFFu);
@@ -3031,6 +3044,11 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   __shared__ KState s_q[QCAP];
   __shared__ __attribute__((aligned(16))) uint32_t s_claim[claim_slots(VCAP)];
   const uint32_t lane = lane_id();
+#ifdef FAC_PHASE_PROF
+  const uint64_t t_life = __builtin_amdgcn_s_memtime();
+  uint64_t t_grp = 0;  // group setup (lookups / hit loads) per 64 windows
+  uint64_t prof_acc[24] = {};  // run_window's slots (per wave, in registers), 22: build epilogue
+#endif
   const uint32_t slot = slot_acquire(P);
   EmitList EL{P.ebuf + (size_t)slot * P.ecap, P.ecap, 0};
   uint4* bsel = (VCAP > 0 && P.bsel) ? P.bsel + (size_t)slot * P.bsel_stride : nullptr;
@@ -3090,6 +3108,9 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
     }
     for (uint64_t v0 = cb; v0 < ce; v0 += 64) {
       if (!((live_groups >> ((v0 - cb) >> 6)) & 1ull)) continue;
+#ifdef FAC_PHASE_PROF
+      const uint64_t t_g0 = __builtin_amdgcn_s_memtime();
+#endif
       const uint64_t v = v0 + lane;
       bool active = v < ce;
       uint32_t kl = 0;
@@ -3127,6 +3148,9 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         active = active && !done;
       }
       uint64_t m = __ballot(active);
+#ifdef FAC_PHASE_PROF
+      t_grp += __builtin_amdgcn_s_memtime() - t_g0;
+#endif
       while (m) {
         const int l = first_lane(m);
         m &= m - 1;
@@ -3142,7 +3166,11 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
 #endif
         const uint32_t qlen =
             run_window<VCAP, QCAP, MAP, LIVE>(P, S, s_vis, s_q, s_claim, cseq, EL, st, rc, popped, cached, err, qhead,
-                                              vcnt, s_live, jbeam, bsel);
+                                              vcnt, s_live, jbeam, bsel
+#ifdef FAC_PHASE_PROF
+                                              , prof_acc
+#endif
+                                              );
 #ifdef FAC_WIN_HIST
         if (lane == 0 && P.rc_mode != 2) {
           const uint32_t b = hist_bucket(popped - popped0);
@@ -3152,7 +3180,14 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           atomicAdd(&g_hist[18 + b], rc.off != EMPTY ? 1ull : 0ull);
         }
 #endif
-        if (P.rc_mode == 2) {  // cache build: entry = list position; what does not fit stays uncached
+        if (LK && P.rc_mode == 2) {  // cache build: entry = list position; what does not fit stays uncached
+#ifdef FAC_PHASE_PROF
+          struct EpAcc {
+            uint64_t t;
+            uint64_t& acc;
+            __device__ ~EpAcc() { acc += __builtin_amdgcn_s_memtime() - t; }
+          } ep_acc{__builtin_amdgcn_s_memtime(), prof_acc[22]};
+#endif
           const uint32_t ent = (uint32_t)(v0 + (uint64_t)l);
           const uint32_t nq = qlen - qhead;
           // live dedup entries: a key is only met again at its own j, and every future state's j is
@@ -3162,12 +3197,21 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           jmin = wave_min_u32(jmin);
           auto live = [&](const KState& k) { return k.node != EMPTY && (k.jm & 0xFFFFu) >= jmin; };
           uint32_t nv = 0, jlive = 0;  // 1 + the largest j among the live entries (0: none)
-          if constexpr (VCAP > 0)
-            for (uint32_t b = 0; b < VCAP; b += 64) {
-              const KState k = s_vis[b + lane];
-              nv += (uint32_t)__popcll(__ballot(live(k)));
-              jlive = max(jlive, live(k) ? (k.jm & 0xFFFFu) + 1u : 0u);
+          // the table is read once: each lane's VCAP/64 slots into registers, their live bits kept
+          constexpr uint32_t NSL = VCAP ? VCAP / 64 : 1;
+          KState kv[NSL];
+          uint32_t lmask = 0;
+          if constexpr (VCAP > 0) {
+#pragma unroll
+            for (uint32_t u = 0; u < NSL; ++u) kv[u] = s_vis[u * 64 + lane];
+#pragma unroll
+            for (uint32_t u = 0; u < NSL; ++u) {
+              const bool lv = live(kv[u]);
+              lmask |= (lv ? 1u : 0u) << u;
+              nv += (uint32_t)__popcll(__ballot(lv));
+              jlive = max(jlive, lv ? (kv[u].jm & 0xFFFFu) + 1u : 0u);
             }
+          }
           // LIVE (dedup-free) build: no table of its own; the snapshot carries the parent's check
           // entries that a later pop can still meet (jmin <= j < the parent's jcheck) -- no beam ran
           // in this build, so they remain the only entries popped before a beam (run_window LIVE)
@@ -3208,9 +3252,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           const unsigned long long off = pool_cur;
           if (!bad) pool_cur += words;
           bad = bad || off + words > P.rc_pool_cap || off > 0xFFFFFFF0ull;
-          RcChars kch;
-          uint64_t kkey;
-          bad = bad || !rc_key(P, S, st, P.rc_k, kch, kkey);
+          // (the key's chars are not stored: rc_publish_kernel reads them from the representative's text)
           uint4* dst = P.rc_pool + off + RC_HDR;  // after the header words
           for (uint32_t i = lane; i < nq && !bad; i += 64) {
             const KState k = s_q[(qhead + i) & (QCAP - 1)];
@@ -3221,16 +3263,22 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           const uint32_t jcheck = min(jlive, jbeam[0]);
           uint32_t ncheck = 0;
           if constexpr (VCAP > 0) {
+            uint32_t cmask = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < NSL; ++u)
+              cmask |= (((lmask >> u) & 1u) && (kv[u].jm & 0xFFFFu) + 1u <= jcheck ? 1u : 0u) << u;
             uint32_t at0 = 0;
-            for (uint32_t pass = 0; pass < 2; ++pass)
-              for (uint32_t b = 0; b < VCAP && !bad; b += 64) {
-                const KState k = s_vis[b + lane];
-                const bool occ = live(k) && (((k.jm & 0xFFFFu) + 1u <= jcheck) == (pass == 0));
+            for (uint32_t pass = 0; pass < 2 && !bad; ++pass) {
+              const uint32_t sel = pass == 0 ? cmask : (lmask & ~cmask);
+#pragma unroll
+              for (uint32_t u = 0; u < NSL; ++u) {
+                const bool occ = (sel >> u) & 1u;
                 const uint64_t m = __ballot(occ);
-                if (occ) dst[nq + at0 + prefix_below(m)] = make_uint4(k.node, k.jm, __float_as_uint(k.pen), k.packed);
+                if (occ) dst[nq + at0 + prefix_below(m)] = make_uint4(kv[u].node, kv[u].jm, __float_as_uint(kv[u].pen), kv[u].packed);
                 at0 += (uint32_t)__popcll(m);
-                if (pass == 0) ncheck = at0;
               }
+              if (pass == 0) ncheck = at0;
+            }
           } else if constexpr (LIVE) {  // every carried entry is a check entry
             uint32_t at0 = 0;
             for (uint32_t b = 0; b < ncarry && !bad; b += 64) {
@@ -3250,8 +3298,6 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
               P.rc_pool[off] = make_uint4(qhead, qlen, nv, (uint32_t)(popped - popped0) + rc.pops);
               // jcheck: dedup entries a resumed dedup-free run must still honour (j + 1 <= jcheck)
               P.rc_pool[off + 1] = make_uint4(EL.n, ncheck ? (jcheck | (ncheck << 16)) : 0u, jbeam[0], jbeam[1]);
-              P.rc_pool[off + 2] = kch.a;
-              P.rc_pool[off + 3] = kch.b;
             }
             P.rc_off[ent] = bad ? EMPTY : (uint32_t)off;
             P.rc_count[ent] = bad ? EMPTY : nq;
@@ -3282,6 +3328,13 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
     if (any_err(err)) break;
   }
   if (lane == 0) atomicAdd(P.counters + 1, (unsigned long long)popped);
+#ifdef FAC_PHASE_PROF
+  if (lane == 0) {
+    for (int i = 0; i < 23; ++i) atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + i], (unsigned long long)prof_acc[i]);
+    atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + 23], (unsigned long long)t_grp);
+    atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + 24], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_life));
+  }
+#endif
   if (lane == 0) cached_lane += cached;
   wave_add_counter(P.counters + 4, cached_lane);
   wave_add_counter(P.counters + 5, res_lane);
@@ -4375,7 +4428,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   bool live_builds = false;
   uint64_t ct_mult = 4;
   std::function<int(const RcTable&, uint32_t, const uint64_t*, hipStream_t, bool, bool)> rc_build_fn;
-  std::function<int(RcTable&, uint32_t, DevBuf&, hipStream_t, bool)> rc_publish_fn;
+  std::function<int(RcTable&, uint32_t, const uint64_t*, DevBuf&, hipStream_t, bool)> rc_publish_fn;
   std::function<int(const DevBuf&, const DevBuf&, const DevBuf&, const DevBuf&, uint32_t, uint32_t, uint32_t, unsigned int&)>
       rc_number_fn;
   // after its build a level's entries are published into an exact-key lookup table (4 slots per
@@ -4605,13 +4658,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       }
       return FAC_OK;
     };
-    auto publish = [&](RcTable& T, uint32_t n_ent, DevBuf& ct, hipStream_t bs, bool cleared = false) -> int {
+    auto publish = [&](RcTable& T, uint32_t n_ent, const uint64_t* reps, DevBuf& ct, hipStream_t bs,
+                       bool cleared = false) -> int {
       const uint32_t cs = ct_slots(n_ent);
       if (!cleared) {
         if (int crc = clear_ct(n_ent, ct, bs)) return crc;
       }
       hipLaunchKernelGGL(rc_publish_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_ent + 255) / 256, cus * 8))),
-                         dim3(256), 0, bs, static_cast<const uint4*>(P.rc_pool), T.off, T.count, n_ent, T.k,
+                         dim3(256), 0, bs, P, reps, static_cast<const uint4*>(P.rc_pool), T.off, T.count, n_ent, T.k,
                          static_cast<uint4*>(ct.p), cs - 1);
       HIP_TRY(hipGetLastError());
       T.ct = static_cast<const uint4*>(ct.p);
@@ -4664,14 +4718,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (n_ent0) {
         int brc = build(L0, n_ent0, static_cast<const uint64_t*>(d_l0rep.p), bstream, true);
         if (brc) return brc;
-        if ((brc = publish(L0, n_ent0, d_ct[kRcLevels - 1], bstream, true))) return brc;
+        if ((brc = publish(L0, n_ent0, static_cast<const uint64_t*>(d_l0rep.p), d_ct[kRcLevels - 1], bstream, true))) return brc;
         tabs.push_back(L0);
         tab_exact.push_back(true);
         HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), bstream));
       }
       int brc = build(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p), bstream, true);
       if (brc) return brc;
-      if ((brc = publish(L1, n_ent1, d_ct[0], bstream, true))) return brc;
+      if ((brc = publish(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p), d_ct[0], bstream, true))) return brc;
       if (bstream != stream) HIP_TRY(hipEventRecord(l1_done, bstream));
       tabs.push_back(L1);
       tab_exact.push_back(true);
@@ -4759,7 +4813,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       for (size_t x = 0; x < Lx.size(); ++x) {
         int brc = build(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), stream, false, true);
         if (brc) return brc;
-        if ((brc = publish(Lx[x], n_entx[x], d_ct[1 + x], stream))) return brc;
+        if ((brc = publish(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), d_ct[1 + x], stream))) return brc;
         tabs.push_back(Lx[x]);
         tab_exact.push_back(!live_builds);
       }
@@ -4889,7 +4943,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     int brc = rc_build_fn(D, demand_keys, static_cast<const uint64_t*>(d_xrep[xi].p), stream, false, true);
     build_cnt = 0;
     if (brc) return brc;
-    if ((brc = rc_publish_fn(D, demand_keys, d_ct[1 + n_sampled], stream, false))) return brc;
+    if ((brc = rc_publish_fn(D, demand_keys, static_cast<const uint64_t*>(d_xrep[xi].p), d_ct[1 + n_sampled], stream, false))) return brc;
     SearchParams R = P;
     R.rc_ntab = 1;
     R.rc_tab[0] = D;
@@ -5050,9 +5104,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         std::fprintf(stderr, "FAC_PROF %s variant=%u,%u beam_select=%llu phaseA=%llu wide=%llu phaseB=%llu phaseC=%llu "
                      "emit=%llu push=%llu window_total=%llu batches=%llu [B: prep=%llu units=%llu finish=%llu] "
                      "states: per-edge=%llu fast=%llu committed=%llu loaded=%llu Bc<=4:%llu <=16:%llu <=40:%llu >40:%llu "
-                     "main_popped=%llu\n",
+                     "main_popped=%llu prologue=%llu flush=%llu build_epilogue=%llu group_setup=%llu wave_life=%llu\n",
                      m ? "builds" : "main", kVariants[vi].vcap, kVariants[vi].qcap, q[0], q[1], q[2], q[3], q[4], q[5],
-                     q[6], q[7], q[8], q[9], q[10], q[11], q[12], q[13], q[14], q[15], q[16], q[17], q[18], q[19], cnt[1]);
+                     q[6], q[7], q[8], q[9], q[10], q[11], q[12], q[13], q[14], q[15], q[16], q[17], q[18], q[19], cnt[1],
+                     q[20], q[21], q[22], q[23], q[24]);
       }
       std::memset(pr, 0, sizeof(pr));
       HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), pr, sizeof(pr)));
