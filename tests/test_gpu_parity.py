@@ -48,6 +48,9 @@ ASCII_VOCAB = ["hello", "world", "vestibulum", "abc", "lorem", "cell", "saddam",
 ASCII_FILLER = ["a", "b", "c", "d", "e", " ", "1", "o", "0", "l", "S", "H"]
 UNI_VOCAB = ["café", "naïve", "Ωμέγα", "Москва", "señor", "école", "résumé"]
 UNI_FILLER = ["a", "é", "ñ", "ω", "м", " ", "o", "0", "é", "Ω", "\r\n", "Σ"]
+# code points beyond the BMP: swaps there take the two-lookup path (GT_SWAP entries are BMP-only)
+ASTRAL_VOCAB = ["a😀b", "𝒜bc", "𐍈𐌹𐍈", "x😀y😀", "hello", "b𝒜a"]
+ASTRAL_FILLER = ["😀", "𝒜", "a", "b", " ", "𐍈", "c", "x", "𐌹", "y"]
 
 
 def random_case(rng, vocab, filler, allow_beam=True, allow_limits=True):
@@ -84,6 +87,7 @@ def random_case(rng, vocab, filler, allow_beam=True, allow_limits=True):
 @pytest.mark.parametrize("seed,vocab,filler", [
     (0x1234_5678_9abc_def1, ASCII_VOCAB, ASCII_FILLER),
     (0xdead_beef_0bad_f00d, UNI_VOCAB, UNI_FILLER),
+    (0x0a57_2a1c_0de5_51de, ASTRAL_VOCAB, ASTRAL_FILLER),
 ])
 def test_differential_random(seed, vocab, filler, per_edge_only, root_cache, monkeypatch):
     """per_edge_only: FAC_NO_FAST disables the O(1) goto-table expansion, so the per-edge unit
