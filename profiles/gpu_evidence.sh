@@ -42,10 +42,6 @@ if has c5; then  # one GPU's full 12.5 GiB share of the 100 GiB stream, CPU base
   timeout -k 10 600 python bench.py --config c5 --steps 2 > "$OUT/bench_c5.json" 2> "$OUT/bench_c5.err"
   cat "$OUT/bench_c5.json"
 fi
-if has c5t; then  # after traffic_c5.json exists
-  timeout -k 10 600 python bench.py --config c5 --steps 2 > "$OUT/bench_c5_traffic.json" 2> "$OUT/bench_c5_traffic.err"
-  cat "$OUT/bench_c5_traffic.json"
-fi
 export TMPDIR=/tmp
 if has kt; then
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o c3 \
@@ -74,6 +70,10 @@ if has pmc5; then  # C5: one GPU's 12.5 GiB share of the 100 GiB stream
   python3 profiles/make_traffic.py c5 102400 1 "$OUT/c5_pmc_FETCH_SIZE.csv" "$OUT/c5_pmc_WRITE_SIZE.csv" "$(python3 -c "import bench; print(bench.sources_sha())")" > "$OUT/traffic5.log"
   cp profiles/traffic_c5.json "$OUT/traffic_c5.json"
   head -c 1500 "$OUT/traffic5.log"
+fi
+if has c5t; then  # after traffic_c5.json exists
+  timeout -k 10 600 python bench.py --config c5 --steps 2 > "$OUT/bench_c5_traffic.json" 2> "$OUT/bench_c5_traffic.err"
+  cat "$OUT/bench_c5_traffic.json"
 fi
 if has c3t; then  # bench after traffic.json exists: the line carries roofline.traffic
   timeout -k 10 400 python bench.py > "$OUT/bench_c3_traffic.json" 2> "$OUT/bench_c3_traffic.err"
