@@ -4579,8 +4579,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       // and lookup probes than it saves (C2 1 GiB: 266 -> 188 ms per step with "5" alone)
       // beamed engines (the reference's select_nth_unstable_by order): 5 and 7 chars, built exactly
       // (measured C3: "5,6" 257.7, "5,7" with keys seen >= 4 times 214.9 ms per step; after the
-      // selects became calls, "5,7" / "5,6,7" at >= 2 sightings 151.8 / 151.1; profiles/r03/sweep_levels.txt)
-      std::string spec = le ? le : (e.mef <= 1u ? "5" : P.beam ? "5,7" : "5,6");
+      // selects became calls, "5,7" / "5,6,7" at >= 2 sightings 151.8 / 151.1; profiles/r03/sweep_levels.txt;
+      // at the final round-3 kernels "5,6,7" 147.1-147.8 against "5,7" 149.0-149.7 over five runs each,
+      // profiles/r03ah, r03ai)
+      std::string spec = le ? le : (e.mef <= 1u ? "5" : P.beam ? "5,6,7" : "5,6");
       for (size_t a = 0; a < spec.size();) {
         const size_t b = spec.find(',', a);
         const uint32_t k = (uint32_t)std::strtoul(spec.substr(a, b == std::string::npos ? std::string::npos : b - a).c_str(), nullptr, 10);
