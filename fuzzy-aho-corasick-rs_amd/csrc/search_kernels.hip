@@ -2363,11 +2363,11 @@ __device__ __forceinline__ void rc_count_insert(const RcCountTarget& T, uint64_t
     }
   }
 }
-// Two levels are counted in one pass over the windows (levels 1 and 0; the two sampled levels):
-// their inserts go out together.
+// Up to three levels are counted in one pass over the windows (level 1; the sampled levels): their
+// inserts go out together and the window's text is read once.
 __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, RcCountTarget t0, RcCountTarget t1,
-                                                       uint32_t stride, uint32_t sat, uint32_t* seen, uint32_t seen_mask,
-                                                       uint32_t probes) {
+                                                       RcCountTarget t2, uint32_t stride, uint32_t sat, uint32_t* seen,
+                                                       uint32_t seen_mask, uint32_t probes) {
   const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
   unsigned err = 0;
   const uint64_t ns = (P.total_windows + stride - 1) / stride;
@@ -2378,8 +2378,8 @@ __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, RcCountTa
     const uint64_t start = S.w_begin + (vid - P.seg_prefix[kl]);
     if (window_skipped(P, S, start, err)) continue;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const RcCountTarget& T = t ? t1 : t0;
+    for (int t = 0; t < 3; ++t) {
+      const RcCountTarget& T = t == 0 ? t0 : t == 1 ? t1 : t2;
       if (!T.k) continue;
       RcChars ch;
       uint64_t k;
@@ -4540,7 +4540,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         L0.k = k0;
       }
       hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P, target(d_rck, d_rcv, d_rcslot, slots, k),
-                         RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u}, stride1, 1u, nullptr, 0u, cprobes);
+                         RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u}, RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u},
+                         stride1, 1u, nullptr, 0u, cprobes);
       HIP_TRY(hipGetLastError());
       unsigned int n_keys = 0;
       if (int nrc = number_entries(d_rck, d_rcv, d_rcslot, d_rcrep, slots, 1u, max_ent, n_keys)) return nrc;
@@ -4786,15 +4787,18 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (int lrc = launch_l1()) return lrc;
       for (size_t x = 0; x < kk.size(); ++x) {
         const uint32_t k2 = kk[x];
-        // levels are counted two per pass over the sampled windows (one each with the first-sighting
-        // bitmap, which is per level)
-        if (seen || x % 2 == 0) {
+        // levels are counted three per pass over the sampled windows (one each with the first-sighting
+        // bitmap, which is per level): with three levels in two passes the second pass ran after the
+        // first one's numbering and held the sampled builds back behind the level-1 build (C3, r03aj)
+        if (seen || x % 3 == 0) {
           if (seen) HIP_TRY(hipMemsetAsync(seen, 0, ((size_t)seen_mask + 1) / 8, stream));
-          const bool pair = !seen && x + 1 < kk.size();
-          const RcCountTarget t1 = pair ? target(d_xk[x + 1], d_xv[x + 1], d_xslot[x + 1], slots2, kk[x + 1])
-                                        : RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u};
+          const RcCountTarget none{nullptr, nullptr, nullptr, 0u, 0u};
+          const RcCountTarget t1 = (!seen && x + 1 < kk.size())
+                                       ? target(d_xk[x + 1], d_xv[x + 1], d_xslot[x + 1], slots2, kk[x + 1]) : none;
+          const RcCountTarget t2 = (!seen && x + 2 < kk.size())
+                                       ? target(d_xk[x + 2], d_xv[x + 2], d_xslot[x + 2], slots2, kk[x + 2]) : none;
           hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid2), dim3(256), 0, stream, P,
-                             target(d_xk[x], d_xv[x], d_xslot[x], slots2, k2), t1, stride2, thr_t, seen, seen_mask,
+                             target(d_xk[x], d_xv[x], d_xslot[x], slots2, k2), t1, t2, stride2, thr_t, seen, seen_mask,
                              cprobes);
           HIP_TRY(hipGetLastError());
         }
