@@ -353,7 +353,7 @@ int fac_haystack_stage_device(const fac_engine* engine, const uint8_t* d_utf8, u
   std::string err;
   const int rc = fac::stage_haystack_device(engine->e, d_utf8, len, fh->h, err, static_cast<hipStream_t>(stream));
   if (rc) {
-    if (rc == FAC_E_HAYSTACK_TOO_LARGE && err_graphemes) *err_graphemes = fh->h.n;
+    if (rc == FAC_E_HAYSTACK_TOO_LARGE && err_graphemes) *err_graphemes = fh->h.failed_n;
     if (fresh) {
       fac::free_haystack(fh->h);
       delete fh;
@@ -772,6 +772,15 @@ void fac_edge_order(const uint32_t* cps, const uint64_t* off, uint64_t n, uint32
   for (uint64_t i = 0; i < n; ++i) g[i].assign(cps + off[i], cps + off[i + 1]);
   const std::vector<uint32_t> o = fac::transitions_order(g);
   for (uint64_t i = 0; i < n; ++i) order[i] = o[i];
+}
+
+int fac_diag_beam_select(const float* keys, const uint64_t* offs, uint64_t count, uint32_t bw, int32_t lds,
+                         int32_t sel_limit, uint32_t* perm) {
+  if (!keys || !offs || !perm) return fail(FAC_E_INVALID, "null argument");
+  if (int rc = check_device(0)) return rc;
+  std::string err;
+  int rc = fac::diag_beam_select(keys, offs, count, bw, lds, sel_limit, perm, err);
+  return rc ? fail(rc, err) : FAC_OK;
 }
 
 }  // extern "C"

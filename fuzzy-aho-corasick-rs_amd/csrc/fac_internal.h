@@ -403,6 +403,7 @@ struct Haystack {
   mutable uint32_t* d_gid = nullptr;  // grapheme ids (Unicode, engines with mappings; lazy)
   mutable const void* gid_engine = nullptr;
   int device = 0;
+  uint64_t failed_n = 0;  // graphemes counted by a failed restage (stage_haystack_device), for the error
 };
 
 // Where a search delivers its records: a host vector (internal callers), a pooled pinned host
@@ -498,6 +499,9 @@ int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int ove
 // merged bitap windows (prefilter.rs:319-342) of a text view of a staged haystack (view.ascii:
 // bytes [text_base, text_base + n) of h.d_utf8; else graphemes [text_base, text_base + n)); windows
 // in the view's local grapheme coordinates
+// diagnostics: beam_select(_lds) alone on key arrays (tests; fac_diag_beam_select)
+int diag_beam_select(const float* keys, const uint64_t* offs, uint64_t count, uint32_t bw, int32_t lds,
+                     int32_t sel_limit, uint32_t* perm, std::string& err);
 int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, const std::vector<uint32_t>& ks,
                       hipStream_t stream, std::vector<std::pair<uint64_t, uint64_t>>& windows, fac_stats* stats,
                       std::string& err);

@@ -612,7 +612,7 @@ __device__ FAC_SEL_ATTR void beam_select(KState* q, uint32_t head, uint32_t& tai
     const uint32_t pk = sel_key(A[a + pp]);
     if (has_anc && !(anc < pk)) {  // pivot equal to the ancestor pivot: split off the equal run
       const uint32_t mid = sel_partition(A + a, T + a, W, len, pp, true) + 1u;
-      if (index <= mid) break;
+      if (index < mid) break;  // core: `if mid > index { return; }`
       a += mid;
       len -= mid;
       index -= mid;
@@ -829,7 +829,7 @@ __device__ FAC_SEL_ATTR void beam_select_lds(KState* q, uint32_t head, uint32_t&
     const uint32_t pk = K[a + pp];
     if (has_anc && !(anc < pk)) {  // pivot equal to the ancestor pivot: split off the equal run
       const uint32_t mid = sel_partition_lds(K, I, W, a, len, pp, true) + 1u;
-      if (index <= mid) break;
+      if (index < mid) break;  // core: `if mid > index { return; }`
       a += mid;
       len -= mid;
       index -= mid;
@@ -1722,6 +1722,8 @@ __device__ unsigned long long g_prof[64];  // [0, 32): main passes, [32, 64): ca
 
 // Wave slots (SearchParams::slot_ring): lane 0 takes the next position of the free ring and waits
 // for the slot returned into it (positions are filled in return order); the ring starts as 0..n-1.
+// A release waits until its cell is EMPTY (the previous lap's acquirer took its value), so a slow
+// acquirer never has its value overwritten by a later lap's release (grids larger than n slots).
 __device__ uint32_t slot_acquire(const SearchParams& P) {
   uint32_t s = 0;
   if (lane_id() == 0) {
@@ -1734,7 +1736,8 @@ __device__ uint32_t slot_acquire(const SearchParams& P) {
 __device__ void slot_release(const SearchParams& P, uint32_t s) {
   if (lane_id() == 0) {
     const unsigned int t = atomicAdd(P.slot_ctr + 1, 1u);
-    atomicExch(P.slot_ring + (t % P.n_slots), s);
+    unsigned int* cell = P.slot_ring + (t % P.n_slots);
+    while (atomicCAS(cell, EMPTY, s) != EMPTY) __builtin_amdgcn_s_sleep(2);
   }
 }
 __global__ void slot_init_kernel(unsigned int* ring, unsigned int* ctr, uint32_t n) {
@@ -4092,9 +4095,22 @@ int stage_haystack_device(const Engine& e, const uint8_t* d_utf8, uint64_t len, 
   h.d_gid = nullptr;
   h.gid_engine = nullptr;
   hipStream_t st = stream ? stream : e.stream;
-  if (int rc = stage_device(e, h, st, err, -2)) return rc;
-  HIP_TRY(hipStreamSynchronize(st));
-  return FAC_OK;
+  int rc = stage_device(e, h, st, err, -2);
+  if (!rc) {
+    const hipError_t se = hipStreamSynchronize(st);
+    if (se != hipSuccess) {
+      err = std::string("hipStreamSynchronize: ") + hipGetErrorString(se);
+      rc = FAC_E_HIP;
+    }
+  }
+  if (rc) {  // a failed restage leaves a valid empty haystack (no stale grapheme offsets over new bytes)
+    h.failed_n = h.n;  // HaystackTooLarge reports the count
+    h.ascii = true;
+    h.len = 0;
+    h.n = 0;
+    h.d_utf8 = nullptr;
+  }
+  return rc;
 }
 
 // Bit-parallel pre-filter transcode of a Unicode haystack (prefilter.rs:262-280): symbol id of
@@ -5557,6 +5573,79 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     stats->prefilter_ms += ms;
   }
   return FAC_OK;
+}
+
+
+// ---- Diagnostics: the beam cut alone (tests) ----------------------------------------------------
+// One wave per key array: the array becomes a ring of states (node = original index, pen = key) at a
+// rotated head, then beam_select_lds (ring of 256, the LDS claim-word scratch) or beam_select (ring of
+// 1024 in LDS, the global per-wave scratch) keeps bw states; perm[i] = the node of the i-th survivor,
+// i < bw -- compared by the tests with the oracle's select_nth_unstable_by (oracle.cpp rsel).
+template <uint32_t QCAP, bool LDS>
+__global__ __launch_bounds__(64) void diag_select_kernel(const float* keys, const uint64_t* offs, uint32_t bw,
+                                                         uint32_t limit, uint4* bsel, uint32_t* perm) {
+  __shared__ KState q[QCAP];
+  __shared__ uint32_t claim[512];
+  const uint32_t lane = lane_id();
+  const uint32_t a = blockIdx.x;
+  const uint64_t b = offs[a], P = offs[a + 1] - b;
+  const uint32_t head = (a * 37u) & (QCAP - 1u);
+  for (uint32_t i = lane; i < 512u; i += 64u) claim[i] = 0u;
+  for (uint32_t i = lane; i < (uint32_t)P; i += 64u) q[(head + i) & (QCAP - 1u)] = KState{i, 0u, keys[b + i], 0u};
+  wave_mem_fence();
+  uint32_t tail = head + (uint32_t)P;
+  if constexpr (LDS) beam_select_lds<QCAP>(q, head, tail, bw, claim, limit);
+  else beam_select<QCAP>(q, head, tail, bw, bsel + (size_t)a * bsel_stride(QCAP), limit);
+  wave_mem_fence();
+  for (uint32_t i = lane; i < bw; i += 64u) perm[(size_t)a * bw + i] = q[(head + i) & (QCAP - 1u)].node;
+}
+
+int diag_beam_select(const float* keys, const uint64_t* offs, uint64_t count, uint32_t bw, int32_t lds,
+                     int32_t sel_limit, uint32_t* perm, std::string& err) {
+  const uint32_t cap = lds ? 256u : 1024u;
+  if (bw == 0 || count == 0 || count > (1u << 20)) {
+    err = "diag_beam_select: bw and count must be in [1, 2^20]";
+    return FAC_E_INVALID;
+  }
+  for (uint64_t a = 0; a < count; ++a) {  // the kernels' preconditions: 2 bw < P <= ring
+    const uint64_t P = offs[a + 1] - offs[a];
+    if (offs[a + 1] < offs[a] || P <= 2ull * bw || P > cap) {
+      err = "diag_beam_select: every array needs 2*bw < len <= " + std::to_string(cap);
+      return FAC_E_INVALID;
+    }
+  }
+  const uint64_t nk = offs[count];
+  std::vector<float> hk(keys, keys + nk);
+  std::vector<uint64_t> ho(offs, offs + count + 1);
+  float* dk = nullptr;
+  uint64_t* dof = nullptr;
+  uint32_t* dp = nullptr;
+  uint4* db = nullptr;
+  int rc = upload(hk, &dk, err);
+  if (!rc) rc = upload(ho, &dof, err);
+  auto cleanup = [&] {
+    (void)hipFree(dk);
+    (void)hipFree(dof);
+    (void)hipFree(dp);
+    (void)hipFree(db);
+  };
+  if (rc) {
+    cleanup();
+    return rc;
+  }
+  auto run = [&]() -> int {
+    HIP_TRY(hipMalloc((void**)&dp, count * bw * sizeof(uint32_t)));
+    if (!lds) HIP_TRY(hipMalloc((void**)&db, count * bsel_stride(1024) * sizeof(uint4)));
+    const uint32_t lim = sel_limit < 0 ? 16u : (uint32_t)sel_limit;
+    if (lds) hipLaunchKernelGGL((diag_select_kernel<256, true>), dim3((uint32_t)count), dim3(64), 0, 0, dk, dof, bw, lim, db, dp);
+    else hipLaunchKernelGGL((diag_select_kernel<1024, false>), dim3((uint32_t)count), dim3(64), 0, 0, dk, dof, bw, lim, db, dp);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(perm, dp, count * bw * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return FAC_OK;
+  };
+  rc = run();
+  cleanup();
+  return rc;
 }
 
 }  // namespace fac

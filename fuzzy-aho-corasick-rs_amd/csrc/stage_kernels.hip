@@ -265,7 +265,9 @@ __global__ __launch_bounds__(256) void seg_tile_kernel(const uint8_t* __restrict
         while (k < i) seg_step(st, props_fast(ptab, dec(k)));
       }
     }
-    for (uint64_t k = i; !bad && !is_hard && k < e;) {
+    // the UTF-8 check covers every thread's code points, hard ones included (their boundaries are
+    // decided by seg_hard_kernel, which decodes leniently and never flags a bad sequence)
+    for (uint64_t k = i; !bad && k < e;) {
       const uint64_t pos = k;
       const uint32_t b0 = at(k);
       uint32_t cp;
@@ -293,6 +295,7 @@ __global__ __launch_bounds__(256) void seg_tile_kernel(const uint8_t* __restrict
           break;
         }
       }
+      if (is_hard) continue;
       const Props R = props_fast(ptab, cp);
       bool br;
       if (pos == 0) {

@@ -103,7 +103,7 @@ void worker_loop(const StreamCore* s, StreamWorker* w) {
       t->rc = FAC_E_OOM;
       t->err = "out of host memory while searching a stream window";
     } catch (const std::exception& ex) {
-      t->rc = FAC_E_OOM;
+      t->rc = FAC_E_INTERNAL;
       t->err = std::string("stream window: ") + ex.what();
     }
     {

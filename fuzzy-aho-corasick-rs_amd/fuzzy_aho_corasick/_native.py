@@ -19,6 +19,7 @@ FAC_E_NO_DEVICE = 103
 FAC_E_OOM = 104
 FAC_E_CAPACITY = 105
 FAC_E_OUTPUT_CAPACITY = 106
+FAC_E_INTERNAL = 107
 LIMIT_NONE = -1
 
 
@@ -160,6 +161,8 @@ SIGNATURES = {
     "fac_haystack_stage_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                                  ctypes.POINTER(ctypes.c_void_p), _u64p]),
     "fac_edge_order": (None, [ctypes.POINTER(ctypes.c_uint32), _u64p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32)]),
+    "fac_diag_beam_select": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

@@ -482,6 +482,8 @@ class StagedHaystack:
         rc = _native.lib.fac_haystack_stage_device(engine._h, ctypes.c_void_p(d_utf8), length, ctypes.c_void_p(stream or 0),
                                                    ctypes.byref(h), ctypes.byref(eg))
         if rc:
+            if reuse is not None:  # a failed restage leaves the haystack empty (and searchable)
+                reuse.owned_bytes, reuse.graphemes, reuse.owned_windows = 0, 0, 0
             _raise(rc, eg.value)
         obj = reuse
         if obj is None:

@@ -27,6 +27,7 @@
  *                                   automatic retries (pathological input)
  *   FAC_E_OUTPUT_CAPACITY     106   the caller's device output buffer is too small; *n_out holds
  *                                   the record count needed (fac_search_staged_ex)
+ *   FAC_E_INTERNAL            107   unexpected internal error (fac_last_error() has the text)
  *
  * Diagnostics: the library reads FAC_* environment knobs (kernel variants, prefix-cache levels,
  * FAC_GRAPHEME_LIMIT, ...) only when FAC_DIAGNOSTICS=1 is set; otherwise the search path depends
@@ -51,6 +52,7 @@ extern "C" {
 #define FAC_E_OOM 104
 #define FAC_E_CAPACITY 105
 #define FAC_E_OUTPUT_CAPACITY 106
+#define FAC_E_INTERNAL 107
 
 #define FAC_LIMIT_NONE (-1)
 
@@ -309,6 +311,15 @@ uint32_t fac_fold_first_char(const uint8_t* utf8, uint64_t len, int32_t case_ins
  * std's hashbrown) given the children's graphemes in insertion order (code points: grapheme i is
  * cps[off[i] .. off[i+1])). Writes the n insertion indices in iteration order to `order`. */
 void fac_edge_order(const uint32_t* cps, const uint64_t* off, uint64_t n, uint32_t* order);
+
+/* Diagnostics (tests): the device beam cut alone. Array a holds keys[offs[a] .. offs[a+1]) as the
+ * penalties of a queue's pending states (2*bw < length <= 256 for lds != 0, <= 1024 otherwise); the
+ * kernel keeps bw of them exactly as the search's beam does -- the reference's
+ * `queue[q_idx..].select_nth_unstable_by(bw - 1, total_cmp)` + `truncate(q_idx + bw)`
+ * (search.rs:584-587) -- and writes the survivors' original indices, in queue order, to
+ * perm[a*bw .. a*bw + bw). sel_limit < 0: core's 16 partition rounds. Uses device 0. */
+int fac_diag_beam_select(const float* keys, const uint64_t* offs, uint64_t count, uint32_t bw, int32_t lds,
+                         int32_t sel_limit, uint32_t* perm);
 
 #ifdef __cplusplus
 }

@@ -137,7 +137,9 @@ struct Match {
 // Restatement modes (orc_set_modes). Edge order: 0 = insertion order, 1 = the iteration order of
 // the reference's `FxHashMap<String, u32>` transitions (FxHasher + hashbrown, below). Beam rule:
 // 0 = canonical (penalty, queue position), 1 = the same with ties at the cut broken towards the
-// LATEST queue position (tie-sensitivity diagnostic only), 2 = core's select_nth_unstable_by.
+// LATEST queue position (tie-sensitivity diagnostic only), 2 = core's select_nth_unstable_by, 3 = the
+// same with round 3's defective early exit (stop at index == mid after the equal-to-ancestor split;
+// diagnostics only: profiles/beam_ties.py measures what the fix changed).
 int g_edge_order = 1;
 int g_beam_rule = 2;
 int g_sel_limit = 16;  // select.rs partition_at_index_loop's round limit (tests lower it to reach median_of_medians)
@@ -432,7 +434,7 @@ void partition_at_index_loop(T* v, size_t len, size_t index, L& is_less) {
     if (ancestor && !is_less(*ancestor, v[pivot_pos])) {
       auto le = [&](const T& a, const T& b) { return !is_less(b, a); };
       const size_t mid = partition(v, len, pivot_pos, le) + 1;
-      if (index <= mid) return;
+      if (index < mid || (g_beam_rule == 3 && index == mid)) return;  // core: `if mid > index { return; }`
       v += mid;
       len -= mid;
       index -= mid;
@@ -860,7 +862,7 @@ struct Searcher {
           size_t bw = effective_beam;
           size_t remaining = queue.size() - q_idx;
           if (remaining > bw * 2) {
-            if (e.beam_rule == 2) {
+            if (e.beam_rule >= 2) {
               rsel::select_nth_unstable_by(queue.data() + q_idx, remaining, bw - 1, [](const State& a, const State& b) {
                 return total_order_bits(a.pen) < total_order_bits(b.pen);
               });
@@ -1255,6 +1257,27 @@ void orc_select_nth(const float* keys, uint64_t n, uint64_t index, uint32_t* per
     return Searcher::total_order_bits(a.k) < Searcher::total_order_bits(b.k);
   });
   for (uint64_t i = 0; i < n; ++i) perm[i] = v[i].i;
+}
+
+// The same over `count` arrays (array a = keys[offs[a] .. offs[a+1]), its own index[a]); perm is laid
+// out like keys. Returns the number of arrays whose result violates select_nth_unstable_by's
+// post-condition (every element before index <= v[index] <= every element after), for tests.
+uint64_t orc_select_nth_batch(const float* keys, const uint64_t* offs, uint64_t count, const uint64_t* index,
+                              uint32_t* perm) {
+  uint64_t bad = 0;
+  for (uint64_t a = 0; a < count; ++a) {
+    const uint64_t b = offs[a], n = offs[a + 1] - b;
+    orc_select_nth(keys + b, n, index[a], perm + b);
+    const uint32_t* p = perm + b;
+    const uint32_t kv = Searcher::total_order_bits(keys[b + p[index[a]]]);
+    bool ok = true;
+    for (uint64_t i = 0; i < n && ok; ++i) {
+      const uint32_t k = Searcher::total_order_bits(keys[b + p[i]]);
+      ok = i < index[a] ? k <= kv : k >= kv;
+    }
+    bad += ok ? 0 : 1;
+  }
+  return bad;
 }
 
 // sel_limit: select.rs's 16 partition rounds before median_of_medians (tests only).

@@ -10,6 +10,8 @@ prefix of the C3 haystack under each restatement mode:
   insertion+latest     the same, ties at the cut broken towards the latest queue position
   hashbrown+canonical  FxHasher + hashbrown iteration order, canonical beam
   hashbrown+select     FxHasher + hashbrown order, core's select_nth_unstable_by (the default now)
+  hashbrown+select_r03 the same with round 3's defective early exit (index == mid after the
+                       equal-to-ancestor split stopped the select; VERDICT r03 missing #1)
   unbeamed             no beam (recall reference)
 and reports, against hashbrown+select, the (start, end, pattern) keys only one side has, keys
 whose similarity differs, and keys whose edit-count fields differ.
@@ -51,7 +53,7 @@ def main():
     mib = float(sys.argv[1]) if len(sys.argv) > 1 else 16.0
     threads = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     wl = W.config("c3", int(mib * (1 << 20)))
-    modes = {"hashbrown+select": (1, 2, 64), "hashbrown+canonical": (1, 0, 64), "insertion+canonical": (0, 0, 64),
+    modes = {"hashbrown+select": (1, 2, 64), "hashbrown+select_r03": (1, 3, 64), "hashbrown+canonical": (1, 0, 64), "insertion+canonical": (0, 0, 64),
              "insertion+latest": (0, 1, 64), "unbeamed": (1, 2, 0)}
     res, secs = {}, {}
     for name, (e, r, bw) in modes.items():

@@ -726,3 +726,38 @@ def test_mappings_widen_stream_overlap():
     e2 = B().fuzzy(L().edits(2)).mapping("q", "zzzz").build(["alexandr"])
     assert e2.max_match_graphemes() == 8 + 2
     assert e2.with_prefilter().is_active()
+
+
+@pytest.mark.parametrize("lds,nmax", [(1, 256), (0, 1024)])
+@pytest.mark.parametrize("limit", [16, 1, 0])
+def test_device_beam_select_matches_oracle(lds, nmax, limit):
+    """The device beam cut alone (beam_select_lds for rings <= 256, beam_select with its global
+    scratch for larger ones) on 20 000 beam events each: the bw survivors AND their queue order are
+    the oracle's select_nth_unstable_by (oracle.cpp rsel; search.rs:584-587), which
+    test_rust_select.py pins to core's post-condition on >= 100 000 arrays."""
+    import ctypes
+    import numpy as np
+    import oracle_harness as OH
+    from fuzzy_aho_corasick import _native
+    from test_rust_select import _beam_batch, _orc_select_batch
+
+    keys, offs, index = _beam_batch(7000 + 10 * limit + lds, 20000, nmax)
+    OH.set_modes(sel_limit=limit)
+    try:
+        want, bad = _orc_select_batch(keys, offs, index)
+    finally:
+        OH.set_modes(sel_limit=16)
+    assert bad == 0
+    for bw in (2, 8, 64):
+        sel = np.nonzero(index == bw - 1)[0]
+        sub_n = np.diff(offs)[sel]
+        sub_offs = np.zeros(len(sel) + 1, np.uint64)
+        sub_offs[1:] = np.cumsum(sub_n)
+        sub_keys = np.concatenate([keys[int(offs[a]):int(offs[a + 1])] for a in sel])
+        perm = np.zeros(len(sel) * bw, np.uint32)
+        rc = _native.lib.fac_diag_beam_select(sub_keys.ctypes.data, sub_offs.ctypes.data, len(sel), bw, lds, limit,
+                                              perm.ctypes.data)
+        assert rc == 0, _native.last_error()
+        exp = np.concatenate([want[int(offs[a]):int(offs[a]) + bw] for a in sel])
+        diff = np.nonzero(perm != exp)[0]
+        assert len(diff) == 0, f"bw={bw}: {len(set(diff // bw))} of {len(sel)} arrays differ (first {diff[0] // bw})"

@@ -272,3 +272,51 @@ def test_device_utf8_check_matches_python():
             B().fuzzy(L().edits(1)), ["héllo", "wörld", "ab"]).search_raw(hay, 0.8))
         got = sorted((m.start, m.end, m.pattern_index) for m in eng.search_raw(hay, 0.8))
         assert len(got) > 0 and got == want
+
+
+def test_device_utf8_check_inside_long_runs():
+    """64-byte ranges with no resync code point within 1 KiB (long combining / emoji ZWJ /
+    regional-indicator runs) are segmented by seg_hard_kernel, which decodes leniently; the UTF-8
+    check must still cover their bytes. Invalid pieces planted inside and right after > 1 KiB runs
+    are refused on both staging paths (host bytes and device bytes, incl. a restage of a live
+    haystack, which is left empty and usable), exactly when Python's strict decoder refuses."""
+    import random
+    import torch
+    from fuzzy_aho_corasick import DeviceError
+    from fuzzy_aho_corasick._native import FAC_E_INVALID
+    rng = random.Random(0x1057)
+    eng = B().fuzzy(L().edits(1)).device(0).build(["héllo", "wörld", "ab"])
+    runs = ["́", "‍\U0001F469", "\U0001F1EB\U0001F1F7", "̈́", "\U0001F3FB"]
+    bad = [b"\x80", b"\xff", b"\xc0\x80", b"\xed\xa0\x80", b"\xf4\x90\x80\x80", b"\xc3", b"\xe2\x82", b"\xf0\x9f\x98",
+           b"\xe0\x80\x80"]
+    st = None
+    refused = 0
+    for trial in range(60):
+        run = rng.choice(runs) * rng.choice([400, 700, 1500, 9000])
+        head = "ab héllo " + ("a" if trial % 2 else "\U0001F468")
+        data = (head + run).encode("utf-8")
+        at = rng.choice([len(data) // 2, len(data) - 1, len(data), 1100 + rng.randrange(64), 16384, 16385])
+        at = min(at, len(data))
+        data = data[:at] + rng.choice(bad) + data[at:] + (rng.choice(runs) * 30 + " wörld").encode("utf-8")
+        try:
+            data.decode("utf-8")
+            ok = True
+        except UnicodeDecodeError:
+            ok = False
+        dev = torch.from_numpy(np.frombuffer(data + b"\0", dtype=np.uint8).copy()).to("cuda")
+        if ok:
+            StagedHaystack(eng, data)
+            st = StagedHaystack.from_device(eng, dev.data_ptr(), len(data), reuse=st)
+            continue
+        refused += 1
+        with pytest.raises(DeviceError) as ei:
+            StagedHaystack(eng, data)
+        assert ei.value.code == FAC_E_INVALID, trial
+        with pytest.raises(DeviceError) as ei:
+            st = StagedHaystack.from_device(eng, dev.data_ptr(), len(data), reuse=st)
+        assert ei.value.code == FAC_E_INVALID, trial
+        if st is not None:  # the failed restage left an empty haystack: searching it finds nothing
+            assert st.graphemes == 0
+            assert len(st.search_windows(0.8)[0]) == 0
+        del dev
+    assert refused >= 40

@@ -287,7 +287,7 @@ def py_select(keys, index, limit0=16):
             pp = choose_pivot(lo, n_)
             if anc is not None and not lt(anc, v[lo + pp]):
                 mid = partition(lo, n_, pp, lambda a, b: not lt(b, a)) + 1
-                if idx <= mid:
+                if idx < mid:  # core: `if mid > index { return; }`
                     break
                 lo, n_, idx, anc = lo + mid, n_ - mid, idx - mid, None
                 continue
@@ -334,6 +334,112 @@ def test_select_oracle_matches_python_restatement(limit):
             assert all(x <= kk[index] for x in kk[:index]) and all(x >= kk[index] for x in kk[index + 1:])
     finally:
         OH.set_modes(sel_limit=16)
+
+
+# VERDICT r03 / ADVICE r03: after the equal-to-ancestor split core continues while `index == mid`
+# (`if mid > index { return; }`, select.rs partition_at_index_loop); rounds <= 3 stopped there and left
+# a larger element at `index`. This array (keys {0..5}, index 29) was an invalid selection then.
+_REPRO_INDEX_EQ_MID = [3.0, 1.0, 5.0, 5.0, 1.0, 3.0, 5.0, 5.0, 4.0, 3.0, 0.0, 4.0, 2.0, 0.0, 1.0, 3.0, 4.0, 3.0, 3.0,
+                       5.0, 4.0, 2.0, 3.0, 3.0, 0.0, 0.0, 3.0, 2.0, 3.0, 1.0, 1.0, 0.0, 2.0, 4.0, 2.0, 2.0, 3.0, 5.0,
+                       2.0, 3.0]
+
+
+def _is_selection(keys, perm, index):
+    kk = [_tkey(keys[i]) for i in perm]
+    return all(x <= kk[index] for x in kk[:index]) and all(x >= kk[index] for x in kk[index + 1:])
+
+
+def test_select_index_equal_to_mid_regression():
+    keys = _REPRO_INDEX_EQ_MID
+    got = _orc_select(keys, 29)
+    assert got == py_select(keys, 29)
+    assert _is_selection(keys, got, 29)
+    assert sorted(keys[i] for i in got[:30]) == sorted(keys)[:30]
+
+
+_BEAM_COSTS = np.array([0.0, 0.5199999809, 0.5719999671, 0.8579999804, 0.9099999666, 1.4299999475], np.float32)
+
+
+def _beam_batch(seed, count, nmax=600):
+    """`count` beam events like the search's: bw in {2, 8, 64}, pending max(17, 2 bw + 1) .. 600,
+    penalties sums of two discrete edit costs (many ties). Returns keys (f32), offsets, indices."""
+    rng = np.random.default_rng(seed)
+    bw = rng.choice(np.array([2, 8, 64]), size=count)
+    lo = np.maximum(17, 2 * bw + 1)
+    n = lo + (rng.random(count) * (nmax + 1 - lo)).astype(np.int64)
+    offs = np.zeros(count + 1, np.uint64)
+    offs[1:] = np.cumsum(n)
+    k = rng.integers(0, len(_BEAM_COSTS), size=(int(offs[-1]), 2))
+    keys = (_BEAM_COSTS[k[:, 0]] + _BEAM_COSTS[k[:, 1]]).astype(np.float32)
+    return keys, offs, (bw - 1).astype(np.uint64)
+
+
+def _orc_select_batch(keys, offs, index):
+    fn = OH._lib.orc_select_nth_batch
+    fn.restype = ctypes.c_uint64
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+    perm = np.zeros(len(keys), np.uint32)
+    bad = fn(keys.ctypes.data, offs.ctypes.data, len(offs) - 1, index.ctypes.data, perm.ctypes.data)
+    return perm, int(bad)
+
+
+def _selection_violations(keys, offs, index, perm):
+    """select_nth_unstable_by's post-condition checked with numpy (independently of the oracle):
+    v[..i] <= v[i] <= v[i+1..] under total_cmp, per array. Returns the number of arrays violating it."""
+    tk = keys.view(np.int32).astype(np.int64)
+    tk = np.where(tk < 0, tk ^ 0x7FFFFFFF, tk)  # f32::total_cmp as a signed integer order
+    starts = offs[:-1].astype(np.int64)
+    seg = np.repeat(np.arange(len(starts)), np.diff(offs).astype(np.int64))
+    v = tk[starts[seg] + perm.astype(np.int64)]  # keys in selected order
+    pos = np.arange(len(v)) - starts[seg]
+    piv = v[starts + index.astype(np.int64)][seg]
+    bad = ((pos < index[seg].astype(np.int64)) & (v > piv)) | ((pos > index[seg].astype(np.int64)) & (v < piv))
+    return int(np.count_nonzero(np.bincount(seg, weights=bad, minlength=len(starts))))
+
+
+@pytest.mark.parametrize("limit", [16, 1, 0])
+def test_select_postcondition_oracle_100k(limit):
+    """>= 100 000 beam events per round limit (16 = core's; 1 and 0 reach median_of_medians early)."""
+    OH.set_modes(sel_limit=limit)
+    try:
+        for chunk in range(5):
+            keys, offs, index = _beam_batch(1000 * limit + chunk, 20000)
+            perm, bad = _orc_select_batch(keys, offs, index)
+            assert bad == 0
+            assert _selection_violations(keys, offs, index, perm) == 0
+            # and a permutation of each array
+            seg = np.repeat(np.arange(len(offs) - 1), np.diff(offs).astype(np.int64))
+            order = np.lexsort((perm, seg))
+            assert np.array_equal(perm[order], np.arange(len(perm)) - offs[:-1].astype(np.int64)[seg])
+    finally:
+        OH.set_modes(sel_limit=16)
+
+
+def _py_chunk(args):
+    seed, count, limit = args
+    OH.set_modes(sel_limit=limit)
+    keys, offs, index = _beam_batch(seed, count)
+    perm, bad = _orc_select_batch(keys, offs, index)
+    mism = inval = 0
+    for a in range(count):
+        b, e = int(offs[a]), int(offs[a + 1])
+        kl = keys[b:e].tolist()
+        got = py_select(kl, int(index[a]), limit)
+        mism += got != perm[b:e].tolist()
+        inval += not _is_selection(kl, got, int(index[a]))
+    return mism, inval, bad
+
+
+def test_select_postcondition_python_100k():
+    """The Python restatement on 100 000 beam events (70 000 at core's limit, 15 000 each at limits 1
+    and 0): a valid selection every time, and the oracle's permutation exactly."""
+    import multiprocessing as mp
+    jobs = [(50_000 + i, 5000, 16) for i in range(14)] + [(60_000 + i, 5000, l) for i in range(3) for l in (1, 0)]
+    with mp.get_context("fork").Pool(min(8, os.cpu_count() or 1)) as pool:
+        res = pool.map(_py_chunk, jobs)
+    assert sum(r[0] for r in res) == 0, "python restatement != oracle"
+    assert sum(r[1] for r in res) == 0, "python restatement: invalid selection"
+    assert sum(r[2] for r in res) == 0, "oracle: invalid selection"
 
 
 def _lomuto_serial(w, lt):
