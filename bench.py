@@ -61,6 +61,11 @@ def parse():
     ap.add_argument("--vocab", type=int, default=50_000,
                     help="filler words drawn from a fixed vocabulary of this many random words; 0: fresh random words")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="single-thread CPU baseline sample budget")
+    ap.add_argument("--cpu-min-mib", type=float, default=None,
+                    help="single-thread CPU baseline: at least this many MiB of the haystack (default c3: 2)")
+    ap.add_argument("--no-fresh-diag", action="store_true",
+                    help="skip diagnostics.fresh_words (c2/c3 at N=1: the same config on SURVEY §8(d)'s fresh-word "
+                         "generator, timed beside the headline)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="all-cores CPU baseline threads (box share: 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None, help="default: profiles/traffic_<config>.json")
@@ -222,9 +227,14 @@ def main():
     achieved = bytes_step / (step_dev_ms / 1e3) / 1e9 if step_dev_ms > 0 else 0.0
     traffic, traffic_note = load_traffic(args, mib)
 
+    fresh = None
+    if (world == 1 and args.config in ("c2", "c3") and args.vocab and device_staging and not args.no_fresh_diag):
+        fresh = fresh_words_diag(args, engine, nbytes, local, stream)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
+        min_mib = args.cpu_min_mib if args.cpu_min_mib is not None else (2.0 if args.config == "c3" else 0.0)
+        cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads, int(min_mib * (1 << 20)))
 
     if rank == 0:
         wave_ms = acc["kernel_ms"] / K
@@ -289,11 +299,51 @@ def main():
                 "h2d_ms_once": h2d_ms,
                 "states_from_prefix_cache_per_step": acc["cached"] / K,
                 "sources_sha": sources_sha(),
+                "fresh_words": fresh,
             },
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def fresh_words_diag(args, engine, nbytes, local, stream, steps=2):
+    """The same engine and size on SURVEY.md §8(d)'s generator taken literally (every filler word
+    fresh, bench.py --vocab 0): device-resident bytes, the same timed step (device staging + search +
+    records D2H), `steps` steps after one warm-up. Reported beside the headline (VERDICT r03 #3)."""
+    import numpy as np
+    import torch
+    from fuzzy_aho_corasick import workloads as W
+    from fuzzy_aho_corasick.engine import StagedHaystack
+    base_seed = {"c2": 2, "c3": 3}[args.config]
+    wl = W.config(args.config, nbytes, seed=base_seed, hay_seed=base_seed + 1000, vocab=None)
+    dev = torch.from_numpy(np.frombuffer(wl.haystack, dtype=np.uint8).copy()).to(torch.device("cuda", local))
+    staged = StagedHaystack.from_device(engine, dev.data_ptr(), len(wl.haystack), stream)
+    n = 0
+
+    def step():
+        hs = StagedHaystack.from_device(engine, dev.data_ptr(), len(wl.haystack), stream, reuse=staged)
+        rows, st = hs.search_windows_records(wl.threshold, stream=stream)
+        return len(rows), st
+
+    step()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    cache = lane = kern = 0.0
+    for _ in range(steps):
+        n, st = step()
+        cache += st.cache_ms
+        lane += st.lane_ms
+        kern += st.kernel_ms
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / steps
+    out = {"value": staged.owned_windows / dt / 1e9, "unit": "Gchars/s", "ms_per_step": dt * 1e3, "steps": steps,
+           "matches_per_step": n, "haystack_bytes": len(wl.haystack), "graphemes": staged.owned_windows,
+           "prefix_cache_ms_per_step": cache / steps, "lane_kernel_ms_per_step": lane / steps,
+           "search_kernel_ms_per_step": kern / steps,
+           "data": "every filler word fresh (SURVEY.md §8(d) generator), same seeds otherwise"}
+    del staged, dev
+    return out
 
 
 def load_traffic(args, mib):
@@ -473,9 +523,9 @@ def run_dry(args, world, rank):
         dist.destroy_process_group()
 
 
-def cpu_baseline(wl, budget_s, threads):
+def cpu_baseline(wl, budget_s, threads, min_bytes=0):
     """The CPU restatement (oracle/, test infrastructure) timed on the host cores on bounded prefixes
-    of the same haystack: one thread on a prefix sized to ~budget_s, and `threads` threads
+    of the same haystack: one thread on a prefix sized to ~budget_s (and at least min_bytes), and `threads` threads
     (start-range sharding, like search_stream_parallel, stream.rs:378-429) on SURVEY §8(d)'s prefix
     (C2/C4/C5: 64 MiB, C3: 16 MiB; shortened if it would take more than ~20 s)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -499,9 +549,12 @@ def cpu_baseline(wl, budget_s, threads):
         pt.search(wl.threshold, prefilter=wl.prefilter)
         dt = time.perf_counter() - t
         rate = pt.n / dt
-        if dt * 4 > budget_s or size >= len(wl.haystack):
+        if (dt * 4 > budget_s and len(pt.data) >= min_bytes) or size >= len(wl.haystack):
             break
-        size = min(len(wl.haystack), int(size * min(8.0, max(2.0, budget_s / max(dt, 1e-3) / 2))))
+        grow = min(8.0, max(2.0, budget_s / max(dt, 1e-3) / 2))
+        if dt * 4 > budget_s:  # the budget is spent but the sample is below min_bytes: straight to it
+            grow = max(grow, min_bytes / max(1, len(pt.data)) * 1.01)
+        size = min(len(wl.haystack), int(size * grow))
     one = {"value": rate / 1e9, "unit": "Gchars/s", "cores": 1, "kind": "port",
            "sample": f"first {len(pt.data)} bytes ({pt.n} graphemes) of the same haystack, {dt:.1f} s, "
                      "oracle/ CPU restatement of the reference algorithm, single thread"}

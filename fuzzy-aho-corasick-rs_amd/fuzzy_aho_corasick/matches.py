@@ -1,7 +1,9 @@
 """FuzzyMatch / FuzzyMatches host-side post-processing (src/matches.rs, src/structs.rs:756-889).
 
-Ranking and overlap resolution run on the host over the (sparse) raw match set the GPU returns;
-they are not on the accelerated path.
+Ranking and overlap resolution (FuzzyMatches::apply, matches.rs:7-149) run on the device
+(rank_kernels.hip via the C ABI's fac_matches_apply) before any Python object is
+built; the host-side code here wraps the ranked records as FuzzyMatch objects and keeps a pure-Python
+apply only for record lists built by hand.
 """
 from __future__ import annotations
 

@@ -26,12 +26,12 @@ SLICE = 32 << 10
 N_SLICES = 32
 
 
-def _workload(name, mib):
+def _workload(name, mib, vocab=50_000):
     nbytes = mib << 20
     if name == "c4":  # bench.py: the C2 engine on the seed-40 haystack
-        return W.config("c4", nbytes, hay_seed=40)
+        return W.config("c4", nbytes, hay_seed=40, vocab=vocab)
     seed = {"c2": 2, "c3": 3}[name]
-    return W.config(name, nbytes, seed=seed, hay_seed=seed + 1000)
+    return W.config(name, nbytes, seed=seed, hay_seed=seed + 1000, vocab=vocab)
 
 
 def _after_space(data: bytes, p: int) -> int:
@@ -47,9 +47,12 @@ def _key(rows):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("name,mib", [("c3", 256), ("c4", 128), ("c2", 1024)])
-def test_benched_config_sampled_windows_match_oracle(name, mib):
-    wl = _workload(name, mib)
+@pytest.mark.parametrize("name,mib,vocab", [("c3", 256, 50_000), ("c4", 128, 50_000), ("c2", 1024, 50_000),
+                                            ("c3", 256, None), ("c2", 1024, None)],
+                         ids=["c3", "c4", "c2", "c3-fresh", "c2-fresh"])
+def test_benched_config_sampled_windows_match_oracle(name, mib, vocab):
+    """vocab None: every filler word fresh, SURVEY.md §8(d)'s generator literally (bench.py --vocab 0)."""
+    wl = _workload(name, mib, vocab)
     data = wl.haystack
     eng = W.builder_for(wl).device(0).build(wl.patterns)
     staged = StagedHaystack(eng, data)
@@ -60,7 +63,7 @@ def test_benched_config_sampled_windows_match_oracle(name, mib):
     recs, starts = recs[order], starts[order]
     halo = (eng.max_match_graphemes() + 2) * 4 + 64  # bytes: at most 4 per grapheme here
     orc = OracleEngine(W.builder_for(wl), wl.patterns)
-    rng = np.random.default_rng({"c2": 21, "c3": 31, "c4": 41}[name])
+    rng = np.random.default_rng({"c2": 21, "c3": 31, "c4": 41}[name] + (0 if vocab else 100))
     picks = sorted(int(x) for x in rng.integers(0, len(data) - 2 * SLICE, size=N_SLICES))
     cases = []
     for p in picks:
