@@ -372,7 +372,7 @@ def run_c5(args, world, rank, local):
     import torch.distributed as dist
     from fuzzy_aho_corasick import workloads as W
     from fuzzy_aho_corasick.engine import StagedHaystack
-    from fuzzy_aho_corasick.distributed import gather_device, records_to_tensor, stream_share_windows
+    from fuzzy_aho_corasick.distributed import gather_device, stream_share_windows
 
     block_bytes = int((args.mib if args.mib is not None else DEFAULT_MIB["c5"]) * (1 << 20))
     wl = W.config("c5", block_bytes, seed=5)
@@ -387,18 +387,26 @@ def run_c5(args, world, rank, local):
     processed_rank = sum(w[2] for w in windows)
     stream = torch.cuda.current_stream().cuda_stream
 
+    dev_recs = [torch.empty(1 << 20, dtype=torch.uint8, device=torch.device("cuda", local))] if world > 1 else None
+
     def step():
         parts, pf_ms, k_ms = [], 0.0, 0.0
+        if world > 1:  # owned records ranked and kept in HBM per window, then one RCCL gather from there
+            n = 0
+            for (g0, g1, commit, base) in windows:
+                dev_recs[0], got, st = staged.stream_window_device(g0, g1, commit, base, wl.threshold, True,
+                                                                   dev_recs[0], n, stream=stream)
+                n += got
+                pf_ms += st.prefilter_ms
+                k_ms += st.kernel_ms
+            gathered = gather_device(dev_recs[0], n, 0)
+            return (gathered.numel() // 32 if gathered is not None else 0), pf_ms, k_ms
         for (g0, g1, commit, base) in windows:
             recs, st = staged.stream_window(g0, g1, commit, base, wl.threshold, True, stream=stream)
             parts.append(recs)
             pf_ms += st.prefilter_ms
             k_ms += st.kernel_ms
         recs = np.concatenate(parts)
-        if world > 1:  # the window records (host, after the per-window ranking) to HBM, then RCCL
-            dev = records_to_tensor(recs).to(torch.device("cuda", local), non_blocking=False)
-            gathered = gather_device(dev, len(recs), 0)
-            return (gathered.numel() // 32 if gathered is not None else 0), pf_ms, k_ms
         return len(recs), pf_ms, k_ms
 
     for _ in range(args.warmup):

@@ -531,6 +531,23 @@ int fac_search_raw(const fac_engine* engine, const uint8_t* utf8, uint64_t len, 
 
 namespace {
 
+// scratch device memory of one call
+struct DevMem {
+  void* p = nullptr;
+  ~DevMem() {
+    if (p) (void)hipFree(p);
+  }
+  int alloc(size_t bytes, std::string& err) {
+    const hipError_t he = hipMalloc(&p, std::max<size_t>(bytes, 16));
+    if (he != hipSuccess) {
+      p = nullptr;
+      err = std::string("hipMalloc: ") + hipGetErrorString(he);
+      return FAC_E_OOM;
+    }
+    return FAC_OK;
+  }
+};
+
 // The staged bytes [bs, be) = graphemes [g0, g1) searched as a text of their own (search_raw on a
 // slice: is_ascii is re-decided on the slice, search.rs:196, prefilter.rs:349-350). A Unicode
 // haystack's host copies must be fetched first (ensure_host).
@@ -679,6 +696,72 @@ int fac_stream_window_staged(const fac_engine* engine, const fac_haystack* hay, 
     }
   }
   return copy_out(owned, out, n_out);
+}
+
+int fac_stream_window_staged_device(const fac_engine* engine, const fac_haystack* hay, uint64_t g_begin, uint64_t g_end,
+                                    uint64_t commit_bytes, uint64_t base, float threshold, int32_t prefilter, void* stream,
+                                    void* device_out, uint64_t device_cap, uint64_t* n_out, fac_stats* stats) {
+  if (!engine || !hay || !n_out || (!device_out && device_cap)) return fail(FAC_E_INVALID, "NULL argument");
+  *n_out = 0;
+  const fac::Haystack& h = hay->h;
+  if (h.open_end || h.base) return fail(FAC_E_INVALID, "stream windows are cut from a whole staged haystack");
+  g_end = std::min(g_end, h.n);
+  g_begin = std::min(g_begin, g_end);
+  std::string err;
+  if (!h.ascii)
+    if (int hrc = fac::ensure_host(h, err)) return fail(hrc, err);
+  const fac::SegDesc view = slice_view(h, g_begin, g_end);
+  const fac::Engine& e = engine->e;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (hipSetDevice(e.device) != hipSuccess) return fail(FAC_E_HIP, "hipSetDevice failed");
+  // the window's searched segments: Prefiltered::raw's merged bitap windows (disjoint and not
+  // adjacent, so their records never share a (start, end, pattern) key and the reference's
+  // best-per-key merge is a no-op before the ranking), or the whole view where it falls back
+  std::vector<fac::SegDesc> segs;
+  std::vector<uint32_t> ks;
+  if (prefilter && e.bitap_ok && prefilter_ks(e, threshold, ks)) {
+    std::vector<std::pair<uint64_t, uint64_t>> windows;
+    if (int rc = fac::prefilter_windows(e, h, view, ks, st, windows, stats, err)) return fail(rc, err);
+    for (auto& w : windows) {
+      const uint64_t gs = w.first, ge = std::min<uint64_t>(w.second, view.n);
+      if (view.ascii) {
+        fac::SegDesc s{};
+        s.ascii = 1u;
+        s.text_base = view.text_base + gs;
+        s.n = ge - gs;
+        s.avail = s.n;
+        s.hay_len = s.n;
+        s.byte_base = view.text_base + gs;
+        s.w_begin = 0;
+        s.w_end = s.n;
+        segs.push_back(s);
+      } else {
+        segs.push_back(slice_view(h, view.text_base + gs, view.text_base + ge));
+      }
+    }
+  } else {
+    segs.push_back(view);
+  }
+  if (segs.empty()) return FAC_OK;
+  // raw records into a device buffer (grown and searched again if a window ever needs more)
+  uint64_t cap = 1u << 16;
+  for (;;) {
+    DevMem raw;
+    if (int rc = raw.alloc(2 * cap * sizeof(fac_match), err)) return fail(rc, err);
+    fac::MatchSink sink;
+    sink.dev = static_cast<fac_match*>(raw.p);
+    sink.dev_cap = cap;
+    if (int rc = fac::launch_search_sink(e, h, segs, threshold, st, 0, sink, stats, err)) return fail(rc, err);
+    if (sink.n > cap) {
+      cap = sink.n;
+      continue;
+    }
+    const int rc = fac::window_owned_device(e, sink.dev, sink.dev + cap, sink.n, view.byte_base, commit_bytes, base, st,
+                                            static_cast<fac_match*>(device_out), device_cap, n_out, err);
+    if (rc == FAC_E_OUTPUT_CAPACITY) return fail(rc, "device output buffer too small (*n_out = records needed)");
+    if (rc) return fail(rc, err);
+    return FAC_OK;
+  }
 }
 
 int fac_matches_apply(const fac_engine* engine, fac_match* matches, uint64_t n, int32_t order, int32_t overlap,

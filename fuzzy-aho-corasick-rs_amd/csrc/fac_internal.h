@@ -496,6 +496,12 @@ int stage_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err,
 void ensure_symbols(const Engine& e, const Haystack& h);
 int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,
                   std::string& err);
+// stream.rs window_matches' tail on the device (rank_kernels.hip): the n raw records of one window
+// at d_a (d_b: scratch of n) ranked sorted().non_overlapping(), those starting before `commit` bytes
+// into the window (which starts at byte byte_base of the staged text) rebased to stream offset `base`
+// and written to d_out; *n_owned their count (FAC_E_OUTPUT_CAPACITY if it exceeds cap)
+int window_owned_device(const Engine& e, fac_match* d_a, fac_match* d_b, uint64_t n, uint64_t byte_base, uint64_t commit,
+                        uint64_t base, hipStream_t s, fac_match* d_out, uint64_t cap, uint64_t* n_owned, std::string& err);
 // merged bitap windows (prefilter.rs:319-342) of a text view of a staged haystack (view.ascii:
 // bytes [text_base, text_base + n) of h.d_utf8; else graphemes [text_base, text_base + n)); windows
 // in the view's local grapheme coordinates

@@ -220,29 +220,37 @@ void walk_host(std::vector<fac_match>& v, const uint64_t* unique_ids, bool uniqu
 
 }  // namespace
 
-int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,
-                  std::string& err) {
-  const uint64_t n = v.size();
+// Device-resident core: the n records at d_a (device) are ranked / resolved; d_b is scratch of n
+// records. *res points at the result (d_a or d_b), *n_res its count. The host walks (unique overlap,
+// clusters above kMaxCluster) bring the ranked list to the host and put their result back into d_a.
+int apply_matches_device(const Engine& e, fac_match* d_a, fac_match* d_b, uint64_t n, int order, int overlap,
+                         const uint64_t* unique_ids, hipStream_t s, fac_match** res, uint64_t* n_res, std::string& err) {
+  *res = d_a;
+  *n_res = n;
   if (n == 0 || (order == 0 && overlap == 0)) return FAC_OK;
-  RK_TRY(hipSetDevice(e.device));
-  hipStream_t s = e.stream;
   const uint32_t T = 256;
   const uint32_t G = (uint32_t)((n + T - 1) / T);
-  Buf d_a, d_b;
-  RK_TRY(d_a.alloc(n * sizeof(fac_match)));
-  RK_TRY(d_b.alloc(n * sizeof(fac_match)));
-  RK_TRY(hipMemcpyAsync(d_a.p, v.data(), n * sizeof(fac_match), hipMemcpyHostToDevice, s));
-  fac_match* ranked = d_a.as<fac_match>();
+  fac_match* ranked = d_a;
   if (order != 0) {
-    RK_TRY(dev_sort(d_a.as<fac_match>(), d_b.as<fac_match>(), n, RankCmp{e.d_pat_bytes, order}, s));
-    ranked = d_b.as<fac_match>();
+    RK_TRY(dev_sort(d_a, d_b, n, RankCmp{e.d_pat_bytes, order}, s));
+    ranked = d_b;
   }
-  if (overlap == 0 || overlap == 2) {  // keep, or the unique walk on the host
+  auto host_walk = [&](bool unique) -> int {
+    std::vector<fac_match> v(n);
     RK_TRY(hipMemcpyAsync(v.data(), ranked, n * sizeof(fac_match), hipMemcpyDeviceToHost, s));
     RK_TRY(hipStreamSynchronize(s));
-    if (overlap == 2) walk_host(v, unique_ids, true);
+    walk_host(v, unique_ids, unique);
+    if (!v.empty()) RK_TRY(hipMemcpyAsync(d_a, v.data(), v.size() * sizeof(fac_match), hipMemcpyHostToDevice, s));
+    RK_TRY(hipStreamSynchronize(s));
+    *res = d_a;
+    *n_res = v.size();
+    return FAC_OK;
+  };
+  if (overlap == 0) {
+    *res = ranked;
     return FAC_OK;
   }
+  if (overlap == 2) return host_walk(true);  // the unique walk on the host
   // ---- non_overlapping: clusters in start order, resolved one thread per cluster
   Buf d_sp, d_sp2, d_ends, d_maxe, d_flag, d_cid, d_head, d_lo, d_hi, d_keep, d_pos, d_kept;
   RK_TRY(d_sp.alloc(n * sizeof(Span)));
@@ -288,12 +296,7 @@ int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int ove
     RK_TRY(hipStreamSynchronize(s));
     uint64_t biggest = 0;
     for (uint64_t c = 0; c < n_clusters; ++c) biggest = std::max(biggest, (c + 1 < n_clusters ? heads[c + 1] : n) - heads[c]);
-    if (biggest > kMaxCluster) {
-      RK_TRY(hipMemcpyAsync(v.data(), ranked, n * sizeof(fac_match), hipMemcpyDeviceToHost, s));
-      RK_TRY(hipStreamSynchronize(s));
-      walk_host(v, nullptr, false);
-      return FAC_OK;
-    }
+    if (biggest > kMaxCluster) return host_walk(false);
   }
   RK_TRY(d_lo.alloc(n * sizeof(uint2)));
   RK_TRY(d_hi.alloc(n * sizeof(uint2)));
@@ -315,20 +318,83 @@ int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int ove
   uint32_t kept = 0;
   RK_TRY(hipMemcpyAsync(&kept, d_pos.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
   RK_TRY(hipStreamSynchronize(s));
-  if (kept == 0) {
-    v.clear();
-    return FAC_OK;
-  }
+  *n_res = kept;
+  if (kept == 0) return FAC_OK;
   RK_TRY(d_kept.alloc((uint64_t)kept * sizeof(Span)));
   hipLaunchKernelGGL(kept_spans_kernel, dim3(G), dim3(T), 0, s, ranked, d_keep.as<uint8_t>(), d_pos.as<uint32_t>(), n,
                      d_kept.as<Span>());
   RK_TRY(dev_sort(d_kept.as<Span>(), d_sp2.as<Span>(), kept, KeptByStart{}, s));
-  fac_match* out = (ranked == d_a.as<fac_match>()) ? d_b.as<fac_match>() : d_a.as<fac_match>();
+  fac_match* out = (ranked == d_a) ? d_b : d_a;
   hipLaunchKernelGGL(gather_kernel, dim3((kept + T - 1) / T), dim3(T), 0, s, ranked, d_sp2.as<Span>(), (uint64_t)kept,
                      out);
   RK_TRY(hipGetLastError());
-  v.resize(kept);
-  RK_TRY(hipMemcpyAsync(v.data(), out, (uint64_t)kept * sizeof(fac_match), hipMemcpyDeviceToHost, s));
+  *res = out;
+  return FAC_OK;
+}
+
+int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,
+                  std::string& err) {
+  const uint64_t n = v.size();
+  if (n == 0 || (order == 0 && overlap == 0)) return FAC_OK;
+  RK_TRY(hipSetDevice(e.device));
+  hipStream_t s = e.stream;
+  Buf d_a, d_b;
+  RK_TRY(d_a.alloc(n * sizeof(fac_match)));
+  RK_TRY(d_b.alloc(n * sizeof(fac_match)));
+  RK_TRY(hipMemcpyAsync(d_a.p, v.data(), n * sizeof(fac_match), hipMemcpyHostToDevice, s));
+  fac_match* res = nullptr;
+  uint64_t nres = 0;
+  if (int rc = apply_matches_device(e, d_a.as<fac_match>(), d_b.as<fac_match>(), n, order, overlap, unique_ids, s, &res,
+                                    &nres, err))
+    return rc;
+  v.resize(nres);
+  if (nres) RK_TRY(hipMemcpyAsync(v.data(), res, nres * sizeof(fac_match), hipMemcpyDeviceToHost, s));
+  RK_TRY(hipStreamSynchronize(s));
+  return FAC_OK;
+}
+
+// stream.rs window_matches' ownership on the device: of a window's records ranked sorted().
+// non_overlapping() (start order), the ones starting before the commit point (a prefix), rebased
+// from the window's bytes to the stream offset `base`, go to out[0 .. owned).
+__global__ void owned_kernel(const fac_match* in, uint64_t n, uint64_t byte_base, uint64_t commit, uint64_t base,
+                             fac_match* out, unsigned long long* owned) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fac_match m = in[i];
+  const uint64_t st = m.start - byte_base;
+  const bool own = st < commit;
+  if (own) {
+    m.start = st + base;
+    m.end = m.end - byte_base + base;
+    out[i] = m;
+  }
+  const uint64_t b = __ballot(own);
+  if (b && (threadIdx.x & 63u) == (uint32_t)(__ffsll((unsigned long long)b) - 1)) atomicAdd(owned, (unsigned long long)__popcll(b));
+}
+
+int window_owned_device(const Engine& e, fac_match* d_a, fac_match* d_b, uint64_t n, uint64_t byte_base, uint64_t commit,
+                        uint64_t base, hipStream_t s, fac_match* d_out, uint64_t cap, uint64_t* n_owned, std::string& err) {
+  *n_owned = 0;
+  if (n == 0) return FAC_OK;
+  fac_match* res = nullptr;
+  uint64_t nres = 0;
+  if (int rc = apply_matches_device(e, d_a, d_b, n, 1, 1, nullptr, s, &res, &nres, err)) return rc;
+  if (nres == 0) return FAC_OK;
+  // the owned count first (a prefix of the start-ordered list), then the copy if it fits
+  Buf d_cnt, d_tmp;
+  RK_TRY(d_cnt.alloc(8));
+  RK_TRY(d_tmp.alloc(nres * sizeof(fac_match)));
+  RK_TRY(hipMemsetAsync(d_cnt.p, 0, 8, s));
+  const uint32_t T = 256;
+  hipLaunchKernelGGL(owned_kernel, dim3((uint32_t)((nres + T - 1) / T)), dim3(T), 0, s, res, nres, byte_base, commit, base,
+                     d_tmp.as<fac_match>(), d_cnt.as<unsigned long long>());
+  RK_TRY(hipGetLastError());
+  unsigned long long owned = 0;
+  RK_TRY(hipMemcpyAsync(&owned, d_cnt.p, 8, hipMemcpyDeviceToHost, s));
+  RK_TRY(hipStreamSynchronize(s));
+  *n_owned = owned;
+  if (owned > cap) return FAC_E_OUTPUT_CAPACITY;
+  if (owned) RK_TRY(hipMemcpyAsync(d_out, d_tmp.p, owned * sizeof(fac_match), hipMemcpyDeviceToDevice, s));
   RK_TRY(hipStreamSynchronize(s));
   return FAC_OK;
 }

@@ -550,6 +550,31 @@ class StagedHaystack:
             _raise(rc)
         return _native.take_records(out, n.value), st
 
+    def stream_window_device(self, g_begin: int, g_end: int, commit_bytes: int, base: int, threshold: float,
+                             prefilter: bool, out, offset: int = 0, stream=None):
+        """fac_stream_window_staged_device: the window's owned records (stream.rs:262-297) written in HBM
+        to `out` (a uint8 CUDA tensor of 32-byte records) from record `offset` on, never visiting the
+        host; `out` is grown (a new tensor, the records before `offset` copied) when it is too small.
+        Returns (out, owned count, fac_stats)."""
+        import torch
+        n = ctypes.c_uint64()
+        st = _native.fac_stats()
+        while True:
+            cap = out.numel() // _native.REC_BYTES - offset
+            ptr = out.data_ptr() + offset * _native.REC_BYTES
+            rc = _native.lib.fac_stream_window_staged_device(
+                self.engine._h, self._h, g_begin, g_end, commit_bytes, base, f32(threshold), int(prefilter),
+                ctypes.c_void_p(stream or 0), ctypes.c_void_p(ptr), max(0, cap), ctypes.byref(n), ctypes.byref(st))
+            if rc == _native.FAC_E_OUTPUT_CAPACITY:
+                grown = torch.empty(max(2 * out.numel(), (offset + n.value) * _native.REC_BYTES * 2),
+                                    dtype=torch.uint8, device=out.device)
+                grown[: offset * _native.REC_BYTES].copy_(out[: offset * _native.REC_BYTES])
+                out = grown
+                continue
+            if rc:
+                _raise(rc)
+            return out, n.value, st
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h and _native.lib is not None:

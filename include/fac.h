@@ -256,6 +256,15 @@ int fac_stream_window_staged(const fac_engine* engine, const fac_haystack* hay, 
                              uint64_t commit_bytes, uint64_t base, float threshold, int32_t prefilter, void* stream,
                              fac_match** out, uint64_t* n_out, fac_stats* stats);
 
+/* fac_stream_window_staged with the owned records left in HBM (no host round trip): the window's
+ * raw records are ranked sorted().non_overlapping() on the device and the owned ones (start before
+ * the commit point) written, rebased to the stream offset `base`, to device_out (room for device_cap
+ * records). *n_out = the owned count; FAC_E_OUTPUT_CAPACITY when it exceeds device_cap (nothing is
+ * written then; grow the buffer and call again). For the multi-GPU gather of C5 (stream.rs:378-429). */
+int fac_stream_window_staged_device(const fac_engine* engine, const fac_haystack* hay, uint64_t g_begin, uint64_t g_end,
+                                    uint64_t commit_bytes, uint64_t base, float threshold, int32_t prefilter, void* stream,
+                                    void* device_out, uint64_t device_cap, uint64_t* n_out, fac_stats* stats);
+
 /* Prefiltered::raw on a staged haystack (prefilter.rs:146-155, 304-374): the bitap scan and the
  * window merge run on the device-resident text, each merged window is re-searched as its own
  * sub-haystack, results are best-per-(start, end, pattern) and sorted. Falls back to the full

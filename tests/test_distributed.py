@@ -239,13 +239,14 @@ def test_bench_rejects_mismatched_world():
     assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)
 
 
-def _c5_worker(rank, world, port, blocks, out_path):
+def _c5_worker(rank, world, port, blocks, out_path, device_style=False):
     sys.path[:0] = [os.path.join(REPO, "fuzzy-aho-corasick-rs_amd"), os.path.join(REPO, "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import numpy as np
     import torch.distributed as dist
     from fuzzy_aho_corasick import workloads as W
     from fuzzy_aho_corasick.distributed import gather_rows, stream_share_windows
+    from fuzzy_aho_corasick._native import MATCH_DTYPE
     from fuzzy_aho_corasick.structs import Order, Overlap
     from oracle_harness import OracleEngine
 
@@ -266,7 +267,25 @@ def _c5_worker(rank, world, port, blocks, out_path):
         text = buf[g0:g1]  # stream.rs window_matches: search(sorted, non_overlapping), starts < commit
         ranked = orc.apply_rows(orc.raw_rows(text, wl.threshold, prefilter=True), Order.Default, Overlap.NonOverlapping)
         rows += [(s + base, e + base) + tuple(r) for (s, e, *r) in ranked if s < commit]
-    got = gather_rows(rows)
+    if device_style:  # bench.py's N > 1 path: window records appended to one buffer, gathered from it
+        import torch
+        from fuzzy_aho_corasick.distributed import gather_device
+        recs = np.zeros(len(rows), dtype=MATCH_DTYPE)
+        for name, col in zip(MATCH_DTYPE.names[:9], zip(*rows) if rows else [[]] * 9):
+            recs[name] = col
+        buf = torch.empty(32, dtype=torch.uint8)  # grown like stream_window_device grows its HBM buffer
+        for i in range(len(recs)):
+            if (i + 1) * 32 > buf.numel():
+                g = torch.empty(2 * buf.numel(), dtype=torch.uint8)
+                g[: i * 32].copy_(buf[: i * 32])
+                buf = g
+            buf[i * 32: (i + 1) * 32].copy_(torch.from_numpy(recs[i: i + 1].view(np.uint8).copy()))
+        t = gather_device(buf, len(recs), 0)
+        got = None if t is None else [(int(r["start"]), int(r["end"]), int(r["pattern_index"]), float(r["similarity"]),
+                                       int(r["insertions"]), int(r["deletions"]), int(r["substitutions"]),
+                                       int(r["swaps"]), int(r["edits"])) for r in t.numpy().view(MATCH_DTYPE)]
+    else:
+        got = gather_rows(rows)
     if rank == 0:
         stream = block * blocks
         full = orc.apply_rows(orc.raw_rows(stream, wl.threshold, prefilter=True), Order.Default, Overlap.NonOverlapping)
@@ -276,8 +295,8 @@ def _c5_worker(rank, world, port, blocks, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_c5_stream_shares_equal_whole_stream_cpu(world):
+@pytest.mark.parametrize("world,device_style", [(2, False), (4, False), (2, True)])
+def test_c5_stream_shares_equal_whole_stream_cpu(world, device_style):
     """bench.py --config c5's cut (stream_share_windows: one contiguous share per rank, windows at
     block and share edges with max_match_graphemes() + 1 of overlap, each searched like stream.rs
     window_matches with the pre-filter and owning the matches that start in it), the oracle as each
@@ -285,7 +304,7 @@ def test_c5_stream_shares_equal_whole_stream_cpu(world):
     (tests.rs:1058-1142: streaming equals whole input for needles spaced past the overlap)."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res.txt")
-        mp.spawn(_c5_worker, args=(world, _free_port(), 5, out), nprocs=world, join=True)
+        mp.spawn(_c5_worker, args=(world, _free_port(), 5, out, device_style), nprocs=world, join=True)
         got, full = eval(open(out).read())
     assert len(full) >= 30
     assert got == full

@@ -114,14 +114,27 @@ def test_stream_windows_on_device_equal_whole_input(prefilter):
     assert len(want) > 50
     overlap = eng.max_match_graphemes() + 1
     st = StagedHaystack(eng, hay)
+    import torch
+    from fuzzy_aho_corasick._native import MATCH_DTYPE
     for win in (64 << 10, 200 << 10):
         got = []
+        # and fac_stream_window_staged_device (bench.py --config c5 at N > 1): every window's owned
+        # records appended in HBM to one buffer, started tiny so it must grow, gathered from there
+        dev = torch.empty(64, dtype=torch.uint8, device="cuda")
+        n = 0
         for c in range(0, len(hay), win):
             c1 = min(len(hay), c + win)
             recs, _ = st.stream_window(c, min(len(hay), c1 + overlap), c1 - c, c, 0.85, prefilter)
             got += [(int(r["start"]), int(r["end"]), int(r["pattern_index"]),
                      int(np.float32(r["similarity"]).view(np.uint32))) for r in recs]
+            dev, k, _ = st.stream_window_device(c, min(len(hay), c1 + overlap), c1 - c, c, 0.85, prefilter, dev, n)
+            assert k == len(recs)
+            n += k
         assert sorted(got) == want, win
+        drecs = dev[: n * 32].cpu().numpy().view(MATCH_DTYPE)
+        assert [tuple(r) for r in drecs] == [tuple(r) for r in np.concatenate(
+            [st.stream_window(c, min(len(hay), min(len(hay), c + win) + overlap), min(len(hay), c + win) - c, c, 0.85,
+                              prefilter)[0] for c in range(0, len(hay), win)])], win
 
 
 def test_haystack_too_large_is_reported(monkeypatch):
