@@ -251,6 +251,7 @@ struct SearchParams {
   int32_t rc_mode;                  // 0 off, 1 use the cache, 2 build it (win_list = representatives)
   uint32_t rc_k;                    // key chars of the level being collected / built (2..8)
   uint32_t rc_ntab;                 // tables a lookup consults (0..kRcLevels), deepest first
+  uint32_t rc_kstart;               // rc_lookup's first probe: the shallowest level with k >= this (0: deepest)
   RcTable rc_tab[kRcLevels];
   uint32_t rc_vmax, rc_emax;        // dedup / best-list entries a snapshot may hold
   uint4* rc_pool;                   // snapshots: header x4, queue, dedup entries, best list

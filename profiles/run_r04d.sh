@@ -4,8 +4,8 @@
 set -eo pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"
-BENCH_ARGS="--vocab 0 --no-fresh-diag" bash profiles/ab_knobs.sh r04d "X=0" "FAC_RC_K2=0" "FAC_RC_LEVELS=6" "FAC_RC_LEVELS=6,7"
-BENCH_ARGS="--no-fresh-diag" bash profiles/ab_knobs.sh r04d_v "FAC_RC_K2=0" "FAC_RC_LEVELS=6,7" "FAC_RC_LEVELS=5,7"
+BENCH_ARGS="--vocab 0 --no-fresh-diag" bash profiles/ab_knobs.sh r04d "X=0" "FAC_RC_K2=0" "FAC_RC_LEVELS=6" "FAC_RC_T2=4"
+BENCH_ARGS="--no-fresh-diag" bash profiles/ab_knobs.sh r04d_v "X=0" "FAC_RC_DEEPEST=1" "FAC_RC_K2=0" "FAC_RC_LEVELS=6,7" "FAC_RC_T2=3" "FAC_RC_T2=4" "FAC_RC_T2=3 FAC_RC_STRIDE2=1"
 OUT=$ROOT/gpurun_out/r04d
 L=fuzzy-aho-corasick-rs_amd/fuzzy_aho_corasick/_lib
 for v in 50000 0; do
