@@ -2716,27 +2716,15 @@ __device__ __forceinline__ bool live_dup(const SearchParams& P, const LiveDedup&
   return hit;
 }
 
-template <uint32_t QL, uint32_t ELN>
-__device__ __forceinline__ void lane_step(const SearchParams& P, uint32_t* s_q, uint4* s_e, const SegDesc& S, uint64_t start,
-                                          const LiveDedup& lv, uint32_t& status, uint32_t& head, uint32_t& tail,
-                                          uint32_t& nel, uint32_t& pops, unsigned& err) {
+// The body of one lane-serial pop after its dedup decision (search.rs:629-1089): node ceiling,
+// emission into the lane's best list, expansion pushed at the tail. LINEAR: the lane's states are
+// a linear array (the cache build keeps its popped states for the dedup scans), else a ring.
+template <uint32_t QL, uint32_t ELN, bool LINEAR>
+__device__ __forceinline__ void lane_expand(const SearchParams& P, uint32_t* s_q, uint4* s_e, const SegDesc& S,
+                                            uint64_t start, const KState& st, uint32_t& status, uint32_t& head,
+                                            uint32_t& tail, uint32_t& nel, unsigned& err) {
   const uint32_t lane = lane_id();
   const bool fast = P.mef != 255u;
-  if (head == tail) {
-    status = LANE_OK;
-    return;
-  }
-  if ((P.beam && tail - head > 2u * P.beam) || pops >= P.lane_popmax) {  // the beam could trigger (:577)
-    status = LANE_BAIL;
-    return;
-  }
-  const uint32_t slot = (head % QL) * 64 + lane;
-  uint32_t jm0, pk0;
-  lane_unpack(s_q[2 * QL * 64 + slot], jm0, pk0);
-  ++head;
-  ++pops;
-  const KState st{s_q[slot], jm0, __uint_as_float(s_q[QL * 64 + slot]), pk0};
-  if (live_dup(P, lv, st)) return;  // :618-622 against the snapshot's popped states
   // the state's reads go out together: node record, char filters, text at j and j + 1
   const DevNode nd = P.nodes[st.node];
   const uint4 aux = P.aux[st.node];
@@ -2788,7 +2776,7 @@ __device__ __forceinline__ void lane_step(const SearchParams& P, uint32_t* s_q, 
   const Prep pr = lane_prep(P, S, st, nd, start, c0, c1, nd.sb);
   auto push = [&](uint32_t node, uint32_t jm, float pen, uint32_t pk) {
     uint32_t w;
-    if (tail - head >= QL || !lane_pack(jm, pk, w)) {
+    if ((LINEAR ? tail >= QL : tail - head >= QL) || !lane_pack(jm, pk, w)) {
       status = LANE_BAIL;
       return false;
     }
@@ -2911,6 +2899,29 @@ __device__ __forceinline__ void lane_step(const SearchParams& P, uint32_t* s_q, 
       }
     }
   }
+}
+
+template <uint32_t QL, uint32_t ELN>
+__device__ __forceinline__ void lane_step(const SearchParams& P, uint32_t* s_q, uint4* s_e, const SegDesc& S, uint64_t start,
+                                          const LiveDedup& lv, uint32_t& status, uint32_t& head, uint32_t& tail,
+                                          uint32_t& nel, uint32_t& pops, unsigned& err) {
+  const uint32_t lane = lane_id();
+  if (head == tail) {
+    status = LANE_OK;
+    return;
+  }
+  if ((P.beam && tail - head > 2u * P.beam) || pops >= P.lane_popmax) {  // the beam could trigger (:577)
+    status = LANE_BAIL;
+    return;
+  }
+  const uint32_t slot = (head % QL) * 64 + lane;
+  uint32_t jm0, pk0;
+  lane_unpack(s_q[2 * QL * 64 + slot], jm0, pk0);
+  ++head;
+  ++pops;
+  const KState st{s_q[slot], jm0, __uint_as_float(s_q[QL * 64 + slot]), pk0};
+  if (live_dup(P, lv, st)) return;  // :618-622 against the snapshot's popped states
+  lane_expand<QL, ELN, false>(P, s_q, s_e, S, start, st, status, head, tail, nel, err);
 }
 
 // Persistent lanes: a lane whose window finishes (or bails) takes the next listed window at once,
@@ -3061,6 +3072,219 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
   }
 }
 
+// ---- Lane-serial cache builds of the sampled levels ----
+// A sampled level's build resumes each key's representative from its parent snapshot and pops only
+// the states of the key's last chars; most keys hold a few states, for which rc_build_kernel spends a
+// table clear, a snapshot load and whole 64-lane batches per key (C3: ~5.4 ns per key at every
+// level, the 7-char keys' mean queue being 0.1). Here every lane builds one key alone, in the
+// reference's sequential order, with the exact dedup of search.rs:617-627: the lane's states are a
+// linear array in LDS, so its popped states stay there for the dedup scans (a skipped pop is blanked),
+// and the parent's live dedup entries are scanned from the pool. A key whose parent queue or pushes
+// do not fit, whose pending count could beam, whose best list or parent dedup list is long, or that
+// has no parent snapshot is marked RC_DEFER and built by rc_build_kernel afterwards (rc_defer_only).
+// The snapshot written is the wave build's: header, queue, the live dedup entries (the union of the
+// parent's and the popped states', each key once with its stored penalty; the jcheck entries first)
+// and the best list.
+constexpr uint32_t RC_DEFER = 0xFFFFFFFDu;
+constexpr uint32_t LB_NVMAX = 48;  // parent dedup entries a lane scans from the pool
+template <uint32_t QB, uint32_t ELN>
+__global__ __launch_bounds__(64) void rc_lane_build_kernel(SearchParams P) {
+  __shared__ uint32_t s_q[3 * QB * 64];  // slot i of lane l at i * 64 + l: node, penalty, position word
+  uint4* s_e = P.ebuf + (size_t)blockIdx.x * P.ecap;  // best lists (this workgroup's emit slice)
+  const uint32_t lane = lane_id();
+  unsigned long long pool_cur = 0, pool_end = 0;  // wave-uniform: this wave's pool chunk
+  uint64_t popped_lane = 0;
+  unsigned err_all = 0;
+  for (;;) {
+    unsigned long long g0 = 0;
+    if (lane == 0) g0 = atomicAdd(P.counters + 7, 64ull);
+    g0 = shfl_u64(g0, 0);
+    if (g0 >= P.total_windows) break;
+    const uint64_t v = g0 + lane;
+    bool active = v < P.total_windows;
+    uint32_t status = 0;
+    SegDesc S{};
+    uint64_t start = 0;
+    RcHit hit{EMPTY, 0u, 0u, 0u, 0u};
+    if (active) {
+      const uint64_t wid = P.win_list[v];
+      const uint32_t kl = find_seg(P, wid);
+      S = P.segs[kl];
+      start = S.w_begin + (wid - P.seg_prefix[kl]);
+      hit = rc_lookup(P, S, start, 0xFFFFFFFFu);
+      if (hit.off != EMPTY && hit.tail == hit.head && !P.rc_keep_final) {  // the parent is final: uncached
+        P.rc_off[v] = EMPTY;
+        P.rc_count[v] = EMPTY;
+        active = false;
+      }
+    }
+    const uint32_t nq0 = active && hit.off != EMPTY ? hit.tail - hit.head : 0u;
+    const uint32_t nv0 = hit.nv_nel & 0xFFFFu, ne0 = hit.nv_nel >> 16;
+    if (active && (hit.off == EMPTY || nq0 > QB || ne0 > ELN || nv0 > LB_NVMAX)) {
+      P.rc_off[v] = RC_DEFER;  // (count EMPTY until the wave build writes it)
+      P.rc_count[v] = EMPTY;
+      active = false;
+    }
+    uint32_t head = 0, tail = 0, nel = 0, pops = 0, jbeam = 0, jp1 = 0;
+    const uint4* pdv = nullptr;  // parent's live dedup entries
+    unsigned err = 0;
+    if (active) {
+      const uint4* src = P.rc_pool + hit.off + RC_HDR;
+      bool fits = true;
+      for (uint32_t i = 0; i < nq0; ++i) {
+        const uint4 q = src[i];
+        uint32_t w;
+        fits = lane_pack(q.y, q.w, w) && fits;
+        s_q[i * 64 + lane] = q.x;
+        s_q[QB * 64 + i * 64 + lane] = q.z;
+        s_q[2 * QB * 64 + i * 64 + lane] = w;
+      }
+      for (uint32_t i = 0; i < ne0; ++i) s_e[i * 64 + lane] = src[nq0 + nv0 + i];
+      pdv = src + nq0;
+      if (P.beam) {
+        const uint4 h1 = P.rc_pool[hit.off + 1];
+        jbeam = h1.z;
+        jp1 = h1.w;
+      }
+      tail = nq0;
+      nel = ne0;
+      status = fits ? LANE_RUN : LANE_BAIL;
+    }
+    while (__ballot(status == LANE_RUN)) {
+      if (status != LANE_RUN) continue;
+      if (head == tail) {
+        status = LANE_OK;
+        continue;
+      }
+      if (P.beam && tail - head > 2u * P.beam) {  // the beam would select here (:577-589)
+        status = LANE_BAIL;
+        continue;
+      }
+      const uint32_t slot = head * 64 + lane;
+      const uint32_t w0 = s_q[2 * QB * 64 + slot];
+      uint32_t jm0, pk0;
+      lane_unpack(w0, jm0, pk0);
+      if ((jm0 & 0xFFFFu) + 1u >= P.rc_k) {  // stop before the first state that reads past the key
+        status = LANE_OK;
+        continue;
+      }
+      const KState st{s_q[slot], jm0, __uint_as_float(s_q[QB * 64 + slot]), pk0};
+      ++head;
+      ++pops;
+      if (P.beam) jp1 = max(jp1, (jm0 & 0xFFFFu) + 1u);
+      // dedup (:617-627): skipped iff a stored entry of the same key holds a penalty <= its own; the
+      // stored penalty of a key is the smallest of the parent's entry and the popped states kept
+      bool skip = false;
+      for (uint32_t i = 0; i + 1 < head && !skip; ++i)
+        if (s_q[i * 64 + lane] == st.node && s_q[2 * QB * 64 + i * 64 + lane] == w0 &&
+            __uint_as_float(s_q[QB * 64 + i * 64 + lane]) <= st.pen)
+          skip = true;
+      for (uint32_t i = 0; i < nv0 && !skip; ++i) {
+        const uint4 e = pdv[i];
+        if (e.x == st.node && e.y == st.jm && e.w == st.packed && __uint_as_float(e.z) <= st.pen) skip = true;
+      }
+      if (skip) {
+        s_q[slot] = EMPTY;  // not a stored entry
+        continue;
+      }
+      lane_expand<QB, ELN, true>(P, s_q, s_e, S, start, st, status, head, tail, nel, err);
+      if (err) status = LANE_BAIL;
+    }
+    // epilogue: the snapshot of every lane that finished
+    const bool fin = status == LANE_OK;
+    if (status == LANE_BAIL) {
+      P.rc_off[v] = RC_DEFER;
+      P.rc_count[v] = EMPTY;
+    }
+    popped_lane += fin ? pops : 0u;
+    uint32_t jmin = 0xFFFFu;
+    for (uint32_t i = head; i < tail; ++i) jmin = min(jmin, s_q[2 * QB * 64 + i * 64 + lane] & 0xFFu);
+    // live dedup entries: kept popped states not superseded by a later kept pop of the same key, and
+    // the parent's entries whose key no kept pop has
+    auto popped_live = [&](uint32_t i) -> bool {
+      const uint32_t n = s_q[i * 64 + lane], w = s_q[2 * QB * 64 + i * 64 + lane];
+      if (n == EMPTY || (w & 0xFFu) < jmin) return false;
+      for (uint32_t k = i + 1; k < head; ++k)
+        if (s_q[k * 64 + lane] == n && s_q[2 * QB * 64 + k * 64 + lane] == w) return false;
+      return true;
+    };
+    auto parent_live = [&](const uint4& e) -> bool {
+      if ((e.y & 0xFFFFu) < jmin) return false;
+      uint32_t w;
+      if (!lane_pack(e.y, e.w, w)) return true;  // no popped state can equal it
+      for (uint32_t k = 0; k < head; ++k)
+        if (s_q[k * 64 + lane] == e.x && s_q[2 * QB * 64 + k * 64 + lane] == w) return false;
+      return true;
+    };
+    uint32_t nv = 0, jlive = 0;
+    if (fin) {
+      for (uint32_t i = 0; i < head; ++i)
+        if (popped_live(i)) {
+          ++nv;
+          jlive = max(jlive, (s_q[2 * QB * 64 + i * 64 + lane] & 0xFFu) + 1u);
+        }
+      for (uint32_t i = 0; i < nv0; ++i) {
+        const uint4 e = pdv[i];
+        if (parent_live(e)) {
+          ++nv;
+          jlive = max(jlive, (e.y & 0xFFFFu) + 1u);
+        }
+      }
+    }
+    const uint32_t nq = tail - head;
+    bool bad = fin && (nel > P.rc_emax || nv > P.rc_vmax);
+    const uint32_t words = (fin && !bad) ? RC_HDR + nq + nv + nel : 0u;
+    // snapshots carved from the wave's pool chunk (one pool atomic per chunk)
+    const uint32_t incl = wave_inclusive_sum(words), tot = shfl_u32(incl, 63);
+    if (tot && pool_cur + tot > pool_end) {
+      const unsigned long long want = max((unsigned long long)tot, (unsigned long long)P.rc_pool_chunk);
+      unsigned long long c = 0;
+      if (lane == 0) c = atomicAdd(P.rc_pool_used, want);
+      pool_cur = shfl_u64(c, 0);
+      pool_end = pool_cur + want;
+    }
+    const unsigned long long off = pool_cur + incl - words;
+    pool_cur += tot;
+    if (fin) {
+      bad = bad || off + words > P.rc_pool_cap || off > 0xFFFFFFF0ull;
+      if (!bad) {
+        uint4* dst = P.rc_pool + off + RC_HDR;
+        for (uint32_t i = 0; i < nq; ++i) {
+          const uint32_t sl = (head + i) * 64 + lane;
+          uint32_t jm, pk;
+          lane_unpack(s_q[2 * QB * 64 + sl], jm, pk);
+          dst[i] = make_uint4(s_q[sl], jm, s_q[QB * 64 + sl], pk);
+        }
+        const uint32_t jcheck = min(jlive, jbeam);
+        uint32_t at = 0, ncheck = 0;
+        for (uint32_t pass = 0; pass < 2; ++pass) {  // the entries with j < jcheck first
+          for (uint32_t i = 0; i < head; ++i) {
+            const uint32_t sl = i * 64 + lane, w = s_q[2 * QB * 64 + sl];
+            if (((w & 0xFFu) + 1u <= jcheck) != (pass == 0) || !popped_live(i)) continue;
+            uint32_t jm, pk;
+            lane_unpack(w, jm, pk);
+            dst[nq + at++] = make_uint4(s_q[sl], jm, s_q[QB * 64 + sl], pk);
+          }
+          for (uint32_t i = 0; i < nv0; ++i) {
+            const uint4 e = pdv[i];
+            if (((e.y & 0xFFFFu) + 1u <= jcheck) != (pass == 0) || !parent_live(e)) continue;
+            dst[nq + at++] = e;
+          }
+          if (pass == 0) ncheck = at;
+        }
+        for (uint32_t i = 0; i < nel; ++i) dst[nq + nv + i] = s_e[i * 64 + lane];
+        P.rc_pool[off] = make_uint4(hit.head + head, hit.tail + (tail - nq0), nv, pops + hit.pops);
+        P.rc_pool[off + 1] = make_uint4(nel, ncheck ? (jcheck | (ncheck << 16)) : 0u, jbeam, jp1);
+      }
+      P.rc_off[v] = bad ? EMPTY : (uint32_t)off;
+      P.rc_count[v] = bad ? EMPTY : nq;
+    }
+    err_all |= err & ~(ERR_QUEUE | ERR_VISITED | ERR_EMIT);
+  }
+  wave_add_counter(P.counters + 1, popped_lane);
+  (void)err_all;
+}
+
 // LK: the window prologue looks snapshots up itself (cache builds); otherwise a main pass with the
 // prefix cache reads the hits rc_lookup_kernel stored.
 template <uint32_t VCAP, uint32_t QCAP, bool MAP, bool LK, bool LIVE = false>
@@ -3156,6 +3380,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           active = !window_skipped(P, S, start, err);
         }
       }
+      if (P.rc_mode == 2 && P.rc_defer_only) active = active && P.rc_off[v] == RC_DEFER;  // after the lane build
       if constexpr (LK)
         if (P.rc_mode != 0 && P.rc_ntab && active) hit = rc_lookup(P, P.segs[kl], start, QCAP);
       if (LK && P.rc_mode == 1) {
@@ -4455,6 +4680,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.rc_region_cnt = nullptr;
   P.rc_ntab = 0;
   P.rc_kstart = 0;
+  P.rc_defer_only = 0;
   P.rc_lane_flush = diag_env("FAC_RC_NO_LANE") ? 0 : 1;
   P.dyn_chunks = diag_env("FAC_STATIC_GRID") ? 0 : 1;
   const bool root_out = !e.nodes.empty() && e.nodes[0].out_end > e.nodes[0].out_begin;
@@ -4690,6 +4916,17 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         grid = (uint32_t)std::min<uint64_t>((n_ent + Q.chunk - 1) / Q.chunk, 0x7FFFFFFFull);
       }
       const bool live_build = live_builds && sampled && Q.rc_ntab > 0;
+      // sampled levels: the lane-serial build first (rc_lane_build_kernel), the wave build then takes
+      // the keys it deferred
+      const bool lane_build = sampled && !live_build && Q.rc_ntab > 0 && !diag_env("FAC_NO_LANE_BUILD");
+      Q.rc_defer_only = 0;
+      if (lane_build) {
+        const uint32_t lg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_ent + 63) / 64, (uint64_t)max_grid));
+        hipLaunchKernelGGL((rc_lane_build_kernel<32, 8>), dim3(lg), dim3(64), 0, bs, Q);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemsetAsync(Q.counters + 7, 0, sizeof(unsigned long long), bs));  // the wave build's work counter
+        Q.rc_defer_only = 1;
+      }
       uint32_t qk = 256;  // launch_rc_build's ring
       while (qk < qbuild) qk <<= 1;
       if (int src = prep_slots(Q, bs, qk, !live_build)) return src;
