@@ -234,6 +234,8 @@ struct SearchParams {
   int32_t rc_lane_flush;         // resumed windows with an empty queue are flushed lane-parallel
   int32_t dyn_chunks;            // 1: chunks from the work counter; 0: static grid-stride
   uint32_t lane_popmax;           // lane_window_kernel: pops after which a window goes back to the wave kernel
+  uint32_t live_nqmax;            // bfs_window_kernel_live: windows resuming with a longer queue go straight to the
+                                  // exact variant (0: none)
   int32_t lane_debug;             // lane_window_kernel: diagnostics counters (FAC_RC_DEBUG)
   // window list mode (re-run of spilled windows) and the spill list of capacity overflows
   const uint64_t* win_list;  // null: virtual windows 0..total_windows; else list of virtual ids

@@ -1768,6 +1768,13 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
 #endif
                            ) {
   const uint32_t lane = lane_id();
+  if constexpr (LIVE)  // a window resuming with a long queue would most likely beam: the exact variant takes it
+    if (P.live_nqmax && rc.off != EMPTY && rc.tail - rc.head > P.live_nqmax) {
+      err |= ERR_QUEUE;
+      head_out = rc.head;
+      vcount_out = 0;
+      return rc.tail;
+    }
   // FAC_PHASE_PROF slots: 12: per-edge states, 13: fast states, 14: committed, 15: loaded, 16-19: Bc
   // buckets, 20: prologue (table clear, snapshot load), 21: flush
   PROF_T(t_win);
@@ -4681,6 +4688,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.rc_ntab = 0;
   P.rc_kstart = 0;
   P.rc_defer_only = 0;
+  P.live_nqmax = 0;
   P.rc_lane_flush = diag_env("FAC_RC_NO_LANE") ? 0 : 1;
   P.dyn_chunks = diag_env("FAC_STATIC_GRID") ? 0 : 1;
   const bool root_out = !e.nodes.empty() && e.nodes[0].out_end > e.nodes[0].out_begin;
@@ -5306,6 +5314,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         if (!ev_lane) HIP_TRY(hipEventCreate(&ev_lane));
         P.lane_debug = diag_env("FAC_RC_DEBUG") ? 1 : 0;
         P.lane_popmax = (uint32_t)std::max<unsigned long>(1, diag_env("FAC_LANE_POPS") ? std::strtoul(diag_env("FAC_LANE_POPS"), nullptr, 10) : 32ul);
+        P.live_nqmax = diag_env("FAC_LIVE_NQMAX") ? (uint32_t)std::strtoul(diag_env("FAC_LIVE_NQMAX"), nullptr, 10) : 0u;
         if (int lrc = launch_lane()) return lrc;
         HIP_TRY(hipEventRecord(ev_lane, stream));
       }
