@@ -3094,6 +3094,9 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
 // and the best list.
 constexpr uint32_t RC_DEFER = 0xFFFFFFFDu;
 constexpr uint32_t LB_NVMAX = 48;  // parent dedup entries a lane scans from the pool
+// diagnostics (FAC_RC_DEBUG): keys built, parent final, deferred: no parent / queue / best / dedup
+// entries / state not packable; bailed while running; pops of the built keys
+__device__ unsigned long long g_lb_dbg[8];
 template <uint32_t QB, uint32_t ELN>
 __global__ __launch_bounds__(64) void rc_lane_build_kernel(SearchParams P) {
   __shared__ uint32_t s_q[3 * QB * 64];  // slot i of lane l at i * 64 + l: node, penalty, position word
@@ -3127,6 +3130,13 @@ __global__ __launch_bounds__(64) void rc_lane_build_kernel(SearchParams P) {
     }
     const uint32_t nq0 = active && hit.off != EMPTY ? hit.tail - hit.head : 0u;
     const uint32_t nv0 = hit.nv_nel & 0xFFFFu, ne0 = hit.nv_nel >> 16;
+    if (P.lane_debug) {
+      const uint32_t c = !active ? 8u : hit.off == EMPTY ? 2u : nq0 > QB ? 3u : ne0 > ELN ? 4u : nv0 > LB_NVMAX ? 5u : 8u;
+      for (uint32_t k = 2; k < 6; ++k) {
+        const uint64_t m = __ballot(c == k);
+        if (m && lane == 0) atomicAdd(&g_lb_dbg[k], (unsigned long long)__popcll(m));
+      }
+    }
     if (active && (hit.off == EMPTY || nq0 > QB || ne0 > ELN || nv0 > LB_NVMAX)) {
       P.rc_off[v] = RC_DEFER;  // (count EMPTY until the wave build writes it)
       P.rc_count[v] = EMPTY;
@@ -3199,6 +3209,13 @@ __global__ __launch_bounds__(64) void rc_lane_build_kernel(SearchParams P) {
     }
     // epilogue: the snapshot of every lane that finished
     const bool fin = status == LANE_OK;
+    if (P.lane_debug) {
+      const uint64_t mf = __ballot(fin), mb = __ballot(status == LANE_BAIL);
+      if (lane == 0) {
+        atomicAdd(&g_lb_dbg[0], (unsigned long long)__popcll(mf));
+        atomicAdd(&g_lb_dbg[6], (unsigned long long)__popcll(mb));
+      }
+    }
     if (status == LANE_BAIL) {
       P.rc_off[v] = RC_DEFER;
       P.rc_count[v] = EMPTY;
@@ -3633,6 +3650,15 @@ template <uint32_t QCAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((FAC_BEAM_WAVES && QCAP <= 256) ? FAC_BEAM_WAVES : 1)))
 void rc_build_kernel(SearchParams P) {
   bfs_window_body<512, QCAP, false, true>(P);  // the prefix cache is off with mappings
+}
+// a smaller build variant (256-entry dedup table, 10 KB of LDS: up to 16 waves per CU, held to 128
+// VGPRs) for the sampled levels, whose keys pop few states: their builds wait on memory, not issue
+// (FAC_BUILD_SMALL=1: A/B)
+#ifndef FAC_SMALL_BUILD_WAVES
+#define FAC_SMALL_BUILD_WAVES 4
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAC_SMALL_BUILD_WAVES))) void rc_build_kernel_small(SearchParams P) {
+  bfs_window_body<256, 256, false, true>(P);
 }
 // dedup-free build of a sampled level of a beamed engine (launch_pass): resumes from the parent
 // snapshot, honours its check entries (run_window LIVE); a key that would beam (or overflow) is left
@@ -4926,12 +4952,22 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       const bool live_build = live_builds && sampled && Q.rc_ntab > 0;
       // sampled levels: the lane-serial build first (rc_lane_build_kernel), the wave build then takes
       // the keys it deferred
-      const bool lane_build = sampled && !live_build && Q.rc_ntab > 0 && !diag_env("FAC_NO_LANE_BUILD");
+      const bool lane_build = sampled && !live_build && Q.rc_ntab > 0 && diag_env("FAC_LANE_BUILD");  // A/B: slower so far
       Q.rc_defer_only = 0;
       if (lane_build) {
         const uint32_t lg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_ent + 63) / 64, (uint64_t)max_grid));
+        Q.lane_debug = diag_env("FAC_RC_DEBUG") ? 1 : 0;
         hipLaunchKernelGGL((rc_lane_build_kernel<32, 8>), dim3(lg), dim3(64), 0, bs, Q);
         HIP_TRY(hipGetLastError());
+        if (Q.lane_debug) {
+          unsigned long long d[8];
+          HIP_TRY(hipStreamSynchronize(bs));
+          HIP_TRY(hipMemcpyFromSymbol(d, HIP_SYMBOL(g_lb_dbg), sizeof(d)));
+          std::fprintf(stderr, "FAC_LB k=%u keys=%u built=%llu deferred: no-parent %llu queue %llu best %llu dedup %llu bailed %llu\n",
+                       T.k, n_ent, d[0], d[2], d[3], d[4], d[5], d[6]);
+          std::memset(d, 0, sizeof(d));
+          HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_lb_dbg), d, sizeof(d)));
+        }
         HIP_TRY(hipMemsetAsync(Q.counters + 7, 0, sizeof(unsigned long long), bs));  // the wave build's work counter
         Q.rc_defer_only = 1;
       }
@@ -4939,6 +4975,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       while (qk < qbuild) qk <<= 1;
       if (int src = prep_slots(Q, bs, qk, !live_build)) return src;
       if (live_build) hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
+      else if (sampled && qbuild <= 256 && diag_env("FAC_BUILD_SMALL")) hipLaunchKernelGGL(rc_build_kernel_small, dim3(grid), dim3(64), 0, bs, Q);
       else launch_rc_build(qbuild, grid, bs, Q);
       const hipError_t le = hipGetLastError();
       if (le != hipSuccess) {
