@@ -254,7 +254,8 @@ struct SearchParams {
   uint32_t rc_k;                    // key chars of the level being collected / built (2..8)
   uint32_t rc_ntab;                 // tables a lookup consults (0..kRcLevels), deepest first
   uint32_t rc_kstart;               // rc_lookup's first probe: the shallowest level with k >= this (0: deepest)
-  uint32_t rc_defer_only;           // cache build: only the keys the lane-serial build deferred (rc_off == RC_DEFER)
+  uint32_t rc_defer_only;           // cache build: only the keys an earlier build deferred (rc_off == RC_DEFER)
+  uint32_t rc_defer_fail;           // cache build: a key that overflows the ring or dedup table is deferred
   RcTable rc_tab[kRcLevels];
   uint32_t rc_vmax, rc_emax;        // dedup / best-list entries a snapshot may hold
   uint4* rc_pool;                   // snapshots: header x4, queue, dedup entries, best list

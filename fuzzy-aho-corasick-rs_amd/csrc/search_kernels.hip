@@ -3574,7 +3574,10 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
               // jcheck: dedup entries a resumed dedup-free run must still honour (j + 1 <= jcheck)
               P.rc_pool[off + 1] = make_uint4(EL.n, ncheck ? (jcheck | (ncheck << 16)) : 0u, jbeam[0], jbeam[1]);
             }
-            P.rc_off[ent] = bad ? EMPTY : (uint32_t)off;
+            // a key the small build variant could not hold (frontier ring or dedup table full) is left
+            // to the full-size build that follows it (rc_defer_fail, rc_defer_only)
+            const bool defer = P.rc_defer_fail && (wave_or(err) & (ERR_QUEUE | ERR_VISITED)) != 0;
+            P.rc_off[ent] = defer ? RC_DEFER : bad ? EMPTY : (uint32_t)off;
             P.rc_count[ent] = bad ? EMPTY : nq;
           }
           (void)vcnt;
@@ -4714,6 +4717,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.rc_ntab = 0;
   P.rc_kstart = 0;
   P.rc_defer_only = 0;
+  P.rc_defer_fail = 0;
   P.live_nqmax = 0;
   P.rc_lane_flush = diag_env("FAC_RC_NO_LANE") ? 0 : 1;
   P.dyn_chunks = diag_env("FAC_STATIC_GRID") ? 0 : 1;
@@ -4974,9 +4978,22 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       uint32_t qk = 256;  // launch_rc_build's ring
       while (qk < qbuild) qk <<= 1;
       if (int src = prep_slots(Q, bs, qk, !live_build)) return src;
-      if (live_build) hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
-      else if (sampled && qbuild <= 256 && diag_env("FAC_BUILD_SMALL")) hipLaunchKernelGGL(rc_build_kernel_small, dim3(grid), dim3(64), 0, bs, Q);
-      else launch_rc_build(qbuild, grid, bs, Q);
+      if (live_build) {
+        hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
+      } else if (sampled && qbuild <= 256 && !lane_build && diag_env("FAC_BUILD_SMALL")) {
+        // the sampled levels' keys pop few states and their builds wait on memory: the small variant
+        // (16 waves per CU) first, then the full-size build takes the keys it could not hold
+        Q.rc_defer_fail = 1;
+        hipLaunchKernelGGL(rc_build_kernel_small, dim3(grid), dim3(64), 0, bs, Q);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemsetAsync(Q.counters + 7, 0, sizeof(unsigned long long), bs));
+        Q.rc_defer_fail = 0;
+        Q.rc_defer_only = 1;
+        if (int src = prep_slots(Q, bs, qk, true)) return src;
+        launch_rc_build(qbuild, grid, bs, Q);
+      } else {
+        launch_rc_build(qbuild, grid, bs, Q);
+      }
       const hipError_t le = hipGetLastError();
       if (le != hipSuccess) {
         err = std::string("kernel launch: ") + hipGetErrorString(le);
