@@ -3655,8 +3655,9 @@ void rc_build_kernel(SearchParams P) {
   bfs_window_body<512, QCAP, false, true>(P);  // the prefix cache is off with mappings
 }
 // a smaller build variant (256-entry dedup table, 10 KB of LDS: up to 16 waves per CU, held to 128
-// VGPRs) for the sampled levels, whose keys pop few states: their builds wait on memory, not issue
-// (FAC_BUILD_SMALL=1: A/B)
+// VGPRs) for the sampled levels, whose keys pop few states: their builds wait on memory, not issue.
+// A key it cannot hold (ring or table full) is deferred to the full-size build. C3 per step: 187.2 ->
+// 174.6 ms (prefix cache 128.3 -> 115.8), fresh words 547.4 -> 506.1 (profiles/r04i; FAC_NO_BUILD_SMALL: A/B)
 #ifndef FAC_SMALL_BUILD_WAVES
 #define FAC_SMALL_BUILD_WAVES 4
 #endif
@@ -4980,7 +4981,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (int src = prep_slots(Q, bs, qk, !live_build)) return src;
       if (live_build) {
         hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
-      } else if (sampled && qbuild <= 256 && !lane_build && diag_env("FAC_BUILD_SMALL")) {
+      } else if (sampled && qbuild <= 256 && !lane_build && !diag_env("FAC_NO_BUILD_SMALL")) {
         // the sampled levels' keys pop few states and their builds wait on memory: the small variant
         // (16 waves per CU) first, then the full-size build takes the keys it could not hold
         Q.rc_defer_fail = 1;
@@ -5092,7 +5093,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         (uint64_t)cus * env_u("FAC_RC_CGRID2", ks.size() >= 2 ? 2 : 4)));
     // (beamed engines: keys seen >= 4 times while the selects were inlined into the window loop and
     // the builds spilled registers; >= 2 since: C3 162.0 -> 151.8 ms, profiles/r03/sweep_levels.txt)
-    const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", s2 > 2 ? 1 : 2));
+    // round 4: beamed engines keep keys seen >= 3 times (C3: a sampled key's build costs about the
+    // same whatever its reuse, ~5 ns; 187.2 -> 174.6 -> 169.0 ms per step with the small build
+    // variant and then >= 3; fresh words 547 -> 506 -> 502 ms; profiles/r04i)
+    const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", s2 > 2 ? 1 : P.beam ? 3 : 2));
     std::vector<RcTable> Lx;        // sampled levels, ascending k
     std::vector<uint32_t> n_entx;   // their entries
     std::vector<size_t> xbuf;       // their count-table buffers
