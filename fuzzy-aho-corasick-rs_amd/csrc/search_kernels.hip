@@ -4588,8 +4588,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     err = "beam width too large for the on-chip frontier";
     return FAC_E_UNSUPPORTED;
   }
+  const bool spill_small = diag_env("FAC_SPILL_SMALL") != nullptr;  // A/B: dedup-free spills to <256, 256> first
   auto escalate = [&](size_t cur) {  // next variant for spilled windows
-    const uint32_t want_v = std::max<uint32_t>(kVariants[cur].vcap * 2, 512);
+    const uint32_t want_v = (spill_small && kVariants[cur].vcap == 0) ? 256u : std::max<uint32_t>(kVariants[cur].vcap * 2, 512);
     for (size_t i = cur + 1; i < nv; ++i)
       if (fits(kVariants[i]) && kVariants[i].vcap >= want_v && kVariants[i].qcap >= kVariants[cur].qcap) return i;
     // past the largest table: an unbeamed, non-exact engine may still trade the table for a
@@ -4981,7 +4982,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (int src = prep_slots(Q, bs, qk, !live_build)) return src;
       if (live_build) {
         hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
-      } else if (sampled && qbuild <= 256 && !lane_build && !diag_env("FAC_NO_BUILD_SMALL")) {
+      } else if ((sampled || (T.k == L1.k && diag_env("FAC_BUILD_SMALL_L1"))) && qbuild <= 256 && !lane_build &&
+                 !diag_env("FAC_NO_BUILD_SMALL")) {
         // the sampled levels' keys pop few states and their builds wait on memory: the small variant
         // (16 waves per CU) first, then the full-size build takes the keys it could not hold
         Q.rc_defer_fail = 1;

@@ -1,0 +1,7 @@
+#!/bin/bash
+# r04j: defaults after r04i, plus A/B of the small variant for level 1 and for the spilled windows
+set -eo pipefail
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$ROOT"
+BENCH_ARGS="--no-fresh-diag" bash profiles/ab_knobs.sh r04j_v "X=0" "FAC_BUILD_SMALL_L1=1" "FAC_SPILL_SMALL=1"
+BENCH_ARGS="--vocab 0 --no-fresh-diag" bash profiles/ab_knobs.sh r04j_f "X=0" "FAC_BUILD_SMALL_L1=1" "FAC_SPILL_SMALL=1" "FAC_RC_K2=0"
