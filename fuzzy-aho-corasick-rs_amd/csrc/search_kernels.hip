@@ -2269,6 +2269,30 @@ __device__ __forceinline__ uint32_t rc_key_hash(uint4 k) {
 // shallower snapshot -- only costs that window some work). On a miss the shallower levels are
 // probed, deepest first. C3 (vocabulary workload): 1.8 random lines per window instead of 2.9 when
 // the deepest level came first (windows settle at 5 chars most often, and 53 M of them finally).
+// one level's probe: 0 miss (or not probed), 1 hit with an open snapshot, 2 final, 3 unusable
+__device__ __forceinline__ uint32_t rc_probe(const RcTable& T, const uint32_t* c, uint32_t enc, bool ok, uint64_t s,
+                                             const SegDesc& S, uint32_t QCAP, uint32_t t, RcHit& h) {
+  if (!(T.k <= enc && (ok || s + T.k <= S.avail))) return 0u;
+  const uint4 want = rc_exact_key(c, T.k);
+  uint32_t slot = rc_key_hash(want) & T.ct_mask;
+  uint4 val = make_uint4(0u, 0u, 0u, 0u);
+  bool hit = false;
+  for (uint32_t p = 0; p < RC_PROBES; ++p, slot = (slot + 1) & T.ct_mask) {  // collisions probe on (rare)
+    const uint4* e = T.ct + 2 * (size_t)slot;
+    const uint4 k2 = e[0];
+    val = e[1];
+    if (!(val.w & RC_OCC)) break;
+    if (k2.x == want.x && k2.y == want.y && k2.z == want.z && k2.w == want.w) {
+      hit = true;
+      break;
+    }
+  }
+  if (!hit) return 0u;
+  const uint32_t nq = val.z & 0xFFFFu;
+  if (nq + 1u > QCAP) return 3u;
+  h = RcHit{val.x, val.y, val.y + nq, ((val.w >> 22) & 0x1FFu) | (val.z & 0xFFFF0000u), val.w & RC_POPS_MASK, t};
+  return nq ? 1u : 2u;
+}
 __device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc& S, uint64_t s, uint32_t QCAP) {
   uint32_t kmax = 0;
   for (uint32_t t = 0; t < P.rc_ntab; ++t) kmax = max(kmax, P.rc_tab[t].k);
@@ -2278,50 +2302,54 @@ __device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc&
 #pragma unroll
   for (uint32_t i = 0; i < 8; ++i)  // keys hold 16-bit units: a longer key would contain char i
     if (enc == 8 && c[i] != RC_PAD && c[i] >= 0xFFFFu) enc = i;
-  // probe of level t: 0 miss (or not probed), 1 hit with an open snapshot, 2 final, 3 unusable
-  RcHit r{EMPTY, 0u, 0u, 0u, 0u};
-  auto probe = [&](uint32_t t, RcHit& h) -> uint32_t {
-    const RcTable& T = P.rc_tab[t];
-    if (!(T.k <= enc && (ok || s + T.k <= S.avail))) return 0u;
-    const uint4 want = rc_exact_key(c, T.k);
-    uint32_t slot = rc_key_hash(want) & T.ct_mask;
-    uint4 val = make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t p = 0; p < RC_PROBES; ++p, slot = (slot + 1) & T.ct_mask) {  // collisions probe on (rare)
-      const uint4* e = T.ct + 2 * (size_t)slot;
-      const uint4 k2 = e[0];
-      val = e[1];
-      if (!(val.w & RC_OCC)) return 0u;
-      if (k2.x == want.x && k2.y == want.y && k2.z == want.z && k2.w == want.w) break;
-      if (p + 1 == RC_PROBES) return 0u;
-    }
-    const uint32_t nq = val.z & 0xFFFFu;
-    if (nq + 1u > QCAP) return 3u;
-    h = RcHit{val.x, val.y, val.y + nq, ((val.w >> 22) & 0x1FFu) | (val.z & 0xFFFF0000u), val.w & RC_POPS_MASK, t};
-    return nq ? 1u : 2u;
-  };
+  // (every loop is unrolled over the level index, and the probe is a force-inlined function: a
+  // dynamic index into the kernel argument's table array, or a lambda capturing the chars, made the
+  // cache builds keep them in scratch, 76 -> 972 B per lane)
   const uint32_t n = P.rc_ntab;
   uint32_t st = 0;  // rc_tab is deepest first: the last level with k >= rc_kstart
-  for (uint32_t t = 0; t < n; ++t)
-    if (P.rc_tab[t].k >= P.rc_kstart) st = t;
-  bool found = false;
-  for (uint32_t t = st + 1; t-- > 0;) {  // st, then deeper while open
-    RcHit h;
-    const uint32_t res = probe(t, h);
+#pragma unroll
+  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t)
+    if (t < n && P.rc_tab[t].k >= P.rc_kstart) st = t;
+  RcHit r{EMPTY, 0u, 0u, 0u, 0u};
+  bool found = false, up = true;
+#pragma unroll
+  for (int t = kRcLevels - 1; t >= 0; --t) {  // st, then deeper while open
+    if (!up || (uint32_t)t > st || (uint32_t)t >= n) continue;
+    RcHit h{EMPTY, 0u, 0u, 0u, 0u};
+    const uint32_t res = rc_probe(P.rc_tab[t], c, enc, ok, s, S, QCAP, (uint32_t)t, h);
     if (res == 1u || res == 2u) {
       r = h;
       found = true;
     }
-    if (res != 1u) break;
+    up = res == 1u;
   }
-  for (uint32_t t = st + 1; !found && t < n; ++t) {  // shallower levels, deepest first
-    RcHit h;
-    const uint32_t res = probe(t, h);
+#pragma unroll
+  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {  // shallower levels, deepest first
+    if (found || t <= st || t >= n) continue;
+    RcHit h{EMPTY, 0u, 0u, 0u, 0u};
+    const uint32_t res = rc_probe(P.rc_tab[t], c, enc, ok, s, S, QCAP, t, h);
     if (res == 1u || res == 2u) {
       r = h;
       found = true;
     }
   }
   return r;
+}
+
+// The cache builds' parent lookups, one thread per key ahead of the build (rc_bhits / rc_bpops): in
+// the build kernel itself the lookup's registers and arrays raised the window loop's pressure (spills
+// and a 972-byte scratch frame per lane).
+__global__ __launch_bounds__(256) void rc_parent_kernel(SearchParams P, uint32_t qcap) {
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < P.total_windows;
+       v += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t wid = P.win_list[v];
+    const uint32_t kl = find_seg(P, wid);
+    const SegDesc S = P.segs[kl];
+    const uint64_t start = S.w_begin + (wid - P.seg_prefix[kl]);
+    const RcHit hit = rc_lookup(P, S, start, qcap);
+    P.rc_bhits[v] = make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel);
+    P.rc_bpops[v] = hit.pops;
+  }
 }
 
 // Lookup table of a built level: every entry with a snapshot is inserted under its exact key (the
@@ -3406,7 +3434,10 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
       }
       if (P.rc_mode == 2 && P.rc_defer_only) active = active && P.rc_off[v] == RC_DEFER;  // after the lane build
       if constexpr (LK)
-        if (P.rc_mode != 0 && P.rc_ntab && active) hit = rc_lookup(P, P.segs[kl], start, QCAP);
+        if (P.rc_mode != 0 && P.rc_ntab && active && P.rc_bhits) {  // rc_parent_kernel's lookup
+          const uint4 h = P.rc_bhits[v];
+          hit = RcHit{h.x, h.y, h.z, h.w, P.rc_bpops[v]};
+        }
       if (LK && P.rc_mode == 1) {
         const bool resumed = active && hit.off != EMPTY;
         res_lane += resumed ? 1u : 0u;
@@ -4609,6 +4640,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   DevBuf d_hits, d_hitp;   // per-window lookups of the main pass
   DevBuf d_voff, d_rcnt;   // ... their windows and per-region counts
   DevBuf d_seen;           // prefix cache: sampled levels' first-sighting bitmap
+  DevBuf d_bhits, d_bpops; // prefix cache builds: the representatives' parent snapshots
   DevBuf d_slots, d_bsel;  // wave-slot rings (one per stream), beam-selection scratch
   ScratchSet* bound = t_scratch;  // a streaming worker's own set, else the engine's
   std::unique_lock<std::mutex> lease(bound ? bound->mu : e.scratch_mu, std::try_to_lock);
@@ -4628,7 +4660,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     bufs.push_back(&d_rcnt);
     bufs.push_back(&d_slots);
     bufs.push_back(&d_bsel);
-    static_assert(Engine::kScratch >= 29 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
+    bufs.push_back(&d_bhits);
+    bufs.push_back(&d_bpops);
+    static_assert(Engine::kScratch >= 31 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
     static_assert(ScratchSet::kSlots >= Engine::kScratch, "stream scratch slots");
     for (size_t i = 0; i < bufs.size(); ++i) bufs[i]->bind(&scratch_p[i], &scratch_n[i]);
   }
@@ -4955,6 +4989,21 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         Q.dyn_chunks = 0;
         grid = (uint32_t)std::min<uint64_t>((n_ent + Q.chunk - 1) / Q.chunk, 0x7FFFFFFFull);
       }
+      Q.rc_bhits = nullptr;
+      Q.rc_bpops = nullptr;
+      if (Q.rc_ntab > 0) {  // the representatives' parent snapshots (rc_parent_kernel)
+        // (each level allocates: the slot keeps the largest, and a level's build is ordered after the
+        // previous one's on this stream or waits for it through l1_done)
+        HIP_TRY(d_bhits.alloc((size_t)n_ent * sizeof(uint4), bs));
+        HIP_TRY(d_bpops.alloc((size_t)n_ent * sizeof(uint32_t), bs));
+        Q.rc_bhits = static_cast<uint4*>(d_bhits.p);
+        Q.rc_bpops = static_cast<uint32_t*>(d_bpops.p);
+        uint32_t qk0 = 256;
+        while (qk0 < qbuild) qk0 <<= 1;
+        hipLaunchKernelGGL(rc_parent_kernel, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_ent + 255) / 256, (uint64_t)cus * 8))),
+                           dim3(256), 0, bs, Q, qk0);
+        HIP_TRY(hipGetLastError());
+      }
       const bool live_build = live_builds && sampled && Q.rc_ntab > 0;
       // sampled levels: the lane-serial build first (rc_lane_build_kernel), the wave build then takes
       // the keys it deferred
@@ -5095,10 +5144,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         (uint64_t)cus * env_u("FAC_RC_CGRID2", ks.size() >= 2 ? 2 : 4)));
     // (beamed engines: keys seen >= 4 times while the selects were inlined into the window loop and
     // the builds spilled registers; >= 2 since: C3 162.0 -> 151.8 ms, profiles/r03/sweep_levels.txt)
-    // round 4: beamed engines keep keys seen >= 3 times (C3: a sampled key's build costs about the
-    // same whatever its reuse, ~5 ns; 187.2 -> 174.6 -> 169.0 ms per step with the small build
-    // variant and then >= 3; fresh words 547 -> 506 -> 502 ms; profiles/r04i)
-    const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", s2 > 2 ? 1 : P.beam ? 3 : 2));
+    // (keys seen >= 3 times measured slower once the small build variant made the builds cheaper:
+    // the lane and wave kernels took more than the builds saved, profiles/r04k)
+    const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", s2 > 2 ? 1 : 2));
     std::vector<RcTable> Lx;        // sampled levels, ascending k
     std::vector<uint32_t> n_entx;   // their entries
     std::vector<size_t> xbuf;       // their count-table buffers

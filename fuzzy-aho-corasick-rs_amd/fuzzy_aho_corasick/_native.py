@@ -171,6 +171,8 @@ SIGNATURES = {
 }
 
 for _name, (_res, _args) in SIGNATURES.items():
+    if "FAC_LIB" in os.environ and not hasattr(lib, _name):
+        continue  # an older diagnostics build (FAC_LIB) may lack newer entry points
     _fn = getattr(lib, _name)
     _fn.restype = _res
     _fn.argtypes = _args
