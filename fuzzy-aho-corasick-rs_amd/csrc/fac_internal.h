@@ -165,7 +165,8 @@ struct RcTable {
   uint32_t ct_mask;                  // lookup slots - 1
 };
 
-constexpr int N_COUNTERS = 11;  // SearchParams::counters (8: lane-searched windows, 9: lane work counter, 10: lookup regions)
+constexpr int N_COUNTERS = 12;  // SearchParams::counters (8: lane-searched windows, 9: lane work counter, 10: lookup
+                                // regions, 11: snapshots a cache build kept)
 constexpr int kRcLevels = 5;   // prefix-cache levels: level 0 (under level 1), level 1, up to 3 sampled levels
 
 struct SearchParams {

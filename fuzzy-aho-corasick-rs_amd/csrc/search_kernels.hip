@@ -3353,6 +3353,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   uint64_t cached_lane = 0;            // per lane: lane-flushed windows' snapshot pops
   unsigned long long pool_cur = 0, pool_end = 0;  // cache build: this wave's snapshot pool chunk
   uint32_t res_lane = 0, triv_lane = 0;  // per lane: resumed windows, of those lane-flushed
+  uint32_t kept_snaps = 0;                // wave-uniform (lane 0's count): snapshots this cache build kept
   // dedup-commit claim sequence (phase C): fresh claims are >= 128, above any stale word the
   // expansion scratch leaves behind (<= 64)
   uint32_t cseq = 1;
@@ -3605,6 +3606,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
             const bool defer = P.rc_defer_fail && (wave_or(err) & (ERR_QUEUE | ERR_VISITED)) != 0;
             P.rc_off[ent] = defer ? RC_DEFER : bad ? EMPTY : (uint32_t)off;
             P.rc_count[ent] = bad ? EMPTY : nq;
+            kept_snaps += bad ? 0u : 1u;
           }
           (void)vcnt;
           err &= ~(ERR_QUEUE | ERR_VISITED | ERR_EMIT);
@@ -3632,6 +3634,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
     if (any_err(err)) break;
   }
   if (lane == 0) atomicAdd(P.counters + 1, (unsigned long long)popped);
+  if (lane == 0 && kept_snaps) atomicAdd(P.counters + 11, (unsigned long long)kept_snaps);  // sizes the lookup table
 #ifdef FAC_PHASE_PROF
   if (lane == 0) {
     for (int i = 0; i < 23; ++i) atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + i], (unsigned long long)prof_acc[i]);
@@ -4194,6 +4197,9 @@ bool debug_poison() {
 // (reproduced 6/60 calls; 0/60 with hipMalloc), so the pool is not used.
 // One pinned, device-mapped host word per host thread (kept for the thread's lifetime): kernels
 // store small results there directly, with no copy to queue behind other streams' work.
+// a device counter into the pinned host word (a kernel, not a D2H blit: see number_entries)
+__global__ void word_kernel(const unsigned long long* src, unsigned int* dst) { *dst = (unsigned int)min(*src, 0xFFFFFFFFull); }
+
 int pinned_word(unsigned int*& host, unsigned int*& dev, std::string& err) {
   thread_local struct Word {  // freed when the thread ends (streaming workers come and go)
     unsigned int* p = nullptr;
@@ -4941,7 +4947,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     // against 258 with exact sampled builds). FAC_LIVE_BUILD=1 brings them back (A/B).
     live_builds = P.beam && !counts && !e.has_map && qbuild <= 256 && diag_env("FAC_LIVE_BUILD") &&
                              !diag_env("FAC_NO_LIVE_BUILD");
-    ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", 4)));
+    ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", diag_env("FAC_RC_CT_ENTRIES") ? 4 : 2)));
     auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, hipStream_t bs, bool cleared = false,
                      bool sampled = false) -> int {
       SearchParams Q = P;
@@ -5036,11 +5042,13 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       }
       return FAC_OK;
     };
+    // n_size: the entries the table is sized for (the snapshots the build kept, when known)
     auto publish = [&](RcTable& T, uint32_t n_ent, const uint64_t* reps, DevBuf& ct, hipStream_t bs,
-                       bool cleared = false) -> int {
-      const uint32_t cs = ct_slots(n_ent);
+                       bool cleared = false, uint32_t n_size = 0xFFFFFFFFu) -> int {
+      if (n_size == 0xFFFFFFFFu) n_size = n_ent;
+      const uint32_t cs = ct_slots(n_size);
       if (!cleared) {
-        if (int crc = clear_ct(n_ent, ct, bs)) return crc;
+        if (int crc = clear_ct(n_size, ct, bs)) return crc;
       }
       hipLaunchKernelGGL(rc_publish_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_ent + 255) / 256, cus * 8))),
                          dim3(256), 0, bs, P, reps, static_cast<const uint4*>(P.rc_pool), T.off, T.count, n_ent, T.k,
@@ -5192,7 +5200,22 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       for (size_t x = 0; x < Lx.size(); ++x) {
         int brc = build(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), stream, false, true);
         if (brc) return brc;
-        if ((brc = publish(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), d_ct[1 + x], stream))) return brc;
+        // the lookup table is sized for the snapshots the build kept (C3: 5.9 M of 8.2 M 5-char entries,
+        // 0.6 M of 5.8 M 7-char ones), read back through the pinned word: tables 4x smaller to clear
+        // and to probe
+        uint32_t kept = n_entx[x];
+        if (!diag_env("FAC_RC_CT_ENTRIES")) {
+          unsigned int* w_host = nullptr;
+          unsigned int* w_dev = nullptr;
+          if (int hrc = pinned_word(w_host, w_dev, err)) return hrc;
+          hipLaunchKernelGGL(word_kernel, dim3(1), dim3(1), 0, stream, static_cast<const unsigned long long*>(d_cnt.p) + 11, w_dev);
+          HIP_TRY(hipGetLastError());
+          HIP_TRY(hipStreamSynchronize(stream));
+          const uint32_t got = *reinterpret_cast<volatile unsigned int*>(w_host);
+          kept = std::min<uint32_t>(kept, got);
+        }
+        if ((brc = publish(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), d_ct[1 + x], stream, false,
+                           kept))) return brc;
         tabs.push_back(Lx[x]);
         tab_exact.push_back(!live_builds);
       }
