@@ -3102,235 +3102,9 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
   }
 }
 
-// ---- Lane-serial cache builds of the sampled levels ----
-// A sampled level's build resumes each key's representative from its parent snapshot and pops only
-// the states of the key's last chars; most keys hold a few states, for which rc_build_kernel spends a
-// table clear, a snapshot load and whole 64-lane batches per key (C3: ~5.4 ns per key at every
-// level, the 7-char keys' mean queue being 0.1). Here every lane builds one key alone, in the
-// reference's sequential order, with the exact dedup of search.rs:617-627: the lane's states are a
-// linear array in LDS, so its popped states stay there for the dedup scans (a skipped pop is blanked),
-// and the parent's live dedup entries are scanned from the pool. A key whose parent queue or pushes
-// do not fit, whose pending count could beam, whose best list or parent dedup list is long, or that
-// has no parent snapshot is marked RC_DEFER and built by rc_build_kernel afterwards (rc_defer_only).
-// The snapshot written is the wave build's: header, queue, the live dedup entries (the union of the
-// parent's and the popped states', each key once with its stored penalty; the jcheck entries first)
-// and the best list.
+// A key a cache build leaves to a later build (rc_off): the small build variant defers the keys it
+// cannot hold to the full-size build (rc_defer_fail / rc_defer_only)
 constexpr uint32_t RC_DEFER = 0xFFFFFFFDu;
-constexpr uint32_t LB_NVMAX = 48;  // parent dedup entries a lane scans from the pool
-// diagnostics (FAC_RC_DEBUG): keys built, parent final, deferred: no parent / queue / best / dedup
-// entries / state not packable; bailed while running; pops of the built keys
-__device__ unsigned long long g_lb_dbg[8];
-template <uint32_t QB, uint32_t ELN>
-__global__ __launch_bounds__(64) void rc_lane_build_kernel(SearchParams P) {
-  __shared__ uint32_t s_q[3 * QB * 64];  // slot i of lane l at i * 64 + l: node, penalty, position word
-  uint4* s_e = P.ebuf + (size_t)blockIdx.x * P.ecap;  // best lists (this workgroup's emit slice)
-  const uint32_t lane = lane_id();
-  unsigned long long pool_cur = 0, pool_end = 0;  // wave-uniform: this wave's pool chunk
-  uint64_t popped_lane = 0;
-  unsigned err_all = 0;
-  for (;;) {
-    unsigned long long g0 = 0;
-    if (lane == 0) g0 = atomicAdd(P.counters + 7, 64ull);
-    g0 = shfl_u64(g0, 0);
-    if (g0 >= P.total_windows) break;
-    const uint64_t v = g0 + lane;
-    bool active = v < P.total_windows;
-    uint32_t status = 0;
-    SegDesc S{};
-    uint64_t start = 0;
-    RcHit hit{EMPTY, 0u, 0u, 0u, 0u};
-    if (active) {
-      const uint64_t wid = P.win_list[v];
-      const uint32_t kl = find_seg(P, wid);
-      S = P.segs[kl];
-      start = S.w_begin + (wid - P.seg_prefix[kl]);
-      hit = rc_lookup(P, S, start, 0xFFFFFFFFu);
-      if (hit.off != EMPTY && hit.tail == hit.head && !P.rc_keep_final) {  // the parent is final: uncached
-        P.rc_off[v] = EMPTY;
-        P.rc_count[v] = EMPTY;
-        active = false;
-      }
-    }
-    const uint32_t nq0 = active && hit.off != EMPTY ? hit.tail - hit.head : 0u;
-    const uint32_t nv0 = hit.nv_nel & 0xFFFFu, ne0 = hit.nv_nel >> 16;
-    if (P.lane_debug) {
-      const uint32_t c = !active ? 8u : hit.off == EMPTY ? 2u : nq0 > QB ? 3u : ne0 > ELN ? 4u : nv0 > LB_NVMAX ? 5u : 8u;
-      for (uint32_t k = 2; k < 6; ++k) {
-        const uint64_t m = __ballot(c == k);
-        if (m && lane == 0) atomicAdd(&g_lb_dbg[k], (unsigned long long)__popcll(m));
-      }
-    }
-    if (active && (hit.off == EMPTY || nq0 > QB || ne0 > ELN || nv0 > LB_NVMAX)) {
-      P.rc_off[v] = RC_DEFER;  // (count EMPTY until the wave build writes it)
-      P.rc_count[v] = EMPTY;
-      active = false;
-    }
-    uint32_t head = 0, tail = 0, nel = 0, pops = 0, jbeam = 0, jp1 = 0;
-    const uint4* pdv = nullptr;  // parent's live dedup entries
-    unsigned err = 0;
-    if (active) {
-      const uint4* src = P.rc_pool + hit.off + RC_HDR;
-      bool fits = true;
-      for (uint32_t i = 0; i < nq0; ++i) {
-        const uint4 q = src[i];
-        uint32_t w;
-        fits = lane_pack(q.y, q.w, w) && fits;
-        s_q[i * 64 + lane] = q.x;
-        s_q[QB * 64 + i * 64 + lane] = q.z;
-        s_q[2 * QB * 64 + i * 64 + lane] = w;
-      }
-      for (uint32_t i = 0; i < ne0; ++i) s_e[i * 64 + lane] = src[nq0 + nv0 + i];
-      pdv = src + nq0;
-      if (P.beam) {
-        const uint4 h1 = P.rc_pool[hit.off + 1];
-        jbeam = h1.z;
-        jp1 = h1.w;
-      }
-      tail = nq0;
-      nel = ne0;
-      status = fits ? LANE_RUN : LANE_BAIL;
-    }
-    while (__ballot(status == LANE_RUN)) {
-      if (status != LANE_RUN) continue;
-      if (head == tail) {
-        status = LANE_OK;
-        continue;
-      }
-      if (P.beam && tail - head > 2u * P.beam) {  // the beam would select here (:577-589)
-        status = LANE_BAIL;
-        continue;
-      }
-      const uint32_t slot = head * 64 + lane;
-      const uint32_t w0 = s_q[2 * QB * 64 + slot];
-      uint32_t jm0, pk0;
-      lane_unpack(w0, jm0, pk0);
-      if ((jm0 & 0xFFFFu) + 1u >= P.rc_k) {  // stop before the first state that reads past the key
-        status = LANE_OK;
-        continue;
-      }
-      const KState st{s_q[slot], jm0, __uint_as_float(s_q[QB * 64 + slot]), pk0};
-      ++head;
-      ++pops;
-      if (P.beam) jp1 = max(jp1, (jm0 & 0xFFFFu) + 1u);
-      // dedup (:617-627): skipped iff a stored entry of the same key holds a penalty <= its own; the
-      // stored penalty of a key is the smallest of the parent's entry and the popped states kept
-      bool skip = false;
-      for (uint32_t i = 0; i + 1 < head && !skip; ++i)
-        if (s_q[i * 64 + lane] == st.node && s_q[2 * QB * 64 + i * 64 + lane] == w0 &&
-            __uint_as_float(s_q[QB * 64 + i * 64 + lane]) <= st.pen)
-          skip = true;
-      for (uint32_t i = 0; i < nv0 && !skip; ++i) {
-        const uint4 e = pdv[i];
-        if (e.x == st.node && e.y == st.jm && e.w == st.packed && __uint_as_float(e.z) <= st.pen) skip = true;
-      }
-      if (skip) {
-        s_q[slot] = EMPTY;  // not a stored entry
-        continue;
-      }
-      lane_expand<QB, ELN, true>(P, s_q, s_e, S, start, st, status, head, tail, nel, err);
-      if (err) status = LANE_BAIL;
-    }
-    // epilogue: the snapshot of every lane that finished
-    const bool fin = status == LANE_OK;
-    if (P.lane_debug) {
-      const uint64_t mf = __ballot(fin), mb = __ballot(status == LANE_BAIL);
-      if (lane == 0) {
-        atomicAdd(&g_lb_dbg[0], (unsigned long long)__popcll(mf));
-        atomicAdd(&g_lb_dbg[6], (unsigned long long)__popcll(mb));
-      }
-    }
-    if (status == LANE_BAIL) {
-      P.rc_off[v] = RC_DEFER;
-      P.rc_count[v] = EMPTY;
-    }
-    popped_lane += fin ? pops : 0u;
-    uint32_t jmin = 0xFFFFu;
-    for (uint32_t i = head; i < tail; ++i) jmin = min(jmin, s_q[2 * QB * 64 + i * 64 + lane] & 0xFFu);
-    // live dedup entries: kept popped states not superseded by a later kept pop of the same key, and
-    // the parent's entries whose key no kept pop has
-    auto popped_live = [&](uint32_t i) -> bool {
-      const uint32_t n = s_q[i * 64 + lane], w = s_q[2 * QB * 64 + i * 64 + lane];
-      if (n == EMPTY || (w & 0xFFu) < jmin) return false;
-      for (uint32_t k = i + 1; k < head; ++k)
-        if (s_q[k * 64 + lane] == n && s_q[2 * QB * 64 + k * 64 + lane] == w) return false;
-      return true;
-    };
-    auto parent_live = [&](const uint4& e) -> bool {
-      if ((e.y & 0xFFFFu) < jmin) return false;
-      uint32_t w;
-      if (!lane_pack(e.y, e.w, w)) return true;  // no popped state can equal it
-      for (uint32_t k = 0; k < head; ++k)
-        if (s_q[k * 64 + lane] == e.x && s_q[2 * QB * 64 + k * 64 + lane] == w) return false;
-      return true;
-    };
-    uint32_t nv = 0, jlive = 0;
-    if (fin) {
-      for (uint32_t i = 0; i < head; ++i)
-        if (popped_live(i)) {
-          ++nv;
-          jlive = max(jlive, (s_q[2 * QB * 64 + i * 64 + lane] & 0xFFu) + 1u);
-        }
-      for (uint32_t i = 0; i < nv0; ++i) {
-        const uint4 e = pdv[i];
-        if (parent_live(e)) {
-          ++nv;
-          jlive = max(jlive, (e.y & 0xFFFFu) + 1u);
-        }
-      }
-    }
-    const uint32_t nq = tail - head;
-    bool bad = fin && (nel > P.rc_emax || nv > P.rc_vmax);
-    const uint32_t words = (fin && !bad) ? RC_HDR + nq + nv + nel : 0u;
-    // snapshots carved from the wave's pool chunk (one pool atomic per chunk)
-    const uint32_t incl = wave_inclusive_sum(words), tot = shfl_u32(incl, 63);
-    if (tot && pool_cur + tot > pool_end) {
-      const unsigned long long want = max((unsigned long long)tot, (unsigned long long)P.rc_pool_chunk);
-      unsigned long long c = 0;
-      if (lane == 0) c = atomicAdd(P.rc_pool_used, want);
-      pool_cur = shfl_u64(c, 0);
-      pool_end = pool_cur + want;
-    }
-    const unsigned long long off = pool_cur + incl - words;
-    pool_cur += tot;
-    if (fin) {
-      bad = bad || off + words > P.rc_pool_cap || off > 0xFFFFFFF0ull;
-      if (!bad) {
-        uint4* dst = P.rc_pool + off + RC_HDR;
-        for (uint32_t i = 0; i < nq; ++i) {
-          const uint32_t sl = (head + i) * 64 + lane;
-          uint32_t jm, pk;
-          lane_unpack(s_q[2 * QB * 64 + sl], jm, pk);
-          dst[i] = make_uint4(s_q[sl], jm, s_q[QB * 64 + sl], pk);
-        }
-        const uint32_t jcheck = min(jlive, jbeam);
-        uint32_t at = 0, ncheck = 0;
-        for (uint32_t pass = 0; pass < 2; ++pass) {  // the entries with j < jcheck first
-          for (uint32_t i = 0; i < head; ++i) {
-            const uint32_t sl = i * 64 + lane, w = s_q[2 * QB * 64 + sl];
-            if (((w & 0xFFu) + 1u <= jcheck) != (pass == 0) || !popped_live(i)) continue;
-            uint32_t jm, pk;
-            lane_unpack(w, jm, pk);
-            dst[nq + at++] = make_uint4(s_q[sl], jm, s_q[QB * 64 + sl], pk);
-          }
-          for (uint32_t i = 0; i < nv0; ++i) {
-            const uint4 e = pdv[i];
-            if (((e.y & 0xFFFFu) + 1u <= jcheck) != (pass == 0) || !parent_live(e)) continue;
-            dst[nq + at++] = e;
-          }
-          if (pass == 0) ncheck = at;
-        }
-        for (uint32_t i = 0; i < nel; ++i) dst[nq + nv + i] = s_e[i * 64 + lane];
-        P.rc_pool[off] = make_uint4(hit.head + head, hit.tail + (tail - nq0), nv, pops + hit.pops);
-        P.rc_pool[off + 1] = make_uint4(nel, ncheck ? (jcheck | (ncheck << 16)) : 0u, jbeam, jp1);
-      }
-      P.rc_off[v] = bad ? EMPTY : (uint32_t)off;
-      P.rc_count[v] = bad ? EMPTY : nq;
-    }
-    err_all |= err & ~(ERR_QUEUE | ERR_VISITED | ERR_EMIT);
-  }
-  wave_add_counter(P.counters + 1, popped_lane);
-  (void)err_all;
-}
 
 // LK: the window prologue looks snapshots up itself (cache builds); otherwise a main pass with the
 // prefix cache reads the hits rc_lookup_kernel stored.
@@ -4994,33 +4768,13 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         HIP_TRY(hipGetLastError());
       }
       const bool live_build = live_builds && sampled && Q.rc_ntab > 0;
-      // sampled levels: the lane-serial build first (rc_lane_build_kernel), the wave build then takes
-      // the keys it deferred
-      const bool lane_build = sampled && !live_build && Q.rc_ntab > 0 && diag_env("FAC_LANE_BUILD");  // A/B: slower so far
       Q.rc_defer_only = 0;
-      if (lane_build) {
-        const uint32_t lg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_ent + 63) / 64, (uint64_t)max_grid));
-        Q.lane_debug = diag_env("FAC_RC_DEBUG") ? 1 : 0;
-        hipLaunchKernelGGL((rc_lane_build_kernel<32, 8>), dim3(lg), dim3(64), 0, bs, Q);
-        HIP_TRY(hipGetLastError());
-        if (Q.lane_debug) {
-          unsigned long long d[8];
-          HIP_TRY(hipStreamSynchronize(bs));
-          HIP_TRY(hipMemcpyFromSymbol(d, HIP_SYMBOL(g_lb_dbg), sizeof(d)));
-          std::fprintf(stderr, "FAC_LB k=%u keys=%u built=%llu deferred: no-parent %llu queue %llu best %llu dedup %llu bailed %llu\n",
-                       T.k, n_ent, d[0], d[2], d[3], d[4], d[5], d[6]);
-          std::memset(d, 0, sizeof(d));
-          HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_lb_dbg), d, sizeof(d)));
-        }
-        HIP_TRY(hipMemsetAsync(Q.counters + 7, 0, sizeof(unsigned long long), bs));  // the wave build's work counter
-        Q.rc_defer_only = 1;
-      }
       uint32_t qk = 256;  // launch_rc_build's ring
       while (qk < qbuild) qk <<= 1;
       if (int src = prep_slots(Q, bs, qk, !live_build)) return src;
       if (live_build) {
         hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
-      } else if ((sampled || (T.k == L1.k && diag_env("FAC_BUILD_SMALL_L1"))) && qbuild <= 256 && !lane_build &&
+      } else if ((sampled || (T.k == L1.k && diag_env("FAC_BUILD_SMALL_L1"))) && qbuild <= 256 &&
                  !diag_env("FAC_NO_BUILD_SMALL")) {
         // the sampled levels' keys pop few states and their builds wait on memory: the small variant
         // (16 waves per CU) first, then the full-size build takes the keys it could not hold

@@ -397,6 +397,29 @@ def test_prefix_cache_two_levels_c3_slice(k2, monkeypatch):
     assert len(on) > 0 and sorted(on.tolist()) == sorted(off.tolist()) == sorted(one.tolist())
 
 
+@pytest.mark.parametrize("knobs", [{}, {"FAC_NO_BUILD_SMALL": "1"}, {"FAC_BUILD_SMALL_L1": "1"},
+                                   {"FAC_RC_DEEPEST": "1", "FAC_RC_CT_ENTRIES": "1"}],
+                         ids=["default", "no-small-build", "small-build-l1", "deepest-first"])
+def test_prefix_cache_round4_paths_c3_slice(knobs, monkeypatch):
+    """Round-4 prefix-cache paths on a C3-shaped haystack with the sampled levels on: the small build
+    variant and the full-size build of the keys it defers (default), the full-size build alone, the
+    small variant for level 1 too, and the round-3 probe order with entry-sized tables: identical
+    records to the cache off, and the deeper levels replaying pops."""
+    from fuzzy_aho_corasick import workloads
+    w = workloads.config("c3", 2 << 20, 3)
+    staged = workloads.builder_for(w).build(w.patterns).stage(w.haystack)
+    monkeypatch.setenv("FAC_RC_MIN2", "1")
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    on, st_on = staged.search_windows_records(w.threshold)
+    monkeypatch.setenv("FAC_RC_K2", "0")
+    one, st_one = staged.search_windows_records(w.threshold)
+    monkeypatch.setenv("FAC_NO_RC", "1")
+    off, _ = staged.search_windows_records(w.threshold)
+    assert st_on.states_cached > st_one.states_cached > 0
+    assert len(on) > 0 and sorted(on.tolist()) == sorted(off.tolist()) == sorted(one.tolist())
+
+
 @pytest.mark.parametrize("demand,levels", [("6", "5"), ("7", "5,6"), ("8", "5,7")])
 def test_prefix_cache_demand_level_c3_slice(demand, levels, monkeypatch):
     """The demand level (keys counted over the windows still open after the lookups and the lane
