@@ -2397,15 +2397,10 @@ __global__ __launch_bounds__(256) void rc_publish_kernel(SearchParams P, const u
 // (a count of c then means c + 1 sightings; bitmap collisions only admit a few singletons). A key
 // that finds no slot within `probes` stays uncounted (not cached).
 // One level's count table (rc_count_kernel): keys of k chars, open addressing with `probes` slots
-// A count-table slot: the key, its count and its representative window together, so an insert
-// touches one line (round 3 kept three arrays: three random lines per insert, 69 GB per C3 step)
-struct alignas(16) RcCountSlot {
-  unsigned long long key;  // 0: empty
-  uint32_t cnt;
-  uint32_t rep;            // virtual window id (< 2^32: a haystack has at most u32::MAX graphemes)
-};
 struct RcCountTarget {
-  RcCountSlot* slots;
+  unsigned long long* keys;
+  uint32_t* cnt;
+  uint64_t* rep;
   uint32_t mask;
   uint32_t k;  // 0: no table
 };
@@ -2413,18 +2408,18 @@ __device__ __forceinline__ void rc_count_insert(const RcCountTarget& T, uint64_t
                                                 uint32_t probes) {
   const uint32_t h = rc_hash(k);
   for (uint32_t p = 0; p < probes; ++p) {
-    RcCountSlot* e = T.slots + ((h + p) & T.mask);
-    unsigned long long kk = e->key;
+    const uint32_t slot = (h + p) & T.mask;
+    unsigned long long kk = T.keys[slot];
     if (kk == 0ull) {
-      kk = atomicCAS(&e->key, 0ull, (unsigned long long)k);
+      kk = atomicCAS(&T.keys[slot], 0ull, (unsigned long long)k);
       if (kk == 0ull) {
-        e->rep = (uint32_t)vid;
-        atomicAdd(&e->cnt, 1u);
+        T.rep[slot] = vid;
+        atomicAdd(&T.cnt[slot], 1u);
         return;
       }
     }
     if (kk == k) {  // sat == 1 (level 1 keeps every key): the inserter's count is all it needs
-      if (sat > 1u && e->cnt < sat) atomicAdd(&e->cnt, 1u);
+      if (sat > 1u && T.cnt[slot] < sat) atomicAdd(&T.cnt[slot], 1u);
       return;
     }
   }
@@ -2478,18 +2473,19 @@ __global__ __launch_bounds__(256) void rc_derive_kernel(SearchParams P, const ui
 // (one same-address atomic per selected wave serialises at one L2 channel): per-block counts over
 // contiguous slot ranges, an exclusive scan of the block counts, then the assignment. Every other
 // slot maps to EMPTY (not cached: the lookup falls through to the next level).
-__device__ __forceinline__ bool rc_selected(const RcCountSlot* slots, uint32_t s, uint32_t thr) {
-  const RcCountSlot e = slots[s];
-  return e.key != 0ull && e.cnt >= thr;
+__device__ __forceinline__ bool rc_selected(const unsigned long long* keys, const uint32_t* cnt, uint32_t s,
+                                            uint32_t thr) {
+  return keys[s] != 0ull && cnt[s] >= thr;
 }
-__global__ __launch_bounds__(64) void rc_sel_count_kernel(const RcCountSlot* slots, uint32_t n_slots, uint32_t range,
-                                                           uint32_t thr, uint32_t* bcount) {
+__global__ __launch_bounds__(64) void rc_sel_count_kernel(const unsigned long long* keys, const uint32_t* cnt,
+                                                           uint32_t n_slots, uint32_t range, uint32_t thr,
+                                                           uint32_t* bcount) {
   __shared__ uint32_t tot;
   if (threadIdx.x == 0) tot = 0;
   __syncthreads();
   const uint32_t b0 = blockIdx.x * range, b1 = min(b0 + range, n_slots);
   uint32_t c = 0;
-  for (uint32_t s = b0 + threadIdx.x; s < b1; s += blockDim.x) c += rc_selected(slots, s, thr) ? 1u : 0u;
+  for (uint32_t s = b0 + threadIdx.x; s < b1; s += blockDim.x) c += rc_selected(keys, cnt, s, thr) ? 1u : 0u;
   c = wave_inclusive_sum(c);
   if (lane_id() == 63) atomicAdd(&tot, c);
   __syncthreads();
@@ -2512,26 +2508,35 @@ __global__ __launch_bounds__(64) void rc_sel_scan_kernel(uint32_t* bcount, uint3
     run += v;
   }
 }
-// rep[entry] = the selected slot's representative window, entries numbered in slot order
-__global__ __launch_bounds__(64) void rc_sel_assign_kernel(const RcCountSlot* slots, uint64_t* rep, const uint32_t* bbase,
-                                                            uint32_t n_slots, uint32_t range, uint32_t thr,
-                                                            uint32_t max_ent) {
+// counts are read and replaced by entries in place (val may alias cnt: a slot is only touched by
+// its own thread); rep[entry] = the slot's representative window
+__global__ __launch_bounds__(64) void rc_sel_assign_kernel(const unsigned long long* keys, const uint32_t* cnt,
+                                                            const uint64_t* rep_slot, uint32_t* val, uint64_t* rep,
+                                                            const uint32_t* bbase, uint32_t n_slots, uint32_t range,
+                                                            uint32_t thr, uint32_t max_ent) {
   __shared__ uint32_t run;
   if (threadIdx.x == 0) run = bbase[blockIdx.x];
   __syncthreads();
   const uint32_t b0 = blockIdx.x * range, b1 = min(b0 + range, n_slots);
   for (uint32_t s0 = b0; s0 < b1; s0 += blockDim.x) {
     const uint32_t s = s0 + threadIdx.x;
-    const bool sel = s < b1 && rc_selected(slots, s, thr);
+    const bool sel = s < b1 && rc_selected(keys, cnt, s, thr);
     const uint64_t m = __ballot(sel);
     uint32_t base = 0;
     if (m) {
       if (lane_id() == (uint32_t)first_lane(m)) base = atomicAdd(&run, (uint32_t)__popcll(m));  // LDS
       base = shfl_u32(base, first_lane(m));
     }
-    if (sel) {
-      const uint32_t ent = base + prefix_below(m);
-      if (ent < max_ent) rep[ent] = slots[s].rep;
+    if (s < b1) {
+      uint32_t v = EMPTY;
+      if (sel) {
+        const uint32_t ent = base + prefix_below(m);
+        if (ent < max_ent) {
+          rep[ent] = rep_slot[s];
+          v = ent;
+        }
+      }
+      val[s] = v;
     }
   }
 }
@@ -4544,7 +4549,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   uint64_t ct_mult = 4;
   std::function<int(const RcTable&, uint32_t, const uint64_t*, hipStream_t, bool, bool)> rc_build_fn;
   std::function<int(RcTable&, uint32_t, const uint64_t*, DevBuf&, hipStream_t, bool)> rc_publish_fn;
-  std::function<int(const DevBuf&, const DevBuf&, uint32_t, uint32_t, uint32_t, unsigned int&)> rc_number_fn;
+  std::function<int(const DevBuf&, const DevBuf&, const DevBuf&, const DevBuf&, uint32_t, uint32_t, uint32_t, unsigned int&)>
+      rc_number_fn;
   // after its build a level's entries are published into an exact-key lookup table (4 slots per
   // entry: a miss usually ends at the first probe)
   auto ct_slots = [&](uint32_t n_ent) {
@@ -4576,12 +4582,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     const uint32_t l1_log2 = (uint32_t)std::min<uint64_t>(24, std::max<uint64_t>(12, env_u("FAC_RC_SLOTS1", 24)));
     uint32_t slots = 1u << 12;
     while (slots < 4ull * max_ent && slots < (1u << l1_log2)) slots <<= 1;
-    HIP_TRY(d_rck.alloc(slots * sizeof(RcCountSlot), stream));
+    HIP_TRY(d_rck.alloc(slots * sizeof(unsigned long long), stream));
+    HIP_TRY(d_rcv.alloc(slots * sizeof(uint32_t), stream));  // key counts, then entries
+    HIP_TRY(d_rcslot.alloc(slots * sizeof(uint64_t), stream));
     HIP_TRY(d_rcb.alloc(8192 * sizeof(uint32_t), stream));
     HIP_TRY(d_rcrep.alloc(max_ent * sizeof(uint64_t), stream));
     HIP_TRY(d_rcc.alloc(2 * (size_t)max_ent * sizeof(uint32_t), stream));  // counts, then offsets
     HIP_TRY(d_rcn.alloc(4 * sizeof(unsigned long long), stream));  // keys, pool words used, level-2 entries
-    L1 = RcTable{0u, slots - 1, nullptr, nullptr,
+    L1 = RcTable{0u, slots - 1, static_cast<const unsigned long long*>(d_rck.p), static_cast<const uint32_t*>(d_rcv.p),
                  static_cast<uint32_t*>(d_rcc.p) + max_ent, static_cast<uint32_t*>(d_rcc.p)};
     P.rc_pool_used = static_cast<unsigned long long*>(d_rcn.p) + 1;
     HIP_TRY(hipEventRecord(ev.a, stream));
@@ -4590,8 +4598,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
 
     // keys counted >= thr -> entries 0..n-1 (slot counts replaced by entries in place), reps by entry;
     // returns n (all selected keys; entries past max_ent stay uncached)
-    auto number_entries = [&](const DevBuf& cslots, const DevBuf& rep, uint32_t n_slots, uint32_t thr, uint32_t cap,
-                              unsigned int& n) -> int {
+    auto number_entries = [&](const DevBuf& keys, const DevBuf& cv, const DevBuf& rslot, const DevBuf& rep,
+                              uint32_t n_slots, uint32_t thr, uint32_t cap, unsigned int& n) -> int {
       const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(8192, n_slots / 4096));
       const uint32_t range = (n_slots + nb - 1) / nb;  // n_slots and nb are powers of two: a multiple of 256
       // the count comes back through pinned host memory written by the scan kernel: a 4-byte D2H copy
@@ -4601,10 +4609,13 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (int hrc = pinned_word(n_host, n_dev, err)) return hrc;
       *reinterpret_cast<volatile unsigned int*>(n_host) = 0u;
       // single-wave workgroups throughout (see rc_sel_scan_kernel)
-      hipLaunchKernelGGL(rc_sel_count_kernel, dim3(nb), dim3(64), 0, stream, static_cast<const RcCountSlot*>(cslots.p),
-                         n_slots, range, thr, static_cast<uint32_t*>(d_rcb.p));
+      hipLaunchKernelGGL(rc_sel_count_kernel, dim3(nb), dim3(64), 0, stream,
+                         static_cast<const unsigned long long*>(keys.p), static_cast<const uint32_t*>(cv.p), n_slots,
+                         range, thr, static_cast<uint32_t*>(d_rcb.p));
       hipLaunchKernelGGL(rc_sel_scan_kernel, dim3(1), dim3(64), 0, stream, static_cast<uint32_t*>(d_rcb.p), nb, n_dev);
-      hipLaunchKernelGGL(rc_sel_assign_kernel, dim3(nb), dim3(64), 0, stream, static_cast<const RcCountSlot*>(cslots.p),
+      hipLaunchKernelGGL(rc_sel_assign_kernel, dim3(nb), dim3(64), 0, stream,
+                         static_cast<const unsigned long long*>(keys.p), static_cast<const uint32_t*>(cv.p),
+                         static_cast<const uint64_t*>(rslot.p), static_cast<uint32_t*>(cv.p),
                          static_cast<uint64_t*>(rep.p), static_cast<const uint32_t*>(d_rcb.p), n_slots, range, thr, cap);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipStreamSynchronize(stream));
@@ -4620,8 +4631,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     RcTable L0{0u, 0u, nullptr, nullptr, nullptr, nullptr};
     n_ent0 = 0;
     const bool want_l0 = !diag_env("FAC_NO_RC_L0");
-    auto target = [](const DevBuf& cslots, uint32_t n_slots, uint32_t k) {
-      return RcCountTarget{static_cast<RcCountSlot*>(cslots.p), n_slots - 1, k};
+    auto target = [](const DevBuf& keys, const DevBuf& cnt, const DevBuf& rep, uint32_t n_slots, uint32_t k) {
+      return RcCountTarget{static_cast<unsigned long long*>(keys.p), static_cast<uint32_t*>(cnt.p),
+                           static_cast<uint64_t*>(rep.p), n_slots - 1, k};
     };
     // Level-1 keys are counted on every stride1-th window, about 32 M windows in all (a power of two,
     // at most 16): a key that only unsampled windows hold stays uncached, and its windows resume from
@@ -4633,22 +4645,26 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     stride1 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_STRIDE1", stride1));
     for (uint32_t k = kpin ? kpin : 4u; k >= (kpin ? kpin : 2u); --k) {
       P.rc_k = k;
-      HIP_TRY(hipMemsetAsync(d_rck.p, 0, slots * sizeof(RcCountSlot), stream));
+      HIP_TRY(hipMemsetAsync(d_rck.p, 0, slots * sizeof(unsigned long long), stream));
+      HIP_TRY(hipMemsetAsync(d_rcv.p, 0, slots * sizeof(uint32_t), stream));
       const uint32_t k0 = std::max<uint64_t>(2, std::min<uint64_t>(k - 1, env_u("FAC_RC_L0K", k - 1)));  // knob: A/B
       const bool l0 = want_l0 && k >= 3 && L0.k == 0;  // the first key length only
-      RcCountTarget t1{nullptr, 0u, 0u};
+      RcCountTarget t1{nullptr, nullptr, nullptr, 0u, 0u};
       if (l0) {
-        HIP_TRY(d_l0k.alloc(slots * sizeof(RcCountSlot), stream));
-        HIP_TRY(hipMemsetAsync(d_l0k.p, 0, slots * sizeof(RcCountSlot), stream));
-        t1 = target(d_l0k, slots, k0);
+        HIP_TRY(d_l0k.alloc(slots * sizeof(unsigned long long), stream));
+        HIP_TRY(d_l0v.alloc(slots * sizeof(uint32_t), stream));
+        HIP_TRY(d_l0slot.alloc(slots * sizeof(uint64_t), stream));
+        HIP_TRY(hipMemsetAsync(d_l0k.p, 0, slots * sizeof(unsigned long long), stream));
+        HIP_TRY(hipMemsetAsync(d_l0v.p, 0, slots * sizeof(uint32_t), stream));
+        t1 = target(d_l0k, d_l0v, d_l0slot, slots, k0);
         L0.k = k0;
       }
-      hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P, target(d_rck, slots, k),
-                         RcCountTarget{nullptr, 0u, 0u}, RcCountTarget{nullptr, 0u, 0u},
+      hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P, target(d_rck, d_rcv, d_rcslot, slots, k),
+                         RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u}, RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u},
                          stride1, 1u, nullptr, 0u, cprobes);
       HIP_TRY(hipGetLastError());
       unsigned int n_keys = 0;
-      if (int nrc = number_entries(d_rck, d_rcrep, slots, 1u, max_ent, n_keys)) return nrc;
+      if (int nrc = number_entries(d_rck, d_rcv, d_rcslot, d_rcrep, slots, 1u, max_ent, n_keys)) return nrc;
       l1_keys = n_keys;
       if (n_keys == 0) break;
       if (!kpin && 8ull * n_keys > (windows + stride1 - 1) / stride1) continue;  // too little reuse: fewer chars per key
@@ -4663,9 +4679,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         HIP_TRY(d_l0rep.alloc(max_ent0 * sizeof(uint64_t), stream));
         HIP_TRY(d_l0c.alloc(2 * (size_t)max_ent0 * sizeof(uint32_t), stream));
         unsigned int n0 = 0;
-        if (int nrc = number_entries(d_l0k, d_l0rep, slots, 1u, max_ent0, n0)) return nrc;
+        if (int nrc = number_entries(d_l0k, d_l0v, d_l0slot, d_l0rep, slots, 1u, max_ent0, n0)) return nrc;
         n_ent0 = std::min(n0, max_ent0);
-        L0 = RcTable{k0, slots - 1, nullptr, nullptr, static_cast<uint32_t*>(d_l0c.p) + max_ent0,
+        L0 = RcTable{k0, slots - 1, static_cast<const unsigned long long*>(d_l0k.p),
+                     static_cast<const uint32_t*>(d_l0v.p), static_cast<uint32_t*>(d_l0c.p) + max_ent0,
                      static_cast<uint32_t*>(d_l0c.p)};
       }
       break;
@@ -4915,10 +4932,13 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       for (uint32_t k2 : ks)
         if (k2 > L1.k) kk.push_back(k2);
       for (size_t x = 0; x < kk.size(); ++x) {  // every level's tables cleared before the level-1 build
-        HIP_TRY(d_xk[x].alloc(slots2 * sizeof(RcCountSlot), stream));
+        HIP_TRY(d_xk[x].alloc(slots2 * sizeof(unsigned long long), stream));
+        HIP_TRY(d_xv[x].alloc(slots2 * sizeof(uint32_t), stream));  // sample counts, then entries
+        HIP_TRY(d_xslot[x].alloc(slots2 * sizeof(uint64_t), stream));
         HIP_TRY(d_xrep[x].alloc(max_ent2 * sizeof(uint64_t), stream));
         HIP_TRY(d_xc[x].alloc(2 * (size_t)max_ent2 * sizeof(uint32_t), stream));
-        HIP_TRY(hipMemsetAsync(d_xk[x].p, 0, slots2 * sizeof(RcCountSlot), stream));
+        HIP_TRY(hipMemsetAsync(d_xk[x].p, 0, slots2 * sizeof(unsigned long long), stream));
+        HIP_TRY(hipMemsetAsync(d_xv[x].p, 0, slots2 * sizeof(uint32_t), stream));
       }
       if (int lrc = launch_l1()) return lrc;
       for (size_t x = 0; x < kk.size(); ++x) {
@@ -4928,21 +4948,22 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         // first one's numbering and held the sampled builds back behind the level-1 build (C3, r03aj)
         if (seen || x % 3 == 0) {
           if (seen) HIP_TRY(hipMemsetAsync(seen, 0, ((size_t)seen_mask + 1) / 8, stream));
-          const RcCountTarget none{nullptr, 0u, 0u};
+          const RcCountTarget none{nullptr, nullptr, nullptr, 0u, 0u};
           const RcCountTarget t1 = (!seen && x + 1 < kk.size())
-                                       ? target(d_xk[x + 1], slots2, kk[x + 1]) : none;
+                                       ? target(d_xk[x + 1], d_xv[x + 1], d_xslot[x + 1], slots2, kk[x + 1]) : none;
           const RcCountTarget t2 = (!seen && x + 2 < kk.size())
-                                       ? target(d_xk[x + 2], slots2, kk[x + 2]) : none;
+                                       ? target(d_xk[x + 2], d_xv[x + 2], d_xslot[x + 2], slots2, kk[x + 2]) : none;
           hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid2), dim3(256), 0, stream, P,
-                             target(d_xk[x], slots2, k2), t1, t2, stride2, thr_t, seen, seen_mask,
+                             target(d_xk[x], d_xv[x], d_xslot[x], slots2, k2), t1, t2, stride2, thr_t, seen, seen_mask,
                              cprobes);
           HIP_TRY(hipGetLastError());
         }
         unsigned int nk2 = 0;
-        if (int nrc = number_entries(d_xk[x], d_xrep[x], slots2, thr_t, max_ent2, nk2)) return nrc;
+        if (int nrc = number_entries(d_xk[x], d_xv[x], d_xslot[x], d_xrep[x], slots2, thr_t, max_ent2, nk2)) return nrc;
         const uint32_t ne = std::min(nk2, max_ent2);
         if (ne == 0) continue;
-        Lx.push_back(RcTable{k2, slots2 - 1, nullptr, nullptr, static_cast<uint32_t*>(d_xc[x].p) + max_ent2,
+        Lx.push_back(RcTable{k2, slots2 - 1, static_cast<const unsigned long long*>(d_xk[x].p),
+                             static_cast<const uint32_t*>(d_xv[x].p), static_cast<uint32_t*>(d_xc[x].p) + max_ent2,
                              static_cast<uint32_t*>(d_xc[x].p)});
         n_entx.push_back(ne);
         xbuf.push_back(x);
@@ -5074,21 +5095,26 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     uint32_t slots_d = 1u << 12;
     while (slots_d < std::min<uint64_t>(windows / 2, 1ull << 26)) slots_d <<= 1;
     const uint32_t max_entd = std::min<uint32_t>(slots_d / 2, 16u << 20);
-    HIP_TRY(d_xk[xi].alloc(slots_d * sizeof(RcCountSlot), stream));
+    HIP_TRY(d_xk[xi].alloc(slots_d * sizeof(unsigned long long), stream));
+    HIP_TRY(d_xv[xi].alloc(slots_d * sizeof(uint32_t), stream));
+    HIP_TRY(d_xslot[xi].alloc(slots_d * sizeof(uint64_t), stream));
     HIP_TRY(d_xrep[xi].alloc(max_entd * sizeof(uint64_t), stream));
     HIP_TRY(d_xc[xi].alloc(2 * (size_t)max_entd * sizeof(uint32_t), stream));
     HIP_TRY(hipEventRecord(ev.a, stream));
-    HIP_TRY(hipMemsetAsync(d_xk[xi].p, 0, slots_d * sizeof(RcCountSlot), stream));
+    HIP_TRY(hipMemsetAsync(d_xk[xi].p, 0, slots_d * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync(d_xv[xi].p, 0, slots_d * sizeof(uint32_t), stream));
     const uint64_t n_reg = P.total_windows / RC_REGION;
     const uint32_t rgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_reg + 3) / 4, (uint64_t)cus * 8));
     hipLaunchKernelGGL(rc_count_open_kernel, dim3(rgrid), dim3(256), 0, stream, P,
-                       RcCountTarget{static_cast<RcCountSlot*>(d_xk[xi].p), slots_d - 1, demand_k});
+                       RcCountTarget{static_cast<unsigned long long*>(d_xk[xi].p), static_cast<uint32_t*>(d_xv[xi].p),
+                                     static_cast<uint64_t*>(d_xslot[xi].p), slots_d - 1, demand_k});
     HIP_TRY(hipGetLastError());
     unsigned int nk = 0;
-    if (int nrc = rc_number_fn(d_xk[xi], d_xrep[xi], slots_d, 2u, max_entd, nk)) return nrc;
+    if (int nrc = rc_number_fn(d_xk[xi], d_xv[xi], d_xslot[xi], d_xrep[xi], slots_d, 2u, max_entd, nk)) return nrc;
     demand_keys = std::min(nk, max_entd);
     if (demand_keys == 0) return FAC_OK;
-    RcTable D{demand_k, slots_d - 1, nullptr, nullptr, static_cast<uint32_t*>(d_xc[xi].p) + max_entd,
+    RcTable D{demand_k, slots_d - 1, static_cast<const unsigned long long*>(d_xk[xi].p),
+              static_cast<const uint32_t*>(d_xv[xi].p), static_cast<uint32_t*>(d_xc[xi].p) + max_entd,
               static_cast<uint32_t*>(d_xc[xi].p)};
     build_cnt = N_COUNTERS;  // the pass's counters hold its records so far
     int brc = rc_build_fn(D, demand_keys, static_cast<const uint64_t*>(d_xrep[xi].p), stream, false, true);

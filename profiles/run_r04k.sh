@@ -7,8 +7,6 @@ cd "$ROOT"
 OUT=$ROOT/gpurun_out/r04k
 mkdir -p "$OUT"
 L=$ROOT/fuzzy-aho-corasick-rs_amd/fuzzy_aho_corasick/_lib
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_golden.py tests/test_gpu_fullsize.py -x -q --timeout 500 --timeout-method thread -k "prefix_cache or lane_serial or dedup_free or differential_random or golden or c3" > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
-tail -2 "$OUT/pytest.log"
 for v in old new old new; do
   lib=$L/libfac.so; [ $v = old ] && lib=$L/libfac_r04a.so
   FAC_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-fresh-diag > "$OUT/b_$v.json" 2> "$OUT/b_$v.err"
@@ -23,6 +21,3 @@ for v in old new; do
   rm -rf "$OUT/kt_$v"
   echo "== $v"; grep -E "rc_build|rc_count_kernel|lookup|lane_window|bfs_window" "$OUT/timeline_$v.txt"
 done
-cd "$ROOT"
-BENCH_ARGS="--no-fresh-diag" bash profiles/ab_knobs.sh r04k_v "X=0" "FAC_BUILD_SMALL_L1=1" "FAC_NO_BUILD_SMALL=1"
-BENCH_ARGS="--vocab 0 --no-fresh-diag" bash profiles/ab_knobs.sh r04k_f "X=0" "FAC_BUILD_SMALL_L1=1" "FAC_RC_K2=0"
