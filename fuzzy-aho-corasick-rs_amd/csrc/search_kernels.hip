@@ -3464,8 +3464,10 @@ void rc_build_kernel(SearchParams P) {
 }
 // a smaller build variant (256-entry dedup table, 10 KB of LDS: up to 16 waves per CU, held to 128
 // VGPRs) for the sampled levels, whose keys pop few states: their builds wait on memory, not issue.
-// A key it cannot hold (ring or table full) is deferred to the full-size build. C3 per step: 187.2 ->
-// 174.6 ms (prefix cache 128.3 -> 115.8), fresh words 547.4 -> 506.1 (profiles/r04i; FAC_NO_BUILD_SMALL: A/B)
+// A key it cannot hold (ring or table full) is deferred to the full-size build. Opt-in (FAC_BUILD_SMALL):
+// it won only against full-size builds slowed by a scratch frame (profiles/r04i); against the fixed
+// ones it loses (C3 158.2 vs 142.2 ms per step, profiles/r04m: its spills and the deferred keys' second
+// build cost more than the occupancy gains)
 #ifndef FAC_SMALL_BUILD_WAVES
 #define FAC_SMALL_BUILD_WAVES 4
 #endif
@@ -4792,7 +4794,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (live_build) {
         hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
       } else if ((sampled || (T.k == L1.k && diag_env("FAC_BUILD_SMALL_L1"))) && qbuild <= 256 &&
-                 !diag_env("FAC_NO_BUILD_SMALL")) {
+                 diag_env("FAC_BUILD_SMALL")) {
         // the sampled levels' keys pop few states and their builds wait on memory: the small variant
         // (16 waves per CU) first, then the full-size build takes the keys it could not hold
         Q.rc_defer_fail = 1;
