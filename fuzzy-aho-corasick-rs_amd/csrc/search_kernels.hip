@@ -1762,8 +1762,7 @@ template <uint32_t VCAP, uint32_t QCAP, bool MAP, bool LIVE = false>
 __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
                            uint32_t& cseq, EmitList& EL, uint64_t start, const RcHit& rc, uint64_t& popped,
                            uint64_t& cached, unsigned& err, uint32_t& head_out, uint32_t& vcount_out,
-                           KState* live = nullptr, uint32_t* jbeam_out = nullptr, uint4* bsel = nullptr,
-                           const uint4* pf = nullptr
+                           KState* live = nullptr, uint32_t* jbeam_out = nullptr, uint4* bsel = nullptr
 #ifdef FAC_PHASE_PROF
                            , uint64_t* prof_acc = nullptr  // the wave's accumulators (bfs_window_body), added up at its end
 #endif
@@ -1817,7 +1816,7 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
       for (uint32_t u = 0; u < 4; ++u) {
         const uint32_t i = b + u * 64 + lane;
         // (a dedup-free variant has no table for the snapshot's dedup entries: not loaded)
-        if (i < nw && (VCAP > 0 || i < nq || i >= nq + nv)) w[u] = (pf && b == 0 && u == 0) ? *pf : src[i];
+        if (i < nw && (VCAP > 0 || i < nq || i >= nq + nv)) w[u] = src[i];
       }
 #pragma unroll
       for (uint32_t u = 0; u < 4; ++u) {
@@ -3233,23 +3232,9 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
 #ifdef FAC_PHASE_PROF
       t_grp += __builtin_amdgcn_s_memtime() - t_g0;
 #endif
-      uint4 pf_cur = make_uint4(0u, 0u, 0u, 0u);  // the current window's first 64 snapshot words, prefetched
-      bool pf_ok = false;
       while (m) {
         const int l = first_lane(m);
         m &= m - 1;
-        // the next window's first 64 snapshot words go out now and overlap this window's own snapshot
-        // load: its prologue then finds them in registers (one dependent load less per window)
-        uint4 pf_next = make_uint4(0u, 0u, 0u, 0u);
-        bool pf_next_ok = false;
-        if (m) {
-          const int ln = first_lane(m);
-          const uint32_t noff = shfl_u32(hit.off, ln);
-          if (noff != EMPTY && noff != RC_DONE) {
-            if ((unsigned long long)noff + RC_HDR + lane < P.rc_pool_cap) pf_next = P.rc_pool[noff + RC_HDR + lane];
-            pf_next_ok = true;
-          }
-        }
         const uint32_t seg = shfl_u32(kl, l);
         const uint64_t st = shfl_u64(start, l);
         const SegDesc S = P.segs[seg];
@@ -3262,13 +3247,11 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
 #endif
         const uint32_t qlen =
             run_window<VCAP, QCAP, MAP, LIVE>(P, S, s_vis, s_q, s_claim, cseq, EL, st, rc, popped, cached, err, qhead,
-                                              vcnt, s_live, jbeam, bsel, pf_ok ? &pf_cur : nullptr
+                                              vcnt, s_live, jbeam, bsel
 #ifdef FAC_PHASE_PROF
                                               , prof_acc
 #endif
                                               );
-        pf_cur = pf_next;
-        pf_ok = pf_next_ok;
 #ifdef FAC_WIN_HIST
         if (lane == 0 && P.rc_mode != 2) {
           const uint32_t b = hist_bucket(popped - popped0);
