@@ -2397,9 +2397,14 @@ __global__ __launch_bounds__(256) void rc_publish_kernel(SearchParams P, const u
 // (a count of c then means c + 1 sightings; bitmap collisions only admit a few singletons). A key
 // that finds no slot within `probes` stays uncounted (not cached).
 // One level's count table (rc_count_kernel): keys of k chars, open addressing with `probes` slots
+// A slot is one 64-bit word: the key hash with its low 4 bits replaced by the key's count (saturating
+// at `sat` <= RC_CSAT), so an insert of a known key touches one line (rounds <= 3 kept the counts in
+// an array of their own: a second random line per insert, C3 69 GB of count traffic per step); the
+// first inserter writes the representative (`rep`, by slot).
+constexpr uint32_t RC_CSAT = 15;
+__device__ __forceinline__ uint32_t rc_slot_count(unsigned long long w) { return (uint32_t)(w & 0xFull); }
 struct RcCountTarget {
   unsigned long long* keys;
-  uint32_t* cnt;
   uint64_t* rep;
   uint32_t mask;
   uint32_t k;  // 0: no table
@@ -2407,19 +2412,23 @@ struct RcCountTarget {
 __device__ __forceinline__ void rc_count_insert(const RcCountTarget& T, uint64_t k, uint64_t vid, uint32_t sat,
                                                 uint32_t probes) {
   const uint32_t h = rc_hash(k);
+  const unsigned long long tag = (k & ~0xFull) ? (k & ~0xFull) : 0x10ull;
   for (uint32_t p = 0; p < probes; ++p) {
     const uint32_t slot = (h + p) & T.mask;
-    unsigned long long kk = T.keys[slot];
-    if (kk == 0ull) {
-      kk = atomicCAS(&T.keys[slot], 0ull, (unsigned long long)k);
-      if (kk == 0ull) {
+    unsigned long long w = T.keys[slot];
+    if (w == 0ull) {
+      w = atomicCAS(&T.keys[slot], 0ull, tag | 1ull);
+      if (w == 0ull) {
         T.rep[slot] = vid;
-        atomicAdd(&T.cnt[slot], 1u);
         return;
       }
     }
-    if (kk == k) {  // sat == 1 (level 1 keeps every key): the inserter's count is all it needs
-      if (sat > 1u && T.cnt[slot] < sat) atomicAdd(&T.cnt[slot], 1u);
+    if ((w & ~0xFull) == tag) {  // counted up to sat (a failed exchange means another sighting landed)
+      while (rc_slot_count(w) < sat) {
+        const unsigned long long old = atomicCAS(&T.keys[slot], w, w + 1ull);
+        if (old == w) break;
+        w = old;
+      }
       return;
     }
   }
@@ -2473,19 +2482,18 @@ __global__ __launch_bounds__(256) void rc_derive_kernel(SearchParams P, const ui
 // (one same-address atomic per selected wave serialises at one L2 channel): per-block counts over
 // contiguous slot ranges, an exclusive scan of the block counts, then the assignment. Every other
 // slot maps to EMPTY (not cached: the lookup falls through to the next level).
-__device__ __forceinline__ bool rc_selected(const unsigned long long* keys, const uint32_t* cnt, uint32_t s,
-                                            uint32_t thr) {
-  return keys[s] != 0ull && cnt[s] >= thr;
+__device__ __forceinline__ bool rc_selected(const unsigned long long* keys, uint32_t s, uint32_t thr) {
+  const unsigned long long w = keys[s];
+  return w != 0ull && rc_slot_count(w) >= thr;
 }
-__global__ __launch_bounds__(64) void rc_sel_count_kernel(const unsigned long long* keys, const uint32_t* cnt,
-                                                           uint32_t n_slots, uint32_t range, uint32_t thr,
-                                                           uint32_t* bcount) {
+__global__ __launch_bounds__(64) void rc_sel_count_kernel(const unsigned long long* keys, uint32_t n_slots,
+                                                           uint32_t range, uint32_t thr, uint32_t* bcount) {
   __shared__ uint32_t tot;
   if (threadIdx.x == 0) tot = 0;
   __syncthreads();
   const uint32_t b0 = blockIdx.x * range, b1 = min(b0 + range, n_slots);
   uint32_t c = 0;
-  for (uint32_t s = b0 + threadIdx.x; s < b1; s += blockDim.x) c += rc_selected(keys, cnt, s, thr) ? 1u : 0u;
+  for (uint32_t s = b0 + threadIdx.x; s < b1; s += blockDim.x) c += rc_selected(keys, s, thr) ? 1u : 0u;
   c = wave_inclusive_sum(c);
   if (lane_id() == 63) atomicAdd(&tot, c);
   __syncthreads();
@@ -2508,9 +2516,8 @@ __global__ __launch_bounds__(64) void rc_sel_scan_kernel(uint32_t* bcount, uint3
     run += v;
   }
 }
-// counts are read and replaced by entries in place (val may alias cnt: a slot is only touched by
-// its own thread); rep[entry] = the slot's representative window
-__global__ __launch_bounds__(64) void rc_sel_assign_kernel(const unsigned long long* keys, const uint32_t* cnt,
+// val[slot] = the slot's entry (EMPTY: not selected); rep[entry] = the slot's representative window
+__global__ __launch_bounds__(64) void rc_sel_assign_kernel(const unsigned long long* keys,
                                                             const uint64_t* rep_slot, uint32_t* val, uint64_t* rep,
                                                             const uint32_t* bbase, uint32_t n_slots, uint32_t range,
                                                             uint32_t thr, uint32_t max_ent) {
@@ -2520,7 +2527,7 @@ __global__ __launch_bounds__(64) void rc_sel_assign_kernel(const unsigned long l
   const uint32_t b0 = blockIdx.x * range, b1 = min(b0 + range, n_slots);
   for (uint32_t s0 = b0; s0 < b1; s0 += blockDim.x) {
     const uint32_t s = s0 + threadIdx.x;
-    const bool sel = s < b1 && rc_selected(keys, cnt, s, thr);
+    const bool sel = s < b1 && rc_selected(keys, s, thr);
     const uint64_t m = __ballot(sel);
     uint32_t base = 0;
     if (m) {
@@ -4585,7 +4592,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     uint32_t slots = 1u << 12;
     while (slots < 4ull * max_ent && slots < (1u << l1_log2)) slots <<= 1;
     HIP_TRY(d_rck.alloc(slots * sizeof(unsigned long long), stream));
-    HIP_TRY(d_rcv.alloc(slots * sizeof(uint32_t), stream));  // key counts, then entries
+    HIP_TRY(d_rcv.alloc(slots * sizeof(uint32_t), stream));  // entries by slot
     HIP_TRY(d_rcslot.alloc(slots * sizeof(uint64_t), stream));
     HIP_TRY(d_rcb.alloc(8192 * sizeof(uint32_t), stream));
     HIP_TRY(d_rcrep.alloc(max_ent * sizeof(uint64_t), stream));
@@ -4598,7 +4605,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     HIP_TRY(hipMemsetAsync(d_rcn.p, 0, 4 * sizeof(unsigned long long), stream));
     const uint32_t cgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256, (uint64_t)cus * env_u("FAC_RC_CGRID", 8)));
 
-    // keys counted >= thr -> entries 0..n-1 (slot counts replaced by entries in place), reps by entry;
+    // keys counted >= thr -> entries 0..n-1 (val by slot), reps by entry;
     // returns n (all selected keys; entries past max_ent stay uncached)
     auto number_entries = [&](const DevBuf& keys, const DevBuf& cv, const DevBuf& rslot, const DevBuf& rep,
                               uint32_t n_slots, uint32_t thr, uint32_t cap, unsigned int& n) -> int {
@@ -4612,12 +4619,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       *reinterpret_cast<volatile unsigned int*>(n_host) = 0u;
       // single-wave workgroups throughout (see rc_sel_scan_kernel)
       hipLaunchKernelGGL(rc_sel_count_kernel, dim3(nb), dim3(64), 0, stream,
-                         static_cast<const unsigned long long*>(keys.p), static_cast<const uint32_t*>(cv.p), n_slots,
-                         range, thr, static_cast<uint32_t*>(d_rcb.p));
+                         static_cast<const unsigned long long*>(keys.p), n_slots, range, thr, static_cast<uint32_t*>(d_rcb.p));
       hipLaunchKernelGGL(rc_sel_scan_kernel, dim3(1), dim3(64), 0, stream, static_cast<uint32_t*>(d_rcb.p), nb, n_dev);
       hipLaunchKernelGGL(rc_sel_assign_kernel, dim3(nb), dim3(64), 0, stream,
-                         static_cast<const unsigned long long*>(keys.p), static_cast<const uint32_t*>(cv.p),
-                         static_cast<const uint64_t*>(rslot.p), static_cast<uint32_t*>(cv.p),
+                         static_cast<const unsigned long long*>(keys.p), static_cast<const uint64_t*>(rslot.p),
+                         static_cast<uint32_t*>(cv.p),
                          static_cast<uint64_t*>(rep.p), static_cast<const uint32_t*>(d_rcb.p), n_slots, range, thr, cap);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipStreamSynchronize(stream));
@@ -4633,9 +4639,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     RcTable L0{0u, 0u, nullptr, nullptr, nullptr, nullptr};
     n_ent0 = 0;
     const bool want_l0 = !diag_env("FAC_NO_RC_L0");
-    auto target = [](const DevBuf& keys, const DevBuf& cnt, const DevBuf& rep, uint32_t n_slots, uint32_t k) {
-      return RcCountTarget{static_cast<unsigned long long*>(keys.p), static_cast<uint32_t*>(cnt.p),
-                           static_cast<uint64_t*>(rep.p), n_slots - 1, k};
+    auto target = [](const DevBuf& keys, const DevBuf& rep, uint32_t n_slots, uint32_t k) {
+      return RcCountTarget{static_cast<unsigned long long*>(keys.p), static_cast<uint64_t*>(rep.p), n_slots - 1, k};
     };
     // Level-1 keys are counted on every stride1-th window, about 32 M windows in all (a power of two,
     // at most 16): a key that only unsampled windows hold stays uncached, and its windows resume from
@@ -4648,21 +4653,19 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     for (uint32_t k = kpin ? kpin : 4u; k >= (kpin ? kpin : 2u); --k) {
       P.rc_k = k;
       HIP_TRY(hipMemsetAsync(d_rck.p, 0, slots * sizeof(unsigned long long), stream));
-      HIP_TRY(hipMemsetAsync(d_rcv.p, 0, slots * sizeof(uint32_t), stream));
       const uint32_t k0 = std::max<uint64_t>(2, std::min<uint64_t>(k - 1, env_u("FAC_RC_L0K", k - 1)));  // knob: A/B
       const bool l0 = want_l0 && k >= 3 && L0.k == 0;  // the first key length only
-      RcCountTarget t1{nullptr, nullptr, nullptr, 0u, 0u};
+      RcCountTarget t1{nullptr, nullptr, 0u, 0u};
       if (l0) {
         HIP_TRY(d_l0k.alloc(slots * sizeof(unsigned long long), stream));
         HIP_TRY(d_l0v.alloc(slots * sizeof(uint32_t), stream));
         HIP_TRY(d_l0slot.alloc(slots * sizeof(uint64_t), stream));
         HIP_TRY(hipMemsetAsync(d_l0k.p, 0, slots * sizeof(unsigned long long), stream));
-        HIP_TRY(hipMemsetAsync(d_l0v.p, 0, slots * sizeof(uint32_t), stream));
-        t1 = target(d_l0k, d_l0v, d_l0slot, slots, k0);
+        t1 = target(d_l0k, d_l0slot, slots, k0);
         L0.k = k0;
       }
-      hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P, target(d_rck, d_rcv, d_rcslot, slots, k),
-                         RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u}, RcCountTarget{nullptr, nullptr, nullptr, 0u, 0u},
+      hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P, target(d_rck, d_rcslot, slots, k),
+                         RcCountTarget{nullptr, nullptr, 0u, 0u}, RcCountTarget{nullptr, nullptr, 0u, 0u},
                          stride1, 1u, nullptr, 0u, cprobes);
       HIP_TRY(hipGetLastError());
       unsigned int n_keys = 0;
@@ -4910,7 +4913,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     // the builds spilled registers; >= 2 since: C3 162.0 -> 151.8 ms, profiles/r03/sweep_levels.txt)
     // (keys seen >= 3 times measured slower once the small build variant made the builds cheaper:
     // the lane and wave kernels took more than the builds saved, profiles/r04k)
-    const uint32_t thr2 = (uint32_t)std::max<uint64_t>(1, env_u("FAC_RC_T2", s2 > 2 ? 1 : 2));
+    const uint32_t thr2 = (uint32_t)std::min<uint64_t>(RC_CSAT, std::max<uint64_t>(1, env_u("FAC_RC_T2", s2 > 2 ? 1 : 2)));
     std::vector<RcTable> Lx;        // sampled levels, ascending k
     std::vector<uint32_t> n_entx;   // their entries
     std::vector<size_t> xbuf;       // their count-table buffers
@@ -4935,12 +4938,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         if (k2 > L1.k) kk.push_back(k2);
       for (size_t x = 0; x < kk.size(); ++x) {  // every level's tables cleared before the level-1 build
         HIP_TRY(d_xk[x].alloc(slots2 * sizeof(unsigned long long), stream));
-        HIP_TRY(d_xv[x].alloc(slots2 * sizeof(uint32_t), stream));  // sample counts, then entries
+        HIP_TRY(d_xv[x].alloc(slots2 * sizeof(uint32_t), stream));  // entries by slot
         HIP_TRY(d_xslot[x].alloc(slots2 * sizeof(uint64_t), stream));
         HIP_TRY(d_xrep[x].alloc(max_ent2 * sizeof(uint64_t), stream));
         HIP_TRY(d_xc[x].alloc(2 * (size_t)max_ent2 * sizeof(uint32_t), stream));
         HIP_TRY(hipMemsetAsync(d_xk[x].p, 0, slots2 * sizeof(unsigned long long), stream));
-        HIP_TRY(hipMemsetAsync(d_xv[x].p, 0, slots2 * sizeof(uint32_t), stream));
       }
       if (int lrc = launch_l1()) return lrc;
       for (size_t x = 0; x < kk.size(); ++x) {
@@ -4950,13 +4952,13 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         // first one's numbering and held the sampled builds back behind the level-1 build (C3, r03aj)
         if (seen || x % 3 == 0) {
           if (seen) HIP_TRY(hipMemsetAsync(seen, 0, ((size_t)seen_mask + 1) / 8, stream));
-          const RcCountTarget none{nullptr, nullptr, nullptr, 0u, 0u};
+          const RcCountTarget none{nullptr, nullptr, 0u, 0u};
           const RcCountTarget t1 = (!seen && x + 1 < kk.size())
-                                       ? target(d_xk[x + 1], d_xv[x + 1], d_xslot[x + 1], slots2, kk[x + 1]) : none;
+                                       ? target(d_xk[x + 1], d_xslot[x + 1], slots2, kk[x + 1]) : none;
           const RcCountTarget t2 = (!seen && x + 2 < kk.size())
-                                       ? target(d_xk[x + 2], d_xv[x + 2], d_xslot[x + 2], slots2, kk[x + 2]) : none;
+                                       ? target(d_xk[x + 2], d_xslot[x + 2], slots2, kk[x + 2]) : none;
           hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid2), dim3(256), 0, stream, P,
-                             target(d_xk[x], d_xv[x], d_xslot[x], slots2, k2), t1, t2, stride2, thr_t, seen, seen_mask,
+                             target(d_xk[x], d_xslot[x], slots2, k2), t1, t2, stride2, thr_t, seen, seen_mask,
                              cprobes);
           HIP_TRY(hipGetLastError());
         }
@@ -5104,12 +5106,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     HIP_TRY(d_xc[xi].alloc(2 * (size_t)max_entd * sizeof(uint32_t), stream));
     HIP_TRY(hipEventRecord(ev.a, stream));
     HIP_TRY(hipMemsetAsync(d_xk[xi].p, 0, slots_d * sizeof(unsigned long long), stream));
-    HIP_TRY(hipMemsetAsync(d_xv[xi].p, 0, slots_d * sizeof(uint32_t), stream));
     const uint64_t n_reg = P.total_windows / RC_REGION;
     const uint32_t rgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_reg + 3) / 4, (uint64_t)cus * 8));
     hipLaunchKernelGGL(rc_count_open_kernel, dim3(rgrid), dim3(256), 0, stream, P,
-                       RcCountTarget{static_cast<unsigned long long*>(d_xk[xi].p), static_cast<uint32_t*>(d_xv[xi].p),
-                                     static_cast<uint64_t*>(d_xslot[xi].p), slots_d - 1, demand_k});
+                       RcCountTarget{static_cast<unsigned long long*>(d_xk[xi].p), static_cast<uint64_t*>(d_xslot[xi].p),
+                                     slots_d - 1, demand_k});
     HIP_TRY(hipGetLastError());
     unsigned int nk = 0;
     if (int nrc = rc_number_fn(d_xk[xi], d_xv[xi], d_xslot[xi], d_xrep[xi], slots_d, 2u, max_entd, nk)) return nrc;

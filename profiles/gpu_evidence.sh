@@ -45,7 +45,7 @@ fi
 export TMPDIR=/tmp
 if has kt; then
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o c3 \
-    -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/kt.log" 2>&1)
+    -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-fresh-diag $BENCH_ARGS > "$OUT/kt.log" 2>&1)
   find "$OUT/kt" -name '*kernel_stats.csv' -exec cp {} "$OUT/c3_kernel_stats.csv" \;
   find "$OUT/kt" -name '*kernel_trace.csv' -exec python3 profiles/step_timeline.py {} \; > "$OUT/c3_step_timeline.txt"
   head -20 "$OUT/c3_kernel_stats.csv"
@@ -54,7 +54,7 @@ fi
 if has pmc; then
   for c in FETCH_SIZE WRITE_SIZE; do
     (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_$c" -o c3 \
-      -- python3 "$ROOT/bench.py" --steps 2 --warmup 0 --no-cpu-baseline > "$OUT/pmc_$c.log" 2>&1)
+      -- python3 "$ROOT/bench.py" --steps 2 --warmup 0 --no-cpu-baseline --no-fresh-diag $BENCH_ARGS > "$OUT/pmc_$c.log" 2>&1)
     find "$OUT/pmc_$c" -name '*counter_collection.csv' -exec cp {} "$OUT/c3_pmc_$c.csv" \;
   done
   python3 profiles/make_traffic.py c3 256 2 "$OUT/c3_pmc_FETCH_SIZE.csv" "$OUT/c3_pmc_WRITE_SIZE.csv" "$(python3 -c "import bench; print(bench.sources_sha())")" > "$OUT/traffic.log"
