@@ -2399,8 +2399,10 @@ __global__ __launch_bounds__(256) void rc_publish_kernel(SearchParams P, const u
 // One level's count table (rc_count_kernel): keys of k chars, open addressing with `probes` slots
 // A slot is one 64-bit word: the key hash with its low 4 bits replaced by the key's count (saturating
 // at `sat` <= RC_CSAT), so an insert of a known key touches one line (rounds <= 3 kept the counts in
-// an array of their own: a second random line per insert, C3 69 GB of count traffic per step); the
-// first inserter writes the representative (`rep`, by slot).
+// an array of their own: a second random line per insert, C3 69 GB of count traffic per step). The
+// representative (`rep`, by slot) is written by the sighting that brings the count to min(sat, 2):
+// any window holding the key is a valid one, and keys seen once (most long keys) are never selected
+// when sat >= 2, so they cost one line.
 constexpr uint32_t RC_CSAT = 15;
 __device__ __forceinline__ uint32_t rc_slot_count(unsigned long long w) { return (uint32_t)(w & 0xFull); }
 struct RcCountTarget {
@@ -2419,14 +2421,17 @@ __device__ __forceinline__ void rc_count_insert(const RcCountTarget& T, uint64_t
     if (w == 0ull) {
       w = atomicCAS(&T.keys[slot], 0ull, tag | 1ull);
       if (w == 0ull) {
-        T.rep[slot] = vid;
+        if (sat <= 1u) T.rep[slot] = vid;
         return;
       }
     }
     if ((w & ~0xFull) == tag) {  // counted up to sat (a failed exchange means another sighting landed)
       while (rc_slot_count(w) < sat) {
         const unsigned long long old = atomicCAS(&T.keys[slot], w, w + 1ull);
-        if (old == w) break;
+        if (old == w) {
+          if (rc_slot_count(w) == 1u) T.rep[slot] = vid;
+          break;
+        }
         w = old;
       }
       return;
