@@ -4560,20 +4560,20 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   RcTable L1{0u, 0u, nullptr, nullptr, nullptr, nullptr};
   uint32_t n_ent0 = 0, qbuild = 0;
   bool live_builds = false;
-  uint64_t ct_mult = 4;
+  uint64_t ct_mult = 4, ct_mult2 = 4;  // lookup slots per entry: levels 0/1 by entries, sampled levels by kept snapshots
   std::function<int(const RcTable&, uint32_t, const uint64_t*, hipStream_t, bool, bool)> rc_build_fn;
   std::function<int(RcTable&, uint32_t, const uint64_t*, DevBuf&, hipStream_t, bool)> rc_publish_fn;
   std::function<int(const DevBuf&, const DevBuf&, const DevBuf&, const DevBuf&, uint32_t, uint32_t, uint32_t, unsigned int&)>
       rc_number_fn;
   // after its build a level's entries are published into an exact-key lookup table (4 slots per
   // entry: a miss usually ends at the first probe)
-  auto ct_slots = [&](uint32_t n_ent) {
+  auto ct_slots = [&](uint32_t n_ent, uint64_t mult) {
     uint32_t cs = 1u << 12;
-    while (cs < ct_mult * n_ent && cs < (1u << 28)) cs <<= 1;
+    while (cs < mult * n_ent && cs < (1u << 28)) cs <<= 1;
     return cs;
   };
-  auto clear_ct = [&](uint32_t n_ent, DevBuf& ct, hipStream_t bs) -> int {
-    const uint32_t cs = ct_slots(n_ent);
+  auto clear_ct = [&](uint32_t n_ent, DevBuf& ct, hipStream_t bs, uint64_t mult = 0) -> int {
+    const uint32_t cs = ct_slots(n_ent, mult ? mult : ct_mult);
     HIP_TRY(ct.alloc((size_t)cs * 2 * sizeof(uint4), bs));
     HIP_TRY(hipMemsetAsync(ct.p, 0, (size_t)cs * 2 * sizeof(uint4), bs));
     return FAC_OK;
@@ -4750,7 +4750,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     // against 258 with exact sampled builds). FAC_LIVE_BUILD=1 brings them back (A/B).
     live_builds = P.beam && !counts && !e.has_map && qbuild <= 256 && diag_env("FAC_LIVE_BUILD") &&
                              !diag_env("FAC_NO_LIVE_BUILD");
-    ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", diag_env("FAC_RC_CT_ENTRIES") ? 4 : 2)));
+    // 4 slots per entry, the sampled levels' per kept snapshot (C3: 5.9 M of 8.2 M 5-char entries kept).
+    // 2 per entry cost C2 76.0 vs 71.0 ms (profiles/r04ab); 4 for the sampled levels: C2 71.1 vs 73.5,
+    // C4 16.45 vs 17.39, C3 135.9 vs 136.8 against 2 (profiles/r04ac)
+    ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", 4)));
+    ct_mult2 = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT2", 4)));
     auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, hipStream_t bs, bool cleared = false,
                      bool sampled = false) -> int {
       SearchParams Q = P;
@@ -4827,11 +4831,12 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     };
     // n_size: the entries the table is sized for (the snapshots the build kept, when known)
     auto publish = [&](RcTable& T, uint32_t n_ent, const uint64_t* reps, DevBuf& ct, hipStream_t bs,
-                       bool cleared = false, uint32_t n_size = 0xFFFFFFFFu) -> int {
+                       bool cleared = false, uint32_t n_size = 0xFFFFFFFFu, uint64_t mult = 0) -> int {
       if (n_size == 0xFFFFFFFFu) n_size = n_ent;
-      const uint32_t cs = ct_slots(n_size);
+      if (!mult) mult = ct_mult;
+      const uint32_t cs = ct_slots(n_size, mult);
       if (!cleared) {
-        if (int crc = clear_ct(n_size, ct, bs)) return crc;
+        if (int crc = clear_ct(n_size, ct, bs, mult)) return crc;
       }
       hipLaunchKernelGGL(rc_publish_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_ent + 255) / 256, cus * 8))),
                          dim3(256), 0, bs, P, reps, static_cast<const uint4*>(P.rc_pool), T.off, T.count, n_ent, T.k,
@@ -5001,7 +5006,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
           kept = std::min<uint32_t>(kept, got);
         }
         if ((brc = publish(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), d_ct[1 + x], stream, false,
-                           kept))) return brc;
+                           kept, ct_mult2))) return brc;
         tabs.push_back(Lx[x]);
         tab_exact.push_back(!live_builds);
       }
