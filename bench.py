@@ -62,7 +62,7 @@ def parse():
                     help="filler words drawn from a fixed vocabulary of this many random words; 0: fresh random words")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="single-thread CPU baseline sample budget")
     ap.add_argument("--cpu-min-mib", type=float, default=None,
-                    help="single-thread CPU baseline: at least this many MiB of the haystack (default c3: 2)")
+                    help="single-thread CPU baseline: at least this many MiB of the haystack (default 2)")
     ap.add_argument("--no-fresh-diag", action="store_true",
                     help="skip diagnostics.fresh_words (c2/c3 at N=1: the same config on SURVEY §8(d)'s fresh-word "
                          "generator, timed beside the headline)")
@@ -233,7 +233,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        min_mib = args.cpu_min_mib if args.cpu_min_mib is not None else (2.0 if args.config == "c3" else 0.0)
+        min_mib = args.cpu_min_mib if args.cpu_min_mib is not None else 2.0  # at least 2 MiB single-thread
         cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads, int(min_mib * (1 << 20)))
 
     if rank == 0:
