@@ -5074,10 +5074,14 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     // one wave per workgroup; each takes its best lists from its own emit-scratch slice
     const uint32_t lgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + LANE_CHUNK - 1) / LANE_CHUNK, (uint64_t)max_grid));
     static_assert(16 * 64 <= 1024, "lane best lists must fit the emit scratch slice (P.ecap >= 1024)");
-    // 16-state rings by default (C3: lane 19 ms + wave kernel 37 ms, against 6 + 58 with 8 states)
+    // 12-state rings by default: 10 KB of LDS, so 16 waves per CU instead of 12 with 16 states, and the
+    // windows that need 13-16 states (the ones that held a wave longest) go to the dedup-free pass.
+    // C3: lane 13.6 -> 7.1 ms, wave 41.0 -> 45.0 ms (133.5 vs 135.7 per step); fresh words 447.5 vs
+    // 442.4 (profiles/r04ab/r04ag.txt). Round 2: 16 states against 8, lane 19 + wave 37 ms vs 6 + 58.
     if (diag_env("FAC_LANE_Q8")) hipLaunchKernelGGL((lane_window_kernel<8, 8>), dim3(lgrid), dim3(64), 0, stream, P);
     else if (diag_env("FAC_LANE_Q32")) hipLaunchKernelGGL((lane_window_kernel<32, 8>), dim3(lgrid), dim3(64), 0, stream, P);
-    else hipLaunchKernelGGL((lane_window_kernel<16, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+    else if (diag_env("FAC_LANE_Q16")) hipLaunchKernelGGL((lane_window_kernel<16, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+    else hipLaunchKernelGGL((lane_window_kernel<12, 8>), dim3(lgrid), dim3(64), 0, stream, P);
     HIP_TRY(hipGetLastError());
     return FAC_OK;
   };

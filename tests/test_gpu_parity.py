@@ -397,14 +397,15 @@ def test_prefix_cache_two_levels_c3_slice(k2, monkeypatch):
     assert len(on) > 0 and sorted(on.tolist()) == sorted(off.tolist()) == sorted(one.tolist())
 
 
-@pytest.mark.parametrize("knobs", [{}, {"FAC_NO_BUILD_SMALL": "1"}, {"FAC_BUILD_SMALL_L1": "1"},
-                                   {"FAC_RC_DEEPEST": "1", "FAC_RC_CT_ENTRIES": "1"}],
-                         ids=["default", "no-small-build", "small-build-l1", "deepest-first"])
+@pytest.mark.parametrize("knobs", [{}, {"FAC_BUILD_SMALL": "1"}, {"FAC_BUILD_SMALL": "1", "FAC_BUILD_SMALL_L1": "1"},
+                                   {"FAC_RC_DEEPEST": "1", "FAC_RC_CT_ENTRIES": "1"}, {"FAC_LANE_Q16": "1"}],
+                         ids=["default", "small-build", "small-build-l1", "deepest-first", "lane-ring-16"])
 def test_prefix_cache_round4_paths_c3_slice(knobs, monkeypatch):
-    """Round-4 prefix-cache paths on a C3-shaped haystack with the sampled levels on: the small build
-    variant and the full-size build of the keys it defers (default), the full-size build alone, the
-    small variant for level 1 too, and the round-3 probe order with entry-sized tables: identical
-    records to the cache off, and the deeper levels replaying pops."""
+    """Round-4 prefix-cache paths on a C3-shaped haystack with the sampled levels on: the default
+    (full-size builds, count slots with the count in the key word, 12-state lane rings), the small
+    build variant and the full-size build of the keys it defers, the small variant for level 1 too,
+    the round-3 probe order with entry-sized tables, and 16-state lane rings: identical records to
+    the cache off, and the deeper levels replaying pops."""
     from fuzzy_aho_corasick import workloads
     w = workloads.config("c3", 2 << 20, 3)
     staged = workloads.builder_for(w).build(w.patterns).stage(w.haystack)
