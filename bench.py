@@ -438,7 +438,8 @@ def run_c5(args, world, rank, local):
     dev_ms = (pf + km) / K
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads)
+        min_mib = args.cpu_min_mib if args.cpu_min_mib is not None else 2.0  # at least 2 MiB single-thread
+        cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads, int(min_mib * (1 << 20)))
     if rank == 0:
         bytes_step = processed_rank + 32 * matches / K / world
         achieved = bytes_step / (dev_ms / 1e3) / 1e9 if dev_ms > 0 else 0.0
