@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round evidence on one MI355X (run through gpurun from the repo root):
 #   bash profiles/gpu_evidence.sh TAG [what...]
-# what: tests smoke c3 c3e2e c2 c4 c5 c5t kt pmc pmc5 c3t  (default: tests smoke c3 c2 c5 kt pmc). Outputs under gpurun_out/TAG/.
+# what: tests smoke c3 c3e2e c2 c4 c5 c5t kt pmc pmc5 pmc2 pmc4 c2t c4t c3t  (default: tests smoke c3 c2 c5 kt pmc). Outputs under gpurun_out/TAG/.
 # Every GPU step has its own time limit; the script stops at the first failing step.
 set -eo pipefail
 TAG=${1:?tag}
@@ -71,6 +71,23 @@ if has pmc5; then  # C5: one GPU's 12.5 GiB share of the 100 GiB stream
   cp profiles/traffic_c5.json "$OUT/traffic_c5.json"
   head -c 1500 "$OUT/traffic5.log"
 fi
+for cfg in c2 c4; do  # pmc2 / pmc4: PMC traffic of the C2 (1 GiB) / C4 (128 MiB) line; c2t / c4t: the line after it
+  mib=1024; [ $cfg = c4 ] && mib=128
+  if has pmc${cfg#c}; then
+    for c in FETCH_SIZE WRITE_SIZE; do
+      (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc${cfg}_$c" -o $cfg \
+        -- python3 "$ROOT/bench.py" --config $cfg --steps 2 --warmup 0 --no-cpu-baseline --no-fresh-diag > "$OUT/pmc${cfg}_$c.log" 2>&1)
+      find "$OUT/pmc${cfg}_$c" -name '*counter_collection.csv' -exec cp {} "$OUT/${cfg}_pmc_$c.csv" \;
+    done
+    python3 profiles/make_traffic.py $cfg $mib 2 "$OUT/${cfg}_pmc_FETCH_SIZE.csv" "$OUT/${cfg}_pmc_WRITE_SIZE.csv" "$(python3 -c "import bench; print(bench.sources_sha())")" > "$OUT/traffic_$cfg.log"
+    cp profiles/traffic_$cfg.json "$OUT/traffic_$cfg.json"
+    head -c 600 "$OUT/traffic_$cfg.log"
+  fi
+  if has ${cfg}t; then  # with the CPU baseline and the traffic just measured
+    timeout -k 10 400 python bench.py --config $cfg > "$OUT/bench_${cfg}_traffic.json" 2> "$OUT/bench_${cfg}_traffic.err"
+    cat "$OUT/bench_${cfg}_traffic.json"
+  fi
+done
 if has c5t; then  # after traffic_c5.json exists
   timeout -k 10 600 python bench.py --config c5 --steps 2 > "$OUT/bench_c5_traffic.json" 2> "$OUT/bench_c5_traffic.err"
   cat "$OUT/bench_c5_traffic.json"
