@@ -398,14 +398,17 @@ def test_prefix_cache_two_levels_c3_slice(k2, monkeypatch):
 
 
 @pytest.mark.parametrize("knobs", [{}, {"FAC_BUILD_SMALL": "1"}, {"FAC_BUILD_SMALL": "1", "FAC_BUILD_SMALL_L1": "1"},
-                                   {"FAC_RC_DEEPEST": "1", "FAC_RC_CT_ENTRIES": "1"}, {"FAC_LANE_Q16": "1"}],
-                         ids=["default", "small-build", "small-build-l1", "deepest-first", "lane-ring-16"])
+                                   {"FAC_RC_DEEPEST": "1", "FAC_RC_CT_ENTRIES": "1"}, {"FAC_LANE_Q16": "1"},
+                                   {"FAC_RC_STRIDE2": "1", "FAC_RC_T2": "3"}, {"FAC_RC_T2": "1"}],
+                         ids=["default", "small-build", "small-build-l1", "deepest-first", "lane-ring-16",
+                              "counts-every-window-thr3", "counts-thr1"])
 def test_prefix_cache_round4_paths_c3_slice(knobs, monkeypatch):
     """Round-4 prefix-cache paths on a C3-shaped haystack with the sampled levels on: the default
     (full-size builds, count slots with the count in the key word, 12-state lane rings), the small
     build variant and the full-size build of the keys it defers, the small variant for level 1 too,
-    the round-3 probe order with entry-sized tables, and 16-state lane rings: identical records to
-    the cache off, and the deeper levels replaying pops."""
+    the round-3 probe order with entry-sized tables, 16-state lane rings, and the count tables'
+    saturating counts at thresholds 3 (every window counted) and 1 (the representative written at
+    the first sighting): identical records to the cache off, and the deeper levels replaying pops."""
     from fuzzy_aho_corasick import workloads
     w = workloads.config("c3", 2 << 20, 3)
     staged = workloads.builder_for(w).build(w.patterns).stage(w.haystack)
