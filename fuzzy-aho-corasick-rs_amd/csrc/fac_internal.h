@@ -255,8 +255,6 @@ struct SearchParams {
   uint32_t rc_k;                    // key chars of the level being collected / built (2..8)
   uint32_t rc_ntab;                 // tables a lookup consults (0..kRcLevels), deepest first
   uint32_t rc_kstart;               // rc_lookup's first probe: the shallowest level with k >= this (0: deepest)
-  uint32_t rc_defer_only;           // cache build: only the keys an earlier build deferred (rc_off == RC_DEFER)
-  uint32_t rc_defer_fail;           // cache build: a key that overflows the ring or dedup table is deferred
   uint4* rc_bhits;                  // cache build: each key's parent snapshot (rc_parent_kernel), as rc_hits
   uint32_t* rc_bpops;               // ... and its pops
   RcTable rc_tab[kRcLevels];

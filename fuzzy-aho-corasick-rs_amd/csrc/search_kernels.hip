@@ -2262,7 +2262,7 @@ __device__ __forceinline__ uint32_t rc_key_hash(uint4 k) {
 // A window's prefix-cache hit (from the levels' exact-key lookup tables): off = EMPTY on a miss.
 // Any level's snapshot resumes the window exactly; the deepest usable one leaves the least work.
 // Probe order: a lookup starts at the shallowest level with k >= P.rc_kstart (the first sampled
-// level; 0 = the deepest level) and goes deeper while the levels hit with an open snapshot: a key
+// level; a k no level has = the deepest level) and goes deeper while the levels hit with an open snapshot: a key
 // whose snapshot is final has no deeper snapshot (its builds stop at the final parent), and a deeper
 // key that is not cached means its extensions are not either (they are counted on the same sampled
 // windows; the rare exception -- a key that failed to build while an extension built from the
@@ -2392,10 +2392,7 @@ __global__ __launch_bounds__(256) void rc_publish_kernel(SearchParams P, const u
 // Prefix-cache keys: every `stride`-th window's key is inserted and counted (level 1: every window,
 // sampled levels: a sample); the first inserter of a key is its representative. Counts saturate
 // at `sat` (only "at least thr" is asked), so a frequent key is not one hot atomic per window.
-// `seen` (optional, sampled levels): a bitmap of key hashes; a key's first sighting only sets its bit,
-// so keys seen once (most long keys) never reach the table and the table is sized for repeated keys
-// (a count of c then means c + 1 sightings; bitmap collisions only admit a few singletons). A key
-// that finds no slot within `probes` stays uncounted (not cached).
+// A key that finds no slot within `probes` stays uncounted (not cached).
 // One level's count table (rc_count_kernel): keys of k chars, open addressing with `probes` slots
 // A slot is one 64-bit word: the key hash with its low 4 bits replaced by the key's count (saturating
 // at `sat` <= RC_CSAT), so an insert of a known key touches one line (rounds <= 3 kept the counts in
@@ -2441,8 +2438,7 @@ __device__ __forceinline__ void rc_count_insert(const RcCountTarget& T, uint64_t
 // Up to three levels are counted in one pass over the windows (level 1; the sampled levels): their
 // inserts go out together and the window's text is read once.
 __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, RcCountTarget t0, RcCountTarget t1,
-                                                       RcCountTarget t2, uint32_t stride, uint32_t sat, uint32_t* seen,
-                                                       uint32_t seen_mask, uint32_t probes) {
+                                                       RcCountTarget t2, uint32_t stride, uint32_t sat, uint32_t probes) {
   const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
   unsigned err = 0;
   const uint64_t ns = (P.total_windows + stride - 1) / stride;
@@ -2459,10 +2455,6 @@ __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, RcCountTa
       RcChars ch;
       uint64_t k;
       if (!rc_key(P, S, start, T.k, ch, k)) continue;
-      if (seen) {
-        const uint32_t b = (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 32) & seen_mask;
-        if (!(atomicOr(&seen[b >> 5], 1u << (b & 31u)) & (1u << (b & 31u)))) continue;  // first sighting
-      }
       rc_count_insert(T, k, vid, sat, probes);
     }
   }
@@ -2581,67 +2573,6 @@ __device__ __forceinline__ bool flush_final(const SearchParams& P, bool resumed,
     triv_lane += 1;
   }
   return triv;
-}
-
-// Spilled windows of a dedup-free first pass restart on the exact variant, which needs an exact
-// snapshot: their hits are looked up again in the levels built by the exact kernel (P.rc_tab).
-__global__ __launch_bounds__(256) void rc_relookup_kernel(SearchParams P, uint64_t n) {
-  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t vid = P.win_list[x];  // an open entry
-    const uint64_t wid = rc_window_of(P, vid);
-    const uint32_t kl = find_seg(P, wid);
-    const SegDesc S = P.segs[kl];
-    const uint64_t start = S.w_begin + (wid - P.seg_prefix[kl]);
-    const RcHit hit = rc_lookup(P, S, start, P.rc_qcap);
-    P.rc_hits[vid] = make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel);
-    P.rc_hit_pops[vid] = hit.pops;
-  }
-}
-
-// Demand level (launch_pass): the keys of the entries still open after the lookups and the lane
-// kernel (the windows the wave kernels would search), counted over exactly those; one wave per
-// region of compacted entries. A key's first inserter (a window) is its representative.
-__global__ __launch_bounds__(256) void rc_count_open_kernel(SearchParams P, RcCountTarget T) {
-  const uint32_t lane = lane_id();
-  const uint64_t n_reg = P.total_windows / RC_REGION;
-  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
-  for (uint64_t rg = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; rg < n_reg; rg += nw) {
-    const uint32_t n = P.rc_region_cnt[rg];
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint64_t e = rg * RC_REGION + i;
-      if (P.rc_hits[e].x == RC_DONE) continue;
-      const uint64_t wid = rc_window_of(P, e);
-      const uint32_t kl = find_seg(P, wid);
-      const SegDesc S = P.segs[kl];
-      const uint64_t start = S.w_begin + (wid - P.seg_prefix[kl]);
-      RcChars ch;
-      uint64_t k;
-      if (rc_key(P, S, start, T.k, ch, k)) rc_count_insert(T, k, wid, 2u, RC_PROBES);
-    }
-  }
-}
-// ... and the open entries' lookups in the new level (P.rc_tab[0] alone): a hit replaces the entry's
-// snapshot (the level is deeper than every other)
-__global__ __launch_bounds__(256) void rc_relookup_open_kernel(SearchParams P) {
-  const uint32_t lane = lane_id();
-  const uint64_t n_reg = P.total_windows / RC_REGION;
-  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
-  for (uint64_t rg = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; rg < n_reg; rg += nw) {
-    const uint32_t n = P.rc_region_cnt[rg];
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint64_t e = rg * RC_REGION + i;
-      if (P.rc_hits[e].x == RC_DONE) continue;
-      const uint64_t wid = rc_window_of(P, e);
-      const uint32_t kl = find_seg(P, wid);
-      const SegDesc S = P.segs[kl];
-      const uint64_t start = S.w_begin + (wid - P.seg_prefix[kl]);
-      const RcHit hit = rc_lookup(P, S, start, P.rc_qcap);
-      if (hit.off != EMPTY) {
-        P.rc_hits[e] = make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel);
-        P.rc_hit_pops[e] = hit.pops;
-      }
-    }
-  }
 }
 
 // Per-window prefix-cache lookups of a main pass (P.rc_mode == 1), ahead of the search kernels:
@@ -3119,10 +3050,6 @@ __global__ __launch_bounds__(64) void lane_window_kernel(SearchParams P) {
   }
 }
 
-// A key a cache build leaves to a later build (rc_off): the small build variant defers the keys it
-// cannot hold to the full-size build (rc_defer_fail / rc_defer_only)
-constexpr uint32_t RC_DEFER = 0xFFFFFFFDu;
-
 // LK: the window prologue looks snapshots up itself (cache builds); otherwise a main pass with the
 // prefix cache reads the hits rc_lookup_kernel stored.
 template <uint32_t VCAP, uint32_t QCAP, bool MAP, bool LK, bool LIVE = false>
@@ -3219,7 +3146,6 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           active = !window_skipped(P, S, start, err);
         }
       }
-      if (P.rc_mode == 2 && P.rc_defer_only) active = active && P.rc_off[v] == RC_DEFER;  // after the lane build
       if constexpr (LK)
         if (P.rc_mode != 0 && P.rc_ntab && active && P.rc_bhits) {  // rc_parent_kernel's lookup
           const uint4 h = P.rc_bhits[v];
@@ -3305,26 +3231,6 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
               jlive = max(jlive, lv ? (kv[u].jm & 0xFFFFu) + 1u : 0u);
             }
           }
-          // LIVE (dedup-free) build: no table of its own; the snapshot carries the parent's check
-          // entries that a later pop can still meet (jmin <= j < the parent's jcheck) -- no beam ran
-          // in this build, so they remain the only entries popped before a beam (run_window LIVE)
-          const uint4* carry = nullptr;
-          uint32_t ncarry = 0, jcp = 0;
-          if constexpr (VCAP == 0 && LIVE) {
-            if (rc.off != EMPTY) {
-              const uint32_t pj = P.rc_pool[rc.off + 1].y;
-              jcp = pj & 0xFFFFu;
-              ncarry = pj >> 16;
-              carry = P.rc_pool + rc.off + RC_HDR + (rc.tail - rc.head);
-            }
-            for (uint32_t b = 0; b < ncarry; b += 64) {
-              const uint4 d = b + lane < ncarry ? carry[b + lane] : make_uint4(EMPTY, 0u, 0u, 0u);
-              const uint32_t dj = d.y & 0xFFFFu;
-              const bool keep = d.x != EMPTY && dj >= jmin && dj + 1u <= jcp;
-              nv += (uint32_t)__popcll(__ballot(keep));
-              jlive = max(jlive, keep ? dj + 1u : 0u);
-            }
-          }
           jlive = wave_inclusive_max(jlive);
           jlive = shfl_u32(jlive, 63);
           bool bad = (wave_or(err) & (ERR_QUEUE | ERR_VISITED | ERR_EMIT)) != 0 || EL.n > P.rc_emax || nv > P.rc_vmax;
@@ -3372,17 +3278,6 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
               }
               if (pass == 0) ncheck = at0;
             }
-          } else if constexpr (LIVE) {  // every carried entry is a check entry
-            uint32_t at0 = 0;
-            for (uint32_t b = 0; b < ncarry && !bad; b += 64) {
-              const uint4 d = b + lane < ncarry ? carry[b + lane] : make_uint4(EMPTY, 0u, 0u, 0u);
-              const uint32_t dj = d.y & 0xFFFFu;
-              const bool keep = d.x != EMPTY && dj >= jmin && dj + 1u <= jcp;
-              const uint64_t m = __ballot(keep);
-              if (keep) dst[nq + at0 + prefix_below(m)] = d;
-              at0 += (uint32_t)__popcll(m);
-            }
-            ncheck = at0;
           }
           for (uint32_t i = lane; i < EL.n && !bad; i += 64) dst[nq + nv + i] = EL.buf[i];
           if (lane == 0) {
@@ -3392,10 +3287,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
               // jcheck: dedup entries a resumed dedup-free run must still honour (j + 1 <= jcheck)
               P.rc_pool[off + 1] = make_uint4(EL.n, ncheck ? (jcheck | (ncheck << 16)) : 0u, jbeam[0], jbeam[1]);
             }
-            // a key the small build variant could not hold (frontier ring or dedup table full) is left
-            // to the full-size build that follows it (rc_defer_fail, rc_defer_only)
-            const bool defer = P.rc_defer_fail && (wave_or(err) & (ERR_QUEUE | ERR_VISITED)) != 0;
-            P.rc_off[ent] = defer ? RC_DEFER : bad ? EMPTY : (uint32_t)off;
+            P.rc_off[ent] = bad ? EMPTY : (uint32_t)off;
             P.rc_count[ent] = bad ? EMPTY : nq;
             kept_snaps += bad ? 0u : 1u;
           }
@@ -3473,24 +3365,6 @@ template <uint32_t QCAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((FAC_BEAM_WAVES && QCAP <= 256) ? FAC_BEAM_WAVES : 1)))
 void rc_build_kernel(SearchParams P) {
   bfs_window_body<512, QCAP, false, true>(P);  // the prefix cache is off with mappings
-}
-// a smaller build variant (256-entry dedup table, 10 KB of LDS: up to 16 waves per CU, held to 128
-// VGPRs) for the sampled levels, whose keys pop few states: their builds wait on memory, not issue.
-// A key it cannot hold (ring or table full) is deferred to the full-size build. Opt-in (FAC_BUILD_SMALL):
-// it won only against full-size builds slowed by a scratch frame (profiles/r04i); against the fixed
-// ones it loses (C3 158.2 vs 142.2 ms per step, profiles/r04m: its spills and the deferred keys' second
-// build cost more than the occupancy gains)
-#ifndef FAC_SMALL_BUILD_WAVES
-#define FAC_SMALL_BUILD_WAVES 4
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAC_SMALL_BUILD_WAVES))) void rc_build_kernel_small(SearchParams P) {
-  bfs_window_body<256, 256, false, true>(P);
-}
-// dedup-free build of a sampled level of a beamed engine (launch_pass): resumes from the parent
-// snapshot, honours its check entries (run_window LIVE); a key that would beam (or overflow) is left
-// uncached, its windows resume from the shallower level
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void rc_build_kernel_live(SearchParams P) {
-  bfs_window_body<0, 256, false, true, true>(P);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -4413,9 +4287,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     err = "beam width too large for the on-chip frontier";
     return FAC_E_UNSUPPORTED;
   }
-  const bool spill_small = diag_env("FAC_SPILL_SMALL") != nullptr;  // A/B: dedup-free spills to <256, 256> first
   auto escalate = [&](size_t cur) {  // next variant for spilled windows
-    const uint32_t want_v = (spill_small && kVariants[cur].vcap == 0) ? 256u : std::max<uint32_t>(kVariants[cur].vcap * 2, 512);
+    const uint32_t want_v = std::max<uint32_t>(kVariants[cur].vcap * 2, 512);
     for (size_t i = cur + 1; i < nv; ++i)
       if (fits(kVariants[i]) && kVariants[i].vcap >= want_v && kVariants[i].qcap >= kVariants[cur].qcap) return i;
     // past the largest table: an unbeamed, non-exact engine may still trade the table for a
@@ -4433,7 +4306,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   DevBuf d_l0k, d_l0v, d_l0slot, d_l0rep, d_l0c;  // prefix cache, level 0
   DevBuf d_hits, d_hitp;   // per-window lookups of the main pass
   DevBuf d_voff, d_rcnt;   // ... their windows and per-region counts
-  DevBuf d_seen;           // prefix cache: sampled levels' first-sighting bitmap
   DevBuf d_bhits, d_bpops; // prefix cache builds: the representatives' parent snapshots
   DevBuf d_slots, d_bsel;  // wave-slot rings (one per stream), beam-selection scratch
   ScratchSet* bound = t_scratch;  // a streaming worker's own set, else the engine's
@@ -4449,7 +4321,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     for (DevBuf* b : {&d_l0k, &d_l0v, &d_l0slot, &d_l0rep, &d_l0c}) bufs.push_back(b);
     bufs.push_back(&d_hits);
     bufs.push_back(&d_hitp);
-    bufs.push_back(&d_seen);
     bufs.push_back(&d_voff);
     bufs.push_back(&d_rcnt);
     bufs.push_back(&d_slots);
@@ -4470,9 +4341,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   uint64_t spill_cap = std::max<uint64_t>(4096, windows / (P.beam ? 8 : 32));
   const uint32_t max_grid = (uint32_t)cus * 16;
   HIP_TRY(d_ebuf.alloc((size_t)max_grid * P.ecap * sizeof(uint4), stream));
-  // two counter sets: the pass's, and (second) a cache build's while a pass is open (demand level)
-  HIP_TRY(d_cnt.alloc(2 * N_COUNTERS * sizeof(unsigned long long), stream));
-  size_t build_cnt = 0;  // counter set the cache builds use
+  HIP_TRY(d_cnt.alloc(N_COUNTERS * sizeof(unsigned long long), stream));
   // wave slots: a ring of max_grid slots per stream a slot-using kernel runs on (this one, the
   // level-1 build's); beamed engines: each slot's beam-selection scratch, sized for 256-state rings
   // at max_grid slots (larger rings get fewer slots, still above their LDS-bound residency)
@@ -4536,9 +4405,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   // least T times get a snapshot built by resuming their representative from its level-1 snapshot.
   // A window resumes from the deepest snapshot its prefix has. Skipped when the root emits (an empty
   // pattern), with mappings (whole-grapheme keys), or when the search is small.
-  RcTable exact_tab[kRcLevels];  // levels whose snapshots are exact (deepest first)
-  uint32_t n_exact_tabs = 0;
-  bool any_inexact = false;
   P.rc_mode = 0;
   P.rc_hits = nullptr;
   P.rc_hit_pops = nullptr;
@@ -4546,25 +4412,16 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.rc_region_cnt = nullptr;
   P.rc_ntab = 0;
   P.rc_kstart = 0;
-  P.rc_defer_only = 0;
-  P.rc_defer_fail = 0;
   P.live_nqmax = 0;
   P.rc_lane_flush = diag_env("FAC_RC_NO_LANE") ? 0 : 1;
   P.dyn_chunks = diag_env("FAC_STATIC_GRID") ? 0 : 1;
   const bool root_out = !e.nodes.empty() && e.nodes[0].out_end > e.nodes[0].out_begin;
   const char* rc_min = diag_env("FAC_RC_MIN");  // env knobs: tests force it on / pin K, A/B turns it off
   const char* kenv = diag_env("FAC_RC_K");
-  // prefix-cache state the main pass's demand level shares with the setup below
   std::vector<RcTable> tabs;      // built levels, ascending k: a build resumes its representatives from them
-  std::vector<bool> tab_exact;    // built by the exact kernel (else dedup-free: rc_build_kernel_live)
   RcTable L1{0u, 0u, nullptr, nullptr, nullptr, nullptr};
   uint32_t n_ent0 = 0, qbuild = 0;
-  bool live_builds = false;
   uint64_t ct_mult = 4, ct_mult2 = 4;  // lookup slots per entry: levels 0/1 by entries, sampled levels by kept snapshots
-  std::function<int(const RcTable&, uint32_t, const uint64_t*, hipStream_t, bool, bool)> rc_build_fn;
-  std::function<int(RcTable&, uint32_t, const uint64_t*, DevBuf&, hipStream_t, bool)> rc_publish_fn;
-  std::function<int(const DevBuf&, const DevBuf&, const DevBuf&, const DevBuf&, uint32_t, uint32_t, uint32_t, unsigned int&)>
-      rc_number_fn;
   // after its build a level's entries are published into an exact-key lookup table (4 slots per
   // entry: a miss usually ends at the first probe)
   auto ct_slots = [&](uint32_t n_ent, uint64_t mult) {
@@ -4673,7 +4530,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       }
       hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid), dim3(256), 0, stream, P, target(d_rck, d_rcslot, slots, k),
                          RcCountTarget{nullptr, nullptr, 0u, 0u}, RcCountTarget{nullptr, nullptr, 0u, 0u},
-                         stride1, 1u, nullptr, 0u, cprobes);
+                         stride1, 1u, cprobes);
       HIP_TRY(hipGetLastError());
       unsigned int n_keys = 0;
       if (int nrc = number_entries(d_rck, d_rcv, d_rcslot, d_rcrep, slots, 1u, max_ent, n_keys)) return nrc;
@@ -4682,7 +4539,9 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (!kpin && 8ull * n_keys > (windows + stride1 - 1) / stride1) continue;  // too little reuse: fewer chars per key
       n_ent1 = std::min(n_keys, max_ent);
       L1.k = k;
-      P.rc_kstart = diag_env("FAC_RC_DEEPEST") ? 0u : k + 1;  // lookups start at the first sampled level (rc_lookup); knob: A/B
+      // lookups start at the first sampled level (rc_lookup); FAC_RC_DEEPEST (A/B): a start no level
+      // reaches, so st stays at the deepest level and the shallower ones follow deepest first
+      P.rc_kstart = diag_env("FAC_RC_DEEPEST") ? 0xFFFFFFFFu : k + 1;
       if (l0) {  // level-0 keys from the level-1 representatives
         hipLaunchKernelGGL(rc_derive_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_ent1 + 255) / 256, cus * 8))), dim3(256),
                            0, stream, P, static_cast<const uint64_t*>(d_rcrep.p), n_ent1, t1, cprobes);
@@ -4740,23 +4599,15 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         if (e) (void)hipEventDestroy(e);
       }
     } l1_done_guard{l1_done};
-    // sampled levels of beamed engines are built dedup-free (not for the auto-beam count pass, which
-    // needs every window's exact queue.len(), nor with mappings)
-    // Dedup-free ("live") builds of the sampled levels leave every key whose build would beam
-    // uncached, and their snapshots are not exact: a main-pass window that beams after its snapshot
-    // restarts from the deepest exact level. With the reference's beam order (select_nth_unstable_by
-    // scatters the survivors, so the key's horizon comes earlier and more windows beam after it)
-    // that restart dominated (C3: 8.2 M windows restarted from 4-char snapshots, 537 ms per step
-    // against 258 with exact sampled builds). FAC_LIVE_BUILD=1 brings them back (A/B).
-    live_builds = P.beam && !counts && !e.has_map && qbuild <= 256 && diag_env("FAC_LIVE_BUILD") &&
-                             !diag_env("FAC_NO_LIVE_BUILD");
+    // (Dedup-free "live" builds of the sampled levels -- every key whose build would beam left
+    // uncached, inexact snapshots -- lost to the exact builds with the reference's beam order: C3 537
+    // vs 258 ms per step; removed in round 5, git history keeps them.)
     // 4 slots per entry, the sampled levels' per kept snapshot (C3: 5.9 M of 8.2 M 5-char entries kept).
     // 2 per entry cost C2 76.0 vs 71.0 ms (profiles/r04ab); 4 for the sampled levels: C2 71.1 vs 73.5,
     // C4 16.45 vs 17.39, C3 135.9 vs 136.8 against 2 (profiles/r04ac)
     ct_mult = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT", 4)));
     ct_mult2 = std::max<uint64_t>(1, std::min<uint64_t>(8, env_u("FAC_RC_CT_MULT2", 4)));
-    auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, hipStream_t bs, bool cleared = false,
-                     bool sampled = false) -> int {
+    auto build = [&](const RcTable& T, uint32_t n_ent, const uint64_t* reps, hipStream_t bs, bool cleared = false) -> int {
       SearchParams Q = P;
       Q.rc_mode = 2;
       Q.rc_k = T.k;
@@ -4776,7 +4627,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       Q.out_cap = out_cap;
       Q.spill = static_cast<uint64_t*>(d_spill.p);
       Q.spill_cap = spill_cap;
-      Q.counters = static_cast<unsigned long long*>(d_cnt.p) + build_cnt;
+      Q.counters = static_cast<unsigned long long*>(d_cnt.p);
       if (!cleared) HIP_TRY(hipMemsetAsync(Q.counters, 0, N_COUNTERS * sizeof(unsigned long long), bs));
       uint32_t grid = std::min<uint32_t>(n_ent, max_grid);
       if (bs != stream && !diag_env("FAC_L1_PERSIST")) {
@@ -4800,28 +4651,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
                            dim3(256), 0, bs, Q, qk0);
         HIP_TRY(hipGetLastError());
       }
-      const bool live_build = live_builds && sampled && Q.rc_ntab > 0;
-      Q.rc_defer_only = 0;
       uint32_t qk = 256;  // launch_rc_build's ring
       while (qk < qbuild) qk <<= 1;
-      if (int src = prep_slots(Q, bs, qk, !live_build)) return src;
-      if (live_build) {
-        hipLaunchKernelGGL(rc_build_kernel_live, dim3(grid), dim3(64), 0, bs, Q);
-      } else if ((sampled || (T.k == L1.k && diag_env("FAC_BUILD_SMALL_L1"))) && qbuild <= 256 &&
-                 diag_env("FAC_BUILD_SMALL")) {
-        // the sampled levels' keys pop few states and their builds wait on memory: the small variant
-        // (16 waves per CU) first, then the full-size build takes the keys it could not hold
-        Q.rc_defer_fail = 1;
-        hipLaunchKernelGGL(rc_build_kernel_small, dim3(grid), dim3(64), 0, bs, Q);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemsetAsync(Q.counters + 7, 0, sizeof(unsigned long long), bs));
-        Q.rc_defer_fail = 0;
-        Q.rc_defer_only = 1;
-        if (int src = prep_slots(Q, bs, qk, true)) return src;
-        launch_rc_build(qbuild, grid, bs, Q);
-      } else {
-        launch_rc_build(qbuild, grid, bs, Q);
-      }
+      if (int src = prep_slots(Q, bs, qk, true)) return src;
+      launch_rc_build(qbuild, grid, bs, Q);
       const hipError_t le = hipGetLastError();
       if (le != hipSuccess) {
         err = std::string("kernel launch: ") + hipGetErrorString(le);
@@ -4846,9 +4679,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       T.ct_mask = cs - 1;
       return FAC_OK;
     };
-    rc_build_fn = build;  // for the main pass's demand level
-    rc_publish_fn = publish;
-    rc_number_fn = number_entries;
     if (n_ent1) {
       const uint64_t n_all = n_ent0 + n_ent1 + (uint64_t)ks.size() * max_ent2_est;
       const uint64_t budget = env_u("FAC_RC_POOL_MB", 16384ull) << 20;
@@ -4894,7 +4724,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         if (brc) return brc;
         if ((brc = publish(L0, n_ent0, static_cast<const uint64_t*>(d_l0rep.p), d_ct[kRcLevels - 1], bstream, true))) return brc;
         tabs.push_back(L0);
-        tab_exact.push_back(true);
         HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), bstream));
       }
       int brc = build(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p), bstream, true);
@@ -4902,7 +4731,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if ((brc = publish(L1, n_ent1, static_cast<const uint64_t*>(d_rcrep.p), d_ct[0], bstream, true))) return brc;
       if (bstream != stream) HIP_TRY(hipEventRecord(l1_done, bstream));
       tabs.push_back(L1);
-      tab_exact.push_back(true);
       return FAC_OK;
     };
     // Sampled levels: every 2nd window's key, kept when seen twice. With a single sampled level
@@ -4929,21 +4757,12 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     std::vector<RcTable> Lx;        // sampled levels, ascending k
     std::vector<uint32_t> n_entx;   // their entries
     std::vector<size_t> xbuf;       // their count-table buffers
-    const uint32_t bloom_log2 = (uint32_t)std::min<uint64_t>(32, env_u("FAC_RC_BLOOM", 0));  // 0: off
     if (n_ent1 && windows >= env_u("FAC_RC_MIN2", 1ull << 20)) {
       const uint64_t samples = (windows + stride2 - 1) / stride2;
       const uint32_t l2_log2 = (uint32_t)std::min<uint64_t>(27, std::max<uint64_t>(12, env_u("FAC_RC_SLOTS2", 27)));
       uint32_t slots2 = 1u << 12;
       while (slots2 < 2ull * samples && slots2 < (1u << l2_log2)) slots2 <<= 1;
-      uint32_t* seen = nullptr;
-      uint32_t seen_mask = 0;
-      if (bloom_log2 >= 16) {
-        HIP_TRY(d_seen.alloc(((size_t)1 << bloom_log2) / 8, stream));
-        seen = static_cast<uint32_t*>(d_seen.p);
-        seen_mask = (uint32_t)(((uint64_t)1 << bloom_log2) - 1);
-      }
-      // with the bitmap a table count of c means c + 1 sightings
-      const uint32_t thr_t = seen ? std::max<uint32_t>(1, thr2 - 1) : thr2;
+      const uint32_t thr_t = thr2;
       const uint32_t max_ent2 = (uint32_t)std::min<uint64_t>(samples, ent_cap);
       std::vector<uint32_t> kk;  // the levels to count; buffers x = position in kk
       for (uint32_t k2 : ks)
@@ -4959,19 +4778,15 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       if (int lrc = launch_l1()) return lrc;
       for (size_t x = 0; x < kk.size(); ++x) {
         const uint32_t k2 = kk[x];
-        // levels are counted three per pass over the sampled windows (one each with the first-sighting
-        // bitmap, which is per level): with three levels in two passes the second pass ran after the
-        // first one's numbering and held the sampled builds back behind the level-1 build (C3, r03aj)
-        if (seen || x % 3 == 0) {
-          if (seen) HIP_TRY(hipMemsetAsync(seen, 0, ((size_t)seen_mask + 1) / 8, stream));
+        // levels are counted three per pass over the sampled windows: with three levels in two passes
+        // the second pass ran after the first one's numbering and held the sampled builds back behind
+        // the level-1 build (C3, r03aj)
+        if (x % 3 == 0) {
           const RcCountTarget none{nullptr, nullptr, 0u, 0u};
-          const RcCountTarget t1 = (!seen && x + 1 < kk.size())
-                                       ? target(d_xk[x + 1], d_xslot[x + 1], slots2, kk[x + 1]) : none;
-          const RcCountTarget t2 = (!seen && x + 2 < kk.size())
-                                       ? target(d_xk[x + 2], d_xslot[x + 2], slots2, kk[x + 2]) : none;
+          const RcCountTarget t1 = x + 1 < kk.size() ? target(d_xk[x + 1], d_xslot[x + 1], slots2, kk[x + 1]) : none;
+          const RcCountTarget t2 = x + 2 < kk.size() ? target(d_xk[x + 2], d_xslot[x + 2], slots2, kk[x + 2]) : none;
           hipLaunchKernelGGL(rc_count_kernel, dim3(cgrid2), dim3(256), 0, stream, P,
-                             target(d_xk[x], d_xslot[x], slots2, k2), t1, t2, stride2, thr_t, seen, seen_mask,
-                             cprobes);
+                             target(d_xk[x], d_xslot[x], slots2, k2), t1, t2, stride2, thr_t, cprobes);
           HIP_TRY(hipGetLastError());
         }
         unsigned int nk2 = 0;
@@ -4989,7 +4804,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     if (n_ent1) {
       if (bstream != stream) HIP_TRY(hipStreamWaitEvent(stream, l1_done, 0));  // level 1 built and published
       for (size_t x = 0; x < Lx.size(); ++x) {
-        int brc = build(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), stream, false, true);
+        int brc = build(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), stream, false);
         if (brc) return brc;
         // the lookup table is sized for the snapshots the build kept (C3: 5.9 M of 8.2 M 5-char entries,
         // 0.6 M of 5.8 M 7-char ones), read back through the pinned word: tables 4x smaller to clear
@@ -5008,17 +4823,12 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         if ((brc = publish(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), d_ct[1 + x], stream, false,
                            kept, ct_mult2))) return brc;
         tabs.push_back(Lx[x]);
-        tab_exact.push_back(!live_builds);
       }
       // the lookups probe deepest first and stop at the first hit: level 0 is reached only by the
       // windows whose level-1 key the sampled count missed
       P.rc_ntab = 0;
       for (size_t t = tabs.size(); t-- > 0;) P.rc_tab[P.rc_ntab++] = tabs[t];
       P.rc_mode = 1;
-      n_exact_tabs = 0;
-      for (size_t t = tabs.size(); t-- > 0;)
-        if (tab_exact[t]) exact_tab[n_exact_tabs++] = tabs[t];
-      any_inexact = n_exact_tabs < tabs.size();
     }
     HIP_TRY(hipEventRecord(ev.b, stream));
     HIP_TRY(hipStreamSynchronize(stream));
@@ -5078,10 +4888,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     // windows that need 13-16 states (the ones that held a wave longest) go to the dedup-free pass.
     // C3: lane 13.6 -> 7.1 ms, wave 41.0 -> 45.0 ms (133.5 vs 135.7 per step); fresh words 447.5 vs
     // 442.4 (profiles/r04ab/r04ag.txt). Round 2: 16 states against 8, lane 19 + wave 37 ms vs 6 + 58.
-    if (diag_env("FAC_LANE_Q8")) hipLaunchKernelGGL((lane_window_kernel<8, 8>), dim3(lgrid), dim3(64), 0, stream, P);
-    else if (diag_env("FAC_LANE_Q32")) hipLaunchKernelGGL((lane_window_kernel<32, 8>), dim3(lgrid), dim3(64), 0, stream, P);
-    else if (diag_env("FAC_LANE_Q16")) hipLaunchKernelGGL((lane_window_kernel<16, 8>), dim3(lgrid), dim3(64), 0, stream, P);
-    else hipLaunchKernelGGL((lane_window_kernel<12, 8>), dim3(lgrid), dim3(64), 0, stream, P);
+    // (The 8-, 16- and 32-state variants were removed in round 5; git history keeps them.)
+    hipLaunchKernelGGL((lane_window_kernel<12, 8>), dim3(lgrid), dim3(64), 0, stream, P);
     HIP_TRY(hipGetLastError());
     return FAC_OK;
   };
@@ -5093,85 +4901,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
                  "wave_cycles=%llu rounds=%llu\n", d[0], d[1], d[2], lms, P.lane_popmax, d[4], d[5], d[6], d[7]);
     std::memset(d, 0, sizeof(d));
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_lane_dbg), d, sizeof(d)));
-    return FAC_OK;
-  };
-  // Demand level (FAC_RC_DEMAND = k chars; 0: off). The sampled levels count keys over a sample of
-  // every window, most of which the lookups finish; here the keys are counted over exactly the
-  // windows still open after the lookups and the lane kernel -- the ones the wave kernels would
-  // search -- and every key at least two of them share gets a snapshot, built from its
-  // representative's deepest snapshot. The open windows then look the new level up (a hit replaces
-  // their entry's snapshot) and the lane kernel runs again over those it leaves small.
-  const uint32_t demand_k = (uint32_t)(diag_env("FAC_RC_DEMAND") ? std::strtoul(diag_env("FAC_RC_DEMAND"), nullptr, 10) : 0ul);
-  bool demand_done = false;
-  uint32_t demand_keys = 0;
-  auto demand_stage = [&]() -> int {
-    uint32_t kmax = 0;
-    for (const RcTable& t : tabs) kmax = std::max(kmax, t.k);
-    const size_t n_sampled = tabs.size() - 1 - (n_ent0 ? 1 : 0);
-    if (!rc_build_fn || demand_k <= kmax || demand_k > 8 || P.rc_ntab >= (uint32_t)kRcLevels ||
-        1 + n_sampled > (size_t)kRcLevels - 2)
-      return FAC_OK;
-    const int xi = kRcLevels - 2;  // the count buffers the sampled levels leave free
-    uint32_t slots_d = 1u << 12;
-    while (slots_d < std::min<uint64_t>(windows / 2, 1ull << 26)) slots_d <<= 1;
-    const uint32_t max_entd = std::min<uint32_t>(slots_d / 2, 16u << 20);
-    HIP_TRY(d_xk[xi].alloc(slots_d * sizeof(unsigned long long), stream));
-    HIP_TRY(d_xv[xi].alloc(slots_d * sizeof(uint32_t), stream));
-    HIP_TRY(d_xslot[xi].alloc(slots_d * sizeof(uint64_t), stream));
-    HIP_TRY(d_xrep[xi].alloc(max_entd * sizeof(uint64_t), stream));
-    HIP_TRY(d_xc[xi].alloc(2 * (size_t)max_entd * sizeof(uint32_t), stream));
-    HIP_TRY(hipEventRecord(ev.a, stream));
-    HIP_TRY(hipMemsetAsync(d_xk[xi].p, 0, slots_d * sizeof(unsigned long long), stream));
-    const uint64_t n_reg = P.total_windows / RC_REGION;
-    const uint32_t rgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_reg + 3) / 4, (uint64_t)cus * 8));
-    hipLaunchKernelGGL(rc_count_open_kernel, dim3(rgrid), dim3(256), 0, stream, P,
-                       RcCountTarget{static_cast<unsigned long long*>(d_xk[xi].p), static_cast<uint64_t*>(d_xslot[xi].p),
-                                     slots_d - 1, demand_k});
-    HIP_TRY(hipGetLastError());
-    unsigned int nk = 0;
-    if (int nrc = rc_number_fn(d_xk[xi], d_xv[xi], d_xslot[xi], d_xrep[xi], slots_d, 2u, max_entd, nk)) return nrc;
-    demand_keys = std::min(nk, max_entd);
-    if (demand_keys == 0) return FAC_OK;
-    RcTable D{demand_k, slots_d - 1, static_cast<const unsigned long long*>(d_xk[xi].p),
-              static_cast<const uint32_t*>(d_xv[xi].p), static_cast<uint32_t*>(d_xc[xi].p) + max_entd,
-              static_cast<uint32_t*>(d_xc[xi].p)};
-    build_cnt = N_COUNTERS;  // the pass's counters hold its records so far
-    int brc = rc_build_fn(D, demand_keys, static_cast<const uint64_t*>(d_xrep[xi].p), stream, false, true);
-    build_cnt = 0;
-    if (brc) return brc;
-    if ((brc = rc_publish_fn(D, demand_keys, static_cast<const uint64_t*>(d_xrep[xi].p), d_ct[1 + n_sampled], stream, false))) return brc;
-    SearchParams R = P;
-    R.rc_ntab = 1;
-    R.rc_tab[0] = D;
-    hipLaunchKernelGGL(rc_relookup_open_kernel, dim3(rgrid), dim3(256), 0, stream, R);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ev.b, stream));
-    HIP_TRY(hipMemsetAsync(static_cast<unsigned long long*>(d_cnt.p) + 9, 0, sizeof(unsigned long long), stream));
-    if (int lrc = launch_lane()) return lrc;
-    HIP_TRY(hipEventRecord(ev_lane, stream));
-    HIP_TRY(hipEventSynchronize(ev_lane));
-    float a = 0.f, b = 0.f;
-    HIP_TRY(hipEventElapsedTime(&a, ev.a, ev.b));
-    HIP_TRY(hipEventElapsedTime(&b, ev.b, ev_lane));
-    cache_ms += a;
-    lane_ms += b;
-    if (int drc = lane_debug_line(b)) return drc;
-    if (diag_env("FAC_RC_DEBUG"))
-      std::fprintf(stderr, "FAC_RC demand level k=%u keys=%u (seen >= 2 among the open windows) %.3f ms, lane again %.3f ms\n",
-                   demand_k, demand_keys, a, b);
-    // a pass run again (buffer growth) looks it up first
-    for (uint32_t t = P.rc_ntab; t > 0; --t) P.rc_tab[t] = P.rc_tab[t - 1];
-    P.rc_tab[0] = D;
-    ++P.rc_ntab;
-    if (!live_builds) {
-      for (uint32_t t = n_exact_tabs; t > 0; --t) exact_tab[t] = exact_tab[t - 1];
-      exact_tab[0] = D;
-      ++n_exact_tabs;
-    } else {
-      any_inexact = true;
-    }
-    tabs.push_back(D);
-    tab_exact.push_back(!live_builds);
     return FAC_OK;
   };
   const uint64_t rc_auto = P.beam ? 256ull : std::min<uint64_t>(4096, std::max<uint64_t>(256, pass_windows / (16ull * max_grid)));
@@ -5243,10 +4972,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         HIP_TRY(hipEventElapsedTime(&lms, ev.b, ev_lane));
         lane_ms += lms;
         if (int drc = lane_debug_line(lms)) return drc;
-      }
-      if (demand_k && lane_on && !demand_done) {
-        demand_done = true;
-        if (int drc = demand_stage()) return drc;
       }
     }
     if (int src = prep_slots(P, stream, kVariants[vi].qcap, kVariants[vi].vcap > 0)) {
@@ -5365,17 +5090,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       spill_cap = std::max<uint64_t>(spill_cap, pass_windows);
     }
     P.win_list = static_cast<const uint64_t*>(d_list.p);
-    if (P.rc_mode == 1 && any_inexact && kVariants[vi].vcap > 0) {
-      // the exact variant restarts the spilled windows from exact snapshots
-      SearchParams R = P;
-      R.rc_ntab = n_exact_tabs;
-      for (uint32_t t = 0; t < n_exact_tabs; ++t) R.rc_tab[t] = exact_tab[t];
-      R.rc_qcap = kVariants[vi].qcap;
-      hipLaunchKernelGGL(rc_relookup_kernel, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((pass_windows + 255) / 256, (uint64_t)cus * 16))),
-                         dim3(256), 0, stream, R, pass_windows);
-      HIP_TRY(hipGetLastError());
-      any_inexact = false;  // those hits are exact now
-    }
     ++retries;
   }
   if (timing)

@@ -397,18 +397,15 @@ def test_prefix_cache_two_levels_c3_slice(k2, monkeypatch):
     assert len(on) > 0 and sorted(on.tolist()) == sorted(off.tolist()) == sorted(one.tolist())
 
 
-@pytest.mark.parametrize("knobs", [{}, {"FAC_BUILD_SMALL": "1"}, {"FAC_BUILD_SMALL": "1", "FAC_BUILD_SMALL_L1": "1"},
-                                   {"FAC_RC_DEEPEST": "1", "FAC_RC_CT_ENTRIES": "1"}, {"FAC_LANE_Q16": "1"},
+@pytest.mark.parametrize("knobs", [{}, {"FAC_RC_DEEPEST": "1", "FAC_RC_CT_ENTRIES": "1"},
                                    {"FAC_RC_STRIDE2": "1", "FAC_RC_T2": "3"}, {"FAC_RC_T2": "1"}],
-                         ids=["default", "small-build", "small-build-l1", "deepest-first", "lane-ring-16",
-                              "counts-every-window-thr3", "counts-thr1"])
+                         ids=["default", "deepest-first", "counts-every-window-thr3", "counts-thr1"])
 def test_prefix_cache_round4_paths_c3_slice(knobs, monkeypatch):
     """Round-4 prefix-cache paths on a C3-shaped haystack with the sampled levels on: the default
-    (full-size builds, count slots with the count in the key word, 12-state lane rings), the small
-    build variant and the full-size build of the keys it defers, the small variant for level 1 too,
-    the round-3 probe order with entry-sized tables, 16-state lane rings, and the count tables'
-    saturating counts at thresholds 3 (every window counted) and 1 (the representative written at
-    the first sighting): identical records to the cache off, and the deeper levels replaying pops."""
+    (count slots with the count in the key word, 12-state lane rings), the deepest-first probe order
+    with entry-sized tables, and the count tables' saturating counts at thresholds 3 (every window
+    counted) and 1 (the representative written at the first sighting): identical records to the
+    cache off, and the deeper levels replaying pops."""
     from fuzzy_aho_corasick import workloads
     w = workloads.config("c3", 2 << 20, 3)
     staged = workloads.builder_for(w).build(w.patterns).stage(w.haystack)
@@ -422,27 +419,6 @@ def test_prefix_cache_round4_paths_c3_slice(knobs, monkeypatch):
     off, _ = staged.search_windows_records(w.threshold)
     assert st_on.states_cached > st_one.states_cached > 0
     assert len(on) > 0 and sorted(on.tolist()) == sorted(off.tolist()) == sorted(one.tolist())
-
-
-@pytest.mark.parametrize("demand,levels", [("6", "5"), ("7", "5,6"), ("8", "5,7")])
-def test_prefix_cache_demand_level_c3_slice(demand, levels, monkeypatch):
-    """The demand level (keys counted over the windows still open after the lookups and the lane
-    kernel, built from their deepest snapshots, looked up again, lane kernel re-run): identical
-    records to the cache off on a C3-shaped haystack, with the level actually replaying pops."""
-    from fuzzy_aho_corasick import workloads
-    w = workloads.config("c3", 2 << 20, 3)
-    eng = workloads.builder_for(w).build(w.patterns)
-    staged = eng.stage(w.haystack)
-    monkeypatch.setenv("FAC_RC_MIN2", "1")
-    monkeypatch.setenv("FAC_RC_LEVELS", levels)
-    monkeypatch.setenv("FAC_RC_DEMAND", "0")
-    base, st_base = staged.search_windows_records(w.threshold)
-    monkeypatch.setenv("FAC_RC_DEMAND", demand)
-    on, st_on = staged.search_windows_records(w.threshold)
-    monkeypatch.setenv("FAC_NO_RC", "1")
-    off, _ = staged.search_windows_records(w.threshold)
-    assert st_on.states_cached > st_base.states_cached
-    assert len(on) > 0 and sorted(on.tolist()) == sorted(off.tolist()) == sorted(base.tolist())
 
 
 def test_prefix_cache_default_on_c3_slice(monkeypatch):
