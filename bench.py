@@ -137,20 +137,28 @@ def main():
     # default step = search_raw on device-resident input: the UTF-8 bytes are uploaded
     # once (H2D reported apart); every step stages them on the device (UTF-8 check, is_ascii, UAX #29
     # segmentation + folding: fac_haystack_stage_device), searches every start window and delivers
-    # the records. --prestaged (diagnostic) stages once outside the timed steps; --shard stages each
-    # rank's halo-sliced shard once from the host.
-    device_staging = not (args.shard or args.prestaged or args.end_to_end)
-    dev_hay, h2d_ms = None, None
+    # the records. --shard: each rank holds its halo-sliced shard's bytes [a, e) in HBM and stages
+    # them the same way in every step (fac_haystack_stage_shard_device), so the strong-scaling step
+    # is the N = 1 step's work split over the ranks. --prestaged (diagnostic) stages once outside the
+    # timed steps.
+    device_staging = not (args.prestaged or args.end_to_end)
+    dev_hay, h2d_ms, plan = None, None, None
     if device_staging:
         import numpy as np
+        from fuzzy_aho_corasick import _native
+        lo, hi = 0, len(wl.haystack)
+        if args.shard:  # fac_shard_plan on the host bytes, once: (a, b, e, global is_ascii, open end)
+            plan = _native.shard_plan(engine.max_match_graphemes(), wl.haystack, world, rank)
+            lo, hi = plan[0], plan[2]
         torch.cuda.synchronize()
         t = time.perf_counter()
-        dev_hay = torch.from_numpy(np.frombuffer(wl.haystack, dtype=np.uint8)).to(torch.device("cuda", local))
+        dev_hay = torch.from_numpy(np.frombuffer(wl.haystack, dtype=np.uint8)[lo:hi].copy()).to(torch.device("cuda", local))
         torch.cuda.synchronize()
         h2d_ms = (time.perf_counter() - t) * 1e3
-        staged = StagedHaystack.from_device(engine, dev_hay.data_ptr(), len(wl.haystack), stream)
-    elif args.shard:
-        staged = StagedHaystack.shard(engine, wl.haystack, world, rank)
+        if args.shard:
+            staged = StagedHaystack.shard_from_device(engine, dev_hay.data_ptr(), plan, stream)
+        else:
+            staged = StagedHaystack.from_device(engine, dev_hay.data_ptr(), len(wl.haystack), stream)
     else:
         staged = StagedHaystack(engine, wl.haystack)
     windows = staged.owned_windows  # graphemes this rank searches per step
@@ -166,7 +174,10 @@ def main():
         hs = staged
         if device_staging:  # synchronous: its kernels are done on return
             t = time.perf_counter()
-            hs = StagedHaystack.from_device(engine, dev_hay.data_ptr(), len(wl.haystack), stream, reuse=staged)
+            if args.shard:
+                hs = StagedHaystack.shard_from_device(engine, dev_hay.data_ptr(), plan, stream, reuse=staged)
+            else:
+                hs = StagedHaystack.from_device(engine, dev_hay.data_ptr(), len(wl.haystack), stream, reuse=staged)
             stage_ms[0] += (time.perf_counter() - t) * 1e3
         if world == 1:  # records D2H into the library's pooled pinned buffers
             rows, st = (hs.search_prefiltered_records(wl.threshold, stream=stream) if wl.prefilter
@@ -260,10 +271,7 @@ def main():
                 "graphemes_per_gpu": windows,
                 "threshold": wl.threshold,
                 "filler_vocabulary": args.vocab or "fresh",
-                "timed_step": ("search_raw from host bytes (H2D + staging + search + records)" if args.end_to_end else
-                               "search_raw on device-resident bytes: device staging (UTF-8 check, is_ascii, UAX #29 "
-                               "segmentation + folding) + search + records" if device_staging else
-                               "search only (haystack staged before the timed steps)"),
+                "timed_step": timed_step_desc(args),
                 "parallelism": (f"shard{world} (strong: one {len(wl.haystack)}-byte haystack, halo-sliced shards)"
                                 if args.shard else f"dp{world} (weak: one haystack per GPU)")
                                + (", RCCL gather of Match records to rank 0" if world > 1 else ""),
@@ -305,6 +313,17 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def timed_step_desc(args) -> str:
+    """What one timed step covers (the line's config.timed_step)."""
+    if args.end_to_end:
+        return "search_raw from host bytes (H2D + staging + search + records)"
+    if args.prestaged:
+        return "search only (haystack staged before the timed steps)"
+    return ("search_raw on device-resident bytes: device staging (UTF-8 check, is_ascii, UAX #29 segmentation + "
+            "folding" + (" of the rank's halo-sliced shard" if args.shard else "") + ") + search + records"
+            + (" gathered to rank 0 over RCCL" if args.gpus and args.gpus > 1 else ""))
 
 
 def fresh_words_diag(args, engine, nbytes, local, stream, steps=2):
@@ -518,7 +537,7 @@ def run_dry(args, world, rank):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     if rank == 0:
-        cfg = {"workload": "dry-run", "records_gathered_per_step": got}
+        cfg = {"workload": "dry-run", "records_gathered_per_step": got, "timed_step": timed_step_desc(args)}
         if args.shard:
             cfg.update(workload=f"dry-run shard: {args.config} slice of {len(wl.haystack)} bytes, {len(wl.patterns)} patterns, "
                                 "oracle compute", shard_union_equals_whole=parity)

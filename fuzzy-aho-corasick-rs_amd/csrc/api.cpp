@@ -364,6 +364,43 @@ int fac_haystack_stage_device(const fac_engine* engine, const uint8_t* d_utf8, u
   return FAC_OK;
 }
 
+int fac_haystack_stage_shard_device(const fac_engine* engine, const uint8_t* d_utf8, uint64_t len, uint64_t owned_bytes,
+                                    int32_t global_ascii, int32_t open_end, uint64_t base, void* stream, fac_haystack** hay,
+                                    uint64_t* err_graphemes) {
+  if (!engine || !hay || (len && !d_utf8) || owned_bytes > len) return fail(FAC_E_INVALID, "bad argument");
+  fac_haystack* fh = *hay;
+  const bool fresh = fh == nullptr;
+  if (fresh) {
+    fh = new (std::nothrow) fac_haystack();
+    if (!fh) return fail(FAC_E_OOM, "out of host memory");
+  } else if (fh->h.own_utf8 && fh->h.d_utf8) {
+    return fail(FAC_E_INVALID, "haystack was not staged from device memory");
+  }
+  std::string err;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : engine->e.stream;
+  // the whole haystack's is_ascii decides the grapheme mode (search.rs:196); a Unicode shard's bytes
+  // are UTF-8 checked by the segmentation
+  int rc = fac::stage_haystack_device(engine->e, d_utf8, len, fh->h, err, st, global_ascii ? 1 : 0);
+  uint64_t owned = 0;
+  if (!rc) rc = fac::graphemes_before(fh->h, owned_bytes, st, owned, err);
+  if (rc) {
+    if (rc == FAC_E_HAYSTACK_TOO_LARGE && err_graphemes) *err_graphemes = fh->h.failed_n;
+    if (fresh) {
+      fac::free_haystack(fh->h);
+      delete fh;
+    } else {  // a failed restage leaves the haystack empty (searchable)
+      fh->h.n = 0;
+      fh->h.len = 0;
+    }
+    return fail(rc, rc == FAC_E_HAYSTACK_TOO_LARGE ? std::string("haystack has more than u32::MAX grapheme clusters") : err);
+  }
+  fh->h.base = base;
+  fh->h.open_end = open_end != 0;
+  fh->h.owned = owned;
+  *hay = fh;
+  return FAC_OK;
+}
+
 int fac_shard_plan(uint64_t max_match_graphemes, const uint8_t* utf8, uint64_t len, int32_t is_ascii, uint64_t n_shards,
                    uint64_t shard, uint64_t plan[4]) {
   if (!plan || (len && !utf8) || n_shards == 0 || shard >= n_shards) return fail(FAC_E_INVALID, "bad argument");
@@ -531,14 +568,17 @@ int fac_search_raw(const fac_engine* engine, const uint8_t* utf8, uint64_t len, 
 
 namespace {
 
-// scratch device memory of one call
+// scratch device memory of one call on stream s (reused by the thread's later calls on s)
 struct DevMem {
   void* p = nullptr;
+  hipStream_t s = nullptr;
+  explicit DevMem(hipStream_t st) : s(st) {}
   ~DevMem() {
-    if (p) (void)hipFree(p);
+    if (p) fac::call_scratch_give(p, s);
   }
   int alloc(size_t bytes, std::string& err) {
-    const hipError_t he = hipMalloc(&p, std::max<size_t>(bytes, 16));
+    hipError_t he = hipSuccess;
+    p = fac::call_scratch_take(std::max<size_t>(bytes, 16), s, &he);
     if (he != hipSuccess) {
       p = nullptr;
       err = std::string("hipMalloc: ") + hipGetErrorString(he);
@@ -746,7 +786,7 @@ int fac_stream_window_staged_device(const fac_engine* engine, const fac_haystack
   // raw records into a device buffer (grown and searched again if a window ever needs more)
   uint64_t cap = 1u << 16;
   for (;;) {
-    DevMem raw;
+    DevMem raw(st);
     if (int rc = raw.alloc(2 * cap * sizeof(fac_match), err)) return fail(rc, err);
     fac::MatchSink sink;
     sink.dev = static_cast<fac_match*>(raw.p);

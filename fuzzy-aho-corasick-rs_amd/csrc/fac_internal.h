@@ -466,6 +466,12 @@ struct ScratchSet {
 };
 void scratch_bind(ScratchSet* s);  // this thread's searches use `s` (nullptr: the engine's)
 void scratch_free(ScratchSet& s);
+// Short-lived call scratch (rank kernels, stream-window record buffers), reused per host thread: a
+// block given back on stream s is handed out again only for work on s, whose order makes the reuse
+// safe without the device-wide synchronisation a hipFree implies (a per-call hipMalloc/hipFree
+// stalled every other stream once per stream window). Grow-only per size class; freed at thread exit.
+void* call_scratch_take(size_t bytes, hipStream_t s, hipError_t* e);
+void call_scratch_give(void* p, hipStream_t s);
 
 // stream.cpp: the WindowReader state (stream.rs:77-159), the windows in flight and the matches
 // ready to hand out. Windows are cut on the host and searched by `depth` worker threads, each with
@@ -499,6 +505,8 @@ uint64_t stream_committed(const StreamCore& s);  // commit point of the windows 
 // staging of the bytes at h.d_utf8 on the device (stage_kernels.hip): mode -2 checks the UTF-8 and
 // decides is_ascii, 0 stages Unicode graphemes, 1 ASCII (asynchronous after its count sync)
 int stage_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err, int mode);
+// graphemes of a staged haystack that start before byte b (a grapheme boundary), synchronously on st
+int graphemes_before(const Haystack& h, uint64_t b, hipStream_t st, uint64_t& out, std::string& err);
 void ensure_symbols(const Engine& e, const Haystack& h);
 int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int overlap, const uint64_t* unique_ids,
                   std::string& err);
@@ -522,9 +530,11 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
 int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack& h, std::string& err,
                    int force_ascii = -1, hipStream_t stream = nullptr);
 // search_raw's staging of bytes already in device memory (borrowed, not copied): the UTF-8 check,
-// is_ascii, segmentation and folding on the device; h may hold buffers of an earlier staging
+// is_ascii, segmentation and folding on the device; h may hold buffers of an earlier staging.
+// mode -2: decide is_ascii from the bytes; 1 / 0: ASCII / Unicode graphemes as given (a shard of a
+// haystack whose global is_ascii is known; Unicode bytes are UTF-8 checked)
 int stage_haystack_device(const Engine& e, const uint8_t* d_utf8, uint64_t len, Haystack& h, std::string& err,
-                          hipStream_t stream);
+                          hipStream_t stream, int mode = -2);
 // start byte of the n-th grapheme counted from the end of s[0, len) (UAX #29, the whole text's
 // segmentation; stream.rs:134-139 grapheme_indices(true).rev().nth(n - 1)); false if it has fewer
 bool nth_grapheme_from_end(const uint8_t* s, uint64_t len, uint64_t n, uint64_t& off);

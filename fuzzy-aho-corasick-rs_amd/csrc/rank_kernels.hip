@@ -169,12 +169,19 @@ __global__ void gather_kernel(const fac_match* m, const Span* order, uint64_t n,
     }                                                               \
   } while (0)
 
+// stream-ordered call scratch (call_scratch_take): every use below is on the stream it was taken for
+thread_local hipStream_t t_buf_stream = nullptr;
 struct Buf {
   void* p = nullptr;
+  hipStream_t s = t_buf_stream;
   ~Buf() {
-    if (p) (void)hipFree(p);
+    if (p) call_scratch_give(p, s);
   }
-  hipError_t alloc(size_t bytes) { return hipMalloc(&p, std::max<size_t>(bytes, 16)); }
+  hipError_t alloc(size_t bytes) {
+    hipError_t e = hipSuccess;
+    p = call_scratch_take(bytes, s, &e);
+    return e;
+  }
   template <class T>
   T* as() const {
     return static_cast<T*>(p);
@@ -228,6 +235,7 @@ int apply_matches_device(const Engine& e, fac_match* d_a, fac_match* d_b, uint64
   *res = d_a;
   *n_res = n;
   if (n == 0 || (order == 0 && overlap == 0)) return FAC_OK;
+  t_buf_stream = s;
   const uint32_t T = 256;
   const uint32_t G = (uint32_t)((n + T - 1) / T);
   fac_match* ranked = d_a;
@@ -338,6 +346,7 @@ int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int ove
   if (n == 0 || (order == 0 && overlap == 0)) return FAC_OK;
   RK_TRY(hipSetDevice(e.device));
   hipStream_t s = e.stream;
+  t_buf_stream = s;
   Buf d_a, d_b;
   RK_TRY(d_a.alloc(n * sizeof(fac_match)));
   RK_TRY(d_b.alloc(n * sizeof(fac_match)));
@@ -380,6 +389,7 @@ int window_owned_device(const Engine& e, fac_match* d_a, fac_match* d_b, uint64_
   uint64_t nres = 0;
   if (int rc = apply_matches_device(e, d_a, d_b, n, 1, 1, nullptr, s, &res, &nres, err)) return rc;
   if (nres == 0) return FAC_OK;
+  t_buf_stream = s;
   // the owned count first (a prefix of the start-ordered list), then the copy if it fits
   Buf d_cnt, d_tmp;
   RK_TRY(d_cnt.alloc(8));
@@ -397,6 +407,60 @@ int window_owned_device(const Engine& e, fac_match* d_a, fac_match* d_b, uint64_
   if (owned) RK_TRY(hipMemcpyAsync(d_out, d_tmp.p, owned * sizeof(fac_match), hipMemcpyDeviceToDevice, s));
   RK_TRY(hipStreamSynchronize(s));
   return FAC_OK;
+}
+
+namespace {
+struct CallBlock {
+  void* p;
+  size_t bytes;
+  hipStream_t s;
+};
+struct CallPool {
+  std::vector<CallBlock> free_blocks;
+  ~CallPool() {
+    for (const CallBlock& b : free_blocks) (void)hipFree(b.p);
+  }
+};
+thread_local CallPool t_call_pool;
+thread_local std::vector<CallBlock> t_call_live;  // handed out: their sizes for the give-back
+}  // namespace
+
+void* call_scratch_take(size_t bytes, hipStream_t s, hipError_t* e) {
+  size_t cls = 256;
+  while (cls < bytes) cls <<= 1;
+  auto& fb = t_call_pool.free_blocks;
+  for (size_t i = 0; i < fb.size(); ++i)
+    if (fb[i].s == s && fb[i].bytes == cls) {
+      const CallBlock b = fb[i];
+      fb[i] = fb.back();
+      fb.pop_back();
+      t_call_live.push_back(b);
+      *e = hipSuccess;
+      return b.p;
+    }
+  void* p = nullptr;
+  *e = hipMalloc(&p, cls);
+  if (*e != hipSuccess) return nullptr;
+  t_call_live.push_back(CallBlock{p, cls, s});
+  return p;
+}
+
+void call_scratch_give(void* p, hipStream_t s) {
+  for (size_t i = 0; i < t_call_live.size(); ++i)
+    if (t_call_live[i].p == p) {
+      CallBlock b = t_call_live[i];
+      t_call_live[i] = t_call_live.back();
+      t_call_live.pop_back();
+      b.s = s;
+      auto& fb = t_call_pool.free_blocks;
+      fb.push_back(b);
+      if (fb.size() > 64) {  // bounded: the oldest block goes (hipFree orders after its stream's work)
+        (void)hipFree(fb.front().p);
+        fb.erase(fb.begin());
+      }
+      return;
+    }
+  (void)hipFree(p);  // not from the pool
 }
 
 }  // namespace fac

@@ -4057,7 +4057,7 @@ int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack&
 }
 
 int stage_haystack_device(const Engine& e, const uint8_t* d_utf8, uint64_t len, Haystack& h, std::string& err,
-                          hipStream_t stream) {
+                          hipStream_t stream, int mode) {
   HIP_TRY(hipSetDevice(e.device));
   if (h.d_utf8 && h.own_utf8) HIP_TRY(hipFree(h.d_utf8));
   h.device = e.device;
@@ -4079,7 +4079,7 @@ int stage_haystack_device(const Engine& e, const uint8_t* d_utf8, uint64_t len, 
   h.d_gid = nullptr;
   h.gid_engine = nullptr;
   hipStream_t st = stream ? stream : e.stream;
-  int rc = stage_device(e, h, st, err, -2);
+  int rc = stage_device(e, h, st, err, mode);
   if (!rc) {
     const hipError_t se = hipStreamSynchronize(st);
     if (se != hipSuccess) {

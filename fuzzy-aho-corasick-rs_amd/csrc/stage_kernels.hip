@@ -553,11 +553,11 @@ int stage_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err,
   unsigned long long sc[4] = {0, 0, 0, 0};
   ST_TRY(hipMemcpyAsync(sc, scal, sizeof(sc), hipMemcpyDeviceToHost, st));
   ST_TRY(hipStreamSynchronize(st));
+  if (sc[0] & 1ull) {  // seg_tile_kernel checks every code point (modes -2 and 0)
+    err = "haystack is not valid UTF-8";
+    return FAC_E_INVALID;
+  }
   if (mode == -2) {
-    if (sc[0] & 1ull) {
-      err = "haystack is not valid UTF-8";
-      return FAC_E_INVALID;
-    }
     h.ascii = !(sc[0] & 2ull);
     if (h.ascii) {
       h.n = len;
@@ -581,6 +581,33 @@ int stage_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err,
   hipLaunchKernelGGL(write_tile_kernel, dim3((uint32_t)((n_units + 3) / 4)), dim3(256), 0, st, h.d_utf8, len, bits, ubase,
                      n_units, tabs.l, e.case_insensitive ? 1 : 0, h.d_off, h.d_text32);
   ST_TRY(hipGetLastError());
+  return FAC_OK;
+}
+
+// graphemes starting before byte `b` (a grapheme boundary) of a staged Unicode haystack: lower_bound
+// over the device grapheme starts, one thread
+__global__ void starts_before_kernel(const uint64_t* off, uint64_t n, uint64_t b, unsigned long long* out) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (off[mid] < b) lo = mid + 1;
+    else hi = mid;
+  }
+  *out = lo;
+}
+
+int graphemes_before(const Haystack& h, uint64_t b, hipStream_t st, uint64_t& out, std::string& err) {
+  if (h.ascii) {
+    out = std::min(b, h.n);
+    return FAC_OK;
+  }
+  unsigned long long* d = static_cast<unsigned long long*>(h.d_stage);  // scal[3]: free after staging
+  hipLaunchKernelGGL(starts_before_kernel, dim3(1), dim3(1), 0, st, h.d_off, h.n, b, d + 3);
+  ST_TRY(hipGetLastError());
+  unsigned long long v = 0;
+  ST_TRY(hipMemcpyAsync(&v, d + 3, 8, hipMemcpyDeviceToHost, st));
+  ST_TRY(hipStreamSynchronize(st));
+  out = v;
   return FAC_OK;
 }
 

@@ -137,6 +137,9 @@ SIGNATURES = {
                                       ctypes.c_uint64, _P(ctypes.c_uint64)]),
     "fac_haystack_stage_shard": (ctypes.c_int, [_engine_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, _P(_hay_p), _u64p]),
+    "fac_haystack_stage_shard_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                       ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_void_p,
+                                                       ctypes.POINTER(ctypes.c_void_p), _u64p]),
     "fac_haystack_owned_windows": (ctypes.c_uint64, [_hay_p]),
     "fac_stream_window_staged": (ctypes.c_int, [_engine_p, _hay_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_uint64, ctypes.c_float, ctypes.c_int32, ctypes.c_void_p,

@@ -500,6 +500,32 @@ class StagedHaystack:
         plan = _native.shard_plan(engine.max_match_graphemes(), data, n_shards, shard, is_ascii)
         return cls(engine, data, _shard=plan)
 
+    @classmethod
+    def shard_from_device(cls, engine: FuzzyAhoCorasick, d_utf8: int, plan, stream=None,
+                          reuse: "StagedHaystack" = None) -> "StagedHaystack":
+        """fac_haystack_stage_shard_device: shard `plan` (a, b, e, global_ascii, open_end from
+        _native.shard_plan) whose bytes [a, e) are already in HBM at `d_utf8` (borrowed), staged on the
+        device like from_device (the per-step staging of a sharded search_raw). `reuse`: a shard
+        staged this way before, restaged in place."""
+        a, b, e, asc, open_end = plan
+        h = ctypes.c_void_p(reuse._h.value if reuse is not None else None)
+        eg = ctypes.c_uint64()
+        rc = _native.lib.fac_haystack_stage_shard_device(engine._h, ctypes.c_void_p(d_utf8), e - a, b - a, int(asc),
+                                                         int(open_end), a, ctypes.c_void_p(stream or 0),
+                                                         ctypes.byref(h), ctypes.byref(eg))
+        if rc:
+            if reuse is not None:
+                reuse.owned_bytes, reuse.graphemes, reuse.owned_windows = 0, 0, 0
+            _raise(rc, eg.value)
+        obj = reuse
+        if obj is None:
+            obj = cls.__new__(cls)
+            obj.engine, obj.data, obj._h, obj._dev_out = engine, None, h, None
+        obj.base, obj.open_end, obj.plan, obj.owned_bytes = a, open_end, plan, b - a
+        obj.graphemes = int(_native.lib.fac_haystack_graphemes(obj._h))
+        obj.owned_windows = int(_native.lib.fac_haystack_owned_windows(obj._h))
+        return obj
+
     def search_device(self, threshold: float, window_begin: int = 0, window_end: int = None, stream=None,
                       auto_beam_prefix: int = 0, torch_device=None):
         """fac_search_staged_ex with the records left in HBM: (uint8 tensor of n * 32 bytes on the

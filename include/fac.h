@@ -244,6 +244,15 @@ int fac_shard_plan(uint64_t max_match_graphemes, const uint8_t* utf8, uint64_t l
 int fac_haystack_stage_shard(const fac_engine* engine, const uint8_t* utf8, uint64_t len, uint64_t owned_bytes,
                              int32_t global_ascii, int32_t open_end, uint64_t base, fac_haystack** out,
                              uint64_t* err_graphemes);
+/* fac_haystack_stage_shard for a shard whose bytes [a, e) are already in device memory (`d_utf8`,
+ * borrowed like fac_haystack_stage_device's, which it otherwise follows: staging on the device,
+ * ordered on `stream`, complete on return; `*hay` NULL or a haystack this function staged before,
+ * restaged in place). The grapheme mode is the global is_ascii; a Unicode shard's bytes are UTF-8
+ * checked on the device. Replaces nothing in the reference: it is the per-step staging of the
+ * sharded search_raw (search.rs:196-203, 296-302 on each rank's slice). */
+int fac_haystack_stage_shard_device(const fac_engine* engine, const uint8_t* d_utf8, uint64_t len, uint64_t owned_bytes,
+                                    int32_t global_ascii, int32_t open_end, uint64_t base, void* stream, fac_haystack** hay,
+                                    uint64_t* err_graphemes);
 /* start windows a staged haystack owns (all of them unless it is a shard) */
 uint64_t fac_haystack_owned_windows(const fac_haystack* hay);
 

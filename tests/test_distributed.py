@@ -230,6 +230,8 @@ def test_bench_shard_dry_run_plans_and_gathers(config):
     j = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
     assert j["n_gpus"] == 4 and j["config"]["records_gathered_per_step"] > 0
     assert j["config"]["shard_union_equals_whole"] is True
+    # the strong-scaling step stages the rank's shard on the device like the N = 1 step
+    assert "device staging" in j["config"]["timed_step"] and "shard" in j["config"]["timed_step"]
 
 
 def test_bench_rejects_mismatched_world():
@@ -239,7 +241,7 @@ def test_bench_rejects_mismatched_world():
     assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)
 
 
-def _c5_worker(rank, world, port, blocks, out_path, device_style=False):
+def _c5_worker(rank, world, port, blocks, out_path, mode="oracle"):
     sys.path[:0] = [os.path.join(REPO, "fuzzy-aho-corasick-rs_amd"), os.path.join(REPO, "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import numpy as np
@@ -263,11 +265,31 @@ def _c5_worker(rank, world, port, blocks, out_path, device_style=False):
     overlap = max(len(p) for p in wl.patterns) + 1 + 1  # max_match_graphemes() + 1, ASCII
     buf = block + block[:overlap]
     rows = []
-    for (g0, g1, commit, base) in stream_share_windows(total, len(block), rank, overlap, n_shares=world):
-        text = buf[g0:g1]  # stream.rs window_matches: search(sorted, non_overlapping), starts < commit
-        ranked = orc.apply_rows(orc.raw_rows(text, wl.threshold, prefilter=True), Order.Default, Overlap.NonOverlapping)
-        rows += [(s + base, e + base) + tuple(r) for (s, e, *r) in ranked if s < commit]
-    if device_style:  # bench.py's N > 1 path: window records appended to one buffer, gathered from it
+    windows = stream_share_windows(total, len(block), rank, overlap, n_shares=world)
+    if mode != "gpu":
+        for (g0, g1, commit, base) in windows:
+            text = buf[g0:g1]  # stream.rs window_matches: search(sorted, non_overlapping), starts < commit
+            ranked = orc.apply_rows(orc.raw_rows(text, wl.threshold, prefilter=True), Order.Default, Overlap.NonOverlapping)
+            rows += [(s + base, e + base) + tuple(r) for (s, e, *r) in ranked if s < commit]
+    as_rows = lambda t: [(int(r["start"]), int(r["end"]), int(r["pattern_index"]), float(r["similarity"]),  # noqa: E731
+                          int(r["insertions"]), int(r["deletions"]), int(r["substitutions"]), int(r["swaps"]),
+                          int(r["edits"])) for r in t.numpy().view(MATCH_DTYPE)]
+    if mode == "gpu":  # bench.py --config c5 at N > 1 itself: each window's owned records ranked and kept in
+        # one HBM buffer by the native fac_stream_window_staged_device, then gather_device from it
+        import torch
+        from fuzzy_aho_corasick.distributed import gather_device
+        from fuzzy_aho_corasick.engine import StagedHaystack
+        staged = StagedHaystack(W.builder_for(wl).device(0).build(wl.patterns), buf)
+        dev = torch.empty(64, dtype=torch.uint8, device="cuda:0")  # too small: grown by the call
+        n = 0
+        for (g0, g1, commit, base) in windows:
+            dev, got_n, _ = staged.stream_window_device(g0, g1, commit, base, wl.threshold, True, dev, n)
+            n += got_n
+        torch.cuda.synchronize()
+        t = gather_device(dev, n, 0)  # gloo: the records leave HBM for the host wire
+        got = None if t is None else as_rows(t)
+    elif mode == "oracle-buffer":  # a CPU mimic of that path: the oracle's window records appended to one
+        # growing buffer (as stream_window_device grows its HBM buffer), gathered from it
         import torch
         from fuzzy_aho_corasick.distributed import gather_device
         recs = np.zeros(len(rows), dtype=MATCH_DTYPE)
@@ -281,9 +303,7 @@ def _c5_worker(rank, world, port, blocks, out_path, device_style=False):
                 buf = g
             buf[i * 32: (i + 1) * 32].copy_(torch.from_numpy(recs[i: i + 1].view(np.uint8).copy()))
         t = gather_device(buf, len(recs), 0)
-        got = None if t is None else [(int(r["start"]), int(r["end"]), int(r["pattern_index"]), float(r["similarity"]),
-                                       int(r["insertions"]), int(r["deletions"]), int(r["substitutions"]),
-                                       int(r["swaps"]), int(r["edits"])) for r in t.numpy().view(MATCH_DTYPE)]
+        got = None if t is None else as_rows(t)
     else:
         got = gather_rows(rows)
     if rank == 0:
@@ -295,8 +315,8 @@ def _c5_worker(rank, world, port, blocks, out_path, device_style=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,device_style", [(2, False), (4, False), (2, True)])
-def test_c5_stream_shares_equal_whole_stream_cpu(world, device_style):
+@pytest.mark.parametrize("world,mode", [(2, "oracle"), (4, "oracle"), (2, "oracle-buffer")])
+def test_c5_stream_shares_equal_whole_stream_cpu(world, mode):
     """bench.py --config c5's cut (stream_share_windows: one contiguous share per rank, windows at
     block and share edges with max_match_graphemes() + 1 of overlap, each searched like stream.rs
     window_matches with the pre-filter and owning the matches that start in it), the oracle as each
@@ -304,7 +324,21 @@ def test_c5_stream_shares_equal_whole_stream_cpu(world, device_style):
     (tests.rs:1058-1142: streaming equals whole input for needles spaced past the overlap)."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res.txt")
-        mp.spawn(_c5_worker, args=(world, _free_port(), 5, out, device_style), nprocs=world, join=True)
+        mp.spawn(_c5_worker, args=(world, _free_port(), 5, out, mode), nprocs=world, join=True)
+        got, full = eval(open(out).read())
+    assert len(full) >= 30
+    assert got == full
+
+
+@pytest.mark.gpu
+def test_c5_stream_shares_device_buffer_gpu():
+    """bench.py --config c5's N > 1 path on the product: two ranks (both on cuda:0, gloo for the
+    exchange) search their shares' stream windows with fac_stream_window_staged_device into one HBM
+    record buffer each (grown from a too-small one), gathered to rank 0 with gather_device == the whole
+    stream searched by the oracle sorted().non_overlapping()."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res.txt")
+        mp.spawn(_c5_worker, args=(2, _free_port(), 5, out, "gpu"), nprocs=2, join=True)
         got, full = eval(open(out).read())
     assert len(full) >= 30
     assert got == full

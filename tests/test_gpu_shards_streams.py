@@ -52,6 +52,41 @@ def test_shards_union_equals_whole(config, nbytes, shards):
         assert rows_key(got) == want, (config, n)
 
 
+@pytest.mark.parametrize("config,nbytes,n", [("c3", 96 << 10, 3), ("c2", 256 << 10, 4)])
+def test_device_staged_shards_equal_host_staged(config, nbytes, n):
+    """bench.py --shard's per-step staging: each rank's shard bytes [a, e) held in HBM and staged on
+    the device (fac_haystack_stage_shard_device, global is_ascii, owned windows counted on the
+    device), restaged in place twice: the same graphemes, owned windows and records as the host-staged
+    shard, and the union over the shards == the whole haystack. A Unicode shard that is all ASCII
+    still stages as graphemes ("\r\n" is one cluster) when the whole haystack is not ASCII."""
+    import torch
+    from fuzzy_aho_corasick import _native
+    wl = W.config(config, nbytes)
+    eng = W.builder_for(wl).device(0).build(wl.patterns)
+    want = rows_key(StagedHaystack(eng, wl.haystack).search_windows(wl.threshold)[0])
+    got = []
+    for r in range(n):
+        plan = _native.shard_plan(eng.max_match_graphemes(), wl.haystack, n, r)
+        host = StagedHaystack.shard(eng, wl.haystack, n, r)
+        dev = torch.from_numpy(np.frombuffer(wl.haystack, np.uint8)[plan[0]:plan[2]].copy()).cuda()
+        sh = StagedHaystack.shard_from_device(eng, dev.data_ptr(), plan)
+        for _ in range(2):
+            sh = StagedHaystack.shard_from_device(eng, dev.data_ptr(), plan, reuse=sh)
+            assert (sh.graphemes, sh.owned_windows) == (host.graphemes, host.owned_windows)
+            rows = sh.search_windows(wl.threshold)[0]
+            assert rows_key(rows) == rows_key(host.search_windows(wl.threshold)[0])
+        got += rows
+    assert rows_key(got) == want and len(want) > 20
+    # an ASCII-only shard of a Unicode haystack: graphemes, not bytes
+    data = ("ab\r\ncd " * 50 + "école \r\n" * 50).encode()
+    plan = _native.shard_plan(eng.max_match_graphemes(), data, 2, 0)
+    assert plan[3] is False
+    dev = torch.from_numpy(np.frombuffer(data, np.uint8)[plan[0]:plan[2]].copy()).cuda()
+    sh = StagedHaystack.shard_from_device(eng, dev.data_ptr(), plan)
+    host = StagedHaystack.shard(eng, data, 2, 0)
+    assert (sh.graphemes, sh.owned_windows) == (host.graphemes, host.owned_windows)
+
+
 def test_search_device_equals_host_records():
     wl, b = _c3_slice(64 << 10)
     eng = b.build(wl.patterns)
