@@ -1702,7 +1702,7 @@ __device__ __forceinline__ fac_match match_record(const SearchParams& P, const S
 
 constexpr uint32_t claim_slots(uint32_t vcap) { return vcap / 2 < 512 ? 512 : vcap / 2; }  // >= ExpScratch
 
-__device__ unsigned long long g_live_dbg[8];  // diagnostics (FAC_RC_DEBUG): live-dedup checks / hits
+__device__ unsigned long long g_live_dbg[12];  // diagnostics (FAC_RC_DEBUG): live-dedup checks / hits, spills
 __device__ unsigned long long g_bad[8];       // diagnostics (FAC_RC_DEBUG): uncached keys by reason
 __device__ unsigned long long g_lk_dbg[16];   // diagnostics (FAC_RC_DEBUG): main lookups by level x final, misses, skips
 #ifdef FAC_WIN_HIST  // diagnostics build (make hist): windows, pops and cycles by pops per window
@@ -1768,6 +1768,7 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
 #endif
                            ) {
   const uint32_t lane = lane_id();
+  const uint64_t popped_w0 = popped;  // diagnostics: this window's pops
   if constexpr (LIVE)  // a window resuming with a long queue would most likely beam: the exact variant takes it
     if (P.live_nqmax && rc.off != EMPTY && rc.tail - rc.head > P.live_nqmax) {
       err |= ERR_QUEUE;
@@ -1862,6 +1863,13 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
       // never shorter than the dedup queue at the same pop). Here it would: the window is spilled
       // and re-run from its start (snapshot) on a dedup variant.
       err |= ERR_QUEUE;
+      if (P.lane_debug && lane == 0) {  // spilled windows: their live pops, snapshot queue, pops / queue at the spill
+        atomicAdd(&g_live_dbg[6], 1ull);
+        atomicAdd(&g_live_dbg[7], (unsigned long long)(popped - popped_w0));
+        atomicAdd(&g_live_dbg[8], (unsigned long long)(rc.off != EMPTY ? rc.tail - rc.head : 1u));
+        atomicAdd(&g_live_dbg[9], (unsigned long long)(tail - (rc.off != EMPTY ? rc.head : 0u)));
+        if (tail - (rc.off != EMPTY ? rc.head : 0u) <= QCAP) atomicAdd(&g_live_dbg[10], 1ull);
+      }
       break;
     }
     // cache build: stop before the first state that reads text past the key
@@ -3549,6 +3557,7 @@ struct QgramParams {
   const uint32_t* pm;      // per pattern: m | k << 8
   uint32_t rows;
   uint32_t* cover;
+  const uint32_t* bits;    // QG_BITS_WORDS: screening bitmap of the grams (qgram_bit)
 };
 __host__ __device__ inline uint32_t qgram_key(uint32_t a, uint32_t b, uint32_t c, uint32_t d, bool q4) {
   return q4 ? (a | (b << 8) | (c << 16) | (d << 24)) : (a | (b << 8) | (c << 16) | 0xFF000000u);
@@ -3571,28 +3580,28 @@ __device__ __forceinline__ uint32_t qgram_find(const QgramParams& Q, uint32_t ke
   }
 }
 
+// The screening bitmap's hash (64 Kbit, bit = the top 16 bits of a multiplicative hash: one multiply
+// per gram; the table probe behind it keeps qgram_hash). Built on the host, copied into LDS per block.
+__host__ __device__ inline uint32_t qgram_bit(uint32_t key) { return (key * 0x9E3779B1u) >> 16; }
+constexpr uint32_t QG_BITS_WORDS = 2048;
+
 // Candidates collect in a per-wave LDS buffer and go out 512 at a time (one list atomic per flush: a
 // same-address atomic per wave turn serialised the scan at one L2 channel, 175 ms per GiB)
 constexpr uint32_t QG_BUF = 512;
-// A 64 Kbit LDS bitmap of the grams' hashes (bit = hash >> 16) screens every position first: only
-// the ~3 % that pass (C5) probe the table in global memory.
-constexpr uint32_t QG_PQ = 128;  // per-wave probe queue (LDS)
+// The bitmap screens every position first: only the ~3 % that pass (C5) probe the table in global
+// memory, 64 at a time from a per-wave LDS queue (one table round trip per 64 passing grams: probing
+// where they stood cost a round trip per wave step, since some lane of 64 passes almost every one).
+// Round 5: a thread's 8 grams (4 positions x 3-/4-gram) are screened together into a pass mask, and
+// the passes join the queue in rounds of one per lane (one ballot per round; round 2 is rare) instead
+// of a ballot per gram.
+constexpr uint32_t QG_PQ = 128;  // per-wave probe queue (LDS): < 64 left after a drain + one round
 __global__ __launch_bounds__(256) void qgram_scan_kernel(QgramParams Q) {
   __shared__ unsigned long long s_buf[4][QG_BUF];
-  __shared__ uint32_t s_bits[2048];
+  __shared__ uint32_t s_bits[QG_BITS_WORDS];
   __shared__ uint32_t s_pk[4][QG_PQ];
   __shared__ uint64_t s_pp[4][QG_PQ];
-  for (uint32_t x = threadIdx.x; x < 2048; x += blockDim.x) s_bits[x] = 0u;
+  for (uint32_t x = threadIdx.x; x < QG_BITS_WORDS; x += blockDim.x) s_bits[x] = Q.bits[x];
   __syncthreads();
-  for (uint32_t x = threadIdx.x; x <= Q.tab_mask; x += blockDim.x) {
-    const uint2 e = Q.tab[x];
-    if (e.y) {
-      const uint32_t b = qgram_hash(e.x) >> 16;
-      atomicOr(&s_bits[b >> 5], 1u << (b & 31u));
-    }
-  }
-  __syncthreads();
-  auto maybe = [&](uint32_t key) { const uint32_t b = qgram_hash(key) >> 16; return (s_bits[b >> 5] >> (b & 31u)) & 1u; };
   unsigned long long* buf = s_buf[threadIdx.x / 64];
   uint32_t nb = 0;  // wave-uniform
   auto flush = [&]() {
@@ -3605,9 +3614,6 @@ __global__ __launch_bounds__(256) void qgram_scan_kernel(QgramParams Q) {
     __builtin_amdgcn_wave_barrier();
     nb = 0;
   };
-  // Positions whose gram passes the bitmap are queued per wave in LDS and probed 64 at a time, one
-  // per lane: probing each of a thread's 8 grams where it stands cost 8 dependent table round trips
-  // per wave step (some lane of 64 passes almost every one), the scan's whole time.
   uint32_t* pk = s_pk[threadIdx.x / 64];
   uint64_t* pp = s_pp[threadIdx.x / 64];
   uint32_t nq = 0;  // wave-uniform
@@ -3643,17 +3649,6 @@ __global__ __launch_bounds__(256) void qgram_scan_kernel(QgramParams Q) {
         if (dst != Q.cand || at < Q.cap) dst[at] = (pos << 24) | ((h >> 8) + y);
     }
   };
-  auto push = [&](bool pass, uint32_t key, uint64_t pos) {  // wave-uniform call
-    const uint64_t m = __ballot(pass);
-    if (!m) return;
-    if (nq + 64 > QG_PQ) drain(false);
-    if (pass) {
-      const uint32_t at = nq + prefix_below(m);
-      pk[at] = key;
-      pp[at] = pos;
-    }
-    nq += (uint32_t)__popcll(m);
-  };
   // a thread takes 4 consecutive positions from two aligned words of symbols (the ids buffer is
   // padded past n; positions whose gram would cross n are not looked up)
   const uint32_t* ids32 = reinterpret_cast<const uint32_t*>(Q.ids);
@@ -3663,15 +3658,37 @@ __global__ __launch_bounds__(256) void qgram_scan_kernel(QgramParams Q) {
   for (uint64_t g0 = base0 - threadIdx.x % 64; g0 < nq4; g0 += stride) {  // whole waves iterate together
     const uint64_t g = g0 + (threadIdx.x % 64);
     const uint64_t w = g < nq4 ? (((uint64_t)ids32[g + 1] << 32) | ids32[g]) : 0ull;
+    // pass mask: bit 2j = the 4-gram at position 4g + j, bit 2j + 1 = its 3-gram
+    uint32_t pm = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
       const uint64_t i = 4 * g + j;
-      const uint32_t a = (uint32_t)(w >> (8 * j)) & 0xFFu, b = (uint32_t)(w >> (8 * j + 8)) & 0xFFu;
-      const uint32_t c = (uint32_t)(w >> (8 * j + 16)) & 0xFFu, d = (uint32_t)(w >> (8 * j + 24)) & 0xFFu;
-      const uint32_t k4 = qgram_key(a, b, c, d, true), k3 = qgram_key(a, b, c, 0u, false);
-      push(g < nq4 && Q.use4 && i + 4 <= Q.n && maybe(k4), k4, i);
-      push(g < nq4 && Q.use3 && i + 3 <= Q.n && maybe(k3), k3, i);
+      const uint32_t k4 = (uint32_t)(w >> (8 * j)), k3 = (k4 & 0xFFFFFFu) | 0xFF000000u;
+      const uint32_t b4 = qgram_bit(k4), b3 = qgram_bit(k3);
+      const bool p4 = Q.use4 && i + 4 <= Q.n && ((s_bits[b4 >> 5] >> (b4 & 31u)) & 1u);
+      const bool p3 = Q.use3 && i + 3 <= Q.n && ((s_bits[b3 >> 5] >> (b3 & 31u)) & 1u);
+      pm |= (p4 ? 1u : 0u) << (2 * j);
+      pm |= (p3 ? 1u : 0u) << (2 * j + 1);
     }
+    if (g >= nq4) pm = 0;
+    // rounds: each lane's next pass joins the queue (in lane order within a round)
+    for (;;) {
+      const bool has = pm != 0;
+      const uint64_t m = __ballot(has);
+      if (!m) break;
+      if (nq + 64 > QG_PQ) drain(false);
+      if (has) {
+        const uint32_t bit = (uint32_t)__builtin_ctz(pm);
+        pm &= pm - 1;
+        const uint32_t j = bit >> 1;
+        const uint32_t k4 = (uint32_t)(w >> (8 * j));
+        const uint32_t at = nq + prefix_below(m);
+        pk[at] = (bit & 1u) ? ((k4 & 0xFFFFFFu) | 0xFF000000u) : k4;
+        pp[at] = 4 * g + j;
+      }
+      nq += (uint32_t)__popcll(m);
+    }
+    if (nq >= 64) drain(false);
   }
   drain(true);
   if (nb) flush();
@@ -3697,32 +3714,46 @@ __global__ __launch_bounds__(256) void qgram_verify_kernel(QgramParams Q, uint64
   uint64_t r[KMAX + 1];
 #pragma unroll
   for (int d = 0; d <= KMAX; ++d) r[d] = d ? ((1ull << d) - 1ull) : 0ull;  // prefilter.rs:415-418
-  for (uint64_t i = s0; i < e_max; ++i) {
-    const uint64_t bc = mask[Q.ids[i]];
-    uint64_t prev_old = r[0];
-    uint64_t prev_new = ((r[0] << 1) | 1ull) & bc;
-    r[0] = prev_new;
-    uint64_t hit = (k == 0) ? prev_new : 0ull;
+  // symbols 8 at a time: their loads, then their masks' loads, go out together (one pair of memory
+  // round trips per 8 symbols instead of per symbol); the recurrence then steps through them
+  constexpr uint32_t U = 8;
+  for (uint64_t i0 = s0; i0 < e_max; i0 += U) {
+    uint32_t sym[U];
 #pragma unroll
-    for (int d = 1; d <= KMAX; ++d) {
-      const uint64_t old = r[d];
-      const uint64_t nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | 1ull;
-      r[d] = nv;
-      prev_old = old;
-      prev_new = nv;
-      if ((uint32_t)d == k) hit = nv;
-    }
-    const uint64_t end = i + 1;
-    if (end >= e_min && (hit & top)) {  // coverage [end - m - k, end), as bitap_kernel
-      const uint64_t span = (uint64_t)m + k;
-      const uint64_t ws = end > span ? end - span : 0;
-      for (uint64_t y = ws; y < end;) {
-        const uint64_t w = y >> 5;
-        const uint32_t l = (uint32_t)(y & 31);
-        const uint32_t cnt = (uint32_t)min((uint64_t)(32 - l), end - y);
-        const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << l;
-        atomicOr(Q.cover + w, bits);
-        y += cnt;
+    for (uint32_t u = 0; u < U; ++u) sym[u] = i0 + u < e_max ? Q.ids[i0 + u] : 0u;
+    uint64_t bcs[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) bcs[u] = mask[sym[u]];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint64_t i = i0 + u;
+      if (i >= e_max) break;
+      const uint64_t bc = bcs[u];
+      uint64_t prev_old = r[0];
+      uint64_t prev_new = ((r[0] << 1) | 1ull) & bc;
+      r[0] = prev_new;
+      uint64_t hit = (k == 0) ? prev_new : 0ull;
+#pragma unroll
+      for (int d = 1; d <= KMAX; ++d) {
+        const uint64_t old = r[d];
+        const uint64_t nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | 1ull;
+        r[d] = nv;
+        prev_old = old;
+        prev_new = nv;
+        if ((uint32_t)d == k) hit = nv;
+      }
+      const uint64_t end = i + 1;
+      if (end >= e_min && (hit & top)) {  // coverage [end - m - k, end), as bitap_kernel
+        const uint64_t span = (uint64_t)m + k;
+        const uint64_t ws = end > span ? end - span : 0;
+        for (uint64_t y = ws; y < end;) {
+          const uint64_t w = y >> 5;
+          const uint32_t l = (uint32_t)(y & 31);
+          const uint32_t cnt = (uint32_t)min((uint64_t)(32 - l), end - y);
+          const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << l;
+          atomicOr(Q.cover + w, bits);
+          y += cnt;
+        }
       }
     }
   }
@@ -4999,10 +5030,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     {
       std::fprintf(stderr, "FAC_RC launch windows=%llu resumed=%llu lane_flushed=%llu lane_searched=%llu popped=%llu\n",
                    (unsigned long long)pass_windows, cnt[5], cnt[6], cnt[8], cnt[1]);
-      unsigned long long d[8];
+      unsigned long long d[12];
       HIP_TRY(hipMemcpyFromSymbol(d, HIP_SYMBOL(g_live_dbg), sizeof(d)));
-      std::fprintf(stderr, "FAC_LIVE lane checks=%llu hits=%llu | wave checks=%llu hits=%llu windows with/without live entries=%llu/%llu\n",
-                   d[0], d[1], d[2], d[3], d[4], d[5]);
+      std::fprintf(stderr, "FAC_LIVE lane checks=%llu hits=%llu | wave checks=%llu hits=%llu windows with/without live entries=%llu/%llu"
+                   " | spills=%llu spill_pops=%llu spill_snapq=%llu spill_pushed=%llu spill_ring_intact=%llu\n",
+                   d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10]);
       std::memset(d, 0, sizeof(d));
       HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_live_dbg), d, sizeof(d)));
     }
@@ -5353,7 +5385,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     else hipLaunchKernelGGL((bitap_kernel<24, uint64_t>), bgrid, dim3(256), 0, stream, B);
   }
   HIP_TRY(hipGetLastError());
-  DevBuf d_qtab, d_qent, d_qmask, d_qpm, d_qcand, d_qn;
+  DevBuf d_qtab, d_qent, d_qmask, d_qpm, d_qcand, d_qn, d_qbits;
   if (!grams.empty()) {
     std::vector<uint32_t> ent(grams.size());
     std::vector<std::pair<uint32_t, uint32_t>> keys;  // (key, first entry << 8 | entries)
@@ -5369,6 +5401,11 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
       while (tab[sl].y) sl = (sl + 1) & (ts - 1);
       tab[sl] = make_uint2(kv.first, kv.second);
     }
+    std::vector<uint32_t> qbits(QG_BITS_WORDS, 0u);  // the scan's screening bitmap
+    for (const auto& kv : keys) {
+      const uint32_t b = qgram_bit(kv.first);
+      qbits[b >> 5] |= 1u << (b & 31u);
+    }
     std::vector<uint32_t> pm(np, 0);
     uint32_t kq = 0;
     bool use3 = false, use4 = false;
@@ -5382,6 +5419,8 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     HIP_TRY(d_qent.alloc(ent.size() * 4, stream));
     HIP_TRY(d_qmask.alloc(e.bp_mask.size() * 8, stream));
     HIP_TRY(d_qpm.alloc(pm.size() * 4, stream));
+    HIP_TRY(d_qbits.alloc(qbits.size() * 4, stream));
+    HIP_TRY(hipMemcpyAsync(d_qbits.p, qbits.data(), qbits.size() * 4, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipMemcpyAsync(d_qtab.p, tab.data(), tab.size() * sizeof(uint2), hipMemcpyHostToDevice, stream));
     HIP_TRY(hipMemcpyAsync(d_qent.p, ent.data(), ent.size() * 4, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipMemcpyAsync(d_qmask.p, e.bp_mask.data(), e.bp_mask.size() * 8, hipMemcpyHostToDevice, stream));
@@ -5400,6 +5439,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     Q.pm = static_cast<const uint32_t*>(d_qpm.p);
     Q.rows = rows;
     Q.cover = static_cast<uint32_t*>(d_cover.p);
+    Q.bits = static_cast<const uint32_t*>(d_qbits.p);
     int cus = 256;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
     const uint32_t sgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, (uint64_t)cus * 16));
