@@ -3591,9 +3591,9 @@ constexpr uint32_t QG_BUF = 512;
 // The bitmap screens every position first: only the ~3 % that pass (C5) probe the table in global
 // memory, 64 at a time from a per-wave LDS queue (one table round trip per 64 passing grams: probing
 // where they stood cost a round trip per wave step, since some lane of 64 passes almost every one).
-// Round 5: a thread's 8 grams (4 positions x 3-/4-gram) are screened together into a pass mask, and
-// the passes join the queue in rounds of one per lane (one ballot per round; round 2 is rare) instead
-// of a ballot per gram.
+// Round 5: a thread's 32 grams (16 positions x 3-/4-gram, one 16-byte load) are screened together
+// into a pass mask, and the passes join the queue in rounds of one per lane (one ballot per round)
+// instead of a ballot per gram.
 constexpr uint32_t QG_PQ = 128;  // per-wave probe queue (LDS): < 64 left after a drain + one round
 __global__ __launch_bounds__(256) void qgram_scan_kernel(QgramParams Q) {
   __shared__ unsigned long long s_buf[4][QG_BUF];
@@ -3649,28 +3649,55 @@ __global__ __launch_bounds__(256) void qgram_scan_kernel(QgramParams Q) {
         if (dst != Q.cand || at < Q.cap) dst[at] = (pos << 24) | ((h >> 8) + y);
     }
   };
-  // a thread takes 4 consecutive positions from two aligned words of symbols (the ids buffer is
-  // padded past n; positions whose gram would cross n are not looked up)
+  // a thread takes 16 consecutive positions from one aligned 16-byte load plus the next word (the ids
+  // buffer is padded 32 bytes past n; positions whose gram would cross n are not looked up); the
+  // next turn's loads are issued before this turn's screening
+  const uint4* ids16 = reinterpret_cast<const uint4*>(Q.ids);
   const uint32_t* ids32 = reinterpret_cast<const uint32_t*>(Q.ids);
-  const uint64_t nq4 = (Q.n + 3) / 4;  // position quads
+  const uint64_t n16 = (Q.n + 15) / 16;  // position sixteens
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t base0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (uint64_t g0 = base0 - threadIdx.x % 64; g0 < nq4; g0 += stride) {  // whole waves iterate together
-    const uint64_t g = g0 + (threadIdx.x % 64);
-    const uint64_t w = g < nq4 ? (((uint64_t)ids32[g + 1] << 32) | ids32[g]) : 0ull;
-    // pass mask: bit 2j = the 4-gram at position 4g + j, bit 2j + 1 = its 3-gram
-    uint32_t pm = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-      const uint64_t i = 4 * g + j;
-      const uint32_t k4 = (uint32_t)(w >> (8 * j)), k3 = (k4 & 0xFFFFFFu) | 0xFF000000u;
-      const uint32_t b4 = qgram_bit(k4), b3 = qgram_bit(k3);
-      const bool p4 = Q.use4 && i + 4 <= Q.n && ((s_bits[b4 >> 5] >> (b4 & 31u)) & 1u);
-      const bool p3 = Q.use3 && i + 3 <= Q.n && ((s_bits[b3 >> 5] >> (b3 & 31u)) & 1u);
-      pm |= (p4 ? 1u : 0u) << (2 * j);
-      pm |= (p3 ? 1u : 0u) << (2 * j + 1);
+  const uint64_t lane64 = threadIdx.x % 64;
+  uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x - lane64;  // whole waves iterate together
+  uint4 an = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t xn = 0;
+  if (g0 + lane64 < n16) {
+    an = ids16[g0 + lane64];
+    xn = ids32[4 * (g0 + lane64) + 4];
+  }
+  for (; g0 < n16; g0 += stride) {
+    const uint64_t g = g0 + lane64;
+    const uint32_t w0 = an.x, w1 = an.y, w2 = an.z, w3 = an.w, w4 = xn;
+    if (g0 + stride + lane64 < n16) {  // prefetch
+      an = ids16[g0 + stride + lane64];
+      xn = ids32[4 * (g0 + stride + lane64) + 4];
     }
-    if (g >= nq4) pm = 0;
+    // symbols j .. j + 3 of this thread's sixteen (value selects: a select of references became a
+    // pointer array in scratch)
+    auto gram4 = [w0, w1, w2, w3, w4](uint32_t j) -> uint32_t {
+      const uint32_t q = j >> 2;
+      uint32_t lo = w0, hi = w1;
+      lo = q >= 1u ? w1 : lo;
+      hi = q >= 1u ? w2 : hi;
+      lo = q >= 2u ? w2 : lo;
+      hi = q >= 2u ? w3 : hi;
+      lo = q >= 3u ? w3 : lo;
+      hi = q >= 3u ? w4 : hi;
+      return __builtin_amdgcn_alignbyte(hi, lo, j & 3u);
+    };
+    // pass mask: bit 2j = the 4-gram at position 16g + j, bit 2j + 1 = its 3-gram
+    uint32_t pm = 0;
+    if (g < n16) {
+#pragma unroll
+      for (uint32_t j = 0; j < 16; ++j) {
+        const uint64_t i = 16 * g + j;
+        const uint32_t k4 = gram4(j), k3 = (k4 & 0xFFFFFFu) | 0xFF000000u;
+        const uint32_t b4 = qgram_bit(k4), b3 = qgram_bit(k3);
+        const bool p4 = Q.use4 && i + 4 <= Q.n && ((s_bits[b4 >> 5] >> (b4 & 31u)) & 1u);
+        const bool p3 = Q.use3 && i + 3 <= Q.n && ((s_bits[b3 >> 5] >> (b3 & 31u)) & 1u);
+        pm |= (p4 ? 1u : 0u) << (2 * j);
+        pm |= (p3 ? 1u : 0u) << (2 * j + 1);
+      }
+    }
     // rounds: each lane's next pass joins the queue (in lane order within a round)
     for (;;) {
       const bool has = pm != 0;
@@ -3681,10 +3708,10 @@ __global__ __launch_bounds__(256) void qgram_scan_kernel(QgramParams Q) {
         const uint32_t bit = (uint32_t)__builtin_ctz(pm);
         pm &= pm - 1;
         const uint32_t j = bit >> 1;
-        const uint32_t k4 = (uint32_t)(w >> (8 * j));
+        const uint32_t k4 = gram4(j);
         const uint32_t at = nq + prefix_below(m);
         pk[at] = (bit & 1u) ? ((k4 & 0xFFFFFFu) | 0xFF000000u) : k4;
-        pp[at] = 4 * g + j;
+        pp[at] = 16 * g + j;
       }
       nq += (uint32_t)__popcll(m);
     }
@@ -3694,7 +3721,8 @@ __global__ __launch_bounds__(256) void qgram_scan_kernel(QgramParams Q) {
   if (nb) flush();
 }
 
-template <int KMAX>
+// W: the automaton word, uint32_t when every q-gram pattern has m <= 32 (half the 64-bit VALU work)
+template <int KMAX, typename W>
 __global__ __launch_bounds__(256) void qgram_verify_kernel(QgramParams Q, uint64_t n_cand) {
   const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (x >= n_cand) return;
@@ -3710,10 +3738,10 @@ __global__ __launch_bounds__(256) void qgram_verify_kernel(QgramParams Q, uint64
   const uint64_t warm = (uint64_t)m + k;
   const uint64_t s0 = e_min - 1 > warm ? e_min - 1 - warm : 0;
   const uint64_t* mask = Q.pmask + (size_t)p * Q.rows;
-  const uint64_t top = 1ull << (m - 1);
-  uint64_t r[KMAX + 1];
+  const W top = (W)1 << (m - 1);
+  W r[KMAX + 1];
 #pragma unroll
-  for (int d = 0; d <= KMAX; ++d) r[d] = d ? ((1ull << d) - 1ull) : 0ull;  // prefilter.rs:415-418
+  for (int d = 0; d <= KMAX; ++d) r[d] = d ? (((W)1 << d) - (W)1) : (W)0;  // prefilter.rs:415-418
   // symbols 8 at a time: their loads, then their masks' loads, go out together (one pair of memory
   // round trips per 8 symbols instead of per symbol); the recurrence then steps through them
   constexpr uint32_t U = 8;
@@ -3721,22 +3749,22 @@ __global__ __launch_bounds__(256) void qgram_verify_kernel(QgramParams Q, uint64
     uint32_t sym[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) sym[u] = i0 + u < e_max ? Q.ids[i0 + u] : 0u;
-    uint64_t bcs[U];
+    W bcs[U];
 #pragma unroll
-    for (uint32_t u = 0; u < U; ++u) bcs[u] = mask[sym[u]];
+    for (uint32_t u = 0; u < U; ++u) bcs[u] = (W)mask[sym[u]];
 #pragma unroll
     for (uint32_t u = 0; u < U; ++u) {
       const uint64_t i = i0 + u;
       if (i >= e_max) break;
-      const uint64_t bc = bcs[u];
-      uint64_t prev_old = r[0];
-      uint64_t prev_new = ((r[0] << 1) | 1ull) & bc;
+      const W bc = bcs[u];
+      W prev_old = r[0];
+      W prev_new = ((r[0] << 1) | (W)1) & bc;
       r[0] = prev_new;
-      uint64_t hit = (k == 0) ? prev_new : 0ull;
+      W hit = (k == 0) ? prev_new : (W)0;
 #pragma unroll
       for (int d = 1; d <= KMAX; ++d) {
-        const uint64_t old = r[d];
-        const uint64_t nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | 1ull;
+        const W old = r[d];
+        const W nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | (W)1;
         r[d] = nv;
         prev_old = old;
         prev_new = nv;
@@ -4934,13 +4962,18 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_lane_dbg), d, sizeof(d)));
     return FAC_OK;
   };
-  const uint64_t rc_auto = P.beam ? 256ull : std::min<uint64_t>(4096, std::max<uint64_t>(256, pass_windows / (16ull * max_grid)));
-  const uint32_t rc_chunk = (uint32_t)std::min<unsigned long>(4096, std::max<unsigned long>(64,
+  // Few windows (the pre-filter's merged windows, small slices): chunks shrink until every wave slot
+  // gets two, down to one window -- 256-window chunks left C5's re-search of ~20 K windows per GiB to
+  // ~70 waves, 3.2 ms per stream window (round 5, profiles/r05b)
+  const uint64_t base_chunk = std::min<uint64_t>(256, std::max<uint64_t>(1, pass_windows / (2ull * max_grid)));
+  const uint64_t rc_auto = P.beam ? base_chunk
+                                  : std::min<uint64_t>(4096, std::max<uint64_t>(base_chunk, pass_windows / (16ull * max_grid)));
+  const uint32_t rc_chunk = (uint32_t)std::min<unsigned long>(4096, std::max<unsigned long>(1,
       diag_env("FAC_RC_CHUNK") ? std::strtoul(diag_env("FAC_RC_CHUNK"), nullptr, 10) : rc_auto));
   for (;;) {
     // spilled windows are few and heavy: one per block turn; behind the prefix-cache lookups most
     // windows are done, so chunks are larger (fewer hand-out atomics; the group prescan skips them)
-    P.chunk = P.win_list ? 1u : (P.rc_mode == 1 ? rc_chunk : 256u);
+    P.chunk = P.win_list ? 1u : (P.rc_mode == 1 ? rc_chunk : (uint32_t)base_chunk);
     P.total_windows = pass_windows;
     const uint64_t want = (pass_windows + P.chunk - 1) / P.chunk;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, max_grid));
@@ -5249,7 +5282,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
   if (n == 0) return FAC_OK;
   const uint32_t np = (uint32_t)e.bp_m.size();
   DevBuf d_ids, d_k, d_cover, d_runs, d_cnt;
-  HIP_TRY(d_ids.alloc(n + 16, stream));
+  HIP_TRY(d_ids.alloc(n + 32, stream));  // padded: the scan's 16-byte loads and next word
   if (view.ascii) {  // transcode, ASCII text (prefilter.rs:253-258): one byte per grapheme
     const uint64_t threads = (n + 15) / 16;
     hipLaunchKernelGGL(transcode_ascii_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, stream,
@@ -5407,12 +5440,13 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
       qbits[b >> 5] |= 1u << (b & 31u);
     }
     std::vector<uint32_t> pm(np, 0);
-    uint32_t kq = 0;
+    uint32_t kq = 0, mq = 0;  // largest edit budget / pattern length on the q-gram path
     bool use3 = false, use4 = false;
     for (uint32_t i = 0; i < np; ++i)
       if (qlen[i]) {
         pm[i] = e.bp_m[i] | (ks[i] << 8);
         kq = std::max(kq, ks[i]);
+        mq = std::max(mq, e.bp_m[i]);
         (qlen[i] == 4 ? use4 : use3) = true;
       }
     HIP_TRY(d_qtab.alloc(tab.size() * sizeof(uint2), stream));
@@ -5442,7 +5476,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     Q.bits = static_cast<const uint32_t*>(d_qbits.p);
     int cus = 256;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
-    const uint32_t sgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, (uint64_t)cus * 16));
+    const uint32_t sgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 4095) / 4096, (uint64_t)cus * 16));
     uint64_t qcap = std::max<uint64_t>(1 << 20, n / 16);
     unsigned long long nc = 0;
     for (;;) {  // candidates: one scan, again with room for all of them if the list overflowed
@@ -5459,11 +5493,19 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     }
     if (nc) {
       const dim3 vg((uint32_t)((nc + 255) / 256));
-      if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-      else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-      else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-      else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-      else hipLaunchKernelGGL((qgram_verify_kernel<24>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+      if (mq <= 32) {
+        if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+        else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+        else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+        else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+        else hipLaunchKernelGGL((qgram_verify_kernel<24, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+      } else {
+        if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint64_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+        else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint64_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+        else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint64_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+        else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint64_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+        else hipLaunchKernelGGL((qgram_verify_kernel<24, uint64_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+      }
       HIP_TRY(hipGetLastError());
     }
     if (diag_env("FAC_RC_DEBUG"))
