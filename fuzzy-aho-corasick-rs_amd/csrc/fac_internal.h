@@ -275,19 +275,6 @@ struct SearchParams {
   uint32_t* rc_count;               // build: queued states of each entry (EMPTY: not cached)
   int32_t rc_keep_final;            // build: snapshot a key whose parent is final too (its level is
                                     // looked up without the parent's: level 1 over level 0)
-  // family builds (rc_family_kernel): a level's entries sorted by their parent snapshot
-  // (fam_key: its pool offset, fam_ent: the entry), the positions where a family starts (fam_heads,
-  // *fam_nheads of them), and the children a family could not build, built alone afterwards
-  const uint32_t* fam_key;
-  const uint32_t* fam_ent;
-  const uint32_t* fam_heads;
-  const unsigned int* fam_nheads;
-  uint32_t* fam_retry;
-  unsigned int* fam_nretry;
-  uint32_t fam_n;
-  const uint32_t* ent_list;         // build: the entry of each list position (null: position = entry)
-  const unsigned int* n_list_dev;   // build: the list's length in device memory (null: total_windows)
-  int32_t fam_debug;                // diagnostics (FAC_FAM_DEBUG, tiny inputs): printf of every snapshot built
   // multi-character mappings (search.rs:776-780, 883-922, 945-961; builder.rs:383-442). With
   // has_map, exact and swap transitions compare whole folded graphemes (ids, 0 = not in the
   // engine's grapheme dictionary): edge_gid per edge, text gids per grapheme (gid32 for Unicode
@@ -485,9 +472,6 @@ void scratch_free(ScratchSet& s);
 // stalled every other stream once per stream window). Grow-only per size class; freed at thread exit.
 void* call_scratch_take(size_t bytes, hipStream_t s, hipError_t* e);
 void call_scratch_give(void* p, hipStream_t s);
-// rank_kernels.hip: (key, value) u32 pairs sorted by the key's bits [0, end_bit) (rocprim radix sort)
-int sort_pairs_u32(const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout, uint64_t n, int end_bit,
-                   hipStream_t s, std::string& err);
 
 // stream.cpp: the WindowReader state (stream.rs:77-159), the windows in flight and the matches
 // ready to hand out. Windows are cut on the host and searched by `depth` worker threads, each with

@@ -18,7 +18,6 @@
 #include <cstring>
 
 #include <rocprim/device/device_merge_sort.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <set>
 #include <unordered_set>
@@ -338,19 +337,6 @@ int apply_matches_device(const Engine& e, fac_match* d_a, fac_match* d_b, uint64
                      out);
   RK_TRY(hipGetLastError());
   *res = out;
-  return FAC_OK;
-}
-
-// (key, value) pairs sorted by key (radix, bits [0, end_bit)), stable, on stream s
-int sort_pairs_u32(const uint32_t* kin, uint32_t* kout, const uint32_t* vin, uint32_t* vout, uint64_t n, int end_bit,
-                   hipStream_t s, std::string& err) {
-  if (n == 0) return FAC_OK;
-  t_buf_stream = s;
-  size_t bytes = 0;
-  RK_TRY(rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vin, vout, (unsigned int)n, 0, end_bit, s));
-  Buf tmp;
-  RK_TRY(tmp.alloc(bytes));
-  RK_TRY(rocprim::radix_sort_pairs(tmp.p, bytes, kin, kout, vin, vout, (unsigned int)n, 0, end_bit, s));
   return FAC_OK;
 }
 

@@ -1249,18 +1249,9 @@ struct Prep {
 };
 constexpr uint32_t PF_SUB = 1u, PF_DEL = 2u, PF_LAST = 4u, PF_CSB = 8u, PF_NEXT = 16u, PF_CUR = 32u, PF_SWAP = 64u,
                    PF_EX = 128u, PF_INS = 256u;
-// Family builds (rc_family_kernel): a boundary state (j = Kp - 1 of a family whose
-// parent key has Kp chars) is expanded once for every child key, whose chars differ only in text[Kp]
-// -- read by the swap and the last edit's next-char filters alone. Its pushes are the union over the
-// children, tagged where a child's char decides: PF_FAM marks the lane, PF_SWPH a swap placeholder.
-constexpr uint32_t PF_FAM = 512u, PF_SWPH = 1024u;
-constexpr uint32_t FAM_REQ_SB = 1u << 31;  // pushed node kept iff it has a single-byte edge for the child's char
-constexpr uint32_t FAM_SWAP = 1u << 30;    // swap from this node: goto(goto(node, child char), text[Kp - 1])
-constexpr uint32_t FAM_NODE = (1u << 30) - 1;
 
-template <bool FAM = false>
 __device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState& st, const DevNode& nd, uint64_t start,
-                          uint32_t c0, uint32_t c1, uint4 own_sb, bool fam = false) {  // c0/c1: text at j / j + 1 (0 past the end)
+                          uint32_t c0, uint32_t c1, uint4 own_sb) {  // c0/c1: text at j / j + 1 (0 past the end)
   Prep r{0u, 0u, 0u, 0u, 0.0f};
   const bool fast = P.mef != 255u;
   const uint64_t n = S.n;
@@ -1274,11 +1265,11 @@ __device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState&
   const bool in_text = j < n;
   r.cur_ch = in_text ? c0 : 0u;
   bool have_next = false;
-  if (in_text && is_last_edit && (!fast || edits < P.mef) && j + 1 < n && !(FAM && fam)) {  // :758-765
+  if (in_text && is_last_edit && (!fast || edits < P.mef) && j + 1 < n) {  // :758-765
     have_next = true;
     r.next_ch = c1;
   }
-  bool subst_ok = false, swap_ok = false, ins_ok = false, del_ok = false, swap_ph = false;
+  bool subst_ok = false, swap_ok = false, ins_ok = false, del_ok = false;
   if (in_text) {
     if (fast) {
       subst_ok = edits < P.mef;
@@ -1288,11 +1279,6 @@ __device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState&
                        : (edits == 0 && ((packed >> 16) & 0xFFu) == 0);
     }
     swap_ok = j + 1 < n && P.p_swp <= r.remaining && (!fast || edits < P.mef);  // :935-937
-    if constexpr (FAM)
-      if (fam) {  // the child's char decides: a placeholder (j + 1 < n, too, is the child's)
-        swap_ph = P.p_swp <= r.remaining && (!fast || edits < P.mef);
-        swap_ok = false;
-      }
     if (swap_ok) r.nch = c1;
     if ((me_rel != 0u || j_rel != 0u) && P.p_ins <= r.remaining) {  // :994-1007
       if (fast) {
@@ -1301,7 +1287,7 @@ __device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState&
         const Lim m = pick_limits(P, nlim);
         ins_ok = m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.ins, packed & 0xFFu)) : false;
       }
-      if (ins_ok && is_last_edit && !node_has_out(nd) && !(FAM && fam)) ins_ok = have_next && sb_word_bit(own_sb, r.next_ch);
+      if (ins_ok && is_last_edit && !node_has_out(nd)) ins_ok = have_next && sb_word_bit(own_sb, r.next_ch);
     }
   }
   if (P.p_del <= r.remaining) {  // :1035-1045
@@ -1320,7 +1306,7 @@ __device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState&
                  : 0u) |
             (have_next ? PF_NEXT : 0u) |
             (is_last_edit && in_text ? PF_CUR : 0u) | (swap_ok ? PF_SWAP : 0u) | (in_text ? PF_EX : 0u) |
-            (ins_ok ? PF_INS : 0u) | (FAM && fam ? PF_FAM : 0u) | (swap_ph ? PF_SWPH : 0u);
+            (ins_ok ? PF_INS : 0u);
   return r;
 }
 
@@ -1373,7 +1359,7 @@ __device__ __forceinline__ int unit_owner(ExpScratch* X, uint32_t R, uint32_t nu
 // the units of all states are dealt to lanes in rounds of 64 (a lane-per-state loop would run
 // for the batch's largest degree). Per edge: the exact/swap first-char match (structs.rs:512-519),
 // substitution (:814-874) and deletion (:1055-1088) keep tests incl. the last-edit dead-end filter.
-template <uint32_t UK, bool MAP, bool FAM = false>
+template <uint32_t UK, bool MAP>
 __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode& nd, const Prep& pr, bool act,
                              uint64_t& msub, uint64_t& mdel, uint32_t& ex, uint32_t& xe) {
   const uint32_t lane = lane_id();
@@ -1382,8 +1368,7 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
   const uint32_t uincl = wave_inclusive_sum(nunit);
   const uint32_t ubase = uincl - nunit;
   const uint32_t U = (uint32_t)__builtin_amdgcn_readlane((int)uincl, 63);
-  // flags 9 bits, deg <= 64 (7 bits), ubase < 4096 (12 bits), bit 28: a family boundary lane
-  const uint32_t pk = (pr.flags & 0x1FFu) | (deg << 9) | (ubase << 16) | ((FAM && (pr.flags & PF_FAM)) ? (1u << 28) : 0u);
+  const uint32_t pk = pr.flags | (deg << 9) | (ubase << 16);  // flags 9 bits, deg <= 64, ubase < 4096
   // the words may hold dedup claims of the previous batch
   X->msub[lane] = 0ull;
   X->mdel[lane] = 0ull;
@@ -1400,7 +1385,7 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
       gc = __shfl(pr.gcur, o);
       gn = __shfl(pr.gnx, o);
     }
-    const uint32_t o_deg = (o_pk >> 9) & 0x7Fu, e0 = (R + lane - ((o_pk >> 16) & 0xFFFu)) * UK;
+    const uint32_t o_deg = (o_pk >> 9) & 0x7Fu, e0 = (R + lane - (o_pk >> 16)) * UK;
     const bool sub_on = o_pk & PF_SUB, del_ok = o_pk & PF_DEL, is_last = o_pk & PF_LAST, need_csb = o_pk & PF_CSB;
     const bool have_next = o_pk & PF_NEXT, have_cur = o_pk & PF_CUR, swap_ok = o_pk & PF_SWAP, ex_on = o_pk & PF_EX;
     uint32_t sb = 0, db = 0, fe = 0u, fx = 0u;  // fe/fx: exx encodings of the unit's first matches
@@ -1425,8 +1410,7 @@ __device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode
       fx = (ok && swap_ok && fx == 0u && msw) ? enc : fx;
       const float sim = similarity(P, ed.ch, cur);
       const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
-      // a family boundary lane keeps every last-edit substitution (tagged per child by push_units)
-      const bool sb_next = child_out || (FAM && (o_pk & (1u << 28))) || (have_next && sb_word_bit(csb, nxt));
+      const bool sb_next = child_out || (have_next && sb_word_bit(csb, nxt));
       const bool sb_cur = child_out || (have_cur && sb_word_bit(csb, cur));
       // the exact edge's bit is cleared by the owner once the first match is known
       const bool keep_sub = ok && sub_on && !(sim < P.min_sym) && !(penalty > rem) && (!is_last || sb_next);
@@ -1474,7 +1458,6 @@ __device__ __forceinline__ bool no_subs(const SearchParams& P, const DevNode& nd
   return __fmul_rn(P.p_sub, __fsub_rn(1.0f, P.sim_ascii[128u * 128u + cur])) > remaining;
 }
 
-template <bool FAM = false>
 __device__ void expand_fast(const SearchParams& P, const KState& st, const DevNode& nd, const Prep& pr, uint4 aux,
                             uint64_t& msub, uint64_t& mdel, uint32_t& ex, uint32_t& xe) {
   const uint32_t deg = node_deg(nd);
@@ -1509,15 +1492,13 @@ __device__ void expand_fast(const SearchParams& P, const KState& st, const DevNo
   }
   if (h1 && ((uint32_t)(g1 >> 48) >> (ch_filt_bit(pr.cur_ch) & 15u) & 1u))
     xe = ((63u - ((uint32_t)(g1 >> 32) & 0xFFu)) << 26) | (uint32_t)(g1 & CHILD26_MASK);
-  // (a family boundary lane keeps every last-edit substitution: the child's char decides, push_units tags)
-  const bool filt = is_last && !(FAM && (pr.flags & PF_FAM));
-  msub = (sub_on && P.p_sub <= pr.remaining) ? (dm & ~exbit & (filt ? (cout | s1) : ~0ull)) : 0ull;  // else no_subs
+  msub = (sub_on && P.p_sub <= pr.remaining) ? (dm & ~exbit & (is_last ? (cout | s1) : ~0ull)) : 0ull;  // else no_subs
   mdel = del_ok ? (dm & (is_last ? (cout | s0) : ~0ull)) : 0ull;
 }
 
 // Per-state completion: exact successor, the exact edge leaves the substitution set, swap target
 // goto(goto(node, text[j+1]), text[j]) (:945-967), push count.
-template <bool MAP, bool FAM = false>
+template <bool MAP>
 __device__ LaneExp lane_finish(const SearchParams& P, const SegDesc& S, uint64_t start, const KState& st,
                                const DevNode& nd, const Prep& pr, uint64_t msub, uint64_t mdel, uint32_t ex,
                                uint32_t xe, unsigned& err) {
@@ -1540,8 +1521,6 @@ __device__ LaneExp lane_finish(const SearchParams& P, const SegDesc& S, uint64_t
       if (!(m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.swp, packed >> 24)) : false)) x.swap = -1;
     }
   }
-  if constexpr (FAM)  // family boundary lane: the swap's target is each child's (resolved at its snapshot)
-    if (pr.flags & PF_SWPH) x.swap = (int64_t)(st.node | FAM_SWAP);
   x.ins = (pr.flags & PF_INS) != 0;
   if constexpr (MAP)  // inside the substitution block (:883), i.e. j < n and subst_ok
     if (pr.flags & PF_SUB) x.mmap = map_mask(P, S, st.node, start + (st.jm & 0xFFFFu), st.pen, err);
@@ -1574,9 +1553,9 @@ __device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t r) {
 // substitutions (edge order), swap, insertion, deletions (edge order), written at the state's
 // exclusive-prefix offset. The owner lane writes exact/swap/insertion; substitutions and deletions
 // are written by the units that cover their edges (balanced like expand_units).
-template <uint32_t QCAP, uint32_t UK, bool MAP, bool FAM = false>
+template <uint32_t QCAP, uint32_t UK, bool MAP>
 __device__ void push_units(const SearchParams& P, ExpScratch* X, KState* q, uint32_t base, const KState& st,
-                           const DevNode& nd, const LaneExp& x, uint32_t cur_ch, bool act, bool famlast = false) {
+                           const DevNode& nd, const LaneExp& x, uint32_t cur_ch, bool act) {
   const uint32_t lane = lane_id();
   const float pen = st.pen;
   const uint32_t j_rel = st.jm & 0xFFFFu;
@@ -1594,9 +1573,7 @@ __device__ void push_units(const SearchParams& P, ExpScratch* X, KState* q, uint
     }
     if (nins) {
       const uint32_t jmi = (j_rel + 1u) | ((st.jm >> 16) << 16);
-      // family boundary, last edit: kept iff the node emits or has a single-byte edge for the child's char
-      const uint32_t tag = (FAM && famlast && !node_has_out(nd)) ? FAM_REQ_SB : 0u;
-      q[(sw_pos + nsw) & (QCAP - 1)] = KState{st.node | tag, jmi, __fadd_rn(pen, P.p_ins), st.packed + 1u};
+      q[(sw_pos + nsw) & (QCAP - 1)] = KState{st.node, jmi, __fadd_rn(pen, P.p_ins), st.packed + 1u};
     }
     if constexpr (MAP)
       if (x.mmap) {  // mapping pushes, after the substitutions (:883-922)
@@ -1628,8 +1605,6 @@ __device__ void push_units(const SearchParams& P, ExpScratch* X, KState* q, uint
     const uint32_t o_sb = __shfl(sub_base, o), o_db = __shfl(del_base, o), o_cur = __shfl(cur_ch, o);
     const float o_pen = __shfl(pen, o);
     const uint32_t o_jm = __shfl(st.jm, o), o_packed = __shfl(st.packed, o);
-    bool o_fl = false;
-    if constexpr (FAM) o_fl = __shfl(famlast ? 1 : 0, o) != 0;
     if (valid) {
       const uint32_t k = R + lane - o_fb;
       const bool is_sub = k < o_ns;
@@ -1641,10 +1616,7 @@ __device__ void push_units(const SearchParams& P, ExpScratch* X, KState* q, uint
         const float sim = similarity(P, ed.ch, o_cur);
         const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
         const uint32_t o_j1 = (o_jm & 0xFFFFu) + 1u;
-        // family boundary, last edit: a child without outputs is kept iff it has a single-byte edge
-        // for the child key's char (the next-char dead-end filter, :839-847)
-        const uint32_t tag = (FAM && o_fl && !(ed.next & EDGE_CHILD_OUTPUT)) ? FAM_REQ_SB : 0u;
-        q[(o_sb + r) & (QCAP - 1)] = KState{child | tag, o_j1 | (o_j1 << 16), __fadd_rn(o_pen, penalty), o_packed + 0x10000u};
+        q[(o_sb + r) & (QCAP - 1)] = KState{child, o_j1 | (o_j1 << 16), __fadd_rn(o_pen, penalty), o_packed + 0x10000u};
       } else {
         q[(o_db + r) & (QCAP - 1)] = KState{child, o_jm, __fadd_rn(o_pen, P.p_del), o_packed + 0x100u};
       }
@@ -1730,10 +1702,7 @@ __device__ __forceinline__ fac_match match_record(const SearchParams& P, const S
 
 constexpr uint32_t claim_slots(uint32_t vcap) { return vcap / 2 < 512 ? 512 : vcap / 2; }  // >= ExpScratch
 
-__device__ unsigned long long g_live_dbg[12];
-// diagnostics (FAC_RC_DEBUG): family builds -- children stopped by a beam, an empty queue, an untagged
-// head, a tagged head (j >= Kp / j < Kp); children retried; forks passed; resumed runs
-__device__ unsigned long long g_fam_dbg[8];  // diagnostics (FAC_RC_DEBUG): live-dedup checks / hits, spills
+__device__ unsigned long long g_live_dbg[12];  // diagnostics (FAC_RC_DEBUG): live-dedup checks / hits, spills
 __device__ unsigned long long g_bad[8];       // diagnostics (FAC_RC_DEBUG): uncached keys by reason
 __device__ unsigned long long g_lk_dbg[16];   // diagnostics (FAC_RC_DEBUG): main lookups by level x final, misses, skips
 #ifdef FAC_WIN_HIST  // diagnostics build (make hist): windows, pops and cycles by pops per window
@@ -1789,22 +1758,11 @@ __global__ void slot_init_kernel(unsigned int* ring, unsigned int* ctr, uint32_t
 // window itself runs dedup-free, which cannot change results while no beam triggers -- except against
 // states popped before the snapshot, whose subtrees a beam may have pruned (live_dup).
 constexpr uint32_t LIVE_CAP = 256;
-// FAM (rc_family_kernel): the parent snapshot rc of a family of child keys of Kp + 1 chars (kfam =
-// Kp) is resumed for the whole family: states with j = Kp - 1, the boundary, read the child's char as
-// their lookahead and push the union of the children's successors, tagged (FAM_REQ_SB / FAM_SWAP).
-// The run pops untagged states with j < Kp and returns before the first other head state (a fork:
-// tagged, or j >= Kp) or before a pop whose union pending count passes 2 bw (fr->beam); fr carries
-// the run's state across the forks (fr->resume: continue from it instead of the snapshot).
-struct FamRun {
-  uint32_t head, tail, vcount, jp1, jbeam, resume, beam;
-  uint32_t allow;  // tagged ring entries every running child drops (at least): the union may pass 2 bw by that
-};
-template <uint32_t VCAP, uint32_t QCAP, bool MAP, bool LIVE = false, bool FAM = false>
+template <uint32_t VCAP, uint32_t QCAP, bool MAP, bool LIVE = false>
 __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegDesc& S, KState* vis, KState* q, uint32_t* claim,
                            uint32_t& cseq, EmitList& EL, uint64_t start, const RcHit& rc, uint64_t& popped,
                            uint64_t& cached, unsigned& err, uint32_t& head_out, uint32_t& vcount_out,
-                           KState* live = nullptr, uint32_t* jbeam_out = nullptr, uint4* bsel = nullptr,
-                           uint32_t kfam = 0, FamRun* fr = nullptr
+                           KState* live = nullptr, uint32_t* jbeam_out = nullptr, uint4* bsel = nullptr
 #ifdef FAC_PHASE_PROF
                            , uint64_t* prof_acc = nullptr  // the wave's accumulators (bfs_window_body), added up at its end
 #endif
@@ -1821,13 +1779,10 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
   // FAC_PHASE_PROF slots: 12: per-edge states, 13: fast states, 14: committed, 15: loaded, 16-19: Bc
   // buckets, 20: prologue (table clear, snapshot load), 21: flush
   PROF_T(t_win);
-  bool resume = false;
-  if constexpr (FAM) resume = fr->resume != 0;
   if constexpr (VCAP > 0)
-    if (!resume)
-      for (uint32_t i = lane; i < VCAP; i += 64) vis[i].node = EMPTY;
+    for (uint32_t i = lane; i < VCAP; i += 64) vis[i].node = EMPTY;
   uint32_t vcount = 0;
-  if (!resume) EL.n = 0;
+  EL.n = 0;
   uint32_t head = 0, tail = 1;
   // LIVE: the snapshot's entries a popped state may still meet have j < jlive (0: none); the table is
   // filled on the first batch that holds such a state (live_loaded), most windows never need it
@@ -1845,20 +1800,12 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
   // states) and reduced over the wave only at beam events and at the end
   uint32_t jp1 = 0, jbeam = 0;
   const bool track_beam = P.rc_mode == 2 && P.beam;
-  if (track_beam && rc.off != EMPTY && !resume) {
+  if (track_beam && rc.off != EMPTY) {
     const uint4 h1 = P.rc_pool[rc.off + 1];
     jbeam = h1.z;
     jp1 = h1.w;
   }
-  if (resume) {
-    if constexpr (FAM) {
-      head = fr->head;
-      tail = fr->tail;
-      vcount = fr->vcount;
-      jp1 = fr->jp1;
-      jbeam = fr->jbeam;
-    }
-  } else if (rc.off != EMPTY) {  // prefix cache hit: resume from the snapshot of the key's representative
+  if (rc.off != EMPTY) {  // prefix cache hit: resume from the snapshot of the key's representative
     const uint4* src = P.rc_pool + rc.off + RC_HDR;  // queue, dedup entries, best list (header in rc)
     head = rc.head;
     tail = rc.tail;
@@ -1898,20 +1845,11 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     q[0] = KState{0u, 0u, 0.0f, 0u};
   }
   __builtin_amdgcn_wave_barrier();
-  uint32_t beam2 = 2u * P.beam;
-  if constexpr (FAM) beam2 += fr->allow;
+  const uint32_t beam2 = 2u * P.beam;
   PROF_ACC(20, t_win);
 
   while (head < tail) {
     PROF_T(t0);
-    if constexpr (FAM) {  // a fork (the family body decides which children stop), or a beam
-      const KState h0 = q[head & (QCAP - 1)];
-      if ((h0.node & (FAM_REQ_SB | FAM_SWAP)) || (h0.jm & 0xFFFFu) >= kfam) break;
-      if (P.beam && tail - head > beam2) {
-        fr->beam = 1;
-        break;
-      }
-    }
     if constexpr (VCAP > 0) {
       if (P.beam && tail - head > beam2) {
         if (P.beam_canonical) beam_select_canonical<QCAP>(q, head, tail, P.beam);  // diagnostics
@@ -1935,20 +1873,13 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
       break;
     }
     // cache build: stop before the first state that reads text past the key
-    if (!FAM && P.rc_mode == 2 && (q[head & (QCAP - 1)].jm & 0xFFFFu) + 1u >= P.rc_k) break;
+    if (P.rc_mode == 2 && (q[head & (QCAP - 1)].jm & 0xFFFFu) + 1u >= P.rc_k) break;
     PROF_ACC(0, t0);
     PROF_T(t1);
-    uint32_t B = min(tail - head, 64u);
-    KState st{EMPTY, 0u, 0.0f, 0u};
-    if (lane < B) st = q[(head + lane) & (QCAP - 1)];
-    if constexpr (FAM) {  // the batch ends before the next fork (the head state is none)
-      const uint64_t fc = __ballot(lane < B && ((st.node & (FAM_REQ_SB | FAM_SWAP)) || (st.jm & 0xFFFFu) >= kfam));
-      if (fc) {
-        B = (uint32_t)first_lane(fc);
-        if (lane >= B) st = KState{EMPTY, 0u, 0.0f, 0u};
-      }
-    }
+    const uint32_t B = min(tail - head, 64u);
     const bool in_b = lane < B;
+    KState st{EMPTY, 0u, 0.0f, 0u};
+    if (in_b) st = q[(head + lane) & (QCAP - 1)];
     // ---- phase A: the state's global reads go out first (node record, own single-byte map,
     // text at j and j + 1) and overlap the dedup probe; then dedup, node ceiling, width
     DevNode nd{};
@@ -2021,11 +1952,6 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     if (mwide & 1ull) {  // first state alone, edge-parallel
       PROF_T(t2);
       const KState s0 = q[head & (QCAP - 1)];
-      if constexpr (FAM)  // expand_wide reads the lookahead itself: the family's children build alone
-        if ((s0.jm & 0xFFFFu) + 1u == kfam) {
-          err |= ERR_QUEUE;
-          break;
-        }
       head += 1;
       popped += 1;
       if (track_beam) jp1 = max(jp1, (s0.jm & 0xFFFFu) + 1u);
@@ -2045,8 +1971,7 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     const bool act = alive && lane < Bc;
     Prep pr{0u, 0u, 0u, 0u, 0.0f};
     PROF_T(tb0);
-    const bool fam = FAM && act && (st.jm & 0xFFFFu) + 1u == kfam;  // a boundary state
-    if (act) pr = lane_prep<FAM>(P, S, st, nd, start, c0, c1, nd.sb, fam);
+    if (act) pr = lane_prep(P, S, st, nd, start, c0, c1, nd.sb);
     if constexpr (MAP) {
       pr.gcur = g0;
       pr.gnx = g1;
@@ -2062,8 +1987,8 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     prof_acc[13] += (uint64_t)__popcll(__ballot(fast));
 #endif
     if (__ballot(act && !fast))  // per-edge path for the states similarity can prune
-      expand_units<FAC_UK, MAP, FAM>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act && !fast, msub, mdel, ex, xe);
-    if (fast) expand_fast<FAM>(P, st, nd, pr, aux, msub, mdel, ex, xe);
+      expand_units<FAC_UK, MAP>(P, reinterpret_cast<ExpScratch*>(claim), nd, pr, act && !fast, msub, mdel, ex, xe);
+    if (fast) expand_fast(P, st, nd, pr, aux, msub, mdel, ex, xe);
 #if defined(FAC_DUP) && FAC_DUP == 1
     if (fast) {
       KState s2{opq(st.node), opq(st.jm), opqf(st.pen), opq(st.packed)};
@@ -2081,7 +2006,7 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
 #endif
     PROF_ACC(10, tb1);
     PROF_T(tb2);
-    if (act) x = lane_finish<MAP, FAM>(P, S, start, st, nd, pr, msub, mdel, ex, xe, err);
+    if (act) x = lane_finish<MAP>(P, S, start, st, nd, pr, msub, mdel, ex, xe, err);
 #if defined(FAC_DUP) && FAC_DUP == 2
     if (act) {
       KState s2{opq(st.node), opq(st.jm), opqf(st.pen), opq(st.packed)};
@@ -2106,7 +2031,7 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     const uint32_t P0 = tail - head;
     const bool trig = lane >= 1 && lane < Bc && P.beam && (P0 - lane + excl > beam2);
     const bool ovf = lane < Bc && (P0 - lane - 1 + incl > QCAP);
-    const bool past = !FAM && P.rc_mode == 2 && lane < Bc && (st.jm & 0xFFFFu) + 1u >= P.rc_k;  // cache build
+    const bool past = P.rc_mode == 2 && lane < Bc && (st.jm & 0xFFFFu) + 1u >= P.rc_k;  // cache build
     const uint64_t mcut = __ballot(trig) | __ballot(ovf) | __ballot(past);
     if (mcut) Bc = min(Bc, (uint32_t)first_lane(mcut));
     if (Bc == 0) {
@@ -2198,8 +2123,8 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     }
     PROF_ACC(5, t5);
     PROF_T(t6);
-    push_units<QCAP, FAC_UK, MAP, FAM>(P, reinterpret_cast<ExpScratch*>(claim), q, tail + excl, st, nd, x, pr.cur_ch,
-                                       alive && lane < Bc && x.count != 0, fam && (pr.flags & PF_LAST));
+    push_units<QCAP, FAC_UK, MAP>(P, reinterpret_cast<ExpScratch*>(claim), q, tail + excl, st, nd, x, pr.cur_ch,
+                                  alive && lane < Bc && x.count != 0);
 #if defined(FAC_DUP) && FAC_DUP == 4
     push_units<QCAP, FAC_UK, MAP>(P, reinterpret_cast<ExpScratch*>(claim), q, opq(tail + excl), st, nd, x, opq(pr.cur_ch),
                              alive && lane < Bc && x.count != 0);  // same entries rewritten
@@ -2225,13 +2150,6 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
   PROF_T(t_fl);
   head_out = head;
   vcount_out = vcount;
-  if constexpr (FAM) {
-    fr->head = head;
-    fr->tail = tail;
-    fr->vcount = vcount;
-    fr->jp1 = jp1;
-    fr->jbeam = jbeam;
-  }
   if (jbeam_out) {
     jbeam_out[0] = jbeam;
     jbeam_out[1] = track_beam ? shfl_u32(wave_inclusive_max(jp1), 63) : 0u;
@@ -2438,7 +2356,7 @@ __global__ __launch_bounds__(256) void rc_parent_kernel(SearchParams P, uint32_t
     const uint64_t start = S.w_begin + (wid - P.seg_prefix[kl]);
     const RcHit hit = rc_lookup(P, S, start, qcap);
     P.rc_bhits[v] = make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel);
-    P.rc_bpops[v] = hit.pops | (hit.lvl << 29);  // pops <= RC_POPS_MASK; the level: family builds' parent key length
+    P.rc_bpops[v] = hit.pops;
   }
 }
 
@@ -3179,10 +3097,9 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   const uint64_t stride = (uint64_t)gridDim.x * P.chunk;
   // behind the lookups a chunk holds the open entries of each region it covers: one sub-range each
   const bool regions = !LK && P.rc_mode == 1 && !P.win_list;
-  const uint64_t total_w = (LK && P.n_list_dev) ? (uint64_t)*P.n_list_dev : P.total_windows;  // a family build's retry list
-  for (uint64_t cb0 = P.dyn_chunks ? next_chunk() : (uint64_t)blockIdx.x * P.chunk; cb0 < total_w;
+  for (uint64_t cb0 = P.dyn_chunks ? next_chunk() : (uint64_t)blockIdx.x * P.chunk; cb0 < P.total_windows;
        cb0 = P.dyn_chunks ? next_chunk() : cb0 + stride) {
-    const uint64_t ce0 = min(cb0 + (uint64_t)P.chunk, total_w);
+    const uint64_t ce0 = min(cb0 + (uint64_t)P.chunk, P.total_windows);
     for (uint64_t cb = cb0, cnext = cb0; cb < ce0 && !any_err(err); cb = cnext) {
     uint64_t ce = ce0;
     cnext = ce0;
@@ -3223,10 +3140,8 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
       uint32_t kl = 0;
       uint64_t start = 0, vid = 0, wid = 0;  // list id (an open entry behind the lookups) and window
       RcHit hit{EMPTY, 0u, 0u, 0u, 0u};  // prefix-cache snapshot of this lane's window
-      // cache build: the entry built (a list of entries, e.g. children a family build left, or every one)
-      const uint32_t ent_l = (LK && P.ent_list && active) ? P.ent_list[v] : (uint32_t)v;
       if (active) {
-        vid = P.win_list ? P.win_list[LK ? (uint64_t)ent_l : v] : v;
+        vid = P.win_list ? P.win_list[v] : v;
         wid = (!LK && P.rc_mode == 1) ? rc_window_of(P, vid) : vid;
         kl = find_seg(P, wid);
         const SegDesc S = P.segs[kl];
@@ -3241,8 +3156,8 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
       }
       if constexpr (LK)
         if (P.rc_mode != 0 && P.rc_ntab && active && P.rc_bhits) {  // rc_parent_kernel's lookup
-          const uint4 h = P.rc_bhits[ent_l];
-          hit = RcHit{h.x, h.y, h.z, h.w, P.rc_bpops[ent_l] & RC_POPS_MASK};  // (bits 29-31: the parent's level)
+          const uint4 h = P.rc_bhits[v];
+          hit = RcHit{h.x, h.y, h.z, h.w, P.rc_bpops[v]};
         }
       if (LK && P.rc_mode == 1) {
         const bool resumed = active && hit.off != EMPTY;
@@ -3254,8 +3169,8 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
         // snapshot would hold the same best list, so the key stays uncached (lookups fall through)
         const bool done = active && hit.off != EMPTY && hit.tail == hit.head && !P.rc_keep_final;
         if (done) {
-          P.rc_off[ent_l] = EMPTY;
-          P.rc_count[ent_l] = EMPTY;
+          P.rc_off[v] = EMPTY;
+          P.rc_count[v] = EMPTY;
         }
         active = active && !done;
       }
@@ -3278,7 +3193,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
 #endif
         const uint32_t qlen =
             run_window<VCAP, QCAP, MAP, LIVE>(P, S, s_vis, s_q, s_claim, cseq, EL, st, rc, popped, cached, err, qhead,
-                                              vcnt, s_live, jbeam, bsel, 0u
+                                              vcnt, s_live, jbeam, bsel
 #ifdef FAC_PHASE_PROF
                                               , prof_acc
 #endif
@@ -3300,7 +3215,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
             __device__ ~EpAcc() { acc += __builtin_amdgcn_s_memtime() - t; }
           } ep_acc{__builtin_amdgcn_s_memtime(), prof_acc[22]};
 #endif
-          const uint32_t ent = shfl_u32(ent_l, l);
+          const uint32_t ent = (uint32_t)(v0 + (uint64_t)l);
           const uint32_t nq = qlen - qhead;
           // live dedup entries: a key is only met again at its own j, and every future state's j is
           // at least the smallest j in the queue (j never decreases along a path)
@@ -3383,13 +3298,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
             P.rc_off[ent] = bad ? EMPTY : (uint32_t)off;
             P.rc_count[ent] = bad ? EMPTY : nq;
             kept_snaps += bad ? 0u : 1u;
-            if (P.fam_debug)
-              printf("KEYSNAP k=%u ent=%u start=%llu parent=%u head=%u qlen=%u nq=%u nv=%u ne=%u bad=%d\n", P.rc_k, ent,
-                     (unsigned long long)shfl_u64(start, l), rc.off, qhead, qlen, nq, nv, EL.n, (int)bad);
           }
-          if (P.fam_debug && !bad)
-            for (uint32_t i = 0; i < nq; ++i)
-              if (lane == 0) printf("KEYQ ent=%u i=%u node=%u jm=%x pen=%f pk=%x\n", ent, i, dst[i].x, dst[i].y, __uint_as_float(dst[i].z), dst[i].w);
           (void)vcnt;
           err &= ~(ERR_QUEUE | ERR_VISITED | ERR_EMIT);
           __builtin_amdgcn_wave_barrier();
@@ -3433,384 +3342,6 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   slot_release(P, slot);
 }
 
-// ---- Family builds ----
-// The keys of a level that resume from one parent snapshot -- their first Kp chars are the parent's
-// key -- are built together: the wave resumes the parent once (run_window FAM). Every pop reads text
-// below Kp (shared) except the boundary states' lookahead, text[Kp]: the swap and the last edit's
-// next-char filters. Those states push the union over the children, tagged (FAM_REQ_SB, FAM_SWAP),
-// so each child's queue is the family ring filtered by its own char. The run pops the untagged
-// states with j < Kp in FIFO order -- the same pops as every child's own build -- and stops at a
-// fork: a head state that is untagged with j >= Kp (every child stops there) or tagged (the children
-// that keep it stop: it is their next pop and has j >= Kp or is theirs alone; the others drop it and
-// the run continues). A child's snapshot is the family's state at its stop, its queue filtered: the
-// reference's state after the same pops. A union pending count past 2 bw (a child's might beam)
-// stops every child still running there (a valid, shallower snapshot point); a wide boundary node, an
-// overflow, and every family of one child or without a parent, leave the children to the per-key
-// build (fam_retry).
-// One child's queue entry at ring position pos, filtered by its char tch (RC_PAD past the end of the
-// text) with t3 = text[Kp - 1]; node = the entry's node (a swap's resolved target) when kept.
-__device__ __forceinline__ bool fam_keep(const SearchParams& P, const KState& e, uint32_t tch, uint32_t t3, uint32_t& node) {
-  node = e.node;
-  if (e.node & FAM_REQ_SB) {  // :839-847 / :1018-1028 dead-end filters with the child's next char
-    node = e.node & FAM_NODE;
-    return tch < 128u && sb_has(P, node, tch);
-  }
-  if (e.node & FAM_SWAP) {  // :935-989: goto(goto(node, text[Kp]), text[Kp - 1]) with node2's limits
-    if (tch == RC_PAD) return false;
-    uint64_t g = 0;
-    if (!gt_get(P, GT_VALID | GT_GOTO | ((uint64_t)(e.node & FAM_NODE) << 21) | tch, true, g)) return false;
-    uint64_t g2 = 0;
-    if (!gt_get(P, GT_VALID | GT_GOTO | ((g & CHILD26_MASK) << 21) | t3, true, g2)) return false;
-    node = (uint32_t)(g2 & CHILD26_MASK);
-    if (P.mef == 255u) {  // within_limits_swap_ahead (:962-967) on the state before the swap
-      const uint32_t packed = e.packed - 0x1000000u, edits = edits_of(packed);
-      const Lim m = pick_limits(P, node_limits(P, node));
-      return m.has ? (lim_lt(m.l.edits, edits) && lim_lt(m.l.swp, packed >> 24)) : false;
-    }
-    return true;
-  }
-  return true;
-}
-
-template <uint32_t QCAP>
-__device__ void rc_family_body(const SearchParams& P) {
-  constexpr uint32_t VCAP = 512, NSL = VCAP / 64, NQL = QCAP / 64, FCH = 4;  // FCH: children per lane
-  static_assert(QCAP <= 256, "family builds: a lane holds its ring entries in registers");
-  __shared__ KState s_vis[VCAP];
-  __shared__ KState s_q[QCAP];
-  __shared__ __attribute__((aligned(16))) uint32_t s_claim[claim_slots(VCAP)];
-  const uint32_t lane = lane_id();
-  const uint32_t slot = slot_acquire(P);
-  EmitList EL{P.ebuf + (size_t)slot * P.ecap, P.ecap, 0};
-  uint64_t popped = 0, cached = 0;
-  unsigned long long pool_cur = 0, pool_end = 0;
-  uint32_t kept_snaps = 0, cseq = 1;
-  for (uint32_t i = lane; i < claim_slots(VCAP); i += 64) s_claim[i] = 0u;
-  __builtin_amdgcn_wave_barrier();
-  unsigned err = 0;
-  const uint32_t nheads = *P.fam_nheads;
-  auto retry = [&](uint32_t fb, uint32_t fe) {  // the children build alone (one list atomic per family)
-    unsigned long long b = 0;
-    if (lane == 0) b = atomicAdd(P.fam_nretry, fe - fb);
-    b = shfl_u64(b, 0);
-    for (uint32_t c = fb + lane; c < fe; c += 64) P.fam_retry[b + (c - fb)] = P.fam_ent[c];
-  };
-  auto retry_active = [&](uint32_t cb, uint32_t am) {  // the children still active (bit u: cb + 64 u + lane)
-    uint32_t n = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < FCH; ++u) n += (uint32_t)__popcll(__ballot((am >> u) & 1u));
-    if (!n) return;
-    unsigned long long b = 0;
-    if (lane == 0) b = atomicAdd(P.fam_nretry, n);
-    b = shfl_u64(b, 0);
-    uint32_t at = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < FCH; ++u) {
-      const bool a = (am >> u) & 1u;
-      const uint64_t m = __ballot(a);
-      if (a) P.fam_retry[b + at + prefix_below(m)] = P.fam_ent[cb + u * 64 + lane];
-      at += (uint32_t)__popcll(m);
-    }
-  };
-  for (;;) {
-    unsigned long long f = 0;
-    if (lane == 0) f = atomicAdd(P.counters + 7, 1ull);
-    f = shfl_u64(f, 0);
-    if (f >= nheads) break;
-    const uint32_t fb = P.fam_heads[f], key = P.fam_key[fb];
-    uint32_t fe = fb + 1;  // the family's end: the first position with another parent
-    for (;;) {
-      const uint32_t v = fe + lane;
-      const uint64_t m = __ballot(v >= P.fam_n || P.fam_key[v] != key);
-      if (m) {
-        fe += (uint32_t)first_lane(m);
-        break;
-      }
-      fe += 64;
-    }
-    const uint32_t e0 = P.fam_ent[fb];
-    const uint4 h = P.rc_bhits[e0];
-    const uint32_t bp = P.rc_bpops[e0];
-    if (h.x == EMPTY || fe - fb < 2) {  // no parent, or a single child: the per-key build
-      retry(fb, fe);
-      continue;
-    }
-    if (h.z == h.y && !P.rc_keep_final) {  // a final parent: its children stay uncached (bfs_window_body)
-      for (uint32_t c = fb + lane; c < fe; c += 64) {
-        P.rc_off[P.fam_ent[c]] = EMPTY;
-        P.rc_count[P.fam_ent[c]] = EMPTY;
-      }
-      continue;
-    }
-    const uint32_t kfam = P.rc_tab[bp >> 29].k;  // the parent key's chars
-    const RcHit rc{h.x, h.y, h.z, h.w, bp & RC_POPS_MASK};
-    const uint64_t wid0 = P.win_list[e0];
-    const uint32_t kl0 = find_seg(P, wid0);
-    const SegDesc S0 = P.segs[kl0];
-    const uint64_t start0 = S0.w_begin + (wid0 - P.seg_prefix[kl0]);
-    unsigned e3 = 0;
-    const uint32_t t3 = text_char(P, S0, start0 + kfam - 1, e3);  // the parent key's last char (shared)
-    for (uint32_t cb = fb; cb < fe; cb += 64 * FCH) {  // at most 64 FCH children per resumed run
-      const uint32_t ce = min(fe, cb + 64 * FCH);
-      if (ce - cb < 2) {
-        retry(cb, ce);
-        continue;
-      }
-      // each child's char past the parent key (RC_PAD past the text's end); am: the active children
-      uint32_t tchv[FCH], am = 0;
-#pragma unroll
-      for (uint32_t u = 0; u < FCH; ++u) {
-        tchv[u] = RC_PAD;
-        const uint32_t c = cb + u * 64 + lane;
-        if (c >= ce) continue;
-        const uint32_t ent = P.fam_ent[c];
-        const uint64_t wid = P.win_list[ent];
-        const uint32_t kl = find_seg(P, wid);
-        const SegDesc S = P.segs[kl];
-        const uint64_t start = S.w_begin + (wid - P.seg_prefix[kl]);
-        if (start + kfam < S.n) {
-          if (start + kfam >= S.avail) {  // not cacheable (rc_chars)
-            P.rc_off[ent] = EMPTY;
-            P.rc_count[ent] = EMPTY;
-            continue;
-          }
-          tchv[u] = text_char(P, S, start + kfam, e3);
-        }
-        am |= 1u << u;
-      }
-      const uint64_t popped0 = popped;
-      FamRun fr{0u, 0u, 0u, 0u, 0u, 0u, 0u};
-      uint32_t nskip = 0;  // tagged head entries every active child dropped so far (no pops)
-      for (;;) {
-        uint32_t qhead = 0, vcnt = 0, jbeam[2] = {0u, 0u};
-        const uint32_t qlen = run_window<VCAP, QCAP, false, false, true>(P, S0, s_vis, s_q, s_claim, cseq, EL, start0, rc, popped,
-                                                                          cached, err, qhead, vcnt, nullptr, jbeam, nullptr, kfam, &fr);
-        (void)vcnt;
-        const bool bad = (wave_or(err) & (ERR_QUEUE | ERR_VISITED | ERR_EMIT)) != 0 || EL.n > P.rc_emax;
-        err &= ~(ERR_QUEUE | ERR_VISITED | ERR_EMIT);
-        if (bad) {
-          if (P.lane_debug) {
-            uint32_t n = 0;
-#pragma unroll
-            for (uint32_t u = 0; u < FCH; ++u) n += (uint32_t)__popcll(__ballot((am >> u) & 1u));
-            if (lane == 0) atomicAdd(&g_fam_dbg[5], (unsigned long long)n);
-          }
-          retry_active(cb, am);
-          am = 0;
-          break;
-        }
-        // the family's ring [qhead, qlen) (at most QCAP) into registers
-        KState qe[NQL];
-#pragma unroll
-        for (uint32_t c = 0; c < NQL; ++c) {
-          const uint32_t i = c * 64 + lane;
-          qe[c] = i < qlen - qhead ? s_q[(qhead + i) & (QCAP - 1)] : KState{EMPTY, 0u, 0.f, 0u};
-        }
-        // the children that stop here: all at an empty queue or an untagged head (j >= Kp); at a
-        // tagged head those that keep it (their next pop would be a state with j >= Kp); at a union
-        // count past 2 bw + allow those whose own pending count passes 2 bw (their next pop beams)
-        uint32_t stop = am, why = qhead < qlen ? 2u : 1u;  // why: diagnostics (g_fam_dbg)
-        bool skip_head = false;
-        const uint32_t beam2 = 2u * P.beam;
-        if (fr.beam) {
-          stop = 0;
-          why = 0;
-          uint32_t maxp = 0;
-#pragma unroll
-          for (uint32_t u = 0; u < FCH; ++u) {
-            uint64_t m = __ballot((am >> u) & 1u);
-            while (m) {
-              const int l = first_lane(m);
-              m &= m - 1;
-              const uint32_t tch = shfl_u32(tchv[u], l);
-              uint32_t pend = 0;
-#pragma unroll
-              for (uint32_t q = 0; q < NQL; ++q) {
-                uint32_t nn = 0;
-                pend += (uint32_t)__popcll(__ballot(qe[q].node != EMPTY && fam_keep(P, qe[q], tch, t3, nn)));
-              }
-              if (pend > beam2) {
-                if (lane == (uint32_t)l) stop |= 1u << u;
-              } else {
-                maxp = max(maxp, pend);
-              }
-            }
-          }
-          fr.allow = (qlen - qhead) - maxp;  // (no child left: unused)
-          fr.beam = 0;
-          if (P.lane_debug) {
-            uint32_t n = 0;
-#pragma unroll
-            for (uint32_t u = 0; u < FCH; ++u) n += (uint32_t)__popcll(__ballot((stop >> u) & 1u));
-            if (lane == 0) atomicAdd(&g_fam_dbg[0], (unsigned long long)n);
-          }
-          retry_active(cb, stop);  // their own builds beam here and go on: built alone
-          am &= ~stop;
-          stop = 0;
-        } else if (qhead < qlen) {
-          const KState h0 = qe[0];  // lane 0's: broadcast
-          const uint32_t hn = shfl_u32(h0.node, 0);
-          if (hn & (FAM_REQ_SB | FAM_SWAP)) {
-            const KState hb{hn, shfl_u32(h0.jm, 0), shfl_f32(h0.pen, 0), shfl_u32(h0.packed, 0)};
-            stop = 0;
-            skip_head = true;
-            why = (hb.jm & 0xFFFFu) >= kfam ? 3u : 4u;
-#pragma unroll
-            for (uint32_t u = 0; u < FCH; ++u) {
-              uint32_t nn = 0;
-              if (((am >> u) & 1u) && fam_keep(P, hb, tchv[u], t3, nn)) stop |= 1u << u;
-            }
-          }
-        }
-        uint64_t any_stop = 0;
-        uint32_t n_stop = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < FCH; ++u) {
-          any_stop |= __ballot((stop >> u) & 1u);
-          n_stop += (uint32_t)__popcll(__ballot((stop >> u) & 1u));
-        }
-        if (P.lane_debug && lane == 0) {
-          atomicAdd(&g_fam_dbg[why], (unsigned long long)n_stop);
-          atomicAdd(&g_fam_dbg[7], 1ull);
-        }
-        if (any_stop) {
-          // the family's dedup table once into registers
-          KState kv[NSL];
-#pragma unroll
-          for (uint32_t u = 0; u < NSL; ++u) kv[u] = s_vis[u * 64 + lane];
-          const uint32_t pops_w = (uint32_t)(popped - popped0) + rc.pops;
-          const uint32_t head_c = qhead - nskip;  // the child's own queue positions
-#pragma unroll
-          for (uint32_t u = 0; u < FCH; ++u) {
-            uint64_t sm = __ballot((stop >> u) & 1u);
-            while (sm) {  // each stopping child's snapshot
-              const int l = first_lane(sm);
-              sm &= sm - 1;
-              const uint32_t ent = P.fam_ent[cb + u * 64 + (uint32_t)l];
-              const uint32_t tch = shfl_u32(tchv[u], l);
-              uint32_t keep = 0, jmin = 0xFFFFu, nq = 0;
-              uint32_t rn[NQL];
-#pragma unroll
-              for (uint32_t q = 0; q < NQL; ++q) {
-                const bool k = qe[q].node != EMPTY && fam_keep(P, qe[q], tch, t3, rn[q]);
-                keep |= (k ? 1u : 0u) << q;
-                nq += (uint32_t)__popcll(__ballot(k));
-                if (k) jmin = min(jmin, qe[q].jm & 0xFFFFu);
-              }
-              jmin = wave_min_u32(jmin);
-              // live dedup entries (j >= the queue's smallest j), as bfs_window_body's build epilogue
-              uint32_t lmask = 0, nv = 0, jlive = 0;
-#pragma unroll
-              for (uint32_t v = 0; v < NSL; ++v) {
-                const bool lv = kv[v].node != EMPTY && (kv[v].jm & 0xFFFFu) >= jmin;
-                lmask |= (lv ? 1u : 0u) << v;
-                nv += (uint32_t)__popcll(__ballot(lv));
-                jlive = max(jlive, lv ? (kv[v].jm & 0xFFFFu) + 1u : 0u);
-              }
-              jlive = shfl_u32(wave_inclusive_max(jlive), 63);
-              bool cbad = nv > P.rc_vmax;
-              const uint32_t words = RC_HDR + nq + nv + EL.n;
-              if (!cbad && pool_cur + words > pool_end) {
-                const unsigned long long want = max((unsigned long long)words, (unsigned long long)P.rc_pool_chunk);
-                unsigned long long cp = 0;
-                if (lane == 0) cp = atomicAdd(P.rc_pool_used, want);
-                pool_cur = shfl_u64(cp, 0);
-                pool_end = pool_cur + want;
-              }
-              const unsigned long long off = pool_cur;
-              if (!cbad) pool_cur += words;
-              cbad = cbad || off + words > P.rc_pool_cap || off > 0xFFFFFFF0ull;
-              uint4* dst = P.rc_pool + off + RC_HDR;
-              if (!cbad) {
-                uint32_t at = 0;  // the kept entries in ring order
-#pragma unroll
-                for (uint32_t q = 0; q < NQL; ++q) {
-                  const bool k = (keep >> q) & 1u;
-                  const uint64_t m = __ballot(k);
-                  if (k) dst[at + prefix_below(m)] = make_uint4(rn[q], qe[q].jm, __float_as_uint(qe[q].pen), qe[q].packed);
-                  at += (uint32_t)__popcll(m);
-                }
-                const uint32_t jcheck = min(jlive, jbeam[0]);
-                uint32_t cmask = 0;
-#pragma unroll
-                for (uint32_t v = 0; v < NSL; ++v)
-                  cmask |= (((lmask >> v) & 1u) && (kv[v].jm & 0xFFFFu) + 1u <= jcheck ? 1u : 0u) << v;
-                uint32_t at0 = 0, ncheck = 0;
-                for (uint32_t pass = 0; pass < 2; ++pass) {
-                  const uint32_t sel = pass == 0 ? cmask : (lmask & ~cmask);
-#pragma unroll
-                  for (uint32_t v = 0; v < NSL; ++v) {
-                    const bool occ = (sel >> v) & 1u;
-                    const uint64_t m = __ballot(occ);
-                    if (occ) dst[nq + at0 + prefix_below(m)] = make_uint4(kv[v].node, kv[v].jm, __float_as_uint(kv[v].pen), kv[v].packed);
-                    at0 += (uint32_t)__popcll(m);
-                  }
-                  if (pass == 0) ncheck = at0;
-                }
-                for (uint32_t i = lane; i < EL.n; i += 64) dst[nq + nv + i] = EL.buf[i];
-                if (lane == 0) {
-                  P.rc_pool[off] = make_uint4(head_c, head_c + nq, nv, pops_w);
-                  P.rc_pool[off + 1] = make_uint4(EL.n, ncheck ? (jcheck | (ncheck << 16)) : 0u, jbeam[0], jbeam[1]);
-                }
-              }
-              if (lane == 0) {
-                P.rc_off[ent] = cbad ? EMPTY : (uint32_t)off;
-                P.rc_count[ent] = cbad ? EMPTY : nq;
-                kept_snaps += cbad ? 0u : 1u;
-                if (P.fam_debug)
-                  printf("FAMSNAP k=%u ent=%u kfam=%u tch=%u t3=%u parent=%u head=%u nskip=%u qlen=%u nq=%u nv=%u ne=%u pops=%u beam=%u bad=%d\n",
-                         P.rc_k, ent, kfam, tch, t3, h.x, qhead, nskip, qlen, nq, nv, EL.n, pops_w, fr.beam, (int)cbad);
-              }
-            }
-          }
-          am &= ~stop;
-        }
-        bool more = false;
-#pragma unroll
-        for (uint32_t u = 0; u < FCH; ++u) more = more || __ballot((am >> u) & 1u) != 0;
-        if (!more) break;
-        if (skip_head) {  // the rest drop the tagged head entry: it is no state of theirs
-          if (P.lane_debug && lane == 0) atomicAdd(&g_fam_dbg[6], 1ull);
-          fr.head += 1;
-          nskip += 1;
-          if (fr.allow) fr.allow -= 1;  // it was one of the entries every running child drops
-        }
-        fr.resume = 1;
-        __builtin_amdgcn_wave_barrier();
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (any_err(err)) break;
-    }
-    if (any_err(err)) break;
-  }
-  if (lane == 0) atomicAdd(P.counters + 1, (unsigned long long)popped);
-  if (lane == 0 && kept_snaps) atomicAdd(P.counters + 11, (unsigned long long)kept_snaps);
-  const unsigned all = wave_or(err);
-  if (lane == 0 && all) atomicOr(reinterpret_cast<unsigned int*>(P.counters + 2), all);
-  (void)cached;
-  slot_release(P, slot);
-}
-
-// the sorted level's family heads: positions whose parent differs from the previous position's
-__global__ __launch_bounds__(256) void rc_family_heads_kernel(const uint32_t* key, uint32_t n, uint32_t* heads,
-                                                              unsigned int* nheads) {
-  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
-    const bool head = v == 0 || key[v] != key[v - 1];
-    const uint64_t m = __ballot(head);
-    unsigned int b = 0;
-    if (m && lane_id() == (uint32_t)first_lane(m)) b = atomicAdd(nheads, (unsigned int)__popcll(m));
-    b = (unsigned int)__shfl((int)b, first_lane(m ? m : 1ull));
-    if (head) heads[b + prefix_below(m)] = v;
-  }
-}
-// sort input: the parent snapshot offset of every entry (EMPTY: none) and the entry itself
-__global__ __launch_bounds__(256) void rc_family_keys_kernel(const uint4* bhits, uint32_t n, uint32_t* key, uint32_t* ent) {
-  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
-    key[v] = bhits[v].x;
-    ent[v] = v;
-  }
-}
-
 // one wavefront per workgroup; the dedup-free variants are held to <= 128 VGPRs (4 waves/SIMD),
 // the dedup variants are bounded by LDS first
 #ifndef FAC_BEAM_WAVES  // waves/SIMD the dedup variants are compiled for (VGPR budget); 0 = unbounded
@@ -3842,11 +3373,6 @@ template <uint32_t QCAP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((FAC_BEAM_WAVES && QCAP <= 256) ? FAC_BEAM_WAVES : 1)))
 void rc_build_kernel(SearchParams P) {
   bfs_window_body<512, QCAP, false, true>(P);  // the prefix cache is off with mappings
-}
-// family builds (rc_family_body): one wave per family of child keys sharing a parent snapshot
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAC_BEAM_WAVES ? FAC_BEAM_WAVES : 1)))
-void rc_family_kernel(SearchParams P) {
-  rc_family_body<256>(P);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -4841,7 +4367,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   DevBuf d_voff, d_rcnt;   // ... their windows and per-region counts
   DevBuf d_bhits, d_bpops; // prefix cache builds: the representatives' parent snapshots
   DevBuf d_slots, d_bsel;  // wave-slot rings (one per stream), beam-selection scratch
-  DevBuf d_fkey, d_fent, d_fheads, d_fretry;  // family builds: sorted parents / entries, heads, retry list
   ScratchSet* bound = t_scratch;  // a streaming worker's own set, else the engine's
   std::unique_lock<std::mutex> lease(bound ? bound->mu : e.scratch_mu, std::try_to_lock);
   void** scratch_p = bound ? bound->p : e.scratch_p;
@@ -4861,8 +4386,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     bufs.push_back(&d_bsel);
     bufs.push_back(&d_bhits);
     bufs.push_back(&d_bpops);
-    for (DevBuf* b : {&d_fkey, &d_fent, &d_fheads, &d_fretry}) bufs.push_back(b);
-    static_assert(Engine::kScratch >= 35 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
+    static_assert(Engine::kScratch >= 31 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
     static_assert(ScratchSet::kSlots >= Engine::kScratch, "stream scratch slots");
     for (size_t i = 0; i < bufs.size(); ++i) bufs[i]->bind(&scratch_p[i], &scratch_n[i]);
   }
@@ -4950,7 +4474,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.live_nqmax = 0;
   P.rc_lane_flush = diag_env("FAC_RC_NO_LANE") ? 0 : 1;
   P.dyn_chunks = diag_env("FAC_STATIC_GRID") ? 0 : 1;
-  P.fam_debug = diag_env("FAC_FAM_DEBUG") ? 1 : 0;
   const bool root_out = !e.nodes.empty() && e.nodes[0].out_end > e.nodes[0].out_begin;
   const char* rc_min = diag_env("FAC_RC_MIN");  // env knobs: tests force it on / pin K, A/B turns it off
   const char* kenv = diag_env("FAC_RC_K");
@@ -5165,9 +4688,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       Q.spill_cap = spill_cap;
       Q.counters = static_cast<unsigned long long*>(d_cnt.p);
       if (!cleared) HIP_TRY(hipMemsetAsync(Q.counters, 0, N_COUNTERS * sizeof(unsigned long long), bs));
-      // every entry reads as uncached until its build writes it (a build that stops on an error leaves
-      // the rest so, and the publish skips them)
-      HIP_TRY(hipMemsetAsync(Q.rc_count, 0xFF, (size_t)n_ent * sizeof(uint32_t), bs));
       uint32_t grid = std::min<uint32_t>(n_ent, max_grid);
       if (bs != stream && !diag_env("FAC_L1_PERSIST")) {
         // beside the sampled-level counts: one chunk per workgroup, so workgroup slots free up all
@@ -5192,52 +4712,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       }
       uint32_t qk = 256;  // launch_rc_build's ring
       while (qk < qbuild) qk <<= 1;
-      // Family builds (rc_family_kernel): the entries sorted by parent snapshot, each family built from
-      // one resumed parent; the children it leaves (single-child families, failures) build alone below
-      // (FAC_FAMILY: a mask over the levels by key chars past level 1's -- bit 0 level 1 itself;
-      // default: none -- measured slower than the per-key builds, round 5 profiles/r05h)
-      const char* fenv = diag_env("FAC_FAMILY");
-      const uint32_t fmask = fenv ? (uint32_t)std::strtoul(fenv, nullptr, 0) : 0u;
-      const uint32_t frank = T.k >= L1.k ? T.k - L1.k : 31u;
-      const bool family = Q.rc_ntab > 0 && qbuild <= 256 && n_ent >= 2 && frank < 31u && ((fmask >> frank) & 1u);
-      if (family) {
-        HIP_TRY(d_fkey.alloc(2 * (size_t)n_ent * sizeof(uint32_t), bs));
-        HIP_TRY(d_fent.alloc(2 * (size_t)n_ent * sizeof(uint32_t), bs));
-        HIP_TRY(d_fheads.alloc((size_t)n_ent * sizeof(uint32_t), bs));
-        HIP_TRY(d_fretry.alloc(((size_t)n_ent + 64) * sizeof(uint32_t), bs));
-        uint32_t* fkey = static_cast<uint32_t*>(d_fkey.p);
-        uint32_t* fent = static_cast<uint32_t*>(d_fent.p);
-        uint32_t* fretry = static_cast<uint32_t*>(d_fretry.p);
-        unsigned int* fcnt = fretry + n_ent;  // [0] heads, [1] children to retry
-        HIP_TRY(hipMemsetAsync(fcnt, 0, 2 * sizeof(unsigned int), bs));
-        const dim3 g1((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_ent + 255) / 256, (uint64_t)cus * 8)));
-        hipLaunchKernelGGL(rc_family_keys_kernel, g1, dim3(256), 0, bs, static_cast<const uint4*>(Q.rc_bhits), n_ent,
-                           fkey + n_ent, fent + n_ent);
-        HIP_TRY(hipGetLastError());
-        if (int src = sort_pairs_u32(fkey + n_ent, fkey, fent + n_ent, fent, n_ent, 32, bs, err)) return src;
-        hipLaunchKernelGGL(rc_family_heads_kernel, g1, dim3(256), 0, bs, fkey, n_ent, static_cast<uint32_t*>(d_fheads.p), fcnt);
-        HIP_TRY(hipGetLastError());
-        SearchParams F = Q;
-        F.fam_key = fkey;
-        F.fam_ent = fent;
-        F.fam_heads = static_cast<const uint32_t*>(d_fheads.p);
-        F.fam_nheads = fcnt;
-        F.fam_retry = fretry;
-        F.fam_nretry = fcnt + 1;
-        F.fam_n = n_ent;
-        F.lane_debug = diag_env("FAC_RC_DEBUG") ? 1 : 0;
-        HIP_TRY(hipMemsetAsync(F.counters + 7, 0, sizeof(unsigned long long), bs));
-        if (int src = prep_slots(F, bs, qk, true)) return src;
-        hipLaunchKernelGGL(rc_family_kernel, dim3(max_grid), dim3(64), 0, bs, F);
-        HIP_TRY(hipGetLastError());
-        // the children left: the per-key build over the retry list (its length read on the device)
-        HIP_TRY(hipMemsetAsync(Q.counters + 7, 0, sizeof(unsigned long long), bs));
-        Q.ent_list = fretry;
-        Q.n_list_dev = fcnt + 1;
-        Q.chunk = 4;
-        Q.dyn_chunks = 1;
-        grid = max_grid;
-      }
       if (int src = prep_slots(Q, bs, qk, true)) return src;
       launch_rc_build(qbuild, grid, bs, Q);
       const hipError_t le = hipGetLastError();
@@ -5596,11 +5070,6 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
                    d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10]);
       std::memset(d, 0, sizeof(d));
       HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_live_dbg), d, sizeof(d)));
-      HIP_TRY(hipMemcpyFromSymbol(d, HIP_SYMBOL(g_fam_dbg), 8 * sizeof(unsigned long long)));
-      std::fprintf(stderr, "FAC_FAM stops beam=%llu empty=%llu untagged=%llu tagged_past=%llu tagged_boundary=%llu retried=%llu"
-                   " forks=%llu runs=%llu\n", d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
-      std::memset(d, 0, sizeof(d));
-      HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_fam_dbg), d, 8 * sizeof(unsigned long long)));
     }
 #ifdef FAC_WIN_HIST
     {
