@@ -236,7 +236,7 @@ struct EmitList {
 
 __device__ __forceinline__ void wave_mem_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup"); }
 
-__device__ __forceinline__ void emit_update(EmitList& L, uint32_t me_rel, uint32_t p, float sim, uint32_t packed, unsigned& err) {
+__device__ void emit_update(EmitList& L, uint32_t me_rel, uint32_t p, float sim, uint32_t packed, unsigned& err) {
   const uint32_t lane = lane_id();
   wave_mem_fence();
   for (uint32_t base = 0; base < L.n; base += 64) {
@@ -974,7 +974,7 @@ __device__ __forceinline__ bool visited_check(KState* vis, uint32_t& vcount, con
 
 // Emission (search.rs:659-737) for one accepted state; lanes spread over the node's output list.
 // Called in FIFO pop order, so the per-window best list keeps the reference's first-found ties.
-__device__ __forceinline__ void emit_state(const SearchParams& P, EmitList& EL, uint32_t me_rel, float pen, uint32_t packed,
+__device__ void emit_state(const SearchParams& P, EmitList& EL, uint32_t me_rel, float pen, uint32_t packed,
                            uint32_t node, unsigned& err) {
   const uint2 orr = P.out_range[node];
   const uint32_t out_begin = orr.x, out_end = orr.y;
@@ -1030,7 +1030,7 @@ __device__ __forceinline__ int64_t wave_find_gid(const SearchParams& P, uint32_t
 }
 
 template <uint32_t QCAP, bool MAP>
-__device__ __forceinline__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, uint32_t head, uint32_t& tail,
+__device__ void expand_wide(const SearchParams& P, const SegDesc& S, KState* q, uint32_t head, uint32_t& tail,
                             const KState& st, const DevNode& nd, uint64_t start, unsigned& err) {
   const uint32_t lane = lane_id();
   const bool fast = P.mef != 255u;
@@ -1250,7 +1250,7 @@ struct Prep {
 constexpr uint32_t PF_SUB = 1u, PF_DEL = 2u, PF_LAST = 4u, PF_CSB = 8u, PF_NEXT = 16u, PF_CUR = 32u, PF_SWAP = 64u,
                    PF_EX = 128u, PF_INS = 256u;
 
-__device__ __forceinline__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState& st, const DevNode& nd, uint64_t start,
+__device__ Prep lane_prep(const SearchParams& P, const SegDesc& S, const KState& st, const DevNode& nd, uint64_t start,
                           uint32_t c0, uint32_t c1, uint4 own_sb) {  // c0/c1: text at j / j + 1 (0 past the end)
   Prep r{0u, 0u, 0u, 0u, 0.0f};
   const bool fast = P.mef != 255u;
@@ -1360,7 +1360,7 @@ __device__ __forceinline__ int unit_owner(ExpScratch* X, uint32_t R, uint32_t nu
 // for the batch's largest degree). Per edge: the exact/swap first-char match (structs.rs:512-519),
 // substitution (:814-874) and deletion (:1055-1088) keep tests incl. the last-edit dead-end filter.
 template <uint32_t UK, bool MAP>
-__device__ __forceinline__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode& nd, const Prep& pr, bool act,
+__device__ void expand_units(const SearchParams& P, ExpScratch* X, const DevNode& nd, const Prep& pr, bool act,
                              uint64_t& msub, uint64_t& mdel, uint32_t& ex, uint32_t& xe) {
   const uint32_t lane = lane_id();
   const uint32_t deg = act ? node_deg(nd) : 0u;
@@ -1458,7 +1458,7 @@ __device__ __forceinline__ bool no_subs(const SearchParams& P, const DevNode& nd
   return __fmul_rn(P.p_sub, __fsub_rn(1.0f, P.sim_ascii[128u * 128u + cur])) > remaining;
 }
 
-__device__ __forceinline__ void expand_fast(const SearchParams& P, const KState& st, const DevNode& nd, const Prep& pr, uint4 aux,
+__device__ void expand_fast(const SearchParams& P, const KState& st, const DevNode& nd, const Prep& pr, uint4 aux,
                             uint64_t& msub, uint64_t& mdel, uint32_t& ex, uint32_t& xe) {
   const uint32_t deg = node_deg(nd);
   const uint64_t dm = deg >= 64u ? ~0ull : ((1ull << deg) - 1ull);
@@ -1499,7 +1499,7 @@ __device__ __forceinline__ void expand_fast(const SearchParams& P, const KState&
 // Per-state completion: exact successor, the exact edge leaves the substitution set, swap target
 // goto(goto(node, text[j+1]), text[j]) (:945-967), push count.
 template <bool MAP>
-__device__ __forceinline__ LaneExp lane_finish(const SearchParams& P, const SegDesc& S, uint64_t start, const KState& st,
+__device__ LaneExp lane_finish(const SearchParams& P, const SegDesc& S, uint64_t start, const KState& st,
                                const DevNode& nd, const Prep& pr, uint64_t msub, uint64_t mdel, uint32_t ex,
                                uint32_t xe, unsigned& err) {
   LaneExp x{-1, -1, false, msub, mdel, 0u, 0ull};
@@ -1552,11 +1552,10 @@ __device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t r) {
 // Pushes of the committed states in the reference's order (search.rs:787-1088): per state exact,
 // substitutions (edge order), swap, insertion, deletions (edge order), written at the state's
 // exclusive-prefix offset. The owner lane writes exact/swap/insertion; substitutions and deletions
-// are written by the units that cover their edges (balanced like expand_units). qoff: the state's ring
-// (live_pair_body: two windows' rings side by side), in states.
+// are written by the units that cover their edges (balanced like expand_units).
 template <uint32_t QCAP, uint32_t UK, bool MAP>
-__device__ __forceinline__ void push_units(const SearchParams& P, ExpScratch* X, KState* q, uint32_t base, const KState& st,
-                           const DevNode& nd, const LaneExp& x, uint32_t cur_ch, bool act, uint32_t qoff = 0) {
+__device__ void push_units(const SearchParams& P, ExpScratch* X, KState* q, uint32_t base, const KState& st,
+                           const DevNode& nd, const LaneExp& x, uint32_t cur_ch, bool act) {
   const uint32_t lane = lane_id();
   const float pen = st.pen;
   const uint32_t j_rel = st.jm & 0xFFFFu;
@@ -1567,14 +1566,14 @@ __device__ __forceinline__ void push_units(const SearchParams& P, ExpScratch* X,
   const uint32_t sw_pos = map_pos + (uint32_t)__popcll(x.mmap);
   const uint32_t del_base = sw_pos + nsw + nins;
   if (act) {
-    if (nex) q[qoff + (base & (QCAP - 1))] = KState{(uint32_t)x.exact, jm1, pen, st.packed};
+    if (nex) q[base & (QCAP - 1)] = KState{(uint32_t)x.exact, jm1, pen, st.packed};
     if (nsw) {
       const uint32_t jm2 = (j_rel + 2u) | ((j_rel + 2u) << 16);
-      q[qoff + (sw_pos & (QCAP - 1))] = KState{(uint32_t)x.swap, jm2, __fadd_rn(pen, P.p_swp), st.packed + 0x1000000u};
+      q[sw_pos & (QCAP - 1)] = KState{(uint32_t)x.swap, jm2, __fadd_rn(pen, P.p_swp), st.packed + 0x1000000u};
     }
     if (nins) {
       const uint32_t jmi = (j_rel + 1u) | ((st.jm >> 16) << 16);
-      q[qoff + ((sw_pos + nsw) & (QCAP - 1))] = KState{st.node, jmi, __fadd_rn(pen, P.p_ins), st.packed + 1u};
+      q[(sw_pos + nsw) & (QCAP - 1)] = KState{st.node, jmi, __fadd_rn(pen, P.p_ins), st.packed + 1u};
     }
     if constexpr (MAP)
       if (x.mmap) {  // mapping pushes, after the substitutions (:883-922)
@@ -1586,7 +1585,7 @@ __device__ __forceinline__ void push_units(const SearchParams& P, ExpScratch* X,
           mm &= mm - 1;
           const uint4 mt = P.map_ent[mb + t];
           const uint32_t jh = j_rel + mt.y;
-          q[qoff + ((pos++) & (QCAP - 1))] = KState{mt.z, jh | (jh << 16), __fadd_rn(pen, __uint_as_float(mt.w)), st.packed + 0x10000u};
+          q[(pos++) & (QCAP - 1)] = KState{mt.z, jh | (jh << 16), __fadd_rn(pen, __uint_as_float(mt.w)), st.packed + 0x10000u};
         }
       }
   }
@@ -1605,7 +1604,7 @@ __device__ __forceinline__ void push_units(const SearchParams& P, ExpScratch* X,
     const uint64_t o_ms = shfl_var_u64(x.msub, o), o_md = shfl_var_u64(x.mdel, o);
     const uint32_t o_sb = __shfl(sub_base, o), o_db = __shfl(del_base, o), o_cur = __shfl(cur_ch, o);
     const float o_pen = __shfl(pen, o);
-    const uint32_t o_jm = __shfl(st.jm, o), o_packed = __shfl(st.packed, o), o_q = __shfl(qoff, o);
+    const uint32_t o_jm = __shfl(st.jm, o), o_packed = __shfl(st.packed, o);
     if (valid) {
       const uint32_t k = R + lane - o_fb;
       const bool is_sub = k < o_ns;
@@ -1617,9 +1616,9 @@ __device__ __forceinline__ void push_units(const SearchParams& P, ExpScratch* X,
         const float sim = similarity(P, ed.ch, o_cur);
         const float penalty = __fmul_rn(P.p_sub, __fsub_rn(1.0f, sim));
         const uint32_t o_j1 = (o_jm & 0xFFFFu) + 1u;
-        q[o_q + ((o_sb + r) & (QCAP - 1))] = KState{child, o_j1 | (o_j1 << 16), __fadd_rn(o_pen, penalty), o_packed + 0x10000u};
+        q[(o_sb + r) & (QCAP - 1)] = KState{child, o_j1 | (o_j1 << 16), __fadd_rn(o_pen, penalty), o_packed + 0x10000u};
       } else {
-        q[o_q + ((o_db + r) & (QCAP - 1))] = KState{child, o_jm, __fadd_rn(o_pen, P.p_del), o_packed + 0x100u};
+        q[(o_db + r) & (QCAP - 1)] = KState{child, o_jm, __fadd_rn(o_pen, P.p_del), o_packed + 0x100u};
       }
     }
   }
@@ -1725,7 +1724,7 @@ __device__ unsigned long long g_prof[64];  // [0, 32): main passes, [32, 64): ca
 // for the slot returned into it (positions are filled in return order); the ring starts as 0..n-1.
 // A release waits until its cell is EMPTY (the previous lap's acquirer took its value), so a slow
 // acquirer never has its value overwritten by a later lap's release (grids larger than n slots).
-__device__ __forceinline__ uint32_t slot_acquire(const SearchParams& P) {
+__device__ uint32_t slot_acquire(const SearchParams& P) {
   uint32_t s = 0;
   if (lane_id() == 0) {
     const unsigned int h = atomicAdd(P.slot_ctr, 1u);
@@ -1734,7 +1733,7 @@ __device__ __forceinline__ uint32_t slot_acquire(const SearchParams& P) {
   }
   return shfl_u32(s, 0);
 }
-__device__ __forceinline__ void slot_release(const SearchParams& P, uint32_t s) {
+__device__ void slot_release(const SearchParams& P, uint32_t s) {
   if (lane_id() == 0) {
     const unsigned int t = atomicAdd(P.slot_ctr + 1, 1u);
     unsigned int* cell = P.slot_ring + (t % P.n_slots);
@@ -3343,453 +3342,6 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   slot_release(P, slot);
 }
 
-// ---- Paired live kernel ----
-// bfs_window_kernel_live with two windows per wave. Every batch takes both windows' next states side
-// by side -- window 0 on lanes [0, B0), window 1 on [B0, B0 + B1) -- so one pass of the batch's
-// dependent loads (node record -> goto lookups -> edges) serves both, and a window with a short
-// queue leaves its lanes to the other. Each window keeps its own ring, best list and live table, and
-// the reference's order within itself (search.rs:576-1089 per window: pops, cuts, emissions and
-// pushes in FIFO order); windows are independent, so interleaving them changes no result. LDS per
-// wave: rings 2 x 4 KB, live tables 2 x 16 B x FAC_PAIR_LCAP, the batch scratch 2 KB.
-#ifndef FAC_PAIR_LCAP  // live table entries per window
-#define FAC_PAIR_LCAP 128
-#endif
-struct PairWin {
-  uint64_t tb;             // the window's text relative to its start: text_base + start,
-  uint32_t n, avail, ascii;  // n - start and avail - start (clamped to 2^24: a window reads j < 2^16)
-  uint32_t seg;
-  uint64_t start, vid, wid;
-  uint32_t head, tail, on;
-  uint32_t jlive, lmode;  // snapshot's jcheck | ncheck << 16; live table 0: not loaded, 1: in LDS, 2: global scan
-  uint32_t rc_off, rc_nq;
-  uint32_t ne;            // best-list entries (the list: the wave slot's emit scratch, half per window)
-};
-
-template <uint32_t QCAP>
-__device__ __forceinline__ void live_pair_body(const SearchParams& P) {
-  constexpr uint32_t LCAP = FAC_PAIR_LCAP;  // live table per window (more check entries than 3/4 of it: spilled)
-  __shared__ KState s_q[2 * QCAP];
-  __shared__ KState s_live[2 * LCAP];
-  __shared__ __attribute__((aligned(16))) uint32_t s_claim[claim_slots(0)];
-  const uint32_t lane = lane_id();
-  const uint32_t slot = slot_acquire(P);
-  uint64_t popped = 0, cached = 0;
-  unsigned err = 0;
-  for (uint32_t i = lane; i < claim_slots(0); i += 64) s_claim[i] = 0u;
-  __builtin_amdgcn_wave_barrier();
-  ExpScratch* const X = reinterpret_cast<ExpScratch*>(s_claim);
-
-  // ---- the window feed: chunks -> sub-ranges (regions) -> 64-window groups -> their open windows
-  // (bfs_window_body's loops as a state machine)
-  auto next_chunk = [&]() __attribute__((always_inline)) -> uint64_t {
-    unsigned long long c = 0;
-    if (lane == 0) c = atomicAdd(P.counters + 7, (unsigned long long)P.chunk);
-    return shfl_u64(c, 0);
-  };
-  const uint64_t stride = (uint64_t)gridDim.x * P.chunk;
-  const bool regions = P.rc_mode == 1 && !P.win_list;
-  uint64_t cb0 = P.dyn_chunks ? next_chunk() : (uint64_t)blockIdx.x * P.chunk;
-  uint64_t ce0 = 0, cb = 0, cnext = 0, ce = 0, v0 = 0, live_groups = 0, gm = 0;
-  uint32_t stage = 0;
-  uint32_t g_kl = 0, g_pops = 0;  // the current group's windows, one per lane
-  uint64_t g_start = 0, g_vid = 0, g_wid = 0;
-  uint4 g_hit = make_uint4(EMPTY, 0u, 0u, 0u);
-  auto load_group = [&]() __attribute__((always_inline)) {
-    const uint64_t v = v0 + lane;
-    bool active = v < ce;
-    g_hit = make_uint4(EMPTY, 0u, 0u, 0u);
-    g_pops = 0;
-    if (active) {
-      g_vid = P.win_list ? P.win_list[v] : v;
-      g_wid = P.rc_mode == 1 ? rc_window_of(P, g_vid) : g_vid;
-      g_kl = find_seg(P, g_wid);
-      const SegDesc S = P.segs[g_kl];
-      g_start = S.w_begin + (g_wid - P.seg_prefix[g_kl]);
-      if (P.rc_mode == 1) {  // skip decision and lookup made by rc_lookup_kernel
-        g_hit = P.rc_hits[g_vid];
-        g_pops = P.rc_hit_pops[g_vid];
-        active = g_hit.x != RC_DONE;
-      } else {
-        active = !window_skipped(P, S, g_start, err);
-      }
-    }
-    gm = __ballot(active);
-  };
-  auto next_window = [&](uint32_t& seg, uint64_t& st, uint64_t& vid, uint64_t& wid, RcHit& rc) __attribute__((always_inline)) -> bool {
-    for (;;) {
-      if (gm) {
-        const int l = first_lane(gm);
-        gm &= gm - 1;
-        seg = shfl_u32(g_kl, l);
-        st = shfl_u64(g_start, l);
-        vid = shfl_u64(g_vid, l);
-        wid = shfl_u64(g_wid, l);
-        rc = RcHit{shfl_u32(g_hit.x, l), shfl_u32(g_hit.y, l), shfl_u32(g_hit.z, l), shfl_u32(g_hit.w, l), shfl_u32(g_pops, l)};
-        return true;
-      }
-      if (any_err(err)) return false;
-      if (stage == 2) {  // the sub-range's next group with open windows
-        v0 += 64;
-        if (v0 < ce) {
-          if ((live_groups >> ((v0 - cb) >> 6)) & 1ull) load_group();
-          continue;
-        }
-        cb = cnext;
-        stage = 1;
-        continue;
-      }
-      if (stage == 1) {  // the chunk's next sub-range
-        if (cb >= ce0) {
-          cb0 = P.dyn_chunks ? next_chunk() : cb0 + stride;
-          stage = 0;
-          continue;
-        }
-        ce = ce0;
-        cnext = ce0;
-        if (regions) {
-          const uint64_t rg = cb / RC_REGION;
-          cnext = min(ce0, (rg + 1) * RC_REGION);
-          ce = min(cnext, rg * RC_REGION + P.rc_region_cnt[rg]);
-          if (cb >= ce) {
-            cb = cnext;
-            continue;
-          }
-        }
-        live_groups = ~0ull;
-        if (P.rc_mode == 1 && !P.win_list && P.chunk > 256) {  // the groups holding open windows
-          live_groups = 0ull;
-          const uint32_t ng = (uint32_t)((ce - cb + 63) / 64);  // P.chunk <= 4096: at most 64 groups
-          const uint32_t* hx = reinterpret_cast<const uint32_t*>(P.rc_hits);
-          for (uint32_t g = 0; g < ng; g += 8) {
-            uint32_t x[8];
-#pragma unroll
-            for (uint32_t q = 0; q < 8; ++q) {
-              const uint64_t v = cb + (uint64_t)(g + q) * 64 + lane;
-              x[q] = (g + q < ng && v < ce) ? hx[4 * v] : RC_DONE;
-            }
-#pragma unroll
-            for (uint32_t q = 0; q < 8; ++q)
-              if (__ballot(x[q] != RC_DONE)) live_groups |= 1ull << (g + q);
-          }
-        }
-        v0 = cb - 64;
-        stage = 2;
-        continue;
-      }
-      if (cb0 >= P.total_windows) return false;
-      ce0 = min(cb0 + (uint64_t)P.chunk, P.total_windows);
-      cb = cb0;
-      stage = 1;
-    }
-  };
-
-  // ---- the two windows
-  PairWin W0, W1;
-  W0.on = W1.on = 0u;
-  uint4* const ebuf = P.ebuf + (size_t)slot * P.ecap;  // the slot's emit scratch: half per window
-  const uint32_t ecap = P.ecap / 2;
-  bool feed = true;
-  // a window's start: the snapshot's queue into the window's ring, its best entries into its list
-  // (run_window's prologue; the dedup entries stay in the pool until a popped state needs them)
-  auto win_start = [&](PairWin& W, uint32_t w) __attribute__((always_inline)) {
-    W.on = 0u;
-    if (!feed) return;
-    uint32_t seg = 0;
-    RcHit rc{EMPTY, 0u, 0u, 0u, 0u};
-    if (!next_window(seg, W.start, W.vid, W.wid, rc)) {
-      feed = false;
-      return;
-    }
-    W.on = 1u;
-    const SegDesc S = P.segs[seg];
-    W.seg = seg;
-    W.tb = S.text_base + W.start;
-    W.n = (uint32_t)min(S.n - W.start, (uint64_t)(1u << 24));
-    W.avail = (uint32_t)min(S.avail > W.start ? S.avail - W.start : 0ull, (uint64_t)(1u << 24));
-    W.ascii = S.ascii;
-    W.ne = 0;
-    W.jlive = 0;
-    W.lmode = 0;
-    W.rc_off = rc.off;
-    W.rc_nq = 0;
-    KState* q = s_q + w * QCAP;
-    if (rc.off != EMPTY) {
-      W.head = rc.head;
-      W.tail = rc.tail;
-      const uint32_t nq = rc.tail - rc.head, nv = rc.nv_nel & 0xFFFFu, ne = rc.nv_nel >> 16;
-      W.rc_nq = nq;
-      if (nv) W.jlive = P.rc_pool[rc.off + 1].y;
-      if (P.lane_debug && lane == 0) atomicAdd(&g_live_dbg[W.jlive ? 4 : 5], 1ull);
-      const uint4* src = P.rc_pool + rc.off + RC_HDR;
-      for (uint32_t b = 0; b < nq; b += 256) {  // four loads in flight per lane, then their stores
-        uint4 v[4];
-#pragma unroll
-        for (uint32_t u = 0; u < 4; ++u) {
-          const uint32_t i = b + u * 64 + lane;
-          if (i < nq) v[u] = src[i];
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < 4; ++u) {
-          const uint32_t i = b + u * 64 + lane;
-          if (i < nq) q[(rc.head + i) & (QCAP - 1)] = KState{v[u].x, v[u].y, __uint_as_float(v[u].z), v[u].w};
-        }
-      }
-      uint4* eb = ebuf + w * ecap;
-      for (uint32_t i = lane; i < ne; i += 64) eb[i] = src[nq + nv + i];
-      W.ne = ne;
-      cached += rc.pops;  // the snapshot's pops (not counted as popped: that is executed work)
-    } else {
-      W.head = 0;
-      W.tail = 1;
-      if (lane == 0) q[0] = KState{0u, 0u, 0.0f, 0u};
-    }
-    __builtin_amdgcn_wave_barrier();
-  };
-  // a window's end: spilled (the dedup variant re-runs it from its start) or flushed (run_window)
-  auto win_end = [&](PairWin& W, uint32_t w, bool spilled) __attribute__((always_inline)) {
-    W.on = 0u;
-    if (spilled) {
-      if (lane == 0) {
-        const unsigned long long k = atomicAdd(P.counters + 3, 1ull);
-        if (k < P.spill_cap) P.spill[k] = W.vid;
-        else err |= ERR_SPILL;
-        if (P.lane_debug) atomicAdd(&g_live_dbg[6], 1ull);
-      }
-      return;
-    }
-    if (P.win_counts && lane == 0) P.win_counts[W.wid] = W.tail;
-    wave_mem_fence();
-    if (W.ne && !any_err(err)) {  // the window's best map (search.rs:1111-1118)
-      unsigned long long base = 0;
-      if (lane == 0) base = atomicAdd(P.counters, (unsigned long long)W.ne);
-      base = shfl_u64(base, 0);
-      const SegDesc S = P.segs[W.seg];
-      const uint64_t sb = S.byte_base + local_byte(P, S, W.start);
-      const uint4* eb = ebuf + w * ecap;
-      for (uint32_t i = lane; i < W.ne; i += 64) {
-        if (base + i >= P.out_cap) break;
-        P.out[base + i] = match_record(P, S, W.start, sb, eb[i]);
-      }
-    }
-  };
-  // the snapshot's check entries of window w into its table on first need (run_window LIVE); too
-  // many for the table: lmode 2, the window is spilled before the batch pops (the dedup variant takes it)
-  auto live_load = [&](PairWin& W, uint32_t w) __attribute__((always_inline)) {
-    const uint32_t nchk = W.jlive >> 16;
-    if (nchk > LCAP - LCAP / 4) {
-      W.lmode = 2u;
-      return;
-    }
-    KState* live = s_live + w * LCAP;
-    for (uint32_t i = lane; i < LCAP; i += 64) live[i].node = EMPTY;
-    __builtin_amdgcn_wave_barrier();
-    const uint4* src = P.rc_pool + W.rc_off + RC_HDR + W.rc_nq;
-    for (uint32_t i = lane; i < nchk; i += 64) {
-      const uint4 e = src[i];
-      uint32_t sl = vis_hash(KState{e.x, e.y, 0.f, e.w}) & (LCAP - 1);
-      while (atomicCAS(&live[sl].node, EMPTY, e.x) != EMPTY) sl = (sl + 1) & (LCAP - 1);
-      live[sl].jm = e.y;
-      live[sl].pen = __uint_as_float(e.z);
-      live[sl].packed = e.w;
-    }
-    __builtin_amdgcn_wave_barrier();
-    W.lmode = 1u;
-  };
-
-  win_start(W0, 0);
-  win_start(W1, 1);
-  const uint32_t beam2 = 2u * P.beam;
-  while ((W0.on | W1.on) && !any_err(err)) {
-    // per window: an empty queue ends it; a pending count past 2 bw spills it (the dedup-free pass
-    // cannot beam)
-    bool again = false;
-    if (W0.on && (W0.head >= W0.tail || (P.beam && W0.tail - W0.head > beam2))) {
-      win_end(W0, 0, W0.head < W0.tail);
-      win_start(W0, 0);
-      again = true;
-    }
-    if (W1.on && (W1.head >= W1.tail || (P.beam && W1.tail - W1.head > beam2))) {
-      win_end(W1, 1, W1.head < W1.tail);
-      win_start(W1, 1);
-      again = true;
-    }
-    if (again) continue;
-    const uint32_t P00 = W0.on ? W0.tail - W0.head : 0u, P01 = W1.on ? W1.tail - W1.head : 0u;
-    const uint32_t B0 = min(P00, max(32u, 64u - min(P01, 64u)));
-    const uint32_t B1 = min(P01, 64u - B0);
-    const uint64_t lo = B0 >= 64u ? ~0ull : ((1ull << B0) - 1ull);  // window 0's lanes
-    const bool s1 = lane >= B0;
-    const uint32_t idx = s1 ? lane - B0 : lane;
-    const bool in_b = lane < B0 + B1;
-    const uint32_t qoff = s1 ? QCAP : 0u;
-    KState st{EMPTY, 0u, 0.0f, 0u};
-    if (in_b) st = s_q[qoff + (((s1 ? W1.head : W0.head) + idx) & (QCAP - 1))];
-    // the lane's text, relative to its window's start
-    SegDesc V{};
-    V.text_base = s1 ? W1.tb : W0.tb;
-    V.n = s1 ? W1.n : W0.n;
-    V.avail = s1 ? W1.avail : W0.avail;
-    V.ascii = s1 ? W1.ascii : W0.ascii;
-    // ---- phase A (run_window): node record, char filters, text at j and j + 1
-    DevNode nd{};
-    uint32_t c0 = 0, c1 = 0;
-    uint4 aux = make_uint4(0, 0, 0, 0);
-    if (in_b) {
-      nd = P.nodes[st.node];
-      aux = P.aux[st.node];
-      const uint64_t j = st.jm & 0xFFFFu;
-      if (j < V.n) c0 = text_char(P, V, j, err);
-      if (j + 1 < V.n) c1 = text_char(P, V, j + 1, err);
-    }
-    // live dedup: the snapshot's popped states a state may still meet (run_window LIVE)
-    bool found = false;
-    uint32_t stored_bits = 0, vslot = EMPTY;
-    const uint32_t jl = s1 ? W1.jlive : W0.jlive;
-    const bool chk = in_b && jl && (st.jm & 0xFFFFu) + 1u <= (jl & 0xFFFFu);
-    const uint64_t mchk = __ballot(chk);
-    if (mchk) {
-      if ((mchk & lo) && W0.lmode == 0u) live_load(W0, 0);
-      if ((mchk & ~lo) && W1.lmode == 0u) live_load(W1, 1);
-      const uint32_t lm = s1 ? W1.lmode : W0.lmode;
-      if (chk && lm == 1u) vis_lookup<LCAP>(s_live + (s1 ? LCAP : 0u), st, found, stored_bits, vslot);
-      if (P.lane_debug && lane == 0) {
-        atomicAdd(&g_live_dbg[2], (unsigned long long)__popcll(mchk));
-        atomicAdd(&g_live_dbg[3], (unsigned long long)__popcll(__ballot(found && __uint_as_float(stored_bits) <= st.pen)));
-      }
-    }
-    const bool lsp0 = W0.on && W0.lmode == 2u, lsp1 = W1.on && W1.lmode == 2u;
-    if (lsp0 || lsp1) {
-      if (lsp0) {
-        win_end(W0, 0, true);
-        win_start(W0, 0);
-      }
-      if (lsp1) {
-        win_end(W1, 1, true);
-        win_start(W1, 1);
-      }
-      continue;
-    }
-    const bool skip = in_b && found && __uint_as_float(stored_bits) <= st.pen;  // :620
-    const bool alive = in_b && !skip && !(st.pen > __fsub_rn(nd.prune_len, __fmul_rn(nd.prune_lw, P.thr)));  // :638-642
-    if (!alive) nd = DevNode{};
-    const uint64_t mwide = __ballot(alive && node_deg(nd) > 64u);
-    // a window whose head state is wide (a node of more than 64 edges) takes this turn alone, its
-    // state expanded edge-parallel (run_window)
-    const bool wd0 = B0 && (mwide & 1ull), wd1 = !wd0 && B1 && ((mwide >> B0) & 1ull);
-    if (wd0 || wd1) {
-      KState* q = s_q + (wd1 ? QCAP : 0u);
-      uint32_t hd = wd1 ? W1.head : W0.head, tl = wd1 ? W1.tail : W0.tail;
-      const KState s0 = q[hd & (QCAP - 1)];
-      hd += 1;
-      popped += 1;
-      const DevNode n0 = P.nodes[s0.node];
-      if (node_has_out(n0)) {
-        EmitList E{ebuf + (wd1 ? ecap : 0u), ecap, wd1 ? W1.ne : W0.ne};
-        emit_state(P, E, s0.jm >> 16, s0.pen, s0.packed, s0.node, err);
-        if (wd1) W1.ne = E.n;
-        else W0.ne = E.n;
-      }
-      SegDesc Vw{};
-      Vw.text_base = wd1 ? W1.tb : W0.tb;
-      Vw.n = wd1 ? W1.n : W0.n;
-      Vw.avail = wd1 ? W1.avail : W0.avail;
-      Vw.ascii = wd1 ? W1.ascii : W0.ascii;
-      unsigned e2 = 0;
-      expand_wide<QCAP, false>(P, Vw, q, hd, tl, s0, n0, 0, e2);
-      err |= e2 & ~ERR_QUEUE;
-      const bool ov = (wave_or(e2) & ERR_QUEUE) != 0;  // the window's ring overflowed: spilled
-      if (wd1) {
-        W1.head = hd;
-        W1.tail = tl;
-        if (ov) {
-          win_end(W1, 1, true);
-          win_start(W1, 1);
-        }
-      } else {
-        W0.head = hd;
-        W0.tail = tl;
-        if (ov) {
-          win_end(W0, 0, true);
-          win_start(W0, 0);
-        }
-      }
-      continue;
-    }
-    uint32_t Bc0 = B0, Bc1 = B1;  // each window's states committed this turn
-    if (mwide & lo) Bc0 = (uint32_t)first_lane(mwide & lo);
-    if (mwide & ~lo) Bc1 = (uint32_t)first_lane(mwide & ~lo) - B0;
-    // ---- phase B: per-lane expansion decisions and push counts
-    const bool act = alive && idx < (s1 ? Bc1 : Bc0);
-    Prep pr{0u, 0u, 0u, 0u, 0.0f};
-    if (act) pr = lane_prep(P, V, st, nd, 0, c0, c1, nd.sb);
-    uint64_t msub = 0, mdel = 0;
-    uint32_t ex = 0u, xe = 0u;
-    const bool fast =
-        act && P.gt_fast && (!(pr.flags & PF_SUB) || P.p_sub <= pr.remaining || no_subs(P, nd, pr.cur_ch, pr.remaining));
-    if (__ballot(act && !fast)) expand_units<FAC_UK, false>(P, X, nd, pr, act && !fast, msub, mdel, ex, xe);
-    if (fast) expand_fast(P, st, nd, pr, aux, msub, mdel, ex, xe);
-    LaneExp x{-1, -1, false, 0ull, 0ull, 0u, 0ull};
-    if (act) x = lane_finish<false>(P, V, 0, st, nd, pr, msub, mdel, ex, xe, err);
-    const uint32_t cnt = (in_b && idx < (s1 ? Bc1 : Bc0)) ? x.count : 0u;
-    const uint32_t incl = wave_inclusive_sum(cnt);
-    const uint32_t base1 = B0 ? (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)B0 - 1) : 0u;
-    const uint32_t inclw = s1 ? incl - base1 : incl, exclw = inclw - cnt;
-    // cuts per window (run_window): before the pop whose pending count passes 2 bw, before a ring overflow
-    const uint32_t P0l = s1 ? P01 : P00, Bl = s1 ? Bc1 : Bc0;
-    const bool trig = in_b && idx >= 1 && idx < Bl && P.beam && (P0l - idx + exclw > beam2);
-    const bool ovf = in_b && idx < Bl && (P0l - idx - 1 + inclw > QCAP);
-    const uint64_t mcut = __ballot(trig) | __ballot(ovf);
-    if (mcut & lo) Bc0 = min(Bc0, (uint32_t)first_lane(mcut & lo));
-    if (mcut & ~lo) Bc1 = min(Bc1, (uint32_t)first_lane(mcut & ~lo) - B0);
-    const bool sp0 = B0 && Bc0 == 0, sp1 = B1 && Bc1 == 0;  // a window that cannot pop: spilled
-    const bool com = in_b && idx < (s1 ? Bc1 : Bc0);
-    // ---- phase D: emissions (FIFO order within each window), then pushes at tail + exclusive prefix
-    uint64_t mem = __ballot(alive && com && node_has_out(nd));
-    while (mem) {
-      const int l = first_lane(mem);
-      mem &= mem - 1;
-      const uint32_t a = shfl_u32(st.jm, l) >> 16, pk = shfl_u32(st.packed, l), nn = shfl_u32(st.node, l);
-      const float pe = shfl_f32(st.pen, l);
-      const bool w1 = (uint32_t)l >= B0;
-      EmitList E{ebuf + (w1 ? ecap : 0u), ecap, w1 ? W1.ne : W0.ne};
-      emit_state(P, E, a, pe, pk, nn, err);
-      if (w1) W1.ne = E.n;
-      else W0.ne = E.n;
-    }
-    push_units<QCAP, FAC_UK, false>(P, X, s_q, (s1 ? W1.tail : W0.tail) + exclw, st, nd, x, pr.cur_ch,
-                                    alive && com && x.count != 0, qoff);
-    __builtin_amdgcn_wave_barrier();
-    if (Bc0) W0.tail += (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)Bc0 - 1);
-    if (Bc1) W1.tail += (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)(B0 + Bc1) - 1) - base1;
-    W0.head += Bc0;
-    W1.head += Bc1;
-    popped += Bc0 + Bc1;
-    if (sp0) {
-      win_end(W0, 0, true);
-      win_start(W0, 0);
-    }
-    if (sp1) {
-      win_end(W1, 1, true);
-      win_start(W1, 1);
-    }
-  }
-  if (lane == 0) {
-    atomicAdd(P.counters + 1, (unsigned long long)popped);
-    if (cached) atomicAdd(P.counters + 4, (unsigned long long)cached);
-  }
-  const unsigned all = wave_or(err);
-  if (lane == 0 && all) atomicOr(reinterpret_cast<unsigned int*>(P.counters + 2), all);
-  slot_release(P, slot);
-}
-
-#ifndef FAC_PAIR_WAVES  // waves/SIMD bfs_window_kernel_pair is compiled for (VGPR budget)
-#define FAC_PAIR_WAVES 3
-#endif
-template <uint32_t QCAP>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FAC_PAIR_WAVES))) void bfs_window_kernel_pair(SearchParams P) {
-  live_pair_body<QCAP>(P);
-}
-
 // one wavefront per workgroup; the dedup-free variants are held to <= 128 VGPRs (4 waves/SIMD),
 // the dedup variants are bounded by LDS first
 #ifndef FAC_BEAM_WAVES  // waves/SIMD the dedup variants are compiled for (VGPR budget); 0 = unbounded
@@ -4308,10 +3860,7 @@ template <uint32_t Q>
 void launch_nd(uint32_t grid, hipStream_t s, const SearchParams& P) {
   if constexpr (Q == 256)
     if (P.beam && !P.has_map) {
-      // two windows per wave (FAC_PAIR; measured slower, profiles/r05_pair)
-      static const bool pair = diag_env("FAC_PAIR") != nullptr;
-      if (pair && !P.live_nqmax) hipLaunchKernelGGL((bfs_window_kernel_pair<Q>), dim3(grid), dim3(64), lds_pad(), s, P);
-      else hipLaunchKernelGGL((bfs_window_kernel_live<Q>), dim3(grid), dim3(64), lds_pad(), s, P);
+      hipLaunchKernelGGL((bfs_window_kernel_live<Q>), dim3(grid), dim3(64), lds_pad(), s, P);
       return;
     }
   if (P.has_map) hipLaunchKernelGGL((bfs_window_kernel_nd<Q, true>), dim3(grid), dim3(64), lds_pad(), s, P);
