@@ -3587,7 +3587,10 @@ constexpr uint32_t QG_BITS_WORDS = 2048;
 
 // Candidates collect in a per-wave LDS buffer and go out 512 at a time (one list atomic per flush: a
 // same-address atomic per wave turn serialised the scan at one L2 channel, 175 ms per GiB)
-constexpr uint32_t QG_BUF = 512;
+constexpr uint32_t QG_BUF = 256;
+// 8 waves per block share the screening bitmap: 8 KB + 3.5 KB per wave = 36 KB, 32 waves per CU (the
+// VGPR limit); 4-wave blocks with 512-entry buffers held 20
+constexpr uint32_t QG_WAVES = 8;
 // The bitmap screens every position first: only the ~3 % that pass (C5) probe the table in global
 // memory, 64 at a time from a per-wave LDS queue (one table round trip per 64 passing grams: probing
 // where they stood cost a round trip per wave step, since some lane of 64 passes almost every one).
@@ -3595,11 +3598,11 @@ constexpr uint32_t QG_BUF = 512;
 // into a pass mask, and the passes join the queue in rounds of one per lane (one ballot per round)
 // instead of a ballot per gram.
 constexpr uint32_t QG_PQ = 128;  // per-wave probe queue (LDS): < 64 left after a drain + one round
-__global__ __launch_bounds__(256) void qgram_scan_kernel(QgramParams Q) {
-  __shared__ unsigned long long s_buf[4][QG_BUF];
+__global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q) {
+  __shared__ unsigned long long s_buf[QG_WAVES][QG_BUF];
   __shared__ uint32_t s_bits[QG_BITS_WORDS];
-  __shared__ uint32_t s_pk[4][QG_PQ];
-  __shared__ uint64_t s_pp[4][QG_PQ];
+  __shared__ uint32_t s_pk[QG_WAVES][QG_PQ];
+  __shared__ uint64_t s_pp[QG_WAVES][QG_PQ];
   for (uint32_t x = threadIdx.x; x < QG_BITS_WORDS; x += blockDim.x) s_bits[x] = Q.bits[x];
   __syncthreads();
   unsigned long long* buf = s_buf[threadIdx.x / 64];
@@ -3742,45 +3745,58 @@ __global__ __launch_bounds__(256) void qgram_verify_kernel(QgramParams Q, uint64
   W r[KMAX + 1];
 #pragma unroll
   for (int d = 0; d <= KMAX; ++d) r[d] = d ? (((W)1 << d) - (W)1) : (W)0;  // prefilter.rs:415-418
-  // symbols 8 at a time: their loads, then their masks' loads, go out together (one pair of memory
-  // round trips per 8 symbols instead of per symbol); the recurrence then steps through them
-  constexpr uint32_t U = 8;
-  for (uint64_t i0 = s0; i0 < e_max; i0 += U) {
-    uint32_t sym[U];
+  // the symbols [s0, e_max) in aligned 4-symbol words, up to 64 per pass, loaded together; their masks
+  // 16 at a time (one round trip for the words and one per 16 masks: C5's candidates span ~23
+  // symbols, three round trips instead of six); W = uint32_t reads the masks' low halves only
+  const uint32_t* ids32 = reinterpret_cast<const uint32_t*>(Q.ids);
+  const uint32_t* mask32 = reinterpret_cast<const uint32_t*>(mask);
+  for (uint64_t base = s0 & ~3ull; base < e_max; base += 64) {
+    uint32_t wd[16];
+    const uint64_t nw = min<uint64_t>(16, (e_max - base + 3) / 4);
 #pragma unroll
-    for (uint32_t u = 0; u < U; ++u) sym[u] = i0 + u < e_max ? Q.ids[i0 + u] : 0u;
-    W bcs[U];
+    for (uint32_t u = 0; u < 16; ++u) wd[u] = u < nw ? ids32[(base >> 2) + u] : 0u;
 #pragma unroll
-    for (uint32_t u = 0; u < U; ++u) bcs[u] = (W)mask[sym[u]];
+    for (uint32_t c = 0; c < 4; ++c) {
+      if (base + 16 * c >= e_max) break;
+      W bcs[16];
 #pragma unroll
-    for (uint32_t u = 0; u < U; ++u) {
-      const uint64_t i = i0 + u;
-      if (i >= e_max) break;
-      const W bc = bcs[u];
-      W prev_old = r[0];
-      W prev_new = ((r[0] << 1) | (W)1) & bc;
-      r[0] = prev_new;
-      W hit = (k == 0) ? prev_new : (W)0;
-#pragma unroll
-      for (int d = 1; d <= KMAX; ++d) {
-        const W old = r[d];
-        const W nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | (W)1;
-        r[d] = nv;
-        prev_old = old;
-        prev_new = nv;
-        if ((uint32_t)d == k) hit = nv;
+      for (uint32_t v = 0; v < 16; ++v) {
+        const uint64_t i = base + 16 * c + v;
+        const uint32_t sym = (wd[4 * c + v / 4] >> (8 * (v % 4))) & 0xFFu;
+        if (i >= s0 && i < e_max) bcs[v] = sizeof(W) == 4 ? (W)mask32[2 * sym] : (W)mask[sym];
+        else bcs[v] = (W)0;
       }
-      const uint64_t end = i + 1;
-      if (end >= e_min && (hit & top)) {  // coverage [end - m - k, end), as bitap_kernel
-        const uint64_t span = (uint64_t)m + k;
-        const uint64_t ws = end > span ? end - span : 0;
-        for (uint64_t y = ws; y < end;) {
-          const uint64_t w = y >> 5;
-          const uint32_t l = (uint32_t)(y & 31);
-          const uint32_t cnt = (uint32_t)min((uint64_t)(32 - l), end - y);
-          const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << l;
-          atomicOr(Q.cover + w, bits);
-          y += cnt;
+#pragma unroll
+      for (uint32_t v = 0; v < 16; ++v) {
+        const uint64_t i = base + 16 * c + v;
+        if (i >= e_max) break;
+        if (i < s0) continue;
+        const W bc = bcs[v];
+        W prev_old = r[0];
+        W prev_new = ((r[0] << 1) | (W)1) & bc;
+        r[0] = prev_new;
+        W hit = (k == 0) ? prev_new : (W)0;
+#pragma unroll
+        for (int d = 1; d <= KMAX; ++d) {
+          const W old = r[d];
+          const W nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | (W)1;
+          r[d] = nv;
+          prev_old = old;
+          prev_new = nv;
+          if ((uint32_t)d == k) hit = nv;
+        }
+        const uint64_t end = i + 1;
+        if (end >= e_min && (hit & top)) {  // coverage [end - m - k, end), as bitap_kernel
+          const uint64_t span = (uint64_t)m + k;
+          const uint64_t ws = end > span ? end - span : 0;
+          for (uint64_t y = ws; y < end;) {
+            const uint64_t w = y >> 5;
+            const uint32_t l = (uint32_t)(y & 31);
+            const uint32_t cnt = (uint32_t)min((uint64_t)(32 - l), end - y);
+            const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << l;
+            atomicOr(Q.cover + w, bits);
+            y += cnt;
+          }
         }
       }
     }
@@ -5282,7 +5298,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
   if (n == 0) return FAC_OK;
   const uint32_t np = (uint32_t)e.bp_m.size();
   DevBuf d_ids, d_k, d_cover, d_runs, d_cnt;
-  HIP_TRY(d_ids.alloc(n + 32, stream));  // padded: the scan's 16-byte loads and next word
+  HIP_TRY(d_ids.alloc(n + 80, stream));  // padded: the scan's 16-byte loads and next word, verify's 64-symbol passes
   if (view.ascii) {  // transcode, ASCII text (prefilter.rs:253-258): one byte per grapheme
     const uint64_t threads = (n + 15) / 16;
     hipLaunchKernelGGL(transcode_ascii_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, stream,
@@ -5476,7 +5492,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     Q.bits = static_cast<const uint32_t*>(d_qbits.p);
     int cus = 256;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
-    const uint32_t sgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 4095) / 4096, (uint64_t)cus * 16));
+    const uint32_t sgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 8191) / 8192, (uint64_t)cus * 8));
     uint64_t qcap = std::max<uint64_t>(1 << 20, n / 16);
     unsigned long long nc = 0;
     for (;;) {  // candidates: one scan, again with room for all of them if the list overflowed
@@ -5484,7 +5500,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
       Q.cand = static_cast<unsigned long long*>(d_qcand.p);
       Q.cap = qcap;
       HIP_TRY(hipMemsetAsync(d_qn.p, 0, 8, stream));
-      hipLaunchKernelGGL(qgram_scan_kernel, dim3(sgrid), dim3(256), 0, stream, Q);
+      hipLaunchKernelGGL(qgram_scan_kernel, dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipMemcpyAsync(&nc, d_qn.p, 8, hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
