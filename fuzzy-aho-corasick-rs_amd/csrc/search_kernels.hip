@@ -3544,8 +3544,14 @@ __global__ __launch_bounds__(256) void bitap_kernel(BitapParams B) {
 // same coverage bits as bitap_kernel. Every hit of every gram-eligible pattern is thus found (and no
 // other: the recurrence is exact), so the merged windows equal the full scan's.
 struct QgramParams {
+  // the text: symbol ids (ids mode), or an ASCII haystack's bytes read directly (bytes mode: the
+  // grams are keyed by case-folded bytes, verify maps bytes to ids through aid); text position i is
+  // buffer byte off + i (the buffer 16-byte aligned), and bytes at or past nsafe are never read
   const uint8_t* ids;
   uint64_t n;
+  uint64_t nsafe;
+  uint32_t off, bytes, ci;
+  const uint8_t* aid;
   const uint2* tab;        // open addressing: {gram key, first entry << 8 | entries} (0: empty slot)
   uint32_t tab_mask;
   const uint32_t* ent;     // entries: pattern << 8 | piece offset
@@ -3598,6 +3604,20 @@ constexpr uint32_t QG_WAVES = 8;
 // into a pass mask, and the passes join the queue in rounds of one per lane (one ballot per round)
 // instead of a ballot per gram.
 constexpr uint32_t QG_PQ = 128;  // per-wave probe queue (LDS): < 64 left after a drain + one round
+// 4 buffer bytes from byte b (4-aligned), zero at and past nsafe
+__device__ __forceinline__ uint32_t qg_word(const QgramParams& Q, uint64_t b) {
+  if (b + 4 <= Q.nsafe) return reinterpret_cast<const uint32_t*>(Q.ids)[b >> 2];
+  uint32_t w = 0;
+  for (uint32_t u = 0; u < 4; ++u)
+    if (b + u < Q.nsafe) w |= (uint32_t)Q.ids[b + u] << (8 * u);
+  return w;
+}
+// ASCII case folding of four bytes < 0x80 (the engine's fold for ASCII haystacks, builder.cpp ascii_id)
+__device__ __forceinline__ uint32_t qg_fold(uint32_t w) {
+  const uint32_t t = w | 0x80808080u;
+  const uint32_t up = ((t - 0x41414141u) & ~(t - 0x5B5B5B5Bu)) & 0x80808080u;  // bytes in 'A'..'Z'
+  return w + (up >> 2);
+}
 __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q) {
   __shared__ unsigned long long s_buf[QG_WAVES][QG_BUF];
   __shared__ uint32_t s_bits[QG_BITS_WORDS];
@@ -3656,23 +3676,33 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
   // buffer is padded 32 bytes past n; positions whose gram would cross n are not looked up); the
   // next turn's loads are issued before this turn's screening
   const uint4* ids16 = reinterpret_cast<const uint4*>(Q.ids);
-  const uint32_t* ids32 = reinterpret_cast<const uint32_t*>(Q.ids);
-  const uint64_t n16 = (Q.n + 15) / 16;  // position sixteens
+  const uint64_t nbuf = Q.off + Q.n;  // buffer bytes of the text
+  const uint64_t n16 = (nbuf + 15) / 16;  // buffer sixteens
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t lane64 = threadIdx.x % 64;
   uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x - lane64;  // whole waves iterate together
+  auto load = [&](uint64_t g, uint4& a, uint32_t& x) {
+    if (16 * g + 20 <= Q.nsafe) {
+      a = ids16[g];
+      x = reinterpret_cast<const uint32_t*>(Q.ids)[4 * g + 4];
+    } else {  // the text's last sixteens: no read at or past nsafe
+      a = make_uint4(qg_word(Q, 16 * g), qg_word(Q, 16 * g + 4), qg_word(Q, 16 * g + 8), qg_word(Q, 16 * g + 12));
+      x = qg_word(Q, 16 * g + 16);
+    }
+  };
   uint4 an = make_uint4(0u, 0u, 0u, 0u);
   uint32_t xn = 0;
-  if (g0 + lane64 < n16) {
-    an = ids16[g0 + lane64];
-    xn = ids32[4 * (g0 + lane64) + 4];
-  }
+  if (g0 + lane64 < n16) load(g0 + lane64, an, xn);
   for (; g0 < n16; g0 += stride) {
     const uint64_t g = g0 + lane64;
-    const uint32_t w0 = an.x, w1 = an.y, w2 = an.z, w3 = an.w, w4 = xn;
-    if (g0 + stride + lane64 < n16) {  // prefetch
-      an = ids16[g0 + stride + lane64];
-      xn = ids32[4 * (g0 + stride + lane64) + 4];
+    uint32_t w0 = an.x, w1 = an.y, w2 = an.z, w3 = an.w, w4 = xn;
+    if (g0 + stride + lane64 < n16) load(g0 + stride + lane64, an, xn);  // prefetch
+    if (Q.bytes && Q.ci) {
+      w0 = qg_fold(w0);
+      w1 = qg_fold(w1);
+      w2 = qg_fold(w2);
+      w3 = qg_fold(w3);
+      w4 = qg_fold(w4);
     }
     // symbols j .. j + 3 of this thread's sixteen (value selects: a select of references became a
     // pointer array in scratch)
@@ -3687,7 +3717,8 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
       hi = q >= 3u ? w4 : hi;
       return __builtin_amdgcn_alignbyte(hi, lo, j & 3u);
     };
-    // pass mask: bit 2j = the 4-gram at position 16g + j, bit 2j + 1 = its 3-gram
+    // pass mask: bit 2j = the 4-gram at buffer byte 16g + j (text position 16g + j - off), bit
+    // 2j + 1 = its 3-gram
     uint32_t pm = 0;
     if (g < n16) {
 #pragma unroll
@@ -3695,8 +3726,9 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
         const uint64_t i = 16 * g + j;
         const uint32_t k4 = gram4(j), k3 = (k4 & 0xFFFFFFu) | 0xFF000000u;
         const uint32_t b4 = qgram_bit(k4), b3 = qgram_bit(k3);
-        const bool p4 = Q.use4 && i + 4 <= Q.n && ((s_bits[b4 >> 5] >> (b4 & 31u)) & 1u);
-        const bool p3 = Q.use3 && i + 3 <= Q.n && ((s_bits[b3 >> 5] >> (b3 & 31u)) & 1u);
+        const bool in = i >= Q.off;
+        const bool p4 = Q.use4 && in && i + 4 <= nbuf && ((s_bits[b4 >> 5] >> (b4 & 31u)) & 1u);
+        const bool p3 = Q.use3 && in && i + 3 <= nbuf && ((s_bits[b3 >> 5] >> (b3 & 31u)) & 1u);
         pm |= (p4 ? 1u : 0u) << (2 * j);
         pm |= (p3 ? 1u : 0u) << (2 * j + 1);
       }
@@ -3714,7 +3746,7 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
         const uint32_t k4 = gram4(j);
         const uint32_t at = nq + prefix_below(m);
         pk[at] = (bit & 1u) ? ((k4 & 0xFFFFFFu) | 0xFF000000u) : k4;
-        pp[at] = 16 * g + j;
+        pp[at] = 16 * g + j - Q.off;
       }
       nq += (uint32_t)__popcll(m);
     }
@@ -3727,6 +3759,10 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
 // W: the automaton word, uint32_t when every q-gram pattern has m <= 32 (half the 64-bit VALU work)
 template <int KMAX, typename W>
 __global__ __launch_bounds__(256) void qgram_verify_kernel(QgramParams Q, uint64_t n_cand) {
+  __shared__ uint8_t s_aid[128];  // bytes mode: byte -> symbol id
+  if (Q.bytes)
+    for (uint32_t i = threadIdx.x; i < 128; i += blockDim.x) s_aid[i] = Q.aid[i];
+  __syncthreads();
   const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (x >= n_cand) return;
   const unsigned long long cd = Q.cand[x];
@@ -3748,29 +3784,37 @@ __global__ __launch_bounds__(256) void qgram_verify_kernel(QgramParams Q, uint64
   // the symbols [s0, e_max) in aligned 4-symbol words, up to 64 per pass, loaded together; their masks
   // 16 at a time (one round trip for the words and one per 16 masks: C5's candidates span ~23
   // symbols, three round trips instead of six); W = uint32_t reads the masks' low halves only
-  const uint32_t* ids32 = reinterpret_cast<const uint32_t*>(Q.ids);
+  // (text positions; buffer byte = position + off, both 4-aligned when base is: off % 4 folded in)
   const uint32_t* mask32 = reinterpret_cast<const uint32_t*>(mask);
-  for (uint64_t base = s0 & ~3ull; base < e_max; base += 64) {
+  const uint32_t sh = Q.off & 3u;
+  for (uint64_t base = (s0 + sh) & ~3ull; base < e_max + sh; base += 64) {  // buffer bytes - (off - sh)
     uint32_t wd[16];
-    const uint64_t nw = min<uint64_t>(16, (e_max - base + 3) / 4);
+    const uint64_t nw = min<uint64_t>(16, (e_max + sh - base + 3) / 4);
+    const uint64_t bb = base + (Q.off - sh);  // the buffer byte of word 0 (4-aligned)
+    if (bb + 64 <= Q.nsafe) {
+      const uint32_t* w32 = reinterpret_cast<const uint32_t*>(Q.ids) + (bb >> 2);
 #pragma unroll
-    for (uint32_t u = 0; u < 16; ++u) wd[u] = u < nw ? ids32[(base >> 2) + u] : 0u;
+      for (uint32_t u = 0; u < 16; ++u) wd[u] = u < nw ? w32[u] : 0u;
+    } else {  // the text's end: no read at or past nsafe
+      for (uint32_t u = 0; u < 16; ++u) wd[u] = u < nw ? qg_word(Q, bb + 4 * u) : 0u;
+    }
 #pragma unroll
     for (uint32_t c = 0; c < 4; ++c) {
-      if (base + 16 * c >= e_max) break;
+      if (base + 16 * c >= e_max + sh) break;
       W bcs[16];
 #pragma unroll
       for (uint32_t v = 0; v < 16; ++v) {
-        const uint64_t i = base + 16 * c + v;
-        const uint32_t sym = (wd[4 * c + v / 4] >> (8 * (v % 4))) & 0xFFu;
-        if (i >= s0 && i < e_max) bcs[v] = sizeof(W) == 4 ? (W)mask32[2 * sym] : (W)mask[sym];
+        const uint64_t i = base + 16 * c + v - sh;  // text position (may wrap below 0: skipped)
+        uint32_t sym = (wd[4 * c + v / 4] >> (8 * (v % 4))) & 0xFFu;
+        if (Q.bytes) sym = s_aid[sym & 0x7Fu];
+        if (base + 16 * c + v >= s0 + sh && i < e_max) bcs[v] = sizeof(W) == 4 ? (W)mask32[2 * sym] : (W)mask[sym];
         else bcs[v] = (W)0;
       }
 #pragma unroll
       for (uint32_t v = 0; v < 16; ++v) {
-        const uint64_t i = base + 16 * c + v;
-        if (i >= e_max) break;
-        if (i < s0) continue;
+        const uint64_t i = base + 16 * c + v - sh;
+        if (base + 16 * c + v >= e_max + sh) break;
+        if (base + 16 * c + v < s0 + sh) continue;
         const W bc = bcs[v];
         W prev_old = r[0];
         W prev_new = ((r[0] << 1) | (W)1) & bc;
@@ -5298,16 +5342,6 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
   if (n == 0) return FAC_OK;
   const uint32_t np = (uint32_t)e.bp_m.size();
   DevBuf d_ids, d_k, d_cover, d_runs, d_cnt;
-  HIP_TRY(d_ids.alloc(n + 80, stream));  // padded: the scan's 16-byte loads and next word, verify's 64-symbol passes
-  if (view.ascii) {  // transcode, ASCII text (prefilter.rs:253-258): one byte per grapheme
-    const uint64_t threads = (n + 15) / 16;
-    hipLaunchKernelGGL(transcode_ascii_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, stream,
-                       h.d_utf8 + view.text_base, n, e.d_ascii_id, static_cast<uint8_t*>(d_ids.p));
-    HIP_TRY(hipGetLastError());
-  } else {
-    ensure_symbols(e, h);
-    HIP_TRY(hipMemcpyAsync(d_ids.p, h.sym.data() + view.text_base, n, hipMemcpyHostToDevice, stream));
-  }
   const uint32_t rows = e.alphabet + 1;
   // Pigeonhole q-gram path (qgram_scan_kernel / qgram_verify_kernel) for the patterns whose k + 1
   // pieces are at least 3 symbols long; the rest go through the full bitap scan.
@@ -5371,6 +5405,38 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     wused[w] += m;
   }
   const uint32_t nw = (uint32_t)wk.size();
+  // Every pattern on the q-gram path of an ASCII text (16-byte aligned bytes): the scan and verify read
+  // the haystack's bytes themselves (grams keyed by case-folded bytes, ids looked up per candidate
+  // symbol), no transcode pass (0.66 ms per GiB at C5). Otherwise the text's symbol ids
+  // (prefilter.rs:253-260): transcoded on the device, or the host's for Unicode text.
+  const uint8_t* vb = h.d_utf8 + view.text_base;
+  const bool bytes_mode = view.ascii && nw == 0 && !grams.empty() && ((uintptr_t)h.d_utf8 & 15u) == 0 &&
+                          !diag_env("FAC_QGRAM_IDS");
+  if (!bytes_mode) {
+    HIP_TRY(d_ids.alloc(n + 80, stream));  // padded: the scan's 16-byte loads and next word, verify's 64-symbol passes
+    if (view.ascii) {  // transcode, ASCII text (prefilter.rs:253-258): one byte per grapheme
+      const uint64_t threads = (n + 15) / 16;
+      hipLaunchKernelGGL(transcode_ascii_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, stream, vb, n,
+                         e.d_ascii_id, static_cast<uint8_t*>(d_ids.p));
+      HIP_TRY(hipGetLastError());
+    } else {
+      ensure_symbols(e, h);
+      HIP_TRY(hipMemcpyAsync(d_ids.p, h.sym.data() + view.text_base, n, hipMemcpyHostToDevice, stream));
+    }
+  } else {  // the grams re-keyed by bytes: each id's folded ASCII char (0x80: none, never in the text)
+    uint8_t byte_of_id[256];
+    std::memset(byte_of_id, 0x80, sizeof(byte_of_id));
+    for (uint32_t b = 0; b < 128; ++b) {
+      const uint32_t id = e.ascii_id[b];
+      if (id && byte_of_id[id] == 0x80) byte_of_id[id] = (uint8_t)(e.case_insensitive && b - 'A' < 26u ? b + 32u : b);
+    }
+    for (auto& g : grams) {
+      const uint32_t k = g.first, q4 = (k >> 24) != 0xFFu;
+      g.first = qgram_key(byte_of_id[k & 0xFFu], byte_of_id[(k >> 8) & 0xFFu], byte_of_id[(k >> 16) & 0xFFu],
+                          q4 ? byte_of_id[k >> 24] : 0u, q4);
+    }
+    std::sort(grams.begin(), grams.end());
+  }
   std::vector<uint64_t> pmask((size_t)rows * nw, 0), ptop(nw, 0);
   for (uint32_t i : order) {
     const uint32_t w = place[i].first, off = place[i].second;
@@ -5479,6 +5545,15 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     QgramParams Q{};
     Q.ids = static_cast<const uint8_t*>(d_ids.p);
     Q.n = n;
+    Q.nsafe = n + 80;
+    if (bytes_mode) {
+      Q.ids = reinterpret_cast<const uint8_t*>((uintptr_t)vb & ~(uintptr_t)15);
+      Q.off = (uint32_t)(vb - Q.ids);
+      Q.nsafe = (uint64_t)(h.d_utf8 + h.len - Q.ids);
+      Q.bytes = 1;
+      Q.ci = e.case_insensitive ? 1u : 0u;
+      Q.aid = e.d_ascii_id;
+    }
     Q.tab = static_cast<const uint2*>(d_qtab.p);
     Q.tab_mask = ts - 1;
     Q.ent = static_cast<const uint32_t*>(d_qent.p);

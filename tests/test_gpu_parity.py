@@ -242,6 +242,44 @@ def test_qgram_prefilter_c5_slice(monkeypatch):
     assert prefilter_windows(gpu, small, w.threshold) == OracleEngine(b, w.patterns).prefilter_windows(small, w.threshold)
 
 
+@pytest.mark.parametrize("ci", [False, True])
+def test_qgram_bytes_mode_matches_ids_and_full_scan(ci, monkeypatch):
+    """Every pattern on the q-gram path of an ASCII text: the scan and verify read the haystack's bytes
+    (grams keyed by case-folded bytes, symbol ids looked up per candidate) instead of a transcoded id
+    buffer. Windows == the id-buffer q-gram path (FAC_QGRAM_IDS) == the packed full scan == the oracle's
+    bitap_windows + merge (prefilter.rs:319-342), mixed-case text, and the pre-filtered search equals the
+    plain one (prefilter.rs:467-546)."""
+    from fuzzy_aho_corasick.engine import prefilter_windows
+    rng = Rng(0xB17E_5_0DE ^ int(ci))
+    alpha = "abcdefghijklmnopqrstuvwxyz"
+    pats = ["".join(alpha[rng.next() % 26] for _ in range(12 + rng.next() % 5)) for _ in range(60)]
+    words = []
+    for _ in range(3000):
+        if rng.next() % 5 == 0:
+            w = list(pats[rng.next() % len(pats)])
+            w[rng.next() % len(w)] = alpha[rng.next() % 26]
+        else:
+            w = [alpha[rng.next() % 26] for _ in range(2 + rng.next() % 10)]
+        words.append("".join(c.upper() if rng.next() % 3 == 0 else c for c in w))
+    hay = " ".join(words) + "."
+    b = B().case_insensitive(ci).fuzzy(L().edits(2))
+    gpu = b.build(pats)
+    orc = OracleEngine(b, pats)
+    for thr in (0.8, 0.9):
+        got = prefilter_windows(gpu, hay, thr)
+        monkeypatch.setenv("FAC_QGRAM_IDS", "1")
+        ids = prefilter_windows(gpu, hay, thr)
+        monkeypatch.setenv("FAC_NO_QGRAM", "1")
+        full = prefilter_windows(gpu, hay, thr)
+        monkeypatch.delenv("FAC_QGRAM_IDS")
+        monkeypatch.delenv("FAC_NO_QGRAM")
+        assert got and got == ids == full == orc.prefilter_windows(hay, thr)
+        for cut in (1, 5, 13):  # other text lengths: the last sixteens read byte by byte up to the end
+            sub = hay[:len(hay) - cut]
+            assert prefilter_windows(gpu, sub, thr) == orc.prefilter_windows(sub, thr)
+    assert rows(gpu.with_prefilter().search(hay, O().threshold(0.8))) == rows(gpu.search(hay, O().threshold(0.8)))
+
+
 def test_edge_inputs():
     b = B().fuzzy(L().edits(2))
     compare(b, ["abc"], "", 0.0)                      # empty haystack

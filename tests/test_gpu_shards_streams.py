@@ -151,7 +151,7 @@ def test_stream_windows_on_device_equal_whole_input(prefilter):
     st = StagedHaystack(eng, hay)
     import torch
     from fuzzy_aho_corasick._native import MATCH_DTYPE
-    for win in (64 << 10, 200 << 10):
+    for win in (64 << 10, 200 << 10, 100_003):  # (100 003: windows at unaligned byte offsets)
         got = []
         # and fac_stream_window_staged_device (bench.py --config c5 at N > 1): every window's owned
         # records appended in HBM to one buffer, started tiny so it must grow, gathered from there
