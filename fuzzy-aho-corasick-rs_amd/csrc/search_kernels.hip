@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <type_traits>
 #include <vector>
 
 #include "fac_internal.h"
@@ -3720,18 +3721,22 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
     // pass mask: bit 2j = the 4-gram at buffer byte 16g + j (text position 16g + j - off), bit
     // 2j + 1 = its 3-gram
     uint32_t pm = 0;
-    if (g < n16) {
+    auto screen = [&](auto all_in) {  // all_in: every gram of the sixteen lies inside the text
 #pragma unroll
       for (uint32_t j = 0; j < 16; ++j) {
         const uint64_t i = 16 * g + j;
         const uint32_t k4 = gram4(j), k3 = (k4 & 0xFFFFFFu) | 0xFF000000u;
         const uint32_t b4 = qgram_bit(k4), b3 = qgram_bit(k3);
-        const bool in = i >= Q.off;
-        const bool p4 = Q.use4 && in && i + 4 <= nbuf && ((s_bits[b4 >> 5] >> (b4 & 31u)) & 1u);
-        const bool p3 = Q.use3 && in && i + 3 <= nbuf && ((s_bits[b3 >> 5] >> (b3 & 31u)) & 1u);
+        const bool in = all_in || i >= Q.off;
+        const bool p4 = Q.use4 && in && (all_in || i + 4 <= nbuf) && ((s_bits[b4 >> 5] >> (b4 & 31u)) & 1u);
+        const bool p3 = Q.use3 && in && (all_in || i + 3 <= nbuf) && ((s_bits[b3 >> 5] >> (b3 & 31u)) & 1u);
         pm |= (p4 ? 1u : 0u) << (2 * j);
         pm |= (p3 ? 1u : 0u) << (2 * j + 1);
       }
+    };
+    if (g < n16) {
+      if (16 * g >= Q.off && 16 * g + 19 <= nbuf) screen(std::true_type{});
+      else screen(std::false_type{});
     }
     // rounds: each lane's next pass joins the queue (in lane order within a round)
     for (;;) {
