@@ -392,6 +392,7 @@ def run_c5(args, world, rank, local):
     from fuzzy_aho_corasick import workloads as W
     from fuzzy_aho_corasick.engine import StagedHaystack
     from fuzzy_aho_corasick.distributed import gather_device, stream_share_windows
+    from fuzzy_aho_corasick._native import MATCH_DTYPE
 
     block_bytes = int((args.mib if args.mib is not None else DEFAULT_MIB["c5"]) * (1 << 20))
     wl = W.config("c5", block_bytes, seed=5)
@@ -406,26 +407,22 @@ def run_c5(args, world, rank, local):
     processed_rank = sum(w[2] for w in windows)
     stream = torch.cuda.current_stream().cuda_stream
 
-    dev_recs = [torch.empty(1 << 20, dtype=torch.uint8, device=torch.device("cuda", local))] if world > 1 else None
+    dev_recs = [torch.empty(1 << 20, dtype=torch.uint8, device=torch.device("cuda", local))]
 
     def step():
-        parts, pf_ms, k_ms = [], 0.0, 0.0
-        if world > 1:  # owned records ranked and kept in HBM per window, then one RCCL gather from there
-            n = 0
-            for (g0, g1, commit, base) in windows:
-                dev_recs[0], got, st = staged.stream_window_device(g0, g1, commit, base, wl.threshold, True,
-                                                                   dev_recs[0], n, stream=stream)
-                n += got
-                pf_ms += st.prefilter_ms
-                k_ms += st.kernel_ms
-            gathered = gather_device(dev_recs[0], n, 0)
-            return (gathered.numel() // 32 if gathered is not None else 0), pf_ms, k_ms
+        # every window's owned records (stream.rs:262-297, ranked on the device) appended in HBM, then
+        # at N > 1 one RCCL gather to rank 0 from there, at N = 1 one copy to host memory
+        pf_ms, k_ms, n = 0.0, 0.0, 0
         for (g0, g1, commit, base) in windows:
-            recs, st = staged.stream_window(g0, g1, commit, base, wl.threshold, True, stream=stream)
-            parts.append(recs)
+            dev_recs[0], got, st = staged.stream_window_device(g0, g1, commit, base, wl.threshold, True,
+                                                               dev_recs[0], n, stream=stream)
+            n += got
             pf_ms += st.prefilter_ms
             k_ms += st.kernel_ms
-        recs = np.concatenate(parts)
+        if world > 1:
+            gathered = gather_device(dev_recs[0], n, 0)
+            return (gathered.numel() // 32 if gathered is not None else 0), pf_ms, k_ms
+        recs = dev_recs[0][: n * 32].cpu().numpy().view(MATCH_DTYPE)
         return len(recs), pf_ms, k_ms
 
     for _ in range(args.warmup):
@@ -465,7 +462,7 @@ def run_c5(args, world, rank, local):
         print(json.dumps({
             "metric": METRIC, "value": processed / elapsed / 1e9, "unit": "Gchars/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8 symbol ids / u32 bitap words",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8 haystack bytes / u32 bitap words",
             "data": f"synthetic: {total / (1 << 30):g} GiB stream = repeats of one {B}-byte block "
                     "(SURVEY.md §8(d) generator, 1 planted needle per MiB), resident in HBM",
             "config": {"workload": "c5: " + WORKLOAD["c5"], "patterns": len(wl.patterns),

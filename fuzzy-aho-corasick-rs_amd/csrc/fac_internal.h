@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <unordered_map>
 #include <string>
@@ -291,6 +292,27 @@ struct SearchParams {
 constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8u, ERR_OUT = 16u, ERR_SPILL = 32u;
 
 // ---------------------------------------------------------------- engine
+// The pre-filter's device tables for one set of edit budgets (search_kernels.hip prefilter_windows):
+// the packed full-scan words and the q-gram path's gram table, screening bitmap and pattern masks.
+// Built on a call's first use and kept by the engine (they depend on the engine and ks alone).
+struct PfTables {
+  std::vector<uint32_t> ks;
+  bool want_bytes = false;  // the key: built for a byte-reading scan (if the q-gram path takes every pattern),
+  bool qgram_on = true;     // and the FAC_NO_QGRAM knob's state
+  bool bytes = false;       // the grams keyed by case-folded bytes (else by symbol ids)
+  uint32_t nw = 0, kmax = 0;  // packed full scan: automaton words, largest edit budget
+  bool w32 = true;
+  void *pmask = nullptr, *ptop = nullptr, *wk = nullptr;
+  bool q = false;           // q-gram path in use
+  uint32_t ts = 0, use3 = 0, use4 = 0, kq = 0, mq = 0;
+  size_t n_qpat = 0, n_grams = 0, n_keys = 0;
+  void *tab = nullptr, *ent = nullptr, *qmask = nullptr, *qpm = nullptr, *qbits = nullptr;
+  ~PfTables() {
+    for (void* p : {pmask, ptop, wk, tab, ent, qmask, qpm, qbits})
+      if (p) (void)hipFree(p);
+  }
+};
+
 struct Engine {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -376,6 +398,8 @@ struct Engine {
   // per-engine device scratch of the search launcher, reused across calls by whichever call holds
   // scratch_mu (a concurrent call on the same engine allocates its own)
   mutable std::mutex scratch_mu;
+  mutable std::mutex pf_mu;  // guards pf_cache
+  mutable std::vector<std::unique_ptr<PfTables>> pf_cache;
   static constexpr int kScratch = 64;
   mutable void* scratch_p[kScratch] = {};
   mutable size_t scratch_n[kScratch] = {};

@@ -4144,6 +4144,7 @@ void free_engine_device(Engine& e) {
                   e.d_map_ent, e.d_map_hay};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  e.pf_cache.clear();
   for (int i = 0; i < Engine::kScratch; ++i)
     if (e.scratch_p[i]) {
       (void)hipFree(e.scratch_p[i]);
@@ -5337,22 +5338,34 @@ int auto_beam_total(const Engine& e, const Haystack& h, const std::vector<SegDes
   return rc;
 }
 
-int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, const std::vector<uint32_t>& ks,
-                      hipStream_t stream, std::vector<std::pair<uint64_t, uint64_t>>& windows, fac_stats* stats,
-                      std::string& err) {
-  windows.clear();
-  HIP_TRY(hipSetDevice(e.device));
-  if (!stream) stream = e.stream;
-  const uint64_t n = view.n;
-  if (n == 0) return FAC_OK;
+// The pre-filter's device tables for the edit budgets ks (PfTables), built once per engine, ks and
+// mode: the packed full-scan words and the q-gram path's tables (want_bytes: keyed by case-folded
+// bytes when the q-gram path takes every pattern). Host work and uploads measured 0.41 ms per C5
+// stream window when rebuilt per call.
+int pf_tables(const Engine& e, const std::vector<uint32_t>& ks, bool want_bytes, const PfTables*& out, std::string& err) {
+  const bool qgram_on = !diag_env("FAC_NO_QGRAM");
+  std::lock_guard<std::mutex> lk(e.pf_mu);
+  for (const auto& t : e.pf_cache)
+    if (t->ks == ks && t->want_bytes == want_bytes && t->qgram_on == qgram_on) {
+      out = t.get();
+      return FAC_OK;
+    }
+  auto T = std::make_unique<PfTables>();
+  T->ks = ks;
+  T->want_bytes = want_bytes;
+  T->qgram_on = qgram_on;
   const uint32_t np = (uint32_t)e.bp_m.size();
-  DevBuf d_ids, d_k, d_cover, d_runs, d_cnt;
   const uint32_t rows = e.alphabet + 1;
+  auto upload_raw = [&](const void* src, size_t bytes, void*& dst) -> int {
+    HIP_TRY(hipMalloc(&dst, std::max<size_t>(bytes, 16)));
+    if (bytes) HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return FAC_OK;
+  };
   // Pigeonhole q-gram path (qgram_scan_kernel / qgram_verify_kernel) for the patterns whose k + 1
   // pieces are at least 3 symbols long; the rest go through the full bitap scan.
   std::vector<uint8_t> qlen(np, 0);
   std::vector<std::pair<uint32_t, uint32_t>> grams;  // (gram key, pattern << 8 | piece offset)
-  if (!diag_env("FAC_NO_QGRAM") && rows <= 256) {
+  if (qgram_on && rows <= 256) {
     std::vector<uint32_t> sym(64);
     for (uint32_t i = 0; i < np; ++i) {
       const uint32_t m = e.bp_m[i], k = ks[i], L = m / (k + 1);
@@ -5410,25 +5423,13 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     wused[w] += m;
   }
   const uint32_t nw = (uint32_t)wk.size();
-  // Every pattern on the q-gram path of an ASCII text (16-byte aligned bytes): the scan and verify read
-  // the haystack's bytes themselves (grams keyed by case-folded bytes, ids looked up per candidate
-  // symbol), no transcode pass (0.66 ms per GiB at C5). Otherwise the text's symbol ids
-  // (prefilter.rs:253-260): transcoded on the device, or the host's for Unicode text.
-  const uint8_t* vb = h.d_utf8 + view.text_base;
-  const bool bytes_mode = view.ascii && nw == 0 && !grams.empty() && ((uintptr_t)h.d_utf8 & 15u) == 0 &&
-                          !diag_env("FAC_QGRAM_IDS");
-  if (!bytes_mode) {
-    HIP_TRY(d_ids.alloc(n + 80, stream));  // padded: the scan's 16-byte loads and next word, verify's 64-symbol passes
-    if (view.ascii) {  // transcode, ASCII text (prefilter.rs:253-258): one byte per grapheme
-      const uint64_t threads = (n + 15) / 16;
-      hipLaunchKernelGGL(transcode_ascii_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, stream, vb, n,
-                         e.d_ascii_id, static_cast<uint8_t*>(d_ids.p));
-      HIP_TRY(hipGetLastError());
-    } else {
-      ensure_symbols(e, h);
-      HIP_TRY(hipMemcpyAsync(d_ids.p, h.sym.data() + view.text_base, n, hipMemcpyHostToDevice, stream));
-    }
-  } else {  // the grams re-keyed by bytes: each id's folded ASCII char (0x80: none, never in the text)
+  T->nw = nw;
+  T->w32 = w32;
+  for (uint32_t i : order) T->kmax = std::max(T->kmax, ks[i]);
+  // Every pattern on the q-gram path: an ASCII text's bytes are read by the scan itself, so its grams
+  // are keyed by each id's folded ASCII char (0x80: none, never in the text)
+  T->bytes = want_bytes && nw == 0 && !grams.empty();
+  if (T->bytes) {
     uint8_t byte_of_id[256];
     std::memset(byte_of_id, 0x80, sizeof(byte_of_id));
     for (uint32_t b = 0; b < 128; ++b) {
@@ -5448,65 +5449,17 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     ptop[w] |= 1ull << (off + e.bp_m[i] - 1);
     for (uint32_t c = 0; c < rows; ++c) pmask[(size_t)c * nw + w] |= e.bp_mask[(size_t)i * rows + c] << off;
   }
-  DevBuf d_pmask, d_ptop;
   if (w32) {
     std::vector<uint32_t> m32(pmask.begin(), pmask.end()), t32(ptop.begin(), ptop.end());
-    HIP_TRY(d_pmask.alloc(m32.size() * 4, stream));
-    HIP_TRY(d_ptop.alloc(t32.size() * 4, stream));
-    HIP_TRY(hipMemcpyAsync(d_pmask.p, m32.data(), m32.size() * 4, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(d_ptop.p, t32.data(), t32.size() * 4, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipStreamSynchronize(stream));  // pageable sources: complete before the vectors go
+    if (int rc = upload_raw(m32.data(), m32.size() * 4, T->pmask)) return rc;
+    if (int rc = upload_raw(t32.data(), t32.size() * 4, T->ptop)) return rc;
   } else {
-    HIP_TRY(d_pmask.alloc(pmask.size() * 8, stream));
-    HIP_TRY(d_ptop.alloc(ptop.size() * 8, stream));
-    HIP_TRY(hipMemcpyAsync(d_pmask.p, pmask.data(), pmask.size() * 8, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(d_ptop.p, ptop.data(), ptop.size() * 8, hipMemcpyHostToDevice, stream));
+    if (int rc = upload_raw(pmask.data(), pmask.size() * 8, T->pmask)) return rc;
+    if (int rc = upload_raw(ptop.data(), ptop.size() * 8, T->ptop)) return rc;
   }
-  HIP_TRY(d_k.alloc(nw * 4, stream));
-  HIP_TRY(hipMemcpyAsync(d_k.p, wk.data(), nw * 4, hipMemcpyHostToDevice, stream));
-  HIP_TRY(hipStreamSynchronize(stream));  // pageable sources: complete before the vectors go
-  const uint64_t n_words = (n + 31) / 32;
-  HIP_TRY(d_cover.alloc(n_words * 4, stream));
-  HIP_TRY(hipMemsetAsync(d_cover.p, 0, n_words * 4, stream));
-  Events ev;
-  HIP_TRY(hipEventCreate(&ev.a));
-  HIP_TRY(hipEventCreate(&ev.b));
-  HIP_TRY(hipEventRecord(ev.a, stream));
-  BitapParams B{};
-  B.ids = static_cast<const uint8_t*>(d_ids.p);
-  B.n = n;
-  B.mask_t = d_pmask.p;
-  B.top = d_ptop.p;
-  B.k = static_cast<const uint32_t*>(d_k.p);
-  B.n_words = nw;
-  B.seg_len = 4096;
-  B.cover = static_cast<uint32_t*>(d_cover.p);
-  const uint64_t segs = (n + B.seg_len - 1) / B.seg_len;
-  const uint64_t waves = segs * ((nw + 63) / 64);
-  uint32_t kmax = 0;
-  for (uint32_t i : order) kmax = std::max(kmax, ks[i]);
-  const dim3 bgrid((uint32_t)std::max<uint64_t>(1, (waves + 3) / 4));
-  if (nw == 0) {
-    // every pattern takes the q-gram path
-  } else if (w32) {
-    if (kmax == 0) hipLaunchKernelGGL((bitap_kernel<0, uint32_t>), bgrid, dim3(256), 0, stream, B);
-    else if (kmax == 1) hipLaunchKernelGGL((bitap_kernel<1, uint32_t>), bgrid, dim3(256), 0, stream, B);
-    else if (kmax == 2) hipLaunchKernelGGL((bitap_kernel<2, uint32_t>), bgrid, dim3(256), 0, stream, B);
-    else if (kmax <= 4) hipLaunchKernelGGL((bitap_kernel<4, uint32_t>), bgrid, dim3(256), 0, stream, B);
-    else if (kmax <= 8) hipLaunchKernelGGL((bitap_kernel<8, uint32_t>), bgrid, dim3(256), 0, stream, B);
-    else if (kmax <= 16) hipLaunchKernelGGL((bitap_kernel<16, uint32_t>), bgrid, dim3(256), 0, stream, B);
-    else hipLaunchKernelGGL((bitap_kernel<24, uint32_t>), bgrid, dim3(256), 0, stream, B);
-  } else {
-    if (kmax <= 1) hipLaunchKernelGGL((bitap_kernel<1, uint64_t>), bgrid, dim3(256), 0, stream, B);
-    else if (kmax <= 2) hipLaunchKernelGGL((bitap_kernel<2, uint64_t>), bgrid, dim3(256), 0, stream, B);
-    else if (kmax <= 4) hipLaunchKernelGGL((bitap_kernel<4, uint64_t>), bgrid, dim3(256), 0, stream, B);
-    else if (kmax <= 8) hipLaunchKernelGGL((bitap_kernel<8, uint64_t>), bgrid, dim3(256), 0, stream, B);
-    else if (kmax <= 16) hipLaunchKernelGGL((bitap_kernel<16, uint64_t>), bgrid, dim3(256), 0, stream, B);
-    else hipLaunchKernelGGL((bitap_kernel<24, uint64_t>), bgrid, dim3(256), 0, stream, B);
-  }
-  HIP_TRY(hipGetLastError());
-  DevBuf d_qtab, d_qent, d_qmask, d_qpm, d_qcand, d_qn, d_qbits;
+  if (int rc = upload_raw(wk.data(), wk.size() * 4, T->wk)) return rc;
   if (!grams.empty()) {
+    T->q = true;
     std::vector<uint32_t> ent(grams.size());
     std::vector<std::pair<uint32_t, uint32_t>> keys;  // (key, first entry << 8 | entries)
     for (size_t a = 0, b; a < grams.size(); a = b) {
@@ -5527,31 +5480,103 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
       qbits[b >> 5] |= 1u << (b & 31u);
     }
     std::vector<uint32_t> pm(np, 0);
-    uint32_t kq = 0, mq = 0;  // largest edit budget / pattern length on the q-gram path
-    bool use3 = false, use4 = false;
     for (uint32_t i = 0; i < np; ++i)
       if (qlen[i]) {
         pm[i] = e.bp_m[i] | (ks[i] << 8);
-        kq = std::max(kq, ks[i]);
-        mq = std::max(mq, e.bp_m[i]);
-        (qlen[i] == 4 ? use4 : use3) = true;
+        T->kq = std::max(T->kq, ks[i]);
+        T->mq = std::max(T->mq, e.bp_m[i]);
+        (qlen[i] == 4 ? T->use4 : T->use3) = 1u;
+        T->n_qpat += 1;
       }
-    HIP_TRY(d_qtab.alloc(tab.size() * sizeof(uint2), stream));
-    HIP_TRY(d_qent.alloc(ent.size() * 4, stream));
-    HIP_TRY(d_qmask.alloc(e.bp_mask.size() * 8, stream));
-    HIP_TRY(d_qpm.alloc(pm.size() * 4, stream));
-    HIP_TRY(d_qbits.alloc(qbits.size() * 4, stream));
-    HIP_TRY(hipMemcpyAsync(d_qbits.p, qbits.data(), qbits.size() * 4, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(d_qtab.p, tab.data(), tab.size() * sizeof(uint2), hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(d_qent.p, ent.data(), ent.size() * 4, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(d_qmask.p, e.bp_mask.data(), e.bp_mask.size() * 8, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(d_qpm.p, pm.data(), pm.size() * 4, hipMemcpyHostToDevice, stream));
+    T->ts = ts;
+    T->n_grams = grams.size();
+    T->n_keys = keys.size();
+    if (int rc = upload_raw(tab.data(), tab.size() * sizeof(uint2), T->tab)) return rc;
+    if (int rc = upload_raw(ent.data(), ent.size() * 4, T->ent)) return rc;
+    if (int rc = upload_raw(e.bp_mask.data(), e.bp_mask.size() * 8, T->qmask)) return rc;
+    if (int rc = upload_raw(pm.data(), pm.size() * 4, T->qpm)) return rc;
+    if (int rc = upload_raw(qbits.data(), qbits.size() * 4, T->qbits)) return rc;
+  }
+  out = T.get();
+  e.pf_cache.push_back(std::move(T));
+  return FAC_OK;
+}
+
+int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, const std::vector<uint32_t>& ks,
+                      hipStream_t stream, std::vector<std::pair<uint64_t, uint64_t>>& windows, fac_stats* stats,
+                      std::string& err) {
+  windows.clear();
+  HIP_TRY(hipSetDevice(e.device));
+  if (!stream) stream = e.stream;
+  const uint64_t n = view.n;
+  if (n == 0) return FAC_OK;
+  // An ASCII text whose bytes lie 16-byte aligned can be read by the q-gram scan itself, with no
+  // transcode pass (0.66 ms per GiB at C5), when the q-gram path takes every pattern (pf_tables)
+  const uint8_t* vb = h.d_utf8 + view.text_base;
+  const bool want_bytes = view.ascii && ((uintptr_t)h.d_utf8 & 15u) == 0 && !diag_env("FAC_QGRAM_IDS");
+  const PfTables* T = nullptr;
+  if (int rc = pf_tables(e, ks, want_bytes, T, err)) return rc;
+  const uint32_t nw = T->nw;
+  DevBuf d_ids, d_cover, d_runs, d_cnt;
+  if (!T->bytes) {  // the text's symbol ids (prefilter.rs:253-260)
+    HIP_TRY(d_ids.alloc(n + 80, stream));  // padded: the scan's 16-byte loads and next word, verify's 64-symbol passes
+    if (view.ascii) {  // transcode, ASCII text (prefilter.rs:253-258): one byte per grapheme
+      const uint64_t threads = (n + 15) / 16;
+      hipLaunchKernelGGL(transcode_ascii_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, stream, vb, n,
+                         e.d_ascii_id, static_cast<uint8_t*>(d_ids.p));
+      HIP_TRY(hipGetLastError());
+    } else {
+      ensure_symbols(e, h);
+      HIP_TRY(hipMemcpyAsync(d_ids.p, h.sym.data() + view.text_base, n, hipMemcpyHostToDevice, stream));
+    }
+  }
+  const uint64_t n_words = (n + 31) / 32;
+  HIP_TRY(d_cover.alloc(n_words * 4, stream));
+  HIP_TRY(hipMemsetAsync(d_cover.p, 0, n_words * 4, stream));
+  Events ev;
+  HIP_TRY(hipEventCreate(&ev.a));
+  HIP_TRY(hipEventCreate(&ev.b));
+  HIP_TRY(hipEventRecord(ev.a, stream));
+  BitapParams B{};
+  B.ids = static_cast<const uint8_t*>(d_ids.p);
+  B.n = n;
+  B.mask_t = T->pmask;
+  B.top = T->ptop;
+  B.k = static_cast<const uint32_t*>(T->wk);
+  B.n_words = nw;
+  B.seg_len = 4096;
+  B.cover = static_cast<uint32_t*>(d_cover.p);
+  const uint64_t segs = (n + B.seg_len - 1) / B.seg_len;
+  const uint64_t waves = segs * ((nw + 63) / 64);
+  const uint32_t kmax = T->kmax;
+  const dim3 bgrid((uint32_t)std::max<uint64_t>(1, (waves + 3) / 4));
+  if (nw == 0) {
+    // every pattern takes the q-gram path
+  } else if (T->w32) {
+    if (kmax == 0) hipLaunchKernelGGL((bitap_kernel<0, uint32_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax == 1) hipLaunchKernelGGL((bitap_kernel<1, uint32_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax == 2) hipLaunchKernelGGL((bitap_kernel<2, uint32_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 4) hipLaunchKernelGGL((bitap_kernel<4, uint32_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 8) hipLaunchKernelGGL((bitap_kernel<8, uint32_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 16) hipLaunchKernelGGL((bitap_kernel<16, uint32_t>), bgrid, dim3(256), 0, stream, B);
+    else hipLaunchKernelGGL((bitap_kernel<24, uint32_t>), bgrid, dim3(256), 0, stream, B);
+  } else {
+    if (kmax <= 1) hipLaunchKernelGGL((bitap_kernel<1, uint64_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 2) hipLaunchKernelGGL((bitap_kernel<2, uint64_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 4) hipLaunchKernelGGL((bitap_kernel<4, uint64_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 8) hipLaunchKernelGGL((bitap_kernel<8, uint64_t>), bgrid, dim3(256), 0, stream, B);
+    else if (kmax <= 16) hipLaunchKernelGGL((bitap_kernel<16, uint64_t>), bgrid, dim3(256), 0, stream, B);
+    else hipLaunchKernelGGL((bitap_kernel<24, uint64_t>), bgrid, dim3(256), 0, stream, B);
+  }
+  HIP_TRY(hipGetLastError());
+  DevBuf d_qcand, d_qn;
+  if (T->q) {
     HIP_TRY(d_qn.alloc(8, stream));
     QgramParams Q{};
     Q.ids = static_cast<const uint8_t*>(d_ids.p);
     Q.n = n;
     Q.nsafe = n + 80;
-    if (bytes_mode) {
+    if (T->bytes) {
       Q.ids = reinterpret_cast<const uint8_t*>((uintptr_t)vb & ~(uintptr_t)15);
       Q.off = (uint32_t)(vb - Q.ids);
       Q.nsafe = (uint64_t)(h.d_utf8 + h.len - Q.ids);
@@ -5559,17 +5584,17 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
       Q.ci = e.case_insensitive ? 1u : 0u;
       Q.aid = e.d_ascii_id;
     }
-    Q.tab = static_cast<const uint2*>(d_qtab.p);
-    Q.tab_mask = ts - 1;
-    Q.ent = static_cast<const uint32_t*>(d_qent.p);
-    Q.use3 = use3;
-    Q.use4 = use4;
+    Q.tab = static_cast<const uint2*>(T->tab);
+    Q.tab_mask = T->ts - 1;
+    Q.ent = static_cast<const uint32_t*>(T->ent);
+    Q.use3 = T->use3;
+    Q.use4 = T->use4;
     Q.n_cand = static_cast<unsigned long long*>(d_qn.p);
-    Q.pmask = static_cast<const uint64_t*>(d_qmask.p);
-    Q.pm = static_cast<const uint32_t*>(d_qpm.p);
-    Q.rows = rows;
+    Q.pmask = static_cast<const uint64_t*>(T->qmask);
+    Q.pm = static_cast<const uint32_t*>(T->qpm);
+    Q.rows = e.alphabet + 1;
     Q.cover = static_cast<uint32_t*>(d_cover.p);
-    Q.bits = static_cast<const uint32_t*>(d_qbits.p);
+    Q.bits = static_cast<const uint32_t*>(T->qbits);
     int cus = 256;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
     const uint32_t sgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 8191) / 8192, (uint64_t)cus * 8));
@@ -5589,7 +5614,8 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     }
     if (nc) {
       const dim3 vg((uint32_t)((nc + 255) / 256));
-      if (mq <= 32) {
+      const uint32_t kq = T->kq;
+      if (T->mq <= 32) {
         if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
         else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
         else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
@@ -5605,9 +5631,8 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
       HIP_TRY(hipGetLastError());
     }
     if (diag_env("FAC_RC_DEBUG"))
-      std::fprintf(stderr, "FAC_QGRAM patterns=%zu/%u grams=%zu keys=%zu candidates=%llu full-scan words=%u\n",
-                   (size_t)std::count_if(qlen.begin(), qlen.end(), [](uint8_t v) { return v != 0; }), np,
-                   grams.size(), keys.size(), nc, nw);
+      std::fprintf(stderr, "FAC_QGRAM patterns=%zu/%zu grams=%zu keys=%zu candidates=%llu full-scan words=%u bytes=%d\n",
+                   T->n_qpat, e.bp_m.size(), T->n_grams, T->n_keys, nc, nw, (int)T->bytes);
   }
   uint64_t cap = 1 << 16;
   HIP_TRY(d_cnt.alloc(8, stream));
