@@ -759,9 +759,16 @@ int fac_stream_window_staged_device(const fac_engine* engine, const fac_haystack
   // best-per-key merge is a no-op before the ranking), or the whole view where it falls back
   std::vector<fac::SegDesc> segs;
   std::vector<uint32_t> ks;
+  const bool timing = fac::diag_env("FAC_TIMING") != nullptr;  // diagnostics: host wall-clock phases
+  const auto t0 = std::chrono::steady_clock::now();
+  auto ms_since = [&](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+  };
+  double t_pf = 0, t_segs = 0, t_search = 0;
   if (prefilter && e.bitap_ok && prefilter_ks(e, threshold, ks)) {
     std::vector<std::pair<uint64_t, uint64_t>> windows;
     if (int rc = fac::prefilter_windows(e, h, view, ks, st, windows, stats, err)) return fail(rc, err);
+    t_pf = ms_since(t0);
     for (auto& w : windows) {
       const uint64_t gs = w.first, ge = std::min<uint64_t>(w.second, view.n);
       if (view.ascii) {
@@ -782,6 +789,7 @@ int fac_stream_window_staged_device(const fac_engine* engine, const fac_haystack
   } else {
     segs.push_back(view);
   }
+  t_segs = ms_since(t0);
   if (segs.empty()) return FAC_OK;
   // raw records into a device buffer (grown and searched again if a window ever needs more)
   uint64_t cap = 1u << 16;
@@ -796,8 +804,12 @@ int fac_stream_window_staged_device(const fac_engine* engine, const fac_haystack
       cap = sink.n;
       continue;
     }
+    t_search = ms_since(t0);
     const int rc = fac::window_owned_device(e, sink.dev, sink.dev + cap, sink.n, view.byte_base, commit_bytes, base, st,
                                             static_cast<fac_match*>(device_out), device_cap, n_out, err);
+    if (timing)
+      std::fprintf(stderr, "FAC_TIMING window: prefilter %.3f, segs %.3f (%zu), search %.3f, owned %.3f ms\n", t_pf,
+                   t_segs - t_pf, segs.size(), t_search - t_segs, ms_since(t0) - t_search);
     if (rc == FAC_E_OUTPUT_CAPACITY) return fail(rc, "device output buffer too small (*n_out = records needed)");
     if (rc) return fail(rc, err);
     return FAC_OK;

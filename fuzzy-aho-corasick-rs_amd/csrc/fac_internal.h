@@ -307,8 +307,10 @@ struct PfTables {
   uint32_t ts = 0, use3 = 0, use4 = 0, kq = 0, mq = 0;
   size_t n_qpat = 0, n_grams = 0, n_keys = 0;
   void *tab = nullptr, *ent = nullptr, *qmask = nullptr, *qpm = nullptr, *qbits = nullptr;
+  void* m16 = nullptr;      // every q-gram pattern m <= 16: 16-bit masks [pattern][rows] for LDS
+  uint32_t m16_words = 0;
   ~PfTables() {
-    for (void* p : {pmask, ptop, wk, tab, ent, qmask, qpm, qbits})
+    for (void* p : {pmask, ptop, wk, tab, ent, qmask, qpm, qbits, m16})
       if (p) (void)hipFree(p);
   }
 };

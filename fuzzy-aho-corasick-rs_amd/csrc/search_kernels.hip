@@ -3555,7 +3555,7 @@ struct QgramParams {
   const uint8_t* aid;
   const uint2* tab;        // open addressing: {gram key, first entry << 8 | entries} (0: empty slot)
   uint32_t tab_mask;
-  const uint32_t* ent;     // entries: pattern << 8 | piece offset
+  const uint2* ent;        // entries: {pattern << 8 | piece offset, m | k << 8} (one load per candidate)
   uint32_t use3, use4;     // gram lengths in use
   unsigned long long* cand;  // candidates: text position << 24 | entry index
   unsigned long long* n_cand;
@@ -3565,6 +3565,8 @@ struct QgramParams {
   uint32_t rows;
   uint32_t* cover;
   const uint32_t* bits;    // QG_BITS_WORDS: screening bitmap of the grams (qgram_bit)
+  const uint32_t* m16;     // every q-gram pattern m <= 16: [pattern][rows] 16-bit masks, m16_words words
+  uint32_t m16_words;
 };
 __host__ __device__ inline uint32_t qgram_key(uint32_t a, uint32_t b, uint32_t c, uint32_t d, bool q4) {
   return q4 ? (a | (b << 8) | (c << 16) | (d << 24)) : (a | (b << 8) | (c << 16) | 0xFF000000u);
@@ -3762,18 +3764,14 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
 }
 
 // W: the automaton word, uint32_t when every q-gram pattern has m <= 32 (half the 64-bit VALU work)
-template <int KMAX, typename W>
-__global__ __launch_bounds__(256) void qgram_verify_kernel(QgramParams Q, uint64_t n_cand) {
-  __shared__ uint8_t s_aid[128];  // bytes mode: byte -> symbol id
-  if (Q.bytes)
-    for (uint32_t i = threadIdx.x; i < 128; i += blockDim.x) s_aid[i] = Q.aid[i];
-  __syncthreads();
-  const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= n_cand) return;
+// One candidate (qgram_verify_kernel). LM: every q-gram pattern has m <= 16 and their masks fit in
+// LDS (16-bit, pattern-major): the mask reads are LDS reads instead of L2 round trips.
+template <int KMAX, typename W, bool LM>
+__device__ __forceinline__ void verify_one(const QgramParams& Q, uint64_t x, const uint8_t* s_aid, const uint16_t* s_m16) {
   const unsigned long long cd = Q.cand[x];
   const uint64_t t = cd >> 24;
-  const uint32_t e = Q.ent[cd & 0xFFFFFFu], p = e >> 8, o = e & 0xFFu;
-  const uint32_t mk = Q.pm[p], m = mk & 0xFFu, k = mk >> 8;
+  const uint2 en = Q.ent[cd & 0xFFFFFFu];
+  const uint32_t p = en.x >> 8, o = en.x & 0xFFu, m = en.y & 0xFFu, k = en.y >> 8;
   // ends the candidate allows, 1-based: [t + m - o - k, t + m - o + k], clipped to the text
   const int64_t lo = (int64_t)t + m - o - k, hi = (int64_t)t + m - o + k;
   const uint64_t e_min = (uint64_t)max<int64_t>(1, lo);
@@ -3782,6 +3780,7 @@ __global__ __launch_bounds__(256) void qgram_verify_kernel(QgramParams Q, uint64
   const uint64_t warm = (uint64_t)m + k;
   const uint64_t s0 = e_min - 1 > warm ? e_min - 1 - warm : 0;
   const uint64_t* mask = Q.pmask + (size_t)p * Q.rows;
+  const uint16_t* mask16 = s_m16 + (size_t)p * Q.rows;  // LM: the pattern's masks in LDS
   const W top = (W)1 << (m - 1);
   W r[KMAX + 1];
 #pragma unroll
@@ -3812,7 +3811,8 @@ __global__ __launch_bounds__(256) void qgram_verify_kernel(QgramParams Q, uint64
         const uint64_t i = base + 16 * c + v - sh;  // text position (may wrap below 0: skipped)
         uint32_t sym = (wd[4 * c + v / 4] >> (8 * (v % 4))) & 0xFFu;
         if (Q.bytes) sym = s_aid[sym & 0x7Fu];
-        if (base + 16 * c + v >= s0 + sh && i < e_max) bcs[v] = sizeof(W) == 4 ? (W)mask32[2 * sym] : (W)mask[sym];
+        if (base + 16 * c + v >= s0 + sh && i < e_max)
+          bcs[v] = LM ? (W)mask16[sym] : sizeof(W) == 4 ? (W)mask32[2 * sym] : (W)mask[sym];
         else bcs[v] = (W)0;
       }
 #pragma unroll
@@ -3849,6 +3849,24 @@ __global__ __launch_bounds__(256) void qgram_verify_kernel(QgramParams Q, uint64
         }
       }
     }
+  }
+}
+
+template <int KMAX, typename W, bool LM>
+__global__ __launch_bounds__(LM ? 512 : 256) void qgram_verify_kernel(QgramParams Q, uint64_t n_cand) {
+  __shared__ uint8_t s_aid[128];  // bytes mode: byte -> symbol id
+  extern __shared__ uint16_t s_m16[];  // LM: Q.m16_words 32-bit words of 16-bit masks
+  if (Q.bytes)
+    for (uint32_t i = threadIdx.x; i < 128; i += blockDim.x) s_aid[i] = Q.aid[i];
+  if constexpr (LM)
+    for (uint32_t i = threadIdx.x; i < Q.m16_words; i += blockDim.x) reinterpret_cast<uint32_t*>(s_m16)[i] = Q.m16[i];
+  __syncthreads();
+  if constexpr (LM) {  // persistent: the table is loaded once per block
+    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n_cand; x += (uint64_t)gridDim.x * blockDim.x)
+      verify_one<KMAX, W, LM>(Q, x, s_aid, s_m16);
+  } else {
+    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < n_cand) verify_one<KMAX, W, LM>(Q, x, s_aid, s_m16);
   }
 }
 
@@ -4063,6 +4081,24 @@ struct DevBuf {
     release();
     s = stream;
     return hipMalloc(&p, bytes);
+  }
+};
+
+// Stream-ordered call scratch (call_scratch_take / give, pooled per thread and size class): the
+// pre-filter's per-call buffers -- hipMalloc + hipFree of C5's 0.5 GB candidate list and 134 MB
+// coverage bitmap per stream window stalled the device ~0.5 ms a window
+struct PoolBuf {
+  void* p = nullptr;
+  hipStream_t s = nullptr;
+  ~PoolBuf() {
+    if (p) call_scratch_give(p, s);
+  }
+  hipError_t alloc(size_t bytes, hipStream_t stream) {
+    if (p) call_scratch_give(p, s);
+    s = stream;
+    hipError_t e = hipSuccess;
+    p = call_scratch_take(std::max<size_t>(bytes, 16), stream, &e);
+    return e;
   }
 };
 
@@ -4458,6 +4494,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   }
   HIP_TRY(d_segs.alloc(segs.size() * sizeof(SegDesc), stream));
   HIP_TRY(d_prefix.alloc(prefix.size() * sizeof(uint64_t), stream));
+  if (timing) std::fprintf(stderr, "FAC_TIMING launch_pass setup before the segment upload %.3f ms\n", host_ms());
   HIP_TRY(hipMemcpyAsync(d_segs.p, segs.data(), segs.size() * sizeof(SegDesc), hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(d_prefix.p, prefix.data(), prefix.size() * sizeof(uint64_t), hipMemcpyHostToDevice, stream));
   uint64_t out_cap = std::max<uint64_t>(4096, windows / 64);
@@ -4560,8 +4597,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     HIP_TRY(hipMemsetAsync(ct.p, 0, (size_t)cs * 2 * sizeof(uint4), bs));
     return FAC_OK;
   };
+  // (segments of < 1024 windows on average -- the pre-filter's merged windows -- share too few keys
+  // for the cache's counts and builds: C5 212.7 vs 241.5 Gchars/s with it off, round 5 profiles/r05s)
   if (!root_out && !e.has_map && fan_root + 1 <= 4096 && kVariants[vi].qcap <= 4096 &&
-      windows >= (rc_min ? std::strtoull(rc_min, nullptr, 10) : 4096ull) && !diag_env("FAC_NO_RC")) {
+      windows >= (rc_min ? std::strtoull(rc_min, nullptr, 10) : 4096ull) &&
+      (rc_min || windows >= 1024ull * segs.size()) && !diag_env("FAC_NO_RC")) {
     auto env_u = [](const char* name, uint64_t dflt) {
       const char* v = diag_env(name);
       return v ? std::strtoull(v, nullptr, 10) : dflt;
@@ -5460,10 +5500,13 @@ int pf_tables(const Engine& e, const std::vector<uint32_t>& ks, bool want_bytes,
   if (int rc = upload_raw(wk.data(), wk.size() * 4, T->wk)) return rc;
   if (!grams.empty()) {
     T->q = true;
-    std::vector<uint32_t> ent(grams.size());
+    std::vector<uint2> ent(grams.size());
     std::vector<std::pair<uint32_t, uint32_t>> keys;  // (key, first entry << 8 | entries)
     for (size_t a = 0, b; a < grams.size(); a = b) {
-      for (b = a; b < grams.size() && grams[b].first == grams[a].first; ++b) ent[b] = grams[b].second;
+      for (b = a; b < grams.size() && grams[b].first == grams[a].first; ++b) {
+        const uint32_t i = grams[b].second >> 8;
+        ent[b] = make_uint2(grams[b].second, e.bp_m[i] | (ks[i] << 8));
+      }
       keys.push_back({grams[a].first, (uint32_t)(a << 8) | (uint32_t)(b - a)});
     }
     uint32_t ts = 64;
@@ -5492,10 +5535,19 @@ int pf_tables(const Engine& e, const std::vector<uint32_t>& ks, bool want_bytes,
     T->n_grams = grams.size();
     T->n_keys = keys.size();
     if (int rc = upload_raw(tab.data(), tab.size() * sizeof(uint2), T->tab)) return rc;
-    if (int rc = upload_raw(ent.data(), ent.size() * 4, T->ent)) return rc;
+    if (int rc = upload_raw(ent.data(), ent.size() * sizeof(uint2), T->ent)) return rc;
     if (int rc = upload_raw(e.bp_mask.data(), e.bp_mask.size() * 8, T->qmask)) return rc;
     if (int rc = upload_raw(pm.data(), pm.size() * 4, T->qpm)) return rc;
     if (int rc = upload_raw(qbits.data(), qbits.size() * 4, T->qbits)) return rc;
+    // m <= 16 everywhere and a table within the 64 KB of dynamic LDS a block takes (two blocks per
+    // CU, C5: 1 000 patterns x 27 rows = 54 KB): verify reads its masks from LDS
+    const size_t n16 = ((size_t)np * rows + 1) & ~(size_t)1;
+    if (T->mq <= 16 && n16 * 2 <= (64u << 10) - 256 && !diag_env("FAC_QGRAM_NO_LDS")) {
+      std::vector<uint16_t> m16(n16, 0);
+      for (size_t i = 0; i < (size_t)np * rows; ++i) m16[i] = (uint16_t)e.bp_mask[i];
+      if (int rc = upload_raw(m16.data(), n16 * 2, T->m16)) return rc;
+      T->m16_words = (uint32_t)(n16 / 2);
+    }
   }
   out = T.get();
   e.pf_cache.push_back(std::move(T));
@@ -5517,7 +5569,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
   const PfTables* T = nullptr;
   if (int rc = pf_tables(e, ks, want_bytes, T, err)) return rc;
   const uint32_t nw = T->nw;
-  DevBuf d_ids, d_cover, d_runs, d_cnt;
+  PoolBuf d_ids, d_cover, d_runs, d_cnt;
   if (!T->bytes) {  // the text's symbol ids (prefilter.rs:253-260)
     HIP_TRY(d_ids.alloc(n + 80, stream));  // padded: the scan's 16-byte loads and next word, verify's 64-symbol passes
     if (view.ascii) {  // transcode, ASCII text (prefilter.rs:253-258): one byte per grapheme
@@ -5569,7 +5621,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     else hipLaunchKernelGGL((bitap_kernel<24, uint64_t>), bgrid, dim3(256), 0, stream, B);
   }
   HIP_TRY(hipGetLastError());
-  DevBuf d_qcand, d_qn;
+  PoolBuf d_qcand, d_qn;
   if (T->q) {
     HIP_TRY(d_qn.alloc(8, stream));
     QgramParams Q{};
@@ -5586,7 +5638,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     }
     Q.tab = static_cast<const uint2*>(T->tab);
     Q.tab_mask = T->ts - 1;
-    Q.ent = static_cast<const uint32_t*>(T->ent);
+    Q.ent = static_cast<const uint2*>(T->ent);
     Q.use3 = T->use3;
     Q.use4 = T->use4;
     Q.n_cand = static_cast<unsigned long long*>(d_qn.p);
@@ -5595,6 +5647,8 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     Q.rows = e.alphabet + 1;
     Q.cover = static_cast<uint32_t*>(d_cover.p);
     Q.bits = static_cast<const uint32_t*>(T->qbits);
+    Q.m16 = static_cast<const uint32_t*>(T->m16);
+    Q.m16_words = T->m16_words;
     int cus = 256;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
     const uint32_t sgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 8191) / 8192, (uint64_t)cus * 8));
@@ -5613,20 +5667,30 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
       qcap = nc;
     }
     if (nc) {
-      const dim3 vg((uint32_t)((nc + 255) / 256));
       const uint32_t kq = T->kq;
-      if (T->mq <= 32) {
-        if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-        else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-        else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-        else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-        else hipLaunchKernelGGL((qgram_verify_kernel<24, uint32_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+      if (T->m16) {  // LDS masks: persistent blocks, two per CU
+        const dim3 vg((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nc + 511) / 512, (uint64_t)cus * 2)));
+        const size_t lds = (size_t)T->m16_words * 4;
+        if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t, true>), vg, dim3(512), lds, stream, Q, (uint64_t)nc);
+        else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t, true>), vg, dim3(512), lds, stream, Q, (uint64_t)nc);
+        else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t, true>), vg, dim3(512), lds, stream, Q, (uint64_t)nc);
+        else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint32_t, true>), vg, dim3(512), lds, stream, Q, (uint64_t)nc);
+        else hipLaunchKernelGGL((qgram_verify_kernel<24, uint32_t, true>), vg, dim3(512), lds, stream, Q, (uint64_t)nc);
       } else {
-        if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint64_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-        else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint64_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-        else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint64_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-        else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint64_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-        else hipLaunchKernelGGL((qgram_verify_kernel<24, uint64_t>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+        const dim3 vg((uint32_t)((nc + 255) / 256));
+        if (T->mq <= 32) {
+          if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+          else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+          else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+          else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint32_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+          else hipLaunchKernelGGL((qgram_verify_kernel<24, uint32_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+        } else {
+          if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint64_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+          else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint64_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+          else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint64_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+          else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint64_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+          else hipLaunchKernelGGL((qgram_verify_kernel<24, uint64_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+        }
       }
       HIP_TRY(hipGetLastError());
     }
