@@ -61,6 +61,41 @@ struct RankCmp {  // "a before b" for Order::{Default, Greedy, CoverageWeighted}
   }
 };
 
+// The same order on the host (window_owned_device's small-window path): host f32 products are
+// rounded once each like __fmul_rn (-ffp-contract=off), and the order is total, so std::sort
+// gives the device sort's result
+inline uint32_t total_key_host(float f) {
+  uint32_t b;
+  std::memcpy(&b, &f, 4);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+struct RankCmpHost {
+  const uint32_t* plen;
+  int order;
+  bool operator()(const fac_match& a, const fac_match& b) const {
+    const uint32_t sa = total_key_host(a.similarity), sb = total_key_host(b.similarity);
+    const uint32_t la = plen[a.pattern_index], lb = plen[b.pattern_index];
+    if (order == 1) {
+      if (sa != sb) return sa > sb;
+      if (la != lb) return la > lb;
+      const uint64_t ta = a.end - a.start, tb = b.end - b.start;
+      if (ta != tb) return ta > tb;
+    } else if (order == 2) {
+      if (la != lb) return la > lb;
+      if (sa != sb) return sa > sb;
+    } else {
+      const volatile float a2 = a.similarity * a.similarity, b2 = b.similarity * b.similarity;
+      const volatile float ca = a2 * (float)la, cb = b2 * (float)lb;
+      const uint32_t ka = total_key_host(ca), kb = total_key_host(cb);
+      if (ka != kb) return ka > kb;
+      if (sa != sb) return sa > sb;
+    }
+    if (a.start != b.start) return a.start < b.start;
+    if (a.end != b.end) return a.end < b.end;
+    return a.pattern_index < b.pattern_index;
+  }
+};
+
 struct Span {
   uint64_t start, end;
   uint32_t rank;     // position in the ranked list
@@ -199,6 +234,7 @@ hipError_t dev_sort(T* in, T* out, uint64_t n, Cmp cmp, hipStream_t s) {
 }
 
 constexpr uint64_t kMaxCluster = 1u << 14;  // larger clusters: the host walk (O(n log n))
+constexpr uint64_t kHostRank = 1u << 14;    // window_owned_device: fewer records are ranked on the host
 
 // The reference's non_overlapping(_unique) walk (matches.rs:83-149) on the host.
 void walk_host(std::vector<fac_match>& v, const uint64_t* unique_ids, bool unique) {
@@ -385,6 +421,27 @@ int window_owned_device(const Engine& e, fac_match* d_a, fac_match* d_b, uint64_
                         uint64_t base, hipStream_t s, fac_match* d_out, uint64_t cap, uint64_t* n_owned, std::string& err) {
   *n_owned = 0;
   if (n == 0) return FAC_OK;
+  if (n <= kHostRank) {  // few records (C5: ~1 000 per 1 GiB window): ranked on the host, not by ~20 launches
+    std::vector<fac_match> v(n);
+    RK_TRY(hipMemcpyAsync(v.data(), d_a, n * sizeof(fac_match), hipMemcpyDeviceToHost, s));
+    RK_TRY(hipStreamSynchronize(s));
+    std::sort(v.begin(), v.end(), RankCmpHost{e.pat_bytes.data(), 1});
+    walk_host(v, nullptr, false);  // non_overlapping, start order
+    uint64_t owned = 0;
+    for (const fac_match& m0 : v) {
+      const uint64_t st = m0.start - byte_base;
+      if (st >= commit) continue;
+      fac_match m = m0;
+      m.start = st + base;
+      m.end = m.end - byte_base + base;
+      v[owned++] = m;
+    }
+    *n_owned = owned;
+    if (owned > cap) return FAC_E_OUTPUT_CAPACITY;
+    if (owned) RK_TRY(hipMemcpyAsync(d_out, v.data(), owned * sizeof(fac_match), hipMemcpyHostToDevice, s));
+    RK_TRY(hipStreamSynchronize(s));
+    return FAC_OK;
+  }
   fac_match* res = nullptr;
   uint64_t nres = 0;
   if (int rc = apply_matches_device(e, d_a, d_b, n, 1, 1, nullptr, s, &res, &nres, err)) return rc;
