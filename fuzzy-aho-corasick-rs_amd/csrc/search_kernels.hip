@@ -3591,7 +3591,12 @@ __device__ __forceinline__ uint32_t qgram_find(const QgramParams& Q, uint32_t ke
 
 // The screening bitmap's hash (64 Kbit, bit = the top 16 bits of a multiplicative hash: one multiply
 // per gram; the table probe behind it keeps qgram_hash). Built on the host, copied into LDS per block.
-__host__ __device__ inline uint32_t qgram_bit(uint32_t key) { return (key * 0x9E3779B1u) >> 16; }
+// (two full-rate 24-bit multiplies: a 32-bit v_mul_lo is quarter rate, and the scan hashes 32 grams per
+// thread-iteration; its VALU count bounds it)
+__host__ __device__ inline uint32_t qg_mul24(uint32_t a, uint32_t b) { return (a & 0xFFFFFFu) * (b & 0xFFFFFFu); }
+__host__ __device__ inline uint32_t qgram_bit(uint32_t key) {
+  return ((qg_mul24(key, 0x9E3779u) ^ qg_mul24(key >> 8, 0x85EBCAu)) >> 12) & 0xFFFFu;
+}
 constexpr uint32_t QG_BITS_WORDS = 2048;
 
 // Candidates collect in a per-wave LDS buffer and go out 512 at a time (one list atomic per flush: a
