@@ -3557,9 +3557,15 @@ struct QgramParams {
   uint32_t tab_mask;
   const uint2* ent;        // entries: {pattern << 8 | piece offset, m | k << 8} (one load per candidate)
   uint32_t use3, use4;     // gram lengths in use
-  unsigned long long* cand;  // candidates: text position << 24 | entry index
-  unsigned long long* n_cand;
-  uint64_t cap;
+  // candidates (text position << 24 | entry index): scan block b fills region b of cand (region
+  // entries, rcnt[b] of them valid), and what does not fit goes to the overflow list ovf
+  unsigned long long* cand;
+  uint64_t region;
+  uint32_t* rcnt;
+  uint32_t nreg;
+  unsigned long long* ovf;
+  unsigned long long* n_ovf;
+  uint64_t ovf_cap;
   const uint64_t* pmask;   // per pattern: [rows] symbol masks (bit j = the pattern's j-th symbol)
   const uint32_t* pm;      // per pattern: m | k << 8
   uint32_t rows;
@@ -3589,21 +3595,31 @@ __device__ __forceinline__ uint32_t qgram_find(const QgramParams& Q, uint32_t ke
   }
 }
 
-// The screening bitmap's hash (64 Kbit, bit = the top 16 bits of a multiplicative hash: one multiply
-// per gram; the table probe behind it keeps qgram_hash). Built on the host, copied into LDS per block.
-// (two full-rate 24-bit multiplies: a 32-bit v_mul_lo is quarter rate, and the scan hashes 32 grams per
-// thread-iteration; its VALU count bounds it)
+// The screening bitmap's hash (64 Kbit; the table probe behind it keeps qgram_hash). Built on the
+// host, copied into LDS per block. Bit = the top 17 bits of P = key[0:24) * A for a 3-gram, of
+// P + key[8:32) * B for a 4-gram: full-rate 24-bit multiplies (a 32-bit v_mul_lo is quarter rate, and
+// the scan's VALU count bounds it); a position's 3- and 4-gram share P (their first three symbols), so
+// the pair costs one multiply and one v_mad_u32_u24, and the scan reads the bit as byte hash >> 18,
+// bit (hash >> 15) & 7 with no masking. 3-gram keys carry 0xFF as their fourth symbol (qgram_key).
+// 128 Kbit: C5's 2 000 4-grams set 1.5 % of the bits (64 Kbit: 3 %), and every passing position
+// costs a queue round and a table probe.
 __host__ __device__ inline uint32_t qg_mul24(uint32_t a, uint32_t b) { return (a & 0xFFFFFFu) * (b & 0xFFFFFFu); }
+constexpr uint32_t QG_HA = 0x9E3779u, QG_HB = 0x85EBCAu;
+#ifndef FAC_QG_BITS_LOG
+#define FAC_QG_BITS_LOG 17
+#endif
+constexpr uint32_t QG_BITS_LOG = FAC_QG_BITS_LOG;  // log2 of the bitmap's bits
 __host__ __device__ inline uint32_t qgram_bit(uint32_t key) {
-  return ((qg_mul24(key, 0x9E3779u) ^ qg_mul24(key >> 8, 0x85EBCAu)) >> 12) & 0xFFFFu;
+  const uint32_t p = qg_mul24(key, QG_HA);
+  return ((key >> 24) == 0xFFu ? p : p + qg_mul24(key >> 8, QG_HB)) >> (32 - QG_BITS_LOG);
 }
-constexpr uint32_t QG_BITS_WORDS = 2048;
+constexpr uint32_t QG_BITS_WORDS = (1u << QG_BITS_LOG) / 32;
 
-// Candidates collect in a per-wave LDS buffer and go out 512 at a time (one list atomic per flush: a
-// same-address atomic per wave turn serialised the scan at one L2 channel, 175 ms per GiB)
-constexpr uint32_t QG_BUF = 256;
-// 8 waves per block share the screening bitmap: 8 KB + 3.5 KB per wave = 36 KB, 32 waves per CU (the
-// VGPR limit); 4-wave blocks with 512-entry buffers held 20
+// Candidates go to the block's own region of the list, reserved with an LDS counter: one global
+// list counter took a same-address atomic per flush of a per-wave buffer, and those atomics
+// serialised at one L2 channel (C5, 34 M candidates per GiB: 256-entry flushes 1.87 ms per GiB,
+// 128-entry 3.68, one atomic per wave turn 175 ms; profiles/r05z). 8 waves per block share the
+// screening bitmap: 16 KB + 1.5 KB per wave = 28 KB.
 constexpr uint32_t QG_WAVES = 8;
 // The bitmap screens every position first: only the ~3 % that pass (C5) probe the table in global
 // memory, 64 at a time from a per-wave LDS queue (one table round trip per 64 passing grams: probing
@@ -3626,25 +3642,20 @@ __device__ __forceinline__ uint32_t qg_fold(uint32_t w) {
   const uint32_t up = ((t - 0x41414141u) & ~(t - 0x5B5B5B5Bu)) & 0x80808080u;  // bytes in 'A'..'Z'
   return w + (up >> 2);
 }
+// U3 / U4: 3- / 4-grams in use (C5: 4-grams only, so the 3-grams' bitmap reads are not issued)
+template <bool U3, bool U4>
 __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q) {
-  __shared__ unsigned long long s_buf[QG_WAVES][QG_BUF];
   __shared__ uint32_t s_bits[QG_BITS_WORDS];
+  __shared__ uint32_t s_cnt, s_fail;  // region entries reserved; the first reservation that did not fit
   __shared__ uint32_t s_pk[QG_WAVES][QG_PQ];
   __shared__ uint64_t s_pp[QG_WAVES][QG_PQ];
   for (uint32_t x = threadIdx.x; x < QG_BITS_WORDS; x += blockDim.x) s_bits[x] = Q.bits[x];
+  if (threadIdx.x == 0) {
+    s_cnt = 0;
+    s_fail = (uint32_t)Q.region;
+  }
   __syncthreads();
-  unsigned long long* buf = s_buf[threadIdx.x / 64];
-  uint32_t nb = 0;  // wave-uniform
-  auto flush = [&]() {
-    unsigned long long b0 = 0;
-    if (lane_id() == 0) b0 = atomicAdd(Q.n_cand, (unsigned long long)nb);
-    b0 = shfl_u64(b0, 0);
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t x = lane_id(); x < nb; x += 64)
-      if (b0 + x < Q.cap) Q.cand[b0 + x] = buf[x];
-    __builtin_amdgcn_wave_barrier();
-    nb = 0;
-  };
+  unsigned long long* const reg = Q.cand + (uint64_t)blockIdx.x * Q.region;
   uint32_t* pk = s_pk[threadIdx.x / 64];
   uint64_t* pp = s_pp[threadIdx.x / 64];
   uint32_t nq = 0;  // wave-uniform
@@ -3663,48 +3674,39 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
       const uint32_t cnt = h & 0xFFu;
       if (!__ballot(cnt)) continue;
       const uint32_t incl = wave_inclusive_sum(cnt), tot = shfl_u32(incl, 63);
-      unsigned long long* dst;
-      uint64_t at;
-      if (tot > QG_BUF) {  // grams shared by many patterns: straight to the list
-        unsigned long long b0 = 0;
-        if (lane == 63) b0 = atomicAdd(Q.n_cand, (unsigned long long)tot);
-        dst = Q.cand;
-        at = shfl_u64(b0, 63) + (incl - cnt);
-      } else {
-        if (nb + tot > QG_BUF) flush();
-        dst = buf;
-        at = nb + incl - cnt;
-        nb += tot;
+      uint32_t r0 = 0;
+      if (lane == 63) r0 = atomicAdd(&s_cnt, tot);
+      r0 = shfl_u32(r0, 63);
+      unsigned long long* dst = reg;
+      uint64_t at = r0 + (incl - cnt), lim = Q.region;
+      if ((uint64_t)r0 + tot > Q.region) {  // region full: the overflow list
+        unsigned long long o0 = 0;
+        if (lane == 63) {
+          atomicMin(&s_fail, r0);
+          o0 = atomicAdd(Q.n_ovf, (unsigned long long)tot);
+        }
+        dst = Q.ovf;
+        at = shfl_u64(o0, 63) + (incl - cnt);
+        lim = Q.ovf_cap;
       }
       for (uint32_t y = 0; y < cnt; ++y, ++at)
-        if (dst != Q.cand || at < Q.cap) dst[at] = (pos << 24) | ((h >> 8) + y);
+        if (at < lim) dst[at] = (pos << 24) | ((h >> 8) + y);
     }
   };
-  // a thread takes 16 consecutive positions from one aligned 16-byte load plus the next word (the ids
-  // buffer is padded 32 bytes past n; positions whose gram would cross n are not looked up); the
-  // next turn's loads are issued before this turn's screening
+  // a thread takes 16 consecutive positions from one aligned 16-byte load plus the next word
+  // (positions whose gram would cross the text's end are not looked up)
   const uint4* ids16 = reinterpret_cast<const uint4*>(Q.ids);
+  const uint32_t* ids32 = reinterpret_cast<const uint32_t*>(Q.ids);
+  const uint8_t* s_bytes = reinterpret_cast<const uint8_t*>(s_bits);
   const uint64_t nbuf = Q.off + Q.n;  // buffer bytes of the text
   const uint64_t n16 = (nbuf + 15) / 16;  // buffer sixteens
+  // sixteens whose 20 bytes lie below nsafe: read with plain loads
+  const uint64_t gdir = min(n16, Q.nsafe >= 20 ? (Q.nsafe - 20) / 16 + 1 : (uint64_t)0);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t lane64 = threadIdx.x % 64;
   uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x - lane64;  // whole waves iterate together
-  auto load = [&](uint64_t g, uint4& a, uint32_t& x) {
-    if (16 * g + 20 <= Q.nsafe) {
-      a = ids16[g];
-      x = reinterpret_cast<const uint32_t*>(Q.ids)[4 * g + 4];
-    } else {  // the text's last sixteens: no read at or past nsafe
-      a = make_uint4(qg_word(Q, 16 * g), qg_word(Q, 16 * g + 4), qg_word(Q, 16 * g + 8), qg_word(Q, 16 * g + 12));
-      x = qg_word(Q, 16 * g + 16);
-    }
-  };
-  uint4 an = make_uint4(0u, 0u, 0u, 0u);
-  uint32_t xn = 0;
-  if (g0 + lane64 < n16) load(g0 + lane64, an, xn);
-  for (; g0 < n16; g0 += stride) {
-    const uint64_t g = g0 + lane64;
-    uint32_t w0 = an.x, w1 = an.y, w2 = an.z, w3 = an.w, w4 = xn;
-    if (g0 + stride + lane64 < n16) load(g0 + stride + lane64, an, xn);  // prefetch
+  auto turn = [&](uint64_t g, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4)
+                  __attribute__((always_inline)) {
     if (Q.bytes && Q.ci) {
       w0 = qg_fold(w0);
       w1 = qg_fold(w1);
@@ -3726,19 +3728,27 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
       return __builtin_amdgcn_alignbyte(hi, lo, j & 3u);
     };
     // pass mask: bit 2j = the 4-gram at buffer byte 16g + j (text position 16g + j - off), bit
-    // 2j + 1 = its 3-gram
+    // 2j + 1 = its 3-gram. Every bitmap read is unconditional (the text bounds are a mask applied
+    // after), so the LDS reads go out in batches: per-gram conditions had made each a branch with its
+    // own wait.
     uint32_t pm = 0;
     auto screen = [&](auto all_in) {  // all_in: every gram of the sixteen lies inside the text
 #pragma unroll
       for (uint32_t j = 0; j < 16; ++j) {
-        const uint64_t i = 16 * g + j;
-        const uint32_t k4 = gram4(j), k3 = (k4 & 0xFFFFFFu) | 0xFF000000u;
-        const uint32_t b4 = qgram_bit(k4), b3 = qgram_bit(k3);
-        const bool in = all_in || i >= Q.off;
-        const bool p4 = Q.use4 && in && (all_in || i + 4 <= nbuf) && ((s_bits[b4 >> 5] >> (b4 & 31u)) & 1u);
-        const bool p3 = Q.use3 && in && (all_in || i + 3 <= nbuf) && ((s_bits[b3 >> 5] >> (b3 & 31u)) & 1u);
-        pm |= (p4 ? 1u : 0u) << (2 * j);
-        pm |= (p3 ? 1u : 0u) << (2 * j + 1);
+        // qgram_bit of the 3-gram (h3) and the 4-gram (h4) at this position
+        const uint32_t k4 = gram4(j), h3 = qg_mul24(k4, QG_HA), h4 = h3 + qg_mul24(k4 >> 8, QG_HB);
+        constexpr uint32_t sh = 32 - QG_BITS_LOG;
+        if constexpr (U4) pm |= __builtin_amdgcn_ubfe(s_bytes[h4 >> (sh + 3)], (h4 >> sh) & 7u, 1u) << (2 * j);
+        if constexpr (U3) pm |= __builtin_amdgcn_ubfe(s_bytes[h3 >> (sh + 3)], (h3 >> sh) & 7u, 1u) << (2 * j + 1);
+      }
+      if (!all_in) {
+        uint32_t ok = 0;
+        for (uint32_t j = 0; j < 16; ++j) {
+          const uint64_t i = 16 * g + j;
+          if (i >= Q.off && i + 4 <= nbuf) ok |= 1u << (2 * j);
+          if (i >= Q.off && i + 3 <= nbuf) ok |= 1u << (2 * j + 1);
+        }
+        pm &= ok;
       }
     };
     if (g < n16) {
@@ -3762,18 +3772,41 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
       }
       nq += (uint32_t)__popcll(m);
     }
+  };
+  // Turns whose every sixteen reads directly: the next turn's loads are issued before this turn's
+  // screening, unconditionally (past the direct range they read sixteen 0 and are not used) -- under
+  // a branch, the load's join waited for it and the prefetch hid nothing. A full probe queue goes out
+  // before the prefetch (loads retire in order: a wait on the probe would wait for the prefetch too).
+  if (g0 + 64 <= gdir) {
+    uint4 an = ids16[g0 + lane64];
+    uint32_t xn = ids32[4 * (g0 + lane64) + 4];
+    for (; g0 + 64 <= gdir; g0 += stride) {
+      const uint32_t w0 = an.x, w1 = an.y, w2 = an.z, w3 = an.w, w4 = xn;
+      if (nq >= 64) drain(false);
+      const uint64_t gn = g0 + stride + lane64 < gdir ? g0 + stride + lane64 : 0;
+      an = ids16[gn];
+      xn = ids32[4 * gn + 4];
+      turn(g0 + lane64, w0, w1, w2, w3, w4);
+    }
+  }
+  // the text's last sixteens (no read at or past nsafe)
+  for (; g0 < n16; g0 += stride) {
+    const uint64_t g = g0 + lane64;
     if (nq >= 64) drain(false);
+    turn(g, qg_word(Q, 16 * g), qg_word(Q, 16 * g + 4), qg_word(Q, 16 * g + 8), qg_word(Q, 16 * g + 12),
+         qg_word(Q, 16 * g + 16));
   }
   drain(true);
-  if (nb) flush();
+  __syncthreads();
+  if (threadIdx.x == 0) Q.rcnt[blockIdx.x] = min(s_cnt, s_fail);
 }
 
 // W: the automaton word, uint32_t when every q-gram pattern has m <= 32 (half the 64-bit VALU work)
 // One candidate (qgram_verify_kernel). LM: every q-gram pattern has m <= 16 and their masks fit in
 // LDS (16-bit, pattern-major): the mask reads are LDS reads instead of L2 round trips.
 template <int KMAX, typename W, bool LM>
-__device__ __forceinline__ void verify_one(const QgramParams& Q, uint64_t x, const uint8_t* s_aid, const uint16_t* s_m16) {
-  const unsigned long long cd = Q.cand[x];
+__device__ __forceinline__ void verify_one(const QgramParams& Q, unsigned long long cd, const uint8_t* s_aid,
+                                           const uint16_t* s_m16) {
   const uint64_t t = cd >> 24;
   const uint2 en = Q.ent[cd & 0xFFFFFFu];
   const uint32_t p = en.x >> 8, o = en.x & 0xFFu, m = en.y & 0xFFu, k = en.y >> 8;
@@ -3858,7 +3891,7 @@ __device__ __forceinline__ void verify_one(const QgramParams& Q, uint64_t x, con
 }
 
 template <int KMAX, typename W, bool LM>
-__global__ __launch_bounds__(LM ? 512 : 256) void qgram_verify_kernel(QgramParams Q, uint64_t n_cand) {
+__global__ __launch_bounds__(LM ? 512 : 256) void qgram_verify_kernel(QgramParams Q) {
   __shared__ uint8_t s_aid[128];  // bytes mode: byte -> symbol id
   extern __shared__ uint16_t s_m16[];  // LM: Q.m16_words 32-bit words of 16-bit masks
   if (Q.bytes)
@@ -3866,12 +3899,11 @@ __global__ __launch_bounds__(LM ? 512 : 256) void qgram_verify_kernel(QgramParam
   if constexpr (LM)
     for (uint32_t i = threadIdx.x; i < Q.m16_words; i += blockDim.x) reinterpret_cast<uint32_t*>(s_m16)[i] = Q.m16[i];
   __syncthreads();
-  if constexpr (LM) {  // persistent: the table is loaded once per block
-    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n_cand; x += (uint64_t)gridDim.x * blockDim.x)
-      verify_one<KMAX, W, LM>(Q, x, s_aid, s_m16);
-  } else {
-    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x < n_cand) verify_one<KMAX, W, LM>(Q, x, s_aid, s_m16);
+  // persistent: block b takes the scan's regions b, b + grid, ..., then (region nreg) the overflow list
+  for (uint32_t r = blockIdx.x; r <= Q.nreg; r += gridDim.x) {
+    const unsigned long long* base = r < Q.nreg ? Q.cand + (uint64_t)r * Q.region : Q.ovf;
+    const uint64_t cnt = r < Q.nreg ? (uint64_t)Q.rcnt[r] : min((uint64_t)*Q.n_ovf, Q.ovf_cap);
+    for (uint64_t x = threadIdx.x; x < cnt; x += blockDim.x) verify_one<KMAX, W, LM>(Q, base[x], s_aid, s_m16);
   }
 }
 
@@ -5626,7 +5658,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     else hipLaunchKernelGGL((bitap_kernel<24, uint64_t>), bgrid, dim3(256), 0, stream, B);
   }
   HIP_TRY(hipGetLastError());
-  PoolBuf d_qcand, d_qn;
+  PoolBuf d_qcand, d_qn, d_qovf, d_qrcnt;
   if (T->q) {
     HIP_TRY(d_qn.alloc(8, stream));
     QgramParams Q{};
@@ -5646,7 +5678,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     Q.ent = static_cast<const uint2*>(T->ent);
     Q.use3 = T->use3;
     Q.use4 = T->use4;
-    Q.n_cand = static_cast<unsigned long long*>(d_qn.p);
+    Q.n_ovf = static_cast<unsigned long long*>(d_qn.p);
     Q.pmask = static_cast<const uint64_t*>(T->qmask);
     Q.pm = static_cast<const uint32_t*>(T->qpm);
     Q.rows = e.alphabet + 1;
@@ -5657,44 +5689,63 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     int cus = 256;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
     const uint32_t sgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 8191) / 8192, (uint64_t)cus * 8));
-    uint64_t qcap = std::max<uint64_t>(1 << 20, n / 16);
-    unsigned long long nc = 0;
-    for (;;) {  // candidates: one scan, again with room for all of them if the list overflowed
-      HIP_TRY(d_qcand.alloc(qcap * 8, stream));
-      Q.cand = static_cast<unsigned long long*>(d_qcand.p);
-      Q.cap = qcap;
+    // regions of 1/16 of a block's positions (C5 fills ~half); the overflow list is checked after
+    Q.nreg = sgrid;
+    Q.region = std::max<uint64_t>(256, (n / sgrid + 15) / 16);
+    HIP_TRY(d_qcand.alloc(Q.region * sgrid * 8, stream));
+    HIP_TRY(d_qrcnt.alloc((size_t)sgrid * 4, stream));
+    Q.cand = static_cast<unsigned long long*>(d_qcand.p);
+    Q.rcnt = static_cast<uint32_t*>(d_qrcnt.p);
+    uint64_t ocap = 1 << 20;
+    unsigned long long nc = 0;  // overflow entries
+    for (;;) {  // candidates: one scan, again with room for all of them if the overflow list overflowed
+      HIP_TRY(d_qovf.alloc(ocap * 8, stream));
+      Q.ovf = static_cast<unsigned long long*>(d_qovf.p);
+      Q.ovf_cap = ocap;
       HIP_TRY(hipMemsetAsync(d_qn.p, 0, 8, stream));
-      hipLaunchKernelGGL(qgram_scan_kernel, dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q);
+      if (Q.use3 && Q.use4) hipLaunchKernelGGL((qgram_scan_kernel<true, true>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q);
+      else if (Q.use4) hipLaunchKernelGGL((qgram_scan_kernel<false, true>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q);
+      else hipLaunchKernelGGL((qgram_scan_kernel<true, false>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipMemcpyAsync(&nc, d_qn.p, 8, hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
-      if (nc <= qcap) break;
-      qcap = nc;
+      if (nc <= ocap) break;
+      ocap = nc;
     }
-    if (nc) {
+    if (diag_env("FAC_TIMING")) {
+      std::vector<uint32_t> rc(sgrid);
+      HIP_TRY(hipMemcpyAsync(rc.data(), d_qrcnt.p, (size_t)sgrid * 4, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      uint64_t tot = nc, mx = 0;
+      for (uint32_t c : rc) tot += c, mx = std::max<uint64_t>(mx, c);
+      std::fprintf(stderr, "FAC_QGRAM text %llu symbols, %llu candidates (%llu overflow, region %llu, fullest %llu), use3 %u use4 %u\n",
+                   (unsigned long long)n, (unsigned long long)tot, nc, (unsigned long long)Q.region,
+                   (unsigned long long)mx, Q.use3, Q.use4);
+    }
+    {
       const uint32_t kq = T->kq;
       if (T->m16) {  // LDS masks: persistent blocks, two per CU
-        const dim3 vg((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nc + 511) / 512, (uint64_t)cus * 2)));
+        const dim3 vg((uint32_t)std::min<uint64_t>(sgrid + 1, (uint64_t)cus * 2));
         const size_t lds = (size_t)T->m16_words * 4;
-        if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t, true>), vg, dim3(512), lds, stream, Q, (uint64_t)nc);
-        else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t, true>), vg, dim3(512), lds, stream, Q, (uint64_t)nc);
-        else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t, true>), vg, dim3(512), lds, stream, Q, (uint64_t)nc);
-        else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint32_t, true>), vg, dim3(512), lds, stream, Q, (uint64_t)nc);
-        else hipLaunchKernelGGL((qgram_verify_kernel<24, uint32_t, true>), vg, dim3(512), lds, stream, Q, (uint64_t)nc);
+        if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t, true>), vg, dim3(512), lds, stream, Q);
+        else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t, true>), vg, dim3(512), lds, stream, Q);
+        else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t, true>), vg, dim3(512), lds, stream, Q);
+        else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint32_t, true>), vg, dim3(512), lds, stream, Q);
+        else hipLaunchKernelGGL((qgram_verify_kernel<24, uint32_t, true>), vg, dim3(512), lds, stream, Q);
       } else {
-        const dim3 vg((uint32_t)((nc + 255) / 256));
+        const dim3 vg((uint32_t)std::min<uint64_t>(sgrid + 1, (uint64_t)cus * 8));
         if (T->mq <= 32) {
-          if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-          else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-          else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-          else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint32_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-          else hipLaunchKernelGGL((qgram_verify_kernel<24, uint32_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+          if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t, false>), vg, dim3(256), 0, stream, Q);
+          else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t, false>), vg, dim3(256), 0, stream, Q);
+          else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t, false>), vg, dim3(256), 0, stream, Q);
+          else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint32_t, false>), vg, dim3(256), 0, stream, Q);
+          else hipLaunchKernelGGL((qgram_verify_kernel<24, uint32_t, false>), vg, dim3(256), 0, stream, Q);
         } else {
-          if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint64_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-          else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint64_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-          else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint64_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-          else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint64_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
-          else hipLaunchKernelGGL((qgram_verify_kernel<24, uint64_t, false>), vg, dim3(256), 0, stream, Q, (uint64_t)nc);
+          if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint64_t, false>), vg, dim3(256), 0, stream, Q);
+          else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint64_t, false>), vg, dim3(256), 0, stream, Q);
+          else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint64_t, false>), vg, dim3(256), 0, stream, Q);
+          else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint64_t, false>), vg, dim3(256), 0, stream, Q);
+          else hipLaunchKernelGGL((qgram_verify_kernel<24, uint64_t, false>), vg, dim3(256), 0, stream, Q);
         }
       }
       HIP_TRY(hipGetLastError());

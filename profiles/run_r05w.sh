@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 5: q-gram scan with unconditional prefetch, branch-free screening and the shared-product hash:
+# pre-filter tests, C5 line and the scan kernel time
+set -eo pipefail
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/r05w
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+L=$ROOT/fuzzy-aho-corasick-rs_amd/fuzzy_aho_corasick/_lib
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "prefilter or qgram or bitap or stream or c5 or bytes or distributed or prefiltered" > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
+tail -1 "$OUT/pytest.log"
+for v in qs8; do
+  lib=$L/libfac_$v.so; [ $v = qs8 ] && lib=$L/libfac.so
+  FAC_LIB=$lib timeout -k 10 300 python bench.py --config c5 --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/c5_$v.json" 2> "$OUT/c5_$v.err"
+  python3 -c "import json;d=json.load(open('$OUT/c5_$v.json'));g=d['diagnostics'];print('$v', round(d['value'],1), round(d['ms_per_step'],2), 'prefilter', round(g['prefilter_ms_per_step'],2), g['matches_per_step'])"
+done
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o c5 \
+  -- python3 "$ROOT/bench.py" --config c5 --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/kt.log" 2>&1)
+f=$(find "$OUT/kt" -name '*kernel_stats.csv' | head -1); python3 - "$f" <<'PY'
+import csv,sys
+for r in list(csv.DictReader(open(sys.argv[1])))[:3]:
+    print(r['Name'][:60], r['Calls'], round(float(r['AverageNs'])/1e6,3))
+PY
