@@ -3805,10 +3805,9 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
 // One candidate (qgram_verify_kernel). LM: every q-gram pattern has m <= 16 and their masks fit in
 // LDS (16-bit, pattern-major): the mask reads are LDS reads instead of L2 round trips.
 template <int KMAX, typename W, bool LM>
-__device__ __forceinline__ void verify_one(const QgramParams& Q, unsigned long long cd, const uint8_t* s_aid,
+__device__ __forceinline__ void verify_one(const QgramParams& Q, unsigned long long cd, uint2 en, const uint8_t* s_aid,
                                            const uint16_t* s_m16) {
   const uint64_t t = cd >> 24;
-  const uint2 en = Q.ent[cd & 0xFFFFFFu];
   const uint32_t p = en.x >> 8, o = en.x & 0xFFu, m = en.y & 0xFFu, k = en.y >> 8;
   // ends the candidate allows, 1-based: [t + m - o - k, t + m - o + k], clipped to the text
   const int64_t lo = (int64_t)t + m - o - k, hi = (int64_t)t + m - o + k;
@@ -3829,6 +3828,9 @@ __device__ __forceinline__ void verify_one(const QgramParams& Q, unsigned long l
   // (text positions; buffer byte = position + off, both 4-aligned when base is: off % 4 folded in)
   const uint32_t* mask32 = reinterpret_cast<const uint32_t*>(mask);
   const uint32_t sh = Q.off & 3u;
+  // per pass, 32-bit bounds relative to the pass's first buffer word (u = 16c + v indexes its
+  // symbols): symbols u in [u_lo, u_hi) are stepped, ends at u >= u_end report (a pass spans 64
+  // symbols, so every bound fits; 64-bit compares per symbol cost as much as the recurrence)
   for (uint64_t base = (s0 + sh) & ~3ull; base < e_max + sh; base += 64) {  // buffer bytes - (off - sh)
     uint32_t wd[16];
     const uint64_t nw = min<uint64_t>(16, (e_max + sh - base + 3) / 4);
@@ -3840,24 +3842,28 @@ __device__ __forceinline__ void verify_one(const QgramParams& Q, unsigned long l
     } else {  // the text's end: no read at or past nsafe
       for (uint32_t u = 0; u < 16; ++u) wd[u] = u < nw ? qg_word(Q, bb + 4 * u) : 0u;
     }
+    const int32_t u_lo = (int32_t)min<int64_t>((int64_t)(s0 + sh) - (int64_t)base, 64);
+    const int32_t u_hi = (int32_t)min<uint64_t>(e_max + sh - base, 64);
+    // end (1-based text position) of symbol u: base + u - sh + 1 >= e_min
+    const int32_t u_end = (int32_t)max<int64_t>(-1, min<int64_t>((int64_t)(e_min + sh) - (int64_t)base - 1, 64));
 #pragma unroll
     for (uint32_t c = 0; c < 4; ++c) {
-      if (base + 16 * c >= e_max + sh) break;
+      if ((int32_t)(16 * c) >= u_hi) break;
       W bcs[16];
 #pragma unroll
       for (uint32_t v = 0; v < 16; ++v) {
-        const uint64_t i = base + 16 * c + v - sh;  // text position (may wrap below 0: skipped)
+        const int32_t u = (int32_t)(16 * c + v);
         uint32_t sym = (wd[4 * c + v / 4] >> (8 * (v % 4))) & 0xFFu;
         if (Q.bytes) sym = s_aid[sym & 0x7Fu];
-        if (base + 16 * c + v >= s0 + sh && i < e_max)
+        if (u >= u_lo && u < u_hi)
           bcs[v] = LM ? (W)mask16[sym] : sizeof(W) == 4 ? (W)mask32[2 * sym] : (W)mask[sym];
         else bcs[v] = (W)0;
       }
 #pragma unroll
       for (uint32_t v = 0; v < 16; ++v) {
-        const uint64_t i = base + 16 * c + v - sh;
-        if (base + 16 * c + v >= e_max + sh) break;
-        if (base + 16 * c + v < s0 + sh) continue;
+        const int32_t u = (int32_t)(16 * c + v);
+        if (u >= u_hi) break;
+        if (u < u_lo) continue;
         const W bc = bcs[v];
         W prev_old = r[0];
         W prev_new = ((r[0] << 1) | (W)1) & bc;
@@ -3872,8 +3878,8 @@ __device__ __forceinline__ void verify_one(const QgramParams& Q, unsigned long l
           prev_new = nv;
           if ((uint32_t)d == k) hit = nv;
         }
-        const uint64_t end = i + 1;
-        if (end >= e_min && (hit & top)) {  // coverage [end - m - k, end), as bitap_kernel
+        if (u >= u_end && (hit & top)) {  // coverage [end - m - k, end), as bitap_kernel
+          const uint64_t end = base + (uint64_t)u - sh + 1;
           const uint64_t span = (uint64_t)m + k;
           const uint64_t ws = end > span ? end - span : 0;
           for (uint64_t y = ws; y < end;) {
@@ -3899,11 +3905,16 @@ __global__ __launch_bounds__(LM ? 512 : 256) void qgram_verify_kernel(QgramParam
   if constexpr (LM)
     for (uint32_t i = threadIdx.x; i < Q.m16_words; i += blockDim.x) reinterpret_cast<uint32_t*>(s_m16)[i] = Q.m16[i];
   __syncthreads();
-  // persistent: block b takes the scan's regions b, b + grid, ..., then (region nreg) the overflow list
+  // persistent: block b takes the scan's regions b, b + grid, ..., then (region nreg) the overflow list.
+  // (Loading two candidates and their entries per thread before verifying either measured no faster:
+  // 1.37 ms per GiB held to 128 VGPRs, 1.96 at 133 VGPRs, against 1.36; profiles/r05_scan.)
   for (uint32_t r = blockIdx.x; r <= Q.nreg; r += gridDim.x) {
     const unsigned long long* base = r < Q.nreg ? Q.cand + (uint64_t)r * Q.region : Q.ovf;
     const uint64_t cnt = r < Q.nreg ? (uint64_t)Q.rcnt[r] : min((uint64_t)*Q.n_ovf, Q.ovf_cap);
-    for (uint64_t x = threadIdx.x; x < cnt; x += blockDim.x) verify_one<KMAX, W, LM>(Q, base[x], s_aid, s_m16);
+    for (uint64_t x = threadIdx.x; x < cnt; x += blockDim.x) {
+      const unsigned long long cd = base[x];
+      verify_one<KMAX, W, LM>(Q, cd, Q.ent[cd & 0xFFFFFFu], s_aid, s_m16);
+    }
   }
 }
 
