@@ -3596,17 +3596,17 @@ __device__ __forceinline__ uint32_t qgram_find(const QgramParams& Q, uint32_t ke
 }
 
 // The screening bitmap's hash (64 Kbit; the table probe behind it keeps qgram_hash). Built on the
-// host, copied into LDS per block. Bit = the top 17 bits of P = key[0:24) * A for a 3-gram, of
+// host, copied into LDS per block. Bit = the top 18 bits of P = key[0:24) * A for a 3-gram, of
 // P + key[8:32) * B for a 4-gram: full-rate 24-bit multiplies (a 32-bit v_mul_lo is quarter rate, and
 // the scan's VALU count bounds it); a position's 3- and 4-gram share P (their first three symbols), so
-// the pair costs one multiply and one v_mad_u32_u24, and the scan reads the bit as byte hash >> 18,
-// bit (hash >> 15) & 7 with no masking. 3-gram keys carry 0xFF as their fourth symbol (qgram_key).
-// 128 Kbit: C5's 2 000 4-grams set 1.5 % of the bits (64 Kbit: 3 %), and every passing position
-// costs a queue round and a table probe.
+// the pair costs one multiply and one v_mad_u32_u24, and the scan reads the bit as byte hash >> 17,
+// bit (hash >> 14) & 7 with no masking. 3-gram keys carry 0xFF as their fourth symbol (qgram_key).
+// 256 Kbit: every false pass costs a queue round and a table probe (C5 scan per GiB, profiles/r05_scan:
+// 64 / 128 / 256 Kbit 1.49 / 1.14 / 1.11 ms).
 __host__ __device__ inline uint32_t qg_mul24(uint32_t a, uint32_t b) { return (a & 0xFFFFFFu) * (b & 0xFFFFFFu); }
 constexpr uint32_t QG_HA = 0x9E3779u, QG_HB = 0x85EBCAu;
 #ifndef FAC_QG_BITS_LOG
-#define FAC_QG_BITS_LOG 17
+#define FAC_QG_BITS_LOG 18
 #endif
 constexpr uint32_t QG_BITS_LOG = FAC_QG_BITS_LOG;  // log2 of the bitmap's bits
 __host__ __device__ inline uint32_t qgram_bit(uint32_t key) {
@@ -3618,8 +3618,8 @@ constexpr uint32_t QG_BITS_WORDS = (1u << QG_BITS_LOG) / 32;
 // Candidates go to the block's own region of the list, reserved with an LDS counter: one global
 // list counter took a same-address atomic per flush of a per-wave buffer, and those atomics
 // serialised at one L2 channel (C5, 34 M candidates per GiB: 256-entry flushes 1.87 ms per GiB,
-// 128-entry 3.68, one atomic per wave turn 175 ms; profiles/r05z). 8 waves per block share the
-// screening bitmap: 16 KB + 1.5 KB per wave = 28 KB.
+// 128-entry 3.68, one atomic per wave turn 175 ms; per-block regions 1.14; profiles/r05_scan). 8 waves
+// per block share the screening bitmap: 32 KB + 1.5 KB per wave = 44 KB, 3 blocks per CU.
 constexpr uint32_t QG_WAVES = 8;
 // The bitmap screens every position first: only the ~3 % that pass (C5) probe the table in global
 // memory, 64 at a time from a per-wave LDS queue (one table round trip per 64 passing grams: probing
