@@ -280,6 +280,34 @@ def test_qgram_bytes_mode_matches_ids_and_full_scan(ci, monkeypatch):
     assert rows(gpu.with_prefilter().search(hay, O().threshold(0.8))) == rows(gpu.search(hay, O().threshold(0.8)))
 
 
+def test_qgram_candidate_regions_overflow(monkeypatch):
+    """Candidates beyond a scan block's region of the list (1/16 of its positions) go to the overflow
+    list, and an overflowing overflow list is regrown and the scan re-run: runs of 'a' (3-18) between
+    other letters, against patterns whose pieces start with "aaa" / "aaaa", make ~36 candidates per
+    run position (~1.5 M in all, past the first 1 Mi-entry overflow list: every block's first
+    reservation overflows); with "a" * 16 alone (4 entries per gram: 256 per queue drain) the regions
+    fill part way before overflowing.
+    Windows == the packed full scan == the oracle."""
+    from fuzzy_aho_corasick.engine import prefilter_windows
+    rng = Rng(0x0F10_0D)
+    pats = ["a" * L for L in range(10, 17)] + ["a" * L + "b" + "a" * (13 - L) for L in range(5, 10)]
+    parts, n = [], 0
+    while n < 800_000:
+        s = "".join("bcdefghij"[rng.next() % 9] for _ in range(10 + rng.next() % 50)) + "a" * (3 + rng.next() % 16)
+        parts.append(s)
+        n += len(s)
+    hay = "".join(parts)
+    b = B().fuzzy(L().edits(2))
+    for sub in (pats, pats[6:7]):
+        gpu = b.build(sub)
+        orc = OracleEngine(b, sub)
+        got = prefilter_windows(gpu, hay, 0.8)
+        monkeypatch.setenv("FAC_NO_QGRAM", "1")
+        full = prefilter_windows(gpu, hay, 0.8)
+        monkeypatch.delenv("FAC_NO_QGRAM")
+        assert got and got == full == orc.prefilter_windows(hay, 0.8)
+
+
 def test_edge_inputs():
     b = B().fuzzy(L().edits(2))
     compare(b, ["abc"], "", 0.0)                      # empty haystack
