@@ -5699,7 +5699,17 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     Q.m16_words = T->m16_words;
     int cus = 256;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
-    const uint32_t sgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 8191) / 8192, (uint64_t)cus * 8));
+    // two full resident rounds of scan blocks (3 per CU at 44 KB of LDS): the scan strides over the
+    // text, so every block does the same work, and a grid of 8 per CU ran 2.7 rounds (the last one 2/3
+    // full); one round left the verify's 2 persistent blocks per CU 1.5 regions each (1.21 vs 1.15 ms)
+    const void* scan_fn = Q.use3 && Q.use4 ? reinterpret_cast<const void*>(&qgram_scan_kernel<true, true>)
+                          : Q.use4         ? reinterpret_cast<const void*>(&qgram_scan_kernel<false, true>)
+                                           : reinterpret_cast<const void*>(&qgram_scan_kernel<true, false>);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scan_fn, 64 * QG_WAVES, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    const uint32_t sgrid =
+        (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 8191) / 8192, (uint64_t)cus * (uint64_t)per_cu * 2));
     // regions of 1/16 of a block's positions (C5 fills ~half); the overflow list is checked after
     Q.nreg = sgrid;
     Q.region = std::max<uint64_t>(256, (n / sgrid + 15) / 16);
