@@ -3618,9 +3618,13 @@ constexpr uint32_t QG_BITS_WORDS = (1u << QG_BITS_LOG) / 32;
 // Candidates go to the block's own region of the list, reserved with an LDS counter: one global
 // list counter took a same-address atomic per flush of a per-wave buffer, and those atomics
 // serialised at one L2 channel (C5, 34 M candidates per GiB: 256-entry flushes 1.87 ms per GiB,
-// 128-entry 3.68, one atomic per wave turn 175 ms; per-block regions 1.14; profiles/r05_scan). 8 waves
-// per block share the screening bitmap: 32 KB + 1.5 KB per wave = 44 KB, 3 blocks per CU.
-constexpr uint32_t QG_WAVES = 8;
+// 128-entry 3.68, one atomic per wave turn 175 ms; per-block regions 1.14; profiles/r05_scan). 16 waves
+// per block share the screening bitmap: 32 KB + 1.5 KB per wave = 56 KB, 2 blocks = 32 waves per CU
+// (8-wave blocks: 44 KB, 3 blocks = 24 waves, 1.09 against 1.00 ms per GiB).
+#ifndef FAC_QG_WAVES
+#define FAC_QG_WAVES 16
+#endif
+constexpr uint32_t QG_WAVES = FAC_QG_WAVES;
 // The bitmap screens every position first: only the ~3 % that pass (C5) probe the table in global
 // memory, 64 at a time from a per-wave LDS queue (one table round trip per 64 passing grams: probing
 // where they stood cost a round trip per wave step, since some lane of 64 passes almost every one).
@@ -5699,7 +5703,7 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     Q.m16_words = T->m16_words;
     int cus = 256;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
-    // two full resident rounds of scan blocks (3 per CU at 44 KB of LDS): the scan strides over the
+    // two full resident rounds of scan blocks (2 per CU at 56 KB of LDS): the scan strides over the
     // text, so every block does the same work, and a grid of 8 per CU ran 2.7 rounds (the last one 2/3
     // full); one round left the verify's 2 persistent blocks per CU 1.5 regions each (1.21 vs 1.15 ms)
     const void* scan_fn = Q.use3 && Q.use4 ? reinterpret_cast<const void*>(&qgram_scan_kernel<true, true>)
