@@ -292,7 +292,10 @@ void fac_engine_free(fac_engine* engine) {
   if (!engine) return;
   fac::free_engine_device(engine->e);
   delete engine;
+  fac::call_scratch_trim();  // the kept call scratch is invisible to callers' allocators
 }
+
+void fac_trim_scratch(void) { fac::call_scratch_trim(); }
 
 uint64_t fac_engine_num_nodes(const fac_engine* engine) { return engine ? engine->e.nodes.size() : 0; }
 uint32_t fac_engine_max_edits_fast(const fac_engine* engine) { return engine ? engine->e.max_edits_fast : 0; }

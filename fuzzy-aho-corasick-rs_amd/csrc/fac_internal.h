@@ -255,7 +255,8 @@ struct SearchParams {
   int32_t rc_mode;                  // 0 off, 1 use the cache, 2 build it (win_list = representatives)
   uint32_t rc_k;                    // key chars of the level being collected / built (2..8)
   uint32_t rc_ntab;                 // tables a lookup consults (0..kRcLevels), deepest first
-  uint32_t rc_kstart;               // rc_lookup's first probe: the shallowest level with k >= this (0: deepest)
+  uint32_t rc_kstart;               // rc_lookup's first probe: the shallowest level with k >= this (0: the
+                                    // shallowest level; a k no level has, 0xFFFFFFFF: the deepest level)
   uint4* rc_bhits;                  // cache build: each key's parent snapshot (rc_parent_kernel), as rc_hits
   uint32_t* rc_bpops;               // ... and its pops
   RcTable rc_tab[kRcLevels];
@@ -492,12 +493,15 @@ struct ScratchSet {
 };
 void scratch_bind(ScratchSet* s);  // this thread's searches use `s` (nullptr: the engine's)
 void scratch_free(ScratchSet& s);
-// Short-lived call scratch (rank kernels, stream-window record buffers), reused per host thread: a
-// block given back on stream s is handed out again only for work on s, whose order makes the reuse
-// safe without the device-wide synchronisation a hipFree implies (a per-call hipMalloc/hipFree
-// stalled every other stream once per stream window). Grow-only per size class; freed at thread exit.
+// Short-lived call scratch (rank kernels, stream-window record buffers), one process-wide pool: a
+// block given back on stream s is handed out again only for work on s (same device), whose order
+// makes the reuse safe without the device-wide synchronisation a hipFree implies (a per-call
+// hipMalloc/hipFree stalled every other stream once per stream window). At most 2 GiB / 64 blocks
+// are kept (oldest freed first); fac_trim_scratch / fac_engine_free release them.
 void* call_scratch_take(size_t bytes, hipStream_t s, hipError_t* e);
 void call_scratch_give(void* p, hipStream_t s);
+void call_scratch_trim();                         // frees every kept block
+void call_scratch_release_stream(hipStream_t s);  // before the library destroys stream s
 
 // stream.cpp: the WindowReader state (stream.rs:77-159), the windows in flight and the matches
 // ready to hand out. Windows are cut on the host and searched by `depth` worker threads, each with

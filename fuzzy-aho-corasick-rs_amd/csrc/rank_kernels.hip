@@ -19,6 +19,7 @@
 
 #include <rocprim/device/device_merge_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <mutex>
 #include <set>
 #include <unordered_set>
 #include <vector>
@@ -467,57 +468,108 @@ int window_owned_device(const Engine& e, fac_match* d_a, fac_match* d_b, uint64_
 }
 
 namespace {
+// One pool per process (not per thread: a stream's blocks must be found again by whoever destroys
+// the stream), keyed by (device, stream, size class). Size classes are powers of two up to 64 MiB
+// and 16 MiB multiples above, so a 0.5 GB block is not rounded to 1 GiB. Given-back blocks are kept
+// up to kPoolCap bytes in all (the oldest go first); call_scratch_release_stream frees a stream's
+// blocks before the library destroys that stream (a new stream may get the same handle), and
+// fac_trim_scratch frees every kept block.
 struct CallBlock {
   void* p;
   size_t bytes;
   hipStream_t s;
+  int device;
 };
+constexpr size_t kPoolCap = size_t(2) << 30;
 struct CallPool {
-  std::vector<CallBlock> free_blocks;
-  ~CallPool() {
-    for (const CallBlock& b : free_blocks) (void)hipFree(b.p);
+  std::mutex mu;
+  std::vector<CallBlock> free_blocks;  // oldest first
+  std::vector<CallBlock> live;         // handed out: their sizes for the give-back
+  size_t free_bytes = 0;
+  void drop_front_locked() {
+    (void)hipFree(free_blocks.front().p);  // hipFree orders after the block's stream work
+    free_bytes -= free_blocks.front().bytes;
+    free_blocks.erase(free_blocks.begin());
   }
 };
-thread_local CallPool t_call_pool;
-thread_local std::vector<CallBlock> t_call_live;  // handed out: their sizes for the give-back
+CallPool& call_pool() {
+  static CallPool* p = new CallPool();  // never destroyed: blocks outlive static destructors' order
+  return *p;
+}
+size_t size_class(size_t bytes) {
+  if (bytes > (size_t(64) << 20)) return (bytes + (size_t(16) << 20) - 1) & ~((size_t(16) << 20) - 1);
+  size_t cls = 256;
+  while (cls < bytes) cls <<= 1;
+  return cls;
+}
 }  // namespace
 
 void* call_scratch_take(size_t bytes, hipStream_t s, hipError_t* e) {
-  size_t cls = 256;
-  while (cls < bytes) cls <<= 1;
-  auto& fb = t_call_pool.free_blocks;
-  for (size_t i = 0; i < fb.size(); ++i)
-    if (fb[i].s == s && fb[i].bytes == cls) {
-      const CallBlock b = fb[i];
-      fb[i] = fb.back();
-      fb.pop_back();
-      t_call_live.push_back(b);
-      *e = hipSuccess;
-      return b.p;
-    }
+  const size_t cls = size_class(bytes);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  CallPool& pool = call_pool();
+  {
+    std::lock_guard<std::mutex> lk(pool.mu);
+    auto& fb = pool.free_blocks;
+    for (size_t i = fb.size(); i-- > 0;)  // newest first: likeliest to be warm
+      if (fb[i].s == s && fb[i].bytes == cls && fb[i].device == dev) {
+        const CallBlock b = fb[i];
+        fb.erase(fb.begin() + (ptrdiff_t)i);
+        pool.free_bytes -= b.bytes;
+        pool.live.push_back(b);
+        *e = hipSuccess;
+        return b.p;
+      }
+  }
   void* p = nullptr;
   *e = hipMalloc(&p, cls);
-  if (*e != hipSuccess) return nullptr;
-  t_call_live.push_back(CallBlock{p, cls, s});
+  if (*e != hipSuccess) {  // kept blocks may be what fills the device: free them and retry once
+    call_scratch_trim();
+    *e = hipMalloc(&p, cls);
+    if (*e != hipSuccess) return nullptr;
+  }
+  std::lock_guard<std::mutex> lk(pool.mu);
+  pool.live.push_back(CallBlock{p, cls, s, dev});
   return p;
 }
 
 void call_scratch_give(void* p, hipStream_t s) {
-  for (size_t i = 0; i < t_call_live.size(); ++i)
-    if (t_call_live[i].p == p) {
-      CallBlock b = t_call_live[i];
-      t_call_live[i] = t_call_live.back();
-      t_call_live.pop_back();
+  CallPool& pool = call_pool();
+  std::lock_guard<std::mutex> lk(pool.mu);
+  for (size_t i = 0; i < pool.live.size(); ++i)
+    if (pool.live[i].p == p) {
+      CallBlock b = pool.live[i];
+      pool.live[i] = pool.live.back();
+      pool.live.pop_back();
       b.s = s;
-      auto& fb = t_call_pool.free_blocks;
-      fb.push_back(b);
-      if (fb.size() > 64) {  // bounded: the oldest block goes (hipFree orders after its stream's work)
-        (void)hipFree(fb.front().p);
-        fb.erase(fb.begin());
-      }
+      pool.free_blocks.push_back(b);
+      pool.free_bytes += b.bytes;
+      while (pool.free_blocks.size() > 64 || (pool.free_bytes > kPoolCap && pool.free_blocks.size() > 1))
+        pool.drop_front_locked();
       return;
     }
   (void)hipFree(p);  // not from the pool
+}
+
+void call_scratch_trim() {
+  CallPool& pool = call_pool();
+  std::lock_guard<std::mutex> lk(pool.mu);
+  while (!pool.free_blocks.empty()) pool.drop_front_locked();
+}
+
+void call_scratch_release_stream(hipStream_t s) {
+  CallPool& pool = call_pool();
+  std::lock_guard<std::mutex> lk(pool.mu);
+  auto& fb = pool.free_blocks;
+  for (size_t i = 0; i < fb.size();)
+    if (fb[i].s == s) {
+      (void)hipFree(fb[i].p);
+      pool.free_bytes -= fb[i].bytes;
+      fb.erase(fb.begin() + (ptrdiff_t)i);
+    } else {
+      ++i;
+    }
 }
 
 }  // namespace fac

@@ -4170,6 +4170,7 @@ void scratch_bind(ScratchSet* s) { t_scratch = s; }
 
 void scratch_free(ScratchSet& s) {
   if (s.aux) {
+    call_scratch_release_stream(s.aux);
     (void)hipStreamDestroy(s.aux);
     s.aux = nullptr;
   }
@@ -4239,9 +4240,15 @@ void free_engine_device(Engine& e) {
       e.scratch_p[i] = nullptr;
       e.scratch_n[i] = 0;
     }
-  if (e.stream) (void)hipStreamDestroy(e.stream);
+  if (e.stream) {
+    call_scratch_release_stream(e.stream);
+    (void)hipStreamDestroy(e.stream);
+  }
   e.stream = nullptr;
-  if (e.aux_stream) (void)hipStreamDestroy(e.aux_stream);
+  if (e.aux_stream) {
+    call_scratch_release_stream(e.aux_stream);
+    (void)hipStreamDestroy(e.aux_stream);
+  }
   e.aux_stream = nullptr;
   e.d_nodes = nullptr;
 }
@@ -5735,7 +5742,9 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
       HIP_TRY(hipMemcpyAsync(&nc, d_qn.p, 8, hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
       if (nc <= ocap) break;
-      ocap = nc;
+      // which candidates overflow depends on wave timing (a block's first failed reservation varies
+      // by up to one drain, 64 x 255 entries): regrow with headroom so the re-scan fits
+      ocap = nc + nc / 4 + (uint64_t)sgrid * 64 * 255;
     }
     if (diag_env("FAC_TIMING")) {
       std::vector<uint32_t> rc(sgrid);

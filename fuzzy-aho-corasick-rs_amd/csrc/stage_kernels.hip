@@ -597,7 +597,9 @@ __global__ void starts_before_kernel(const uint64_t* off, uint64_t n, uint64_t b
 }
 
 int graphemes_before(const Haystack& h, uint64_t b, hipStream_t st, uint64_t& out, std::string& err) {
-  if (h.ascii) {
+  // an empty (e.g. the last, empty shard of a short text) or unstaged haystack: stage_device returned
+  // before allocating d_stage, and no grapheme starts before any byte
+  if (h.ascii || h.n == 0 || !h.d_stage) {
     out = std::min(b, h.n);
     return FAC_OK;
   }

@@ -235,7 +235,10 @@ void stream_close(StreamCore* s) {
     w->th.join();
     (void)hipSetDevice(s->e->device);
     scratch_free(w->scratch);
-    if (w->stream) (void)hipStreamDestroy(w->stream);
+    if (w->stream) {
+      call_scratch_release_stream(w->stream);
+      (void)hipStreamDestroy(w->stream);
+    }
     delete w;
   }
   delete s;

@@ -114,6 +114,7 @@ SIGNATURES = {
     "fac_last_error": (ctypes.c_char_p, []),
     "fac_build": (ctypes.c_int, [_P(fac_pattern), ctypes.c_uint64, _P(fac_config), _P(_engine_p)]),
     "fac_engine_free": (None, [_engine_p]),
+    "fac_trim_scratch": (None, []),
     "fac_search_raw": (ctypes.c_int, [_engine_p, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_float,
                                       _P(_P(fac_match)), _u64p, _u64p]),
     "fac_matches_free": (None, [_P(fac_match)]),

@@ -157,6 +157,9 @@ const char* fac_last_error(void);
 int fac_build(const fac_pattern* patterns, uint64_t n_patterns, const fac_config* cfg,
               fac_engine** out);
 void fac_engine_free(fac_engine* engine);
+/* Frees the device blocks the library keeps for reuse between calls (per-call scratch of the
+ * pre-filter, ranking and stream windows; at most 2 GiB are kept, fac_engine_free trims too). */
+void fac_trim_scratch(void);
 
 /* FuzzyAhoCorasick::search_raw (search.rs:187-395): best-per-(start,end,pattern) matches at or
  * above `threshold`, unordered. *out is allocated by the library (fac_matches_free). On

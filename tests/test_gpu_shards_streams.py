@@ -87,6 +87,27 @@ def test_device_staged_shards_equal_host_staged(config, nbytes, n):
     assert (sh.graphemes, sh.owned_windows) == (host.graphemes, host.owned_windows)
 
 
+def test_empty_unicode_shard_stages_on_device():
+    """A short Unicode text over many ranks leaves the last shards empty (plan (len, len, len, ...)):
+    staging such a shard fresh from device memory must not touch the unallocated staging scratch
+    (graphemes_before on an empty haystack), and gives the host-staged shard's (empty) result."""
+    import torch
+    from fuzzy_aho_corasick import _native
+    eng = B().fuzzy(L().edits(1)).device(0).build(["é"])
+    data = "é!".encode()  # 3 bytes
+    n = 8
+    empty = 0
+    for r in range(n):
+        plan = _native.shard_plan(eng.max_match_graphemes(), data, n, r)
+        host = StagedHaystack.shard(eng, data, n, r)
+        dev = torch.from_numpy(np.frombuffer(data, np.uint8)[plan[0]:plan[2]].copy()).cuda()
+        sh = StagedHaystack.shard_from_device(eng, dev.data_ptr() if plan[2] > plan[0] else 0, plan)
+        assert (sh.graphemes, sh.owned_windows) == (host.graphemes, host.owned_windows), (r, plan)
+        assert rows_key(sh.search_windows(0.5)[0]) == rows_key(host.search_windows(0.5)[0])
+        empty += plan[0] == plan[2]
+    assert empty > 0
+
+
 def test_search_device_equals_host_records():
     wl, b = _c3_slice(64 << 10)
     eng = b.build(wl.patterns)
