@@ -64,8 +64,10 @@ def parse():
     ap.add_argument("--cpu-min-mib", type=float, default=None,
                     help="single-thread CPU baseline: at least this many MiB of the haystack (default 2)")
     ap.add_argument("--no-fresh-diag", action="store_true",
-                    help="skip diagnostics.fresh_words (c2/c3 at N=1: the same config on SURVEY §8(d)'s fresh-word "
-                         "generator, timed beside the headline)")
+                    help="skip every extra diagnostics leg: fresh_words (c2/c3 at N=1: the same config on SURVEY "
+                         "§8(d)'s fresh-word generator), strong_emulated (N=1: the --shard step of every shard of "
+                         "N in {2,4,8} timed one after another on this GPU), strong (N>1: the --shard step measured "
+                         "beside the weak one), and the default run's c2 / c5 legs")
     ap.add_argument("--cpu-threads", type=int, default=16, help="all-cores CPU baseline threads (box share: 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None, help="default: profiles/traffic_<config>.json")
@@ -238,9 +240,18 @@ def main():
     achieved = bytes_step / (step_dev_ms / 1e3) / 1e9 if step_dev_ms > 0 else 0.0
     traffic, traffic_note = load_traffic(args, mib)
 
-    fresh = None
+    fresh = strong = legs = None
     if (world == 1 and args.config in ("c2", "c3") and args.vocab and device_staging and not args.no_fresh_diag):
         fresh = fresh_words_diag(args, engine, nbytes, local, stream)
+    if args.config in ("c2", "c3", "c4") and device_staging and not args.shard and not args.no_fresh_diag:
+        base_hay = wl.haystack if world == 1 else base_haystack(args, nbytes, vocab)
+        if world == 1:  # every shard of N in {2, 4, 8} on this GPU, one after another
+            strong = strong_emulated(engine, base_hay, wl.threshold, local, stream, elapsed / args.steps * 1e3)
+        else:  # the --shard step on the same ranks, beside the weak one
+            strong = strong_measured(engine, base_hay, wl.threshold, world, rank, local, stream, args.steps)
+        del base_hay
+    if world == 1 and args.config == "c3" and device_staging and not args.no_fresh_diag and args.mib is None:
+        legs = default_legs(args, local)  # C2 (1 GiB) and C5 (one GPU's 12.5 GiB share) in the driver's run
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -308,6 +319,8 @@ def main():
                 "states_from_prefix_cache_per_step": acc["cached"] / K,
                 "sources_sha": sources_sha(),
                 "fresh_words": fresh,
+                ("strong_emulated" if world == 1 else "strong"): strong,
+                **(legs or {}),
             },
         }
         print(json.dumps(line), flush=True)
@@ -365,6 +378,152 @@ def fresh_words_diag(args, engine, nbytes, local, stream, steps=2):
     return out
 
 
+def base_haystack(args, nbytes, vocab):
+    """Rank 0's haystack of the config (the one --shard splits)."""
+    from fuzzy_aho_corasick import workloads as W
+    if args.config == "c4":
+        return W.config("c4", nbytes, hay_seed=40, vocab=vocab).haystack
+    base_seed = {"c1": 1, "c2": 2, "c3": 3}[args.config]
+    return W.config(args.config, nbytes, seed=base_seed, hay_seed=base_seed + 1000, vocab=vocab).haystack
+
+
+def shard_steps(engine, hay, n, r, local, stream, world=1):
+    """The --shard step on shard r of n of `hay`: the shard's bytes [a, e) resident in HBM, staged on
+    the device (fac_haystack_stage_shard_device) and searched in every step, records to rank 0 (RCCL
+    gather at world > 1, else D2H). Returns (the staged shard, step(threshold), the device bytes,
+    [records of the last step])."""
+    import numpy as np
+    import torch
+    from fuzzy_aho_corasick import _native
+    from fuzzy_aho_corasick.engine import StagedHaystack
+    from fuzzy_aho_corasick.distributed import gather_device
+    plan = _native.shard_plan(engine.max_match_graphemes(), hay, n, r)
+    a, e = plan[0], plan[2]
+    dev = torch.from_numpy(np.frombuffer(hay, dtype=np.uint8)[a:e].copy()).to(torch.device("cuda", local))
+    staged = StagedHaystack.shard_from_device(engine, dev.data_ptr() if e > a else 0, plan, stream)
+    nrec = [0]
+
+    def step(threshold):
+        hs = StagedHaystack.shard_from_device(engine, dev.data_ptr() if e > a else 0, plan, stream, reuse=staged)
+        if world == 1:
+            rows, _ = hs.search_windows_records(threshold, stream=stream)
+            nrec[0] = len(rows)
+            return
+        recs, k, _ = hs.search_device(threshold, stream=stream)
+        got = gather_device(recs, k, 0)
+        nrec[0] = got.numel() // 32 if got is not None else k
+
+    return staged, step, dev, nrec
+
+
+def _time_shard(engine, hay, n, r, local, stream, steps, threshold, world=1):
+    import torch
+    import torch.distributed as dist
+    staged, step, dev, nrec = shard_steps(engine, hay, n, r, local, stream, world=world)
+    step(threshold)  # warm-up
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        step(threshold)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    out = (dt, staged.owned_windows, nrec[0], staged.owned_bytes)
+    del staged, dev
+    return out
+
+
+def strong_emulated(engine, hay, threshold, local, stream, full_ms, ns=(2, 4, 8), steps=3):
+    """Strong scaling of the headline, estimated on one GPU: for N in `ns`, every
+    shard r of N of the same haystack (fac_shard_plan: owned bytes + halo) is staged from HBM and
+    searched with the --shard step, one shard after another; an N-GPU step would take the slowest
+    shard's time (+ the record gather), so predicted_speedup = the N = 1 step / max_rank_ms."""
+    out = {"method": "every shard of N timed alone on this GPU (the --shard step: device staging of the shard + "
+                     "search + records D2H), predicted N-GPU step = the slowest shard; the RCCL gather excluded",
+           "n1_ms": full_ms}
+    for n in ns:
+        ms = []
+        for r in range(n):
+            dt, w, k, b = _time_shard(engine, hay, n, r, local, stream, steps, threshold)
+            ms.append(dt / steps * 1e3)
+        out[str(n)] = {"max_rank_ms": max(ms), "min_rank_ms": min(ms), "sum_rank_ms": sum(ms),
+                       "predicted_speedup": full_ms / max(ms), "rank_ms": [round(x, 2) for x in ms]}
+    return out
+
+
+def strong_measured(engine, hay, threshold, world, rank, local, stream, steps):
+    """At N > 1 (default weak run): the --shard step of one haystack over the same ranks, timed like
+    the headline (barrier + synchronize on both sides, max over ranks); value = every rank's owned
+    windows / that time."""
+    import torch
+    import torch.distributed as dist
+    dt, w, k, b = _time_shard(engine, hay, world, rank, local, stream, steps, threshold, world=world)
+    t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    g = torch.tensor([w], device="cuda", dtype=torch.int64)
+    dist.all_reduce(g)
+    dt = float(t.item())
+    return {"value": int(g.item()) * steps / dt / 1e9, "unit": "Gchars/s", "ms_per_step": dt / steps * 1e3,
+            "steps": steps, "haystack_bytes": len(hay), "records_per_step": k,
+            "step": "--shard: one haystack, every rank stages its halo-sliced shard on the device and searches it, "
+                    "records gathered to rank 0 over RCCL"}
+
+
+def default_legs(args, local):
+    """The default run's extra configs (measured by the driver's own run): C2 (edits 1,
+    1K ASCII patterns, 1 GiB, the C2 step) and C5 (one GPU's 12.5 GiB share of the 100 GiB stream)."""
+    import numpy as np
+    import torch
+    from fuzzy_aho_corasick import workloads as W
+    from fuzzy_aho_corasick.engine import StagedHaystack
+    out = {}
+    stream = torch.cuda.current_stream().cuda_stream
+    t0 = time.perf_counter()
+    wl = W.config("c2", DEFAULT_MIB["c2"] << 20, seed=2, hay_seed=1002)
+    eng = W.builder_for(wl).device(local).build(wl.patterns)
+    dev = torch.from_numpy(np.frombuffer(wl.haystack, dtype=np.uint8).copy()).to(torch.device("cuda", local))
+    staged = StagedHaystack.from_device(eng, dev.data_ptr(), len(wl.haystack), stream)
+    gen_s = time.perf_counter() - t0
+    acc = dict(cache=0.0, lane=0.0, kern=0.0, n=0)
+
+    def step():
+        hs = StagedHaystack.from_device(eng, dev.data_ptr(), len(wl.haystack), stream, reuse=staged)
+        rows, st = hs.search_windows_records(wl.threshold, stream=stream)
+        return len(rows), st
+
+    step()
+    torch.cuda.synchronize()
+    steps = 5
+    t = time.perf_counter()
+    for _ in range(steps):
+        n, st = step()
+        acc["n"] = n
+        acc["cache"] += st.cache_ms
+        acc["lane"] += st.lane_ms
+        acc["kern"] += st.kernel_ms
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / steps
+    alg = len(wl.haystack) + 32 * acc["n"]
+    out["c2"] = {"value": staged.owned_windows / dt / 1e9, "unit": "Gchars/s", "ms_per_step": dt * 1e3, "steps": steps,
+                 "workload": "c2: " + WORKLOAD["c2"], "haystack_bytes": len(wl.haystack), "matches_per_step": acc["n"],
+                 "prefix_cache_ms_per_step": acc["cache"] / steps, "lane_kernel_ms_per_step": acc["lane"] / steps,
+                 "search_kernel_ms_per_step": acc["kern"] / steps,
+                 "roofline_frac_step": alg / dt / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": alg,
+                 "setup_s": gen_s, "timed_step": timed_step_desc(args)}
+    del staged, dev, eng, wl
+    torch.cuda.empty_cache()
+    c5 = c5_measure(args, 1, 0, local, steps=2, warmup=1, gib=100.0)
+    c5.pop("_wl")
+    out["c5"] = {k: c5[k] for k in ("value", "unit", "ms_per_step", "steps", "bytes_per_gpu", "stream_windows_per_gpu",
+                                    "window_bytes", "matches_per_step", "prefilter_ms_per_step",
+                                    "research_kernel_ms_per_step", "roofline_frac_kernels", "roofline_frac_step",
+                                    "setup_s", "workload")}
+    return out
+
+
 def load_traffic(args, mib):
     """PMC traffic per step (profiles/make_traffic.py) if it was measured on this config, size and
     these sources; else (None, why)."""
@@ -379,14 +538,14 @@ def load_traffic(args, mib):
     return tj.get("hbm_bytes_per_step"), tj.get("source")
 
 
-def run_c5(args, world, rank, local):
-    """C5: a 100 GiB stream = 100 x one deterministic 1 GiB block (1 needle per MiB),
-    resident once in HBM as block || block[:halo]. GPU g processes its contiguous 1/8 of the stream
-    as windows cut at block and share boundaries, each searched on the device exactly like
+def c5_measure(args, world, rank, local, steps, warmup, gib):
+    """C5: a `gib` GiB stream = repeats of one deterministic 1 GiB block (1 needle per
+    MiB), resident once in HBM as block || block[:halo]. GPU g processes its contiguous 1/8 of the
+    stream as windows cut at block and share boundaries, each searched on the device exactly like
     stream.rs window_matches: the window's text (its bytes plus max_match_graphemes() + 1 of
     overlap, stream.rs:256-258) through Prefiltered::search, ranked sorted().non_overlapping(), and
-    the matches starting before the commit point kept, at absolute offsets."""
-    import numpy as np
+    the matches starting before the commit point kept, at absolute offsets. Returns the timing dict
+    (every rank; elapsed is the max over ranks)."""
     import torch
     import torch.distributed as dist
     from fuzzy_aho_corasick import workloads as W
@@ -394,18 +553,20 @@ def run_c5(args, world, rank, local):
     from fuzzy_aho_corasick.distributed import gather_device, stream_share_windows
     from fuzzy_aho_corasick._native import MATCH_DTYPE
 
-    block_bytes = int((args.mib if args.mib is not None else DEFAULT_MIB["c5"]) * (1 << 20))
+    t_setup = time.perf_counter()
+    block_bytes = int((args.mib if (args.mib is not None and args.config == "c5") else DEFAULT_MIB["c5"]) * (1 << 20))
     wl = W.config("c5", block_bytes, seed=5)
     block = wl.haystack
     engine = W.builder_for(wl).device(local).build(wl.patterns)
     overlap = engine.max_match_graphemes() + 1  # stream_overlap (stream.rs:256-258); ASCII: bytes
     B = len(block)
     staged = StagedHaystack(engine, block + block[:overlap])
-    total = int(args.gib * (1 << 30)) // B * B  # whole blocks
+    total = int(gib * (1 << 30)) // B * B  # whole blocks
     # this GPU's 1/8 of the stream (weak scaling: rank r takes share r)
     windows = stream_share_windows(total, B, rank, overlap)
     processed_rank = sum(w[2] for w in windows)
     stream = torch.cuda.current_stream().cuda_stream
+    setup_s = time.perf_counter() - t_setup
 
     dev_recs = [torch.empty(1 << 20, dtype=torch.uint8, device=torch.device("cuda", local))]
 
@@ -425,14 +586,14 @@ def run_c5(args, world, rank, local):
         recs = dev_recs[0][: n * 32].cpu().numpy().view(MATCH_DTYPE)
         return len(recs), pf_ms, k_ms
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     matches = pf = km = 0
-    for _ in range(args.steps):
+    for _ in range(steps):
         n, a, b = step()
         matches += n
         pf += a
@@ -448,37 +609,56 @@ def run_c5(args, world, rank, local):
     pr = torch.tensor([processed_rank], dtype=torch.int64, device="cuda")
     if world > 1:
         dist.all_reduce(pr)
-    processed = int(pr.item()) * args.steps
-    traffic, traffic_note = load_traffic(args, args.gib * 1024)  # c5 traffic is keyed by the stream size
-    K = max(1, args.steps)
+    processed = int(pr.item()) * steps
+    K = max(1, steps)
     dev_ms = (pf + km) / K
+    bytes_step = processed_rank + 32 * matches / K / world
+    out = {"value": processed / elapsed / 1e9, "unit": "Gchars/s", "ms_per_step": elapsed / steps * 1e3, "steps": steps,
+           "elapsed_s": elapsed, "bytes_per_gpu": processed_rank, "stream_bytes": total,
+           "stream_windows_per_gpu": len(windows), "window_bytes": B, "overlap": overlap, "block_bytes": B,
+           "matches_per_step": matches / K, "prefilter_ms_per_step": pf / K, "research_kernel_ms_per_step": km / K,
+           "dev_ms": dev_ms, "algorithmic_bytes": bytes_step,
+           "roofline_frac_kernels": (bytes_step / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if dev_ms > 0 else None,
+           "roofline_frac_step": bytes_step / (elapsed / steps) / 1e9 / HBM_PEAK_GBS,
+           "setup_s": setup_s, "workload": "c5: " + WORKLOAD["c5"], "patterns": len(wl.patterns),
+           "threshold": wl.threshold, "_wl": wl}
+    del staged, engine
+    return out
+
+
+def run_c5(args, world, rank, local):
+    """C5 line (--config c5): c5_measure at the requested stream size, CPU baseline on rank 0 at N = 1."""
+    r = c5_measure(args, world, rank, local, args.steps, args.warmup, args.gib)
+    wl = r.pop("_wl")
+    traffic, traffic_note = load_traffic(args, args.gib * 1024)  # c5 traffic is keyed by the stream size
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         min_mib = args.cpu_min_mib if args.cpu_min_mib is not None else 2.0  # at least 2 MiB single-thread
         cpu = cpu_baseline(wl, args.cpu_seconds, args.cpu_threads, int(min_mib * (1 << 20)))
     if rank == 0:
-        bytes_step = processed_rank + 32 * matches / K / world
-        achieved = bytes_step / (dev_ms / 1e3) / 1e9 if dev_ms > 0 else 0.0
+        achieved = r["algorithmic_bytes"] / (r["dev_ms"] / 1e3) / 1e9 if r["dev_ms"] > 0 else 0.0
         print(json.dumps({
-            "metric": METRIC, "value": processed / elapsed / 1e9, "unit": "Gchars/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "metric": METRIC, "value": r["value"], "unit": "Gchars/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": r["ms_per_step"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8 haystack bytes / u32 bitap words",
-            "data": f"synthetic: {total / (1 << 30):g} GiB stream = repeats of one {B}-byte block "
+            "data": f"synthetic: {r['stream_bytes'] / (1 << 30):g} GiB stream = repeats of one {r['block_bytes']}-byte block "
                     "(SURVEY.md §8(d) generator, 1 planted needle per MiB), resident in HBM",
-            "config": {"workload": "c5: " + WORKLOAD["c5"], "patterns": len(wl.patterns),
-                       "stream_bytes": total, "bytes_per_gpu": processed_rank, "stream_windows_per_gpu": len(windows),
-                       "window_overlap_graphemes": overlap, "threshold": wl.threshold,
+            "config": {"workload": r["workload"], "patterns": r["patterns"],
+                       "stream_bytes": r["stream_bytes"], "bytes_per_gpu": r["bytes_per_gpu"],
+                       "stream_windows_per_gpu": r["stream_windows_per_gpu"], "window_bytes": r["window_bytes"],
+                       "window_overlap_graphemes": r["overlap"], "threshold": r["threshold"],
                        "parallelism": f"dp{world} (each GPU its 1/8 of the stream; RCCL gather of Match records)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
                          "kernel": "pre-filter (q-gram scan + per-candidate bitap verify; packed bitap scan for "
                                    "patterns with pieces < 3 symbols) + runs_kernel + re-search of the merged windows",
-                         "avg_kernel_ms": dev_ms, "algorithmic_bytes_per_launch": bytes_step},
+                         "avg_kernel_ms": r["dev_ms"], "algorithmic_bytes_per_launch": r["algorithmic_bytes"]},
             "cpu_baseline": cpu,
-            "diagnostics": {"matches_per_step": matches / K, "prefilter_ms_per_step": pf / K,
-                            "research_kernel_ms_per_step": km / K, "sources_sha": sources_sha()},
+            "diagnostics": {"matches_per_step": r["matches_per_step"], "prefilter_ms_per_step": r["prefilter_ms_per_step"],
+                            "research_kernel_ms_per_step": r["research_kernel_ms_per_step"], "sources_sha": sources_sha()},
         }), flush=True)
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

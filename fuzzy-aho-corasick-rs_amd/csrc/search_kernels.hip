@@ -2034,6 +2034,20 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     const bool ovf = lane < Bc && (P0 - lane - 1 + incl > QCAP);
     const bool past = P.rc_mode == 2 && lane < Bc && (st.jm & 0xFFFFu) + 1u >= P.rc_k;  // cache build
     const uint64_t mcut = __ballot(trig) | __ballot(ovf) | __ballot(past);
+#ifdef FAC_PHASE_PROF
+    {  // cut reasons (the first cut lane's): 25 beam trigger, 26 ring, 27 key end (builds), 29 wide node
+      const uint64_t mt = __ballot(trig), mo = __ballot(ovf), mp = __ballot(past);
+      const uint32_t f = mcut ? (uint32_t)first_lane(mcut) : 64u;
+      if (f < Bc) {
+        prof_acc[25] += ((mt >> f) & 1ull) ? 1 : 0;
+        prof_acc[26] += ((mo >> f) & 1ull) ? 1 : 0;
+        prof_acc[27] += ((mp >> f) & 1ull) ? 1 : 0;
+      } else if (Bc < B) {
+        prof_acc[29] += 1;
+      }
+      prof_acc[31] += B == 64u ? 1 : 0;
+    }
+#endif
     if (mcut) Bc = min(Bc, (uint32_t)first_lane(mcut));
     if (Bc == 0) {
       err |= ERR_QUEUE;
@@ -2077,6 +2091,10 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
         }
         dup |= __ballot(d2);
       }
+#ifdef FAC_PHASE_PROF
+      prof_acc[28] += (dup && (uint32_t)first_lane(dup) < Bc) ? 1 : 0;  // cut by an in-batch duplicate
+      prof_acc[30] += (uint64_t)__popcll(dup & ((Bc >= 64u) ? ~0ull : ((1ull << Bc) - 1ull)));  // duplicate lanes
+#endif
       if (dup) Bc = min(Bc, (uint32_t)first_lane(dup));  // lane 0 is never a duplicate
       const bool wrc = wr && lane < Bc;
       const uint32_t n_ins = (uint32_t)__popcll(__ballot(wrc && !found));
@@ -3071,7 +3089,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
 #ifdef FAC_PHASE_PROF
   const uint64_t t_life = __builtin_amdgcn_s_memtime();
   uint64_t t_grp = 0;  // group setup (lookups / hit loads) per 64 windows
-  uint64_t prof_acc[24] = {};  // run_window's slots (per wave, in registers), 22: build epilogue
+  uint64_t prof_acc[32] = {};  // run_window's slots (per wave, in registers), 22: build epilogue
 #endif
   const uint32_t slot = slot_acquire(P);
   EmitList EL{P.ebuf + (size_t)slot * P.ecap, P.ecap, 0};
@@ -3330,6 +3348,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
 #ifdef FAC_PHASE_PROF
   if (lane == 0) {
     for (int i = 0; i < 23; ++i) atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + i], (unsigned long long)prof_acc[i]);
+    for (int i = 25; i < 32; ++i) atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + i], (unsigned long long)prof_acc[i]);
     atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + 23], (unsigned long long)t_grp);
     atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + 24], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_life));
   }
@@ -5256,10 +5275,11 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         std::fprintf(stderr, "FAC_PROF %s variant=%u,%u beam_select=%llu phaseA=%llu wide=%llu phaseB=%llu phaseC=%llu "
                      "emit=%llu push=%llu window_total=%llu batches=%llu [B: prep=%llu units=%llu finish=%llu] "
                      "states: per-edge=%llu fast=%llu committed=%llu loaded=%llu Bc<=4:%llu <=16:%llu <=40:%llu >40:%llu "
-                     "main_popped=%llu prologue=%llu flush=%llu build_epilogue=%llu group_setup=%llu wave_life=%llu\n",
+                     "main_popped=%llu prologue=%llu flush=%llu build_epilogue=%llu group_setup=%llu wave_life=%llu "
+                     "cuts: beam=%llu ring=%llu key_end=%llu dup=%llu wide=%llu dup_lanes=%llu full_batches=%llu\n",
                      m ? "builds" : "main", kVariants[vi].vcap, kVariants[vi].qcap, q[0], q[1], q[2], q[3], q[4], q[5],
                      q[6], q[7], q[8], q[9], q[10], q[11], q[12], q[13], q[14], q[15], q[16], q[17], q[18], q[19], cnt[1],
-                     q[20], q[21], q[22], q[23], q[24]);
+                     q[20], q[21], q[22], q[23], q[24], q[25], q[26], q[27], q[28], q[29], q[30], q[31]);
       }
       std::memset(pr, 0, sizeof(pr));
       HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), pr, sizeof(pr)));
