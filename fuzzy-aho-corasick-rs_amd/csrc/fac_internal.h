@@ -246,6 +246,7 @@ struct SearchParams {
   // auto-beam pass 1 (search.rs:1096-1103): per window queue.len() under exact dedup
   uint32_t* win_counts;  // null: not recorded
   int32_t exact_dedup;   // dedup must be exact (beam, or counting for auto-beam)
+  int32_t dup_cut;       // diagnostics (FAC_DUP_CUT=1): cut a batch at an in-batch duplicate instead of resolving it
   // prefix cache (launch_pass): a state at j reads text[j] and text[j + 1], so the
   // pops before the first state with j >= rc_k - 1 depend only on the window's first rc_k chars;
   // windows sharing them resume from one snapshot (queue, dedup entries, best list, counters)

@@ -70,6 +70,12 @@ __device__ __forceinline__ uint64_t shfl_var_u64(uint64_t v, int src) {  // per-
   return ((uint64_t)hi << 32) | lo;
 }
 
+// f32 -> u32 preserving the order of every non-NaN value: penalties compared as u32
+__device__ __forceinline__ uint32_t pen_order(float f) {
+  uint32_t b = __float_as_uint(f);
+  b = b == 0x80000000u ? 0u : b;  // -0 == +0, as the reference's <= compares them
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   const int I = -1;  // identity for unsigned min (0xFFFFFFFF)
   int x = (int)v;
@@ -1713,7 +1719,8 @@ __device__ __forceinline__ uint32_t hist_bucket(uint64_t pops) {  // 0, 1-15, 16
 }
 #endif
 #ifdef FAC_PHASE_PROF  // diagnostics build (make prof): cycles per phase of run_window
-__device__ unsigned long long g_prof[64];  // [0, 32): main passes, [32, 64): cache builds
+constexpr int kProf = 48;  // accumulator slots per pass kind
+__device__ unsigned long long g_prof[2 * kProf];  // [0, kProf): main passes, [kProf, 2 kProf): cache builds
 #define PROF_T(t) const uint64_t t = __builtin_amdgcn_s_memtime()
 #define PROF_ACC(i, t0) prof_acc[i] += __builtin_amdgcn_s_memtime() - (t0)
 #else
@@ -1782,6 +1789,8 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
   PROF_T(t_win);
   if constexpr (VCAP > 0)
     for (uint32_t i = lane; i < VCAP; i += 64) vis[i].node = EMPTY;
+  PROF_ACC(37, t_win);
+  PROF_T(t_load);
   uint32_t vcount = 0;
   EL.n = 0;
   uint32_t head = 0, tail = 1;
@@ -1847,6 +1856,7 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
   }
   __builtin_amdgcn_wave_barrier();
   const uint32_t beam2 = 2u * P.beam;
+  PROF_ACC(38, t_load);
   PROF_ACC(20, t_win);
 
   while (head < tail) {
@@ -2055,12 +2065,17 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     }
     PROF_ACC(3, t3);
     PROF_T(t4);
-    // ---- phase C: dedup commit (search.rs:617-627 in FIFO order). Only writers matter: a skipped
-    // state's decision cannot change within the batch (stored penalties only decrease). Lanes with
-    // the same key found the same slot in phase A, so each writer claims its slot (lowest lane
-    // wins); a writer whose key equals its slot's winner, or an earlier losing writer's key, would
-    // see a changed table entry in sequential order: the batch is cut before the first such lane.
-    // Winners write in parallel; losers (distinct keys that met at one empty slot) insert serially.
+    // ---- phase C: dedup commit (search.rs:617-627 in FIFO order). Lanes with the same key found
+    // the same slot in phase A, so each writer claims its slot (lowest lane wins). A writer whose key
+    // equals an earlier writer's sees, in sequential order, the table entry that earlier pop left:
+    // it is skipped iff the smallest penalty among the same-key writers before it (the stored
+    // penalty is above all of them) is <= its own (search.rs:618-622), else it lowers the entry. Those
+    // in-batch duplicates are resolved here (a segmented prefix minimum over the batch) instead of
+    // cutting the batch before them; their pushes drop out of the prefix sums below, and the beam /
+    // ring cuts taken above with their pushes counted stay conservative (a cut only ends the batch
+    // early; the next batch re-checks the beam at its first pop). Winners write in parallel; losers
+    // (distinct keys that met at one claim word or empty slot) insert serially in lane order.
+    uint64_t nskip = 0;  // wave-uniform: in-batch duplicates the sequential order skips
     if constexpr (VCAP > 0) {
       const bool wr = lane < Bc && !skip;
       cseq += 1;
@@ -2080,7 +2095,7 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
       const bool loser = wr && w != lane && !same;
       uint64_t dup = __ballot(same);
       const uint64_t lmask = __ballot(loser);
-      if (lmask) {
+      if (lmask && P.dup_cut) {
         bool d2 = false;
         uint64_t mm = lmask;
         while (mm) {
@@ -2092,10 +2107,24 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
         dup |= __ballot(d2);
       }
 #ifdef FAC_PHASE_PROF
-      prof_acc[28] += (dup && (uint32_t)first_lane(dup) < Bc) ? 1 : 0;  // cut by an in-batch duplicate
+      prof_acc[28] += (dup && (uint32_t)first_lane(dup) < Bc) ? 1 : 0;  // batches holding an in-batch duplicate
       prof_acc[30] += (uint64_t)__popcll(dup & ((Bc >= 64u) ? ~0ull : ((1ull << Bc) - 1ull)));  // duplicate lanes
 #endif
-      if (dup) Bc = min(Bc, (uint32_t)first_lane(dup));  // lane 0 is never a duplicate
+      if (P.dup_cut) {  // diagnostics (FAC_DUP_CUT): the round-5 rule, cut before the first duplicate
+        if (dup) Bc = min(Bc, (uint32_t)first_lane(dup));  // lane 0 is never a duplicate
+        dup = 0;
+      }
+      // same-key duplicates of a winner: prefix minimum over the writers of their key before them
+      const uint64_t bmask = Bc >= 64u ? ~0ull : ((1ull << Bc) - 1ull);
+      uint64_t ds = dup & bmask;
+      while (ds) {
+        const int l = first_lane(ds);
+        ds &= ds - 1;
+        const uint32_t kn = shfl_u32(st.node, l), kj = shfl_u32(st.jm, l), kp = shfl_u32(st.packed, l);
+        const bool eq = wr && lane < (uint32_t)l && kn == st.node && kj == st.jm && kp == st.packed;
+        const uint32_t mn = wave_min_u32(eq ? pen_order(st.pen) : 0xFFFFFFFFu);
+        if (mn <= pen_order(shfl_f32(st.pen, l))) nskip |= 1ull << l;
+      }
       const bool wrc = wr && lane < Bc;
       const uint32_t n_ins = (uint32_t)__popcll(__ballot(wrc && !found));
       const bool full = vcount + n_ins >= VCAP - VCAP / 8;
@@ -2106,6 +2135,15 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
         }
         vcount += (uint32_t)__popcll(__ballot(wrc && w == lane && !found));
         __builtin_amdgcn_wave_barrier();
+        // the same-key duplicates that are not skipped lower the entry, in lane order (each below
+        // every earlier one: the last leaves the smallest)
+        uint64_t dl = dup & bmask & ~nskip;
+        while (dl) {
+          const int l = first_lane(dl);
+          dl &= dl - 1;
+          if (lane == (uint32_t)l) vis[vslot].pen = st.pen;
+          __builtin_amdgcn_wave_barrier();
+        }
         uint64_t ml = __ballot(wrc && loser);
         while (ml) {
           const int l = first_lane(ml);
@@ -2115,25 +2153,32 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
           kt.jm = shfl_u32(st.jm, l);
           kt.pen = shfl_f32(st.pen, l);
           kt.packed = shfl_u32(st.packed, l);
-          visited_check<VCAP>(vis, vcount, kt, P.exact_dedup != 0, err);
+          if (visited_check<VCAP>(vis, vcount, kt, P.exact_dedup != 0, err)) nskip |= 1ull << l;  // a loser's duplicate
         }
       } else {  // near-full table: the reference order, one state at a time
+        nskip = 0;
+        const uint64_t mw = __ballot(wr);
         for (uint32_t t = 0; t < Bc; ++t) {
-          if (!((__ballot(wr) >> t) & 1ull)) continue;
+          if (!((mw >> t) & 1ull)) continue;
           KState kt;
           kt.node = shfl_u32(st.node, t);
           kt.jm = shfl_u32(st.jm, t);
           kt.pen = shfl_f32(st.pen, t);
           kt.packed = shfl_u32(st.packed, t);
-          visited_check<VCAP>(vis, vcount, kt, P.exact_dedup != 0, err);
+          if (visited_check<VCAP>(vis, vcount, kt, P.exact_dedup != 0, err)) nskip |= 1ull << t;
         }
       }
       __builtin_amdgcn_wave_barrier();
     }
     PROF_ACC(4, t4);
     PROF_T(t5);
+    // in-batch duplicates skipped above push nothing: the pushes' offsets without them
+    const bool keep = alive && lane < Bc && !((nskip >> lane) & 1ull);
+    const uint32_t cnt2 = keep ? x.count : 0u;
+    const uint32_t incl2 = nskip ? wave_inclusive_sum(cnt2) : incl;
+    const uint32_t excl2 = incl2 - cnt2;
     // ---- phase D: emissions (FIFO order), then pushes at tail + exclusive prefix
-    uint64_t mem = __ballot(alive && lane < Bc && node_has_out(nd));
+    uint64_t mem = __ballot(keep && node_has_out(nd));
     while (mem) {
       const int l = first_lane(mem);
       mem &= mem - 1;
@@ -2142,14 +2187,14 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     }
     PROF_ACC(5, t5);
     PROF_T(t6);
-    push_units<QCAP, FAC_UK, MAP>(P, reinterpret_cast<ExpScratch*>(claim), q, tail + excl, st, nd, x, pr.cur_ch,
-                                  alive && lane < Bc && x.count != 0);
+    push_units<QCAP, FAC_UK, MAP>(P, reinterpret_cast<ExpScratch*>(claim), q, tail + excl2, st, nd, x, pr.cur_ch,
+                                  keep && x.count != 0);
 #if defined(FAC_DUP) && FAC_DUP == 4
-    push_units<QCAP, FAC_UK, MAP>(P, reinterpret_cast<ExpScratch*>(claim), q, opq(tail + excl), st, nd, x, opq(pr.cur_ch),
-                             alive && lane < Bc && x.count != 0);  // same entries rewritten
+    push_units<QCAP, FAC_UK, MAP>(P, reinterpret_cast<ExpScratch*>(claim), q, opq(tail + excl2), st, nd, x, opq(pr.cur_ch),
+                             keep && x.count != 0);  // same entries rewritten
 #endif
     __builtin_amdgcn_wave_barrier();
-    tail += shfl_u32(incl, Bc - 1);
+    tail += shfl_u32(incl2, Bc - 1);
     if (track_beam && lane < Bc) jp1 = max(jp1, (st.jm & 0xFFFFu) + 1u);
     head += Bc;
     popped += Bc;
@@ -3089,7 +3134,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
 #ifdef FAC_PHASE_PROF
   const uint64_t t_life = __builtin_amdgcn_s_memtime();
   uint64_t t_grp = 0;  // group setup (lookups / hit loads) per 64 windows
-  uint64_t prof_acc[32] = {};  // run_window's slots (per wave, in registers), 22: build epilogue
+  uint64_t prof_acc[kProf] = {};  // run_window's slots (per wave, in registers), 22: build epilogue, 32-36 its parts
 #endif
   const uint32_t slot = slot_acquire(P);
   EmitList EL{P.ebuf + (size_t)slot * P.ecap, P.ecap, 0};
@@ -3234,6 +3279,17 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
             __device__ ~EpAcc() { acc += __builtin_amdgcn_s_memtime() - t; }
           } ep_acc{__builtin_amdgcn_s_memtime(), prof_acc[22]};
 #endif
+#ifdef FAC_PHASE_PROF
+          uint64_t t_ep = __builtin_amdgcn_s_memtime();
+          auto ep_lap = [&](int slot) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            prof_acc[slot] += t - t_ep;
+            t_ep = t;
+          };
+#define EP_LAP(i) ep_lap(i)
+#else
+#define EP_LAP(i)
+#endif
           const uint32_t ent = (uint32_t)(v0 + (uint64_t)l);
           const uint32_t nq = qlen - qhead;
           // live dedup entries: a key is only met again at its own j, and every future state's j is
@@ -3265,6 +3321,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
             const unsigned we = wave_or(err);
             atomicAdd(&g_bad[(we & ERR_QUEUE) ? 0 : (we & ERR_VISITED) ? 1 : (we & ERR_EMIT) ? 2 : EL.n > P.rc_emax ? 3 : 4], 1ull);
           }
+          EP_LAP(32);
           const uint32_t words = RC_HDR + nq + nv + EL.n;
           // the wave carves snapshots out of its own pool chunk: one pool atomic per chunk, not per
           // snapshot (a same-address atomic per entry serialises the build at one L2 channel)
@@ -3278,12 +3335,14 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           const unsigned long long off = pool_cur;
           if (!bad) pool_cur += words;
           bad = bad || off + words > P.rc_pool_cap || off > 0xFFFFFFF0ull;
+          EP_LAP(33);
           // (the key's chars are not stored: rc_publish_kernel reads them from the representative's text)
           uint4* dst = P.rc_pool + off + RC_HDR;  // after the header words
           for (uint32_t i = lane; i < nq && !bad; i += 64) {
             const KState k = s_q[(qhead + i) & (QCAP - 1)];
             dst[i] = make_uint4(k.node, k.jm, __float_as_uint(k.pen), k.packed);
           }
+          EP_LAP(34);
           // compacted in slot order, the entries a resumed dedup-free run must still honour (j < jcheck)
           // first: ncheck of them
           const uint32_t jcheck = min(jlive, jbeam[0]);
@@ -3306,6 +3365,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
               if (pass == 0) ncheck = at0;
             }
           }
+          EP_LAP(35);
           for (uint32_t i = lane; i < EL.n && !bad; i += 64) dst[nq + nv + i] = EL.buf[i];
           if (lane == 0) {
             if (!bad) {
@@ -3321,6 +3381,8 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           (void)vcnt;
           err &= ~(ERR_QUEUE | ERR_VISITED | ERR_EMIT);
           __builtin_amdgcn_wave_barrier();
+          EP_LAP(36);
+#undef EP_LAP
           if (any_err(err)) break;
           continue;
         }
@@ -3347,10 +3409,11 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
   if (lane == 0 && kept_snaps) atomicAdd(P.counters + 11, (unsigned long long)kept_snaps);  // sizes the lookup table
 #ifdef FAC_PHASE_PROF
   if (lane == 0) {
-    for (int i = 0; i < 23; ++i) atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + i], (unsigned long long)prof_acc[i]);
-    for (int i = 25; i < 32; ++i) atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + i], (unsigned long long)prof_acc[i]);
-    atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + 23], (unsigned long long)t_grp);
-    atomicAdd(&g_prof[(P.rc_mode == 2 ? 32 : 0) + 24], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_life));
+    const int pb = P.rc_mode == 2 ? kProf : 0;
+    for (int i = 0; i < kProf; ++i)
+      if (i != 23 && i != 24) atomicAdd(&g_prof[pb + i], (unsigned long long)prof_acc[i]);
+    atomicAdd(&g_prof[pb + 23], (unsigned long long)t_grp);
+    atomicAdd(&g_prof[pb + 24], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_life));
   }
 #endif
   if (lane == 0) cached_lane += cached;
@@ -4471,6 +4534,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.has_pattern_limits = e.has_pattern_limits;
   P.beam = beam;
   P.exact_dedup = exact_dedup ? 1 : 0;
+  P.dup_cut = diag_env("FAC_DUP_CUT") ? 1 : 0;
   P.window_skip = e.window_skip;
   P.has_map = e.has_map ? 1 : 0;
   if (e.has_map) {  // multi-character mappings: whole-grapheme ids (ensure_gids for Unicode text)
@@ -5268,18 +5332,20 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
 #endif
 #ifdef FAC_PHASE_PROF
     {
-      unsigned long long pr[64];
+      unsigned long long pr[2 * kProf];
       HIP_TRY(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_prof), sizeof(pr)));
       for (int m = 0; m < 2; ++m) {
-        const unsigned long long* q = pr + 32 * m;
+        const unsigned long long* q = pr + kProf * m;
         std::fprintf(stderr, "FAC_PROF %s variant=%u,%u beam_select=%llu phaseA=%llu wide=%llu phaseB=%llu phaseC=%llu "
                      "emit=%llu push=%llu window_total=%llu batches=%llu [B: prep=%llu units=%llu finish=%llu] "
                      "states: per-edge=%llu fast=%llu committed=%llu loaded=%llu Bc<=4:%llu <=16:%llu <=40:%llu >40:%llu "
                      "main_popped=%llu prologue=%llu flush=%llu build_epilogue=%llu group_setup=%llu wave_life=%llu "
-                     "cuts: beam=%llu ring=%llu key_end=%llu dup=%llu wide=%llu dup_lanes=%llu full_batches=%llu\n",
+                     "cuts: beam=%llu ring=%llu key_end=%llu dup=%llu wide=%llu dup_lanes=%llu full_batches=%llu "
+                     "epilogue: scan=%llu pool=%llu queue=%llu dedup=%llu tail=%llu prologue: clear=%llu load=%llu\n",
                      m ? "builds" : "main", kVariants[vi].vcap, kVariants[vi].qcap, q[0], q[1], q[2], q[3], q[4], q[5],
                      q[6], q[7], q[8], q[9], q[10], q[11], q[12], q[13], q[14], q[15], q[16], q[17], q[18], q[19], cnt[1],
-                     q[20], q[21], q[22], q[23], q[24], q[25], q[26], q[27], q[28], q[29], q[30], q[31]);
+                     q[20], q[21], q[22], q[23], q[24], q[25], q[26], q[27], q[28], q[29], q[30], q[31],
+                     q[32], q[33], q[34], q[35], q[36], q[37], q[38]);
       }
       std::memset(pr, 0, sizeof(pr));
       HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), pr, sizeof(pr)));

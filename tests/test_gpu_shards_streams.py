@@ -94,7 +94,7 @@ def test_empty_unicode_shard_stages_on_device():
     import torch
     from fuzzy_aho_corasick import _native
     eng = B().fuzzy(L().edits(1)).device(0).build(["é"])
-    data = "é!".encode()  # 3 bytes
+    data = "éé".encode()  # 4 bytes: shards 6 and 7 of 8 are (4, 4, 4)
     n = 8
     empty = 0
     for r in range(n):
