@@ -576,7 +576,7 @@ __device__ void sel_s_mom(const A& v0, uint32_t len, uint32_t k) {  // median_of
 #define FAC_SEL_ATTR __attribute__((noinline))
 #endif
 template <uint32_t QCAP>
-__device__ FAC_SEL_ATTR void beam_select(KState* q, uint32_t head, uint32_t& tail, uint32_t bw, uint4* scratch, uint32_t limit0) {
+__device__ FAC_SEL_ATTR void beam_select(KState* q, uint32_t head, uint32_t tail, uint32_t bw, uint4* scratch, uint32_t limit0) {
   const uint32_t lane = lane_id();
   const uint32_t P = tail - head;
   uint4* qq = reinterpret_cast<uint4*>(q);
@@ -773,7 +773,7 @@ __device__ uint32_t sel_partition_lds(uint32_t* K, uint16_t* I, uint32_t* W, uin
 }
 
 template <uint32_t QCAP>
-__device__ FAC_SEL_ATTR void beam_select_lds(KState* q, uint32_t head, uint32_t& tail, uint32_t bw, uint32_t* scratch, uint32_t limit0) {
+__device__ FAC_SEL_ATTR void beam_select_lds(KState* q, uint32_t head, uint32_t tail, uint32_t bw, uint32_t* scratch, uint32_t limit0) {
   static_assert(QCAP <= 256, "LDS select: rings of up to 256 states");
   const uint32_t lane = lane_id();
   const uint32_t P = tail - head;
@@ -871,7 +871,7 @@ __device__ FAC_SEL_ATTR void beam_select_lds(KState* q, uint32_t head, uint32_t&
 // Diagnostics only (FAC_BEAM_CANONICAL, rounds 1-2's rule): keep the bw smallest by (penalty,
 // queue position) in queue order -- not the reference's order; for A/B measurements of the tie rule.
 template <uint32_t QCAP>
-__device__ FAC_SEL_ATTR void beam_select_canonical(KState* q, uint32_t head, uint32_t& tail, uint32_t bw) {
+__device__ FAC_SEL_ATTR void beam_select_canonical(KState* q, uint32_t head, uint32_t tail, uint32_t bw) {
   constexpr int PER = QCAP / 64;
   const uint32_t lane = lane_id();
   const uint32_t P = tail - head;
@@ -971,7 +971,7 @@ __device__ __forceinline__ bool visited_check(KState* vis, uint32_t& vcount, con
         return false;  // without a beam, expanding a duplicate cannot change results
       }
       if (lane == (uint32_t)fe) vis[slot] = s;
-      vcount += 1;
+      vcount = __builtin_amdgcn_readfirstlane(vcount + 1);  // wave-uniform: kept in an SGPR
       return false;
     }
   }
@@ -1848,7 +1848,7 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
         }
       }
     }
-    if constexpr (VCAP > 0) vcount = nv;
+    if constexpr (VCAP > 0) vcount = __builtin_amdgcn_readfirstlane(nv);
     EL.n = ne;
     cached += rc.pops;  // the snapshot's pops (not counted as popped: that is executed work)
   } else if (lane == 0) {
@@ -1863,9 +1863,12 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
     PROF_T(t0);
     if constexpr (VCAP > 0) {
       if (P.beam && tail - head > beam2) {
+        // (tail by value: a reference into these noinline calls kept it in scratch memory for the whole
+        // window loop, reloaded with a full vmcnt wait wherever it was read)
         if (P.beam_canonical) beam_select_canonical<QCAP>(q, head, tail, P.beam);  // diagnostics
         else if constexpr (QCAP <= 256) beam_select_lds<QCAP>(q, head, tail, P.beam, claim, P.sel_limit);  // :577-589
         else beam_select<QCAP>(q, head, tail, P.beam, bsel, P.sel_limit);
+        tail = head + P.beam;  // truncate(bw) (:587)
         if (track_beam) jbeam = max(jbeam, shfl_u32(wave_inclusive_max(jp1), 63));
       }
     } else if (P.beam && tail - head > beam2) {
@@ -2133,7 +2136,7 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
           if (found) vis[vslot].pen = st.pen;  // lower the stored penalty (:623)
           else vis[vslot] = st;                // insert (:626)
         }
-        vcount += (uint32_t)__popcll(__ballot(wrc && w == lane && !found));
+        vcount = __builtin_amdgcn_readfirstlane(vcount + (uint32_t)__popcll(__ballot(wrc && w == lane && !found)));
         __builtin_amdgcn_wave_barrier();
         // the same-key duplicates that are not skipped lower the entry, in lane order (each below
         // every earlier one: the last leaves the smallest)
@@ -3299,19 +3302,19 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           jmin = wave_min_u32(jmin);
           auto live = [&](const KState& k) { return k.node != EMPTY && (k.jm & 0xFFFFu) >= jmin; };
           uint32_t nv = 0, jlive = 0;  // 1 + the largest j among the live entries (0: none)
-          // the table is read once: each lane's VCAP/64 slots into registers, their live bits kept
+          // each lane's VCAP/64 slots, their live bits kept; the entries are read from LDS again by the
+          // writing passes below (held in registers, the 8 slots' 32 VGPRs made this the kernel's
+          // register peak and pushed loop state into scratch)
           constexpr uint32_t NSL = VCAP ? VCAP / 64 : 1;
-          KState kv[NSL];
           uint32_t lmask = 0;
           if constexpr (VCAP > 0) {
 #pragma unroll
-            for (uint32_t u = 0; u < NSL; ++u) kv[u] = s_vis[u * 64 + lane];
-#pragma unroll
             for (uint32_t u = 0; u < NSL; ++u) {
-              const bool lv = live(kv[u]);
+              const KState kvu = s_vis[u * 64 + lane];
+              const bool lv = live(kvu);
               lmask |= (lv ? 1u : 0u) << u;
               nv += (uint32_t)__popcll(__ballot(lv));
-              jlive = max(jlive, lv ? (kv[u].jm & 0xFFFFu) + 1u : 0u);
+              jlive = max(jlive, lv ? (kvu.jm & 0xFFFFu) + 1u : 0u);
             }
           }
           jlive = wave_inclusive_max(jlive);
@@ -3348,18 +3351,15 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           const uint32_t jcheck = min(jlive, jbeam[0]);
           uint32_t ncheck = 0;
           if constexpr (VCAP > 0) {
-            uint32_t cmask = 0;
-#pragma unroll
-            for (uint32_t u = 0; u < NSL; ++u)
-              cmask |= (((lmask >> u) & 1u) && (kv[u].jm & 0xFFFFu) + 1u <= jcheck ? 1u : 0u) << u;
             uint32_t at0 = 0;
             for (uint32_t pass = 0; pass < 2 && !bad; ++pass) {
-              const uint32_t sel = pass == 0 ? cmask : (lmask & ~cmask);
 #pragma unroll
               for (uint32_t u = 0; u < NSL; ++u) {
-                const bool occ = (sel >> u) & 1u;
+                const KState kvu = s_vis[u * 64 + lane];
+                const bool chk = (kvu.jm & 0xFFFFu) + 1u <= jcheck;
+                const bool occ = ((lmask >> u) & 1u) && (pass == 0 ? chk : !chk);
                 const uint64_t m = __ballot(occ);
-                if (occ) dst[nq + at0 + prefix_below(m)] = make_uint4(kv[u].node, kv[u].jm, __float_as_uint(kv[u].pen), kv[u].packed);
+                if (occ) dst[nq + at0 + prefix_below(m)] = make_uint4(kvu.node, kvu.jm, __float_as_uint(kvu.pen), kvu.packed);
                 at0 += (uint32_t)__popcll(m);
               }
               if (pass == 0) ncheck = at0;
