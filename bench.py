@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5", "stream"])
     ap.add_argument("--mib", type=float, default=None, help="haystack MiB per rank (c5: block MiB)")
     ap.add_argument("--shard", action="store_true", help="strong scaling: shard one haystack over the ranks")
     ap.add_argument("--end-to-end", action="store_true",
@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--prestaged", action="store_true",
                     help="diagnostic: stage the haystack once before the timed steps (search only)")
     ap.add_argument("--gib", type=float, default=100.0, help="c5: total stream GiB (each GPU takes 1/8)")
+    ap.add_argument("--window-kib", type=float, default=256.0,
+                    help="c5: stream window bytes (KiB; the crate's DEFAULT_WINDOW, stream.rs:65); 0: one window per 1 GiB block")
     ap.add_argument("--vocab", type=int, default=50_000,
                     help="filler words drawn from a fixed vocabulary of this many random words; 0: fresh random words")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="single-thread CPU baseline sample budget")
@@ -119,6 +121,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL on ROCm
     if args.config == "c5":
         return run_c5(args, world, rank, local)
+    if args.config == "stream":
+        return run_stream(args, world, rank, local)
 
     from fuzzy_aho_corasick import workloads as W
     from fuzzy_aho_corasick.engine import StagedHaystack
@@ -518,7 +522,7 @@ def default_legs(args, local):
     c5 = c5_measure(args, 1, 0, local, steps=2, warmup=1, gib=100.0)
     c5.pop("_wl")
     out["c5"] = {k: c5[k] for k in ("value", "unit", "ms_per_step", "steps", "bytes_per_gpu", "stream_windows_per_gpu",
-                                    "window_bytes", "matches_per_step", "prefilter_ms_per_step",
+                                    "window_bytes", "batches_per_step", "matches_per_step", "prefilter_ms_per_step",
                                     "research_kernel_ms_per_step", "roofline_frac_kernels", "roofline_frac_step",
                                     "setup_s", "workload")}
     return out
@@ -563,20 +567,29 @@ def c5_measure(args, world, rank, local, steps, warmup, gib):
     staged = StagedHaystack(engine, block + block[:overlap])
     total = int(gib * (1 << 30)) // B * B  # whole blocks
     # this GPU's 1/8 of the stream (weak scaling: rank r takes share r)
-    windows = stream_share_windows(total, B, rank, overlap)
+    window_bytes = int(args.window_kib * 1024) if args.window_kib else None  # None: 1 GiB block windows
+    windows = stream_share_windows(total, B, rank, overlap, window=window_bytes)
     processed_rank = sum(w[2] for w in windows)
+    # batches: the windows of one block pass (contiguous in the resident block), one batched call each
+    batches, cur = [], []
+    for w in windows:
+        if cur and w[0] < cur[-1][0]:
+            batches.append(cur)
+            cur = []
+        cur.append(w)
+    if cur:
+        batches.append(cur)
     stream = torch.cuda.current_stream().cuda_stream
     setup_s = time.perf_counter() - t_setup
 
     dev_recs = [torch.empty(1 << 20, dtype=torch.uint8, device=torch.device("cuda", local))]
 
     def step():
-        # every window's owned records (stream.rs:262-297, ranked on the device) appended in HBM, then
-        # at N > 1 one RCCL gather to rank 0 from there, at N = 1 one copy to host memory
+        # every window's owned records (stream.rs:262-297) appended in HBM in stream order, then at
+        # N > 1 one RCCL gather to rank 0 from there, at N = 1 one copy to host memory
         pf_ms, k_ms, n = 0.0, 0.0, 0
-        for (g0, g1, commit, base) in windows:
-            dev_recs[0], got, st = staged.stream_window_device(g0, g1, commit, base, wl.threshold, True,
-                                                               dev_recs[0], n, stream=stream)
+        for bw in batches:
+            dev_recs[0], got, st = staged.stream_windows_device(bw, wl.threshold, True, dev_recs[0], n, stream=stream)
             n += got
             pf_ms += st.prefilter_ms
             k_ms += st.kernel_ms
@@ -615,7 +628,8 @@ def c5_measure(args, world, rank, local, steps, warmup, gib):
     bytes_step = processed_rank + 32 * matches / K / world
     out = {"value": processed / elapsed / 1e9, "unit": "Gchars/s", "ms_per_step": elapsed / steps * 1e3, "steps": steps,
            "elapsed_s": elapsed, "bytes_per_gpu": processed_rank, "stream_bytes": total,
-           "stream_windows_per_gpu": len(windows), "window_bytes": B, "overlap": overlap, "block_bytes": B,
+           "stream_windows_per_gpu": len(windows), "window_bytes": window_bytes or B, "overlap": overlap, "block_bytes": B,
+           "batches_per_step": len(batches),
            "matches_per_step": matches / K, "prefilter_ms_per_step": pf / K, "research_kernel_ms_per_step": km / K,
            "dev_ms": dev_ms, "algorithmic_bytes": bytes_step,
            "roofline_frac_kernels": (bytes_step / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if dev_ms > 0 else None,
@@ -646,6 +660,7 @@ def run_c5(args, world, rank, local):
             "config": {"workload": r["workload"], "patterns": r["patterns"],
                        "stream_bytes": r["stream_bytes"], "bytes_per_gpu": r["bytes_per_gpu"],
                        "stream_windows_per_gpu": r["stream_windows_per_gpu"], "window_bytes": r["window_bytes"],
+                       "batches_per_step": r["batches_per_step"],
                        "window_overlap_graphemes": r["overlap"], "threshold": r["threshold"],
                        "parallelism": f"dp{world} (each GPU its 1/8 of the stream; RCCL gather of Match records)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -659,6 +674,72 @@ def run_c5(args, world, rank, local):
         }), flush=True)
     if world > 1:
         import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+class _RepeatReader:
+    """An in-memory reader of `total` bytes: repeats of `block` (io.RawIOBase-like read(n))."""
+
+    def __init__(self, block: bytes, total: int):
+        self.block, self.total, self.pos = memoryview(block), total, 0
+
+    def read(self, n: int) -> bytes:
+        n = min(n, self.total - self.pos)
+        if n <= 0:
+            return b""
+        o = self.pos % len(self.block)
+        take = min(n, len(self.block) - o)
+        self.pos += take
+        return bytes(self.block[o:o + take])
+
+
+def stream_measure(local, gib, steps, warmup=1):
+    """The product's streaming API itself (FuzzyAhoCorasick::search_stream, stream.rs:319-335, over
+    fac_stream_*): an in-memory reader of `gib` GiB (repeats of C5's 1 GiB block, SURVEY §8(d)
+    generator) read in READ_CHUNK pieces, windows of the crate's 256 KiB cut as its WindowReader
+    does, each searched without the pre-filter (the crate's search_stream has none), ranked and cut
+    at its commit point; every match delivered to the callback. Host bytes in, matches out: H2D
+    copies inside the timed region."""
+    from fuzzy_aho_corasick import workloads as W
+    t0 = time.perf_counter()
+    wl = W.config("c5", 1 << 30, seed=5)
+    engine = W.builder_for(wl).device(local).build(wl.patterns)
+    total = int(gib * (1 << 30))
+    setup_s = time.perf_counter() - t0
+    hits = [0]
+
+    def on_match(m):
+        hits[0] += 1
+
+    for _ in range(warmup):
+        engine.search_stream(_RepeatReader(wl.haystack, min(total, 1 << 30)), wl.threshold, on_match)
+    hits[0] = 0
+    t = time.perf_counter()
+    for _ in range(steps):
+        n = engine.search_stream(_RepeatReader(wl.haystack, total), wl.threshold, on_match)
+        assert n == total
+    dt = (time.perf_counter() - t) / steps
+    return {"value": total / dt / 1e9, "unit": "Gchars/s", "ms_per_step": dt * 1e3, "steps": steps,
+            "stream_bytes": total, "matches_per_step": hits[0] / steps, "setup_s": setup_s,
+            "workload": "search_stream (fac_stream_*) over an in-memory reader of C5 data, 256 KiB windows, "
+                        "no pre-filter (as the crate's search_stream), edits=1, 1K patterns (10-16), threshold 0.85",
+            "timed": "host bytes -> window cuts -> batched H2D + search + per-window ranking -> matches to a callback"}
+
+
+def run_stream(args, world, rank, local):
+    """--config stream: stream_measure on this rank (N > 1: every rank its own stream, weak)."""
+    import torch.distributed as dist
+    r = stream_measure(local, args.gib if args.gib != 100.0 else 8.0, args.steps, args.warmup)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": r["value"] * world, "unit": "Gchars/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": r["ms_per_step"],
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8 haystack bytes",
+                          "data": "synthetic: repeats of C5's 1 GiB block (SURVEY.md §8(d) generator), in host memory",
+                          "config": {"workload": r["workload"], "stream_bytes_per_gpu": r["stream_bytes"],
+                                     "window_bytes": 256 * 1024, "timed_step": r["timed"]},
+                          "diagnostics": {"matches_per_step": r["matches_per_step"], "sources_sha": sources_sha()}}),
+              flush=True)
+    if world > 1:
         dist.destroy_process_group()
 
 

@@ -670,6 +670,97 @@ int prefiltered_staged(const fac::Engine& e, const fac::Haystack& h, float thres
   return prefiltered_view(e, h, whole(h), threshold, stream, merged, stats, err);
 }
 
+
+}  // namespace
+
+namespace fac {
+
+// A batch of stream windows of one staged ASCII haystack searched together (stream.rs
+// window_matches for each, :262-297): wins holds (g_begin, g_end, commit_bytes, base) per window,
+// sorted by g_begin, each overlapping only its neighbours. With the pre-filter, one q-gram pass over
+// the windows' union gives every window its own merged bitap windows (the automaton starts at the
+// window's first byte, its coverage stays inside it); without it each window is one segment. All
+// segments, tagged with their window, go to one launch; then every window's records are ranked
+// sorted().non_overlapping() and cut at its commit point on the host. FAC_E_UNSUPPORTED (nothing
+// done) when the batch does not qualify: a Unicode haystack (a window's grapheme segmentation
+// depends on where its text starts and ends), windows out of order or overlapping beyond their
+// neighbours, or pre-filter tables that need the packed full scan.
+int stream_windows_batch(const Engine& e, const Haystack& h, const uint64_t* wins, uint64_t n_windows, float threshold,
+                         bool prefilter, hipStream_t st, std::vector<fac_match>& owned, fac_stats* stats, std::string& err) {
+  owned.clear();
+  if (!h.ascii || h.open_end || h.base || n_windows == 0 || n_windows >= (1u << 24)) return FAC_E_UNSUPPORTED;
+  std::vector<std::pair<uint64_t, uint64_t>> span(n_windows);
+  std::vector<WinOwn> own(n_windows);
+  uint64_t u0 = UINT64_MAX, u1 = 0;
+  for (uint64_t w = 0; w < n_windows; ++w) {
+    const uint64_t ge = std::min<uint64_t>(wins[4 * w + 1], h.n), gb = std::min<uint64_t>(wins[4 * w], ge);
+    span[w] = {gb, ge};
+    own[w] = WinOwn{gb, wins[4 * w + 2], wins[4 * w + 3]};  // ASCII: grapheme = byte
+    u0 = std::min(u0, gb);
+    u1 = std::max(u1, ge);
+    if (w && gb < span[w - 1].first) return FAC_E_UNSUPPORTED;
+    if (w >= 2 && span[w - 2].second >= gb) return FAC_E_UNSUPPORTED;  // same parity must not touch
+  }
+  if (u1 <= u0) return FAC_OK;
+  const SegDesc view = slice_view(h, u0, u1);
+  std::vector<SegDesc> segs;
+  std::vector<uint32_t> ks;
+  if (prefilter && e.bitap_ok && prefilter_ks(e, threshold, ks)) {
+    std::vector<std::pair<uint64_t, uint64_t>> rel(n_windows), runs;
+    for (uint64_t w = 0; w < n_windows; ++w) rel[w] = {span[w].first - u0, span[w].second - u0};
+    std::vector<uint32_t> run_win;
+    if (int rc = prefilter_windows_ex(e, h, view, ks, st, &rel, runs, &run_win, stats, err)) return rc;
+    segs.reserve(runs.size());
+    for (size_t r = 0; r < runs.size(); ++r) {
+      SegDesc s{};
+      s.ascii = 1u;
+      s.text_base = view.text_base + runs[r].first;
+      s.n = runs[r].second - runs[r].first;
+      s.avail = s.n;
+      s.hay_len = s.n;
+      s.byte_base = s.text_base;
+      s.w_begin = 0;
+      s.w_end = s.n;
+      s.pad = run_win[r];
+      segs.push_back(s);
+    }
+  } else {  // no pre-filter (or the reference's fallback to a full search, prefilter.rs:311-317)
+    for (uint64_t w = 0; w < n_windows; ++w) {
+      if (span[w].second <= span[w].first) continue;
+      SegDesc s = slice_view(h, span[w].first, span[w].second);
+      s.pad = (uint32_t)w;
+      segs.push_back(s);
+    }
+  }
+  if (segs.empty()) return FAC_OK;
+  uint64_t cap = 1u << 16;
+  for (;;) {  // raw records into a device buffer, grown and searched again if it was too small
+    DevMem raw(st);
+    if (int rc = raw.alloc(cap * sizeof(fac_match), err)) return rc;
+    MatchSink sink;
+    sink.dev = static_cast<fac_match*>(raw.p);
+    sink.dev_cap = cap;
+    if (int rc = launch_search_sink(e, h, segs, threshold, st, 0, sink, stats, err)) return rc;
+    if (sink.n > cap) {
+      cap = sink.n;
+      continue;
+    }
+    std::vector<fac_match> recs(sink.n);
+    if (sink.n) {
+      if (hipMemcpyAsync(recs.data(), sink.dev, sink.n * sizeof(fac_match), hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess) {
+        err = "hipMemcpyAsync of a stream batch's records failed";
+        return FAC_E_HIP;
+      }
+    }
+    windows_owned_host(e, recs, own, owned);
+    return FAC_OK;
+  }
+}
+
+}  // namespace fac
+
+namespace {
 }  // namespace
 
 extern "C" {
@@ -817,6 +908,43 @@ int fac_stream_window_staged_device(const fac_engine* engine, const fac_haystack
     if (rc) return fail(rc, err);
     return FAC_OK;
   }
+}
+
+int fac_stream_windows_staged_device(const fac_engine* engine, const fac_haystack* hay, const uint64_t* windows,
+                                     uint64_t n_windows, float threshold, int32_t prefilter, void* stream, void* device_out,
+                                     uint64_t device_cap, uint64_t* n_out, fac_stats* stats) {
+  if (!engine || !hay || !n_out || (!windows && n_windows) || (!device_out && device_cap))
+    return fail(FAC_E_INVALID, "NULL argument");
+  *n_out = 0;
+  const fac::Haystack& h = hay->h;
+  if (h.open_end || h.base) return fail(FAC_E_INVALID, "stream windows are cut from a whole staged haystack");
+  const fac::Engine& e = engine->e;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (hipSetDevice(e.device) != hipSuccess) return fail(FAC_E_HIP, "hipSetDevice failed");
+  std::vector<fac_match> owned;
+  std::string err;
+  int rc = fac::stream_windows_batch(e, h, windows, n_windows, threshold, prefilter != 0, st, owned, stats, err);
+  if (rc == FAC_E_UNSUPPORTED) {  // window by window (fac_stream_window_staged)
+    owned.clear();
+    for (uint64_t w = 0; w < n_windows; ++w) {
+      fac_match* part = nullptr;
+      uint64_t np = 0;
+      rc = fac_stream_window_staged(engine, hay, windows[4 * w], windows[4 * w + 1], windows[4 * w + 2], windows[4 * w + 3],
+                                    threshold, prefilter, stream, &part, &np, stats);
+      if (rc) return rc;
+      owned.insert(owned.end(), part, part + np);
+      fac_matches_free(part);
+    }
+  } else if (rc) {
+    return fail(rc, err);
+  }
+  *n_out = owned.size();
+  if (owned.size() > device_cap) return fail(FAC_E_OUTPUT_CAPACITY, "device output buffer too small (*n_out = records needed)");
+  if (!owned.empty() &&
+      (hipMemcpyAsync(device_out, owned.data(), owned.size() * sizeof(fac_match), hipMemcpyHostToDevice, st) != hipSuccess ||
+       hipStreamSynchronize(st) != hipSuccess))
+    return fail(FAC_E_HIP, "hipMemcpyAsync of the owned records failed");
+  return FAC_OK;
 }
 
 int fac_matches_apply(const fac_engine* engine, fac_match* matches, uint64_t n, int32_t order, int32_t overlap,

@@ -148,7 +148,7 @@ struct SegDesc {
   uint64_t byte_base;  // global byte offset of local byte 0 (added to every output offset)
   uint64_t w_begin, w_end;  // local start windows to search
   uint32_t ascii;      // 1: grapheme == byte (AsciiGraphemes), 0: Unicode graphemes
-  uint32_t pad;
+  uint32_t pad;        // tag copied into the records' pad bytes (24 bits; a batch's stream window), else 0
 };
 
 // one prefix-cache level: open-addressing table of key hashes -> entry -> snapshot
@@ -517,7 +517,9 @@ struct StreamCore {
   uint64_t overlap = 1;
   std::vector<uint8_t> buf;
   uint64_t base = 0, total = 0;
+  uint64_t carry = 0;  // bytes the last window left in the buffer (its text after the commit point)
   bool done = false;
+  StreamTask* pending = nullptr;  // windows cut but not yet dispatched (one batch)
   std::vector<fac_match> ready;
   std::vector<uint8_t> ready_text;  // matched bytes of `ready`, concatenated
   static constexpr uint32_t depth = 2;
@@ -547,6 +549,17 @@ int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int ove
 // and written to d_out; *n_owned their count (FAC_E_OUTPUT_CAPACITY if it exceeds cap)
 int window_owned_device(const Engine& e, fac_match* d_a, fac_match* d_b, uint64_t n, uint64_t byte_base, uint64_t commit,
                         uint64_t base, hipStream_t s, fac_match* d_out, uint64_t cap, uint64_t* n_owned, std::string& err);
+// A stream window of a batch: its text starts at staged byte byte_base, it owns the matches starting
+// before commit bytes into it, and byte_base maps to stream offset base.
+struct WinOwn {
+  uint64_t byte_base, commit, base;
+};
+void windows_owned_host(const Engine& e, std::vector<fac_match>& recs, const std::vector<WinOwn>& wins,
+                        std::vector<fac_match>& out);
+// api.cpp: a batch of stream windows (g_begin, g_end, commit_bytes, base) x n of a whole staged ASCII
+// haystack searched in one pass; FAC_E_UNSUPPORTED when the batch does not qualify (see there)
+int stream_windows_batch(const Engine& e, const Haystack& h, const uint64_t* wins, uint64_t n_windows, float threshold,
+                         bool prefilter, hipStream_t st, std::vector<fac_match>& owned, fac_stats* stats, std::string& err);
 // merged bitap windows (prefilter.rs:319-342) of a text view of a staged haystack (view.ascii:
 // bytes [text_base, text_base + n) of h.d_utf8; else graphemes [text_base, text_base + n)); windows
 // in the view's local grapheme coordinates
@@ -556,6 +569,14 @@ int diag_beam_select(const float* keys, const uint64_t* offs, uint64_t count, ui
 int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, const std::vector<uint32_t>& ks,
                       hipStream_t stream, std::vector<std::pair<uint64_t, uint64_t>>& windows, fac_stats* stats,
                       std::string& err);
+// the same for a batch of stream windows of the view (wins: [lo, hi) text positions, sorted, each
+// overlapping only its neighbours): one scan of the view, every window's merged bitap windows as if
+// its text were searched alone; run_win = each merged window's stream window. FAC_E_UNSUPPORTED
+// when the tables need the packed full scan.
+int prefilter_windows_ex(const Engine& e, const Haystack& h, const SegDesc& view, const std::vector<uint32_t>& ks,
+                         hipStream_t stream, const std::vector<std::pair<uint64_t, uint64_t>>* wins,
+                         std::vector<std::pair<uint64_t, uint64_t>>& windows, std::vector<uint32_t>* run_win,
+                         fac_stats* stats, std::string& err);
 // force_ascii: -1 decide from the bytes (search.rs:196), 0 Unicode graphemes, 1 ASCII bytes (a
 // shard of a haystack whose global is_ascii is already known)
 int stage_haystack(const Engine& e, const uint8_t* utf8, uint64_t len, Haystack& h, std::string& err,

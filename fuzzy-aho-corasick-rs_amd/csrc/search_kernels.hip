@@ -29,6 +29,7 @@
 #include <cstring>
 #include <functional>
 #include <type_traits>
+#include <tuple>
 #include <vector>
 
 #include "fac_internal.h"
@@ -1703,7 +1704,10 @@ __device__ __forceinline__ fac_match match_record(const SearchParams& P, const S
   m.substitutions = (ent.w >> 16) & 0xFFu;
   m.swaps = ent.w >> 24;
   m.edits = (uint8_t)edits_of(ent.w);
-  m.pad[0] = m.pad[1] = m.pad[2] = 0;
+  // the segment's tag (SegDesc::pad, 0 unless a batch of stream windows marks each record's window)
+  m.pad[0] = (uint8_t)S.pad;
+  m.pad[1] = (uint8_t)(S.pad >> 8);
+  m.pad[2] = (uint8_t)(S.pad >> 16);
   return m;
 }
 
@@ -3655,7 +3659,17 @@ struct QgramParams {
   const uint32_t* bits;    // QG_BITS_WORDS: screening bitmap of the grams (qgram_bit)
   const uint32_t* m16;     // every q-gram pattern m <= 16: [pattern][rows] 16-bit masks, m16_words words
   uint32_t m16_words;
+  // stream windows (a batch of stream.rs windows searched by one pass over their union, the view):
+  // window w is the text [wlo[w], whi[w]) of the view, sorted by wlo, overlapping only its neighbours;
+  // its coverage goes to cover (w even) or cover2 (w odd), so same-parity windows never touch.
+  // wtab[t >> QG_WSH]: the last window starting at or before that bucket's first position.
+  uint32_t nwin;
+  const uint64_t* wlo;
+  const uint64_t* whi;
+  const uint32_t* wtab;
+  uint32_t* cover2;
 };
+constexpr uint32_t QG_WSH = 16;  // window-table buckets of 64 Ki positions
 __host__ __device__ inline uint32_t qgram_key(uint32_t a, uint32_t b, uint32_t c, uint32_t d, bool q4) {
   return q4 ? (a | (b << 8) | (c << 16) | (d << 24)) : (a | (b << 8) | (c << 16) | 0xFF000000u);
 }
@@ -3890,18 +3904,21 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
 // W: the automaton word, uint32_t when every q-gram pattern has m <= 32 (half the 64-bit VALU work)
 // One candidate (qgram_verify_kernel). LM: every q-gram pattern has m <= 16 and their masks fit in
 // LDS (16-bit, pattern-major): the mask reads are LDS reads instead of L2 round trips.
+// The text is [wlo, whi) of the view (the whole view, or one stream window of a batch): the
+// recurrence starts from its initial state at wlo (prefilter.rs:415-418, a window's text begins
+// there) or m + k symbols before the first end it reports, and coverage bits go to `cover`.
 template <int KMAX, typename W, bool LM>
 __device__ __forceinline__ void verify_one(const QgramParams& Q, unsigned long long cd, uint2 en, const uint8_t* s_aid,
-                                           const uint16_t* s_m16) {
+                                           const uint16_t* s_m16, uint64_t wlo, uint64_t whi, uint32_t* cover) {
   const uint64_t t = cd >> 24;
   const uint32_t p = en.x >> 8, o = en.x & 0xFFu, m = en.y & 0xFFu, k = en.y >> 8;
   // ends the candidate allows, 1-based: [t + m - o - k, t + m - o + k], clipped to the text
   const int64_t lo = (int64_t)t + m - o - k, hi = (int64_t)t + m - o + k;
-  const uint64_t e_min = (uint64_t)max<int64_t>(1, lo);
-  const uint64_t e_max = (uint64_t)min<int64_t>((int64_t)Q.n, hi);
+  const uint64_t e_min = (uint64_t)max<int64_t>((int64_t)wlo + 1, lo);
+  const uint64_t e_max = (uint64_t)min<int64_t>((int64_t)whi, hi);
   if (e_min > e_max) return;
   const uint64_t warm = (uint64_t)m + k;
-  const uint64_t s0 = e_min - 1 > warm ? e_min - 1 - warm : 0;
+  const uint64_t s0 = e_min - 1 > wlo + warm ? e_min - 1 - warm : wlo;
   const uint64_t* mask = Q.pmask + (size_t)p * Q.rows;
   const uint16_t* mask16 = s_m16 + (size_t)p * Q.rows;  // LM: the pattern's masks in LDS
   const W top = (W)1 << (m - 1);
@@ -3967,13 +3984,13 @@ __device__ __forceinline__ void verify_one(const QgramParams& Q, unsigned long l
         if (u >= u_end && (hit & top)) {  // coverage [end - m - k, end), as bitap_kernel
           const uint64_t end = base + (uint64_t)u - sh + 1;
           const uint64_t span = (uint64_t)m + k;
-          const uint64_t ws = end > span ? end - span : 0;
+          const uint64_t ws = end > wlo + span ? end - span : wlo;
           for (uint64_t y = ws; y < end;) {
             const uint64_t w = y >> 5;
             const uint32_t l = (uint32_t)(y & 31);
             const uint32_t cnt = (uint32_t)min((uint64_t)(32 - l), end - y);
             const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << l;
-            atomicOr(Q.cover + w, bits);
+            atomicOr(cover + w, bits);
             y += cnt;
           }
         }
@@ -3982,7 +3999,9 @@ __device__ __forceinline__ void verify_one(const QgramParams& Q, unsigned long l
   }
 }
 
-template <int KMAX, typename W, bool LM>
+// WIN: a batch of stream windows -- each candidate is verified for the window(s) holding its gram
+// position (two in an overlap), with that window's bounds and coverage bitmap
+template <int KMAX, typename W, bool LM, bool WIN>
 __global__ __launch_bounds__(LM ? 512 : 256) void qgram_verify_kernel(QgramParams Q) {
   __shared__ uint8_t s_aid[128];  // bytes mode: byte -> symbol id
   extern __shared__ uint16_t s_m16[];  // LM: Q.m16_words 32-bit words of 16-bit masks
@@ -3999,7 +4018,20 @@ __global__ __launch_bounds__(LM ? 512 : 256) void qgram_verify_kernel(QgramParam
     const uint64_t cnt = r < Q.nreg ? (uint64_t)Q.rcnt[r] : min((uint64_t)*Q.n_ovf, Q.ovf_cap);
     for (uint64_t x = threadIdx.x; x < cnt; x += blockDim.x) {
       const unsigned long long cd = base[x];
-      verify_one<KMAX, W, LM>(Q, cd, Q.ent[cd & 0xFFFFFFu], s_aid, s_m16);
+      if constexpr (!WIN) {
+        verify_one<KMAX, W, LM>(Q, cd, Q.ent[cd & 0xFFFFFFu], s_aid, s_m16, 0, Q.n, Q.cover);
+      } else {
+        const uint64_t t = cd >> 24;
+        uint32_t w = Q.wtab[t >> QG_WSH];
+        while (w + 1 < Q.nwin && Q.wlo[w + 1] <= t) ++w;
+        const uint2 en = Q.ent[cd & 0xFFFFFFu];
+        for (uint32_t d = 0; d < 2; ++d) {  // the window holding t, then its predecessor if they overlap at t
+          if (d > w) break;
+          const uint32_t ww = w - d;
+          const uint64_t lo = Q.wlo[ww], hi = Q.whi[ww];
+          if (t >= lo && t < hi) verify_one<KMAX, W, LM>(Q, cd, en, s_aid, s_m16, lo, hi, (ww & 1u) ? Q.cover2 : Q.cover);
+        }
+      }
     }
   }
 }
@@ -5699,10 +5731,50 @@ int pf_tables(const Engine& e, const std::vector<uint32_t>& ks, bool want_bytes,
   return FAC_OK;
 }
 
+// qgram_verify_kernel for the tables' edit budget and mask layout: LDS masks in persistent blocks (two
+// per CU), else global masks, 32- or 64-bit automaton words
+template <bool WIN>
+void launch_qverify(const PfTables& T, const QgramParams& Q, dim3 vg, hipStream_t stream) {
+  const uint32_t kq = T.kq;
+  if (T.m16) {
+    const size_t lds = (size_t)T.m16_words * 4;
+    if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t, true, WIN>), vg, dim3(512), lds, stream, Q);
+    else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t, true, WIN>), vg, dim3(512), lds, stream, Q);
+    else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t, true, WIN>), vg, dim3(512), lds, stream, Q);
+    else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint32_t, true, WIN>), vg, dim3(512), lds, stream, Q);
+    else hipLaunchKernelGGL((qgram_verify_kernel<24, uint32_t, true, WIN>), vg, dim3(512), lds, stream, Q);
+  } else if (T.mq <= 32) {
+    if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t, false, WIN>), vg, dim3(256), 0, stream, Q);
+    else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t, false, WIN>), vg, dim3(256), 0, stream, Q);
+    else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t, false, WIN>), vg, dim3(256), 0, stream, Q);
+    else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint32_t, false, WIN>), vg, dim3(256), 0, stream, Q);
+    else hipLaunchKernelGGL((qgram_verify_kernel<24, uint32_t, false, WIN>), vg, dim3(256), 0, stream, Q);
+  } else {
+    if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint64_t, false, WIN>), vg, dim3(256), 0, stream, Q);
+    else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint64_t, false, WIN>), vg, dim3(256), 0, stream, Q);
+    else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint64_t, false, WIN>), vg, dim3(256), 0, stream, Q);
+    else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint64_t, false, WIN>), vg, dim3(256), 0, stream, Q);
+    else hipLaunchKernelGGL((qgram_verify_kernel<24, uint64_t, false, WIN>), vg, dim3(256), 0, stream, Q);
+  }
+}
+
 int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, const std::vector<uint32_t>& ks,
                       hipStream_t stream, std::vector<std::pair<uint64_t, uint64_t>>& windows, fac_stats* stats,
                       std::string& err) {
+  return prefilter_windows_ex(e, h, view, ks, stream, nullptr, windows, nullptr, stats, err);
+}
+
+// wins (optional): a batch of stream windows, [lo, hi) text positions of the view sorted by lo,
+// each overlapping only its neighbours and not adjacent to the next-but-one (lo[w + 2] > hi[w]).
+// Every window's bitap windows are its own -- the automaton starts at its lo, its coverage stays in
+// it -- from one scan of the view; run_win receives each merged window's stream window. Returns
+// FAC_E_UNSUPPORTED when some pattern needs the packed full scan (not window-aware).
+int prefilter_windows_ex(const Engine& e, const Haystack& h, const SegDesc& view, const std::vector<uint32_t>& ks,
+                         hipStream_t stream, const std::vector<std::pair<uint64_t, uint64_t>>* wins,
+                         std::vector<std::pair<uint64_t, uint64_t>>& windows, std::vector<uint32_t>* run_win,
+                         fac_stats* stats, std::string& err) {
   windows.clear();
+  if (run_win) run_win->clear();
   HIP_TRY(hipSetDevice(e.device));
   if (!stream) stream = e.stream;
   const uint64_t n = view.n;
@@ -5714,7 +5786,9 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
   const PfTables* T = nullptr;
   if (int rc = pf_tables(e, ks, want_bytes, T, err)) return rc;
   const uint32_t nw = T->nw;
-  PoolBuf d_ids, d_cover, d_runs, d_cnt;
+  const bool win = wins && !wins->empty();
+  if (win && (nw != 0 || !T->q)) return FAC_E_UNSUPPORTED;  // the packed full scan has no window bounds
+  PoolBuf d_ids, d_cover, d_runs, d_cnt, d_cover2, d_wlo, d_whi, d_wtab;
   if (!T->bytes) {  // the text's symbol ids (prefilter.rs:253-260)
     HIP_TRY(d_ids.alloc(n + 80, stream));  // padded: the scan's 16-byte loads and next word, verify's 64-symbol passes
     if (view.ascii) {  // transcode, ASCII text (prefilter.rs:253-258): one byte per grapheme
@@ -5730,6 +5804,31 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
   const uint64_t n_words = (n + 31) / 32;
   HIP_TRY(d_cover.alloc(n_words * 4, stream));
   HIP_TRY(hipMemsetAsync(d_cover.p, 0, n_words * 4, stream));
+  std::vector<uint64_t> wlo, whi;
+  std::vector<uint32_t> wtab;
+  if (win) {  // the batch's window bounds and bucket table (QgramParams::wtab)
+    const size_t nwin = wins->size();
+    wlo.resize(nwin);
+    whi.resize(nwin);
+    for (size_t w = 0; w < nwin; ++w) {
+      wlo[w] = (*wins)[w].first;
+      whi[w] = std::min<uint64_t>((*wins)[w].second, n);
+    }
+    wtab.resize((size_t)((n >> QG_WSH) + 1));
+    uint32_t w = 0;
+    for (size_t b = 0; b < wtab.size(); ++b) {
+      while (w + 1 < nwin && wlo[w + 1] <= ((uint64_t)b << QG_WSH)) ++w;
+      wtab[b] = w;
+    }
+    HIP_TRY(d_cover2.alloc(n_words * 4, stream));
+    HIP_TRY(hipMemsetAsync(d_cover2.p, 0, n_words * 4, stream));
+    HIP_TRY(d_wlo.alloc(nwin * 8, stream));
+    HIP_TRY(d_whi.alloc(nwin * 8, stream));
+    HIP_TRY(d_wtab.alloc(wtab.size() * 4, stream));
+    HIP_TRY(hipMemcpyAsync(d_wlo.p, wlo.data(), nwin * 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_whi.p, whi.data(), nwin * 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d_wtab.p, wtab.data(), wtab.size() * 4, hipMemcpyHostToDevice, stream));
+  }
   Events ev;
   HIP_TRY(hipEventCreate(&ev.a));
   HIP_TRY(hipEventCreate(&ev.b));
@@ -5794,6 +5893,13 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
     Q.bits = static_cast<const uint32_t*>(T->qbits);
     Q.m16 = static_cast<const uint32_t*>(T->m16);
     Q.m16_words = T->m16_words;
+    if (win) {
+      Q.nwin = (uint32_t)wlo.size();
+      Q.wlo = static_cast<const uint64_t*>(d_wlo.p);
+      Q.whi = static_cast<const uint64_t*>(d_whi.p);
+      Q.wtab = static_cast<const uint32_t*>(d_wtab.p);
+      Q.cover2 = static_cast<uint32_t*>(d_cover2.p);
+    }
     int cus = 256;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
     // two full resident rounds of scan blocks (2 per CU at 56 KB of LDS): the scan strides over the
@@ -5843,61 +5949,67 @@ int prefilter_windows(const Engine& e, const Haystack& h, const SegDesc& view, c
                    (unsigned long long)mx, Q.use3, Q.use4);
     }
     {
-      const uint32_t kq = T->kq;
-      if (T->m16) {  // LDS masks: persistent blocks, two per CU
-        const dim3 vg((uint32_t)std::min<uint64_t>(sgrid + 1, (uint64_t)cus * 2));
-        const size_t lds = (size_t)T->m16_words * 4;
-        if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t, true>), vg, dim3(512), lds, stream, Q);
-        else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t, true>), vg, dim3(512), lds, stream, Q);
-        else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t, true>), vg, dim3(512), lds, stream, Q);
-        else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint32_t, true>), vg, dim3(512), lds, stream, Q);
-        else hipLaunchKernelGGL((qgram_verify_kernel<24, uint32_t, true>), vg, dim3(512), lds, stream, Q);
-      } else {
-        const dim3 vg((uint32_t)std::min<uint64_t>(sgrid + 1, (uint64_t)cus * 8));
-        if (T->mq <= 32) {
-          if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint32_t, false>), vg, dim3(256), 0, stream, Q);
-          else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint32_t, false>), vg, dim3(256), 0, stream, Q);
-          else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint32_t, false>), vg, dim3(256), 0, stream, Q);
-          else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint32_t, false>), vg, dim3(256), 0, stream, Q);
-          else hipLaunchKernelGGL((qgram_verify_kernel<24, uint32_t, false>), vg, dim3(256), 0, stream, Q);
-        } else {
-          if (kq <= 1) hipLaunchKernelGGL((qgram_verify_kernel<1, uint64_t, false>), vg, dim3(256), 0, stream, Q);
-          else if (kq <= 2) hipLaunchKernelGGL((qgram_verify_kernel<2, uint64_t, false>), vg, dim3(256), 0, stream, Q);
-          else if (kq <= 4) hipLaunchKernelGGL((qgram_verify_kernel<4, uint64_t, false>), vg, dim3(256), 0, stream, Q);
-          else if (kq <= 8) hipLaunchKernelGGL((qgram_verify_kernel<8, uint64_t, false>), vg, dim3(256), 0, stream, Q);
-          else hipLaunchKernelGGL((qgram_verify_kernel<24, uint64_t, false>), vg, dim3(256), 0, stream, Q);
-        }
-      }
+      const dim3 vg((uint32_t)std::min<uint64_t>(sgrid + 1, (uint64_t)cus * (T->m16 ? 2 : 8)));
+      if (Q.nwin) launch_qverify<true>(*T, Q, vg, stream);
+      else launch_qverify<false>(*T, Q, vg, stream);
       HIP_TRY(hipGetLastError());
     }
     if (diag_env("FAC_RC_DEBUG"))
       std::fprintf(stderr, "FAC_QGRAM patterns=%zu/%zu grams=%zu keys=%zu candidates=%llu full-scan words=%u bytes=%d\n",
                    T->n_qpat, e.bp_m.size(), T->n_grams, T->n_keys, nc, nw, (int)T->bytes);
   }
-  uint64_t cap = 1 << 16;
+  // maximal runs of each bitmap (with windows: cover holds the even windows', cover2 the odd ones';
+  // same-parity windows are not adjacent, so no run spans two of them)
+  std::vector<uint32_t> par[2];  // the windows of each parity, ascending lo
+  if (win)
+    for (uint32_t w = 0; w < (uint32_t)wlo.size(); ++w) par[w & 1].push_back(w);
+  std::vector<std::tuple<uint64_t, uint64_t, uint32_t>> runs;  // (start, end, stream window)
   HIP_TRY(d_cnt.alloc(8, stream));
-  for (;;) {
-    HIP_TRY(d_runs.alloc(cap * 16, stream));
-    HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 8, stream));
-    hipLaunchKernelGGL(runs_kernel, dim3((uint32_t)((n_words + 255) / 256)), dim3(256), 0, stream,
-                       static_cast<const uint32_t*>(d_cover.p), n_words, n, static_cast<unsigned long long*>(d_runs.p),
-                       static_cast<unsigned long long*>(d_cnt.p), cap);
-    HIP_TRY(hipGetLastError());
-    unsigned long long c = 0;
-    HIP_TRY(hipMemcpyAsync(&c, d_cnt.p, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    if (c > cap) {
-      cap = c;
-      continue;
+  for (int pass = 0; pass < (win ? 2 : 1); ++pass) {
+    const uint32_t* cov = static_cast<const uint32_t*>(pass ? d_cover2.p : d_cover.p);
+    uint64_t cap = 1 << 16;
+    for (;;) {
+      HIP_TRY(d_runs.alloc(cap * 16, stream));
+      HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 8, stream));
+      hipLaunchKernelGGL(runs_kernel, dim3((uint32_t)((n_words + 255) / 256)), dim3(256), 0, stream, cov, n_words, n,
+                         static_cast<unsigned long long*>(d_runs.p), static_cast<unsigned long long*>(d_cnt.p), cap);
+      HIP_TRY(hipGetLastError());
+      unsigned long long c = 0;
+      HIP_TRY(hipMemcpyAsync(&c, d_cnt.p, 8, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (c > cap) {
+        cap = c;
+        continue;
+      }
+      std::vector<unsigned long long> buf(2 * c);
+      if (c) HIP_TRY(hipMemcpyAsync(buf.data(), d_runs.p, c * 16, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipEventRecord(ev.b, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      for (uint64_t i = 0; i < c; ++i) {
+        uint32_t w = 0xFFFFFFFFu;
+        if (win) {  // the window of this parity whose [lo, hi) holds the run
+          const auto& v = par[pass];
+          auto it = std::upper_bound(v.begin(), v.end(), (uint64_t)buf[2 * i],
+                                     [&](uint64_t x, uint32_t ww) { return x < wlo[ww]; });
+          if (it != v.begin() && buf[2 * i] < whi[*(it - 1)]) w = *(it - 1);
+          if (w == 0xFFFFFFFFu) {
+            err = "internal: a pre-filter run outside every stream window";
+            return FAC_E_INTERNAL;
+          }
+        }
+        runs.emplace_back(buf[2 * i], buf[2 * i + 1], w);
+      }
+      break;
     }
-    std::vector<unsigned long long> buf(2 * c);
-    if (c) HIP_TRY(hipMemcpyAsync(buf.data(), d_runs.p, c * 16, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipEventRecord(ev.b, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    windows.resize(c);
-    for (uint64_t i = 0; i < c; ++i) windows[i] = {buf[2 * i], buf[2 * i + 1]};
-    std::sort(windows.begin(), windows.end());
-    break;
+  }
+  std::sort(runs.begin(), runs.end(), [](const auto& x, const auto& y) {
+    return std::get<2>(x) != std::get<2>(y) ? std::get<2>(x) < std::get<2>(y) : std::get<0>(x) < std::get<0>(y);
+  });
+  windows.resize(runs.size());
+  if (run_win) run_win->resize(runs.size());
+  for (size_t r = 0; r < runs.size(); ++r) {
+    windows[r] = {std::get<0>(runs[r]), std::get<1>(runs[r])};
+    if (run_win) (*run_win)[r] = std::get<2>(runs[r]);
   }
   if (stats) {
     float ms = 0.f;

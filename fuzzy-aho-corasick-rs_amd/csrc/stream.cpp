@@ -8,12 +8,14 @@
 // with too few graphemes the window grows and more input is awaited. The buffer then drops the
 // committed prefix.
 //
-// Each cut window is handed to one of `depth` (2) worker threads, window k to worker k % depth. A
-// worker owns a HIP stream and a device scratch set: it stages the window (H2D + device
-// segmentation + folding), searches it as its own haystack, ranks it sorted().non_overlapping()
-// and keeps the matches it owns (stream.rs:262-297), so window k + 1's copies and kernels overlap
-// window k's (double buffering) while the host cuts window k + 2. Finished windows are handed out
-// strictly in window order.
+// Consecutive windows are collected into batches of about 32 MiB of text, and each batch is handed
+// to one of `depth` (2) worker threads, batch k to worker k % depth. A worker owns a HIP stream and
+// a device scratch set. An all-ASCII batch is staged once (H2D) and its windows searched in one
+// launch, each as its own text (stream_windows_batch); a batch with other text stages and searches
+// its windows one by one (H2D + device segmentation + folding each). Every window is ranked
+// sorted().non_overlapping() and keeps the matches it owns (stream.rs:262-297). Batch k + 1's
+// copies and kernels overlap batch k's (double buffering) while the host cuts the windows of batch
+// k + 2. Finished batches are handed out strictly in window order.
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -29,10 +31,16 @@
 
 namespace fac {
 
+// A batch of consecutive windows: text holds stream bytes [base, base + text.size()), window w is
+// text[off, off + len) and owns the matches starting before off + commit.
+struct StreamWin {
+  uint64_t off, len, commit;
+};
 struct StreamTask {
-  std::vector<uint8_t> text;  // the window's text (valid UTF-8 prefix of the buffer)
-  uint64_t base = 0, commit = 0;
-  std::vector<fac_match> res;  // owned matches, absolute offsets
+  std::vector<uint8_t> text;
+  uint64_t base = 0;
+  std::vector<StreamWin> wins;
+  std::vector<fac_match> res;  // owned matches of every window, in window order, absolute offsets
   std::vector<uint8_t> res_text;
   int rc = FAC_OK;
   std::string err;
@@ -54,11 +62,12 @@ namespace {
 std::mutex g_done_mu;  // guards StreamTask::done across workers and the feeding thread
 std::condition_variable g_done_cv;
 
-// Search one window and keep the matches it owns (stream.rs:262-297).
-void run_window_task(const StreamCore& s, StreamWorker& w, StreamTask& t) {
+// Search one window (text[off, off + len) of the task) and keep the matches it owns (stream.rs:262-297).
+int search_one_window(const StreamCore& s, StreamWorker& w, const StreamTask& t, const StreamWin& win,
+                      std::vector<fac_match>& owned, std::string& err) {
   Haystack h;
-  t.rc = stage_haystack(*s.e, t.text.data(), t.text.size(), h, t.err, -1, w.stream);
-  if (!t.rc) {
+  int rc = stage_haystack(*s.e, t.text.data() + win.off, win.len, h, err, -1, w.stream);
+  if (!rc) {
     SegDesc seg{};
     seg.text_base = 0;
     seg.n = h.n;
@@ -69,19 +78,60 @@ void run_window_task(const StreamCore& s, StreamWorker& w, StreamTask& t) {
     seg.w_end = h.n;
     seg.ascii = h.ascii ? 1u : 0u;
     std::vector<fac_match> res;
-    t.rc = launch_search(*s.e, h, {seg}, s.threshold, w.stream, res, nullptr, t.err);
-    if (!t.rc) t.rc = apply_matches(*s.e, res, /*Default*/ 1, /*NonOverlapping*/ 1, nullptr, t.err);
-    if (!t.rc)
+    rc = launch_search(*s.e, h, {seg}, s.threshold, w.stream, res, nullptr, err);
+    if (!rc) rc = apply_matches(*s.e, res, /*Default*/ 1, /*NonOverlapping*/ 1, nullptr, err);
+    if (!rc)
       for (const fac_match& m : res) {
-        if (m.start >= t.commit) continue;
+        if (m.start >= win.commit) continue;
         fac_match a = m;
-        a.start += t.base;
-        a.end += t.base;
-        t.res.push_back(a);
-        t.res_text.insert(t.res_text.end(), t.text.begin() + (ptrdiff_t)m.start, t.text.begin() + (ptrdiff_t)m.end);
+        a.start += t.base + win.off;
+        a.end += t.base + win.off;
+        owned.push_back(a);
       }
   }
   free_haystack(h);
+  return rc;
+}
+
+// Search a batch of windows. An all-ASCII batch is staged once and searched as one launch over its
+// windows (stream_windows_batch: each window its own text, ranked and cut per window); otherwise each
+// window is staged and searched alone (its grapheme segmentation depends on where its text starts
+// and ends).
+void run_window_task(const StreamCore& s, StreamWorker& w, StreamTask& t) {
+  std::vector<fac_match> owned;
+  bool batched = false;
+  if (t.wins.size() > 1 && ascii_only(t.text.data(), t.text.size())) {
+    Haystack h;
+    t.rc = stage_haystack(*s.e, t.text.data(), t.text.size(), h, t.err, 1, w.stream);
+    if (!t.rc) {
+      std::vector<uint64_t> wins(4 * t.wins.size());
+      for (size_t i = 0; i < t.wins.size(); ++i) {
+        wins[4 * i] = t.wins[i].off;
+        wins[4 * i + 1] = t.wins[i].off + t.wins[i].len;
+        wins[4 * i + 2] = t.wins[i].commit;
+        wins[4 * i + 3] = t.base + t.wins[i].off;
+      }
+      const int rc = stream_windows_batch(*s.e, h, wins.data(), t.wins.size(), s.threshold, false, w.stream, owned,
+                                          nullptr, t.err);
+      if (rc != FAC_E_UNSUPPORTED) {
+        t.rc = rc;
+        batched = true;
+      }
+    }
+    free_haystack(h);
+    if (t.rc) batched = true;  // a staging failure is the task's error
+  }
+  if (!batched) {
+    owned.clear();
+    for (const StreamWin& win : t.wins)
+      if ((t.rc = search_one_window(s, w, t, win, owned, t.err))) break;
+  }
+  if (!t.rc)
+    for (const fac_match& m : owned) {
+      t.res.push_back(m);
+      t.res_text.insert(t.res_text.end(), t.text.begin() + (ptrdiff_t)(m.start - t.base),
+                        t.text.begin() + (ptrdiff_t)(m.end - t.base));
+    }
   std::vector<uint8_t>().swap(t.text);
 }
 
@@ -125,7 +175,7 @@ int collect(StreamCore& s, bool all, std::string& err) {
       g_done_cv.wait(lk, [&] { return t->done; });
     }
     s.inflight.erase(s.inflight.begin());
-    s.handed = t->base + t->commit;
+    if (!t->wins.empty()) s.handed = t->base + t->wins.back().off + t->wins.back().commit;
     if (t->rc && !s.failed) {
       s.failed = t->rc;
       s.fail_msg = t->err;
@@ -164,34 +214,59 @@ int dispatch(StreamCore& s, StreamTask* t, std::string& err) {
   return FAC_OK;
 }
 
-// Cut windows while the buffer allows (next_window, stream.rs:102-158).
+// Cut windows while the buffer allows (next_window, stream.rs:102-158). The crate's reader reads
+// 64 KiB pieces until it holds >= window bytes, so a window's text is the carry left by the previous
+// window plus whole 64 KiB reads (the last one partial at the end of the input); fed in larger pieces,
+// the buffer is cut the same way. Consecutive windows join the pending batch, dispatched once it holds
+// kBatchBytes of text or the input ends.
+constexpr uint64_t kRead = 64 * 1024, kBatchBytes = 32ull << 20;
+
+int flush_batch(StreamCore& s, std::string& err) {
+  if (!s.pending) return FAC_OK;
+  StreamTask* t = s.pending;
+  s.pending = nullptr;
+  return dispatch(s, t, err);
+}
+
 int pump(StreamCore& s, bool eof, std::string& err) {
-  while (!s.done && (eof || s.buf.size() >= s.window)) {
-    const uint64_t valid = utf8_valid_prefix(s.buf.data(), s.buf.size());
-    const bool last = s.buf.size() < s.window;  // reached only at end of input
+  while (!s.done) {
+    const uint64_t avail = s.buf.size();
+    const uint64_t want = s.carry >= s.window ? s.carry : s.carry + (s.window - s.carry + kRead - 1) / kRead * kRead;
+    if (!eof && avail < want) break;  // the reader would block for more input
+    const uint64_t len = std::min(avail, want);
+    const uint64_t valid = utf8_valid_prefix(s.buf.data(), len);
+    const bool last = len < s.window;  // reached only at end of input
     uint64_t commit = valid;
     if (!last) {
       // byte start of the overlap-th grapheme from the end; none or 0: grow and read more
       uint64_t off = 0;
       if (!nth_grapheme_from_end(s.buf.data(), valid, s.overlap, off) || off == 0) {
         s.window += std::max<uint64_t>(s.window, 64 * 1024);
-        if (eof) continue;  // input ended: the next round is the last window
-        return FAC_OK;
+        continue;  // (at end of input the next round is the last window)
       }
       commit = off;
     }
-    StreamTask* t = new StreamTask();
-    t->text.assign(s.buf.begin(), s.buf.begin() + (ptrdiff_t)valid);
-    t->base = s.base;
-    t->commit = commit;
-    if (int rc = dispatch(s, t, err)) return rc;
+    if (!s.pending) {
+      s.pending = new StreamTask();
+      s.pending->base = s.base;
+    }
+    StreamTask* t = s.pending;
+    const uint64_t off = s.base - t->base;  // the window's first byte in the batch text
+    if (off + valid > t->text.size())
+      t->text.insert(t->text.end(), s.buf.begin() + (ptrdiff_t)(t->text.size() - off), s.buf.begin() + (ptrdiff_t)valid);
+    t->wins.push_back(StreamWin{off, valid, commit});
     if (last) {
       s.done = true;
       break;
     }
     s.buf.erase(s.buf.begin(), s.buf.begin() + (ptrdiff_t)commit);
     s.base += commit;
+    s.carry = len - commit;
+    if (t->text.size() >= kBatchBytes)
+      if (int rc = flush_batch(s, err)) return rc;
   }
+  if (eof || s.done)
+    if (int rc = flush_batch(s, err)) return rc;
   return collect(s, eof, err);
 }
 
@@ -224,7 +299,9 @@ StreamCore* stream_open(const Engine& e, float threshold, uint64_t window) {
 
 void stream_close(StreamCore* s) {
   std::string err;
-  (void)collect(*s, true, err);  // windows still in flight (an abandoned stream)
+  delete s->pending;  // windows cut but never dispatched (an abandoned stream)
+  s->pending = nullptr;
+  (void)collect(*s, true, err);  // windows still in flight
   for (StreamWorker* w : s->workers) {
     if (!w) continue;
     {

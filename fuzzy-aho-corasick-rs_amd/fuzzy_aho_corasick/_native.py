@@ -149,6 +149,9 @@ SIGNATURES = {
                                                        ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float, ctypes.c_int32,
                                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, _u64p,
                                                        _P(fac_stats)]),
+    "fac_stream_windows_staged_device": (ctypes.c_int, [_engine_p, _hay_p, _u64p, ctypes.c_uint64, ctypes.c_float,
+                                                        ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                        _u64p, _P(fac_stats)]),
     "fac_search_staged_prefiltered": (ctypes.c_int, [_engine_p, _hay_p, ctypes.c_float, ctypes.c_void_p,
                                                      _P(_P(fac_match)), _u64p, _P(fac_stats)]),
     "fac_matches_apply": (ctypes.c_int, [_engine_p, _P(fac_match), ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,

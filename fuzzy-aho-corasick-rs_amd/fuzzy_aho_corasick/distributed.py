@@ -37,11 +37,14 @@ def shard_bounds(n_windows: int, world: int, rank: int) -> Tuple[int, int]:
 
 
 def stream_share_windows(total: int, block: int, share_index: int, overlap: int,
-                         n_shares: int = 8) -> List[Tuple[int, int, int, int]]:
+                         n_shares: int = 8, window: int = None) -> List[Tuple[int, int, int, int]]:
     """C5's cut of a stream of `total` bytes = total / block repeats of one `block`-byte block (SURVEY
     §8(d)): the stream is split into `n_shares` contiguous shares (one per GPU of the 8-GPU node;
     GPU g takes share g, so a run on fewer GPUs keeps each GPU's work: weak scaling), and the share
-    into windows cut at block and share boundaries. A window is searched exactly like stream.rs window_matches (:262-297): its text
+    into windows cut at block and share boundaries and every `window` bytes (None: blocks only; the
+    crate's DEFAULT_WINDOW is 256 KiB, stream.rs:65 -- its WindowReader fed 64 KiB reads cuts windows
+    of window + overlap bytes that commit `window` bytes each, :102-158, which is this cut shifted by
+    the overlap). A window is searched exactly like stream.rs window_matches (:262-297): its text
     is its bytes plus `overlap` following bytes (max_match_graphemes() + 1 of an ASCII stream,
     :256-258, clipped at the stream's end), and it owns the matches starting in its bytes. The block
     is resident once as block || block[:overlap], so every window is a contiguous slice of it:
@@ -53,6 +56,8 @@ def stream_share_windows(total: int, block: int, share_index: int, overlap: int,
     c = lo
     while c < hi:
         c1 = min(hi, (c // block + 1) * block)
+        if window:
+            c1 = min(c1, c + window)
         o = c % block
         end = min(total, c1 + overlap)
         out.append((o, o + (end - c), c1 - c, c))

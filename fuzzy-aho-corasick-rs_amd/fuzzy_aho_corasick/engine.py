@@ -383,7 +383,10 @@ def prefilter_windows(engine: "FuzzyAhoCorasick", haystack: str, threshold: floa
     return [(buf[2 * i], buf[2 * i + 1]) for i in range(n)]
 
 
-READ_CHUNK = 64 * 1024  # WindowReader's read() size (stream.rs:94)
+# read() size of the streaming methods. The library cuts windows as the crate's WindowReader does with
+# its 64 KiB reads (stream.rs:94, 102-158) whatever the feed size, so a larger read only means fewer
+# calls across the C ABI (and lets a feed fill whole batches of windows).
+READ_CHUNK = 4 << 20
 
 
 class StreamMatch:
@@ -591,6 +594,33 @@ class StagedHaystack:
             rc = _native.lib.fac_stream_window_staged_device(
                 self.engine._h, self._h, g_begin, g_end, commit_bytes, base, f32(threshold), int(prefilter),
                 ctypes.c_void_p(stream or 0), ctypes.c_void_p(ptr), max(0, cap), ctypes.byref(n), ctypes.byref(st))
+            if rc == _native.FAC_E_OUTPUT_CAPACITY:
+                grown = torch.empty(max(2 * out.numel(), (offset + n.value) * _native.REC_BYTES * 2),
+                                    dtype=torch.uint8, device=out.device)
+                grown[: offset * _native.REC_BYTES].copy_(out[: offset * _native.REC_BYTES])
+                out = grown
+                continue
+            if rc:
+                _raise(rc)
+            return out, n.value, st
+
+    def stream_windows_device(self, windows, threshold: float, prefilter: bool, out, offset: int = 0, stream=None):
+        """fac_stream_windows_staged_device: a batch of stream windows, `windows` = [(g_begin, g_end,
+        commit_bytes, base), ...] in stream order, searched together (one pre-filter pass and one search
+        launch on an ASCII haystack); their owned records, in window order, written in HBM to `out`
+        from record `offset` on (grown like stream_window_device). Returns (out, owned count, fac_stats)."""
+        import numpy as np
+        import torch
+        arr = np.ascontiguousarray(np.asarray(windows, dtype=np.uint64).reshape(-1, 4))
+        wp = arr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        n = ctypes.c_uint64()
+        st = _native.fac_stats()
+        while True:
+            cap = out.numel() // _native.REC_BYTES - offset
+            ptr = out.data_ptr() + offset * _native.REC_BYTES
+            rc = _native.lib.fac_stream_windows_staged_device(
+                self.engine._h, self._h, wp, len(arr), f32(threshold), int(prefilter), ctypes.c_void_p(stream or 0),
+                ctypes.c_void_p(ptr), max(0, cap), ctypes.byref(n), ctypes.byref(st))
             if rc == _native.FAC_E_OUTPUT_CAPACITY:
                 grown = torch.empty(max(2 * out.numel(), (offset + n.value) * _native.REC_BYTES * 2),
                                     dtype=torch.uint8, device=out.device)

@@ -277,6 +277,18 @@ int fac_stream_window_staged_device(const fac_engine* engine, const fac_haystack
                                     uint64_t commit_bytes, uint64_t base, float threshold, int32_t prefilter, void* stream,
                                     void* device_out, uint64_t device_cap, uint64_t* n_out, fac_stats* stats);
 
+/* A batch of streaming windows (stream.rs:262-297 window_matches for each; the crate cuts them
+ * DEFAULT_WINDOW = 256 KiB apart, stream.rs:65): windows[4 w .. 4 w + 3] = (g_begin, g_end,
+ * commit_bytes, base) of window w, ascending g_begin, each overlapping only its neighbours. Every
+ * window is searched as its own text exactly like fac_stream_window_staged_device; on an ASCII
+ * haystack the batch is one pre-filter pass over the windows' union (each window's bitap automaton
+ * starting at its first byte) and one search launch over every window's segments, then per-window
+ * ranking and commit cut. The owned records of all windows go to device_out in window order;
+ * *n_out = their count (FAC_E_OUTPUT_CAPACITY when it exceeds device_cap). */
+int fac_stream_windows_staged_device(const fac_engine* engine, const fac_haystack* hay, const uint64_t* windows,
+                                     uint64_t n_windows, float threshold, int32_t prefilter, void* stream, void* device_out,
+                                     uint64_t device_cap, uint64_t* n_out, fac_stats* stats);
+
 /* Prefiltered::raw on a staged haystack (prefilter.rs:146-155, 304-374): the bitap scan and the
  * window merge run on the device-resident text, each merged window is re-searched as its own
  * sub-haystack, results are best-per-(start, end, pattern) and sorted. Falls back to the full

@@ -193,6 +193,82 @@ def test_stream_windows_on_device_equal_whole_input(prefilter):
                               prefilter)[0] for c in range(0, len(hay), win)])], win
 
 
+def _window_cuts(n, win, overlap):
+    return [(c, min(n, min(n, c + win) + overlap), min(n, c + win) - c, c) for c in range(0, n, win)]
+
+
+@pytest.mark.parametrize("prefilter", [True, False])
+def test_stream_window_batches_equal_single_windows(prefilter):
+    """fac_stream_windows_staged_device (bench.py C5 at the crate's 256 KiB windows, stream.rs:65):
+    a batch of stream windows searched in one pre-filter pass over their union and one search launch
+    gives every window exactly what fac_stream_window_staged_device gives it alone -- records, order
+    and fields -- including matches planted across window boundaries (in the overlaps, where two
+    windows verify the same candidate with different automaton starts) and windows at unaligned byte
+    offsets; and the union over the windows equals the whole input's sorted().non_overlapping()
+    search by the oracle."""
+    import torch
+    from fuzzy_aho_corasick._native import MATCH_DTYPE
+    pats, hay = _sparse_c5(1 << 20, 3 << 10)
+    b = B().fuzzy(L().edits(1)).device(0)
+    eng = b.build(pats)
+    overlap = eng.max_match_graphemes() + 1
+    # plant needles straddling the cuts of the 8 KiB windows
+    ba = bytearray(hay)
+    win = 8 << 10
+    for i, c in enumerate(range(win, len(ba) - 64, win)):
+        p = pats[i % len(pats)].encode()
+        at = c - len(p) // 2 - (i % 5)
+        ba[at - 1: at + len(p) + 1] = b" " + p + b" "
+    hay = bytes(ba)
+    st = StagedHaystack(eng, hay)
+    orc = OracleEngine(b, pats)
+    orc = orc.with_prefilter() if prefilter else orc
+    opts = O().threshold(0.85).sorted().non_overlapping()
+    want = []  # the oracle, window by window (window_matches: sorted().non_overlapping(), start < commit)
+    for (g0, g1, commit, base) in _window_cuts(len(hay), win, overlap):
+        want += [(base + m.start, base + m.end, m.pattern_index, m.sim_bits())
+                 for m in orc.search(hay[g0:g1].decode(), opts) if m.start < commit]
+    want.sort()
+    assert len(want) > 300
+    for w in (win, 100_003, 256 << 10):
+        cuts = _window_cuts(len(hay), w, overlap)
+        single = [st.stream_window(*c, 0.85, prefilter)[0] for c in cuts]
+        single = np.concatenate(single) if single else np.zeros(0, MATCH_DTYPE)
+        for batch in (len(cuts), 7):
+            dev = torch.empty(64, dtype=torch.uint8, device="cuda")
+            n = 0
+            for a in range(0, len(cuts), batch):
+                dev, k, _ = st.stream_windows_device(cuts[a: a + batch], 0.85, prefilter, dev, n)
+                n += k
+            got = dev[: n * 32].cpu().numpy().view(MATCH_DTYPE)
+            assert [tuple(r) for r in got] == [tuple(r) for r in single], (w, batch)
+        if w == win:
+            key = sorted((int(r["start"]), int(r["end"]), int(r["pattern_index"]),
+                          int(np.float32(r["similarity"]).view(np.uint32))) for r in single)
+            assert key == want
+
+
+@pytest.mark.parametrize("unicode_tail", [False, True])
+def test_search_stream_batches_match_oracle_emulation(unicode_tail):
+    """search_stream over fac_stream_* with many windows per batch (stream.cpp: an ASCII batch staged
+    once and searched in one launch, each window its own text) == the crate's WindowReader (64 KiB
+    reads) + per-window sorted().non_overlapping() search replayed on the CPU oracle; fed in 4 MiB
+    pieces, the windows are cut as the 64 KiB reads would cut them. With a Unicode tail the last
+    batch takes the per-window path."""
+    import io
+    from stream_emulation import stream_rows
+    pats, hay = _sparse_c5(2 << 20, 2 << 10)
+    if unicode_tail:
+        hay = hay + ("école " + pats[3] + " Москва ").encode() * 2000
+    b = B().fuzzy(L().edits(1)).device(0)
+    eng = b.build(pats)
+    got = sorted((m.start, m.end, m.pattern_index, int(np.float32(m.similarity).view(np.uint32)), m.text)
+                 for m in eng.stream_matches(io.BytesIO(hay), 0.85))
+    want = sorted(stream_rows(OracleEngine(b, pats), hay, 0.85, eng.max_match_graphemes() + 1))
+    assert len(want) > 500
+    assert got == want
+
+
 def test_haystack_too_large_is_reported(monkeypatch):
     """search_raw's SearchError::HaystackTooLarge{graphemes} (search.rs:198-201, error.rs:13-16)
     crosses the C ABI as return code 1 with the grapheme count; the u32::MAX limit is lowered by the
