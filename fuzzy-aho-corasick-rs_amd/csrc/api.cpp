@@ -709,7 +709,10 @@ int stream_windows_batch(const Engine& e, const Haystack& h, const uint64_t* win
     std::vector<std::pair<uint64_t, uint64_t>> rel(n_windows), runs;
     for (uint64_t w = 0; w < n_windows; ++w) rel[w] = {span[w].first - u0, span[w].second - u0};
     std::vector<uint32_t> run_win;
-    if (int rc = prefilter_windows_ex(e, h, view, ks, st, &rel, runs, &run_win, stats, err)) return rc;
+    // (one window is the whole view: the plain pass, no window bounds or second bitmap)
+    if (int rc = prefilter_windows_ex(e, h, view, ks, st, n_windows > 1 ? &rel : nullptr, runs, &run_win, stats, err))
+      return rc;
+    if (n_windows == 1) run_win.assign(runs.size(), 0u);
     segs.reserve(runs.size());
     for (size_t r = 0; r < runs.size(); ++r) {
       SegDesc s{};

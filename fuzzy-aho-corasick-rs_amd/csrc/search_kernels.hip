@@ -3668,6 +3668,9 @@ struct QgramParams {
   const uint64_t* whi;
   const uint32_t* wtab;
   uint32_t* cover2;
+  // wsh != 0: window w is [w << wsh, min(n, (w + 1) << wsh) + wov)) -- the crate's fixed-size cut,
+  // bounds computed instead of loaded
+  uint32_t wsh, wov;
 };
 constexpr uint32_t QG_WSH = 16;  // window-table buckets of 64 Ki positions
 __host__ __device__ inline uint32_t qgram_key(uint32_t a, uint32_t b, uint32_t c, uint32_t d, bool q4) {
@@ -4022,13 +4025,19 @@ __global__ __launch_bounds__(LM ? 512 : 256) void qgram_verify_kernel(QgramParam
         verify_one<KMAX, W, LM>(Q, cd, Q.ent[cd & 0xFFFFFFu], s_aid, s_m16, 0, Q.n, Q.cover);
       } else {
         const uint64_t t = cd >> 24;
-        uint32_t w = Q.wtab[t >> QG_WSH];
-        while (w + 1 < Q.nwin && Q.wlo[w + 1] <= t) ++w;
+        uint32_t w;
+        if (Q.wsh) {
+          w = (uint32_t)min(t >> Q.wsh, (uint64_t)(Q.nwin - 1));
+        } else {
+          w = Q.wtab[t >> QG_WSH];
+          while (w + 1 < Q.nwin && Q.wlo[w + 1] <= t) ++w;
+        }
         const uint2 en = Q.ent[cd & 0xFFFFFFu];
         for (uint32_t d = 0; d < 2; ++d) {  // the window holding t, then its predecessor if they overlap at t
           if (d > w) break;
           const uint32_t ww = w - d;
-          const uint64_t lo = Q.wlo[ww], hi = Q.whi[ww];
+          const uint64_t lo = Q.wsh ? (uint64_t)ww << Q.wsh : Q.wlo[ww];
+          const uint64_t hi = Q.wsh ? min(Q.n, lo + (1ull << Q.wsh) + Q.wov) : Q.whi[ww];
           if (t >= lo && t < hi) verify_one<KMAX, W, LM>(Q, cd, en, s_aid, s_m16, lo, hi, (ww & 1u) ? Q.cover2 : Q.cover);
         }
       }
@@ -5899,6 +5908,18 @@ int prefilter_windows_ex(const Engine& e, const Haystack& h, const SegDesc& view
       Q.whi = static_cast<const uint64_t*>(d_whi.p);
       Q.wtab = static_cast<const uint32_t*>(d_wtab.p);
       Q.cover2 = static_cast<uint32_t*>(d_cover2.p);
+      // the fixed-size cut (window w at w * 2^sh, its text 2^sh + ov bytes): bounds by arithmetic
+      if (wlo.size() > 1 && wlo[0] == 0 && (wlo[1] & (wlo[1] - 1)) == 0 && wlo[1] >= 64 && whi[0] > wlo[1]) {
+        const uint32_t sh = (uint32_t)__builtin_ctzll(wlo[1]);
+        const uint64_t ov = whi[0] - wlo[1];
+        bool uni = ov < (1ull << 31);
+        for (size_t w = 0; w < wlo.size() && uni; ++w)
+          uni = wlo[w] == ((uint64_t)w << sh) && whi[w] == std::min<uint64_t>(n, wlo[w] + (1ull << sh) + ov);
+        if (uni) {
+          Q.wsh = sh;
+          Q.wov = (uint32_t)ov;
+        }
+      }
     }
     int cus = 256;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e.device));
@@ -5964,43 +5985,54 @@ int prefilter_windows_ex(const Engine& e, const Haystack& h, const SegDesc& view
   if (win)
     for (uint32_t w = 0; w < (uint32_t)wlo.size(); ++w) par[w & 1].push_back(w);
   std::vector<std::tuple<uint64_t, uint64_t, uint32_t>> runs;  // (start, end, stream window)
-  HIP_TRY(d_cnt.alloc(8, stream));
-  for (int pass = 0; pass < (win ? 2 : 1); ++pass) {
-    const uint32_t* cov = static_cast<const uint32_t*>(pass ? d_cover2.p : d_cover.p);
-    uint64_t cap = 1 << 16;
-    for (;;) {
-      HIP_TRY(d_runs.alloc(cap * 16, stream));
-      HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 8, stream));
+  const int npass = win ? 2 : 1;
+  PoolBuf d_runs2;
+  PoolBuf* rbuf[2] = {&d_runs, &d_runs2};
+  uint64_t cap[2] = {1u << 16, 1u << 16};
+  HIP_TRY(d_cnt.alloc(16, stream));
+  for (;;) {  // both bitmaps' runs in one round trip; again with room for all of them if a list overflowed
+    HIP_TRY(hipMemsetAsync(d_cnt.p, 0, 16, stream));
+    for (int pass = 0; pass < npass; ++pass) {
+      const uint32_t* cov = static_cast<const uint32_t*>(pass ? d_cover2.p : d_cover.p);
+      HIP_TRY(rbuf[pass]->alloc(cap[pass] * 16, stream));
       hipLaunchKernelGGL(runs_kernel, dim3((uint32_t)((n_words + 255) / 256)), dim3(256), 0, stream, cov, n_words, n,
-                         static_cast<unsigned long long*>(d_runs.p), static_cast<unsigned long long*>(d_cnt.p), cap);
+                         static_cast<unsigned long long*>(rbuf[pass]->p), static_cast<unsigned long long*>(d_cnt.p) + pass,
+                         cap[pass]);
       HIP_TRY(hipGetLastError());
-      unsigned long long c = 0;
-      HIP_TRY(hipMemcpyAsync(&c, d_cnt.p, 8, hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
-      if (c > cap) {
-        cap = c;
-        continue;
+    }
+    unsigned long long c[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(c, d_cnt.p, 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    bool again = false;
+    for (int pass = 0; pass < npass; ++pass)
+      if (c[pass] > cap[pass]) {
+        cap[pass] = c[pass];
+        again = true;
       }
-      std::vector<unsigned long long> buf(2 * c);
-      if (c) HIP_TRY(hipMemcpyAsync(buf.data(), d_runs.p, c * 16, hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipEventRecord(ev.b, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
-      for (uint64_t i = 0; i < c; ++i) {
+    if (again) continue;
+    std::vector<unsigned long long> buf[2];
+    for (int pass = 0; pass < npass; ++pass) {
+      buf[pass].resize(2 * c[pass]);
+      if (c[pass]) HIP_TRY(hipMemcpyAsync(buf[pass].data(), rbuf[pass]->p, c[pass] * 16, hipMemcpyDeviceToHost, stream));
+    }
+    HIP_TRY(hipEventRecord(ev.b, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    for (int pass = 0; pass < npass; ++pass)
+      for (uint64_t i = 0; i < c[pass]; ++i) {
+        const uint64_t r0 = buf[pass][2 * i], r1 = buf[pass][2 * i + 1];
         uint32_t w = 0xFFFFFFFFu;
-        if (win) {  // the window of this parity whose [lo, hi) holds the run
+        if (win) {  // the window of this bitmap's parity whose [lo, hi) holds the run
           const auto& v = par[pass];
-          auto it = std::upper_bound(v.begin(), v.end(), (uint64_t)buf[2 * i],
-                                     [&](uint64_t x, uint32_t ww) { return x < wlo[ww]; });
-          if (it != v.begin() && buf[2 * i] < whi[*(it - 1)]) w = *(it - 1);
+          auto it = std::upper_bound(v.begin(), v.end(), r0, [&](uint64_t x, uint32_t ww) { return x < wlo[ww]; });
+          if (it != v.begin() && r0 < whi[*(it - 1)]) w = *(it - 1);
           if (w == 0xFFFFFFFFu) {
             err = "internal: a pre-filter run outside every stream window";
             return FAC_E_INTERNAL;
           }
         }
-        runs.emplace_back(buf[2 * i], buf[2 * i + 1], w);
+        runs.emplace_back(r0, r1, w);
       }
-      break;
-    }
+    break;
   }
   std::sort(runs.begin(), runs.end(), [](const auto& x, const auto& y) {
     return std::get<2>(x) != std::get<2>(y) ? std::get<2>(x) < std::get<2>(y) : std::get<0>(x) < std::get<0>(y);

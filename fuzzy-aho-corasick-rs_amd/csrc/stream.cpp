@@ -229,18 +229,22 @@ int flush_batch(StreamCore& s, std::string& err) {
 }
 
 int pump(StreamCore& s, bool eof, std::string& err) {
+  // the buffer's unconsumed bytes start at `at` (the committed prefix is dropped once per call: an
+  // erase per window moved the rest of a large feed again for every window)
+  uint64_t at = 0;
   while (!s.done) {
-    const uint64_t avail = s.buf.size();
+    const uint8_t* b = s.buf.data() + at;
+    const uint64_t avail = s.buf.size() - at;
     const uint64_t want = s.carry >= s.window ? s.carry : s.carry + (s.window - s.carry + kRead - 1) / kRead * kRead;
     if (!eof && avail < want) break;  // the reader would block for more input
     const uint64_t len = std::min(avail, want);
-    const uint64_t valid = utf8_valid_prefix(s.buf.data(), len);
+    const uint64_t valid = utf8_valid_prefix(b, len);
     const bool last = len < s.window;  // reached only at end of input
     uint64_t commit = valid;
     if (!last) {
       // byte start of the overlap-th grapheme from the end; none or 0: grow and read more
       uint64_t off = 0;
-      if (!nth_grapheme_from_end(s.buf.data(), valid, s.overlap, off) || off == 0) {
+      if (!nth_grapheme_from_end(b, valid, s.overlap, off) || off == 0) {
         s.window += std::max<uint64_t>(s.window, 64 * 1024);
         continue;  // (at end of input the next round is the last window)
       }
@@ -252,19 +256,22 @@ int pump(StreamCore& s, bool eof, std::string& err) {
     }
     StreamTask* t = s.pending;
     const uint64_t off = s.base - t->base;  // the window's first byte in the batch text
-    if (off + valid > t->text.size())
-      t->text.insert(t->text.end(), s.buf.begin() + (ptrdiff_t)(t->text.size() - off), s.buf.begin() + (ptrdiff_t)valid);
+    if (off + valid > t->text.size()) t->text.insert(t->text.end(), b + (t->text.size() - off), b + valid);
     t->wins.push_back(StreamWin{off, valid, commit});
     if (last) {
       s.done = true;
       break;
     }
-    s.buf.erase(s.buf.begin(), s.buf.begin() + (ptrdiff_t)commit);
+    at += commit;
     s.base += commit;
     s.carry = len - commit;
     if (t->text.size() >= kBatchBytes)
-      if (int rc = flush_batch(s, err)) return rc;
+      if (int rc = flush_batch(s, err)) {
+        s.buf.erase(s.buf.begin(), s.buf.begin() + (ptrdiff_t)at);
+        return rc;
+      }
   }
+  s.buf.erase(s.buf.begin(), s.buf.begin() + (ptrdiff_t)at);
   if (eof || s.done)
     if (int rc = flush_batch(s, err)) return rc;
   return collect(s, eof, err);

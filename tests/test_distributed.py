@@ -241,7 +241,7 @@ def test_bench_rejects_mismatched_world():
     assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)
 
 
-def _c5_worker(rank, world, port, blocks, out_path, mode="oracle"):
+def _c5_worker(rank, world, port, blocks, out_path, mode="oracle", window=None):
     sys.path[:0] = [os.path.join(REPO, "fuzzy-aho-corasick-rs_amd"), os.path.join(REPO, "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import numpy as np
@@ -265,7 +265,8 @@ def _c5_worker(rank, world, port, blocks, out_path, mode="oracle"):
     overlap = max(len(p) for p in wl.patterns) + 1 + 1  # max_match_graphemes() + 1, ASCII
     buf = block + block[:overlap]
     rows = []
-    windows = stream_share_windows(total, len(block), rank, overlap, n_shares=world)
+    windows = stream_share_windows(total, len(block), rank, overlap, n_shares=world, window=window)
+    assert sum(w[2] for w in windows) == total // world + (total % world if rank == world - 1 else 0)
     if mode != "gpu":
         for (g0, g1, commit, base) in windows:
             text = buf[g0:g1]  # stream.rs window_matches: search(sorted, non_overlapping), starts < commit
@@ -282,9 +283,21 @@ def _c5_worker(rank, world, port, blocks, out_path, mode="oracle"):
         staged = StagedHaystack(W.builder_for(wl).device(0).build(wl.patterns), buf)
         dev = torch.empty(64, dtype=torch.uint8, device="cuda:0")  # too small: grown by the call
         n = 0
-        for (g0, g1, commit, base) in windows:
-            dev, got_n, _ = staged.stream_window_device(g0, g1, commit, base, wl.threshold, True, dev, n)
-            n += got_n
+        if window is None:
+            for (g0, g1, commit, base) in windows:
+                dev, got_n, _ = staged.stream_window_device(g0, g1, commit, base, wl.threshold, True, dev, n)
+                n += got_n
+        else:  # bench.py's batches: the windows of one block pass per fac_stream_windows_staged_device call
+            batches, cur = [], []
+            for w in windows:
+                if cur and w[0] < cur[-1][0]:
+                    batches.append(cur)
+                    cur = []
+                cur.append(w)
+            batches += [cur] if cur else []
+            for bw in batches:
+                dev, got_n, _ = staged.stream_windows_device(bw, wl.threshold, True, dev, n)
+                n += got_n
         torch.cuda.synchronize()
         t = gather_device(dev, n, 0)  # gloo: the records leave HBM for the host wire
         got = None if t is None else as_rows(t)
@@ -315,8 +328,9 @@ def _c5_worker(rank, world, port, blocks, out_path, mode="oracle"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode", [(2, "oracle"), (4, "oracle"), (2, "oracle-buffer")])
-def test_c5_stream_shares_equal_whole_stream_cpu(world, mode):
+@pytest.mark.parametrize("world,mode,window", [(2, "oracle", None), (4, "oracle", None), (2, "oracle-buffer", None),
+                                               (2, "oracle", 8 << 10)])
+def test_c5_stream_shares_equal_whole_stream_cpu(world, mode, window):
     """bench.py --config c5's cut (stream_share_windows: one contiguous share per rank, windows at
     block and share edges with max_match_graphemes() + 1 of overlap, each searched like stream.rs
     window_matches with the pre-filter and owning the matches that start in it), the oracle as each
@@ -324,21 +338,22 @@ def test_c5_stream_shares_equal_whole_stream_cpu(world, mode):
     (tests.rs:1058-1142: streaming equals whole input for needles spaced past the overlap)."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res.txt")
-        mp.spawn(_c5_worker, args=(world, _free_port(), 5, out, mode), nprocs=world, join=True)
+        mp.spawn(_c5_worker, args=(world, _free_port(), 5, out, mode, window), nprocs=world, join=True)
         got, full = eval(open(out).read())
     assert len(full) >= 30
     assert got == full
 
 
 @pytest.mark.gpu
-def test_c5_stream_shares_device_buffer_gpu():
+@pytest.mark.parametrize("window", [None, 8 << 10])
+def test_c5_stream_shares_device_buffer_gpu(window):
     """bench.py --config c5's N > 1 path on the product: two ranks (both on cuda:0, gloo for the
     exchange) search their shares' stream windows with fac_stream_window_staged_device into one HBM
     record buffer each (grown from a too-small one), gathered to rank 0 with gather_device == the whole
     stream searched by the oracle sorted().non_overlapping()."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res.txt")
-        mp.spawn(_c5_worker, args=(2, _free_port(), 5, out, "gpu"), nprocs=2, join=True)
+        mp.spawn(_c5_worker, args=(2, _free_port(), 5, out, "gpu", window), nprocs=2, join=True)
         got, full = eval(open(out).read())
     assert len(full) >= 30
     assert got == full
