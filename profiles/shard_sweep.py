@@ -2,7 +2,7 @@
 every step like bench.py --shard) timed one after another on one GPU under prefix-cache knob settings
 (FAC_DIAGNOSTICS=1 knobs, read at each call), beside the whole haystack under the same setting.
 
-    python profiles/shard_sweep.py [N] [setting ...]   setting: NAME=VAL[,NAME=VAL] or 'default'
+    python profiles/shard_sweep.py [N] [setting ...]   setting: NAME=VAL[;NAME=VAL] or 'default'
 """
 import json
 import os
@@ -33,7 +33,7 @@ def main():
         os.environ.clear()
         os.environ.update(base_env)
         if s != "default":
-            for kv in s.split(","):
+            for kv in s.split(";"):
                 k, v = kv.split("=", 1)
                 os.environ[k] = v
 
