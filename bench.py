@@ -420,10 +420,36 @@ def shard_steps(engine, hay, n, r, local, stream, world=1):
     return staged, step, dev, nrec
 
 
-def _time_shard(engine, hay, n, r, local, stream, steps, threshold, world=1):
+def key_part_steps(engine, hay, n, r, local, stream, world=1):
+    """The key-split step on part r of n of `hay`: the whole haystack resident in HBM and staged on
+    the device in every step (fac_haystack_stage_device), searching only the start windows whose first
+    two characters hash to part r (fac_haystack_set_key_partition), records to rank 0 (RCCL gather at
+    world > 1, else D2H). Same return shape as shard_steps."""
+    import numpy as np
+    import torch
+    from fuzzy_aho_corasick.engine import StagedHaystack
+    from fuzzy_aho_corasick.distributed import gather_device
+    dev = torch.from_numpy(np.frombuffer(hay, dtype=np.uint8).copy()).to(torch.device("cuda", local))
+    staged = StagedHaystack.from_device(engine, dev.data_ptr(), len(hay), stream).set_key_partition(n, r)
+    nrec = [0]
+
+    def step(threshold):
+        hs = StagedHaystack.from_device(engine, dev.data_ptr(), len(hay), stream, reuse=staged)
+        if world == 1:
+            rows, _ = hs.search_windows_records(threshold, stream=stream)
+            nrec[0] = len(rows)
+            return
+        recs, k, _ = hs.search_device(threshold, stream=stream)
+        got = gather_device(recs, k, 0)
+        nrec[0] = got.numel() // 32 if got is not None else k
+
+    return staged, step, dev, nrec
+
+
+def _time_shard(engine, hay, n, r, local, stream, steps, threshold, world=1, keys=False):
     import torch
     import torch.distributed as dist
-    staged, step, dev, nrec = shard_steps(engine, hay, n, r, local, stream, world=world)
+    staged, step, dev, nrec = (key_part_steps if keys else shard_steps)(engine, hay, n, r, local, stream, world=world)
     step(threshold)  # warm-up
     if world > 1:
         dist.barrier()
@@ -435,45 +461,57 @@ def _time_shard(engine, hay, n, r, local, stream, steps, threshold, world=1):
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t
-    out = (dt, staged.owned_windows, nrec[0], staged.owned_bytes)
+    out = (dt, staged.owned_windows if not keys else staged.graphemes / n, nrec[0], staged.owned_bytes)
     del staged, dev
     return out
 
 
 def strong_emulated(engine, hay, threshold, local, stream, full_ms, ns=(2, 4, 8), steps=3):
-    """Strong scaling of the headline, estimated on one GPU: for N in `ns`, every
-    shard r of N of the same haystack (fac_shard_plan: owned bytes + halo) is staged from HBM and
-    searched with the --shard step, one shard after another; an N-GPU step would take the slowest
-    shard's time (+ the record gather), so predicted_speedup = the N = 1 step / max_rank_ms."""
-    out = {"method": "every shard of N timed alone on this GPU (the --shard step: device staging of the shard + "
-                     "search + records D2H), predicted N-GPU step = the slowest shard; the RCCL gather excluded",
+    """Strong scaling of the headline, estimated on one GPU: for N in `ns`, every part
+    r of N of the same haystack is staged from HBM and searched, one part after another; an N-GPU step
+    takes the slowest part's time (+ the record gather), so predicted_speedup = the N = 1 step /
+    max_rank_ms. Two splits: "shards" (bench.py --shard: contiguous byte ranges + halo, fac_shard_plan,
+    each shard staging only its bytes) and "keys" (fac_haystack_set_key_partition: every rank stages
+    the whole haystack and searches the start windows whose first two characters hash to its part, so
+    a prefix-cache key is built once, on one GPU, for all its windows)."""
+    out = {"method": "every part of N timed alone on this GPU (device staging + search + records D2H), predicted "
+                     "N-GPU step = the slowest part; the RCCL gather excluded",
            "n1_ms": full_ms}
-    for n in ns:
-        ms = []
-        for r in range(n):
-            dt, w, k, b = _time_shard(engine, hay, n, r, local, stream, steps, threshold)
-            ms.append(dt / steps * 1e3)
-        out[str(n)] = {"max_rank_ms": max(ms), "min_rank_ms": min(ms), "sum_rank_ms": sum(ms),
-                       "predicted_speedup": full_ms / max(ms), "rank_ms": [round(x, 2) for x in ms]}
+    for keys in (False, True):
+        res = {}
+        for n in ns:
+            ms = []
+            for r in range(n):
+                dt, w, k, b = _time_shard(engine, hay, n, r, local, stream, steps, threshold, keys=keys)
+                ms.append(dt / steps * 1e3)
+            res[str(n)] = {"max_rank_ms": max(ms), "min_rank_ms": min(ms), "sum_rank_ms": sum(ms),
+                           "predicted_speedup": full_ms / max(ms), "rank_ms": [round(x, 2) for x in ms]}
+        out["keys" if keys else "shards"] = res
     return out
 
 
 def strong_measured(engine, hay, threshold, world, rank, local, stream, steps):
-    """At N > 1 (default weak run): the --shard step of one haystack over the same ranks, timed like
-    the headline (barrier + synchronize on both sides, max over ranks); value = every rank's owned
-    windows / that time."""
+    """At N > 1 (default weak run): one haystack over the same ranks, timed like the headline (barrier +
+    synchronize on both sides, max over ranks), split both ways -- "shards" (--shard: contiguous byte
+    ranges) and "keys" (fac_haystack_set_key_partition); value = the haystack's windows / that time."""
     import torch
     import torch.distributed as dist
-    dt, w, k, b = _time_shard(engine, hay, world, rank, local, stream, steps, threshold, world=world)
-    t = torch.tensor([dt], device="cuda", dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    g = torch.tensor([w], device="cuda", dtype=torch.int64)
-    dist.all_reduce(g)
-    dt = float(t.item())
-    return {"value": int(g.item()) * steps / dt / 1e9, "unit": "Gchars/s", "ms_per_step": dt / steps * 1e3,
+    out = {}
+    for keys in (False, True):
+        dt, w, k, b = _time_shard(engine, hay, world, rank, local, stream, steps, threshold, world=world, keys=keys)
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        g = torch.tensor([float(w)], device="cuda", dtype=torch.float64)
+        dist.all_reduce(g)
+        dt = float(t.item())
+        out["keys" if keys else "shards"] = {
+            "value": float(g.item()) * steps / dt / 1e9, "unit": "Gchars/s", "ms_per_step": dt / steps * 1e3,
             "steps": steps, "haystack_bytes": len(hay), "records_per_step": k,
-            "step": "--shard: one haystack, every rank stages its halo-sliced shard on the device and searches it, "
-                    "records gathered to rank 0 over RCCL"}
+            "step": ("every rank stages the whole haystack on the device and searches its key part "
+                     "(fac_haystack_set_key_partition)" if keys else
+                     "--shard: every rank stages its halo-sliced shard on the device and searches it")
+                    + ", records gathered to rank 0 over RCCL"}
+    return out
 
 
 def default_legs(args, local):

@@ -479,6 +479,16 @@ int fac_haystack_stage_shard(const fac_engine* engine, const uint8_t* utf8, uint
 
 uint64_t fac_haystack_owned_windows(const fac_haystack* hay) { return hay ? std::min(hay->h.n, hay->h.owned) : 0; }
 
+int fac_haystack_set_key_partition(const fac_engine* engine, fac_haystack* hay, uint32_t parts, uint32_t part) {
+  if (!engine || !hay || parts == 0 || part >= parts) return fail(FAC_E_INVALID, "bad argument");
+  // auto-beam switches the beam on after a running count over the windows in order
+  // (search.rs:1096-1103): a key partition has no such order
+  if (parts > 1 && engine->e.has_auto_beam) return fail(FAC_E_UNSUPPORTED, "key partitions do not support auto_beam");
+  hay->h.kparts = parts;
+  hay->h.kpart = part;
+  return FAC_OK;
+}
+
 uint64_t fac_haystack_graphemes(const fac_haystack* hay) { return hay ? hay->h.n : 0; }
 
 uint64_t fac_haystack_grapheme_starts(const fac_haystack* hay, uint64_t* out, uint64_t cap) {

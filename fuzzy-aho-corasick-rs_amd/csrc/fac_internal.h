@@ -247,6 +247,7 @@ struct SearchParams {
   uint32_t* win_counts;  // null: not recorded
   int32_t exact_dedup;   // dedup must be exact (beam, or counting for auto-beam)
   int32_t dup_cut;       // diagnostics (FAC_DUP_CUT=1): cut a batch at an in-batch duplicate instead of resolving it
+  uint32_t kp_n, kp_r;   // key partition of the haystack's start windows (Haystack::kparts / kpart)
   // prefix cache (launch_pass): a state at j reads text[j] and text[j + 1], so the
   // pops before the first state with j >= rc_k - 1 depend only on the window's first rc_k chars;
   // windows sharing them resume from one snapshot (queue, dedup entries, best list, counters)
@@ -419,6 +420,10 @@ struct Haystack {
   uint64_t base = 0;
   bool open_end = false;
   uint64_t owned = UINT64_MAX;
+  // key partition (fac_haystack_set_key_partition): only the start windows whose first two
+  // characters hash to part (of parts) are searched -- a strong-scaling split of one haystack that
+  // keeps every window of a prefix on one GPU, so each GPU's prefix cache covers whole keys
+  uint32_t kparts = 1, kpart = 0;
   uint8_t* d_utf8 = nullptr;
   bool own_utf8 = true;          // false: the caller's device bytes (fac_haystack_stage_device)
   uint32_t* d_text32 = nullptr;  // Unicode only

@@ -2246,6 +2246,20 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
   return tail;  // states pushed this window, the root included: the reference's queue.len()
 }
 
+// Key partition (Haystack::kparts): a start window belongs to part hash(its first two characters,
+// folded as the keys fold them) mod parts. Every prefix-cache key extends its window's first two
+// characters (keys hold >= 2), so a key's windows -- and its snapshot -- live in one part.
+__device__ __forceinline__ bool window_owned_kp(const SearchParams& P, const SegDesc& S, uint64_t s, unsigned& err) {
+  if (P.kp_n <= 1u) return true;
+  const uint32_t c0 = text_char(P, S, s, err);
+  const uint32_t c1 = s + 1 < S.n ? text_char(P, S, s + 1, err) : 0xFFFFFFFFu;
+  uint32_t h = (c0 * 0x9E3779B1u) ^ (c1 * 0x85EBCA6Bu);
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  return h % P.kp_n == P.kp_r;
+}
+
 // 2-gram window skip (search.rs:535-553)
 __device__ __forceinline__ bool window_skipped(const SearchParams& P, const SegDesc& S, uint64_t s, unsigned& err) {
   if (!P.window_skip) return false;
@@ -2526,7 +2540,7 @@ __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, RcCountTa
     const uint32_t kl = find_seg(P, vid);
     const SegDesc S = P.segs[kl];
     const uint64_t start = S.w_begin + (vid - P.seg_prefix[kl]);
-    if (window_skipped(P, S, start, err)) continue;
+    if (window_skipped(P, S, start, err) || !window_owned_kp(P, S, start, err)) continue;
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       const RcCountTarget& T = t == 0 ? t0 : t == 1 ? t1 : t2;
@@ -2682,7 +2696,7 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
       kl = find_seg(P, v);
       const SegDesc S = P.segs[kl];
       start = S.w_begin + (v - P.seg_prefix[kl]);
-      active = !window_skipped(P, S, start, err);
+      active = !window_skipped(P, S, start, err) && window_owned_kp(P, S, start, err);
     }
     RcHit hit{EMPTY, 0u, 0u, 0u, 0u};
     if (active) hit = rc_lookup(P, P.segs[kl], start, P.rc_qcap);
@@ -3222,7 +3236,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           hit = RcHit{h.x, h.y, h.z, h.w, P.rc_hit_pops[vid]};
           active = h.x != RC_DONE;
         } else {
-          active = !window_skipped(P, S, start, err);
+          active = !window_skipped(P, S, start, err) && (P.rc_mode != 0 || window_owned_kp(P, S, start, err));
         }
       }
       if constexpr (LK)
@@ -4576,6 +4590,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.beam = beam;
   P.exact_dedup = exact_dedup ? 1 : 0;
   P.dup_cut = diag_env("FAC_DUP_CUT") ? 1 : 0;
+  P.kp_n = h.kparts;
+  P.kp_r = h.kpart;
   P.window_skip = e.window_skip;
   P.has_map = e.has_map ? 1 : 0;
   if (e.has_map) {  // multi-character mappings: whole-grapheme ids (ensure_gids for Unicode text)

@@ -142,6 +142,7 @@ SIGNATURES = {
                                                        ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_void_p,
                                                        ctypes.POINTER(ctypes.c_void_p), _u64p]),
     "fac_haystack_owned_windows": (ctypes.c_uint64, [_hay_p]),
+    "fac_haystack_set_key_partition": (ctypes.c_int, [_engine_p, _hay_p, ctypes.c_uint32, ctypes.c_uint32]),
     "fac_stream_window_staged": (ctypes.c_int, [_engine_p, _hay_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_uint64, ctypes.c_float, ctypes.c_int32, ctypes.c_void_p,
                                                 _P(_P(fac_match)), _u64p, _P(fac_stats)]),

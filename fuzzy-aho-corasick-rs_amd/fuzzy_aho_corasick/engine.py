@@ -529,6 +529,16 @@ class StagedHaystack:
         obj.owned_windows = int(_native.lib.fac_haystack_owned_windows(obj._h))
         return obj
 
+    def set_key_partition(self, parts: int, part: int) -> "StagedHaystack":
+        """fac_haystack_set_key_partition: later searches cover only the start windows whose first two
+        characters hash to `part` of `parts` (a strong-scaling split that keeps whole prefix-cache keys
+        on one GPU). parts = 1 restores the whole haystack."""
+        rc = _native.lib.fac_haystack_set_key_partition(self.engine._h, self._h, parts, part)
+        if rc:
+            _raise(rc)
+        self.key_partition = (parts, part)
+        return self
+
     def search_device(self, threshold: float, window_begin: int = 0, window_end: int = None, stream=None,
                       auto_beam_prefix: int = 0, torch_device=None):
         """fac_search_staged_ex with the records left in HBM: (uint8 tensor of n * 32 bytes on the

@@ -258,6 +258,13 @@ int fac_haystack_stage_shard_device(const fac_engine* engine, const uint8_t* d_u
                                     uint64_t* err_graphemes);
 /* start windows a staged haystack owns (all of them unless it is a shard) */
 uint64_t fac_haystack_owned_windows(const fac_haystack* hay);
+/* Strong-scaling split by key instead of by position: searches of `hay` cover only the start windows
+ * whose first two (folded) characters hash to `part` of `parts` (parts = 1: all). Every window of a
+ * prefix lands in one part, so each GPU's prefix cache holds whole keys -- a position
+ * shard of 1/N shares its keys with every other shard and rebuilds them. The union of the parts'
+ * records is the whole haystack's search_raw (windows are independent). FAC_E_UNSUPPORTED for
+ * auto_beam engines (a running count over windows in order, search.rs:1096-1103). */
+int fac_haystack_set_key_partition(const fac_engine* engine, fac_haystack* hay, uint32_t parts, uint32_t part);
 
 /* One streaming window on the device (stream.rs:262-297 window_matches): the graphemes
  * [g_begin, g_end) of a staged haystack are searched as the window's text (Prefiltered::search if

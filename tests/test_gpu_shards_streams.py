@@ -87,6 +87,35 @@ def test_device_staged_shards_equal_host_staged(config, nbytes, n):
     assert (sh.graphemes, sh.owned_windows) == (host.graphemes, host.owned_windows)
 
 
+@pytest.mark.parametrize("config,nbytes,parts", [("c3", 96 << 10, (2, 3, 8)), ("c2", 256 << 10, (2, 5)), ("c3", 700, (3,))])
+def test_key_partitions_union_equals_whole(config, nbytes, parts):
+    """fac_haystack_set_key_partition (bench.py's key-split strong scaling): the parts' start windows
+    (by a hash of their first two characters) are disjoint and cover the haystack, so the union of
+    the parts' records equals the whole haystack's search_raw on every field -- with the prefix cache
+    (each part counts, builds and looks up only its own keys; the C3 engine is beamed) and without it
+    (700 bytes), restaged in place between searches like the bench step."""
+    import torch
+    wl = W.config(config, nbytes)
+    eng = W.builder_for(wl).device(0).build(wl.patterns)
+    want = rows_key(StagedHaystack(eng, wl.haystack).search_windows(wl.threshold)[0])
+    assert len(want) > 3
+    dev = torch.from_numpy(np.frombuffer(wl.haystack, np.uint8).copy()).cuda()
+    for n in parts:
+        got, sizes = [], []
+        for r in range(n):
+            sh = StagedHaystack.from_device(eng, dev.data_ptr(), len(wl.haystack)).set_key_partition(n, r)
+            for _ in range(2):
+                sh = StagedHaystack.from_device(eng, dev.data_ptr(), len(wl.haystack), reuse=sh)
+                rows = sh.search_windows(wl.threshold)[0]
+            got += rows
+            sizes.append(len(rows))
+        assert rows_key(got) == want, (config, n)
+        assert len(want) < 20 or min(sizes) > 0, sizes
+    ab = B().fuzzy(L().edits(1)).auto_beam(1000, 2).device(0).build(["needle"])
+    with pytest.raises(Exception):
+        StagedHaystack(ab, b"a needle here").set_key_partition(2, 0)
+
+
 def test_empty_unicode_shard_stages_on_device():
     """A short Unicode text over many ranks leaves the last shards empty (plan (len, len, len, ...)):
     staging such a shard fresh from device memory must not touch the unallocated staging scratch
