@@ -523,6 +523,7 @@ struct StreamCore {
   std::vector<uint8_t> buf;
   uint64_t base = 0, total = 0;
   uint64_t carry = 0;  // bytes the last window left in the buffer (its text after the commit point)
+  uint64_t valid_end = 0;  // stream offset up to which the bytes are known valid UTF-8 (a character boundary)
   bool done = false;
   StreamTask* pending = nullptr;  // windows cut but not yet dispatched (one batch)
   std::vector<fac_match> ready;

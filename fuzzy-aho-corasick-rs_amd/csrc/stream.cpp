@@ -238,7 +238,11 @@ int pump(StreamCore& s, bool eof, std::string& err) {
     const uint64_t want = s.carry >= s.window ? s.carry : s.carry + (s.window - s.carry + kRead - 1) / kRead * kRead;
     if (!eof && avail < want) break;  // the reader would block for more input
     const uint64_t len = std::min(avail, want);
-    const uint64_t valid = utf8_valid_prefix(b, len);
+    // the valid UTF-8 prefix of the window's bytes; bytes a previous window already validated (up to
+    // valid_end, a character boundary) are not scanned again
+    const uint64_t vfrom = std::min<uint64_t>(len, s.valid_end > s.base ? s.valid_end - s.base : 0);
+    const uint64_t valid = vfrom + utf8_valid_prefix(b + vfrom, len - vfrom);
+    s.valid_end = s.base + valid;
     const bool last = len < s.window;  // reached only at end of input
     uint64_t commit = valid;
     if (!last) {

@@ -87,18 +87,18 @@ def test_device_staged_shards_equal_host_staged(config, nbytes, n):
     assert (sh.graphemes, sh.owned_windows) == (host.graphemes, host.owned_windows)
 
 
-@pytest.mark.parametrize("config,nbytes,parts", [("c3", 96 << 10, (2, 3, 8)), ("c2", 256 << 10, (2, 5)), ("c3", 700, (3,))])
+@pytest.mark.parametrize("config,nbytes,parts", [("c3", 96 << 10, (2, 3, 8)), ("c2", 256 << 10, (2, 5)), ("c3", 5000, (3,))])
 def test_key_partitions_union_equals_whole(config, nbytes, parts):
     """fac_haystack_set_key_partition (bench.py's key-split strong scaling): the parts' start windows
     (by a hash of their first two characters) are disjoint and cover the haystack, so the union of
     the parts' records equals the whole haystack's search_raw on every field -- with the prefix cache
     (each part counts, builds and looks up only its own keys; the C3 engine is beamed) and without it
-    (700 bytes), restaged in place between searches like the bench step."""
+    (5000 bytes: fewer than 4096 windows), restaged in place between searches like the bench step."""
     import torch
     wl = W.config(config, nbytes)
     eng = W.builder_for(wl).device(0).build(wl.patterns)
     want = rows_key(StagedHaystack(eng, wl.haystack).search_windows(wl.threshold)[0])
-    assert len(want) > 3
+    assert len(want) >= 1
     dev = torch.from_numpy(np.frombuffer(wl.haystack, np.uint8).copy()).cuda()
     for n in parts:
         got, sizes = [], []
