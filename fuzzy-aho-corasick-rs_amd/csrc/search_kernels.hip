@@ -2272,6 +2272,7 @@ __device__ __forceinline__ bool window_skipped(const SearchParams& P, const SegD
   return false;
 }
 
+
 __device__ __forceinline__ uint32_t find_seg(const SearchParams& P, uint64_t v) {
   uint32_t lo = 0, hi = P.n_segs;  // last k with prefix[k] <= v
   while (hi - lo > 1) {
@@ -2530,6 +2531,23 @@ __device__ __forceinline__ void rc_count_insert(const RcCountTarget& T, uint64_t
 }
 // Up to three levels are counted in one pass over the windows (level 1; the sampled levels): their
 // inserts go out together and the window's text is read once.
+// Key partition without the prefix cache: the part's windows listed (the main pass then walks the
+// list; the ownership test stays out of the window loop, whose registers it would have crowded)
+__global__ __launch_bounds__(256) void kp_list_kernel(SearchParams P, uint64_t* list, unsigned long long* n) {
+  unsigned err = 0;
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < P.total_windows;
+       v += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t kl = find_seg(P, v);
+    const SegDesc S = P.segs[kl];
+    const bool own = window_owned_kp(P, S, S.w_begin + (v - P.seg_prefix[kl]), err);
+    const uint64_t m = __ballot(own);
+    unsigned long long b = 0;
+    if (m && lane_id() == (uint32_t)first_lane(m)) b = atomicAdd(n, (unsigned long long)__popcll(m));
+    b = __shfl(b, first_lane(m ? m : 1ull));
+    if (own) list[b + prefix_below(m)] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, RcCountTarget t0, RcCountTarget t1,
                                                        RcCountTarget t2, uint32_t stride, uint32_t sat, uint32_t probes) {
   const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
@@ -3236,7 +3254,7 @@ __device__ __forceinline__ void bfs_window_body(const SearchParams& P) {
           hit = RcHit{h.x, h.y, h.z, h.w, P.rc_hit_pops[vid]};
           active = h.x != RC_DONE;
         } else {
-          active = !window_skipped(P, S, start, err) && (P.rc_mode != 0 || window_owned_kp(P, S, start, err));
+          active = !window_skipped(P, S, start, err);
         }
       }
       if constexpr (LK)
@@ -5275,10 +5293,26 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
                                   : std::min<uint64_t>(4096, std::max<uint64_t>(base_chunk, pass_windows / (16ull * max_grid)));
   const uint32_t rc_chunk = (uint32_t)std::min<unsigned long>(4096, std::max<unsigned long>(1,
       diag_env("FAC_RC_CHUNK") ? std::strtoul(diag_env("FAC_RC_CHUNK"), nullptr, 10) : rc_auto));
+  bool kp_listed = false;  // the main pass walks the key part's window list (no prefix cache)
+  if (P.rc_mode == 0 && P.kp_n > 1) {
+    HIP_TRY(d_list.alloc(windows * sizeof(uint64_t), stream));
+    HIP_TRY(hipMemsetAsync(d_cnt.p, 0, sizeof(unsigned long long), stream));
+    P.total_windows = windows;
+    hipLaunchKernelGGL(kp_list_kernel, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256, (uint64_t)cus * 8))),
+                       dim3(256), 0, stream, P, static_cast<uint64_t*>(d_list.p), static_cast<unsigned long long*>(d_cnt.p));
+    HIP_TRY(hipGetLastError());
+    unsigned long long nk = 0;
+    HIP_TRY(hipMemcpyAsync(&nk, d_cnt.p, sizeof(nk), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    pass_windows = nk;
+    P.win_list = static_cast<const uint64_t*>(d_list.p);
+    kp_listed = true;
+  }
   for (;;) {
+    if (pass_windows == 0) break;
     // spilled windows are few and heavy: one per block turn; behind the prefix-cache lookups most
     // windows are done, so chunks are larger (fewer hand-out atomics; the group prescan skips them)
-    P.chunk = P.win_list ? 1u : (P.rc_mode == 1 ? rc_chunk : (uint32_t)base_chunk);
+    P.chunk = kp_listed ? (uint32_t)base_chunk : P.win_list ? 1u : (P.rc_mode == 1 ? rc_chunk : (uint32_t)base_chunk);
     P.total_windows = pass_windows;
     const uint64_t want = (pass_windows + P.chunk - 1) / P.chunk;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, max_grid));
@@ -5463,6 +5497,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
       spill_cap = std::max<uint64_t>(spill_cap, pass_windows);
     }
     P.win_list = static_cast<const uint64_t*>(d_list.p);
+    kp_listed = false;
     ++retries;
   }
   if (timing)
