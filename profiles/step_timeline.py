@@ -17,6 +17,8 @@ def prev_kernel(i):  # the last kernel before i that is not a runtime fill / cop
 
 
 starts = [i for i, n in enumerate(names) if 'ascii_or_kernel' in n]
+if len(starts) < 2:  # a shard staged in Unicode mode (no is_ascii pass): its segmentation starts the step
+    starts = [i for i, n in enumerate(names) if 'seg_tile_kernel' in n]
 if len(starts) < 2:
     starts = [i for i, n in enumerate(names) if 'rc_count_kernel' in n and 'window_kernel' in prev_kernel(i)]
 a, b = (starts[-2], starts[-1]) if len(starts) >= 2 else (starts[-1], len(rows))
