@@ -698,7 +698,8 @@ namespace fac {
 int stream_windows_batch(const Engine& e, const Haystack& h, const uint64_t* wins, uint64_t n_windows, float threshold,
                          bool prefilter, hipStream_t st, std::vector<fac_match>& owned, fac_stats* stats, std::string& err) {
   owned.clear();
-  if (!h.ascii || h.open_end || h.base || n_windows == 0 || n_windows >= (1u << 24)) return FAC_E_UNSUPPORTED;
+  if (!h.ascii || h.open_end || h.base || n_windows == 0 || n_windows >= (1u << 24) || h.len >= (1ull << kWinTagShift))
+    return FAC_E_UNSUPPORTED;
   std::vector<std::pair<uint64_t, uint64_t>> span(n_windows);
   std::vector<WinOwn> own(n_windows);
   uint64_t u0 = UINT64_MAX, u1 = 0;
@@ -731,17 +732,16 @@ int stream_windows_batch(const Engine& e, const Haystack& h, const uint64_t* win
       s.n = runs[r].second - runs[r].first;
       s.avail = s.n;
       s.hay_len = s.n;
-      s.byte_base = s.text_base;
+      s.byte_base = s.text_base | ((uint64_t)run_win[r] << kWinTagShift);  // the window tag (WinOwn)
       s.w_begin = 0;
       s.w_end = s.n;
-      s.pad = run_win[r];
       segs.push_back(s);
     }
   } else {  // no pre-filter (or the reference's fallback to a full search, prefilter.rs:311-317)
     for (uint64_t w = 0; w < n_windows; ++w) {
       if (span[w].second <= span[w].first) continue;
       SegDesc s = slice_view(h, span[w].first, span[w].second);
-      s.pad = (uint32_t)w;
+      s.byte_base |= (uint64_t)w << kWinTagShift;  // the window tag (WinOwn)
       segs.push_back(s);
     }
   }

@@ -148,7 +148,7 @@ struct SegDesc {
   uint64_t byte_base;  // global byte offset of local byte 0 (added to every output offset)
   uint64_t w_begin, w_end;  // local start windows to search
   uint32_t ascii;      // 1: grapheme == byte (AsciiGraphemes), 0: Unicode graphemes
-  uint32_t pad;        // tag copied into the records' pad bytes (24 bits; a batch's stream window), else 0
+  uint32_t pad;
 };
 
 // one prefix-cache level: open-addressing table of key hashes -> entry -> snapshot
@@ -247,7 +247,6 @@ struct SearchParams {
   uint32_t* win_counts;  // null: not recorded
   int32_t exact_dedup;   // dedup must be exact (beam, or counting for auto-beam)
   int32_t dup_cut;       // diagnostics (FAC_DUP_CUT=1): cut a batch at an in-batch duplicate instead of resolving it
-  uint32_t kp_n, kp_r;   // key partition of the haystack's start windows (Haystack::kparts / kpart)
   // prefix cache (launch_pass): a state at j reads text[j] and text[j + 1], so the
   // pops before the first state with j >= rc_k - 1 depend only on the window's first rc_k chars;
   // windows sharing them resume from one snapshot (queue, dedup entries, best list, counters)
@@ -290,6 +289,9 @@ struct SearchParams {
   const uint2* map_range;     // per node [begin, end) into map_ent
   const uint4* map_ent;       // {hay begin (into map_hay), hay length, next node, penalty bits}
   const uint32_t* map_hay;    // haystack-side grapheme ids
+  // key partition of the haystack's start windows (Haystack::kparts / kpart), last: fields added
+  // in the middle moved every later kernel argument and changed the window kernels' allocation
+  uint32_t kp_n, kp_r;
 };
 
 constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8u, ERR_OUT = 16u, ERR_SPILL = 32u;
@@ -556,10 +558,13 @@ int apply_matches(const Engine& e, std::vector<fac_match>& v, int order, int ove
 int window_owned_device(const Engine& e, fac_match* d_a, fac_match* d_b, uint64_t n, uint64_t byte_base, uint64_t commit,
                         uint64_t base, hipStream_t s, fac_match* d_out, uint64_t cap, uint64_t* n_owned, std::string& err);
 // A stream window of a batch: its text starts at staged byte byte_base, it owns the matches starting
-// before commit bytes into it, and byte_base maps to stream offset base.
+// before commit bytes into it, and byte_base maps to stream offset base. A batch's ASCII segments
+// carry their window in the bits of SegDesc::byte_base from kWinTagShift up, so every record's start
+// and end come back tagged (the kernels only add byte offsets to byte_base for ASCII text).
 struct WinOwn {
   uint64_t byte_base, commit, base;
 };
+constexpr uint32_t kWinTagShift = 40;
 void windows_owned_host(const Engine& e, std::vector<fac_match>& recs, const std::vector<WinOwn>& wins,
                         std::vector<fac_match>& out);
 // api.cpp: a batch of stream windows (g_begin, g_end, commit_bytes, base) x n of a whole staged ASCII

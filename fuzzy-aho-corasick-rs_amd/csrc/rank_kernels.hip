@@ -467,20 +467,26 @@ int window_owned_device(const Engine& e, fac_match* d_a, fac_match* d_b, uint64_
   return FAC_OK;
 }
 
-// A batch of stream windows' raw records (each tagged with its window in pad[0..2]): per window,
+// A batch of stream windows' raw records (start and end tagged with the window, kWinTagShift): per window,
 // sorted().non_overlapping() and the matches starting before its commit point, rebased to stream
 // offsets (stream.rs:262-297), appended to `out` in window order with the tag cleared.
 void windows_owned_host(const Engine& e, std::vector<fac_match>& recs, const std::vector<WinOwn>& wins,
                         std::vector<fac_match>& out) {
   const size_t nw = wins.size();
   std::vector<uint64_t> first(nw + 1, 0);
-  auto tag = [](const fac_match& m) { return (uint32_t)m.pad[0] | ((uint32_t)m.pad[1] << 8) | ((uint32_t)m.pad[2] << 16); };
+  auto tag = [](const fac_match& m) { return (uint32_t)(m.start >> kWinTagShift); };
+  constexpr uint64_t low = (1ull << kWinTagShift) - 1;
   for (const fac_match& m : recs) ++first[tag(m) + 1];
   for (size_t w = 0; w < nw; ++w) first[w + 1] += first[w];
   std::vector<fac_match> by(recs.size());
   {
     std::vector<uint64_t> at(first.begin(), first.end() - 1);
-    for (const fac_match& m : recs) by[at[tag(m)]++] = m;
+    for (const fac_match& m : recs) {
+      fac_match u = m;
+      u.start &= low;
+      u.end &= low;
+      by[at[tag(m)]++] = u;
+    }
   }
   std::vector<fac_match> v;
   for (size_t w = 0; w < nw; ++w) {
@@ -493,7 +499,6 @@ void windows_owned_host(const Engine& e, std::vector<fac_match>& recs, const std
       if (st >= wins[w].commit) continue;
       m.start = st + wins[w].base;
       m.end = m.end - wins[w].byte_base + wins[w].base;
-      m.pad[0] = m.pad[1] = m.pad[2] = 0;
       out.push_back(m);
     }
   }

@@ -1704,10 +1704,7 @@ __device__ __forceinline__ fac_match match_record(const SearchParams& P, const S
   m.substitutions = (ent.w >> 16) & 0xFFu;
   m.swaps = ent.w >> 24;
   m.edits = (uint8_t)edits_of(ent.w);
-  // the segment's tag (SegDesc::pad, 0 unless a batch of stream windows marks each record's window)
-  m.pad[0] = (uint8_t)S.pad;
-  m.pad[1] = (uint8_t)(S.pad >> 8);
-  m.pad[2] = (uint8_t)(S.pad >> 16);
+  m.pad[0] = m.pad[1] = m.pad[2] = 0;
   return m;
 }
 
