@@ -2426,6 +2426,64 @@ __device__ __forceinline__ RcHit rc_lookup(const SearchParams& P, const SegDesc&
   }
   return r;
 }
+// rc_lookup in two halves for rc_lookup_kernel: the start level and the deeper ones while open
+// (found: a usable hit), then -- for the windows that found none -- the shallower levels. The
+// kernel defers the second half of a wave's missing windows into full waves of them.
+struct RcKey {
+  uint32_t c[8];
+  uint32_t enc;
+  bool ok;
+};
+__device__ __forceinline__ uint32_t rc_start_level(const SearchParams& P) {
+  uint32_t st = 0;  // rc_tab is deepest first: the last level with k >= rc_kstart
+#pragma unroll
+  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t)
+    if (t < P.rc_ntab && P.rc_tab[t].k >= P.rc_kstart) st = t;
+  return st;
+}
+__device__ __forceinline__ void rc_key_of(const SearchParams& P, const SegDesc& S, uint64_t s, RcKey& K) {
+  uint32_t kmax = 0;
+  for (uint32_t t = 0; t < P.rc_ntab; ++t) kmax = max(kmax, P.rc_tab[t].k);
+  K.ok = rc_chars(P, S, s, kmax, K.c);
+  K.enc = 8;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i)
+    if (K.enc == 8 && K.c[i] != RC_PAD && K.c[i] >= 0xFFFFu) K.enc = i;
+}
+__device__ __forceinline__ RcHit rc_lookup_deep(const SearchParams& P, const SegDesc& S, uint64_t s, uint32_t QCAP,
+                                                const RcKey& K, uint32_t st, bool& found) {
+  RcHit r{EMPTY, 0u, 0u, 0u, 0u};
+  found = false;
+  bool up = true;
+#pragma unroll
+  for (int t = kRcLevels - 1; t >= 0; --t) {  // st, then deeper while open
+    if (!up || (uint32_t)t > st || (uint32_t)t >= P.rc_ntab) continue;
+    RcHit h{EMPTY, 0u, 0u, 0u, 0u};
+    const uint32_t res = rc_probe(P.rc_tab[t], K.c, K.enc, K.ok, s, S, QCAP, (uint32_t)t, h);
+    if (res == 1u || res == 2u) {
+      r = h;
+      found = true;
+    }
+    up = res == 1u;
+  }
+  return r;
+}
+__device__ __forceinline__ RcHit rc_lookup_shallow(const SearchParams& P, const SegDesc& S, uint64_t s, uint32_t QCAP,
+                                                   const RcKey& K, uint32_t st) {
+  RcHit r{EMPTY, 0u, 0u, 0u, 0u};
+  bool found = false;
+#pragma unroll
+  for (uint32_t t = 0; t < (uint32_t)kRcLevels; ++t) {  // shallower levels, deepest first
+    if (found || t <= st || t >= P.rc_ntab) continue;
+    RcHit h{EMPTY, 0u, 0u, 0u, 0u};
+    const uint32_t res = rc_probe(P.rc_tab[t], K.c, K.enc, K.ok, s, S, QCAP, t, h);
+    if (res == 1u || res == 2u) {
+      r = h;
+      found = true;
+    }
+  }
+  return r;
+}
 
 // The cache builds' parent lookups, one thread per key ahead of the build (rc_bhits / rc_bpops): in
 // the build kernel itself the lookup's registers and arrays raised the window loop's pressure (spills
@@ -2690,11 +2748,18 @@ __device__ __forceinline__ bool flush_final(const SearchParams& P, bool resumed,
 // A wave takes whole regions from a work counter (counters[10]). Keeps the lookup's registers out of
 // the search kernels.
 __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
+  // per wave: region offsets of windows whose start-level chain found nothing, probed on the
+  // shallower levels once 64 of them are queued (or at the region's end) -- a full wave's round trip
+  // instead of one for every 64 windows that hold a few such lanes (C2: 17 % of windows, C3: 30 %)
+  __shared__ uint16_t s_dq[4][128];
+  uint16_t* dq = s_dq[threadIdx.x / 64];
   const uint32_t lane = lane_id();
   uint64_t cached_lane = 0;
   uint32_t res_lane = 0, triv_lane = 0;
   unsigned err = 0;
   const uint64_t n_reg = (P.total_windows + RC_REGION - 1) / RC_REGION;
+  const uint32_t st = rc_start_level(P);
+  const bool shallower = st + 1 < P.rc_ntab;
   for (;;) {
     unsigned long long rg = 0;
     if (lane == 0) rg = atomicAdd(P.counters + 10, 1ull);
@@ -2702,39 +2767,79 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
     if (rg >= n_reg) break;
     const uint64_t rbase = rg * RC_REGION;
     uint32_t n_open = 0;  // wave-uniform
-    for (uint32_t it = 0; it < RC_REGION; it += 64) {
-    const uint64_t v = rbase + it + lane;  // whole waves iterate together (ballots, DPP scans)
-    bool active = v < P.total_windows;
-    uint32_t kl = 0;
-    uint64_t start = 0;
-    if (active) {
-      kl = find_seg(P, v);
-      const SegDesc S = P.segs[kl];
-      start = S.w_begin + (v - P.seg_prefix[kl]);
-      active = !window_skipped(P, S, start, err) && window_owned_kp(P, S, start, err);
-    }
-    RcHit hit{EMPTY, 0u, 0u, 0u, 0u};
-    if (active) hit = rc_lookup(P, P.segs[kl], start, P.rc_qcap);
-    const bool resumed = active && hit.off != EMPTY;
-    res_lane += resumed ? 1u : 0u;
-    if (P.lane_debug) {  // diagnostics: windows by the level they resume from (x final), misses, skips
-      const uint32_t cat = !(v < P.total_windows) ? 15u : !active ? 13u : !resumed ? 12u : hit.lvl * 2u + (hit.tail == hit.head ? 1u : 0u);
-      for (uint32_t c = 0; c < 14; ++c) {
-        const uint64_t m = __ballot(cat == c);
-        if (m && lane == 0) atomicAdd(&g_lk_dbg[c], (unsigned long long)__popcll(m));
+    uint32_t nq = 0;      // wave-uniform: deferred windows queued
+    // a window's outcome: finished here (flush_final) or stored open for the searches
+    auto settle = [&](bool active, const RcHit& hit, uint32_t kl, uint64_t start, uint64_t v, uint32_t off) {
+      const bool resumed = active && hit.off != EMPTY;
+      res_lane += resumed ? 1u : 0u;
+      if (P.lane_debug) {  // diagnostics: windows by the level they resume from (x final), misses, skips
+        const uint32_t cat = !active ? 13u : !resumed ? 12u : hit.lvl * 2u + (hit.tail == hit.head ? 1u : 0u);
+        for (uint32_t c = 0; c < 14; ++c) {
+          const uint64_t m = __ballot(cat == c && off != 0xFFFFu);
+          if (m && lane == 0) atomicAdd(&g_lk_dbg[c], (unsigned long long)__popcll(m));
+        }
       }
+      const bool fin = flush_final(P, resumed, hit, kl, start, v, cached_lane, triv_lane);
+      const bool open = active && !fin;
+      const uint64_t om = __ballot(open);
+      if (open) {
+        const uint64_t e = rbase + n_open + prefix_below(om);
+        P.rc_hits[e] = make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel);
+        P.rc_hit_pops[e] = hit.pops;
+        P.rc_voff[e] = off;
+      }
+      n_open += (uint32_t)__popcll(om);
+    };
+    auto drain = [&](bool all) {
+      while (nq >= 64 || (all && nq > 0)) {
+        const uint32_t take = min(nq, 64u);
+        __builtin_amdgcn_wave_barrier();
+        const bool act = lane < take;
+        const uint32_t off = act ? (uint32_t)dq[nq - take + lane] : 0xFFFFu;
+        __builtin_amdgcn_wave_barrier();
+        nq -= take;
+        uint32_t kl = 0;
+        uint64_t start = 0;
+        const uint64_t v = rbase + (act ? off : 0u);
+        RcHit hit{EMPTY, 0u, 0u, 0u, 0u};
+        if (act) {
+          kl = find_seg(P, v);
+          const SegDesc S = P.segs[kl];
+          start = S.w_begin + (v - P.seg_prefix[kl]);
+          RcKey K;
+          rc_key_of(P, S, start, K);
+          hit = rc_lookup_shallow(P, S, start, P.rc_qcap, K, st);
+        }
+        settle(act, hit, kl, start, v, act ? off : 0xFFFFu);
+      }
+    };
+    for (uint32_t it = 0; it < RC_REGION; it += 64) {
+      const uint64_t v = rbase + it + lane;  // whole waves iterate together (ballots, DPP scans)
+      bool active = v < P.total_windows;
+      uint32_t kl = 0;
+      uint64_t start = 0;
+      if (active) {
+        kl = find_seg(P, v);
+        const SegDesc S = P.segs[kl];
+        start = S.w_begin + (v - P.seg_prefix[kl]);
+        active = !window_skipped(P, S, start, err) && window_owned_kp(P, S, start, err);
+      }
+      RcHit hit{EMPTY, 0u, 0u, 0u, 0u};
+      bool found = false;
+      if (active) {
+        const SegDesc S = P.segs[kl];
+        RcKey K;
+        rc_key_of(P, S, start, K);
+        hit = rc_lookup_deep(P, S, start, P.rc_qcap, K, st, found);
+      }
+      const bool defer = active && !found && shallower;
+      const uint64_t dm = __ballot(defer);
+      if (defer) dq[nq + prefix_below(dm)] = (uint16_t)(it + lane);
+      nq += (uint32_t)__popcll(dm);
+      settle(active && !defer, hit, kl, start, v, (v < P.total_windows && !defer) ? it + lane : 0xFFFFu);
+      if (nq >= 64) drain(false);
     }
-    const bool fin = flush_final(P, resumed, hit, kl, start, v, cached_lane, triv_lane);
-    const bool open = active && !fin;
-    const uint64_t om = __ballot(open);
-    if (open) {
-      const uint64_t e = rbase + n_open + prefix_below(om);
-      P.rc_hits[e] = make_uint4(hit.off, hit.head, hit.tail, hit.nv_nel);
-      P.rc_hit_pops[e] = hit.pops;
-      P.rc_voff[e] = it + lane;
-    }
-    n_open += (uint32_t)__popcll(om);
-    }
+    drain(true);
     if (lane == 0) P.rc_region_cnt[rg] = n_open;
   }
   wave_add_counter(P.counters + 4, cached_lane);
