@@ -292,6 +292,10 @@ struct SearchParams {
   // key partition of the haystack's start windows (Haystack::kparts / kpart), last: fields added
   // in the middle moved every later kernel argument and changed the window kernels' allocation
   uint32_t kp_n, kp_r;
+  // the key part's start windows, ascending (rc_count_kernel / rc_lookup_kernel walk them; the
+  // lookup stores each open window as its list region's base + offset, so the searches' entry ->
+  // window mapping needs no list)
+  const uint64_t* kp_wlist;
 };
 
 constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8u, ERR_OUT = 16u, ERR_SPILL = 32u;

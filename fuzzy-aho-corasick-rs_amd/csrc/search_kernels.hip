@@ -2586,20 +2586,53 @@ __device__ __forceinline__ void rc_count_insert(const RcCountTarget& T, uint64_t
 }
 // Up to three levels are counted in one pass over the windows (level 1; the sampled levels): their
 // inserts go out together and the window's text is read once.
-// Key partition without the prefix cache: the part's windows listed (the main pass then walks the
-// list; the ownership test stays out of the window loop, whose registers it would have crowded)
-__global__ __launch_bounds__(256) void kp_list_kernel(SearchParams P, uint64_t* list, unsigned long long* n) {
+// The key part's start windows, listed in ascending order (count per block of KP_CHUNK windows, host
+// scan, then each block writes its windows at its offset in window order). The count, lookup and
+// cache-off searches then walk the part's windows only; the ownership test stays out of the window
+// loops, whose registers it would crowd.
+constexpr uint32_t KP_CHUNK = 4096;
+__device__ __forceinline__ bool kp_owned_window(const SearchParams& P, uint64_t v) {
   unsigned err = 0;
-  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < P.total_windows;
-       v += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t kl = find_seg(P, v);
-    const SegDesc S = P.segs[kl];
-    const bool own = window_owned_kp(P, S, S.w_begin + (v - P.seg_prefix[kl]), err);
+  const uint32_t kl = find_seg(P, v);
+  const SegDesc S = P.segs[kl];
+  return window_owned_kp(P, S, S.w_begin + (v - P.seg_prefix[kl]), err);
+}
+__global__ __launch_bounds__(256) void kp_count_kernel(SearchParams P, uint32_t* bcount) {
+  __shared__ uint32_t s_n;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const uint64_t b0 = (uint64_t)blockIdx.x * KP_CHUNK;
+  uint32_t n = 0;
+  for (uint32_t r = threadIdx.x; r < KP_CHUNK; r += 256) {
+    const uint64_t v = b0 + r;
+    if (v < P.total_windows && kp_owned_window(P, v)) ++n;
+  }
+  n = (uint32_t)__popcll(__ballot(n & 1u)) + 2u * (uint32_t)__popcll(__ballot(n & 2u)) +
+      4u * (uint32_t)__popcll(__ballot(n & 4u)) + 8u * (uint32_t)__popcll(__ballot(n & 8u)) +
+      16u * (uint32_t)__popcll(__ballot(n & 16u));  // n <= 16 per thread
+  if (lane_id() == 0) atomicAdd(&s_n, n);
+  __syncthreads();
+  if (threadIdx.x == 0) bcount[blockIdx.x] = s_n;
+}
+__global__ __launch_bounds__(256) void kp_write_kernel(SearchParams P, const uint64_t* boff, uint64_t* list) {
+  __shared__ uint32_t s_w[4];
+  const uint64_t b0 = (uint64_t)blockIdx.x * KP_CHUNK;
+  uint64_t at = boff[blockIdx.x];
+  const uint32_t wv = threadIdx.x / 64;
+  for (uint32_t r = 0; r < KP_CHUNK; r += 256) {  // rounds of 256 windows, in window order
+    const uint64_t v = b0 + r + threadIdx.x;
+    const bool own = v < P.total_windows && kp_owned_window(P, v);
     const uint64_t m = __ballot(own);
-    unsigned long long b = 0;
-    if (m && lane_id() == (uint32_t)first_lane(m)) b = atomicAdd(n, (unsigned long long)__popcll(m));
-    b = __shfl(b, first_lane(m ? m : 1ull));
-    if (own) list[b + prefix_below(m)] = v;
+    if (lane_id() == 0) s_w[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (uint32_t x = 0; x < 4; ++x) {
+      before += x < wv ? s_w[x] : 0u;
+      tot += s_w[x];
+    }
+    if (own) list[at + before + prefix_below(m)] = v;
+    at += tot;
+    __syncthreads();
   }
 }
 
@@ -2609,11 +2642,11 @@ __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, RcCountTa
   unsigned err = 0;
   const uint64_t ns = (P.total_windows + stride - 1) / stride;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gstride) {
-    const uint64_t vid = i * stride;
+    const uint64_t vid = P.kp_wlist ? P.kp_wlist[i * stride] : i * stride;  // a key part: its windows
     const uint32_t kl = find_seg(P, vid);
     const SegDesc S = P.segs[kl];
     const uint64_t start = S.w_begin + (vid - P.seg_prefix[kl]);
-    if (window_skipped(P, S, start, err) || !window_owned_kp(P, S, start, err)) continue;
+    if (window_skipped(P, S, start, err)) continue;
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       const RcCountTarget& T = t == 0 ? t0 : t == 1 ? t1 : t2;
@@ -2769,13 +2802,14 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
     uint32_t n_open = 0;  // wave-uniform
     uint32_t nq = 0;      // wave-uniform: deferred windows queued
     // a window's outcome: finished here (flush_final) or stored open for the searches
+    // off: the window's offset from the region base (its voff), 0xFFFFFFFF for no window
     auto settle = [&](bool active, const RcHit& hit, uint32_t kl, uint64_t start, uint64_t v, uint32_t off) {
       const bool resumed = active && hit.off != EMPTY;
       res_lane += resumed ? 1u : 0u;
       if (P.lane_debug) {  // diagnostics: windows by the level they resume from (x final), misses, skips
         const uint32_t cat = !active ? 13u : !resumed ? 12u : hit.lvl * 2u + (hit.tail == hit.head ? 1u : 0u);
         for (uint32_t c = 0; c < 14; ++c) {
-          const uint64_t m = __ballot(cat == c && off != 0xFFFFu);
+          const uint64_t m = __ballot(cat == c && off != 0xFFFFFFFFu);
           if (m && lane == 0) atomicAdd(&g_lk_dbg[c], (unsigned long long)__popcll(m));
         }
       }
@@ -2795,12 +2829,13 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
         const uint32_t take = min(nq, 64u);
         __builtin_amdgcn_wave_barrier();
         const bool act = lane < take;
-        const uint32_t off = act ? (uint32_t)dq[nq - take + lane] : 0xFFFFu;
+        const uint32_t qo = act ? (uint32_t)dq[nq - take + lane] : 0u;
         __builtin_amdgcn_wave_barrier();
         nq -= take;
         uint32_t kl = 0;
         uint64_t start = 0;
-        const uint64_t v = rbase + (act ? off : 0u);
+        const uint64_t v = P.kp_wlist ? (act ? P.kp_wlist[rbase + qo] : rbase) : rbase + qo;
+        const uint32_t off = act ? (uint32_t)(v - rbase) : 0xFFFFFFFFu;
         RcHit hit{EMPTY, 0u, 0u, 0u, 0u};
         if (act) {
           kl = find_seg(P, v);
@@ -2810,19 +2845,22 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
           rc_key_of(P, S, start, K);
           hit = rc_lookup_shallow(P, S, start, P.rc_qcap, K, st);
         }
-        settle(act, hit, kl, start, v, act ? off : 0xFFFFu);
+        settle(act, hit, kl, start, v, off);
       }
     };
     for (uint32_t it = 0; it < RC_REGION; it += 64) {
-      const uint64_t v = rbase + it + lane;  // whole waves iterate together (ballots, DPP scans)
-      bool active = v < P.total_windows;
+      const uint64_t e = rbase + it + lane;  // whole waves iterate together (ballots, DPP scans)
+      bool active = e < P.total_windows;
+      // the window: the entry itself, or a key part's e-th window (ascending, so v >= e and the
+      // stored offset v - rbase maps back through the searches' rc_window_of)
+      const uint64_t v = (P.kp_wlist && active) ? P.kp_wlist[e] : e;
       uint32_t kl = 0;
       uint64_t start = 0;
       if (active) {
         kl = find_seg(P, v);
         const SegDesc S = P.segs[kl];
         start = S.w_begin + (v - P.seg_prefix[kl]);
-        active = !window_skipped(P, S, start, err) && window_owned_kp(P, S, start, err);
+        active = !window_skipped(P, S, start, err);
       }
       RcHit hit{EMPTY, 0u, 0u, 0u, 0u};
       bool found = false;
@@ -2836,7 +2874,7 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
       const uint64_t dm = __ballot(defer);
       if (defer) dq[nq + prefix_below(dm)] = (uint16_t)(it + lane);
       nq += (uint32_t)__popcll(dm);
-      settle(active && !defer, hit, kl, start, v, (v < P.total_windows && !defer) ? it + lane : 0xFFFFu);
+      settle(active && !defer, hit, kl, start, v, (e < P.total_windows && !defer) ? (uint32_t)(v - rbase) : 0xFFFFFFFFu);
       if (nq >= 64) drain(false);
     }
     drain(true);
@@ -4665,7 +4703,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     segs.push_back(c);
     prefix.push_back(prefix.back() + (c.w_end - c.w_begin));
   }
-  const uint64_t windows = prefix.back();
+  uint64_t windows = prefix.back();  // (a key part: its own windows, set once they are listed)
   if (windows == 0) return FAC_OK;
 
   SearchParams P{};
@@ -4865,6 +4903,36 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   P.segs = static_cast<const SegDesc*>(d_segs.p);
   P.seg_prefix = static_cast<const uint64_t*>(d_prefix.p);
   P.win_list = nullptr;
+  P.kp_wlist = nullptr;
+  // a key part (Haystack::kparts): its windows listed in ascending order; from here on `windows`
+  // counts them (the cache policy, lookups and searches see the part alone)
+  PoolBuf d_kpl, d_kpc;
+  if (P.kp_n > 1) {
+    const uint64_t nb = (windows + KP_CHUNK - 1) / KP_CHUNK;
+    HIP_TRY(d_kpl.alloc(windows * sizeof(uint64_t), stream));
+    HIP_TRY(d_kpc.alloc(nb * 12, stream));  // counts (u32), then offsets (u64)
+    P.total_windows = windows;
+    hipLaunchKernelGGL(kp_count_kernel, dim3((uint32_t)nb), dim3(256), 0, stream, P, static_cast<uint32_t*>(d_kpc.p));
+    HIP_TRY(hipGetLastError());
+    std::vector<uint32_t> bc(nb);
+    HIP_TRY(hipMemcpyAsync(bc.data(), d_kpc.p, nb * 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    std::vector<uint64_t> bo(nb);
+    uint64_t tot = 0;
+    for (uint64_t b = 0; b < nb; ++b) {
+      bo[b] = tot;
+      tot += bc[b];
+    }
+    uint64_t* d_bo = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(d_kpc.p) + ((nb * 4 + 7) & ~7ull));
+    HIP_TRY(hipMemcpyAsync(d_bo, bo.data(), nb * 8, hipMemcpyHostToDevice, stream));
+    hipLaunchKernelGGL(kp_write_kernel, dim3((uint32_t)nb), dim3(256), 0, stream, P, d_bo, static_cast<uint64_t*>(d_kpl.p));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(stream));  // (bo is pageable host memory)
+    windows = tot;
+    P.total_windows = windows;
+    P.kp_wlist = static_cast<const uint64_t*>(d_kpl.p);
+    if (windows == 0) return FAC_OK;
+  }
 
   int rc = FAC_OK;
   uint64_t retries = 0, launches = 0, popped = 0, cached_pops = 0, pass_windows = windows;
@@ -5396,18 +5464,8 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   const uint32_t rc_chunk = (uint32_t)std::min<unsigned long>(4096, std::max<unsigned long>(1,
       diag_env("FAC_RC_CHUNK") ? std::strtoul(diag_env("FAC_RC_CHUNK"), nullptr, 10) : rc_auto));
   bool kp_listed = false;  // the main pass walks the key part's window list (no prefix cache)
-  if (P.rc_mode == 0 && P.kp_n > 1) {
-    HIP_TRY(d_list.alloc(windows * sizeof(uint64_t), stream));
-    HIP_TRY(hipMemsetAsync(d_cnt.p, 0, sizeof(unsigned long long), stream));
-    P.total_windows = windows;
-    hipLaunchKernelGGL(kp_list_kernel, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((windows + 255) / 256, (uint64_t)cus * 8))),
-                       dim3(256), 0, stream, P, static_cast<uint64_t*>(d_list.p), static_cast<unsigned long long*>(d_cnt.p));
-    HIP_TRY(hipGetLastError());
-    unsigned long long nk = 0;
-    HIP_TRY(hipMemcpyAsync(&nk, d_cnt.p, sizeof(nk), hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    pass_windows = nk;
-    P.win_list = static_cast<const uint64_t*>(d_list.p);
+  if (P.rc_mode == 0 && P.kp_wlist) {
+    P.win_list = P.kp_wlist;
     kp_listed = true;
   }
   for (;;) {
