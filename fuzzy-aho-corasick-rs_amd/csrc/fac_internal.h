@@ -296,6 +296,9 @@ struct SearchParams {
   // lookup stores each open window as its list region's base + offset, so the searches' entry ->
   // window mapping needs no list)
   const uint64_t* kp_wlist;
+  // dense start-level key bitmaps (rc_dense_*_kernel, search_kernels.hip): rank table, alphabet size,
+  // "final without records" and "cached" bits over the keys of ranked characters; null: none
+  const uint32_t* rc_dense;
 };
 
 constexpr unsigned ERR_QUEUE = 1u, ERR_VISITED = 2u, ERR_EMIT = 4u, ERR_HALO = 8u, ERR_OUT = 16u, ERR_SPILL = 32u;

@@ -2538,6 +2538,121 @@ __global__ __launch_bounds__(256) void rc_publish_kernel(SearchParams P, const u
   }
 }
 
+// Dense start-level bitmaps (P.rc_dense). Most windows' start-level snapshot is final without
+// records (C2: 732 M of 1.07 G windows), and the lookup learns that from a random line of a lookup
+// table of up to 256 MB. Over an alphabet of the A most frequent ASCII characters of such keys
+// (A^k <= 2^24), a key of ranked characters has a dense index, and two bitmaps of at most 2 MB each
+// (L2-resident) answer the common cases: bit F -- the key's snapshot is final with no records, so the
+// window is done (a final snapshot is a property of the key: no window starting with it reads past
+// it, and it holds no match); bit C -- the key has a snapshot at this level at all (clear: the probe
+// would miss, so the window goes straight to the shallower levels). F is exact; C is a hint (a set
+// bit whose key is not in the table only costs the probe). Keys with an unranked character, and
+// windows too close to the text end or the halo (their chars read as RC_PAD), take the probes.
+// Words: [0, 32) rank bytes (0xFF: unranked), [32] A (0: off), [33] k, [64, 192) the histogram,
+// [RC_DENSE_F, +2^19) bits F, [RC_DENSE_C, +2^19) bits C.
+constexpr uint32_t RC_DENSE_LOG2 = 24, RC_DENSE_F = 256, RC_DENSE_C = RC_DENSE_F + (1u << (RC_DENSE_LOG2 - 5));
+constexpr size_t RC_DENSE_WORDS = RC_DENSE_C + (1u << (RC_DENSE_LOG2 - 5));
+__device__ __forceinline__ bool rc_dense_entry(const SearchParams& P, const uint64_t* reps, const uint4* pool,
+                                               const uint32_t* off, const uint32_t* count, uint32_t ent, uint32_t k,
+                                               uint32_t c[8], bool& fin_empty) {
+  if (count[ent] == EMPTY) return false;
+  const uint32_t o = off[ent];
+  const uint4 h0 = pool[o], h1 = pool[o + 1];
+  fin_empty = h0.y == h0.x && h1.x == 0u;  // rc_publish_kernel: nq = 0, ne = 0
+  const uint64_t wid = reps[ent];
+  const uint32_t kl = find_seg(P, wid);
+  const SegDesc S = P.segs[kl];
+  if (!rc_chars(P, S, S.w_begin + (wid - P.seg_prefix[kl]), k, c)) return false;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i)
+    if (i < k && c[i] >= 128u) return false;  // RC_PAD included
+  return true;
+}
+// character histogram of the level's final record-less keys (ASCII keys only)
+__global__ __launch_bounds__(256) void rc_dense_hist_kernel(SearchParams P, const uint64_t* reps, const uint4* pool,
+                                                            const uint32_t* off, const uint32_t* count, uint32_t n_ent,
+                                                            uint32_t k, uint32_t* dense) {
+  __shared__ uint32_t h[128];
+  if (threadIdx.x < 128) h[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t n_fe = 0, n_cached = 0;
+  for (uint32_t ent = blockIdx.x * blockDim.x + threadIdx.x; ent < n_ent; ent += gridDim.x * blockDim.x) {
+    uint32_t c[8];
+    bool fe = false;
+    n_cached += count[ent] != EMPTY ? 1u : 0u;
+    if (!rc_dense_entry(P, reps, pool, off, count, ent, k, c, fe) || !fe) continue;
+    ++n_fe;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i)
+      if (i < k) atomicAdd(&h[c[i]], 1u);  // LDS
+  }
+  __syncthreads();
+  if (threadIdx.x < 128 && h[threadIdx.x]) atomicAdd(&dense[64 + threadIdx.x], h[threadIdx.x]);
+  if (n_fe) atomicAdd(&dense[36], n_fe);
+  if (n_cached) atomicAdd(&dense[37], n_cached);
+}
+// ranks by descending count (ties: lower character first), A = the most with A^k <= 2^24; one block
+// of 128 threads, one character each
+// (A = 0 -- no bitmaps -- when fewer than min_pm per mille of the cached keys are ASCII and final
+// without records: C3 finishes 1.5 % of its windows through them, not worth the lookups' test)
+__global__ __launch_bounds__(128) void rc_dense_rank_kernel(uint32_t k, uint32_t min_pm, uint32_t* dense) {
+  __shared__ uint32_t h[128];
+  const uint32_t ch = threadIdx.x;
+  h[ch] = dense[64 + ch];
+  __syncthreads();
+  const uint32_t v = h[ch];
+  uint32_t r = 0, used = 0;
+  for (uint32_t o = 0; o < 128; ++o) {
+    const uint32_t w = h[o];
+    r += (w > v || (w == v && o < ch)) ? 1u : 0u;
+    used += w ? 1u : 0u;
+  }
+  uint32_t A = 0;
+  for (;;) {
+    uint64_t p = 1;
+    for (uint32_t i = 0; i < k && p <= (1ull << RC_DENSE_LOG2); ++i) p *= (uint64_t)(A + 1);
+    if (A + 1 > used || p > (1ull << RC_DENSE_LOG2)) break;
+    ++A;
+  }
+  if (A < 2 || (uint64_t)dense[36] * 1000u < (uint64_t)dense[37] * min_pm) A = 0;
+  reinterpret_cast<uint8_t*>(dense)[ch] = (v && r < A) ? (uint8_t)r : (uint8_t)0xFF;
+  if (ch == 0) {
+    dense[32] = A;
+    dense[33] = k;
+  }
+}
+// dense index of a key: its ranks as base-A digits, first character most significant (Horner), so
+// the next window's index slides: (idx - r0 * A^(k-1)) * A + r_k (dl_tile)
+__device__ __forceinline__ bool rc_dense_index(const uint8_t* rank, uint32_t A, uint32_t k, const uint32_t c[8],
+                                               uint32_t& idx) {
+  idx = 0;
+  bool ok = true;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) {
+    if (i >= k) continue;
+    const uint32_t r = c[i] < 128u ? (uint32_t)rank[c[i]] : 0xFFu;
+    ok = ok && r < A;
+    idx = __umul24(idx, A) + (r < A ? r : 0u);
+  }
+  return ok;
+}
+__global__ __launch_bounds__(256) void rc_dense_fill_kernel(SearchParams P, const uint64_t* reps, const uint4* pool,
+                                                            const uint32_t* off, const uint32_t* count, uint32_t n_ent,
+                                                            uint32_t k, uint32_t* dense) {
+  __shared__ uint8_t s_rank[128];
+  if (threadIdx.x < 128) s_rank[threadIdx.x] = reinterpret_cast<const uint8_t*>(dense)[threadIdx.x];
+  __syncthreads();
+  const uint32_t A = dense[32];
+  if (A == 0) return;
+  for (uint32_t ent = blockIdx.x * blockDim.x + threadIdx.x; ent < n_ent; ent += gridDim.x * blockDim.x) {
+    uint32_t c[8], idx = 0;
+    bool fe = false;
+    if (!rc_dense_entry(P, reps, pool, off, count, ent, k, c, fe) || !rc_dense_index(s_rank, A, k, c, idx)) continue;
+    atomicOr(&dense[RC_DENSE_C + (idx >> 5)], 1u << (idx & 31u));
+    if (fe) atomicOr(&dense[RC_DENSE_F + (idx >> 5)], 1u << (idx & 31u));
+  }
+}
+
 // Prefix-cache keys: every `stride`-th window's key is inserted and counted (level 1: every window,
 // sampled levels: a sample); the first inserter of a key is its representative. Counts saturate
 // at `sat` (only "at least thr" is asked), so a frequent key is not one hot atomic per window.
@@ -2633,6 +2748,213 @@ __global__ __launch_bounds__(256) void kp_write_kernel(SearchParams P, const uin
     if (own) list[at + before + prefix_below(m)] = v;
     at += tot;
     __syncthreads();
+  }
+}
+
+// The windows the dense bitmaps leave open (bit F clear), listed in ascending order ahead of the
+// main lookups, which then walk the list as they walk a key part's (P.kp_wlist; the source is the
+// key part's list or every window): C2 lists 0.34 G of its 1.07 G windows. Per block of KP_CHUNK
+// source windows one 64-bit mask per wave round (window b0 + 64 m + lane), the block's count, then a
+// one-block scan and the writes.
+// F-done test of one window (the lookup's dense check: chars past the text or the halo are RC_PAD,
+// unranked)
+__device__ __forceinline__ bool dl_window_done(const SearchParams& P, const uint8_t* rank, uint32_t A, uint32_t k, uint64_t v) {
+  const uint32_t kl = find_seg(P, v);
+  const SegDesc S = P.segs[kl];
+  uint32_t c[8], idx = 0;
+  (void)rc_chars(P, S, S.w_begin + (v - P.seg_prefix[kl]), k, c);
+  return rc_dense_index(rank, A, k, c, idx) && ((P.rc_dense[RC_DENSE_F + (idx >> 5)] >> (idx & 31u)) & 1u);
+}
+// a thread's 16 consecutive windows of a staged tile (ranks s_r, 0xFF unranked): bit w of the result
+// set when window b0 + 16 t + w exists and the bitmaps do not finish it
+template <uint32_t K>
+__device__ __forceinline__ uint32_t dl_tile(const SearchParams& P, const uint8_t* s_r, uint32_t A, uint64_t b0, uint64_t last) {
+  uint32_t rw[6];
+#pragma unroll
+  for (uint32_t x = 0; x < 6; ++x) rw[x] = reinterpret_cast<const uint32_t*>(s_r)[threadIdx.x * 4u + x];
+  uint32_t r[16 + K - 1], bad = 0;
+#pragma unroll
+  for (uint32_t p = 0; p < 16 + K - 1; ++p) {
+    const uint32_t v = (rw[p >> 2] >> ((p & 3u) * 8u)) & 0xFFu;
+    bad |= v < A ? 0u : 1u << p;
+    r[p] = v < A ? v : 0u;
+  }
+  uint32_t top = 1;  // A^(K-1)
+#pragma unroll
+  for (uint32_t i = 1; i < K; ++i) top = __umul24(top, A);
+  uint32_t idx[16];
+  uint32_t x = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < K; ++i) x = __umul24(x, A) + r[i];
+  idx[0] = x;
+#pragma unroll
+  for (uint32_t w = 1; w < 16; ++w) {
+    x = __umul24(x - __umul24(r[w - 1], top), A) + r[w + K - 1];
+    idx[w] = x;
+  }
+  const uint64_t q0 = b0 + threadIdx.x * 16ull;
+  uint32_t okm = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < 16; ++w) okm |= (((bad >> w) & ((1u << K) - 1u)) == 0u && q0 + w <= last) ? 1u << w : 0u;
+  uint32_t bw[16];
+#pragma unroll
+  for (uint32_t w = 0; w < 16; ++w) bw[w] = ((okm >> w) & 1u) ? P.rc_dense[RC_DENSE_F + (idx[w] >> 5)] : 0u;
+  uint32_t pat = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < 16; ++w) {
+    const bool done = ((okm >> w) & 1u) && ((bw[w] >> (idx[w] & 31u)) & 1u);
+    pat |= (q0 + w <= last && !done) ? 1u << w : 0u;
+  }
+  return pat;
+}
+__global__ __launch_bounds__(256) void dl_mask_kernel(SearchParams P, unsigned long long* masks, uint32_t* bcount) {
+  __shared__ uint8_t s_rank[128];
+  __shared__ __attribute__((aligned(16))) uint8_t s_r[KP_CHUNK + 32];  // the tile's character ranks
+  __shared__ uint32_t s_pat[256];
+  __shared__ uint32_t s_n;
+  if (threadIdx.x < 128) s_rank[threadIdx.x] = reinterpret_cast<const uint8_t*>(P.rc_dense)[threadIdx.x];
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const uint32_t A = P.rc_dense[32], k = P.rc_dense[33];
+  const uint64_t b0 = (uint64_t)blockIdx.x * KP_CHUNK;
+  const uint64_t last = min(b0 + KP_CHUNK, P.total_windows) - 1;
+  const uint32_t kl = find_seg(P, b0);
+  uint32_t n = 0;
+  if (!P.kp_wlist && find_seg(P, last) == kl) {
+    // one segment: stage the ranks of the tile's chars (coalesced), then 16 consecutive windows a
+    // thread, their bitmap words loaded together
+    const SegDesc S = P.segs[kl];
+    const uint64_t s0 = S.w_begin + (b0 - P.seg_prefix[kl]);
+    constexpr uint32_t kLoads = (KP_CHUNK + 32 + 255) / 256;
+    uint32_t cs[kLoads];
+    const uint64_t jmax = min(S.n, S.avail);
+    if (S.ascii) {  // every load issued before the first is used
+#pragma unroll
+      for (uint32_t u = 0; u < kLoads; ++u) {
+        const uint64_t j = s0 + threadIdx.x + u * 256u;
+        cs[u] = j < jmax ? (uint32_t)P.utf8[S.text_base + j] : RC_PAD;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kLoads; ++u)
+        if (P.case_insensitive && cs[u] - 'A' < 26u) cs[u] += 32u;
+    } else {
+#pragma unroll
+      for (uint32_t u = 0; u < kLoads; ++u) {
+        const uint64_t j = s0 + threadIdx.x + u * 256u;
+        cs[u] = j < jmax ? P.text32[S.text_base + j] : RC_PAD;
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kLoads; ++u) {
+      const uint32_t q = threadIdx.x + u * 256u;
+      if (q < KP_CHUNK + 32) s_r[q] = cs[u] < 128u ? s_rank[cs[u]] : (uint8_t)0xFF;
+    }
+    __syncthreads();
+    uint32_t pat = 0;
+    switch (k) {
+      case 2: pat = dl_tile<2>(P, s_r, A, b0, last); break;
+      case 3: pat = dl_tile<3>(P, s_r, A, b0, last); break;
+      case 4: pat = dl_tile<4>(P, s_r, A, b0, last); break;
+      case 5: pat = dl_tile<5>(P, s_r, A, b0, last); break;
+      case 6: pat = dl_tile<6>(P, s_r, A, b0, last); break;
+      case 7: pat = dl_tile<7>(P, s_r, A, b0, last); break;
+      default: pat = dl_tile<8>(P, s_r, A, b0, last); break;
+    }
+    s_pat[threadIdx.x] = pat;
+    __syncthreads();
+    if (threadIdx.x < 64) {  // mask m: windows 64 m .. 64 m + 63 = threads 4 m .. 4 m + 3
+      const uint32_t m = threadIdx.x;
+      const unsigned long long mk = (unsigned long long)s_pat[4 * m] | ((unsigned long long)s_pat[4 * m + 1] << 16) |
+                                    ((unsigned long long)s_pat[4 * m + 2] << 32) | ((unsigned long long)s_pat[4 * m + 3] << 48);
+      masks[(uint64_t)blockIdx.x * (KP_CHUNK / 64) + m] = mk;
+      n = (uint32_t)__popcll(mk);
+    }
+  } else {
+    for (uint32_t r = 0; r < KP_CHUNK; r += 256) {
+      const uint64_t i = b0 + r + threadIdx.x;
+      const bool keep = i <= last && !dl_window_done(P, s_rank, A, k, P.kp_wlist ? P.kp_wlist[i] : i);
+      const unsigned long long m = __ballot(keep);
+      if (lane_id() == 0) {
+        masks[(uint64_t)blockIdx.x * (KP_CHUNK / 64) + (r + threadIdx.x) / 64] = m;
+        n += (uint32_t)__popcll(m);
+      }
+    }
+  }
+  if (n) atomicAdd(&s_n, n);  // LDS
+  __syncthreads();
+  if (threadIdx.x == 0) bcount[blockIdx.x] = s_n;
+}
+// the share of F-done windows, from 16384 spread over the windows (dense[34..35], u64): the lookups
+// take the list only when it leaves enough out
+__global__ __launch_bounds__(256) void rc_dense_sample_kernel(SearchParams P, uint64_t windows) {
+  __shared__ uint8_t s_rank[128];
+  if (threadIdx.x < 128) s_rank[threadIdx.x] = reinterpret_cast<const uint8_t*>(P.rc_dense)[threadIdx.x];
+  __syncthreads();
+  const uint32_t A = P.rc_dense[32], k = P.rc_dense[33];
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, ns = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t i = g * windows / ns;
+  const bool done = A && i < windows && dl_window_done(P, s_rank, A, k, P.kp_wlist ? P.kp_wlist[i] : i);
+  const unsigned long long m = __ballot(done);
+  if (lane_id() == 0 && m)
+    atomicAdd(reinterpret_cast<unsigned long long*>(const_cast<uint32_t*>(P.rc_dense) + 34), (unsigned long long)__popcll(m));
+}
+__global__ __launch_bounds__(1024) void dl_scan_kernel(const uint32_t* bcount, uint64_t* boff, uint64_t nb,
+                                                       unsigned long long* total) {
+  __shared__ unsigned long long wsum[16];
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  const uint64_t per = ((nb + 1023) / 1024 + 7) & ~7ull;  // 8-entry runs: 16-byte aligned loads
+  const uint64_t a = min(nb, (uint64_t)t * per), b = min(nb, a + per);
+  unsigned long long sum = 0;
+  uint64_t i = a;
+  for (; i + 8 <= b; i += 8) {
+    const uint4 u0 = *reinterpret_cast<const uint4*>(bcount + i), u1 = *reinterpret_cast<const uint4*>(bcount + i + 4);
+    sum += (unsigned long long)u0.x + u0.y + u0.z + u0.w + u1.x + u1.y + u1.z + u1.w;
+  }
+  for (; i < b; ++i) sum += bcount[i];
+  unsigned long long x = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  if (t == 0) {
+    unsigned long long run = 0;
+    for (int i = 0; i < 16; ++i) {
+      const unsigned long long v = wsum[i];
+      wsum[i] = run;
+      run += v;
+    }
+    *total = run;
+  }
+  __syncthreads();
+  unsigned long long run = wsum[w] + x - sum;
+  for (uint64_t i = a; i < b; ++i) {
+    boff[i] = run;
+    run += bcount[i];
+  }
+}
+__global__ __launch_bounds__(256) void dl_write_kernel(SearchParams P, const unsigned long long* masks, const uint64_t* boff,
+                                                       uint64_t* list) {
+  __shared__ uint32_t s_pre[KP_CHUNK / 64];
+  const unsigned long long* bm = masks + (uint64_t)blockIdx.x * (KP_CHUNK / 64);
+  if (threadIdx.x < 64) {  // exclusive scan of the 64 masks' counts (one wave)
+    const uint32_t c = (uint32_t)__popcll(bm[threadIdx.x]);
+    uint32_t x = c;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (threadIdx.x >= (uint32_t)o) x += y;
+    }
+    s_pre[threadIdx.x] = x - c;
+  }
+  __syncthreads();
+  const uint64_t b0 = (uint64_t)blockIdx.x * KP_CHUNK, at = boff[blockIdx.x];
+  const uint32_t lane = lane_id();
+  for (uint32_t m = threadIdx.x / 64; m < KP_CHUNK / 64; m += 4) {
+    const unsigned long long mk = bm[m];
+    if (!((mk >> lane) & 1ull)) continue;
+    const uint64_t i = b0 + 64ull * m + lane;
+    list[at + s_pre[m] + prefix_below(mk)] = P.kp_wlist ? P.kp_wlist[i] : i;
   }
 }
 
@@ -2785,6 +3107,7 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
   // shallower levels once 64 of them are queued (or at the region's end) -- a full wave's round trip
   // instead of one for every 64 windows that hold a few such lanes (C2: 17 % of windows, C3: 30 %)
   __shared__ uint16_t s_dq[4][128];
+  __shared__ uint8_t s_rank[128];  // the dense bitmaps' character ranks (rc_dense_rank_kernel)
   uint16_t* dq = s_dq[threadIdx.x / 64];
   const uint32_t lane = lane_id();
   uint64_t cached_lane = 0;
@@ -2793,6 +3116,11 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
   const uint64_t n_reg = (P.total_windows + RC_REGION - 1) / RC_REGION;
   const uint32_t st = rc_start_level(P);
   const bool shallower = st + 1 < P.rc_ntab;
+  const uint32_t dA = P.rc_dense ? P.rc_dense[32] : 0u, dk = P.rc_dense ? P.rc_dense[33] : 0u;
+  if (dA) {
+    if (threadIdx.x < 128) s_rank[threadIdx.x] = reinterpret_cast<const uint8_t*>(P.rc_dense)[threadIdx.x];
+    __syncthreads();
+  }
   for (;;) {
     unsigned long long rg = 0;
     if (lane == 0) rg = atomicAdd(P.counters + 10, 1ull);
@@ -2863,18 +3191,35 @@ __global__ __launch_bounds__(256) void rc_lookup_kernel(SearchParams P) {
         active = !window_skipped(P, S, start, err);
       }
       RcHit hit{EMPTY, 0u, 0u, 0u, 0u};
-      bool found = false;
+      bool found = false, done = false;
       if (active) {
         const SegDesc S = P.segs[kl];
         RcKey K;
         rc_key_of(P, S, start, K);
-        hit = rc_lookup_deep(P, S, start, P.rc_qcap, K, st, found);
+        uint32_t idx = 0;
+        bool absent = false;
+        if (dA && rc_dense_index(s_rank, dA, dk, K.c, idx)) {  // the dense bitmaps (rc_dense_fill_kernel)
+          const uint32_t wf = P.rc_dense[RC_DENSE_F + (idx >> 5)], wc = P.rc_dense[RC_DENSE_C + (idx >> 5)];
+          done = (wf >> (idx & 31u)) & 1u;
+          absent = !((wc >> (idx & 31u)) & 1u);
+        }
+        if (!done && !absent) hit = rc_lookup_deep(P, S, start, P.rc_qcap, K, st, found);
+      }
+      if (P.lane_debug) {
+        const uint64_t m = __ballot(done);
+        if (m && lane == 0) atomicAdd(&g_lk_dbg[14], (unsigned long long)__popcll(m));
+      }
+      if (done) {  // final without records at the start level: nothing to write (flush_final's counts)
+        res_lane += 1;
+        triv_lane += 1;
+        active = false;
       }
       const bool defer = active && !found && shallower;
       const uint64_t dm = __ballot(defer);
       if (defer) dq[nq + prefix_below(dm)] = (uint16_t)(it + lane);
       nq += (uint32_t)__popcll(dm);
-      settle(active && !defer, hit, kl, start, v, (e < P.total_windows && !defer) ? (uint32_t)(v - rbase) : 0xFFFFFFFFu);
+      settle(active && !defer, hit, kl, start, v,
+             (e < P.total_windows && !defer && !done) ? (uint32_t)(v - rbase) : 0xFFFFFFFFu);
       if (nq >= 64) drain(false);
     }
     drain(true);
@@ -4826,6 +5171,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   DevBuf d_voff, d_rcnt;   // ... their windows and per-region counts
   DevBuf d_bhits, d_bpops; // prefix cache builds: the representatives' parent snapshots
   DevBuf d_slots, d_bsel;  // wave-slot rings (one per stream), beam-selection scratch
+  DevBuf d_dense;          // the start level's dense key bitmaps
   ScratchSet* bound = t_scratch;  // a streaming worker's own set, else the engine's
   std::unique_lock<std::mutex> lease(bound ? bound->mu : e.scratch_mu, std::try_to_lock);
   void** scratch_p = bound ? bound->p : e.scratch_p;
@@ -4845,6 +5191,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     bufs.push_back(&d_bsel);
     bufs.push_back(&d_bhits);
     bufs.push_back(&d_bpops);
+    bufs.push_back(&d_dense);
     static_assert(Engine::kScratch >= 31 + 5 * (kRcLevels - 1) + kRcLevels, "engine scratch slots");
     static_assert(ScratchSet::kSlots >= Engine::kScratch, "stream scratch slots");
     for (size_t i = 0; i < bufs.size(); ++i) bufs[i]->bind(&scratch_p[i], &scratch_n[i]);
@@ -4938,7 +5285,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   uint64_t retries = 0, launches = 0, popped = 0, cached_pops = 0, pass_windows = windows;
   unsigned long long cnt[N_COUNTERS] = {};
   float ms_total = 0.f, cache_ms = 0.f, lane_ms = 0.f;
-  uint64_t lane_windows = 0;
+  uint64_t lane_windows = 0, dense_done = 0;
   hipEvent_t ev_lane = nullptr;  // end of the lane-serial kernel (destroyed on return)
   struct EvGuard {
     hipEvent_t& e;
@@ -4971,6 +5318,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   RcTable L1{0u, 0u, nullptr, nullptr, nullptr, nullptr};
   uint32_t n_ent0 = 0, qbuild = 0;
   uint64_t ct_mult = 4, ct_mult2 = 4;  // lookup slots per entry: levels 0/1 by entries, sampled levels by kept snapshots
+  unsigned int* dense_w_host = nullptr;  // the dense bitmaps' sampled share of finished windows
+  unsigned int* dense_w_dev = nullptr;
+  uint32_t dense_pm = 0;
+  bool dense_list = false, dense_built = false;
   // after its build a level's entries are published into an exact-key lookup table (4 slots per
   // entry: a miss usually ends at the first probe)
   auto ct_slots = [&](uint32_t n_ent, uint64_t mult) {
@@ -5374,7 +5725,31 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
         }
         if ((brc = publish(Lx[x], n_entx[x], static_cast<const uint64_t*>(d_xrep[xbuf[x]].p), d_ct[1 + x], stream, false,
                            kept, ct_mult2))) return brc;
+        // the first sampled level is where the main lookups start (P.rc_kstart = level 1's k + 1)
+        if (x == 0 && P.rc_kstart == L1.k + 1 && !P.win_counts && P.rc_lane_flush && !diag_env("FAC_RC_NO_DENSE")) {
+          HIP_TRY(d_dense.alloc(RC_DENSE_WORDS * sizeof(uint32_t), stream));
+          HIP_TRY(hipMemsetAsync(d_dense.p, 0, RC_DENSE_WORDS * sizeof(uint32_t), stream));
+          uint32_t* dn = static_cast<uint32_t*>(d_dense.p);
+          const uint64_t* reps = static_cast<const uint64_t*>(d_xrep[xbuf[x]].p);
+          const dim3 dg(std::max<uint32_t>(1, std::min<uint32_t>((n_entx[x] + 255) / 256, cus * 4)));
+          hipLaunchKernelGGL(rc_dense_hist_kernel, dg, dim3(256), 0, stream, P, reps, static_cast<const uint4*>(P.rc_pool),
+                             Lx[x].off, Lx[x].count, n_entx[x], Lx[x].k, dn);
+          hipLaunchKernelGGL(rc_dense_rank_kernel, dim3(1), dim3(128), 0, stream, Lx[x].k,
+                             (uint32_t)env_u("FAC_RC_DENSE_KEYS", 50), dn);
+          hipLaunchKernelGGL(rc_dense_fill_kernel, dg, dim3(256), 0, stream, P, reps, static_cast<const uint4*>(P.rc_pool),
+                             Lx[x].off, Lx[x].count, n_entx[x], Lx[x].k, dn);
+          HIP_TRY(hipGetLastError());
+          P.rc_dense = dn;
+          dense_built = true;
+        }
         tabs.push_back(Lx[x]);
+      }
+      if (P.rc_dense) {  // the share of windows the dense bitmaps finish, read after the sync below
+        if (int hrc = pinned_word(dense_w_host, dense_w_dev, err)) return hrc;
+        hipLaunchKernelGGL(rc_dense_sample_kernel, dim3(64), dim3(256), 0, stream, P, windows);
+        hipLaunchKernelGGL(word_kernel, dim3(1), dim3(1), 0, stream,
+                           reinterpret_cast<const unsigned long long*>(P.rc_dense + 34), dense_w_dev);
+        HIP_TRY(hipGetLastError());
       }
       // the lookups probe deepest first and stop at the first hit: level 0 is reached only by the
       // windows whose level-1 key the sampled count missed
@@ -5385,6 +5760,15 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     HIP_TRY(hipEventRecord(ev.b, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     HIP_TRY(hipEventElapsedTime(&cache_ms, ev.a, ev.b));
+    if (P.rc_dense) {
+      // F-done windows among 16384 sampled: below FAC_RC_DENSE_OFF per mille the bitmaps are dropped
+      // (their test costs the lookup more than it saves), from FAC_RC_DENSE_LIST per mille the lookups
+      // walk the list of the others (dl_*_kernel)
+      dense_pm = (uint32_t)((uint64_t)*reinterpret_cast<volatile unsigned int*>(dense_w_host) * 1000 / 16384);
+      const uint32_t off_pm = (uint32_t)env_u("FAC_RC_DENSE_OFF", 50), list_pm = (uint32_t)env_u("FAC_RC_DENSE_LIST", 250);
+      if (dense_pm < off_pm) P.rc_dense = nullptr;
+      dense_list = dense_pm >= list_pm;
+    }
     if (P.rc_mode == 1 && diag_env("FAC_RC_DEBUG")) {  // diagnostics: keys, pool use, cached entries
       unsigned long long rcn[2] = {0, 0};
       HIP_TRY(hipMemcpy(rcn, d_rcn.p, sizeof(rcn), hipMemcpyDeviceToHost));
@@ -5463,6 +5847,7 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
                                   : std::min<uint64_t>(4096, std::max<uint64_t>(base_chunk, pass_windows / (16ull * max_grid)));
   const uint32_t rc_chunk = (uint32_t)std::min<unsigned long>(4096, std::max<unsigned long>(1,
       diag_env("FAC_RC_CHUNK") ? std::strtoul(diag_env("FAC_RC_CHUNK"), nullptr, 10) : rc_auto));
+  PoolBuf d_dl, d_dlm;     // the windows the dense bitmaps leave open (dl_*_kernel) and their masks
   bool kp_listed = false;  // the main pass walks the key part's window list (no prefix cache)
   if (P.rc_mode == 0 && P.kp_wlist) {
     P.win_list = P.kp_wlist;
@@ -5485,8 +5870,36 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
     HIP_TRY(hipMemsetAsync(d_cnt.p, 0, N_COUNTERS * sizeof(unsigned long long), stream));
     if (debug_poison()) HIP_TRY(hipMemsetAsync(d_out.p, 0xAB, out_cap * sizeof(fac_match), stream));
     if (P.rc_mode == 1 && !P.win_list) {  // every window's lookup (+ flush of finished windows) first
+      uint64_t lk_windows = pass_windows;
+      if (P.rc_dense && dense_list && !diag_env("FAC_RC_NO_DENSE_LIST")) {  // the windows bit F leaves open, listed
+        const uint64_t nb = (lk_windows + KP_CHUNK - 1) / KP_CHUNK;
+        const size_t mask_b = nb * (KP_CHUNK / 64) * 8, cnt_b = (nb * 4 + 7) & ~7ull;
+        HIP_TRY(d_dlm.alloc(mask_b + cnt_b + nb * 8 + 8, stream));
+        auto* masks = static_cast<unsigned long long*>(d_dlm.p);
+        auto* bcount = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_dlm.p) + mask_b);
+        auto* boff = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(d_dlm.p) + mask_b + cnt_b);
+        unsigned int* w_host = nullptr;
+        unsigned int* w_dev = nullptr;
+        if (int hrc = pinned_word(w_host, w_dev, err)) return hrc;
+        P.total_windows = lk_windows;
+        hipLaunchKernelGGL(dl_mask_kernel, dim3((uint32_t)nb), dim3(256), 0, stream, P, masks, bcount);
+        auto* total = reinterpret_cast<unsigned long long*>(boff + nb);
+        hipLaunchKernelGGL(dl_scan_kernel, dim3(1), dim3(1024), 0, stream, bcount, boff, nb, total);
+        hipLaunchKernelGGL(word_kernel, dim3(1), dim3(1), 0, stream, total, w_dev);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(stream));
+        const uint64_t listed = *reinterpret_cast<volatile unsigned int*>(w_host);
+        HIP_TRY(d_dl.alloc(std::max<uint64_t>(1, listed) * sizeof(uint64_t), stream));
+        hipLaunchKernelGGL(dl_write_kernel, dim3((uint32_t)nb), dim3(256), 0, stream, P, masks, boff,
+                           static_cast<uint64_t*>(d_dl.p));
+        HIP_TRY(hipGetLastError());
+        P.kp_wlist = static_cast<const uint64_t*>(d_dl.p);
+        lk_windows = listed;
+        dense_done += pass_windows - listed;
+      }
       // the open windows' hits, compacted per region (entries: n_reg * RC_REGION at most)
-      const uint64_t n_reg = (windows + RC_REGION - 1) / RC_REGION;
+      const uint64_t n_reg = std::max<uint64_t>(1, (lk_windows + RC_REGION - 1) / RC_REGION);
+      P.total_windows = lk_windows;
       HIP_TRY(d_hits.alloc(n_reg * RC_REGION * sizeof(uint4), stream));
       HIP_TRY(d_hitp.alloc(n_reg * RC_REGION * sizeof(uint32_t), stream));
       HIP_TRY(d_voff.alloc(n_reg * RC_REGION * sizeof(uint32_t), stream));
@@ -5527,7 +5940,10 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
           std::snprintf(b, sizeof(b), " k=%u: open %llu final %llu |", P.rc_tab[t].k, d[2 * t], d[2 * t + 1]);
           lv += b;
         }
-        std::fprintf(stderr, "FAC_LK%s miss %llu skipped %llu\n", lv.c_str(), d[12], d[13]);
+        uint32_t dk[2] = {0, 0};  // the start level's cached keys: ASCII and final without records, all
+        if (dense_built) HIP_TRY(hipMemcpy(dk, static_cast<uint32_t*>(d_dense.p) + 36, sizeof(dk), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "FAC_LK%s miss %llu skipped %llu dense-final %llu unlisted %llu (sampled %u per mille; keys %u of %u)\n",
+                     lv.c_str(), d[12], d[13], d[14], (unsigned long long)dense_done, dense_pm, dk[0], dk[1]);
         std::memset(d, 0, sizeof(d));
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_lk_dbg), d, sizeof(d)));
       }

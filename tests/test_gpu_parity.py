@@ -506,6 +506,48 @@ def test_prefix_cache_default_on_c3_slice(monkeypatch):
     _staged_vs_oracle(workloads.builder_for(w), w.patterns, hay, w.threshold)
 
 
+def test_dense_start_level_bitmaps(monkeypatch, capfd):
+    """The start level's dense key bitmaps (rc_dense_*_kernel: "final without records" and "cached"
+    bits over keys of the most frequent ASCII characters) finish most C2 windows without a lookup-table
+    probe -- left out of the lookups' window list (dl_*_kernel), or, with the list off, inside the
+    lookup: records == both == the bitmaps off (FAC_RC_NO_DENSE) == the cache off, on C2- and C3-shaped
+    slices with the sampled level on, and the C2 slice finishes windows through them (FAC_RC_DEBUG)."""
+    import re
+    from fuzzy_aho_corasick import workloads
+    monkeypatch.setenv("FAC_RC_MIN2", "1")
+    for cfg, mib in (("c2", 4), ("c3", 2)):
+        w = workloads.config(cfg, mib << 20, 3)
+        staged = workloads.builder_for(w).build(w.patterns).stage(w.haystack)
+        monkeypatch.setenv("FAC_RC_DEBUG", "1")
+        capfd.readouterr()
+        dense, st = staged.search_windows_records(w.threshold)
+        err = capfd.readouterr().err
+        monkeypatch.delenv("FAC_RC_DEBUG")
+        m = re.findall(r"dense-final (\d+) unlisted (\d+)", err)
+        assert m, err[-2000:]
+        if cfg == "c2":
+            assert int(m[-1][1]) > 0, err[-2000:]
+        monkeypatch.setenv("FAC_RC_NO_DENSE_LIST", "1")
+        monkeypatch.setenv("FAC_RC_DEBUG", "1")
+        capfd.readouterr()
+        inloop, _ = staged.search_windows_records(w.threshold)
+        err = capfd.readouterr().err
+        monkeypatch.delenv("FAC_RC_DEBUG")
+        monkeypatch.delenv("FAC_RC_NO_DENSE_LIST")
+        m = re.findall(r"dense-final (\d+) unlisted (\d+)", err)
+        if cfg == "c2":
+            assert m and int(m[-1][0]) > 0 and int(m[-1][1]) == 0, err[-2000:]
+        assert sorted(inloop.tolist()) == sorted(dense.tolist()), cfg
+        monkeypatch.setenv("FAC_RC_NO_DENSE", "1")
+        plain, _ = staged.search_windows_records(w.threshold)
+        monkeypatch.delenv("FAC_RC_NO_DENSE")
+        monkeypatch.setenv("FAC_NO_RC", "1")
+        off, _ = staged.search_windows_records(w.threshold)
+        monkeypatch.delenv("FAC_NO_RC")
+        assert st.states_cached > 0, cfg
+        assert len(dense) > 0 and sorted(dense.tolist()) == sorted(plain.tolist()) == sorted(off.tolist()), cfg
+
+
 @pytest.mark.parametrize("stride", ["4", "16"])
 def test_prefix_cache_sampled_level1(stride, monkeypatch):
     """Level-1 keys counted on every stride-th window (the default from 64 M windows): windows whose
