@@ -2548,10 +2548,16 @@ __global__ __launch_bounds__(256) void rc_publish_kernel(SearchParams P, const u
 // would miss, so the window goes straight to the shallower levels). F is exact; C is a hint (a set
 // bit whose key is not in the table only costs the probe). Keys with an unranked character, and
 // windows too close to the text end or the halo (their chars read as RC_PAD), take the probes.
-// Words: [0, 32) rank bytes (0xFF: unranked), [32] A (0: off), [33] k, [64, 192) the histogram,
-// [RC_DENSE_F, +2^19) bits F, [RC_DENSE_C, +2^19) bits C.
+// A third bitmap, F4, holds bit F for level 1's shorter keys (k1 chars, the same ranks): a window
+// whose k1-char key is final without records is done too (C2: the 178 M windows whose 5-char key
+// is absent because its 4-char parent is final). The window list (dl_*_kernel) tests both.
+// Words: [0, 32) rank bytes (0xFF: unranked), [32] A (0: off), [33] k, [34, 36) the sampled count
+// (u64), [36] / [37] the level's final record-less ASCII keys / cached keys, [38] k1 (0: no F4),
+// [64, 192) the histogram, [RC_DENSE_F, +2^19) bits F, [RC_DENSE_C, +2^19) bits C,
+// [RC_DENSE_F4, +2^19) bits F4.
 constexpr uint32_t RC_DENSE_LOG2 = 24, RC_DENSE_F = 256, RC_DENSE_C = RC_DENSE_F + (1u << (RC_DENSE_LOG2 - 5));
-constexpr size_t RC_DENSE_WORDS = RC_DENSE_C + (1u << (RC_DENSE_LOG2 - 5));
+constexpr uint32_t RC_DENSE_F4 = RC_DENSE_C + (1u << (RC_DENSE_LOG2 - 5));
+constexpr size_t RC_DENSE_WORDS = RC_DENSE_F4 + (1u << (RC_DENSE_LOG2 - 5));
 __device__ __forceinline__ bool rc_dense_entry(const SearchParams& P, const uint64_t* reps, const uint4* pool,
                                                const uint32_t* off, const uint32_t* count, uint32_t ent, uint32_t k,
                                                uint32_t c[8], bool& fin_empty) {
@@ -2595,7 +2601,7 @@ __global__ __launch_bounds__(256) void rc_dense_hist_kernel(SearchParams P, cons
 // of 128 threads, one character each
 // (A = 0 -- no bitmaps -- when fewer than min_pm per mille of the cached keys are ASCII and final
 // without records: C3 finishes 1.5 % of its windows through them, not worth the lookups' test)
-__global__ __launch_bounds__(128) void rc_dense_rank_kernel(uint32_t k, uint32_t min_pm, uint32_t* dense) {
+__global__ __launch_bounds__(128) void rc_dense_rank_kernel(uint32_t k, uint32_t k1, uint32_t min_pm, uint32_t* dense) {
   __shared__ uint32_t h[128];
   const uint32_t ch = threadIdx.x;
   h[ch] = dense[64 + ch];
@@ -2619,6 +2625,7 @@ __global__ __launch_bounds__(128) void rc_dense_rank_kernel(uint32_t k, uint32_t
   if (ch == 0) {
     dense[32] = A;
     dense[33] = k;
+    dense[38] = k1 < k ? k1 : 0u;
   }
 }
 // dense index of a key: its ranks as base-A digits, first character most significant (Horner), so
@@ -2636,9 +2643,10 @@ __device__ __forceinline__ bool rc_dense_index(const uint8_t* rank, uint32_t A, 
   }
   return ok;
 }
+// bits F (at f_off) and C (at c_off, 0: none) of a level's entries
 __global__ __launch_bounds__(256) void rc_dense_fill_kernel(SearchParams P, const uint64_t* reps, const uint4* pool,
                                                             const uint32_t* off, const uint32_t* count, uint32_t n_ent,
-                                                            uint32_t k, uint32_t* dense) {
+                                                            uint32_t k, uint32_t* dense, uint32_t f_off, uint32_t c_off) {
   __shared__ uint8_t s_rank[128];
   if (threadIdx.x < 128) s_rank[threadIdx.x] = reinterpret_cast<const uint8_t*>(dense)[threadIdx.x];
   __syncthreads();
@@ -2648,8 +2656,8 @@ __global__ __launch_bounds__(256) void rc_dense_fill_kernel(SearchParams P, cons
     uint32_t c[8], idx = 0;
     bool fe = false;
     if (!rc_dense_entry(P, reps, pool, off, count, ent, k, c, fe) || !rc_dense_index(s_rank, A, k, c, idx)) continue;
-    atomicOr(&dense[RC_DENSE_C + (idx >> 5)], 1u << (idx & 31u));
-    if (fe) atomicOr(&dense[RC_DENSE_F + (idx >> 5)], 1u << (idx & 31u));
+    if (c_off) atomicOr(&dense[c_off + (idx >> 5)], 1u << (idx & 31u));
+    if (fe) atomicOr(&dense[f_off + (idx >> 5)], 1u << (idx & 31u));
   }
 }
 
@@ -2763,7 +2771,9 @@ __device__ __forceinline__ bool dl_window_done(const SearchParams& P, const uint
   const SegDesc S = P.segs[kl];
   uint32_t c[8], idx = 0;
   (void)rc_chars(P, S, S.w_begin + (v - P.seg_prefix[kl]), k, c);
-  return rc_dense_index(rank, A, k, c, idx) && ((P.rc_dense[RC_DENSE_F + (idx >> 5)] >> (idx & 31u)) & 1u);
+  if (rc_dense_index(rank, A, k, c, idx) && ((P.rc_dense[RC_DENSE_F + (idx >> 5)] >> (idx & 31u)) & 1u)) return true;
+  const uint32_t k1 = P.rc_dense[38];
+  return k1 && rc_dense_index(rank, A, k1, c, idx) && ((P.rc_dense[RC_DENSE_F4 + (idx >> 5)] >> (idx & 31u)) & 1u);
 }
 // a thread's 16 consecutive windows of a staged tile (ranks s_r, 0xFF unranked): bit w of the result
 // set when window b0 + 16 t + w exists and the bitmaps do not finish it
@@ -2799,12 +2809,32 @@ __device__ __forceinline__ uint32_t dl_tile(const SearchParams& P, const uint8_t
   uint32_t bw[16];
 #pragma unroll
   for (uint32_t w = 0; w < 16; ++w) bw[w] = ((okm >> w) & 1u) ? P.rc_dense[RC_DENSE_F + (idx[w] >> 5)] : 0u;
+  uint32_t done = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < 16; ++w) done |= (((okm >> w) & 1u) && ((bw[w] >> (idx[w] & 31u)) & 1u)) ? 1u << w : 0u;
+  const uint32_t k1 = P.rc_dense[38];
+  if (k1) {  // the k1-char prefix: the high digits of idx, idx / A^(K - k1)
+    uint32_t D = 1;
+    for (uint32_t i = k1; i < K; ++i) D = __umul24(D, A);
+    const float inv = 1.0f / (float)D;
+    const uint32_t m1 = (1u << k1) - 1u;
+    uint32_t i4[16], ok4 = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 16; ++w) {
+      uint32_t q = (uint32_t)((float)idx[w] * inv);  // exact below 2^24 up to one step
+      if (__umul24(q, D) > idx[w]) --q;
+      else if (__umul24(q + 1u, D) <= idx[w]) ++q;
+      i4[w] = q;
+      ok4 |= (!((done >> w) & 1u) && ((bad >> w) & m1) == 0u && q0 + w <= last) ? 1u << w : 0u;
+    }
+#pragma unroll
+    for (uint32_t w = 0; w < 16; ++w) bw[w] = ((ok4 >> w) & 1u) ? P.rc_dense[RC_DENSE_F4 + (i4[w] >> 5)] : 0u;
+#pragma unroll
+    for (uint32_t w = 0; w < 16; ++w) done |= (((ok4 >> w) & 1u) && ((bw[w] >> (i4[w] & 31u)) & 1u)) ? 1u << w : 0u;
+  }
   uint32_t pat = 0;
 #pragma unroll
-  for (uint32_t w = 0; w < 16; ++w) {
-    const bool done = ((okm >> w) & 1u) && ((bw[w] >> (idx[w] & 31u)) & 1u);
-    pat |= (q0 + w <= last && !done) ? 1u << w : 0u;
-  }
+  for (uint32_t w = 0; w < 16; ++w) pat |= (q0 + w <= last && !((done >> w) & 1u)) ? 1u << w : 0u;
   return pat;
 }
 __global__ __launch_bounds__(256) void dl_mask_kernel(SearchParams P, unsigned long long* masks, uint32_t* bcount) {
@@ -5734,10 +5764,15 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
           const dim3 dg(std::max<uint32_t>(1, std::min<uint32_t>((n_entx[x] + 255) / 256, cus * 4)));
           hipLaunchKernelGGL(rc_dense_hist_kernel, dg, dim3(256), 0, stream, P, reps, static_cast<const uint4*>(P.rc_pool),
                              Lx[x].off, Lx[x].count, n_entx[x], Lx[x].k, dn);
-          hipLaunchKernelGGL(rc_dense_rank_kernel, dim3(1), dim3(128), 0, stream, Lx[x].k,
+          const bool f4 = n_ent1 && L1.k < Lx[x].k && !diag_env("FAC_RC_NO_DENSE4");
+          hipLaunchKernelGGL(rc_dense_rank_kernel, dim3(1), dim3(128), 0, stream, Lx[x].k, f4 ? L1.k : 0u,
                              (uint32_t)env_u("FAC_RC_DENSE_KEYS", 50), dn);
           hipLaunchKernelGGL(rc_dense_fill_kernel, dg, dim3(256), 0, stream, P, reps, static_cast<const uint4*>(P.rc_pool),
-                             Lx[x].off, Lx[x].count, n_entx[x], Lx[x].k, dn);
+                             Lx[x].off, Lx[x].count, n_entx[x], Lx[x].k, dn, RC_DENSE_F, RC_DENSE_C);
+          if (f4)  // level 1 (built and published: the stream waited for it above)
+            hipLaunchKernelGGL(rc_dense_fill_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_ent1 + 255) / 256, cus * 4))),
+                               dim3(256), 0, stream, P, static_cast<const uint64_t*>(d_rcrep.p),
+                               static_cast<const uint4*>(P.rc_pool), L1.off, L1.count, n_ent1, L1.k, dn, RC_DENSE_F4, 0u);
           HIP_TRY(hipGetLastError());
           P.rc_dense = dn;
           dense_built = true;
