@@ -116,6 +116,12 @@ __device__ SegState seg_init(const Props& L) {
 // boundary before code point R (GB3-GB999), then R becomes the left code point
 __device__ bool seg_step(SegState& st, const Props& R) {
   const Props& L = st.L;
+  // two plain code points (GCB Other, not Extended_Pictographic, no InCB: letters, digits, spaces,
+  // most punctuation) -- no rule but GB999 applies, and the state resets; most of the text
+  if (L.g == GCB_Other && R.g == GCB_Other && !L.pict && !R.pict && L.ib == INCB_None && R.ib == INCB_None) {
+    st = SegState{R, 0u, false, false, 0};
+    return true;
+  }
   bool brk;
   if (L.g == GCB_CR && R.g == GCB_LF) brk = false;                                              // GB3
   else if (is_ctl(L.g)) brk = true;                                                             // GB4
@@ -184,6 +190,9 @@ __device__ __forceinline__ uint32_t fold_fast(const uint16_t* __restrict__ ltab,
   return lower_first(cp);
 }
 
+constexpr uint32_t kPropLds = 0x800;  // code points whose property / lowercase bytes the staging kernels keep in LDS
+__device__ __forceinline__ Props props_of(uint32_t v) { return Props{(uint8_t)(v & 15u), (uint8_t)(v >> 5), (v & 16u) != 0}; }
+
 // Per 16 KiB tile (one workgroup, 64 bytes per thread, the tile staged in LDS): the C ABI's UTF-8
 // check (unicode.cpp utf8_valid_serial = Rust's str::from_utf8) over the code points starting in the
 // thread's bytes -- a segment runs from the first byte that is not a continuation byte to the next
@@ -198,17 +207,31 @@ __global__ __launch_bounds__(256) void seg_tile_kernel(const uint8_t* __restrict
                                                        uint32_t* __restrict__ ucnt, uint8_t* __restrict__ hard,
                                                        unsigned long long* __restrict__ scal, int skip_if_ascii) {
   if (skip_if_ascii && !(scal[0] & 2ull)) return;  // ascii_or_kernel found no byte >= 0x80
-  __shared__ __attribute__((aligned(16))) uint8_t tile[kTile];
+  // the tile, transposed: word w of thread t's 64 bytes at word w * 256 + t, so the threads' reads
+  // of their own bytes (byte j of each, together) fall in 64 different banks; the row-major tile made
+  // every such read a 32-way conflict (lanes 64 bytes apart)
+  __shared__ __attribute__((aligned(16))) uint32_t tileT[kTile / 4];
+  __shared__ uint8_t s_pt[kPropLds];  // ptab[0, kPropLds): Latin, Greek, Cyrillic, ... in LDS
   __shared__ uint32_t red[8];
+  uint8_t* const tileB = reinterpret_cast<uint8_t*>(tileT);
+  auto tix = [](uint32_t q) { return ((((q >> 2) & 15u) << 8 | (q >> 6)) << 2) | (q & 3u); };  // tile byte q -> LDS byte
   const uint64_t t0 = (uint64_t)blockIdx.x * kTile, t1 = min(n, t0 + (uint64_t)kTile);
+  for (uint32_t i = threadIdx.x; i < kPropLds; i += 256u) s_pt[i] = ptab[i];
   if (aligned && t1 - t0 == kTile) {
-    for (uint32_t i = threadIdx.x * 16u; i < kTile; i += 256u * 16u)
-      *reinterpret_cast<uint4*>(tile + i) = *reinterpret_cast<const uint4*>(s + t0 + i);
+    for (uint32_t i = threadIdx.x * 16u; i < kTile; i += 256u * 16u) {
+      const uint4 v = *reinterpret_cast<const uint4*>(s + t0 + i);
+      const uint32_t tp = i >> 6, w0 = (i >> 2) & 15u;
+      tileT[(w0 << 8) | tp] = v.x;
+      tileT[((w0 + 1) << 8) | tp] = v.y;
+      tileT[((w0 + 2) << 8) | tp] = v.z;
+      tileT[((w0 + 3) << 8) | tp] = v.w;
+    }
   } else {
-    for (uint32_t i = threadIdx.x; i < kTile; i += 256u) tile[i] = t0 + i < n ? s[t0 + i] : 0;
+    for (uint32_t i = threadIdx.x; i < kTile; i += 256u) tileB[tix(i)] = t0 + i < n ? s[t0 + i] : 0;
   }
   __syncthreads();
-  auto at = [&](uint64_t p) -> uint32_t { return (p >= t0 && p < t1) ? tile[p - t0] : s[p]; };
+  auto at = [&](uint64_t p) -> uint32_t { return (p >= t0 && p < t1) ? tileB[tix((uint32_t)(p - t0))] : s[p]; };
+  auto props_fast = [&](const uint8_t* tab, uint32_t cp) { return cp >= 0x80u && cp < kPropLds ? props_of(s_pt[cp]) : fac::props_fast(tab, cp); };
   auto cont = [&](uint64_t p) { return (at(p) & 0xC0u) == 0x80u; };
   auto dec = [&](uint64_t& i) -> uint32_t {  // unicode.cpp utf8_decode, bounded by n
     const uint32_t b0 = at(i);
@@ -239,7 +262,8 @@ __global__ __launch_bounds__(256) void seg_tile_kernel(const uint8_t* __restrict
   uint32_t hi = 0;
   if (a < n) {
     const uint64_t b = min(a + 64, n);
-    for (uint64_t p = a; p < b; ++p) hi |= at(p);
+#pragma unroll
+    for (uint32_t w = 0; w < 16; ++w) hi |= tileT[(w << 8) | threadIdx.x];  // own bytes (0 past n)
     uint64_t i = seg_start(a, bad);
     if (a == 0 && i != 0) bad = true;
     bool bad2 = false;
@@ -310,7 +334,7 @@ __global__ __launch_bounds__(256) void seg_tile_kernel(const uint8_t* __restrict
     hard[a >> 6] = is_hard ? 1 : 0;
   }
   uint32_t c = (uint32_t)__popcll(mask);
-  uint32_t f = (bad ? 1u : 0u) | ((hi & 0x80u) ? 2u : 0u) | (is_hard ? 4u : 0u);
+  uint32_t f = (bad ? 1u : 0u) | ((hi & 0x80808080u) ? 2u : 0u) | (is_hard ? 4u : 0u);
   for (int o = 32; o > 0; o >>= 1) {
     c += __shfl_down(c, o, 64);
     f |= (uint32_t)__shfl_down((int)f, o, 64);
@@ -418,11 +442,18 @@ __global__ __launch_bounds__(1024) void unit_scan_kernel(const uint32_t* ucnt, u
 // Grapheme starts (h.d_off) and text_chars (h.d_text32: the folded first code point per grapheme,
 // search.rs:406-412, grapheme.rs:112-119), one wave per tile in byte order: four boundary bits per
 // lane per step, a wave scan gives each start its slot, so consecutive lanes write consecutive slots.
-__global__ __launch_bounds__(256) void write_tile_kernel(const uint8_t* __restrict__ s, uint64_t n,
+// A lane reads its 4 bytes and the next 4 as two words with its boundary word (one round trip per
+// step: every code point starting in its 4 bytes decodes from those 8), and folds through an LDS copy
+// of ltab below kPropLds (was: a dependent byte load per continuation byte and a global ltab load).
+__global__ __launch_bounds__(256) void write_tile_kernel(const uint8_t* __restrict__ s, uint64_t n, int aligned,
                                                          const unsigned long long* __restrict__ bits,
                                                          const uint64_t* __restrict__ ubase, uint64_t n_units,
                                                          const uint16_t* __restrict__ ltab, int ci, uint64_t* __restrict__ off,
                                                          uint32_t* __restrict__ text32) {
+  __shared__ uint16_t s_lt[kPropLds];
+  if (ci)
+    for (uint32_t i = threadIdx.x; i < kPropLds; i += blockDim.x) s_lt[i] = ltab[i];
+  __syncthreads();
   const uint64_t u = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
   const uint32_t lane = threadIdx.x & 63u;
   if (u >= n_units) return;  // whole waves
@@ -430,10 +461,17 @@ __global__ __launch_bounds__(256) void write_tile_kernel(const uint8_t* __restri
   const uint64_t b = u * kTile, e = min(n, b + (uint64_t)kTile);
   for (uint64_t p0 = b; p0 < e; p0 += 256) {
     const uint64_t p = p0 + 4ull * lane;
-    uint32_t f = 0;
+    uint32_t f = 0, wa = 0, wb = 0;
     if (p < e) {
       f = (uint32_t)(bits[p >> 6] >> (p & 63)) & 0xFu;
       if (p + 4 > e) f &= (1u << (uint32_t)(e - p)) - 1u;
+      if (aligned && p + 8 <= n) {
+        wa = *reinterpret_cast<const uint32_t*>(s + p);
+        wb = *reinterpret_cast<const uint32_t*>(s + p + 4);
+      } else {
+        for (uint32_t q = 0; q < 8; ++q)
+          if (p + q < n) (q < 4 ? wa : wb) |= (uint32_t)s[p + q] << (8 * (q & 3u));
+      }
     }
     const uint32_t c = __popc(f);
     uint32_t x = c;
@@ -442,12 +480,23 @@ __global__ __launch_bounds__(256) void write_tile_kernel(const uint8_t* __restri
       if (lane >= (uint32_t)o) x += y;
     }
     uint64_t o = base + x - c;
+    const uint64_t w8 = (uint64_t)wa | ((uint64_t)wb << 32);
     for (uint32_t k = 0; k < 4; ++k)
       if ((f >> k) & 1u) {
-        uint64_t i = p + k;
+        const uint64_t i = p + k;
+        auto at = [&](uint32_t d) { return (uint32_t)(w8 >> (8 * (k + d))) & 0xFFu; };  // byte i + d (d <= 3)
+        const uint32_t b0 = at(0);
+        uint32_t cp;  // decode(s, n, i) on the registers
+        if (b0 < 0x80u) cp = b0;
+        else if ((b0 & 0xE0u) == 0xC0u && i + 1 < n) cp = ((b0 & 0x1Fu) << 6) | (at(1) & 0x3Fu);
+        else if ((b0 & 0xF0u) == 0xE0u && i + 2 < n) cp = ((b0 & 0x0Fu) << 12) | ((at(1) & 0x3Fu) << 6) | (at(2) & 0x3Fu);
+        else if ((b0 & 0xF8u) == 0xF0u && i + 3 < n)
+          cp = ((b0 & 0x07u) << 18) | ((at(1) & 0x3Fu) << 12) | ((at(2) & 0x3Fu) << 6) | (at(3) & 0x3Fu);
+        else cp = 0xFFFD;
         off[o] = i;
-        const uint32_t cp = decode(s, n, i);
-        text32[o] = ci ? fold_fast(ltab, cp) : cp;
+        uint32_t fc = cp;
+        if (ci) fc = cp >= 0x80u && cp < kPropLds && s_lt[cp] ? (uint32_t)s_lt[cp] : fold_fast(ltab, cp);
+        text32[o] = fc;
         ++o;
       }
     base += __shfl(x, 63, 64);
@@ -578,7 +627,7 @@ int stage_device(const Engine& e, Haystack& h, hipStream_t st, std::string& err,
     h.off_cap = h.n + 1;
   }
   ST_TRY(hipMemcpyAsync(h.d_off + h.n, &h.len, 8, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(write_tile_kernel, dim3((uint32_t)((n_units + 3) / 4)), dim3(256), 0, st, h.d_utf8, len, bits, ubase,
+  hipLaunchKernelGGL(write_tile_kernel, dim3((uint32_t)((n_units + 3) / 4)), dim3(256), 0, st, h.d_utf8, len, aligned, bits, ubase,
                      n_units, tabs.l, e.case_insensitive ? 1 : 0, h.d_off, h.d_text32);
   ST_TRY(hipGetLastError());
   return FAC_OK;
