@@ -316,7 +316,7 @@ struct PfTables {
   bool w32 = true;
   void *pmask = nullptr, *ptop = nullptr, *wk = nullptr;
   bool q = false;           // q-gram path in use
-  uint32_t ts = 0, use3 = 0, use4 = 0, kq = 0, mq = 0;
+  uint32_t ts = 0, use3 = 0, use4 = 0, use5 = 0, kq = 0, mq = 0;
   size_t n_qpat = 0, n_grams = 0, n_keys = 0;
   void *tab = nullptr, *ent = nullptr, *qmask = nullptr, *qpm = nullptr, *qbits = nullptr;
   void* m16 = nullptr;      // every q-gram pattern m <= 16: 16-bit masks [pattern][rows] for LDS

@@ -4190,6 +4190,7 @@ struct QgramParams {
   uint32_t tab_mask;
   const uint2* ent;        // entries: {pattern << 8 | piece offset, m | k << 8} (one load per candidate)
   uint32_t use3, use4;     // gram lengths in use
+  uint32_t use5;           // 4-gram probes screened by the 5-gram (pieces of >= 5 symbols)
   // candidates (text position << 24 | entry index): scan block b fills region b of cand (region
   // entries, rcnt[b] of them valid), and what does not fit goes to the overflow list ovf
   unsigned long long* cand;
@@ -4260,6 +4261,17 @@ __host__ __device__ inline uint32_t qgram_bit(uint32_t key) {
   return ((key >> 24) == 0xFFu ? p : p + qg_mul24(key >> 8, QG_HB)) >> (32 - QG_BITS_LOG);
 }
 constexpr uint32_t QG_BITS_WORDS = (1u << QG_BITS_LOG) / 32;
+// A piece of >= 5 symbols is screened by its first five (round 6): its table key stays the 4-gram,
+// but its bit is qgram_bit5 of the 4-gram and the fifth symbol, so a text position whose 4-gram
+// matches a piece while its fifth symbol does not (C5: most of the 34 M candidates per GiB of
+// 4-gram screening -- random vocabulary words sharing four letters with a pattern piece) rarely
+// passes, and the verify no longer runs for it. Exact: a true hit keeps a whole piece, whose first
+// five symbols lie in the text.
+constexpr uint32_t QG_HC = 0xC2B2AEu;
+__host__ __device__ inline uint32_t qgram_bit5(uint32_t key4, uint32_t c5) {
+  const uint32_t h4 = qg_mul24(key4, QG_HA) + qg_mul24(key4 >> 8, QG_HB);
+  return (h4 + qg_mul24((key4 >> 16) | (c5 << 16), QG_HC)) >> (32 - QG_BITS_LOG);
+}
 
 // Candidates go to the block's own region of the list, reserved with an LDS counter: one global
 // list counter took a same-address atomic per flush of a per-wave buffer, and those atomics
@@ -4293,7 +4305,7 @@ __device__ __forceinline__ uint32_t qg_fold(uint32_t w) {
   return w + (up >> 2);
 }
 // U3 / U4: 3- / 4-grams in use (C5: 4-grams only, so the 3-grams' bitmap reads are not issued)
-template <bool U3, bool U4>
+template <bool U3, bool U4, bool U5>
 __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q) {
   __shared__ uint32_t s_bits[QG_BITS_WORDS];
   __shared__ uint32_t s_cnt, s_fail;  // region entries reserved; the first reservation that did not fit
@@ -4385,10 +4397,16 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
     auto screen = [&](auto all_in) {  // all_in: every gram of the sixteen lies inside the text
 #pragma unroll
       for (uint32_t j = 0; j < 16; ++j) {
-        // qgram_bit of the 3-gram (h3) and the 4-gram (h4) at this position
+        // qgram_bit of the 3-gram (h3) and the 4-gram (h4) at this position, qgram_bit5 (h5)
         const uint32_t k4 = gram4(j), h3 = qg_mul24(k4, QG_HA), h4 = h3 + qg_mul24(k4 >> 8, QG_HB);
         constexpr uint32_t sh = 32 - QG_BITS_LOG;
         if constexpr (U4) pm |= __builtin_amdgcn_ubfe(s_bytes[h4 >> (sh + 3)], (h4 >> sh) & 7u, 1u) << (2 * j);
+        if constexpr (U5) {
+          const uint32_t wq = (j + 4) >> 2;  // symbol j + 4: in w1..w4 (j + 4 <= 19)
+          const uint32_t c5 = ((wq == 1u ? w1 : wq == 2u ? w2 : wq == 3u ? w3 : w4) >> (8 * ((j + 4) & 3u))) & 0xFFu;
+          const uint32_t h5 = h4 + qg_mul24((k4 >> 16) | (c5 << 16), QG_HC);
+          pm |= __builtin_amdgcn_ubfe(s_bytes[h5 >> (sh + 3)], (h5 >> sh) & 7u, 1u) << (2 * j);
+        }
         if constexpr (U3) pm |= __builtin_amdgcn_ubfe(s_bytes[h3 >> (sh + 3)], (h3 >> sh) & 7u, 1u) << (2 * j + 1);
       }
       if (!all_in) {
@@ -4451,6 +4469,20 @@ __global__ __launch_bounds__(64 * QG_WAVES) void qgram_scan_kernel(QgramParams Q
   if (threadIdx.x == 0) Q.rcnt[blockIdx.x] = min(s_cnt, s_fail);
 }
 
+// coverage [end - span, end) clipped to the text start wlo, as bitap_kernel (a hit: rare, kept out
+// of the verify's unrolled symbol loop)
+__device__ __attribute__((noinline)) void qgram_cover(uint32_t* cover, uint64_t wlo, uint64_t span, uint64_t end) {
+  const uint64_t ws = end > wlo + span ? end - span : wlo;
+  for (uint64_t y = ws; y < end;) {
+    const uint64_t w = y >> 5;
+    const uint32_t l = (uint32_t)(y & 31);
+    const uint32_t cnt = (uint32_t)min((uint64_t)(32 - l), end - y);
+    const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << l;
+    atomicOr(cover + w, bits);
+    y += cnt;
+  }
+}
+
 // W: the automaton word, uint32_t when every q-gram pattern has m <= 32 (half the 64-bit VALU work)
 // One candidate (qgram_verify_kernel). LM: every q-gram pattern has m <= 16 and their masks fit in
 // LDS (16-bit, pattern-major): the mask reads are LDS reads instead of L2 round trips.
@@ -4481,6 +4513,48 @@ __device__ __forceinline__ void verify_one(const QgramParams& Q, unsigned long l
   // (text positions; buffer byte = position + off, both 4-aligned when base is: off % 4 folded in)
   const uint32_t* mask32 = reinterpret_cast<const uint32_t*>(mask);
   const uint32_t sh = Q.off & 3u;
+  auto cover_end = [&](uint64_t end) { qgram_cover(cover, wlo, (uint64_t)m + k, end); };
+  {
+    // Short spans (every C5 candidate: m + 3k + 1 <= 23 symbols): the symbols [s0, e_max) from eight
+    // words realigned to s0 (v_alignbyte), stepped exactly -- the general loop below runs whole
+    // 16-symbol chunks from the aligned word before s0 (32 steps for C5's ~20; round 5: 941 VALU
+    // instructions per candidate)
+    const uint64_t ns = e_max - s0;
+    const uint64_t wb = (s0 + sh) & ~3ull, bb = wb + (Q.off - sh);
+    if (ns <= 28 && bb + 32 <= Q.nsafe) {
+      const uint32_t* w32 = reinterpret_cast<const uint32_t*>(Q.ids) + (bb >> 2);
+      uint32_t wd[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) wd[u] = w32[u];
+      const uint32_t al = (uint32_t)(s0 + sh - wb);
+      uint32_t sw[7];
+#pragma unroll
+      for (uint32_t u = 0; u < 7; ++u) sw[u] = __builtin_amdgcn_alignbyte(wd[u + 1], wd[u], al);
+      const uint32_t nsym = (uint32_t)ns, t_end = (uint32_t)(e_min - 1 - s0);
+#pragma unroll
+      for (uint32_t t = 0; t < 28; ++t) {
+        if (t >= nsym) continue;  // (not break: the loop must unroll -- sw is indexed by t)
+        uint32_t sym = (sw[t >> 2] >> (8 * (t & 3u))) & 0xFFu;
+        if (Q.bytes) sym = s_aid[sym & 0x7Fu];
+        const W bc = LM ? (W)mask16[sym] : sizeof(W) == 4 ? (W)mask32[2 * sym] : (W)mask[sym];
+        W prev_old = r[0];
+        W prev_new = ((r[0] << 1) | (W)1) & bc;
+        r[0] = prev_new;
+        W hit = (k == 0) ? prev_new : (W)0;
+#pragma unroll
+        for (int d = 1; d <= KMAX; ++d) {
+          const W old = r[d];
+          const W nv = ((old << 1) & bc) | ((prev_old | prev_new) << 1) | prev_old | (W)1;
+          r[d] = nv;
+          prev_old = old;
+          prev_new = nv;
+          if ((uint32_t)d == k) hit = nv;
+        }
+        if (t >= t_end && (hit & top)) cover_end(s0 + t + 1);
+      }
+      return;
+    }
+  }
   // per pass, 32-bit bounds relative to the pass's first buffer word (u = 16c + v indexes its
   // symbols): symbols u in [u_lo, u_hi) are stepped, ends at u >= u_end report (a pass spans 64
   // symbols, so every bound fits; 64-bit compares per symbol cost as much as the recurrence)
@@ -4531,19 +4605,7 @@ __device__ __forceinline__ void verify_one(const QgramParams& Q, unsigned long l
           prev_new = nv;
           if ((uint32_t)d == k) hit = nv;
         }
-        if (u >= u_end && (hit & top)) {  // coverage [end - m - k, end), as bitap_kernel
-          const uint64_t end = base + (uint64_t)u - sh + 1;
-          const uint64_t span = (uint64_t)m + k;
-          const uint64_t ws = end > wlo + span ? end - span : wlo;
-          for (uint64_t y = ws; y < end;) {
-            const uint64_t w = y >> 5;
-            const uint32_t l = (uint32_t)(y & 31);
-            const uint32_t cnt = (uint32_t)min((uint64_t)(32 - l), end - y);
-            const uint32_t bits = (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << l;
-            atomicOr(cover + w, bits);
-            y += cnt;
-          }
-        }
+        if (u >= u_end && (hit & top)) cover_end(base + (uint64_t)u - sh + 1);
       }
     }
   }
@@ -6253,8 +6315,14 @@ int pf_tables(const Engine& e, const std::vector<uint32_t>& ks, bool want_bytes,
   // pieces are at least 3 symbols long; the rest go through the full bitap scan.
   std::vector<uint8_t> qlen(np, 0);
   std::vector<std::pair<uint32_t, uint32_t>> grams;  // (gram key, pattern << 8 | piece offset)
+  std::vector<uint32_t> gram5;                       // per gram: its piece's fifth symbol (0xFFFF: none)
   if (qgram_on && rows <= 256) {
     std::vector<uint32_t> sym(64);
+    // 5-gram screens only when no piece is screened by its 3-gram: 3-grams pass so often that they
+    // make most candidates, and the extra screen then costs more than it removes (C5: 33.0 M
+    // candidates per GiB either way, scan 1.02 -> 1.16 ms per GiB)
+    bool any3 = false;
+    for (uint32_t i = 0; i < np; ++i) any3 = any3 || (e.bp_m[i] <= 63 && e.bp_m[i] / (ks[i] + 1) == 3);
     for (uint32_t i = 0; i < np; ++i) {
       const uint32_t m = e.bp_m[i], k = ks[i], L = m / (k + 1);
       if (L < 3 || m > 63) continue;
@@ -6266,19 +6334,32 @@ int pf_tables(const Engine& e, const std::vector<uint32_t>& ks, bool want_bytes,
         one = one && hits == 1;
       }
       if (!one) continue;
+      const bool five = L >= 5 && !any3 && !diag_env("FAC_QG_NO5");
       const uint32_t q = std::min<uint32_t>(4, L);
-      qlen[i] = (uint8_t)q;
+      qlen[i] = (uint8_t)(five ? 5 : q);
       for (uint32_t r = 0; r <= k; ++r) {
         const uint32_t o = (uint32_t)((uint64_t)r * m / (k + 1));
         grams.push_back({qgram_key(sym[o], sym[o + 1], sym[o + 2], q == 4 ? sym[o + 3] : 0u, q == 4), (i << 8) | o});
       }
     }
     std::sort(grams.begin(), grams.end());
+    for (const auto& g : grams) {  // (after the sort: gram5 follows grams' order)
+      const uint32_t i = g.second >> 8, o = g.second & 0xFFu;
+      if (qlen[i] != 5) {
+        gram5.push_back(0xFFFFu);
+        continue;
+      }
+      uint32_t c = 0;
+      for (uint32_t cc = 0; cc < rows; ++cc)
+        if ((e.bp_mask[(size_t)i * rows + cc] >> (o + 4)) & 1ull) c = cc;
+      gram5.push_back(c);
+    }
     for (size_t a = 0, b; a < grams.size(); a = b) {  // at most 255 entries per gram (table word)
       for (b = a; b < grams.size() && grams[b].first == grams[a].first; ++b) {}
       if (b - a > 255) {
         std::fill(qlen.begin(), qlen.end(), 0);
         grams.clear();
+        gram5.clear();
         break;
       }
     }
@@ -6324,12 +6405,18 @@ int pf_tables(const Engine& e, const std::vector<uint32_t>& ks, bool want_bytes,
       const uint32_t id = e.ascii_id[b];
       if (id && byte_of_id[id] == 0x80) byte_of_id[id] = (uint8_t)(e.case_insensitive && b - 'A' < 26u ? b + 32u : b);
     }
-    for (auto& g : grams) {
-      const uint32_t k = g.first, q4 = (k >> 24) != 0xFFu;
-      g.first = qgram_key(byte_of_id[k & 0xFFu], byte_of_id[(k >> 8) & 0xFFu], byte_of_id[(k >> 16) & 0xFFu],
-                          q4 ? byte_of_id[k >> 24] : 0u, q4);
+    std::vector<std::pair<std::pair<uint32_t, uint32_t>, uint32_t>> g5(grams.size());
+    for (size_t x = 0; x < grams.size(); ++x) {
+      const uint32_t k = grams[x].first, q4 = (k >> 24) != 0xFFu;
+      g5[x] = {{qgram_key(byte_of_id[k & 0xFFu], byte_of_id[(k >> 8) & 0xFFu], byte_of_id[(k >> 16) & 0xFFu],
+                          q4 ? byte_of_id[k >> 24] : 0u, q4), grams[x].second},
+               gram5[x] == 0xFFFFu ? 0xFFFFu : (uint32_t)byte_of_id[gram5[x]]};
     }
-    std::sort(grams.begin(), grams.end());
+    std::sort(g5.begin(), g5.end());
+    for (size_t x = 0; x < g5.size(); ++x) {
+      grams[x] = g5[x].first;
+      gram5[x] = g5[x].second;
+    }
   }
   std::vector<uint64_t> pmask((size_t)rows * nw, 0), ptop(nw, 0);
   for (uint32_t i : order) {
@@ -6366,8 +6453,8 @@ int pf_tables(const Engine& e, const std::vector<uint32_t>& ks, bool want_bytes,
       tab[sl] = make_uint2(kv.first, kv.second);
     }
     std::vector<uint32_t> qbits(QG_BITS_WORDS, 0u);  // the scan's screening bitmap
-    for (const auto& kv : keys) {
-      const uint32_t b = qgram_bit(kv.first);
+    for (size_t x = 0; x < grams.size(); ++x) {
+      const uint32_t b = gram5[x] == 0xFFFFu ? qgram_bit(grams[x].first) : qgram_bit5(grams[x].first, gram5[x]);
       qbits[b >> 5] |= 1u << (b & 31u);
     }
     std::vector<uint32_t> pm(np, 0);
@@ -6376,7 +6463,7 @@ int pf_tables(const Engine& e, const std::vector<uint32_t>& ks, bool want_bytes,
         pm[i] = e.bp_m[i] | (ks[i] << 8);
         T->kq = std::max(T->kq, ks[i]);
         T->mq = std::max(T->mq, e.bp_m[i]);
-        (qlen[i] == 4 ? T->use4 : T->use3) = 1u;
+        (qlen[i] == 5 ? T->use5 : qlen[i] == 4 ? T->use4 : T->use3) = 1u;
         T->n_qpat += 1;
       }
     T->ts = ts;
@@ -6556,6 +6643,7 @@ int prefilter_windows_ex(const Engine& e, const Haystack& h, const SegDesc& view
     Q.ent = static_cast<const uint2*>(T->ent);
     Q.use3 = T->use3;
     Q.use4 = T->use4;
+    Q.use5 = T->use5;
     Q.n_ovf = static_cast<unsigned long long*>(d_qn.p);
     Q.pmask = static_cast<const uint64_t*>(T->qmask);
     Q.pm = static_cast<const uint32_t*>(T->qpm);
@@ -6588,9 +6676,17 @@ int prefilter_windows_ex(const Engine& e, const Haystack& h, const SegDesc& view
     // two full resident rounds of scan blocks (2 per CU at 56 KB of LDS): the scan strides over the
     // text, so every block does the same work, and a grid of 8 per CU ran 2.7 rounds (the last one 2/3
     // full); one round left the verify's 2 persistent blocks per CU 1.5 regions each (1.21 vs 1.15 ms)
-    const void* scan_fn = Q.use3 && Q.use4 ? reinterpret_cast<const void*>(&qgram_scan_kernel<true, true>)
-                          : Q.use4         ? reinterpret_cast<const void*>(&qgram_scan_kernel<false, true>)
-                                           : reinterpret_cast<const void*>(&qgram_scan_kernel<true, false>);
+    // instantiations by the gram kinds in use (3-grams alone, 4-grams, 5-gram screens, or mixed)
+    const uint32_t qk = (Q.use3 ? 1u : 0u) | (Q.use4 ? 2u : 0u) | (Q.use5 ? 4u : 0u);
+    const void* scan_fns[8] = {reinterpret_cast<const void*>(&qgram_scan_kernel<true, false, false>),
+                               reinterpret_cast<const void*>(&qgram_scan_kernel<true, false, false>),
+                               reinterpret_cast<const void*>(&qgram_scan_kernel<false, true, false>),
+                               reinterpret_cast<const void*>(&qgram_scan_kernel<true, true, false>),
+                               reinterpret_cast<const void*>(&qgram_scan_kernel<false, false, true>),
+                               reinterpret_cast<const void*>(&qgram_scan_kernel<true, false, true>),
+                               reinterpret_cast<const void*>(&qgram_scan_kernel<false, true, true>),
+                               reinterpret_cast<const void*>(&qgram_scan_kernel<true, true, true>)};
+    const void* scan_fn = scan_fns[qk];
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scan_fn, 64 * QG_WAVES, 0) != hipSuccess || per_cu < 1)
       per_cu = 1;
@@ -6610,9 +6706,15 @@ int prefilter_windows_ex(const Engine& e, const Haystack& h, const SegDesc& view
       Q.ovf = static_cast<unsigned long long*>(d_qovf.p);
       Q.ovf_cap = ocap;
       HIP_TRY(hipMemsetAsync(d_qn.p, 0, 8, stream));
-      if (Q.use3 && Q.use4) hipLaunchKernelGGL((qgram_scan_kernel<true, true>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q);
-      else if (Q.use4) hipLaunchKernelGGL((qgram_scan_kernel<false, true>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q);
-      else hipLaunchKernelGGL((qgram_scan_kernel<true, false>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q);
+      switch (qk) {
+        case 2: hipLaunchKernelGGL((qgram_scan_kernel<false, true, false>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q); break;
+        case 3: hipLaunchKernelGGL((qgram_scan_kernel<true, true, false>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q); break;
+        case 4: hipLaunchKernelGGL((qgram_scan_kernel<false, false, true>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q); break;
+        case 5: hipLaunchKernelGGL((qgram_scan_kernel<true, false, true>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q); break;
+        case 6: hipLaunchKernelGGL((qgram_scan_kernel<false, true, true>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q); break;
+        case 7: hipLaunchKernelGGL((qgram_scan_kernel<true, true, true>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q); break;
+        default: hipLaunchKernelGGL((qgram_scan_kernel<true, false, false>), dim3(sgrid), dim3(64 * QG_WAVES), 0, stream, Q); break;
+      }
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipMemcpyAsync(&nc, d_qn.p, 8, hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));
@@ -6627,9 +6729,9 @@ int prefilter_windows_ex(const Engine& e, const Haystack& h, const SegDesc& view
       HIP_TRY(hipStreamSynchronize(stream));
       uint64_t tot = nc, mx = 0;
       for (uint32_t c : rc) tot += c, mx = std::max<uint64_t>(mx, c);
-      std::fprintf(stderr, "FAC_QGRAM text %llu symbols, %llu candidates (%llu overflow, region %llu, fullest %llu), use3 %u use4 %u\n",
+      std::fprintf(stderr, "FAC_QGRAM text %llu symbols, %llu candidates (%llu overflow, region %llu, fullest %llu), use3 %u use4 %u use5 %u\n",
                    (unsigned long long)n, (unsigned long long)tot, nc, (unsigned long long)Q.region,
-                   (unsigned long long)mx, Q.use3, Q.use4);
+                   (unsigned long long)mx, Q.use3, Q.use4, Q.use5);
     }
     {
       const dim3 vg((uint32_t)std::min<uint64_t>(sgrid + 1, (uint64_t)cus * (T->m16 ? 2 : 8)));
