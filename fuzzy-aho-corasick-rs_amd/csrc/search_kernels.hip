@@ -2246,15 +2246,18 @@ __device__ __forceinline__ uint32_t run_window(const SearchParams& P, const SegD
 // Key partition (Haystack::kparts): a start window belongs to part hash(its first two characters,
 // folded as the keys fold them) mod parts. Every prefix-cache key extends its window's first two
 // characters (keys hold >= 2), so a key's windows -- and its snapshot -- live in one part.
-__device__ __forceinline__ bool window_owned_kp(const SearchParams& P, const SegDesc& S, uint64_t s, unsigned& err) {
-  if (P.kp_n <= 1u) return true;
-  const uint32_t c0 = text_char(P, S, s, err);
-  const uint32_t c1 = s + 1 < S.n ? text_char(P, S, s + 1, err) : 0xFFFFFFFFu;
+__device__ __forceinline__ bool kp_owned_chars(const SearchParams& P, uint32_t c0, uint32_t c1) {
   uint32_t h = (c0 * 0x9E3779B1u) ^ (c1 * 0x85EBCA6Bu);
   h ^= h >> 15;
   h *= 0x2C1B3C6Du;
   h ^= h >> 12;
   return h % P.kp_n == P.kp_r;
+}
+__device__ __forceinline__ bool window_owned_kp(const SearchParams& P, const SegDesc& S, uint64_t s, unsigned& err) {
+  if (P.kp_n <= 1u) return true;
+  const uint32_t c0 = text_char(P, S, s, err);
+  const uint32_t c1 = s + 1 < S.n ? text_char(P, S, s + 1, err) : 0xFFFFFFFFu;
+  return kp_owned_chars(P, c0, c1);
 }
 
 // 2-gram window skip (search.rs:535-553)
@@ -2709,54 +2712,16 @@ __device__ __forceinline__ void rc_count_insert(const RcCountTarget& T, uint64_t
 }
 // Up to three levels are counted in one pass over the windows (level 1; the sampled levels): their
 // inserts go out together and the window's text is read once.
-// The key part's start windows, listed in ascending order (count per block of KP_CHUNK windows, host
-// scan, then each block writes its windows at its offset in window order). The count, lookup and
-// cache-off searches then walk the part's windows only; the ownership test stays out of the window
-// loops, whose registers it would crowd.
+// The key part's start windows, listed in ascending order (kp_mask_kernel: one mask per 64 windows
+// and a count per block of KP_CHUNK; dl_scan_kernel; dl_write_kernel writes each block's windows at
+// its offset in window order). The count, lookup and cache-off searches then walk the part's windows
+// only; the ownership test stays out of the window loops, whose registers it would crowd.
 constexpr uint32_t KP_CHUNK = 4096;
 __device__ __forceinline__ bool kp_owned_window(const SearchParams& P, uint64_t v) {
   unsigned err = 0;
   const uint32_t kl = find_seg(P, v);
   const SegDesc S = P.segs[kl];
   return window_owned_kp(P, S, S.w_begin + (v - P.seg_prefix[kl]), err);
-}
-__global__ __launch_bounds__(256) void kp_count_kernel(SearchParams P, uint32_t* bcount) {
-  __shared__ uint32_t s_n;
-  if (threadIdx.x == 0) s_n = 0;
-  __syncthreads();
-  const uint64_t b0 = (uint64_t)blockIdx.x * KP_CHUNK;
-  uint32_t n = 0;
-  for (uint32_t r = threadIdx.x; r < KP_CHUNK; r += 256) {
-    const uint64_t v = b0 + r;
-    if (v < P.total_windows && kp_owned_window(P, v)) ++n;
-  }
-  n = (uint32_t)__popcll(__ballot(n & 1u)) + 2u * (uint32_t)__popcll(__ballot(n & 2u)) +
-      4u * (uint32_t)__popcll(__ballot(n & 4u)) + 8u * (uint32_t)__popcll(__ballot(n & 8u)) +
-      16u * (uint32_t)__popcll(__ballot(n & 16u));  // n <= 16 per thread
-  if (lane_id() == 0) atomicAdd(&s_n, n);
-  __syncthreads();
-  if (threadIdx.x == 0) bcount[blockIdx.x] = s_n;
-}
-__global__ __launch_bounds__(256) void kp_write_kernel(SearchParams P, const uint64_t* boff, uint64_t* list) {
-  __shared__ uint32_t s_w[4];
-  const uint64_t b0 = (uint64_t)blockIdx.x * KP_CHUNK;
-  uint64_t at = boff[blockIdx.x];
-  const uint32_t wv = threadIdx.x / 64;
-  for (uint32_t r = 0; r < KP_CHUNK; r += 256) {  // rounds of 256 windows, in window order
-    const uint64_t v = b0 + r + threadIdx.x;
-    const bool own = v < P.total_windows && kp_owned_window(P, v);
-    const uint64_t m = __ballot(own);
-    if (lane_id() == 0) s_w[wv] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t before = 0, tot = 0;
-    for (uint32_t x = 0; x < 4; ++x) {
-      before += x < wv ? s_w[x] : 0u;
-      tot += s_w[x];
-    }
-    if (own) list[at + before + prefix_below(m)] = v;
-    at += tot;
-    __syncthreads();
-  }
 }
 
 // The windows the dense bitmaps leave open (bit F clear), listed in ascending order ahead of the
@@ -2986,6 +2951,54 @@ __global__ __launch_bounds__(256) void dl_write_kernel(SearchParams P, const uns
     const uint64_t i = b0 + 64ull * m + lane;
     list[at + s_pre[m] + prefix_below(mk)] = P.kp_wlist ? P.kp_wlist[i] : i;
   }
+}
+
+// The key part's windows as dl_mask_kernel's masks (then dl_scan_kernel / dl_write_kernel list them):
+// one segment per block -- the tile's chars staged in LDS with coalesced loads, each wave testing 64
+// consecutive windows per round (their two chars: consecutive LDS words); else window by window.
+__global__ __launch_bounds__(256) void kp_mask_kernel(SearchParams P, unsigned long long* masks, uint32_t* bcount) {
+  __shared__ uint32_t s_c[KP_CHUNK + 1];
+  __shared__ uint32_t s_n;
+  if (threadIdx.x == 0) s_n = 0;
+  const uint64_t b0 = (uint64_t)blockIdx.x * KP_CHUNK;
+  const uint64_t last = min(b0 + KP_CHUNK, P.total_windows) - 1;
+  const uint32_t kl = find_seg(P, b0);
+  const bool tile = find_seg(P, last) == kl;
+  if (tile) {
+    const SegDesc S = P.segs[kl];
+    const uint64_t s0 = S.w_begin + (b0 - P.seg_prefix[kl]);
+    constexpr uint32_t kLoads = (KP_CHUNK + 1 + 255) / 256;
+    uint32_t cs[kLoads];
+#pragma unroll
+    for (uint32_t u = 0; u < kLoads; ++u) {  // window_owned_kp's chars: past the halo 0, past the text ~0
+      const uint64_t j = s0 + threadIdx.x + u * 256u;
+      uint32_t c = 0xFFFFFFFFu;
+      if (j < S.n) c = j >= S.avail ? 0u : S.ascii ? (uint32_t)P.utf8[S.text_base + j] : P.text32[S.text_base + j];
+      cs[u] = c;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kLoads; ++u) {
+      const uint32_t q = threadIdx.x + u * 256u;
+      uint32_t c = cs[u];
+      if (S.ascii && P.case_insensitive && c - 'A' < 26u) c += 32u;
+      if (q <= KP_CHUNK) s_c[q] = c;
+    }
+  }
+  __syncthreads();
+  uint32_t n = 0;
+  for (uint32_t r = 0; r < KP_CHUNK; r += 256) {
+    const uint32_t q = r + threadIdx.x;
+    bool own = b0 + q <= last;
+    if (own) own = tile ? kp_owned_chars(P, s_c[q], s_c[q + 1]) : kp_owned_window(P, b0 + q);
+    const unsigned long long m = __ballot(own);
+    if (lane_id() == 0) {
+      masks[(uint64_t)blockIdx.x * (KP_CHUNK / 64) + q / 64] = m;
+      n += (uint32_t)__popcll(m);
+    }
+  }
+  if (n) atomicAdd(&s_n, n);  // LDS
+  __syncthreads();
+  if (threadIdx.x == 0) bcount[blockIdx.x] = s_n;
 }
 
 __global__ __launch_bounds__(256) void rc_count_kernel(SearchParams P, RcCountTarget t0, RcCountTarget t1,
@@ -5347,26 +5360,28 @@ int launch_pass(const Engine& e, const Haystack& h, const std::vector<SegDesc>& 
   // counts them (the cache policy, lookups and searches see the part alone)
   PoolBuf d_kpl, d_kpc;
   if (P.kp_n > 1) {
+    // masks (kp_mask_kernel), a one-block scan, the total through the pinned word, the list writes
     const uint64_t nb = (windows + KP_CHUNK - 1) / KP_CHUNK;
-    HIP_TRY(d_kpl.alloc(windows * sizeof(uint64_t), stream));
-    HIP_TRY(d_kpc.alloc(nb * 12, stream));  // counts (u32), then offsets (u64)
+    const size_t mask_b = nb * (KP_CHUNK / 64) * 8, cnt_b = (nb * 4 + 7) & ~7ull;
+    HIP_TRY(d_kpc.alloc(mask_b + cnt_b + nb * 8 + 8, stream));
+    auto* masks = static_cast<unsigned long long*>(d_kpc.p);
+    auto* bcount = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_kpc.p) + mask_b);
+    auto* boff = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(d_kpc.p) + mask_b + cnt_b);
+    auto* total = reinterpret_cast<unsigned long long*>(boff + nb);
+    unsigned int* w_host = nullptr;
+    unsigned int* w_dev = nullptr;
+    if (int hrc = pinned_word(w_host, w_dev, err)) return hrc;
     P.total_windows = windows;
-    hipLaunchKernelGGL(kp_count_kernel, dim3((uint32_t)nb), dim3(256), 0, stream, P, static_cast<uint32_t*>(d_kpc.p));
+    hipLaunchKernelGGL(kp_mask_kernel, dim3((uint32_t)nb), dim3(256), 0, stream, P, masks, bcount);
+    hipLaunchKernelGGL(dl_scan_kernel, dim3(1), dim3(1024), 0, stream, bcount, boff, nb, total);
+    hipLaunchKernelGGL(word_kernel, dim3(1), dim3(1), 0, stream, total, w_dev);
     HIP_TRY(hipGetLastError());
-    std::vector<uint32_t> bc(nb);
-    HIP_TRY(hipMemcpyAsync(bc.data(), d_kpc.p, nb * 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
-    std::vector<uint64_t> bo(nb);
-    uint64_t tot = 0;
-    for (uint64_t b = 0; b < nb; ++b) {
-      bo[b] = tot;
-      tot += bc[b];
-    }
-    uint64_t* d_bo = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(d_kpc.p) + ((nb * 4 + 7) & ~7ull));
-    HIP_TRY(hipMemcpyAsync(d_bo, bo.data(), nb * 8, hipMemcpyHostToDevice, stream));
-    hipLaunchKernelGGL(kp_write_kernel, dim3((uint32_t)nb), dim3(256), 0, stream, P, d_bo, static_cast<uint64_t*>(d_kpl.p));
+    const uint64_t tot = *reinterpret_cast<volatile unsigned int*>(w_host);
+    HIP_TRY(d_kpl.alloc(std::max<uint64_t>(1, tot) * sizeof(uint64_t), stream));
+    hipLaunchKernelGGL(dl_write_kernel, dim3((uint32_t)nb), dim3(256), 0, stream, P, masks, boff,
+                       static_cast<uint64_t*>(d_kpl.p));
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(stream));  // (bo is pageable host memory)
     windows = tot;
     P.total_windows = windows;
     P.kp_wlist = static_cast<const uint64_t*>(d_kpl.p);

@@ -451,9 +451,13 @@ __global__ __launch_bounds__(256) void write_tile_kernel(const uint8_t* __restri
                                                          const uint16_t* __restrict__ ltab, int ci, uint64_t* __restrict__ off,
                                                          uint32_t* __restrict__ text32) {
   __shared__ uint16_t s_lt[kPropLds];
+  __shared__ uint64_t s_off[4][256];  // a step's grapheme starts and chars, written out coalesced
+  __shared__ uint32_t s_tx[4][256];
   if (ci)
     for (uint32_t i = threadIdx.x; i < kPropLds; i += blockDim.x) s_lt[i] = ltab[i];
   __syncthreads();
+  uint64_t* const w_off = s_off[threadIdx.x / 64];
+  uint32_t* const w_tx = s_tx[threadIdx.x / 64];
   const uint64_t u = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
   const uint32_t lane = threadIdx.x & 63u;
   if (u >= n_units) return;  // whole waves
@@ -479,7 +483,7 @@ __global__ __launch_bounds__(256) void write_tile_kernel(const uint8_t* __restri
       const uint32_t y = __shfl_up(x, o, 64);
       if (lane >= (uint32_t)o) x += y;
     }
-    uint64_t o = base + x - c;
+    uint32_t o = x - c;  // the grapheme's slot in this step
     const uint64_t w8 = (uint64_t)wa | ((uint64_t)wb << 32);
     for (uint32_t k = 0; k < 4; ++k)
       if ((f >> k) & 1u) {
@@ -493,13 +497,20 @@ __global__ __launch_bounds__(256) void write_tile_kernel(const uint8_t* __restri
         else if ((b0 & 0xF8u) == 0xF0u && i + 3 < n)
           cp = ((b0 & 0x07u) << 18) | ((at(1) & 0x3Fu) << 12) | ((at(2) & 0x3Fu) << 6) | (at(3) & 0x3Fu);
         else cp = 0xFFFD;
-        off[o] = i;
         uint32_t fc = cp;
         if (ci) fc = cp >= 0x80u && cp < kPropLds && s_lt[cp] ? (uint32_t)s_lt[cp] : fold_fast(ltab, cp);
-        text32[o] = fc;
+        w_off[o] = i;
+        w_tx[o] = fc;
         ++o;
       }
-    base += __shfl(x, 63, 64);
+    const uint32_t tot = __shfl(x, 63, 64);
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t q = lane; q < tot; q += 64) {
+      off[base + q] = w_off[q];
+      text32[base + q] = w_tx[q];
+    }
+    __builtin_amdgcn_wave_barrier();
+    base += tot;
   }
 }
 
