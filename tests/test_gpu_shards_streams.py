@@ -277,6 +277,41 @@ def test_stream_window_batches_equal_single_windows(prefilter):
             assert key == want
 
 
+def test_dense_window_list_across_segments(monkeypatch, capfd):
+    """The dense bitmaps' window list (dl_mask_kernel) over a batch of stream windows: 100 003-byte
+    windows make segments whose boundaries fall inside the list's 4096-window blocks, so blocks take
+    the window-by-window path as well as the staged-tile one. Prefix cache and sampled level forced on:
+    records == bitmaps off == cache off, and windows are left out of the lookups (FAC_RC_DEBUG)."""
+    import re
+    import torch
+    from fuzzy_aho_corasick._native import MATCH_DTYPE
+    pats, hay = _sparse_c5(3 << 20, 3 << 10)
+    eng = B().fuzzy(L().edits(1)).device(0).build(pats)
+    st = StagedHaystack(eng, hay)
+    cuts = _window_cuts(len(hay), 100_003, eng.max_match_graphemes() + 1)
+    monkeypatch.setenv("FAC_RC_MIN", "1")
+    monkeypatch.setenv("FAC_RC_MIN2", "1")
+
+    def run():
+        dev = torch.empty(64, dtype=torch.uint8, device="cuda")
+        dev, k, _ = st.stream_windows_device(cuts, 0.85, False, dev, 0)
+        return [tuple(r) for r in dev[: k * 32].cpu().numpy().view(MATCH_DTYPE)]
+
+    monkeypatch.setenv("FAC_RC_DEBUG", "1")
+    capfd.readouterr()
+    dense = run()
+    err = capfd.readouterr().err
+    monkeypatch.delenv("FAC_RC_DEBUG")
+    m = re.findall(r"unlisted (\d+)", err)
+    assert m and int(m[-1]) > 0, err[-2000:]
+    monkeypatch.setenv("FAC_RC_NO_DENSE", "1")
+    plain = run()
+    monkeypatch.delenv("FAC_RC_NO_DENSE")
+    monkeypatch.setenv("FAC_NO_RC", "1")
+    off = run()
+    assert len(dense) > 100 and dense == plain == off
+
+
 @pytest.mark.parametrize("unicode_tail", [False, True])
 def test_search_stream_batches_match_oracle_emulation(unicode_tail):
     """search_stream over fac_stream_* with many windows per batch (stream.cpp: an ASCII batch staged
