@@ -116,6 +116,28 @@ def test_key_partitions_union_equals_whole(config, nbytes, parts):
         StagedHaystack(ab, b"a needle here").set_key_partition(2, 0)
 
 
+def test_key_partitions_with_dense_window_lists(monkeypatch):
+    """Key parts of a C2 slice with the sampled level forced on, so the dense bitmaps' list is built from
+    the key part's list (dl_mask_kernel's per-window path over P.kp_wlist): the parts' union == the whole
+    search, with the bitmaps on and off."""
+    import torch
+    monkeypatch.setenv("FAC_RC_MIN2", "1")
+    wl = W.config("c2", 4 << 20)
+    eng = W.builder_for(wl).device(0).build(wl.patterns)
+    want = rows_key(StagedHaystack(eng, wl.haystack).search_windows(wl.threshold)[0])
+    assert len(want) >= 100
+    dev = torch.from_numpy(np.frombuffer(wl.haystack, np.uint8).copy()).cuda()
+    for dense in (True, False):
+        if not dense:
+            monkeypatch.setenv("FAC_RC_NO_DENSE", "1")
+        for n in (2, 3):
+            got = []
+            for r in range(n):
+                sh = StagedHaystack.from_device(eng, dev.data_ptr(), len(wl.haystack)).set_key_partition(n, r)
+                got += sh.search_windows(wl.threshold)[0]
+            assert rows_key(got) == want, (dense, n)
+
+
 def test_empty_unicode_shard_stages_on_device():
     """A short Unicode text over many ranks leaves the last shards empty (plan (len, len, len, ...)):
     staging such a shard fresh from device memory must not touch the unallocated staging scratch
